@@ -1,0 +1,119 @@
+/*
+ * orbx.h -- C ABI of the MI355X-native ORB-SLAM2 hot path (liborbx.so).
+ *
+ * Plain C, plain pointers and sizes; never throws; every call returns an
+ * orbx_status (0 = ok, <0 = error).  Each handle owns one HIP stream, so two
+ * handles may be driven from two host threads concurrently (the reference
+ * runs the left and right extractors on two std::threads,
+ * src/Frame.cc:80-84).  A single handle is not thread-safe, exactly like the
+ * reference's ORBextractor (shared mvImagePyramid).
+ *
+ * Entry point -> reference interface it replaces:
+ *   orbx_extractor_create       ORBextractor::ORBextractor      src/ORBextractor.cc:416-490, include/ORBextractor.h:77
+ *   orbx_extractor_scale_tables GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
+ *                               GetInverseScaleSigmaSquares     include/ORBextractor.h:85-103
+ *   orbx_extractor_get_levels   GetLevels                       include/ORBextractor.h:82
+ *   orbx_extract                ORBextractor::operator()        src/ORBextractor.cc:1138-1211, include/ORBextractor.h:78-79
+ *   orbx_pyramid_level          public mvImagePyramid[level]    include/ORBextractor.h:104 (read at src/Frame.cc:556,681,694,700)
+ *   orbx_extract_batch_device   frame-batch form of operator() (one launch per stage for n images)
+ *   orbx_stereo_match           Frame::ComputeStereoMatches     src/Frame.cc:547-788, include/Frame.h:111
+ *   orbx_stereo_frames_device   extract(L)+extract(R)+ComputeStereoMatches for n stereo frames
+ *   orbx_descriptor_distance_device
+ *                               ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1844-1860, include/ORBmatcher.h:50
+ */
+#ifndef ORBX_H
+#define ORBX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int orbx_status;
+#define ORBX_OK 0
+#define ORBX_ERR_ARG (-1)        /* bad argument / null pointer               */
+#define ORBX_ERR_CAPACITY (-2)   /* caller buffer too small                   */
+#define ORBX_ERR_HIP (-3)        /* HIP runtime error (launch, alloc, copy)   */
+#define ORBX_ERR_NODEV (-4)      /* no usable gfx950 device                   */
+#define ORBX_ERR_SIZE (-5)       /* image geometry outside supported range    */
+#define ORBX_ERR_STATE (-6)      /* call requires a previous extraction       */
+
+/* Layout-identical to cv::KeyPoint (28 bytes). class_id is always -1. */
+typedef struct {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} orbx_keypoint;
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST) */
+typedef struct {
+  int nfeatures;
+  float scale_factor;
+  int nlevels;     /* 1..16 */
+  int ini_th_fast;
+  int min_th_fast;
+} orbx_extractor_params;
+
+typedef struct orbx_extractor orbx_extractor;
+
+orbx_status orbx_extractor_create(const orbx_extractor_params* params, int device, orbx_extractor** out);
+void orbx_extractor_destroy(orbx_extractor* h);
+int orbx_extractor_get_levels(const orbx_extractor* h);
+/* Any output pointer may be NULL; arrays hold nlevels floats. */
+orbx_status orbx_extractor_scale_tables(const orbx_extractor* h, float* scale, float* inv_scale,
+                                        float* sigma2, float* inv_sigma2);
+/* Upper bound on keypoints per image for this geometry (size kps/desc buffers with it). */
+int orbx_extractor_max_keypoints(orbx_extractor* h, int width, int height);
+
+/* Drop-in ORBextractor::operator(): host image in, host keypoints/descriptors out.
+ * An empty image (w or h == 0, or img == NULL) returns ORBX_OK with *n = 0,
+ * mirroring the reference's silent return. desc receives n*32 bytes, row i <-> kps[i].
+ * Output order is level-major, exactly the reference's. */
+orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height, size_t stride,
+                         orbx_keypoint* kps, int cap, uint8_t* desc, int* n);
+
+/* Copy level `level` of image `image` of the last extraction to host memory
+ * (dst may be NULL to query the size). */
+orbx_status orbx_pyramid_level(orbx_extractor* h, int image, int level, uint8_t* dst, size_t dst_stride,
+                               int* width, int* height);
+
+/* Device-resident batch: n_images u8 images of width x height, image i at
+ * d_images + i*image_pitch (row stride = width).  Outputs on device: image i
+ * writes d_counts[i] keypoints to d_kps + i*kp_capacity and descriptors to
+ * d_desc + i*kp_capacity*32.  stream: hipStream_t (NULL = the handle's own).
+ * Asynchronous; the input buffer must stay alive until the stream completes
+ * and, for orbx_stereo_* on the same batch, until those complete too
+ * (level 0 of the pyramid is the input itself). */
+orbx_status orbx_extract_batch_device(orbx_extractor* h, int n_images, const uint8_t* d_images, int width,
+                                      int height, size_t image_pitch, orbx_keypoint* d_kps, uint8_t* d_desc,
+                                      int32_t* d_counts, int kp_capacity, void* stream);
+
+/* Drop-in Frame::ComputeStereoMatches: host keypoints/descriptors, pyramids
+ * from the last extraction of `left` and `right` (image 0 of each).  bf =
+ * baseline*fx (mbf), baseline = mb.  Writes uRight[nL], depth[nL] (-1 = no match). */
+orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const orbx_keypoint* kpsL,
+                              const uint8_t* descL, int nL, const orbx_keypoint* kpsR, const uint8_t* descR,
+                              int nR, float bf, float baseline, float* uRight, float* depth);
+
+/* Device-resident stereo frames: d_images holds 2*n_frames images ordered
+ * L0,R0,L1,R1,... (pitch image_pitch).  Runs extraction of all 2n images and
+ * the stereo matcher of every frame.  Per image i: d_counts[i], d_kps/d_desc as
+ * in orbx_extract_batch_device.  Per frame f: d_uright/d_depth + f*kp_capacity
+ * hold the left keypoints' results; d_nmatches[f] = surviving matches. */
+orbx_status orbx_stereo_frames_device(orbx_extractor* h, int n_frames, const uint8_t* d_images, int width,
+                                      int height, size_t image_pitch, orbx_keypoint* d_kps, uint8_t* d_desc,
+                                      int32_t* d_counts, int kp_capacity, float bf, float baseline,
+                                      float* d_uright, float* d_depth, int32_t* d_nmatches, void* stream);
+
+/* Batched ORBmatcher::DescriptorDistance on device: d_out[i] = popcount(a_i ^ b_i). */
+orbx_status orbx_descriptor_distance_device(const uint8_t* d_a, const uint8_t* d_b, int n, int32_t* d_out,
+                                            void* stream);
+
+/* Library/device info: returns the number of visible HIP devices (<=0: none). */
+int orbx_device_count(void);
+const char* orbx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBX_H */

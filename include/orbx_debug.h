@@ -1,0 +1,29 @@
+/*
+ * orbx_debug.h -- introspection of liborbx.so intermediate buffers (test use).
+ * Copies one stage buffer of image `image` of the handle's last extraction to
+ * host memory so the parity tests can localise a mismatch to a stage.
+ */
+#ifndef ORBX_DEBUG_H
+#define ORBX_DEBUG_H
+#include "orbx.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  ORBX_DBG_BLUR_LEVEL = 1,  /* arg = level: blurred level image (w*h bytes)                 */
+  ORBX_DBG_CELL_COUNTS = 2, /* int32 per FAST cell (all levels, row-major per level)         */
+  ORBX_DBG_CELL_TABLE = 3,  /* int32 x8 per cell: level,x0,y0,x1,y1,cand_off,cap,0           */
+  ORBX_DBG_CANDIDATES = 4,  /* u32 per candidate slot (score<<24|y<<12|x), cand_total slots   */
+  ORBX_DBG_OCT_COUNTS = 5,  /* int32 per level                                                */
+  ORBX_DBG_OCT_OUT = 6,     /* u32 per octree output slot, oct_total slots                    */
+  ORBX_DBG_LEVEL_INFO = 7   /* int32 x8 per level: w,h,cell_begin,cell_end,oct_off,oct_cap,nfeat,nIni */
+};
+
+/* Returns the number of bytes the item occupies (copies min(cap, size)); <0 on error. */
+long long orbx_debug_copy(orbx_extractor* h, int what, int image, int arg, void* dst, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,157 @@
+"""ctypes binding of the CPU oracle (oracle/orb_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by orb_slam2_commit_amd/.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liborb_oracle.so")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise RuntimeError("oracle not built: run `make -C oracle`")
+        L = C.CDLL(_LIB_PATH)
+        P = C.c_void_p
+        L.oracle_extract.argtypes = [C.POINTER(Params), P, C.c_int, C.c_int, C.c_size_t, P, C.c_int, P, P,
+                                     C.c_size_t, P]
+        L.oracle_scale_tables.argtypes = [C.POINTER(Params), P, P, P, P, P]
+        L.oracle_resize_linear.argtypes = [P, C.c_int, C.c_int, P, C.c_int, C.c_int]
+        L.oracle_gaussian_blur7.argtypes = [P, C.c_int, C.c_int, P]
+        L.oracle_fast_window.argtypes = [P, C.c_int, C.c_int, C.c_size_t, C.c_int, P, C.c_int]
+        L.oracle_fast_score.argtypes = [P, C.c_size_t, C.c_int, C.c_int]
+        L.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
+        L.oracle_fast_atan2.restype = C.c_float
+        L.oracle_cosf.argtypes = [C.c_float]
+        L.oracle_cosf.restype = C.c_float
+        L.oracle_sinf.argtypes = [C.c_float]
+        L.oracle_sinf.restype = C.c_float
+        L.oracle_descriptor_distance.argtypes = [P, P]
+        L.oracle_hamming_pairs.argtypes = [P, P, C.c_int, P]
+        L.oracle_stereo_match.argtypes = [C.POINTER(Params), P, P, C.c_int, P, P, C.c_int, P, P, P,
+                                          C.c_float, C.c_float, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7):
+    return Params(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast)
+
+
+def scale_tables(p):
+    n = p.nlevels
+    s, i, s2, i2 = (np.zeros(n, np.float32) for _ in range(4))
+    f = np.zeros(n, np.int32)
+    lib().oracle_scale_tables(C.byref(p), _p(s), _p(i), _p(s2), _p(i2), _p(f))
+    return dict(scale=s, inv_scale=i, sigma2=s2, inv_sigma2=i2, features_per_level=f)
+
+
+class Extraction:
+    def __init__(self, kps, desc, pyramid, level_wh):
+        self.keypoints = kps
+        self.descriptors = desc
+        self.pyramid_flat = pyramid
+        self.level_wh = level_wh
+
+    def level(self, l):
+        off = int(sum(int(w) * int(h) for w, h in self.level_wh[:l]))
+        w, h = (int(v) for v in self.level_wh[l])
+        return self.pyramid_flat[off:off + w * h].reshape(h, w)
+
+
+def extract(p, img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = p.nfeatures + 8 * p.nlevels + 64
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    pyr = np.zeros(w * h * (p.nlevels + 1), np.uint8)
+    wh = np.zeros((p.nlevels, 2), np.int32)
+    n = lib().oracle_extract(C.byref(p), _p(img), w, h, w, _p(kps), cap, _p(desc), _p(pyr), pyr.size, _p(wh))
+    if n < 0:
+        raise RuntimeError("oracle_extract failed: %d" % n)
+    return Extraction(kps[:n].copy(), desc[:n].copy(), pyr, wh)
+
+
+def stereo_match(p, exL, exR, bf, baseline):
+    nL, nR = len(exL.keypoints), len(exR.keypoints)
+    uR = np.zeros(nL, np.float32)
+    depth = np.zeros(nL, np.float32)
+    kL = np.ascontiguousarray(exL.keypoints)
+    kR = np.ascontiguousarray(exR.keypoints)
+    dL = np.ascontiguousarray(exL.descriptors)
+    dR = np.ascontiguousarray(exR.descriptors)
+    lib().oracle_stereo_match(C.byref(p), _p(kL), _p(dL), nL, _p(kR), _p(dR), nR,
+                              _p(exL.pyramid_flat), _p(exR.pyramid_flat), _p(exL.level_wh),
+                              C.c_float(bf), C.c_float(baseline), _p(uR), _p(depth))
+    return uR, depth
+
+
+def resize_linear(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear(_p(src), src.shape[1], src.shape[0], _p(out), dw, dh)
+    return out
+
+
+def gaussian_blur7(src):
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros_like(src)
+    lib().oracle_gaussian_blur7(_p(src), src.shape[1], src.shape[0], _p(out))
+    return out
+
+
+def fast_window(img, threshold):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = w * h
+    out = np.zeros(cap, np.uint32)
+    n = lib().oracle_fast_window(_p(img), w, h, w, threshold, _p(out), cap)
+    out = out[:n]
+    return np.stack([out & 0xFFF, (out >> 12) & 0xFFF, out >> 24], axis=1).astype(np.int32)
+
+
+def fast_score(img, x, y):
+    img = np.ascontiguousarray(img, np.uint8)
+    return lib().oracle_fast_score(_p(img), img.shape[1], x, y)
+
+
+def fast_atan2(y, x):
+    return lib().oracle_fast_atan2(y, x)
+
+
+def cosf(x):
+    return lib().oracle_cosf(x)
+
+
+def sinf(x):
+    return lib().oracle_sinf(x)
+
+
+def hamming_pairs(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    d = np.zeros(len(a), np.int32)
+    lib().oracle_hamming_pairs(_p(a), _p(b), len(a), _p(d))
+    return d

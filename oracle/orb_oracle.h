@@ -1,0 +1,80 @@
+/*
+ * orb_oracle.h -- C ABI of the CPU ORACLE (test infrastructure only).
+ *
+ * THIS IS NOT THE PRODUCT.  It is a single-threaded C++ restatement of the
+ * reference's hot path used as the parity checker by tests/, by
+ * __graft_entry__.smoke() and as the `cpu_baseline` leg of bench.py.  Nothing
+ * under orb_slam2_commit_amd/ may include, link or call it.
+ *
+ * Parity status: the reference (qpc001/ORB_SLAM2_Commit) needs OpenCV, Eigen
+ * and the missing g2o/DBoW2 .cpp sources and cannot be built here, and it
+ * ships no tests, fixtures or golden vectors.  The
+ * oracle is therefore "parity unpinned" against the genuine binary; it is
+ * pinned instead by independent known-answer tests in tests/ (FAST-9 segment
+ * test by brute force, Gaussian kernel integers, resize coefficients,
+ * fastAtan2 vs atan2, popcount vs numpy) and by the committed fixtures it
+ * generated (tests/golden/).
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cv::KeyPoint layout (28 bytes). */
+typedef struct {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} oracle_keypoint;
+
+typedef struct {
+  int nfeatures;
+  float scale_factor;
+  int nlevels;
+  int ini_th_fast;
+  int min_th_fast;
+} oracle_params;
+
+/* Scale tables (ORBextractor ctor, src/ORBextractor.cc:416-490). Arrays of nlevels. */
+int oracle_scale_tables(const oracle_params* p, float* scale, float* inv_scale,
+                        float* sigma2, float* inv_sigma2, int* features_per_level);
+
+/* Full ORBextractor::operator() (src/ORBextractor.cc:1138-1211).
+ * pyramid_out (optional): concatenation of the nlevels level images, each
+ * w_l*h_l bytes, row-major, no padding; level sizes written to level_wh (2*nlevels).
+ * Returns number of keypoints, or <0 on error (-2: cap too small). */
+int oracle_extract(const oracle_params* p, const uint8_t* img, int w, int h, size_t stride,
+                   oracle_keypoint* kps, int cap, uint8_t* desc,
+                   uint8_t* pyramid_out, size_t pyramid_cap, int* level_wh);
+
+/* Stage probes for unit tests. */
+int oracle_resize_linear(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh);
+int oracle_gaussian_blur7(const uint8_t* src, int w, int h, uint8_t* dst);
+/* FAST-9 with NMS on a window (OpenCV FAST_t<16> semantics). Writes packed
+ * (score<<24 | y<<12 | x) in emission order; returns count. */
+int oracle_fast_window(const uint8_t* img, int w, int h, size_t stride, int threshold,
+                       uint32_t* out, int cap);
+int oracle_fast_score(const uint8_t* img, size_t stride, int x, int y);
+float oracle_fast_atan2(float y, float x);
+float oracle_cosf(float x);
+float oracle_sinf(float x);
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1844-1860). */
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
+void oracle_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int32_t* d);
+
+/* Frame::ComputeStereoMatches (src/Frame.cc:547-788).
+ * pyrL/pyrR: pyramids in oracle_extract's pyramid_out layout. */
+int oracle_stereo_match(const oracle_params* p,
+                        const oracle_keypoint* kpsL, const uint8_t* descL, int nL,
+                        const oracle_keypoint* kpsR, const uint8_t* descR, int nR,
+                        const uint8_t* pyrL, const uint8_t* pyrR, const int* level_wh,
+                        float bf, float baseline, float* uRight, float* depth);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

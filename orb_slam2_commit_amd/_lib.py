@@ -1,0 +1,96 @@
+"""ctypes loader for liborbx.so (the HIP kernels + C ABI of include/orbx.h).
+
+There is no CPU fallback: if the shared library is missing or cannot be
+loaded, or no gfx950 device is visible when a handle is created, the call
+raises.  Build with ``python -c "import __graft_entry__ as g; g.build()"`` or
+``make -C orb_slam2_commit_amd/csrc``.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liborbx.so")
+
+ORBX_OK = 0
+ORBX_ERR_ARG = -1
+ORBX_ERR_CAPACITY = -2
+ORBX_ERR_HIP = -3
+ORBX_ERR_NODEV = -4
+ORBX_ERR_SIZE = -5
+ORBX_ERR_STATE = -6
+_ERRS = {ORBX_ERR_ARG: "bad argument", ORBX_ERR_CAPACITY: "capacity", ORBX_ERR_HIP: "HIP runtime error",
+         ORBX_ERR_NODEV: "no HIP device", ORBX_ERR_SIZE: "unsupported geometry", ORBX_ERR_STATE: "no extraction yet"}
+
+# Layout-identical to cv::KeyPoint / orbx_keypoint (28 bytes).
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__("%s failed: %s (%d)" % (what, _ERRS.get(code, "error"), code))
+        self.code = code
+
+
+class ExtractorParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+# Every entry point of include/orbx.h with its ctypes signature.
+P = C.c_void_p
+SIGNATURES = {
+    "orbx_extractor_create": ([C.POINTER(ExtractorParams), C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_extractor_destroy": ([P], None),
+    "orbx_extractor_get_levels": ([P], C.c_int),
+    "orbx_extractor_scale_tables": ([P, P, P, P, P], C.c_int),
+    "orbx_extractor_max_keypoints": ([P, C.c_int, C.c_int], C.c_int),
+    "orbx_extract": ([P, P, C.c_int, C.c_int, C.c_size_t, P, C.c_int, P, C.POINTER(C.c_int)], C.c_int),
+    "orbx_pyramid_level": ([P, C.c_int, C.c_int, P, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
+    "orbx_extract_batch_device": ([P, C.c_int, P, C.c_int, C.c_int, C.c_size_t, P, P, P, C.c_int, P], C.c_int),
+    "orbx_stereo_match": ([P, P, P, P, C.c_int, P, P, C.c_int, C.c_float, C.c_float, P, P], C.c_int),
+    "orbx_stereo_frames_device": ([P, C.c_int, P, C.c_int, C.c_int, C.c_size_t, P, P, P, C.c_int, C.c_float,
+                                   C.c_float, P, P, P, P], C.c_int),
+    "orbx_descriptor_distance_device": ([P, P, C.c_int, P, P], C.c_int),
+    "orbx_device_count": ([], C.c_int),
+    "orbx_version": ([], C.c_char_p),
+    # include/orbx_debug.h
+    "orbx_debug_copy": ([P, C.c_int, C.c_int, C.c_int, P, C.c_size_t], C.c_longlong),
+}
+
+_lib = None
+
+
+def lib():
+    """Load liborbx.so (raises if it is absent: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("liborbx.so not found at %s -- build it first (make -C orb_slam2_commit_amd/csrc)"
+                               % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def check(code, what):
+    if code != ORBX_OK:
+        raise OrbxError(code, what)
+
+
+def ptr(a):
+    """Host numpy array or torch tensor (host or device) -> void*."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(C.c_void_p)
+    if hasattr(a, "data_ptr"):
+        return C.c_void_p(a.data_ptr())
+    raise TypeError(type(a))

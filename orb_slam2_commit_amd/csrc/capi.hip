@@ -1,0 +1,713 @@
+// capi.hip -- host side of liborbx.so: the C ABI declared in include/orbx.h.
+//
+// An orbx_extractor owns: one HIP stream, the parameter tables of the
+// reference constructor (src/ORBextractor.cc:416-490), a plan per image
+// geometry (level sizes, FAST cell table, resize coefficient tables, blur
+// tiles; built once on the host and uploaded), and device buffers grown to the
+// largest batch seen.  Nothing here computes results on the CPU: every output
+// comes from the HIP kernels in extract.hip / stereo.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <new>
+#include <utility>
+#include <vector>
+
+#include "../../include/orbx.h"
+#include "orbx_internal.h"
+#include "orbx_stereo.h"
+
+namespace orbx {
+hipError_t upload_constants(const int* umax16, const int* gauss7);
+hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells, const int* tile_level,
+                                 const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B, int n_img,
+                                 orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t st);
+size_t octree_smem_host(int NC, int cell_cap);
+hipError_t octree_set_smem_limit(size_t bytes);
+}  // namespace orbx
+
+using namespace orbx;
+
+namespace {
+
+inline int round_even(float v) { return (int)std::nearbyintf(v); }
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    release();
+    size_t c = std::max<size_t>(count, 1);
+    hipError_t e = hipMalloc((void**)&p, c * sizeof(T));
+    if (e == hipSuccess) n = c;
+    return e;
+  }
+};
+
+struct Tables {
+  std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+  std::vector<int> nfeat;
+  int umax[16];
+};
+
+// ORBextractor::ORBextractor (src/ORBextractor.cc:416-490): scale factors in
+// float from a double member, per-level quotas with cvRound, umax circle.
+Tables make_tables(const orbx_extractor_params& p) {
+  Tables t;
+  const double sf = (double)p.scale_factor;
+  const int n = p.nlevels;
+  t.scale.assign(n, 1.0f);
+  t.sigma2.assign(n, 1.0f);
+  for (int i = 1; i < n; i++) {
+    t.scale[i] = (float)((double)t.scale[i - 1] * sf);
+    t.sigma2[i] = t.scale[i] * t.scale[i];
+  }
+  t.inv_scale.resize(n);
+  t.inv_sigma2.resize(n);
+  for (int i = 0; i < n; i++) {
+    t.inv_scale[i] = 1.0f / t.scale[i];
+    t.inv_sigma2[i] = 1.0f / t.sigma2[i];
+  }
+  t.nfeat.resize(n);
+  const float factor = (float)(1.0f / sf);
+  float ndes = (float)p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)n));
+  int sum = 0;
+  for (int l = 0; l < n - 1; l++) {
+    t.nfeat[l] = round_even(ndes);
+    sum += t.nfeat[l];
+    ndes *= factor;
+  }
+  t.nfeat[n - 1] = std::max(p.nfeatures - sum, 0);
+  int vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1);
+  int vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
+  for (int v = 0; v < 16; v++) t.umax[v] = 0;
+  for (int v = 0; v <= vmax; ++v) t.umax[v] = (int)std::nearbyint(std::sqrt(225.0 - v * v));
+  for (int v = 15, v0 = 0; v >= vmin; --v) {
+    while (t.umax[v0] == t.umax[v0 + 1]) ++v0;
+    t.umax[v] = v0;
+    ++v0;
+  }
+  return t;
+}
+
+// getGaussianKernel(7, 2, CV_32F) -> x256 -> cvRound (OpenCV 3.2 8U separable path).
+void gaussian_int_kernel(int k[7]) {
+  float cf[7];
+  double sum = 0;
+  const double scale2X = -0.5 / (2.0 * 2.0);
+  for (int i = 0; i < 7; i++) {
+    double x = i - 3.0;
+    cf[i] = (float)std::exp(scale2X * x * x);
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 7; i++) {
+    cf[i] = (float)(cf[i] * sum);
+    k[i] = round_even(cf[i] * 256.0f);
+  }
+}
+
+struct Plan {
+  Geometry G{};
+  std::vector<CellInfo> cells;
+  std::vector<int> tile_level;
+  std::vector<ResizeX> xt;
+  std::vector<ResizeY> yt;
+  DevBuf<Geometry> dG;
+  DevBuf<CellInfo> dcells;
+  DevBuf<int> dtiles;
+  DevBuf<ResizeX> dxt;
+  DevBuf<ResizeY> dyt;
+};
+
+// Builds the per-geometry plan.  Level sizes: ComputePyramid
+// (src/ORBextractor.cc:1219-1221); FAST cells: ComputeKeyPointsOctTree
+// (:826-880); octree roots: DistributeOctTree (:567-570); resize tables:
+// OpenCV 3.2 resizeGeneric_ coefficient setup.
+orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, int H, Plan& P) {
+  Geometry& G = P.G;
+  std::memset(&G, 0, sizeof(G));
+  G.nlevels = p.nlevels;
+  G.width = W;
+  G.height = H;
+  G.ini_th = p.ini_th_fast;
+  G.min_th = p.min_th_fast;
+  long long pyr = 0, blur = 0;
+  int cand = 0, oct = 0, ntiles = 0, node_cap = 64, cell_cap = 1;
+  P.cells.clear();
+  P.tile_level.clear();
+  P.xt.clear();
+  P.yt.clear();
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelGeom& L = G.lv[l];
+    L.w = round_even((float)W * t.inv_scale[l]);
+    L.h = round_even((float)H * t.inv_scale[l]);
+    if (L.w < 1 || L.h < 1 || L.w > 4095 || L.h > 4095) return ORBX_ERR_SIZE;
+    L.off = l == 0 ? 0 : pyr;
+    if (l > 0) pyr += (long long)L.w * L.h;
+    L.boff = blur;
+    blur += (long long)L.w * L.h;
+    L.minBX = L.minBY = kEdgeThresholdHost - 3;
+    L.maxBX = L.w - kEdgeThresholdHost + 3;
+    L.maxBY = L.h - kEdgeThresholdHost + 3;
+    L.scale = t.scale[l];
+    L.kp_size = (float)(int)(31 * t.scale[l]);
+    L.nfeat = t.nfeat[l];
+    // FAST cells
+    L.cell_begin = (int)P.cells.size();
+    L.cand_begin = cand;
+    const float width = (float)(L.maxBX - L.minBX), height = (float)(L.maxBY - L.minBY);
+    const int nCols = (int)(width / 30), nRows = (int)(height / 30);
+    if (width > 0 && height > 0 && nCols > 0 && nRows > 0) {
+      const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+      for (int i = 0; i < nRows; i++) {
+        const float iniY = (float)(L.minBY + i * hCell);
+        float maxY = iniY + hCell + 6;
+        if (iniY >= L.maxBY - 3) continue;
+        if (maxY > L.maxBY) maxY = (float)L.maxBY;
+        for (int j = 0; j < nCols; j++) {
+          const float iniX = (float)(L.minBX + j * wCell);
+          float maxX = iniX + wCell + 6;
+          if (iniX >= L.maxBX - 6) continue;
+          if (maxX > L.maxBX) maxX = (float)L.maxBX;
+          CellInfo c{};
+          c.level = (int16_t)l;
+          c.x0 = (int16_t)((int)iniX + 3);
+          c.y0 = (int16_t)((int)iniY + 3);
+          c.x1 = (int16_t)((int)maxX - 4);
+          c.y1 = (int16_t)((int)maxY - 4);
+          if (c.x1 < c.x0 || c.y1 < c.y0) continue;
+          const int cw = c.x1 - c.x0 + 1, ch = c.y1 - c.y0 + 1;
+          if (cw > 64 || ch > 64) return ORBX_ERR_SIZE;
+          c.cap = ((cw + 1) / 2) * ((ch + 1) / 2);
+          c.cand_off = cand;
+          cand += c.cap;
+          P.cells.push_back(c);
+        }
+      }
+    }
+    L.cell_end = (int)P.cells.size();
+    L.cand_cap = cand - L.cand_begin;
+    cell_cap = std::max(cell_cap, L.cell_end - L.cell_begin);
+    // octree roots
+    int nIni = 1;
+    if (L.maxBY - L.minBY > 0) nIni = (int)std::round((float)(L.maxBX - L.minBX) / (L.maxBY - L.minBY));
+    if (nIni < 1) nIni = 1;
+    L.nIni = nIni;
+    L.hX = (float)(L.maxBX - L.minBX) / nIni;
+    L.oct_cap = std::max(L.nfeat + 3, 4 * nIni);
+    L.oct_off = oct;
+    oct += L.oct_cap;
+    node_cap = std::max(node_cap, (L.oct_cap + 63) / 64 * 64);
+    // blur tiles
+    L.tiles_x = (L.w + kBlurTileW - 1) / kBlurTileW;
+    L.tiles_y = (L.h + kBlurTileH - 1) / kBlurTileH;
+    L.tile_begin = ntiles;
+    ntiles += L.tiles_x * L.tiles_y;
+    for (int q = 0; q < L.tiles_x * L.tiles_y; q++) P.tile_level.push_back(l);
+    // resize tables (source = level l-1)
+    if (l > 0) {
+      const LevelGeom& S = G.lv[l - 1];
+      const int sw = S.w, sh = S.h, dw = L.w, dh = L.h;
+      const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+      L.xtab_off = (int)P.xt.size();
+      for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw && sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        ResizeX X;
+        X.sx0 = sx;
+        X.sx1 = std::min(sx + 1, sw - 1);
+        X.a0 = (int16_t)round_even((1.f - fx) * 2048);
+        X.a1 = (int16_t)round_even(fx * 2048);
+        if (sx + 1 >= sw) {  // xmax region: D = S[sx]*2048
+          X.a0 = 2048;
+          X.a1 = 0;
+        }
+        P.xt.push_back(X);
+      }
+      L.ytab_off = (int)P.yt.size();
+      for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)std::floor(fy);
+        fy -= sy;
+        ResizeY Y;
+        Y.sy0 = std::min(std::max(sy, 0), sh - 1);
+        Y.sy1 = std::min(std::max(sy + 1, 0), sh - 1);
+        Y.b0 = (int16_t)round_even((1.f - fy) * 2048);
+        Y.b1 = (int16_t)round_even(fy * 2048);
+        P.yt.push_back(Y);
+      }
+    }
+  }
+  G.pyr_bytes = (pyr + 255) & ~255LL;
+  G.blur_bytes = (blur + 255) & ~255LL;
+  G.ncells = (int)P.cells.size();
+  G.cand_total = std::max(cand, 1);
+  G.oct_total = oct;
+  G.max_kps = oct;
+  G.ntiles = ntiles;
+  G.node_cap = node_cap;
+  G.cell_cap = cell_cap;
+  if (node_cap > 8192) return ORBX_ERR_SIZE;
+  if (octree_smem_host(node_cap, cell_cap) > 160 * 1024 - 1024) return ORBX_ERR_SIZE;
+  return ORBX_OK;
+}
+
+}  // namespace
+
+struct orbx_extractor {
+  orbx_extractor_params params{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Tables tables;
+  std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
+  // batch buffers
+  int batch_cap = 0;
+  long long bytes_pyr = 0, bytes_blur = 0, n_cand = 0, n_oct = 0, n_cells = 0;
+  DevBuf<uint8_t> pyr, blur, kdig;
+  DevBuf<uint32_t> cand, kpos, oct;
+  DevBuf<int> cell_count, knode, oct_count;
+  // host-API staging
+  DevBuf<uint8_t> in, desc;
+  DevBuf<orbx_keypoint> kps;
+  DevBuf<int32_t> counts;
+  // stereo scratch
+  DevBuf<uint64_t> rkeys;
+  DevBuf<int> oct_start, sad;
+  DevBuf<float> uR, depth;
+  DevBuf<int32_t> nmatch, nbuf;
+  DevBuf<orbx_keypoint> skL, skR;
+  DevBuf<uint8_t> sdL, sdR;
+  // last batch (mvImagePyramid)
+  Plan* last_plan = nullptr;
+  const uint8_t* last_in = nullptr;
+  size_t last_pitch = 0;
+  int last_n = 0;
+};
+
+namespace {
+
+orbx_status hip_status(hipError_t e) { return e == hipSuccess ? ORBX_OK : ORBX_ERR_HIP; }
+
+orbx_status get_plan(orbx_extractor* h, int W, int H, Plan** out) {
+  auto key = std::make_pair(W, H);
+  auto it = h->plans.find(key);
+  if (it != h->plans.end()) {
+    *out = it->second.get();
+    return ORBX_OK;
+  }
+  std::unique_ptr<Plan> P(new (std::nothrow) Plan());
+  if (!P) return ORBX_ERR_HIP;
+  orbx_status s = build_plan(h->params, h->tables, W, H, *P);
+  if (s != ORBX_OK) return s;
+  hipError_t e;
+  if ((e = P->dG.ensure(1)) != hipSuccess) return ORBX_ERR_HIP;
+  if ((e = P->dcells.ensure(P->cells.size())) != hipSuccess) return ORBX_ERR_HIP;
+  if ((e = P->dtiles.ensure(P->tile_level.size())) != hipSuccess) return ORBX_ERR_HIP;
+  if ((e = P->dxt.ensure(P->xt.size())) != hipSuccess) return ORBX_ERR_HIP;
+  if ((e = P->dyt.ensure(P->yt.size())) != hipSuccess) return ORBX_ERR_HIP;
+  e = hipMemcpy(P->dG.p, &P->G, sizeof(Geometry), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !P->cells.empty())
+    e = hipMemcpy(P->dcells.p, P->cells.data(), P->cells.size() * sizeof(CellInfo), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !P->tile_level.empty())
+    e = hipMemcpy(P->dtiles.p, P->tile_level.data(), P->tile_level.size() * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !P->xt.empty())
+    e = hipMemcpy(P->dxt.p, P->xt.data(), P->xt.size() * sizeof(ResizeX), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !P->yt.empty())
+    e = hipMemcpy(P->dyt.p, P->yt.data(), P->yt.size() * sizeof(ResizeY), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  e = octree_set_smem_limit(octree_smem_host(P->G.node_cap, P->G.cell_cap));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  *out = P.get();
+  h->plans[key] = std::move(P);
+  return ORBX_OK;
+}
+
+orbx_status ensure_batch(orbx_extractor* h, const Plan& P, int n) {
+  const Geometry& G = P.G;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
+  chk(h->pyr.ensure((size_t)G.pyr_bytes * n + 256));
+  chk(h->blur.ensure((size_t)G.blur_bytes * n + 256));
+  chk(h->cand.ensure((size_t)G.cand_total * n));
+  chk(h->kpos.ensure((size_t)G.cand_total * n));
+  chk(h->knode.ensure((size_t)G.cand_total * n));
+  chk(h->kdig.ensure((size_t)G.cand_total * n));
+  chk(h->cell_count.ensure((size_t)std::max(G.ncells, 1) * n));
+  chk(h->oct.ensure((size_t)G.oct_total * n));
+  chk(h->oct_count.ensure((size_t)G.nlevels * n));
+  return hip_status(e);
+}
+
+BatchPtrs batch_ptrs(orbx_extractor* h, const uint8_t* in, size_t pitch) {
+  BatchPtrs B;
+  B.in = in;
+  B.in_pitch = pitch;
+  B.pyr = h->pyr.p;
+  B.blur = h->blur.p;
+  B.cand = h->cand.p;
+  B.cell_count = h->cell_count.p;
+  B.kpos = h->kpos.p;
+  B.knode = h->knode.p;
+  B.kdig = h->kdig.p;
+  B.oct = h->oct.p;
+  B.oct_count = h->oct_count.p;
+  return B;
+}
+
+orbx_status run_extract(orbx_extractor* h, Plan* P, int n, const uint8_t* d_in, size_t pitch, orbx_keypoint* d_kps,
+                        uint8_t* d_desc, int32_t* d_counts, int kp_cap, hipStream_t st) {
+  if (kp_cap < P->G.max_kps) return ORBX_ERR_CAPACITY;
+  orbx_status s = ensure_batch(h, *P, n);
+  if (s != ORBX_OK) return s;
+  BatchPtrs B = batch_ptrs(h, d_in, pitch);
+  hipError_t e = launch_extract_stages(P->G, P->dG.p, P->dcells.p, P->dtiles.p, P->dxt.p, P->dyt.p, B, n, d_kps,
+                                       d_desc, d_counts, kp_cap, st);
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  h->last_plan = P;
+  h->last_in = d_in;
+  h->last_pitch = pitch;
+  h->last_n = n;
+  return ORBX_OK;
+}
+
+hipStream_t pick_stream(orbx_extractor* h, void* s) { return s ? (hipStream_t)s : h->stream; }
+
+bool params_ok(const orbx_extractor_params* p) {
+  return p && p->nlevels >= 1 && p->nlevels <= kMaxLevelsPlan && p->scale_factor > 0.f && p->nfeatures >= 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* orbx_version(void) { return "orbx 0.1.0 (gfx950)"; }
+
+int orbx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+orbx_status orbx_extractor_create(const orbx_extractor_params* params, int device, orbx_extractor** out) {
+  if (!out || !params_ok(params)) return ORBX_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ORBX_ERR_NODEV;
+  if (device < 0 || device >= n) return ORBX_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return ORBX_ERR_HIP;
+  orbx_extractor* h = new (std::nothrow) orbx_extractor();
+  if (!h) return ORBX_ERR_HIP;
+  h->params = *params;
+  h->device = device;
+  h->tables = make_tables(*params);
+  int gauss[7];
+  gaussian_int_kernel(gauss);
+  if (upload_constants(h->tables.umax, gauss) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return ORBX_ERR_HIP;
+  }
+  *out = h;
+  return ORBX_OK;
+}
+
+void orbx_extractor_destroy(orbx_extractor* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) {
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipStreamDestroy(h->stream);
+  }
+  delete h;
+}
+
+int orbx_extractor_get_levels(const orbx_extractor* h) { return h ? h->params.nlevels : ORBX_ERR_ARG; }
+
+orbx_status orbx_extractor_scale_tables(const orbx_extractor* h, float* scale, float* inv_scale, float* sigma2,
+                                        float* inv_sigma2) {
+  if (!h) return ORBX_ERR_ARG;
+  const int n = h->params.nlevels;
+  for (int i = 0; i < n; i++) {
+    if (scale) scale[i] = h->tables.scale[i];
+    if (inv_scale) inv_scale[i] = h->tables.inv_scale[i];
+    if (sigma2) sigma2[i] = h->tables.sigma2[i];
+    if (inv_sigma2) inv_sigma2[i] = h->tables.inv_sigma2[i];
+  }
+  return ORBX_OK;
+}
+
+int orbx_extractor_max_keypoints(orbx_extractor* h, int width, int height) {
+  if (!h) return ORBX_ERR_ARG;
+  Plan* P = nullptr;
+  orbx_status s = get_plan(h, width, height, &P);
+  return s == ORBX_OK ? P->G.max_kps : s;
+}
+
+orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int height, size_t stride,
+                         orbx_keypoint* kps, int cap, uint8_t* desc, int* n) {
+  if (!h || !n) return ORBX_ERR_ARG;
+  *n = 0;
+  if (!img || width <= 0 || height <= 0) return ORBX_OK;  // src/ORBextractor.cc:1141
+  if (stride < (size_t)width) return ORBX_ERR_ARG;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  Plan* P = nullptr;
+  orbx_status s = get_plan(h, width, height, &P);
+  if (s != ORBX_OK) return s;
+  const int kcap = P->G.max_kps;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
+  chk(h->in.ensure((size_t)width * height));
+  chk(h->kps.ensure(kcap));
+  chk(h->desc.ensure((size_t)kcap * 32));
+  chk(h->counts.ensure(1));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  hipStream_t st = h->stream;
+  if (hipMemcpy2DAsync(h->in.p, width, img, stride, width, height, hipMemcpyHostToDevice, st) != hipSuccess)
+    return ORBX_ERR_HIP;
+  s = run_extract(h, P, 1, h->in.p, (size_t)width * height, h->kps.p, h->desc.p, h->counts.p, kcap, st);
+  if (s != ORBX_OK) return s;
+  int32_t cnt = 0;
+  chk(hipMemcpyAsync(&cnt, h->counts.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  chk(hipStreamSynchronize(st));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  *n = cnt;
+  if (cnt > cap) return ORBX_ERR_CAPACITY;
+  if (cnt > 0) {
+    if (kps) chk(hipMemcpyAsync(kps, h->kps.p, sizeof(orbx_keypoint) * cnt, hipMemcpyDeviceToHost, st));
+    if (desc) chk(hipMemcpyAsync(desc, h->desc.p, (size_t)32 * cnt, hipMemcpyDeviceToHost, st));
+    chk(hipStreamSynchronize(st));
+  }
+  return hip_status(e);
+}
+
+orbx_status orbx_pyramid_level(orbx_extractor* h, int image, int level, uint8_t* dst, size_t dst_stride,
+                               int* width, int* height) {
+  if (!h) return ORBX_ERR_ARG;
+  if (!h->last_plan) return ORBX_ERR_STATE;
+  const Geometry& G = h->last_plan->G;
+  if (level < 0 || level >= G.nlevels || image < 0 || image >= h->last_n) return ORBX_ERR_ARG;
+  const int w = G.lv[level].w, hh = G.lv[level].h;
+  if (width) *width = w;
+  if (height) *height = hh;
+  if (!dst) return ORBX_OK;
+  if (dst_stride < (size_t)w) return ORBX_ERR_ARG;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  BatchPtrs B = batch_ptrs(h, h->last_in, h->last_pitch);
+  const uint8_t* src = level_ptr(G, B, image, level);
+  hipError_t e = hipMemcpy2DAsync(dst, dst_stride, src, w, w, hh, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  return hip_status(e);
+}
+
+orbx_status orbx_extract_batch_device(orbx_extractor* h, int n_images, const uint8_t* d_images, int width,
+                                      int height, size_t image_pitch, orbx_keypoint* d_kps, uint8_t* d_desc,
+                                      int32_t* d_counts, int kp_capacity, void* stream) {
+  if (!h || n_images < 0 || !d_kps || !d_desc || !d_counts) return ORBX_ERR_ARG;
+  if (n_images == 0) return ORBX_OK;
+  if (!d_images || width <= 0 || height <= 0 || image_pitch < (size_t)width * height) return ORBX_ERR_ARG;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  Plan* P = nullptr;
+  orbx_status s = get_plan(h, width, height, &P);
+  if (s != ORBX_OK) return s;
+  return run_extract(h, P, n_images, d_images, image_pitch, d_kps, d_desc, d_counts, kp_capacity,
+                     pick_stream(h, stream));
+}
+
+static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_frames, const orbx_keypoint* kL,
+                              const uint8_t* dL, const int32_t* nL, long long kL_stride, long long nL_stride,
+                              const orbx_keypoint* kR, const uint8_t* dR, const int32_t* nR, long long kR_stride,
+                              long long nR_stride, int l_step, int l_off, int r_step, int r_off, int maxL,
+                              float bf, float baseline, float* uR, float* depth, long long out_stride,
+                              int32_t* nmatches, hipStream_t st) {
+  orbx_extractor* h = hl;
+  Plan* P = hl->last_plan;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
+  chk(h->rkeys.ensure((size_t)n_frames * kMaxStereoKps));
+  chk(h->oct_start.ensure((size_t)n_frames * (kMaxLevelsPlan + 1)));
+  chk(h->sad.ensure((size_t)n_frames * out_stride));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  StereoArgs A;
+  std::memset(&A, 0, sizeof(A));
+  A.kpL = kL;
+  A.dL = dL;
+  A.nL = nL;
+  A.kL_stride = kL_stride;
+  A.n_stride_L = nL_stride;
+  A.kpR = kR;
+  A.dR = dR;
+  A.nR = nR;
+  A.kR_stride = kR_stride;
+  A.n_stride_R = nR_stride;
+  A.BL = batch_ptrs(hl, hl->last_in, hl->last_pitch);
+  A.BR = batch_ptrs(hr, hr->last_in, hr->last_pitch);
+  A.l_step = l_step;
+  A.l_off = l_off;
+  A.r_step = r_step;
+  A.r_off = r_off;
+  A.nlevels = P->G.nlevels;
+  A.maxL = maxL;
+  for (int l = 0; l < P->G.nlevels; l++) A.inv_scale[l] = hl->tables.inv_scale[l];
+  A.bf = bf;
+  A.minZ = baseline;
+  A.minD = 0.f;
+  A.maxD = bf / baseline;  // mbf/minZ, src/Frame.cc:595-597
+  A.uR = uR;
+  A.depth = depth;
+  A.sad = h->sad.p;
+  A.out_stride = out_stride;
+  A.rkeys = h->rkeys.p;
+  A.oct_start = h->oct_start.p;
+  A.nmatches = nmatches;
+  return hip_status(launch_stereo(A, P->dG.p, n_frames, maxL, st));
+}
+
+orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const orbx_keypoint* kpsL,
+                              const uint8_t* descL, int nL, const orbx_keypoint* kpsR, const uint8_t* descR,
+                              int nR, float bf, float baseline, float* uRight, float* depth) {
+  if (!left || !right || !uRight || !depth || nL < 0 || nR < 0) return ORBX_ERR_ARG;
+  if ((nL > 0 && (!kpsL || !descL)) || (nR > 0 && (!kpsR || !descR))) return ORBX_ERR_ARG;
+  if (!left->last_plan || !right->last_plan) return ORBX_ERR_STATE;
+  if (left->last_plan->G.width != right->last_plan->G.width ||
+      left->last_plan->G.height != right->last_plan->G.height || left->device != right->device)
+    return ORBX_ERR_ARG;
+  if (nR > kMaxStereoKps) return ORBX_ERR_CAPACITY;
+  if (nL == 0) return ORBX_OK;
+  orbx_extractor* h = left;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
+  chk(h->skL.ensure(nL));
+  chk(h->sdL.ensure((size_t)nL * 32));
+  chk(h->skR.ensure(std::max(nR, 1)));
+  chk(h->sdR.ensure((size_t)std::max(nR, 1) * 32));
+  chk(h->uR.ensure(nL));
+  chk(h->depth.ensure(nL));
+  chk(h->nmatch.ensure(1));
+  chk(h->nbuf.ensure(2));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  hipStream_t st = h->stream;
+  // the right handle's last extraction must be complete before we read its pyramid
+  chk(hipStreamSynchronize(right->stream));
+  int32_t ns[2] = {nL, nR};
+  chk(hipMemcpyAsync(h->nbuf.p, ns, sizeof(ns), hipMemcpyHostToDevice, st));
+  chk(hipMemcpyAsync(h->skL.p, kpsL, sizeof(orbx_keypoint) * nL, hipMemcpyHostToDevice, st));
+  chk(hipMemcpyAsync(h->sdL.p, descL, (size_t)32 * nL, hipMemcpyHostToDevice, st));
+  if (nR > 0) {
+    chk(hipMemcpyAsync(h->skR.p, kpsR, sizeof(orbx_keypoint) * nR, hipMemcpyHostToDevice, st));
+    chk(hipMemcpyAsync(h->sdR.p, descR, (size_t)32 * nR, hipMemcpyHostToDevice, st));
+  }
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  orbx_status s = run_stereo(left, right, 1, h->skL.p, h->sdL.p, h->nbuf.p, 0, 0, h->skR.p, h->sdR.p, h->nbuf.p + 1,
+                             0, 0, 0, 0, 0, 0, nL, bf, baseline, h->uR.p, h->depth.p, nL, h->nmatch.p, st);
+  if (s != ORBX_OK) return s;
+  chk(hipMemcpyAsync(uRight, h->uR.p, sizeof(float) * nL, hipMemcpyDeviceToHost, st));
+  chk(hipMemcpyAsync(depth, h->depth.p, sizeof(float) * nL, hipMemcpyDeviceToHost, st));
+  chk(hipStreamSynchronize(st));
+  return hip_status(e);
+}
+
+orbx_status orbx_stereo_frames_device(orbx_extractor* h, int n_frames, const uint8_t* d_images, int width,
+                                      int height, size_t image_pitch, orbx_keypoint* d_kps, uint8_t* d_desc,
+                                      int32_t* d_counts, int kp_capacity, float bf, float baseline,
+                                      float* d_uright, float* d_depth, int32_t* d_nmatches, void* stream) {
+  if (!h || n_frames < 0 || !d_uright || !d_depth || !d_nmatches) return ORBX_ERR_ARG;
+  if (n_frames == 0) return ORBX_OK;
+  orbx_status s = orbx_extract_batch_device(h, 2 * n_frames, d_images, width, height, image_pitch, d_kps, d_desc,
+                                            d_counts, kp_capacity, stream);
+  if (s != ORBX_OK) return s;
+  if (h->last_plan->G.max_kps > kMaxStereoKps) return ORBX_ERR_CAPACITY;
+  const long long kc = kp_capacity;
+  return run_stereo(h, h, n_frames, d_kps, d_desc, d_counts, 2 * kc, 2, d_kps + kc, d_desc + kc * 32, d_counts + 1,
+                    2 * kc, 2, 2, 0, 2, 1, h->last_plan->G.max_kps, bf, baseline, d_uright, d_depth, kc,
+                    d_nmatches, pick_stream(h, stream));
+}
+
+orbx_status orbx_descriptor_distance_device(const uint8_t* d_a, const uint8_t* d_b, int n, int32_t* d_out,
+                                            void* stream) {
+  if (n < 0 || (n > 0 && (!d_a || !d_b || !d_out))) return ORBX_ERR_ARG;
+  return hip_status(launch_hamming(d_a, d_b, n, d_out, (hipStream_t)stream));
+}
+
+}  // extern "C"
+
+#include "../../include/orbx_debug.h"
+
+extern "C" long long orbx_debug_copy(orbx_extractor* h, int what, int image, int arg, void* dst, size_t cap) {
+  if (!h) return ORBX_ERR_ARG;
+  if (!h->last_plan) return ORBX_ERR_STATE;
+  const Plan& P = *h->last_plan;
+  const Geometry& G = P.G;
+  if (image < 0 || image >= h->last_n) return ORBX_ERR_ARG;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBX_ERR_HIP;
+  std::vector<int> host;
+  const void* src = nullptr;
+  size_t bytes = 0;
+  bool device_src = true;
+  switch (what) {
+    case ORBX_DBG_BLUR_LEVEL:
+      if (arg < 0 || arg >= G.nlevels) return ORBX_ERR_ARG;
+      src = h->blur.p + (size_t)image * G.blur_bytes + G.lv[arg].boff;
+      bytes = (size_t)G.lv[arg].w * G.lv[arg].h;
+      break;
+    case ORBX_DBG_CELL_COUNTS:
+      src = h->cell_count.p + (size_t)image * G.ncells;
+      bytes = sizeof(int) * G.ncells;
+      break;
+    case ORBX_DBG_CELL_TABLE:
+      for (const CellInfo& c : P.cells) {
+        int v[8] = {c.level, c.x0, c.y0, c.x1, c.y1, c.cand_off, c.cap, 0};
+        host.insert(host.end(), v, v + 8);
+      }
+      device_src = false;
+      break;
+    case ORBX_DBG_CANDIDATES:
+      src = h->cand.p + (size_t)image * G.cand_total;
+      bytes = sizeof(uint32_t) * G.cand_total;
+      break;
+    case ORBX_DBG_OCT_COUNTS:
+      src = h->oct_count.p + (size_t)image * G.nlevels;
+      bytes = sizeof(int) * G.nlevels;
+      break;
+    case ORBX_DBG_OCT_OUT:
+      src = h->oct.p + (size_t)image * G.oct_total;
+      bytes = sizeof(uint32_t) * G.oct_total;
+      break;
+    case ORBX_DBG_LEVEL_INFO:
+      for (int l = 0; l < G.nlevels; l++) {
+        const LevelGeom& L = G.lv[l];
+        int v[8] = {L.w, L.h, L.cell_begin, L.cell_end, L.oct_off, L.oct_cap, L.nfeat, L.nIni};
+        host.insert(host.end(), v, v + 8);
+      }
+      device_src = false;
+      break;
+    default:
+      return ORBX_ERR_ARG;
+  }
+  if (!device_src) {
+    bytes = host.size() * sizeof(int);
+    if (dst) std::memcpy(dst, host.data(), std::min(bytes, cap));
+    return (long long)bytes;
+  }
+  if (dst && cap) {
+    if (hipMemcpy(dst, src, std::min(bytes, cap), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_ERR_HIP;
+  }
+  return (long long)bytes;
+}

@@ -1,0 +1,762 @@
+// extract.hip -- ORB extraction (ORBextractor::operator(), src/ORBextractor.cc:1138-1211)
+// as a batched chain of gfx950 kernels.  One launch per stage covers every
+// image of the batch:
+//
+//   k_resize   x(nlevels-1)  ComputePyramid            src/ORBextractor.cc:1215-1250
+//   k_fast                   per-cell FAST + fallback  src/ORBextractor.cc:843-915
+//   k_blur                   GaussianBlur 7x7 s=2      src/ORBextractor.cc:1186-1190
+//   k_octree                 DistributeOctTree         src/ORBextractor.cc:562-815
+//   k_describe               IC_Angle + rBRIEF + scale src/ORBextractor.cc:77-152,1192-1207
+//
+// Integer/byte work throughout (HBM-bound); the only float math is the
+// orientation/rotation and it is compiled without FP contraction so it rounds
+// exactly like the CPU path.
+#include <hip/hip_runtime.h>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+
+namespace orbx {
+
+__constant__ int8_t c_pattern[1024] = {
+#include "brief_pattern_31.inc"
+};
+__constant__ int c_umax[16];
+
+constexpr int BS = 256;
+
+// ---------------------------------------------------------------- block scan
+// Exclusive scan of a[0..n) in LDS (in place); returns the total. All threads call.
+__device__ int block_exclusive_scan(int* a, int n) {
+  __shared__ int wsum[BS / 64 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int chunk = (n + BS - 1) / BS;
+  const int b = tid * chunk, e = min(n, b + chunk);
+  int local = 0;
+  for (int i = b; i < e; i++) local += a[i];
+  int incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    int s = 0;
+    for (int w = 0; w < BS / 64; w++) {
+      int t = wsum[w];
+      wsum[w] = s;
+      s += t;
+    }
+    wsum[BS / 64] = s;
+  }
+  __syncthreads();
+  int run = wsum[wid] + incl - local;
+  for (int i = b; i < e; i++) {
+    int v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  const int total = wsum[BS / 64];
+  __syncthreads();
+  return total;
+}
+
+__device__ int block_sum(int v) {
+  __shared__ int red[BS / 64];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int s = 0;
+  for (int w = 0; w < BS / 64; w++) s += red[w];
+  __syncthreads();
+  return s;
+}
+
+// ------------------------------------------------------------------ resize
+// cv::resize INTER_LINEAR 8U (OpenCV 3.2 fixed point, coefficient tables built
+// on the host exactly as resizeGeneric_ does).  One thread per output pixel.
+__global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, const ResizeX* __restrict__ xt,
+                                               const ResizeY* __restrict__ yt, BatchPtrs B, int l) {
+  const LevelGeom& L = G->lv[l];
+  const LevelGeom& S = G->lv[l - 1];
+  const int img = blockIdx.z;
+  const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (dx >= L.w || dy >= L.h) return;
+  const uint8_t* src = level_ptr(*G, B, img, l - 1);
+  uint8_t* dst = B.pyr + (size_t)img * G->pyr_bytes + L.off;
+  const ResizeX X = xt[L.xtab_off + dx];
+  const ResizeY Y = yt[L.ytab_off + dy];
+  const uint8_t* r0 = src + (size_t)Y.sy0 * S.w;
+  const uint8_t* r1 = src + (size_t)Y.sy1 * S.w;
+  const int h0 = r0[X.sx0] * X.a0 + r0[X.sx1] * X.a1;
+  const int h1 = r1[X.sx0] * X.a0 + r1[X.sx1] * X.a1;
+  const int v = (((Y.b0 * (h0 >> 4)) >> 16) + ((Y.b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+  dst[(size_t)dy * L.w + dx] = (uint8_t)v;
+}
+
+// ----------------------------------------------------------------- blur
+// GaussianBlur(7x7, sigma=2, BORDER_REFLECT_101), OpenCV 3.2 8U fixed point:
+// integer kernel {k0..k6} (x256), exact integer row+column sums, then
+// rint(acc/65536) on SIMD column groups (x < w&~3) and (acc+2^15)>>16 on the
+// scalar tail; saturate to u8.  64x16 output tile per block, staged in LDS.
+__constant__ int c_gauss[7];
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+  if (n == 1) return 0;
+  while ((unsigned)p >= (unsigned)n) p = p < 0 ? -p : 2 * n - 2 - p;
+  return p;
+}
+
+__global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
+                                             BatchPtrs B) {
+  __shared__ uint8_t tin[kBlurTileH + 6][kBlurTileW + 8];
+  __shared__ int trow[kBlurTileH + 6][kBlurTileW];
+  const int tile = blockIdx.x, img = blockIdx.y;
+  const int l = tile_level[tile];
+  const LevelGeom& L = G->lv[l];
+  const int t = tile - L.tile_begin;
+  const int x0 = (t % L.tiles_x) * kBlurTileW, y0 = (t / L.tiles_x) * kBlurTileH;
+  const uint8_t* src = level_ptr(*G, B, img, l);
+  uint8_t* dst = B.blur + (size_t)img * G->blur_bytes + L.boff;
+  const int w = L.w, h = L.h;
+  for (int q = threadIdx.x; q < (kBlurTileH + 6) * (kBlurTileW + 6); q += BS) {
+    const int ty = q / (kBlurTileW + 6), tx = q % (kBlurTileW + 6);
+    const int sy = reflect101(y0 + ty - 3, h), sx = reflect101(x0 + tx - 3, w);
+    tin[ty][tx] = src[(size_t)sy * w + sx];
+  }
+  __syncthreads();
+  const int k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
+  for (int q = threadIdx.x; q < (kBlurTileH + 6) * kBlurTileW; q += BS) {
+    const int ty = q / kBlurTileW, tx = q % kBlurTileW;
+    const uint8_t* r = &tin[ty][tx];
+    trow[ty][tx] = k3 * r[3] + k2 * (r[2] + r[4]) + k1 * (r[1] + r[5]) + k0 * (r[0] + r[6]);
+  }
+  __syncthreads();
+  const int simd_w = w & ~3;
+  const int tx = threadIdx.x & 63;
+  const int x = x0 + tx;
+  if (x >= w) return;
+  for (int ty = threadIdx.x >> 6; ty < kBlurTileH; ty += BS / 64) {
+    const int y = y0 + ty;
+    if (y >= h) break;
+    const int acc = k3 * trow[ty + 3][tx] + k2 * (trow[ty + 2][tx] + trow[ty + 4][tx]) +
+                    k1 * (trow[ty + 1][tx] + trow[ty + 5][tx]) + k0 * (trow[ty][tx] + trow[ty + 6][tx]);
+    int v;
+    if (x < simd_w)
+      v = (int)__builtin_rintf((float)acc * (1.0f / 65536.0f));
+    else
+      v = (acc + (1 << 15)) >> 16;
+    dst[(size_t)y * w + x] = (uint8_t)min(max(v, 0), 255);
+  }
+}
+
+// ------------------------------------------------------------------- FAST
+// One block per FAST cell window.  cv::FAST(window, th, nonmax) semantics
+// (OpenCV 3.2 FAST_t<16>): a pixel of the detection region is a corner at
+// threshold t iff >= 9 contiguous ring pixels are all > v+t or all < v-t;
+// its cornerScore<16> S satisfies corner_t <=> S >= t, so one score map serves
+// both thresholds.  NMS is strict against the 8 neighbours inside the region
+// (0 outside).  If nothing survives at iniThFAST the cell uses minThFAST
+// (src/ORBextractor.cc:892-900).  Survivors are written in row-major order.
+constexpr int kMaxCell = 64;  // wCell,hCell <= 60
+
+__device__ __forceinline__ int fast_score(const uint8_t* t, int ts, int tlo) {
+  const int v = t[0];
+  int p[16];
+  p[0] = t[3 * ts];
+  p[1] = t[3 * ts + 1];
+  p[2] = t[2 * ts + 2];
+  p[3] = t[ts + 3];
+  p[4] = t[3];
+  p[5] = t[-ts + 3];
+  p[6] = t[-2 * ts + 2];
+  p[7] = t[-3 * ts + 1];
+  p[8] = t[-3 * ts];
+  p[9] = t[-3 * ts - 1];
+  p[10] = t[-2 * ts - 2];
+  p[11] = t[-ts - 3];
+  p[12] = t[-3];
+  p[13] = t[ts - 3];
+  p[14] = t[2 * ts - 2];
+  p[15] = t[3 * ts - 1];
+  uint32_t dark = 0, bright = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    dark |= (uint32_t)(p[k] < v - tlo) << k;
+    bright |= (uint32_t)(p[k] > v + tlo) << k;
+  }
+  auto run9 = [](uint32_t m) {
+    m |= m << 16;
+    uint32_t r = m & (m >> 1);
+    r &= r >> 2;
+    r &= r >> 4;
+    r &= m >> 8;
+    return r != 0;
+  };
+  if (!run9(dark) && !run9(bright)) return -1;
+  int d[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) d[k] = v - p[k];
+  int a0 = -1000, b0 = 1000;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    int mn = d[k], mx = d[k];
+#pragma unroll
+    for (int j = 1; j < 9; j++) {
+      mn = min(mn, d[(k + j) & 15]);
+      mx = max(mx, d[(k + j) & 15]);
+    }
+    a0 = max(a0, mn);
+    b0 = min(b0, mx);
+  }
+  return max(a0, -b0) - 1;
+}
+
+__global__ __launch_bounds__(BS) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
+                                             BatchPtrs B) {
+  __shared__ uint8_t tile[(kMaxCell + 6) * (kMaxCell + 6)];
+  __shared__ int16_t sc[kMaxCell * kMaxCell];
+  __shared__ int wtot[BS / 64 + 1];
+  const int cell = blockIdx.x, img = blockIdx.y;
+  const CellInfo c = cells[cell];
+  const LevelGeom& L = G->lv[c.level];
+  const uint8_t* base = level_ptr(*G, B, img, c.level);
+  const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TW = W + 6, TH = H + 6;
+  for (int q = threadIdx.x; q < TW * TH; q += BS) {
+    const int ty = q / TW, tx = q - ty * TW;
+    tile[q] = base[(size_t)(c.y0 - 3 + ty) * L.w + (c.x0 - 3 + tx)];
+  }
+  __syncthreads();
+  const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255);
+  const int tlo = min(ini, mint);
+  const int npx = W * H;
+  for (int q = threadIdx.x; q < npx; q += BS) {
+    const int y = q / W, x = q - y * W;
+    const int s = fast_score(&tile[(y + 3) * TW + x + 3], TW, tlo);
+    sc[q] = (int16_t)(s >= tlo ? s : -1);
+  }
+  __syncthreads();
+  auto kept = [&](int q, int t) -> bool {
+    const int s = sc[q];
+    if (s < t) return false;
+    const int y = q / W, x = q - y * W;
+    for (int dy = -1; dy <= 1; dy++) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= H) continue;
+      for (int dx = -1; dx <= 1; dx++) {
+        const int xx = x + dx;
+        if ((dx == 0 && dy == 0) || xx < 0 || xx >= W) continue;
+        const int n = sc[yy * W + xx];
+        if (n >= t && !(s > n)) return false;
+      }
+    }
+    return true;
+  };
+  int cnt_ini = 0;
+  for (int q = threadIdx.x; q < npx; q += BS) cnt_ini += kept(q, ini) ? 1 : 0;
+  cnt_ini = block_sum(cnt_ini);
+  const int t = cnt_ini > 0 ? ini : mint;
+  // row-major compaction: contiguous chunk per thread
+  const int chunk = (npx + BS - 1) / BS;
+  const int qb = threadIdx.x * chunk, qe = min(npx, qb + chunk);
+  int mine = 0;
+  for (int q = qb; q < qe; q++) mine += kept(q, t) ? 1 : 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wtot[wid] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < BS / 64; w++) {
+      int v = wtot[w];
+      wtot[w] = s;
+      s += v;
+    }
+    wtot[BS / 64] = s;
+  }
+  __syncthreads();
+  int pos = wtot[wid] + incl - mine;
+  uint32_t* out = B.cand + (size_t)img * G->cand_total + c.cand_off;
+  for (int q = qb; q < qe; q++) {
+    if (!kept(q, t)) continue;
+    const int y = q / W, x = q - y * W;
+    if (pos < c.cap)
+      out[pos] = ((uint32_t)sc[q] << 24) | ((uint32_t)(c.y0 + y) << 12) | (uint32_t)(c.x0 + x);
+    pos++;
+  }
+  if (threadIdx.x == 0) B.cell_count[(size_t)img * G->ncells + cell] = min(wtot[BS / 64], c.cap);
+}
+
+// ----------------------------------------------------------------- octree
+// One block per (level, image).  Restates DistributeOctTree as rounds over an
+// explicit node list held in LDS (list order == the reference's std::list
+// order): each round splits the selected nodes, pushes their non-empty
+// children to the front (reversed, as successive push_front do) and keeps the
+// rest in order.  Keypoints never move; each keeps the index of its node.
+// Phase 2 sorts (size, creation sequence) descending -- the reference sorts
+// by (size, heap pointer); DESIGN.md §Parity documents the tie-break.
+struct OctSmem {
+  int16_t* x0;  // [2*NC] double-buffered node list
+  int16_t* y0;
+  int16_t* x1;
+  int16_t* y1;
+  int* cnt;
+  int* seq;
+  int* ccnt;       // [NC*4]
+  int16_t* cidx;   // [NC*4]
+  int16_t* nidx;   // [NC]
+  int* sa;         // [NC]
+  int* sb;         // [NC]
+  uint64_t* key;   // [NP2] (also best)
+  int* cpre;       // [cell_cap+1]
+  int* ctrl;       // [8]
+};
+
+__host__ __device__ inline int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+__host__ __device__ inline size_t octree_smem_bytes(int NC, int cell_cap) {
+  const int NP2 = next_pow2(NC);
+  size_t b = 0;
+  b += 2 * 4 * NC * sizeof(int16_t);
+  b += 2 * 2 * NC * sizeof(int);
+  b += NC * 4 * sizeof(int);
+  b += NC * 4 * sizeof(int16_t);
+  b += NC * sizeof(int16_t);
+  b += 2 * NC * sizeof(int);
+  b = (b + 7) & ~(size_t)7;
+  b += (size_t)NP2 * sizeof(uint64_t);
+  b += (cell_cap + 1) * sizeof(int);
+  b += 8 * sizeof(int);
+  return b;
+}
+
+__device__ __forceinline__ void bitonic_sort_desc(uint64_t* k, int n) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < n / 2; i += BS) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const uint64_t a = k[lo], b = k[hi];
+        if (desc ? (a < b) : (a > b)) {
+          k[lo] = b;
+          k[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(BS) void k_octree(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
+                                               BatchPtrs B) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int l = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const LevelGeom& L = G->lv[l];
+  const int NC = G->node_cap;
+  const int NP2 = next_pow2(NC);
+  OctSmem s;
+  {
+    unsigned char* p = smem_raw;
+    s.x0 = (int16_t*)p; p += NC * 4;
+    s.y0 = (int16_t*)p; p += NC * 4;
+    s.x1 = (int16_t*)p; p += NC * 4;
+    s.y1 = (int16_t*)p; p += NC * 4;
+    s.cnt = (int*)p; p += NC * 8;
+    s.seq = (int*)p; p += NC * 8;
+    s.ccnt = (int*)p; p += NC * 16;
+    s.cidx = (int16_t*)p; p += NC * 8;
+    s.nidx = (int16_t*)p; p += NC * 2;
+    s.sa = (int*)p; p += NC * 4;
+    s.sb = (int*)p; p += NC * 4;
+    p = (unsigned char*)(((uintptr_t)p + 7) & ~(uintptr_t)7);
+    s.key = (uint64_t*)p; p += (size_t)NP2 * 8;
+    s.cpre = (int*)p; p += (G->cell_cap + 1) * 4;
+    s.ctrl = (int*)p;
+  }
+  uint32_t* oct_out = B.oct + (size_t)img * G->oct_total + L.oct_off;
+  int* oct_cnt = B.oct_count + (size_t)img * G->nlevels + l;
+  const size_t kbase = (size_t)img * G->cand_total + L.cand_begin;
+  uint32_t* kpos = B.kpos + kbase;
+  int* knode = B.knode + kbase;
+  uint8_t* kdig = B.kdig + kbase;
+
+  // 1. candidates of this level in vToDistributeKeys order (cells row-major)
+  const int ncl = L.cell_end - L.cell_begin;
+  for (int c = tid; c < ncl; c += BS) s.cpre[c] = B.cell_count[(size_t)img * G->ncells + L.cell_begin + c];
+  __syncthreads();
+  const int T = block_exclusive_scan(s.cpre, ncl);
+  if (tid == 0) s.cpre[ncl] = T;
+  if (T == 0) {
+    if (tid == 0) *oct_cnt = 0;
+    return;
+  }
+  const int nIni = L.nIni;
+  const float hX = L.hX;
+  const int minBX = L.minBX, minBY = L.minBY;
+  for (int i = tid; i < nIni; i += BS) s.ccnt[i] = 0;
+  __syncthreads();
+  const uint32_t* cand = B.cand + (size_t)img * G->cand_total;
+  for (int k = tid; k < T; k += BS) {
+    int lo = 0, hi = ncl - 1;  // last c with cpre[c] <= k
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s.cpre[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    const CellInfo& ci = cells[L.cell_begin + lo];
+    const uint32_t v = cand[ci.cand_off + (k - s.cpre[lo])];
+    const int xr = (int)(v & 0xFFF) - minBX, yr = (int)((v >> 12) & 0xFFF) - minBY;
+    kpos[k] = (v & 0xFF000000u) | ((uint32_t)yr << 12) | (uint32_t)xr;
+    int root = (int)((float)xr / hX);
+    root = min(max(root, 0), nIni - 1);
+    knode[k] = root;
+    atomicAdd(&s.ccnt[root], 1);
+  }
+  __syncthreads();
+  // 2. roots -> list (empty roots erased, src/ORBextractor.cc:604-615)
+  for (int i = tid; i < nIni; i += BS) s.sa[i] = s.ccnt[i] > 0 ? 1 : 0;
+  __syncthreads();
+  int S = block_exclusive_scan(s.sa, nIni);
+  for (int i = tid; i < nIni; i += BS) {
+    if (s.ccnt[i] > 0) {
+      const int ni = s.sa[i];
+      s.x0[ni] = (int16_t)(int)(hX * (float)i);
+      s.x1[ni] = (int16_t)(int)(hX * (float)(i + 1));
+      s.y0[ni] = 0;
+      s.y1[ni] = (int16_t)(L.maxBY - minBY);
+      s.cnt[ni] = s.ccnt[i];
+      s.seq[ni] = i;
+      s.nidx[i] = (int16_t)ni;
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < T; k += BS) knode[k] = s.nidx[knode[k]];
+  int cur = 0;
+  int seqBase = nIni;
+  int phase = 1;
+  const int N = L.nfeat;
+  for (int round = 0; round < 256; round++) {
+    __syncthreads();
+    const int nb = cur ^ 1;
+    for (int i = tid; i < S * 4; i += BS) s.ccnt[i] = 0;
+    __syncthreads();
+    // kp pass A: child digit of every keypoint whose node splits (count > 1)
+    for (int k = tid; k < T; k += BS) {
+      const int n = knode[k];
+      if ((s.cnt + cur * NC)[n] > 1) {
+        const int nx0 = (s.x0 + cur * NC)[n], ny0 = (s.y0 + cur * NC)[n];
+        const int hx = (int)__builtin_ceilf((float)((s.x1 + cur * NC)[n] - nx0) / 2);
+        const int hy = (int)__builtin_ceilf((float)((s.y1 + cur * NC)[n] - ny0) / 2);
+        const uint32_t v = kpos[k];
+        const float fx = (float)(int)(v & 0xFFF), fy = (float)(int)((v >> 12) & 0xFFF);
+        const int d = (fx < (float)(nx0 + hx) ? 0 : 1) + (fy < (float)(ny0 + hy) ? 0 : 2);
+        kdig[k] = (uint8_t)d;
+        atomicAdd(&s.ccnt[n * 4 + d], 1);
+      }
+    }
+    __syncthreads();
+    int C, Snew;
+    if (phase == 1) {
+      // split every node with > 1 keypoint, in list order
+      if (tid == 0) s.ctrl[0] = 0;
+      for (int i = tid; i < S; i += BS) {
+        const bool split = (s.cnt + cur * NC)[i] > 1;
+        int nc = 0;
+        if (split)
+          for (int d = 0; d < 4; d++) nc += s.ccnt[i * 4 + d] > 0;
+        s.sa[i] = nc;
+        s.sb[i] = split ? 0 : 1;
+      }
+      __syncthreads();
+      C = block_exclusive_scan(s.sa, S);
+      const int Sg = block_exclusive_scan(s.sb, S);
+      int nexp = 0;
+      for (int i = tid; i < S; i += BS) {
+        if ((s.cnt + cur * NC)[i] > 1) {
+          const int nx0 = (s.x0 + cur * NC)[i], ny0 = (s.y0 + cur * NC)[i], nx1 = (s.x1 + cur * NC)[i], ny1 = (s.y1 + cur * NC)[i];
+          const int hx = (int)__builtin_ceilf((float)(nx1 - nx0) / 2);
+          const int hy = (int)__builtin_ceilf((float)(ny1 - ny0) / 2);
+          int rank = 0;
+          for (int d = 0; d < 4; d++) {
+            const int cc = s.ccnt[i * 4 + d];
+            if (cc == 0) continue;
+            const int p = s.sa[i] + rank++;
+            const int ni = C - 1 - p;
+            (s.x0 + nb * NC)[ni] = (int16_t)((d & 1) ? nx0 + hx : nx0);
+            (s.x1 + nb * NC)[ni] = (int16_t)((d & 1) ? nx1 : nx0 + hx);
+            (s.y0 + nb * NC)[ni] = (int16_t)((d & 2) ? ny0 + hy : ny0);
+            (s.y1 + nb * NC)[ni] = (int16_t)((d & 2) ? ny1 : ny0 + hy);
+            (s.cnt + nb * NC)[ni] = cc;
+            (s.seq + nb * NC)[ni] = seqBase + p;
+            s.cidx[i * 4 + d] = (int16_t)ni;
+            nexp += cc > 1;
+          }
+        } else {
+          const int ni = C + s.sb[i];
+          (s.x0 + nb * NC)[ni] = (s.x0 + cur * NC)[i];
+          (s.x1 + nb * NC)[ni] = (s.x1 + cur * NC)[i];
+          (s.y0 + nb * NC)[ni] = (s.y0 + cur * NC)[i];
+          (s.y1 + nb * NC)[ni] = (s.y1 + cur * NC)[i];
+          (s.cnt + nb * NC)[ni] = (s.cnt + cur * NC)[i];
+          (s.seq + nb * NC)[ni] = (s.seq + cur * NC)[i];
+          s.nidx[i] = (int16_t)ni;
+        }
+      }
+      nexp = block_sum(nexp);
+      for (int k = tid; k < T; k += BS) {
+        const int n = knode[k];
+        knode[k] = (s.cnt + cur * NC)[n] > 1 ? s.cidx[n * 4 + kdig[k]] : s.nidx[n];
+      }
+      Snew = C + Sg;
+      seqBase += C;
+      const bool finish = Snew >= N || Snew == S;
+      S = Snew;
+      cur = nb;
+      if (finish) break;
+      if (Snew + 3 * nexp > N) phase = 2;
+    } else {
+      // phase 2: split the largest (size, seq) first until the list reaches N
+      for (int i = tid; i < S; i += BS) s.sa[i] = (s.cnt + cur * NC)[i] > 1 ? 1 : 0;
+      __syncthreads();
+      const int M = block_exclusive_scan(s.sa, S);
+      const int P2 = next_pow2(max(M, 2));
+      for (int i = tid; i < P2; i += BS) s.key[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < S; i += BS)
+        if ((s.cnt + cur * NC)[i] > 1)
+          s.key[s.sa[i]] = ((uint64_t)(s.cnt + cur * NC)[i] << 43) | ((uint64_t)(s.seq + cur * NC)[i] << 13) | (uint64_t)i;
+      __syncthreads();
+      bitonic_sort_desc(s.key, P2);
+      if (tid == 0) s.ctrl[1] = M - 1;
+      for (int j = tid; j < M; j += BS) {
+        const int n = (int)(s.key[j] & 0x1FFF);
+        int nc = 0;
+        for (int d = 0; d < 4; d++) nc += s.ccnt[n * 4 + d] > 0;
+        s.sb[j] = nc - 1;
+      }
+      __syncthreads();
+      // inclusive prefix of growth; first j reaching N
+      block_exclusive_scan(s.sb, M);  // exclusive
+      for (int j = tid; j < M; j += BS) {
+        const int n = (int)(s.key[j] & 0x1FFF);
+        int nc = 0;
+        for (int d = 0; d < 4; d++) nc += s.ccnt[n * 4 + d] > 0;
+        if (S + s.sb[j] + (nc - 1) >= N) atomicMin(&s.ctrl[1], j);
+      }
+      __syncthreads();
+      const int m = s.ctrl[1];
+      // children positions in processing order j = 0..m
+      for (int j = tid; j < M; j += BS) {
+        int nc = 0;
+        if (j <= m) {
+          const int n = (int)(s.key[j] & 0x1FFF);
+          for (int d = 0; d < 4; d++) nc += s.ccnt[n * 4 + d] > 0;
+        }
+        s.sb[j] = nc;
+      }
+      for (int i = tid; i < S; i += BS) s.nidx[i] = -1;  // -1: processed marker set below
+      __syncthreads();
+      C = block_exclusive_scan(s.sb, M);
+      for (int j = tid; j <= m; j += BS) {
+        const int n = (int)(s.key[j] & 0x1FFF);
+        s.nidx[n] = -2;  // processed
+      }
+      __syncthreads();
+      for (int i = tid; i < S; i += BS) s.sa[i] = s.nidx[i] == -2 ? 0 : 1;
+      __syncthreads();
+      const int rest = block_exclusive_scan(s.sa, S);
+      for (int j = tid; j <= m; j += BS) {
+        const int i = (int)(s.key[j] & 0x1FFF);
+        const int nx0 = (s.x0 + cur * NC)[i], ny0 = (s.y0 + cur * NC)[i], nx1 = (s.x1 + cur * NC)[i], ny1 = (s.y1 + cur * NC)[i];
+        const int hx = (int)__builtin_ceilf((float)(nx1 - nx0) / 2);
+        const int hy = (int)__builtin_ceilf((float)(ny1 - ny0) / 2);
+        int rank = 0;
+        for (int d = 0; d < 4; d++) {
+          const int cc = s.ccnt[i * 4 + d];
+          if (cc == 0) continue;
+          const int p = s.sb[j] + rank++;
+          const int ni = C - 1 - p;
+          (s.x0 + nb * NC)[ni] = (int16_t)((d & 1) ? nx0 + hx : nx0);
+          (s.x1 + nb * NC)[ni] = (int16_t)((d & 1) ? nx1 : nx0 + hx);
+          (s.y0 + nb * NC)[ni] = (int16_t)((d & 2) ? ny0 + hy : ny0);
+          (s.y1 + nb * NC)[ni] = (int16_t)((d & 2) ? ny1 : ny0 + hy);
+          (s.cnt + nb * NC)[ni] = cc;
+          (s.seq + nb * NC)[ni] = seqBase + p;
+          s.cidx[i * 4 + d] = (int16_t)ni;
+        }
+      }
+      for (int i = tid; i < S; i += BS) {
+        if (s.nidx[i] == -2) continue;
+        const int ni = C + s.sa[i];
+        (s.x0 + nb * NC)[ni] = (s.x0 + cur * NC)[i];
+        (s.x1 + nb * NC)[ni] = (s.x1 + cur * NC)[i];
+        (s.y0 + nb * NC)[ni] = (s.y0 + cur * NC)[i];
+        (s.y1 + nb * NC)[ni] = (s.y1 + cur * NC)[i];
+        (s.cnt + nb * NC)[ni] = (s.cnt + cur * NC)[i];
+        (s.seq + nb * NC)[ni] = (s.seq + cur * NC)[i];
+        s.nidx[i] = (int16_t)ni;
+      }
+      __syncthreads();
+      for (int k = tid; k < T; k += BS) {
+        const int n = knode[k];
+        // processed nodes' slots were overwritten? no: nidx[n]==-2 only for processed
+        const int ni = s.nidx[n];
+        knode[k] = ni == -2 ? s.cidx[n * 4 + kdig[k]] : ni;
+      }
+      Snew = C + rest;
+      seqBase += C;
+      const bool finish = Snew >= N || Snew == S;
+      S = Snew;
+      cur = nb;
+      if (finish) break;
+    }
+  }
+  __syncthreads();
+  // 3. best response per node: max score, then lowest candidate index
+  for (int i = tid; i < S; i += BS) s.key[i] = 0;
+  __syncthreads();
+  for (int k = tid; k < T; k += BS) {
+    const uint32_t v = kpos[k];
+    const uint32_t x = (v & 0xFFF) + minBX, y = ((v >> 12) & 0xFFF) + minBY;
+    const uint64_t key = ((uint64_t)(v >> 24) << 56) | ((uint64_t)(0xFFFFFFu - (uint32_t)k) << 24) |
+                         (uint64_t)((y << 12) | x);
+    atomicMax((unsigned long long*)&s.key[knode[k]], (unsigned long long)key);
+  }
+  __syncthreads();
+  const int nout = min(S, L.oct_cap);
+  for (int i = tid; i < nout; i += BS) {
+    const uint64_t key = s.key[i];
+    oct_out[i] = ((uint32_t)(key >> 56) << 24) | (uint32_t)(key & 0xFFFFFF);
+  }
+  if (tid == 0) *oct_cnt = nout;
+}
+
+// --------------------------------------------------------------- describe
+// One wave per keypoint: IC_Angle on the raw level (src/ORBextractor.cc:77-105),
+// computeOrbDescriptor on the blurred level (:110-152), then the keypoint
+// record in level-major output order with pt *= mvScaleFactor[l] (:1201-1207).
+__global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
+                                                 orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                 int32_t* __restrict__ counts, int kp_cap) {
+  const int img = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
+  const int nl = G->nlevels;
+  int pre[kMaxLevelsPlan + 1];
+  pre[0] = 0;
+  for (int l = 0; l < nl; l++) pre[l + 1] = pre[l] + B.oct_count[(size_t)img * nl + l];
+  const int total = pre[nl];
+  if (blockIdx.x == 0 && threadIdx.x == 0) counts[img] = total;
+  if (i >= total) return;
+  int l = 0;
+  while (pre[l + 1] <= i) l++;
+  const LevelGeom& L = G->lv[l];
+  const uint32_t v = B.oct[(size_t)img * G->oct_total + L.oct_off + (i - pre[l])];
+  const int x = v & 0xFFF, y = (v >> 12) & 0xFFF, score = v >> 24;
+  const int w = L.w;
+  // IC_Angle: lanes 0..61 -> column u = lane%31-15, rows v in [-15,0] or [1,15]
+  const uint8_t* raw = level_ptr(*G, B, img, l);
+  int m01 = 0, m10 = 0;
+  if (lane < 62) {
+    const int u = (lane % 31) - 15;
+    const int au = u < 0 ? -u : u;
+    const int vb = lane < 31 ? -15 : 1, ve = lane < 31 ? 0 : 15;
+    for (int vv = vb; vv <= ve; vv++) {
+      const int av = vv < 0 ? -vv : vv;
+      if (au > c_umax[av]) continue;
+      const int I = raw[(size_t)(y + vv) * w + (x + u)];
+      m10 += u * I;
+      m01 += vv * I;
+    }
+  }
+  m01 = wave_sum(m01);
+  m10 = wave_sum(m10);
+  const float angle = fast_atan2((float)m01, (float)m10);
+  const float factorPI = (float)(3.14159265358979323846 / 180.f);
+  float sn, cs;
+  sincos_det(angle * factorPI, &sn, &cs);
+  const float a = cs, b = sn;
+  const uint8_t* blur = B.blur + (size_t)img * G->blur_bytes + L.boff;
+  const uint8_t* center = blur + (size_t)y * w + x;
+  int bits = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int pair = lane * 4 + k;  // bit (pair & 7) of byte pair >> 3
+    int t[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const int idx = 4 * pair + 2 * e;
+      const float px = (float)c_pattern[idx], py = (float)c_pattern[idx + 1];
+      const int r = round_even(px * b + py * a);
+      const int c = round_even(px * a - py * b);
+      t[e] = center[r * w + c];
+    }
+    bits |= (t[0] < t[1]) << k;
+  }
+  const int other = __shfl_xor(bits, 1, 64);
+  uint8_t* d = desc + ((size_t)img * kp_cap + i) * 32;
+  if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(bits | (other << 4));
+  if (lane == 0) {
+    orbx_keypoint kp;
+    float fx = (float)x, fy = (float)y;
+    if (l != 0) {
+      fx *= L.scale;
+      fy *= L.scale;
+    }
+    kp.x = fx;
+    kp.y = fy;
+    kp.size = L.kp_size;
+    kp.angle = angle;
+    kp.response = (float)score;
+    kp.octave = l;
+    kp.class_id = -1;
+    kps[(size_t)img * kp_cap + i] = kp;
+  }
+}
+
+// ------------------------------------------------------------------ launch
+hipError_t upload_constants(const int* umax16, const int* gauss7) {
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax16, 16 * sizeof(int));
+  if (e != hipSuccess) return e;
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_gauss), gauss7, 7 * sizeof(int));
+}
+
+hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells,
+                                 const int* tile_level, const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B,
+                                 int n_img, orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap,
+                                 hipStream_t st) {
+  for (int l = 1; l < Gh.nlevels; l++) {
+    dim3 grid((Gh.lv[l].w + 63) / 64, (Gh.lv[l].h + 3) / 4, n_img);
+    hipLaunchKernelGGL(k_resize, grid, dim3(BS), 0, st, Gd, xt, yt, B, l);
+  }
+  if (Gh.ncells > 0) hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(BS), 0, st, Gd, cells, B);
+  else (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
+  hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
+  if (Gh.ncells > 0) {
+    const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap);
+    hipLaunchKernelGGL(k_octree, dim3(Gh.nlevels, n_img), dim3(BS), smem, st, Gd, cells, B);
+  }
+  const int nb = (Gh.max_kps + BS / 64 - 1) / (BS / 64);
+  hipLaunchKernelGGL(k_describe, dim3(max(nb, 1), n_img), dim3(BS), 0, st, Gd, B, kps, desc, counts, kp_cap);
+  return hipGetLastError();
+}
+
+size_t octree_smem_host(int NC, int cell_cap) { return octree_smem_bytes(NC, cell_cap); }
+
+hipError_t octree_set_smem_limit(size_t bytes) {
+  return hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+}  // namespace orbx

@@ -1,0 +1,107 @@
+// orbx_device.h -- device-side numerics shared by the HIP kernels.
+//
+// Everything here is compiled with -ffp-contract=off: every float/double
+// expression rounds exactly as written, so results equal the CPU restatement
+// of the reference (oracle/) bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace orbx {
+
+constexpr int kHalfPatch = 15;      // HALF_PATCH_SIZE, src/ORBextractor.cc:73
+constexpr int kEdgeThreshold = 19;  // EDGE_THRESHOLD, src/ORBextractor.cc:74
+constexpr int kMaxLevels = 16;
+
+// cvRound (SSE2 cvtss2si): round half to even.
+__device__ __forceinline__ int round_even(float v) { return (int)__builtin_rintf(v); }
+
+// fastAtan2 (OpenCV 3.2 core): degrees in [0,360).
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+  const float p1 = 0.9997878412794807f * (float)(180 / 3.14159265358979323846);
+  const float p3 = -0.3258083974640975f * (float)(180 / 3.14159265358979323846);
+  const float p5 = 0.1555786518463281f * (float)(180 / 3.14159265358979323846);
+  const float p7 = -0.04432655554792128f * (float)(180 / 3.14159265358979323846);
+  const float eps = (float)2.2204460492503131e-16;  // (float)DBL_EPSILON
+  float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + eps);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + eps);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+// Deterministic float sin/cos: double-precision Cody-Waite reduction + Taylor
+// polynomials, rounded once to float (same operation sequence as the CPU
+// restatement).
+__device__ __forceinline__ void sincos_det(float xf, float* s_out, float* c_out) {
+  const double x = (double)xf;
+  const double kInvPio2 = 6.36619772367581382433e-01;
+  const double kPio2Hi = 1.57079632673412561417e+00;
+  const double kPio2Lo = 6.07710050650619224932e-11;
+  double kd = __builtin_rint(x * kInvPio2);
+  int q = (int)kd;
+  double r = (x - kd * kPio2Hi) - kd * kPio2Lo;
+  double r2 = r * r;
+  double ps = 1.0 / 51090942171709440000.0;
+  ps = ps * r2 - 1.0 / 121645100408832000.0;
+  ps = ps * r2 + 1.0 / 355687428096000.0;
+  ps = ps * r2 - 1.0 / 1307674368000.0;
+  ps = ps * r2 + 1.0 / 6227020800.0;
+  ps = ps * r2 - 1.0 / 39916800.0;
+  ps = ps * r2 + 1.0 / 362880.0;
+  ps = ps * r2 - 1.0 / 5040.0;
+  ps = ps * r2 + 1.0 / 120.0;
+  ps = ps * r2 - 1.0 / 6.0;
+  double sr = r + r * (r2 * ps);
+  double pc = 1.0 / 2432902008176640000.0;
+  pc = pc * r2 - 1.0 / 6402373705728000.0;
+  pc = pc * r2 + 1.0 / 20922789888000.0;
+  pc = pc * r2 - 1.0 / 87178291200.0;
+  pc = pc * r2 + 1.0 / 479001600.0;
+  pc = pc * r2 - 1.0 / 3628800.0;
+  pc = pc * r2 + 1.0 / 40320.0;
+  pc = pc * r2 - 1.0 / 720.0;
+  pc = pc * r2 + 1.0 / 24.0;
+  pc = pc * r2 - 0.5;
+  double cr = 1.0 + r2 * pc;
+  double s, c;
+  switch (q & 3) {
+    case 0: s = sr; c = cr; break;
+    case 1: s = cr; c = -sr; break;
+    case 2: s = -sr; c = -cr; break;
+    default: s = -cr; c = sr; break;
+  }
+  *s_out = (float)s;
+  *c_out = (float)c;
+}
+
+// Hamming distance of two 256-bit descriptors held as 4 x u64.
+__device__ __forceinline__ int hamming256(const uint64_t a[4], const uint64_t b[4]) {
+  return __popcll(a[0] ^ b[0]) + __popcll(a[1] ^ b[1]) + __popcll(a[2] ^ b[2]) + __popcll(a[3] ^ b[3]);
+}
+
+// Wave (64-lane) reductions.
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint32_t w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+}  // namespace orbx

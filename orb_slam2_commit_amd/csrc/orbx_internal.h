@@ -1,0 +1,89 @@
+// orbx_internal.h -- geometry "plan" of one (width, height, params) extractor
+// configuration, laid out for the device, plus kernel launch entry points.
+//
+// HBM layout per image (all u8, row-major, stride = level width):
+//   level 0            : the caller's input image itself (never copied)
+//   pyramid  (levels>=1): pyr  + img*pyr_bytes  + lv[l].off
+//   blurred  (all levels): blur + img*blur_bytes + lv[l].boff
+//   FAST candidates     : cand + img*cand_total + cells[c].cand_off   (u32 score<<24|y<<12|x)
+//   octree output       : oct  + img*oct_total  + lv[l].oct_off        (same packing, list order)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbx.h"
+
+namespace orbx {
+
+constexpr int kMaxLevelsPlan = 16;
+constexpr int kEdgeThresholdHost = 19;  // EDGE_THRESHOLD, src/ORBextractor.cc:74
+
+struct LevelGeom {
+  int w, h;
+  long long off;    // offset of level in per-image pyramid buffer (levels >= 1)
+  long long boff;   // offset of level in per-image blurred buffer
+  int minBX, minBY, maxBX, maxBY;  // FAST border box, src/ORBextractor.cc:829-832
+  int cell_begin, cell_end;        // range in the cell table (row-major)
+  int cand_begin, cand_cap;        // candidate slots of the level in the per-image buffer
+  int nfeat;                       // mnFeaturesPerLevel[l]
+  int nIni;                        // octree root count, src/ORBextractor.cc:567
+  float hX;                        // root width
+  int oct_off, oct_cap;            // octree output slots
+  float scale;                     // mvScaleFactor[l]
+  float kp_size;                   // (float)(int)(PATCH_SIZE * scale)
+  int xtab_off, ytab_off;          // resize tables (levels >= 1)
+  int tile_begin, tiles_x, tiles_y;  // blur tiles
+};
+
+struct Geometry {
+  int nlevels, width, height;
+  int ini_th, min_th;
+  LevelGeom lv[kMaxLevelsPlan];
+  long long pyr_bytes, blur_bytes;
+  int ncells, cand_total, oct_total, max_kps, ntiles;
+  int node_cap;   // octree LDS node capacity (max over levels, multiple of 64)
+  int cell_cap;   // max cells in one level
+};
+
+struct CellInfo {
+  int16_t level, pad;
+  int16_t x0, y0, x1, y1;  // FAST detection region (inclusive, level coordinates)
+  int cand_off, cap;
+};
+
+struct ResizeX {  // horizontal tap of one output column
+  int sx0, sx1;
+  int16_t a0, a1;
+};
+struct ResizeY {
+  int sy0, sy1;
+  int16_t b0, b1;
+};
+
+constexpr int kBlurTileW = 64, kBlurTileH = 16;
+
+// Device pointers for one batch.
+struct BatchPtrs {
+  const uint8_t* in;
+  size_t in_pitch;
+  uint8_t* pyr;
+  uint8_t* blur;
+  uint32_t* cand;
+  int* cell_count;
+  uint32_t* kpos;   // octree scratch
+  int* knode;
+  uint8_t* kdig;
+  uint32_t* oct;
+  int* oct_count;
+};
+
+__host__ __device__ inline const uint8_t* level_ptr(const Geometry& G, const BatchPtrs& B, int img, int l) {
+  return l == 0 ? B.in + (size_t)img * B.in_pitch : B.pyr + (size_t)img * G.pyr_bytes + G.lv[l].off;
+}
+
+// Launchers (extract.hip). All asynchronous on `stream`.
+hipError_t launch_extract(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells, const ResizeX* xt,
+                          const ResizeY* yt, const BatchPtrs& B, int n_img, orbx_keypoint* kps,
+                          uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t stream);
+
+}  // namespace orbx

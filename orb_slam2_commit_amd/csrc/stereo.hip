@@ -1,0 +1,326 @@
+// stereo.hip -- Frame::ComputeStereoMatches (src/Frame.cc:547-788) batched over
+// stereo frames, plus batched ORBmatcher::DescriptorDistance
+// (src/ORBmatcher.cc:1844-1860).
+//
+//   k_stereo_prep     per frame: right keypoints sorted by (octave, y) -- replaces
+//                     the reference's row-band table (:564-590); the candidate
+//                     set of a left keypoint is then 3 contiguous ranges.
+//   k_stereo_match    one wave per left keypoint: band Hamming argmin (strict <,
+//                     lowest index), 11x11 SAD over +-5 px on the unblurred
+//                     pyramid level, parabola, depth (:600-770).
+//   k_stereo_finalize per frame: median SAD by 2-pass radix select, reject
+//                     SAD >= 1.5*1.4*median (:774-787).
+#include <hip/hip_runtime.h>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+#include "orbx_stereo.h"
+
+namespace orbx {
+
+constexpr int SBS = 256;
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+
+__global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A) {
+  __shared__ uint64_t keys[kMaxStereoKps];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int nR = min(A.nR[(size_t)f * A.n_stride_R], kMaxStereoKps);
+  const orbx_keypoint* kR = A.kpR + (size_t)f * A.kR_stride;
+  int P2 = 2;
+  while (P2 < nR) P2 <<= 1;
+  for (int i = tid; i < P2; i += SBS) {
+    uint64_t k = ~0ull;
+    if (i < nR) {
+      const orbx_keypoint kp = kR[i];
+      k = ((uint64_t)(uint32_t)kp.octave << 44) | ((uint64_t)fbits(kp.y) << 12) | (uint64_t)i;
+    }
+    keys[i] = k;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P2 / 2; i += SBS) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const uint64_t a = keys[lo], b = keys[hi];
+        if (asc ? (a > b) : (a < b)) {
+          keys[lo] = b;
+          keys[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  uint64_t* out = A.rkeys + (size_t)f * kMaxStereoKps;
+  for (int i = tid; i < nR; i += SBS) out[i] = keys[i];
+  // octave starts
+  int* os = A.oct_start + (size_t)f * (kMaxLevelsPlan + 1);
+  for (int o = tid; o <= A.nlevels; o += SBS) {
+    int lo = 0, hi = nR;  // first i with octave >= o
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((int)(keys[mid] >> 44) < o) lo = mid + 1; else hi = mid;
+    }
+    os[o] = lo;
+  }
+}
+
+constexpr int kKpsPerBlock = 128;
+
+__global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
+  __shared__ float ry[kMaxStereoKps];
+  __shared__ float rx[kMaxStereoKps];
+  __shared__ int16_t ridx[kMaxStereoKps];
+  __shared__ int ost[kMaxLevelsPlan + 1];
+  const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
+  const int base = blockIdx.x * kKpsPerBlock;
+  if (base >= nL) return;
+  const int nR = min(A.nR[(size_t)f * A.n_stride_R], kMaxStereoKps);
+  const orbx_keypoint* kR = A.kpR + (size_t)f * A.kR_stride;
+  const uint64_t* keys = A.rkeys + (size_t)f * kMaxStereoKps;
+  for (int i = tid; i < nR; i += SBS) {
+    const uint64_t k = keys[i];
+    const int idx = (int)(k & 0xFFF);
+    ry[i] = __uint_as_float((uint32_t)(k >> 12));
+    ridx[i] = (int16_t)idx;
+    rx[i] = kR[idx].x;
+  }
+  for (int o = tid; o <= G->nlevels; o += SBS) ost[o] = A.oct_start[(size_t)f * (kMaxLevelsPlan + 1) + o];
+  __syncthreads();
+  const orbx_keypoint* kL = A.kpL + (size_t)f * A.kL_stride;
+  const uint8_t* dL = A.dL + (size_t)f * A.kL_stride * 32;
+  const uint8_t* dR = A.dR + (size_t)f * A.kR_stride * 32;
+  const int limg = f * A.l_step + A.l_off, rimg = f * A.r_step + A.r_off;
+  const int nl = G->nlevels;
+  for (int iL = base + wid; iL < min(nL, base + kKpsPerBlock); iL += SBS / 64) {
+    const orbx_keypoint kp = kL[iL];
+    const int levelL = kp.octave;
+    const float vL = kp.y, uL = kp.x;
+    const int Y = (int)vL;
+    const float minU = uL - A.maxD, maxU = uL - A.minD;
+    float* outU = A.uR + (size_t)f * A.out_stride + iL;
+    float* outD = A.depth + (size_t)f * A.out_stride + iL;
+    int* outS = A.sad + (size_t)f * A.out_stride + iL;
+    if (lane == 0) {
+      *outU = -1.0f;
+      *outD = -1.0f;
+      *outS = -1;
+    }
+    if (maxU < 0) continue;
+    // candidate ranges per octave
+    int rb[3], re[3];
+    for (int q = 0; q < 3; q++) {
+      rb[q] = re[q] = 0;
+      const int o = levelL - 1 + q;
+      if (o < 0 || o >= nl) continue;
+      const float r = 2.0f * G->lv[o].scale;
+      int lo = ost[o], hi = ost[o + 1];
+      // first with ceil(y + r) >= Y
+      int a = lo, b = hi;
+      while (a < b) {
+        const int m = (a + b) >> 1;
+        if ((int)__builtin_ceilf(ry[m] + r) >= Y) b = m; else a = m + 1;
+      }
+      // first (from a) with floor(y - r) > Y
+      int c = a, d = hi;
+      while (c < d) {
+        const int m = (c + d) >> 1;
+        if ((int)__builtin_floorf(ry[m] - r) > Y) d = m; else c = m + 1;
+      }
+      rb[q] = a;
+      re[q] = c;
+    }
+    const int n0 = re[0] - rb[0], n1 = re[1] - rb[1], n2 = re[2] - rb[2];
+    const int K = n0 + n1 + n2;
+    uint64_t ld[4];
+    {
+      const uint64_t* p = (const uint64_t*)(dL + (size_t)iL * 32);
+      ld[0] = p[0]; ld[1] = p[1]; ld[2] = p[2]; ld[3] = p[3];
+    }
+    uint32_t best = 0xFFFFFFFFu;
+    for (int j = lane; j < K; j += 64) {
+      const int pos = j < n0 ? rb[0] + j : (j < n0 + n1 ? rb[1] + (j - n0) : rb[2] + (j - n0 - n1));
+      const float uR = rx[pos];
+      if (!(uR >= minU && uR <= maxU)) continue;
+      const int idx = ridx[pos];
+      const uint64_t* p = (const uint64_t*)(dR + (size_t)idx * 32);
+      uint64_t rd[4] = {p[0], p[1], p[2], p[3]};
+      const int dist = hamming256(ld, rd);
+      const uint32_t key = ((uint32_t)dist << 12) | (uint32_t)idx;
+      best = key < best ? key : best;
+    }
+    best = wave_min_u32(best);
+    const int bestDist = best == 0xFFFFFFFFu ? 100 : (int)(best >> 12);
+    if (bestDist >= 75) continue;  // thOrbDist = (TH_HIGH+TH_LOW)/2 (also < TH_HIGH)
+    const int bestIdxR = (int)(best & 0xFFF);
+    // SAD refinement on the unblurred level kpL.octave
+    const LevelGeom& Lv = G->lv[levelL];
+    const float uR0 = kR[bestIdxR].x;
+    const float sf = A.inv_scale[levelL];
+    const float scaleduL = __builtin_roundf(kp.x * sf);
+    const float scaledvL = __builtin_roundf(kp.y * sf);
+    const float scaleduR0 = __builtin_roundf(uR0 * sf);
+    const int w = 5, L = 5;
+    const float iniu = scaleduR0 + L - w;
+    const float endu = scaleduR0 + L + w + 1;
+    if (iniu < 0 || endu >= Lv.w) continue;
+    // the reference asserts (cv::Mat::colRange/rowRange) when a patch leaves
+    // the level; unreachable for keypoints >= 16 px inside their level
+    if (scaleduR0 - 2 * w < 0 || scaledvL - w < 0 || scaledvL + w >= Lv.h || scaleduL - w < 0 ||
+        scaleduL + w >= Lv.w)
+      continue;
+    const uint8_t* imL = level_ptr(*G, A.BL, limg, levelL);
+    const uint8_t* imR = level_ptr(*G, A.BR, rimg, levelL);
+    const int lw = Lv.w;
+    const int cy = (int)scaledvL, cxL = (int)scaleduL, cxR0 = (int)scaleduR0;
+    int part = 0;
+    if (lane < 55) {
+      const int inc = lane % 11 - L;
+      const int g = lane / 11;
+      const int cL = imL[(size_t)cy * lw + cxL];
+      const int cx = cxR0 + inc;
+      const int cR = imR[(size_t)cy * lw + cx];
+      for (int dy = g; dy < 2 * w + 1; dy += 5) {
+        const uint8_t* pl = imL + (size_t)(cy - w + dy) * lw + cxL - w;
+        const uint8_t* pr = imR + (size_t)(cy - w + dy) * lw + cx - w;
+#pragma unroll
+        for (int dx = 0; dx < 2 * w + 1; dx++) {
+          const int a = (int)pl[dx] - cL, c = (int)pr[dx] - cR;
+          part += a > c ? a - c : c - a;
+        }
+      }
+    }
+    const int src = lane < 11 ? lane : 0;
+    int sad = __shfl(part, src, 64) + __shfl(part, src + 11, 64) + __shfl(part, src + 22, 64) +
+              __shfl(part, src + 33, 64) + __shfl(part, src + 44, 64);
+    // first strict minimum over inc = -5..5 (lanes 0..10)
+    uint32_t skey = lane < 11 ? ((uint32_t)sad << 4) | (uint32_t)lane : 0xFFFFFFFFu;
+    skey = wave_min_u32(skey);
+    const int bi = (int)(skey & 15);
+    const int bestSad = (int)(skey >> 4);
+    const int bestinc = bi - L;
+    if (bestinc == -L || bestinc == L) continue;
+    const float d1 = (float)__shfl(sad, bi - 1, 64);
+    const float d2 = (float)bestSad;
+    const float d3 = (float)__shfl(sad, bi + 1, 64);
+    const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+    if (deltaR < -1 || deltaR > 1) continue;
+    float bestuR = Lv.scale * ((float)scaleduR0 + (float)bestinc + deltaR);
+    float disparity = uL - bestuR;
+    if (disparity >= A.minD && disparity < A.maxD) {
+      if (disparity <= 0) {
+        disparity = 0.01f;
+        bestuR = uL - 0.01f;
+      }
+      if (lane == 0) {
+        *outD = A.bf / disparity;
+        *outU = bestuR;
+        *outS = bestSad;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(SBS) void k_stereo_finalize(StereoArgs A) {
+  __shared__ int hist[256];
+  __shared__ int sel[4];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
+  const int* sad = A.sad + (size_t)f * A.out_stride;
+  float* uR = A.uR + (size_t)f * A.out_stride;
+  float* depth = A.depth + (size_t)f * A.out_stride;
+  for (int i = tid; i < 256; i += SBS) hist[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < nL; i += SBS) {
+    const int s = sad[i];
+    if (s >= 0) atomicAdd(&hist[(s >> 8) & 255], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0;
+    for (int b = 0; b < 256; b++) n += hist[b];
+    sel[0] = n;
+    const int k = n / 2;
+    int acc = 0, b = 0;
+    for (; b < 256; b++) {
+      if (acc + hist[b] > k) break;
+      acc += hist[b];
+    }
+    sel[1] = b;
+    sel[2] = k - acc;
+  }
+  __syncthreads();
+  const int n = sel[0];
+  if (n == 0) {
+    if (tid == 0) A.nmatches[f] = 0;
+    return;
+  }
+  const int hb = sel[1], k2 = sel[2];
+  __syncthreads();
+  for (int i = tid; i < 256; i += SBS) hist[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < nL; i += SBS) {
+    const int s = sad[i];
+    if (s >= 0 && ((s >> 8) & 255) == hb) atomicAdd(&hist[s & 255], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0, b = 0;
+    for (; b < 256; b++) {
+      if (acc + hist[b] > k2) break;
+      acc += hist[b];
+    }
+    sel[3] = (hb << 8) | b;
+  }
+  __syncthreads();
+  const float median = (float)sel[3];
+  const float th = 1.5f * 1.4f * median;
+  int kept = 0;
+  for (int i = tid; i < nL; i += SBS) {
+    const int s = sad[i];
+    if (s < 0) continue;
+    if ((float)s >= th) {
+      uR[i] = -1.0f;
+      depth[i] = -1.0f;
+    } else {
+      kept++;
+    }
+  }
+  kept = wave_sum(kept);
+  __shared__ int ksum;
+  if (tid == 0) ksum = 0;
+  __syncthreads();
+  if ((tid & 63) == 0) atomicAdd(&ksum, kept);
+  __syncthreads();
+  if (tid == 0) A.nmatches[f] = ksum;
+}
+
+__global__ __launch_bounds__(SBS) void k_hamming(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int n,
+                                                 int32_t* __restrict__ out) {
+  const int i = blockIdx.x * SBS + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t* pa = (const uint64_t*)(a + (size_t)i * 32);
+  const uint64_t* pb = (const uint64_t*)(b + (size_t)i * 32);
+  uint64_t x[4] = {pa[0], pa[1], pa[2], pa[3]};
+  uint64_t y[4] = {pb[0], pb[1], pb[2], pb[3]};
+  out[i] = hamming256(x, y);
+}
+
+hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st) {
+  hipLaunchKernelGGL(k_stereo_prep, dim3(n_frames), dim3(SBS), 0, st, A);
+  const int nb = (maxL + kKpsPerBlock - 1) / kKpsPerBlock;
+  hipLaunchKernelGGL(k_stereo_match, dim3(max(nb, 1), n_frames), dim3(SBS), 0, st, A, Gd);
+  hipLaunchKernelGGL(k_stereo_finalize, dim3(n_frames), dim3(SBS), 0, st, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hamming, dim3((n + SBS - 1) / SBS), dim3(SBS), 0, st, a, b, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace orbx

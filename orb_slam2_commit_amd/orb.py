@@ -1,0 +1,189 @@
+"""Host-side mirror of the reference's hot-path classes over liborbx.so.
+
+Names, argument meaning and error behaviour follow the reference:
+
+* ``ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)``
+  (include/ORBextractor.h:77) with ``__call__(image, mask)`` ==
+  ``operator()`` (src/ORBextractor.cc:1138-1211), ``GetLevels``,
+  ``GetScaleFactor(s)``, ``GetInverseScaleFactors``, ``GetScaleSigmaSquares``,
+  ``GetInverseScaleSigmaSquares`` and ``mvImagePyramid``.
+* ``ORBmatcher.DescriptorDistance`` (src/ORBmatcher.cc:1844-1860), batched.
+* ``compute_stereo_matches`` == ``Frame::ComputeStereoMatches``
+  (src/Frame.cc:547-788).
+
+Every result is computed by the HIP kernels; this module only moves bytes.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import KEYPOINT_DTYPE, check, ptr
+
+TH_HIGH = 100  # src/ORBmatcher.cc:37
+TH_LOW = 50    # src/ORBmatcher.cc:38
+HISTO_LENGTH = 30  # src/ORBmatcher.cc:39
+
+
+class ORBextractor:
+    """GPU ORB extractor with the reference constructor signature."""
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0):
+        L = _lib.lib()
+        self.params = _lib.ExtractorParams(int(nfeatures), float(scaleFactor), int(nlevels), int(iniThFAST),
+                                           int(minThFAST))
+        h = C.c_void_p()
+        check(L.orbx_extractor_create(C.byref(self.params), int(device), C.byref(h)), "orbx_extractor_create")
+        self._h = h
+        self.nfeatures = int(nfeatures)
+        self.scaleFactor = float(scaleFactor)
+        self.nlevels = int(nlevels)
+        self.device = int(device)
+        n = self.nlevels
+        self._tables = [np.zeros(n, np.float32) for _ in range(4)]
+        check(L.orbx_extractor_scale_tables(h, *[ptr(t) for t in self._tables]), "orbx_extractor_scale_tables")
+        self._last_shape = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().orbx_extractor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- reference accessors (include/ORBextractor.h:82-104)
+    def GetLevels(self):
+        return _lib.lib().orbx_extractor_get_levels(self._h)
+
+    def GetScaleFactor(self):
+        return self.scaleFactor
+
+    def GetScaleFactors(self):
+        return self._tables[0].copy()
+
+    def GetInverseScaleFactors(self):
+        return self._tables[1].copy()
+
+    def GetScaleSigmaSquares(self):
+        return self._tables[2].copy()
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._tables[3].copy()
+
+    def max_keypoints(self, width, height):
+        n = _lib.lib().orbx_extractor_max_keypoints(self._h, int(width), int(height))
+        if n < 0:
+            check(n, "orbx_extractor_max_keypoints")
+        return n
+
+    # --- ORBextractor::operator()
+    def __call__(self, image, mask=None):
+        """Returns (keypoints structured array [cv::KeyPoint layout], descriptors uint8[n,32] or None).
+
+        ``mask`` is accepted and ignored, as in the reference."""
+        if image is None or getattr(image, "size", 0) == 0:
+            return np.zeros(0, KEYPOINT_DTYPE), None
+        img = np.asarray(image)
+        assert img.dtype == np.uint8 and img.ndim == 2, "image must be CV_8UC1"  # src/ORBextractor.cc:1146
+        h, w = img.shape
+        if img.strides[1] != 1:
+            img = np.ascontiguousarray(img)
+        cap = self.max_keypoints(w, h)
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int(0)
+        check(_lib.lib().orbx_extract(self._h, ptr(img), w, h, img.strides[0], ptr(kps), cap, ptr(desc), C.byref(n)),
+              "orbx_extract")
+        self._last_shape = (w, h)
+        n = n.value
+        if n == 0:
+            return kps[:0].copy(), None  # descriptors.release(), src/ORBextractor.cc:1163-1164
+        return kps[:n].copy(), desc[:n].copy()
+
+    @property
+    def mvImagePyramid(self):
+        return [self.pyramid_level(l) for l in range(self.nlevels)]
+
+    def pyramid_level(self, level, image=0):
+        L = _lib.lib()
+        w, h = C.c_int(0), C.c_int(0)
+        check(L.orbx_pyramid_level(self._h, image, level, None, 0, C.byref(w), C.byref(h)), "orbx_pyramid_level")
+        out = np.zeros((h.value, w.value), np.uint8)
+        check(L.orbx_pyramid_level(self._h, image, level, ptr(out), w.value, C.byref(w), C.byref(h)),
+              "orbx_pyramid_level")
+        return out
+
+    # --- device batch API (inputs/outputs are torch CUDA tensors)
+    def extract_batch_device(self, images, kps, desc, counts, stream=None):
+        """images: uint8 [n,H,W] device tensor; kps: uint8 [n,cap,28]; desc: uint8 [n,cap,32]; counts: int32 [n]."""
+        n, h, w = images.shape
+        cap = kps.shape[1]
+        check(_lib.lib().orbx_extract_batch_device(self._h, n, ptr(images), w, h, h * w, ptr(kps), ptr(desc),
+                                                   ptr(counts), cap, _stream_ptr(stream)),
+              "orbx_extract_batch_device")
+
+    def stereo_frames_device(self, images, kps, desc, counts, bf, baseline, uright, depth, nmatches, stream=None):
+        """images: uint8 [2n,H,W] ordered L0,R0,L1,R1...; uright/depth: float32 [n,cap]; nmatches: int32 [n]."""
+        n2, h, w = images.shape
+        cap = kps.shape[1]
+        check(_lib.lib().orbx_stereo_frames_device(self._h, n2 // 2, ptr(images), w, h, h * w, ptr(kps), ptr(desc),
+                                                   ptr(counts), cap, C.c_float(bf), C.c_float(baseline),
+                                                   ptr(uright), ptr(depth), ptr(nmatches), _stream_ptr(stream)),
+              "orbx_stereo_frames_device")
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    if hasattr(stream, "cuda_stream"):
+        return C.c_void_p(stream.cuda_stream)
+    return C.c_void_p(int(stream))
+
+
+def compute_stereo_matches(extractor_left, extractor_right, kps_left, desc_left, kps_right, desc_right, bf,
+                           baseline):
+    """Frame::ComputeStereoMatches on the pyramids of the extractors' last calls.
+
+    Returns (mvuRight float32[N], mvDepth float32[N]) with -1 for no match."""
+    nL, nR = len(kps_left), len(kps_right)
+    uR = np.full(nL, -1.0, np.float32)
+    depth = np.full(nL, -1.0, np.float32)
+    if nL == 0:
+        return uR, depth
+    kL = np.ascontiguousarray(kps_left, KEYPOINT_DTYPE)
+    kR = np.ascontiguousarray(kps_right, KEYPOINT_DTYPE)
+    dL = np.ascontiguousarray(desc_left, np.uint8)
+    dR = np.ascontiguousarray(desc_right if desc_right is not None else np.zeros((0, 32), np.uint8), np.uint8)
+    check(_lib.lib().orbx_stereo_match(extractor_left._h, extractor_right._h, ptr(kL), ptr(dL), nL, ptr(kR),
+                                       ptr(dR), nR, C.c_float(bf), C.c_float(baseline), ptr(uR), ptr(depth)),
+          "orbx_stereo_match")
+    return uR, depth
+
+
+class ORBmatcher:
+    """ORBmatcher(nnratio=0.6, checkOri=True) -- include/ORBmatcher.h:47."""
+
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        """Hamming distance of 32-byte descriptors; a, b: [32] or [n,32] uint8 (computed on the GPU)."""
+        import torch
+        a = np.atleast_2d(np.ascontiguousarray(a, np.uint8))
+        b = np.atleast_2d(np.ascontiguousarray(b, np.uint8))
+        assert a.shape == b.shape and a.shape[1] == 32
+        n = a.shape[0]
+        da = torch.from_numpy(a).cuda()
+        db = torch.from_numpy(b).cuda()
+        out = torch.empty(n, dtype=torch.int32, device=da.device)
+        s = torch.cuda.current_stream()
+        check(_lib.lib().orbx_descriptor_distance_device(ptr(da), ptr(db), n, ptr(out), _stream_ptr(s)),
+              "orbx_descriptor_distance_device")
+        d = out.cpu().numpy()
+        return int(d[0]) if n == 1 else d

@@ -1,0 +1,95 @@
+"""Seeded synthetic stereo imagery (SURVEY.md §8d "Synthetic inputs").
+
+No datasets exist in the container, so every benchmark and parity case runs on
+images generated here from ``numpy.random.default_rng(seed)``:
+
+* left image: low-frequency background (uniform noise at 1/8 resolution,
+  bilinearly upsampled) + random filled triangles/quads/ellipses with grey
+  levels U[0,255] + Gaussian noise sigma=2, clipped to u8;
+* right image: the left scene warped horizontally by a piecewise-constant
+  disparity field d in [2, 60] px (per random vertical band) + independent
+  noise sigma=2.
+
+Shapes follow the BASELINE.json configs: KITTI 1241x376 (2000 features),
+EuRoC 752x480 (1200), TUM 640x480 (1000).
+"""
+import numpy as np
+
+CONFIGS = {
+    "kitti": dict(width=1241, height=376, nfeatures=2000, fx=718.856, bf=386.1448),
+    "euroc": dict(width=752, height=480, nfeatures=1200, fx=435.2047, bf=47.9064),
+    "tum": dict(width=640, height=480, nfeatures=1000, fx=517.306408, bf=40.0),
+}
+
+
+def _upsample(small, h, w):
+    sh, sw = small.shape
+    ys = np.linspace(0, sh - 1, h)
+    xs = np.linspace(0, sw - 1, w)
+    y0 = np.floor(ys).astype(int)
+    x0 = np.floor(xs).astype(int)
+    y1 = np.minimum(y0 + 1, sh - 1)
+    x1 = np.minimum(x0 + 1, sw - 1)
+    fy = (ys - y0)[:, None]
+    fx = (xs - x0)[None, :]
+    a = small[y0][:, x0] * (1 - fx) + small[y0][:, x1] * fx
+    b = small[y1][:, x0] * (1 - fx) + small[y1][:, x1] * fx
+    return a * (1 - fy) + b * fy
+
+
+def _scene(rng, h, w, n_shapes):
+    img = _upsample(rng.uniform(40, 215, size=(h // 8 + 2, w // 8 + 2)), h, w)
+    for _ in range(n_shapes):
+        kind = rng.integers(0, 3)
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        r = rng.uniform(6, 70)
+        x0, x1 = int(max(cx - r, 0)), int(min(cx + r + 1, w))
+        y0, y1 = int(max(cy - r, 0)), int(min(cy + r + 1, h))
+        if x1 <= x0 or y1 <= y0:
+            continue
+        yy, xx = np.mgrid[y0:y1, x0:x1]
+        if kind == 0:  # ellipse
+            ax, ay = r, r * rng.uniform(0.3, 1.0)
+            m = ((xx - cx) / ax) ** 2 + ((yy - cy) / ay) ** 2 <= 1.0
+        else:  # convex polygon (triangle or quad) via half-planes
+            k = 3 if kind == 1 else 4
+            ang = np.sort(rng.uniform(0, 2 * np.pi, k))
+            px = cx + r * np.cos(ang)
+            py = cy + r * np.sin(ang)
+            m = np.ones(xx.shape, bool)
+            for i in range(k):
+                ax_, ay_ = px[i], py[i]
+                bx_, by_ = px[(i + 1) % k], py[(i + 1) % k]
+                m &= (bx_ - ax_) * (yy - ay_) - (by_ - ay_) * (xx - ax_) >= 0
+        img[y0:y1, x0:x1][m] = rng.uniform(0, 255)
+    return img
+
+
+def stereo_pair(seed, width=1241, height=376, n_shapes=None, stress=False):
+    """Return (left, right) uint8 arrays of shape (height, width)."""
+    rng = np.random.default_rng(seed)
+    if stress:
+        return (rng.integers(0, 256, (height, width), dtype=np.uint8),
+                rng.integers(0, 256, (height, width), dtype=np.uint8))
+    if n_shapes is None:
+        n_shapes = int(rng.integers(200, 600))
+    pad = 64
+    scene = _scene(rng, height, width + pad, n_shapes)
+    left = scene[:, :width]
+    # piecewise-constant disparity over random vertical bands
+    n_bands = int(rng.integers(4, 12))
+    cuts = np.sort(rng.integers(0, width, n_bands - 1))
+    disp = np.empty(width, np.int64)
+    edges = np.concatenate([[0], cuts, [width]])
+    for i in range(n_bands):
+        disp[edges[i]:edges[i + 1]] = rng.integers(2, 61)
+    cols = np.arange(width) + disp  # right(x) = left(x + d): points shift left in the right view
+    right = scene[:, cols]
+    left = left + rng.normal(0, 2, left.shape)
+    right = right + rng.normal(0, 2, right.shape)
+    return (np.clip(np.rint(left), 0, 255).astype(np.uint8),
+            np.clip(np.rint(right), 0, 255).astype(np.uint8))
+
+
+def mono_image(seed, width=640, height=480):
+    return stereo_pair(seed, width, height)[0]

@@ -1,0 +1,159 @@
+"""GPU parity: every stage of the HIP extractor vs the CPU oracle, bit-exact.
+
+Parity bar (BASELINE.json north_star): keypoints, descriptors,
+pyramid/blurred pixels, FAST candidates and octree selections are integer or
+exactly-rounded float data and must be bit-identical to the oracle.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+from orb_slam2_commit_amd import ORBextractor, synth
+from orb_slam2_commit_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+DBG_BLUR, DBG_CELL_COUNTS, DBG_CELL_TABLE, DBG_CAND, DBG_OCT_COUNTS, DBG_OCT_OUT, DBG_LEVEL = 1, 2, 3, 4, 5, 6, 7
+
+
+def dbg(ex, what, image=0, arg=0, dtype=np.int32):
+    L = _lib.lib()
+    n = L.orbx_debug_copy(ex._h, what, image, arg, None, 0)
+    assert n >= 0, n
+    buf = np.zeros(n, np.uint8)
+    L.orbx_debug_copy(ex._h, what, image, arg, _lib.ptr(buf), n)
+    return buf.view(dtype)
+
+
+CASES = [
+    ("kitti", 0, 1241, 376, 2000),
+    ("kitti", 1, 1241, 376, 2000),
+    ("euroc", 2, 752, 480, 1200),
+    ("tum", 3, 640, 480, 1000),
+    ("small", 4, 320, 240, 500),
+]
+
+
+def _image(seed, w, h, stress=False):
+    return synth.stereo_pair(seed, w, h, stress=stress)[0]
+
+
+@pytest.mark.parametrize("name,seed,w,h,nf", CASES)
+def test_pyramid_and_blur(gpu, name, seed, w, h, nf):
+    img = _image(seed, w, h)
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    ex(img)
+    ref = oracle.extract(oracle.params(nf, 1.2, 8, 20, 7), img)
+    for l in range(8):
+        lvl = ex.pyramid_level(l)
+        assert np.array_equal(lvl, ref.level(l)), "pyramid level %d differs" % l
+        blur = dbg(ex, DBG_BLUR, 0, l, np.uint8).reshape(lvl.shape)
+        assert np.array_equal(blur, oracle.gaussian_blur7(ref.level(l))), "blurred level %d differs" % l
+
+
+@pytest.mark.parametrize("name,seed,w,h,nf", CASES[:3])
+def test_fast_cells(gpu, name, seed, w, h, nf):
+    img = _image(seed, w, h)
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    ex(img)
+    ref = oracle.extract(p, img)
+    cells = dbg(ex, DBG_CELL_TABLE).reshape(-1, 8)
+    counts = dbg(ex, DBG_CELL_COUNTS)
+    cand = dbg(ex, DBG_CAND, dtype=np.uint32)
+    bad = 0
+    for ci, (lvl, x0, y0, x1, y1, off, cap, _) in enumerate(cells):
+        im = ref.level(lvl)
+        win = im[y0 - 3:y1 + 4, x0 - 3:x1 + 4]  # the reference's FAST window [iniY,maxY) x [iniX,maxX)
+        got = cand[off:off + counts[ci]]
+        exp = oracle.fast_window(win, 20)
+        if len(exp) == 0:
+            exp = oracle.fast_window(win, 7)
+        exp_packed = (exp[:, 2].astype(np.uint32) << 24) | ((exp[:, 1] + y0 - 3).astype(np.uint32) << 12) | \
+            (exp[:, 0] + x0 - 3).astype(np.uint32)
+        if not np.array_equal(got, exp_packed):
+            bad += 1
+    assert bad == 0, "%d/%d cells differ" % (bad, len(cells))
+
+
+@pytest.mark.parametrize("name,seed,w,h,nf", CASES)
+def test_extract_bitexact(gpu, name, seed, w, h, nf):
+    img = _image(seed, w, h)
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    kps, desc = ex(img)
+    ref = oracle.extract(oracle.params(nf, 1.2, 8, 20, 7), img)
+    assert len(kps) == len(ref.keypoints)
+    assert np.array_equal(kps["octave"], ref.keypoints["octave"])
+    lv = np.bincount(kps["octave"], minlength=8)
+    assert np.array_equal(kps.view(np.uint8), ref.keypoints.view(np.uint8)), "keypoints differ"
+    assert np.array_equal(desc, ref.descriptors), "descriptors differ"
+    assert lv.sum() == len(kps)
+
+
+@pytest.mark.parametrize("seed", [10, 11])
+def test_extract_stress_noise(gpu, seed):
+    """i.i.d. uniform noise: dense FAST responses, heavy octree phase 2."""
+    img = _image(seed, 640, 480, stress=True)
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    kps, desc = ex(img)
+    ref = oracle.extract(oracle.params(1000, 1.2, 8, 20, 7), img)
+    assert np.array_equal(kps.view(np.uint8), ref.keypoints.view(np.uint8))
+    assert np.array_equal(desc, ref.descriptors)
+
+
+@pytest.mark.parametrize("params", [(1000, 1.2, 8, 20, 7), (500, 1.5, 4, 30, 10), (300, 1.1, 12, 12, 5),
+                                    (150, 1.2, 1, 20, 7)])
+def test_extract_param_sweep(gpu, params):
+    img = _image(21, 512, 384)
+    ex = ORBextractor(*params)
+    kps, desc = ex(img)
+    ref = oracle.extract(oracle.params(*params), img)
+    assert np.array_equal(kps.view(np.uint8), ref.keypoints.view(np.uint8))
+    assert np.array_equal(desc, ref.descriptors) if desc is not None else len(ref.keypoints) == 0
+
+
+def test_edge_cases(gpu):
+    ex = ORBextractor(500, 1.2, 8, 20, 7)
+    k, d = ex(np.zeros((0, 0), np.uint8))  # empty: silent return
+    assert len(k) == 0 and d is None
+    flat = np.full((240, 320), 128, np.uint8)  # no corners at all
+    k, d = ex(flat)
+    ref = oracle.extract(oracle.params(500, 1.2, 8, 20, 7), flat)
+    assert len(k) == 0 and len(ref.keypoints) == 0 and d is None
+    tiny = _image(5, 64, 48)  # only level 0..2 have FAST cells
+    k, d = ex(tiny)
+    ref = oracle.extract(oracle.params(500, 1.2, 8, 20, 7), tiny)
+    assert np.array_equal(k.view(np.uint8), ref.keypoints.view(np.uint8))
+
+
+def test_scale_tables(gpu):
+    ex = ORBextractor(2000, 1.2, 8, 20, 7)
+    t = oracle.scale_tables(oracle.params(2000, 1.2, 8, 20, 7))
+    assert np.array_equal(ex.GetScaleFactors(), t["scale"])
+    assert np.array_equal(ex.GetInverseScaleFactors(), t["inv_scale"])
+    assert np.array_equal(ex.GetScaleSigmaSquares(), t["sigma2"])
+    assert np.array_equal(ex.GetInverseScaleSigmaSquares(), t["inv_sigma2"])
+    assert ex.GetLevels() == 8
+
+
+def test_batch_device_equals_host(gpu):
+    import torch
+    imgs = np.stack([_image(30 + i, 752, 480) for i in range(4)])
+    ex = ORBextractor(1200, 1.2, 8, 20, 7)
+    cap = ex.max_keypoints(752, 480)
+    d_img = torch.from_numpy(imgs).to(gpu)
+    kps = torch.zeros((4, cap, 28), dtype=torch.uint8, device=gpu)
+    desc = torch.zeros((4, cap, 32), dtype=torch.uint8, device=gpu)
+    cnt = torch.zeros(4, dtype=torch.int32, device=gpu)
+    ex.extract_batch_device(d_img, kps, desc, cnt, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    cnt = cnt.cpu().numpy()
+    kps = kps.cpu().numpy()
+    desc = desc.cpu().numpy()
+    for i in range(4):
+        ref = oracle.extract(oracle.params(1200, 1.2, 8, 20, 7), imgs[i])
+        assert cnt[i] == len(ref.keypoints)
+        assert np.array_equal(kps[i, :cnt[i]].reshape(-1), ref.keypoints.view(np.uint8).reshape(-1))
+        assert np.array_equal(desc[i, :cnt[i]], ref.descriptors)
