@@ -1,0 +1,221 @@
+"""Benchmark: frames/sec ORB extract+match on KITTI-00-shaped stereo (BASELINE.json configs[1]).
+
+One "step" = one pass of the hot path over one batch of B synthetic stereo
+frames resident in HBM: ORB extraction of the 2B images (1241x376, 2000
+features, 8 levels x1.2, FAST 20/7) + Frame::ComputeStereoMatches of the B
+frames, all inside liborbx.so (orbx_stereo_frames_device).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+
+For N>1 the driver launches one rank per GPU with torch.distributed.run;
+frames shard across ranks with no data-path collective ("weak" scaling), the
+timed region is bracketed by barrier + synchronize and the max over ranks is
+reported.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec ORB extract+match (2k kp) + LocalBA iters/sec, KITTI-00 stereo"
+KITTI = dict(width=1241, height=376, nfeatures=2000, fx=718.856, bf=386.1448)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128, help="stereo frames per step per GPU")
+    ap.add_argument("--unique", type=int, default=16, help="distinct synthetic stereo pairs tiled into the batch")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (tools/profile.py); null if absent")
+    return ap.parse_args()
+
+
+def level_sizes(w, h, inv_scales):
+    """ComputePyramid level sizes: cvRound((float)cols * mvInvScaleFactor[l]) (src/ORBextractor.cc:1219-1221)."""
+    return [(int(np.rint(np.float32(w) * np.float32(s))), int(np.rint(np.float32(h) * np.float32(s))))
+            for s in inv_scales]
+
+
+def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, cand_per_img):
+    """Algorithmic HBM bytes of one launch of `stage` over the batch."""
+    sP = sum(P)
+    if stage == "k_resize":  # per launch average over the 7 level launches: read P_{l-1} + write P_l
+        return n_img * sum(P[l - 1] + P[l] for l in range(1, len(P))) / (len(P) - 1)
+    if stage == "k_fast":  # every level pixel read once + 4-B candidates written
+        return n_img * (sP + 4 * cand_per_img)
+    if stage == "k_blur":  # every level pixel read + written once
+        return n_img * 2 * sP
+    if stage == "k_octree":  # 4-B candidates read + 4-B selections written
+        return n_img * (4 * cand_per_img + 4 * kps_per_img)
+    if stage == "k_describe":  # raw + blurred levels read, 4-B selection read, 28-B kp + 32-B desc written
+        return n_img * (2 * sP + 64 * kps_per_img)
+    if stage == "k_stereo_match":  # per frame: NL*(32+28+8) + NR*(32+28) + Nacc*352
+        return n_frames * (kps_per_img * 68 + kps_per_img * 60 + acc_per_frame * 352)
+    if stage == "k_stereo_prep":
+        return n_frames * kps_per_img * (28 + 8)
+    if stage == "k_stereo_finalize":
+        return n_frames * kps_per_img * 12
+    return None
+
+
+def cpu_baseline(pairs, seconds):
+    """Single-thread CPU restatement (oracle/) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    p = oracle.params(KITTI["nfeatures"], 1.2, 8, 20, 7)
+    bf, fx = KITTI["bf"], KITTI["fx"]
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        L, R = pairs[n % len(pairs)]
+        oL, oR = oracle.extract(p, L), oracle.extract(p, R)
+        oracle.stereo_match(p, oL, oR, bf, bf / fx)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 3:
+            break
+    return dict(value=round(n / el, 3), unit="frames/s", cores=1, kind="port",
+                sample="%d KITTI-shaped stereo frames (extract L + extract R + stereo match), oracle/ C++ "
+                       "restatement, 1 thread, %.1f s" % (n, el))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from orb_slam2_commit_amd import ORBextractor, synth
+    from orb_slam2_commit_amd import _lib
+
+    W, H, B = KITTI["width"], KITTI["height"], args.batch
+    # synthetic frames: distinct seeds per rank (frame shards), tiled into the batch
+    pairs = [synth.stereo_pair(1000 * rank + s, W, H) for s in range(args.unique)]
+    host = np.stack([pairs[f % len(pairs)][k] for f in range(B) for k in (0, 1)])
+    images = torch.from_numpy(host).to(dev)
+    ex = ORBextractor(KITTI["nfeatures"], 1.2, 8, 20, 7, device=local)
+    cap = ex.max_keypoints(W, H)
+    kps = torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev)
+    desc = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+    uR = torch.empty((B, cap), dtype=torch.float32, device=dev)
+    depth = torch.empty((B, cap), dtype=torch.float32, device=dev)
+    nmatch = torch.zeros(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    bf, baseline = KITTI["bf"], KITTI["bf"] / KITTI["fx"]
+
+    def step():
+        ex.stereo_frames_device(images, kps, desc, counts, bf, baseline, uR, depth, nmatch, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    L = _lib.lib()
+    L.orbx_profile_reset(ex._h)
+    L.orbx_profile_enable(ex._h, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    L.orbx_profile_enable(ex._h, 0)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-stage live HIP-event timings on the stream the kernels ran on
+    import ctypes as C
+    stages = {}
+    for s in range(L.orbx_profile_read(ex._h, -1, None, None, None)):
+        ms, n, name = C.c_double(), C.c_longlong(), C.c_char_p()
+        L.orbx_profile_read(ex._h, s, C.byref(ms), C.byref(n), C.byref(name))
+        if n.value:
+            stages[name.value.decode()] = (ms.value, n.value)
+    cnt = counts.cpu().numpy()
+    nm = nmatch.cpu().numpy()
+    kps_per_img = float(cnt.mean())
+    acc_per_frame = float(nm.mean())  # surviving matches (lower bound of SAD refinements)
+    # candidates per image (FAST survivors) from the last batch
+    ncand = L.orbx_debug_copy(ex._h, 2, 0, 0, None, 0) // 4
+    cc = np.zeros(ncand, np.int32)
+    L.orbx_debug_copy(ex._h, 2, 0, 0, _lib.ptr(cc), cc.nbytes)
+    cand_per_img = float(cc.sum())
+    P = [w * h for (w, h) in level_sizes(W, H, ex.GetInverseScaleFactors())]
+    dom = max(stages, key=lambda k: stages[k][0]) if stages else None
+    roofline = None
+    if dom:
+        ms_tot, nl = stages[dom]
+        avg_s = ms_tot / nl / 1e3
+        nbytes = algorithmic_bytes(dom, 2 * B, B, P, kps_per_img, acc_per_frame, cand_per_img)
+        achieved = nbytes / avg_s / 1e9
+        traffic = None
+        if os.path.exists(args.traffic):
+            try:
+                traffic = json.load(open(args.traffic)).get("per_launch_bytes", {}).get(dom)
+            except Exception:
+                traffic = None
+        roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic,
+                        algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4))
+
+    frames = B * args.steps * world
+    value = frames / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded stereo scenes, %d distinct pairs per rank tiled into the batch)" % args.unique,
+        "config": {"workload": "KITTI-00 stereo 1241x376, 2000 features, extract L+R + ComputeStereoMatches",
+                   "batch_frames_per_gpu": B, "global_batch_frames": B * world, "nlevels": 8,
+                   "scale_factor": 1.2, "fast_th": [20, 7], "parallelism": "frame-sharded x%d" % world},
+        "roofline": roofline,
+        "stage_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()},
+        "keypoints_per_image": round(kps_per_img, 1),
+        "stereo_matches_per_frame": round(acc_per_frame, 1),
+        "localba_iters_per_s": None,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pairs, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -109,6 +109,15 @@ orbx_status orbx_stereo_frames_device(orbx_extractor* h, int n_frames, const uin
 orbx_status orbx_descriptor_distance_device(const uint8_t* d_a, const uint8_t* d_b, int n, int32_t* d_out,
                                             void* stream);
 
+/* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
+ * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel
+ * launch of the handle is bracketed by events on its stream.
+ * orbx_profile_read(h, -1, ...) returns the number of stages; for stage >= 0 it
+ * fills the accumulated milliseconds, launch count and kernel name. */
+orbx_status orbx_profile_enable(orbx_extractor* h, int enable);
+orbx_status orbx_profile_reset(orbx_extractor* h);
+int orbx_profile_read(orbx_extractor* h, int stage, double* total_ms, long long* launches, const char** name);
+
 /* Library/device info: returns the number of visible HIP devices (<=0: none). */
 int orbx_device_count(void);
 const char* orbx_version(void);

@@ -57,6 +57,10 @@ SIGNATURES = {
     "orbx_descriptor_distance_device": ([P, P, C.c_int, P, P], C.c_int),
     "orbx_device_count": ([], C.c_int),
     "orbx_version": ([], C.c_char_p),
+    "orbx_profile_enable": ([P, C.c_int], C.c_int),
+    "orbx_profile_reset": ([P], C.c_int),
+    "orbx_profile_read": ([P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_longlong),
+                           C.POINTER(C.c_char_p)], C.c_int),
     # include/orbx_debug.h
     "orbx_debug_copy": ([P, C.c_int, C.c_int, C.c_int, P, C.c_size_t], C.c_longlong),
 }

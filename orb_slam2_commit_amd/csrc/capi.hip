@@ -20,12 +20,14 @@
 #include "../../include/orbx.h"
 #include "orbx_internal.h"
 #include "orbx_stereo.h"
+#include "orbx_prof.h"
 
 namespace orbx {
 hipError_t upload_constants(const int* umax16, const int* gauss7);
 hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells, const int* tile_level,
                                  const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B, int n_img,
-                                 orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t st);
+                                 orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t st,
+                                 StageTimer* T);
 size_t octree_smem_host(int NC, int cell_cap);
 hipError_t octree_set_smem_limit(size_t bytes);
 }  // namespace orbx
@@ -293,6 +295,7 @@ struct orbx_extractor {
   DevBuf<int32_t> nmatch, nbuf;
   DevBuf<orbx_keypoint> skL, skR;
   DevBuf<uint8_t> sdL, sdR;
+  StageTimer timer;
   // last batch (mvImagePyramid)
   Plan* last_plan = nullptr;
   const uint8_t* last_in = nullptr;
@@ -377,7 +380,7 @@ orbx_status run_extract(orbx_extractor* h, Plan* P, int n, const uint8_t* d_in, 
   if (s != ORBX_OK) return s;
   BatchPtrs B = batch_ptrs(h, d_in, pitch);
   hipError_t e = launch_extract_stages(P->G, P->dG.p, P->dcells.p, P->dtiles.p, P->dxt.p, P->dyt.p, B, n, d_kps,
-                                       d_desc, d_counts, kp_cap, st);
+                                       d_desc, d_counts, kp_cap, st, &h->timer);
   if (e != hipSuccess) return ORBX_ERR_HIP;
   h->last_plan = P;
   h->last_in = d_in;
@@ -575,7 +578,7 @@ static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_fram
   A.rkeys = h->rkeys.p;
   A.oct_start = h->oct_start.p;
   A.nmatches = nmatches;
-  return hip_status(launch_stereo(A, P->dG.p, n_frames, maxL, st));
+  return hip_status(launch_stereo(A, P->dG.p, n_frames, maxL, st, &h->timer));
 }
 
 orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const orbx_keypoint* kpsL,
@@ -637,6 +640,32 @@ orbx_status orbx_stereo_frames_device(orbx_extractor* h, int n_frames, const uin
   return run_stereo(h, h, n_frames, d_kps, d_desc, d_counts, 2 * kc, 2, d_kps + kc, d_desc + kc * 32, d_counts + 1,
                     2 * kc, 2, 2, 0, 2, 1, h->last_plan->G.max_kps, bf, baseline, d_uright, d_depth, kc,
                     d_nmatches, pick_stream(h, stream));
+}
+
+orbx_status orbx_profile_enable(orbx_extractor* h, int enable) {
+  if (!h) return ORBX_ERR_ARG;
+  h->timer.flush();
+  h->timer.enabled = enable != 0;
+  return ORBX_OK;
+}
+
+orbx_status orbx_profile_reset(orbx_extractor* h) {
+  if (!h) return ORBX_ERR_ARG;
+  (void)hipSetDevice(h->device);
+  h->timer.reset();
+  return ORBX_OK;
+}
+
+int orbx_profile_read(orbx_extractor* h, int stage, double* total_ms, long long* launches, const char** name) {
+  if (!h) return ORBX_ERR_ARG;
+  if (stage < 0) return ST_COUNT;
+  if (stage >= ST_COUNT) return ORBX_ERR_ARG;
+  (void)hipSetDevice(h->device);
+  h->timer.flush();
+  if (total_ms) *total_ms = h->timer.total_ms[stage];
+  if (launches) *launches = h->timer.launches[stage];
+  if (name) *name = kStageNames[stage];
+  return ORBX_OK;
 }
 
 orbx_status orbx_descriptor_distance_device(const uint8_t* d_a, const uint8_t* d_b, int n, int32_t* d_out,

@@ -15,6 +15,7 @@
 
 #include "orbx_device.h"
 #include "orbx_internal.h"
+#include "orbx_prof.h"
 
 namespace orbx {
 
@@ -736,20 +737,33 @@ hipError_t upload_constants(const int* umax16, const int* gauss7) {
 hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells,
                                  const int* tile_level, const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B,
                                  int n_img, orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap,
-                                 hipStream_t st) {
+                                 hipStream_t st, StageTimer* T) {
   for (int l = 1; l < Gh.nlevels; l++) {
     dim3 grid((Gh.lv[l].w + 63) / 64, (Gh.lv[l].h + 3) / 4, n_img);
+    T->begin(st);
     hipLaunchKernelGGL(k_resize, grid, dim3(BS), 0, st, Gd, xt, yt, B, l);
+    T->end(ST_RESIZE, st);
   }
-  if (Gh.ncells > 0) hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(BS), 0, st, Gd, cells, B);
-  else (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
+  if (Gh.ncells > 0) {
+    T->begin(st);
+    hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(BS), 0, st, Gd, cells, B);
+    T->end(ST_FAST, st);
+  } else {
+    (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
+  }
+  T->begin(st);
   hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
+  T->end(ST_BLUR, st);
   if (Gh.ncells > 0) {
     const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap);
+    T->begin(st);
     hipLaunchKernelGGL(k_octree, dim3(Gh.nlevels, n_img), dim3(BS), smem, st, Gd, cells, B);
+    T->end(ST_OCTREE, st);
   }
   const int nb = (Gh.max_kps + BS / 64 - 1) / (BS / 64);
+  T->begin(st);
   hipLaunchKernelGGL(k_describe, dim3(max(nb, 1), n_img), dim3(BS), 0, st, Gd, B, kps, desc, counts, kp_cap);
+  T->end(ST_DESCRIBE, st);
   return hipGetLastError();
 }
 

@@ -81,9 +81,4 @@ __host__ __device__ inline const uint8_t* level_ptr(const Geometry& G, const Bat
   return l == 0 ? B.in + (size_t)img * B.in_pitch : B.pyr + (size_t)img * G.pyr_bytes + G.lv[l].off;
 }
 
-// Launchers (extract.hip). All asynchronous on `stream`.
-hipError_t launch_extract(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells, const ResizeX* xt,
-                          const ResizeY* yt, const BatchPtrs& B, int n_img, orbx_keypoint* kps,
-                          uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t stream);
-
 }  // namespace orbx

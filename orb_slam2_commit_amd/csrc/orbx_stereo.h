@@ -32,7 +32,9 @@ struct StereoArgs {
   int32_t* nmatches;
 };
 
-hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st);
+struct StageTimer;
+hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st,
+                         StageTimer* T);
 hipError_t launch_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* out, hipStream_t st);
 
 }  // namespace orbx

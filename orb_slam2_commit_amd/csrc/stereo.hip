@@ -15,6 +15,7 @@
 #include "orbx_device.h"
 #include "orbx_internal.h"
 #include "orbx_stereo.h"
+#include "orbx_prof.h"
 
 namespace orbx {
 
@@ -309,11 +310,18 @@ __global__ __launch_bounds__(SBS) void k_hamming(const uint8_t* __restrict__ a, 
   out[i] = hamming256(x, y);
 }
 
-hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st) {
+hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st,
+                         StageTimer* T) {
+  T->begin(st);
   hipLaunchKernelGGL(k_stereo_prep, dim3(n_frames), dim3(SBS), 0, st, A);
+  T->end(ST_STEREO_PREP, st);
   const int nb = (maxL + kKpsPerBlock - 1) / kKpsPerBlock;
+  T->begin(st);
   hipLaunchKernelGGL(k_stereo_match, dim3(max(nb, 1), n_frames), dim3(SBS), 0, st, A, Gd);
+  T->end(ST_STEREO_MATCH, st);
+  T->begin(st);
   hipLaunchKernelGGL(k_stereo_finalize, dim3(n_frames), dim3(SBS), 0, st, A);
+  T->end(ST_STEREO_FINAL, st);
   return hipGetLastError();
 }
 
