@@ -159,8 +159,9 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
     if (L.w < 1 || L.h < 1 || L.w > 4095 || L.h > 4095) return ORBX_ERR_SIZE;
     L.off = l == 0 ? 0 : pyr;
     if (l > 0) pyr += (long long)L.w * L.h;
+    L.bstride = (L.w + 15) & ~15;
     L.boff = blur;
-    blur += (long long)L.w * L.h;
+    blur += ((long long)L.bstride * L.h + 255) & ~255LL;
     L.minBX = L.minBY = kEdgeThresholdHost - 3;
     L.maxBX = L.w - kEdgeThresholdHost + 3;
     L.maxBY = L.h - kEdgeThresholdHost + 3;
@@ -192,7 +193,7 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
           c.y1 = (int16_t)((int)maxY - 4);
           if (c.x1 < c.x0 || c.y1 < c.y0) continue;
           const int cw = c.x1 - c.x0 + 1, ch = c.y1 - c.y0 + 1;
-          if (cw > 64 || ch > 64) return ORBX_ERR_SIZE;
+          if (cw > 60 || ch > 60) return ORBX_ERR_SIZE;  // k_fast LDS tile bound
           c.cap = ((cw + 1) / 2) * ((ch + 1) / 2);
           c.cand_off = cand;
           cand += c.cap;
@@ -691,11 +692,16 @@ extern "C" long long orbx_debug_copy(orbx_extractor* h, int what, int image, int
   size_t bytes = 0;
   bool device_src = true;
   switch (what) {
-    case ORBX_DBG_BLUR_LEVEL:
+    case ORBX_DBG_BLUR_LEVEL: {
       if (arg < 0 || arg >= G.nlevels) return ORBX_ERR_ARG;
-      src = h->blur.p + (size_t)image * G.blur_bytes + G.lv[arg].boff;
-      bytes = (size_t)G.lv[arg].w * G.lv[arg].h;
-      break;
+      const LevelGeom& L = G.lv[arg];
+      bytes = (size_t)L.w * L.h;
+      if (dst && cap >= bytes) {
+        const uint8_t* b = h->blur.p + (size_t)image * G.blur_bytes + L.boff;
+        if (hipMemcpy2D(dst, L.w, b, L.bstride, L.w, L.h, hipMemcpyDeviceToHost) != hipSuccess) return ORBX_ERR_HIP;
+      }
+      return (long long)bytes;
+    }
     case ORBX_DBG_CELL_COUNTS:
       src = h->cell_count.p + (size_t)image * G.ncells;
       bytes = sizeof(int) * G.ncells;

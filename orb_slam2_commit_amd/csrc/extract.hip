@@ -75,6 +75,48 @@ __device__ int block_sum(int v) {
   return s;
 }
 
+// ------------------------------------------------------------ LDS staging
+// Copy an nrows x ncols byte window (row stride `stride`, any alignment) into
+// LDS (row stride ls).  Every load is an aligned dword and all MAXK loads of a
+// thread are issued before the first LDS write, so the window costs one
+// memory latency instead of one per row.  Needs ncols+6 <= 4*dwpr and the
+// dword-rounded span to stay inside the buffer (true for level windows that
+// start >= 3 bytes into a row and end >= 3 bytes before its end).
+template <int MAXK>
+__device__ __forceinline__ void window_to_lds(const uint8_t* base, size_t stride, int nrows, int ncols, uint8_t* lds,
+                                              int ls, int tid, int nth) {
+  const int dwpr = (ncols + 6) / 4 + 1;
+  const int total = nrows * dwpr;
+  uint32_t v[MAXK];
+  int rr[MAXK], cc[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; k++) {
+    const int q = tid + k * nth;
+    v[k] = 0;
+    rr[k] = -1;
+    cc[k] = 0;
+    if (q < total) {
+      const int r = q / dwpr, j = q - r * dwpr;
+      const uintptr_t a = (uintptr_t)(base + (size_t)r * stride);
+      const int sh = (int)(a & 3);
+      if (4 * j < sh + ncols) {
+        v[k] = *((const uint32_t*)(a & ~(uintptr_t)3) + j);
+        rr[k] = r;
+        cc[k] = 4 * j - sh;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXK; k++) {
+    if (rr[k] < 0) continue;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int c = cc[k] + b;
+      if (c >= 0 && c < ncols) lds[rr[k] * ls + c] = (uint8_t)(v[k] >> (8 * b));
+    }
+  }
+}
+
 // ------------------------------------------------------------------ resize
 // cv::resize INTER_LINEAR 8U (OpenCV 3.2 fixed point, coefficient tables built
 // on the host exactly as resizeGeneric_ does).  One thread per output pixel.
@@ -111,78 +153,154 @@ __device__ __forceinline__ int reflect101(int p, int n) {
   return p;
 }
 
+// Tile of kBlurTileW x kBlurTileH outputs per 256-thread block.  Input tile
+// col 0 = x0-4 so that every 4-output group reads 3 aligned LDS dwords; row
+// sums (<= 257*255 = 65535) are packed u16; outputs go out as aligned dwords
+// (blurred rows are padded to a 16-byte stride).
+constexpr int kBIn = kBlurTileW + 8;  // input tile row stride (bytes)
 __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
                                              BatchPtrs B) {
-  __shared__ uint8_t tin[kBlurTileH + 6][kBlurTileW + 8];
-  __shared__ int trow[kBlurTileH + 6][kBlurTileW];
-  const int tile = blockIdx.x, img = blockIdx.y;
+  __shared__ __align__(16) uint8_t tin[(kBlurTileH + 6) * kBIn];
+  __shared__ __align__(16) uint16_t trow[(kBlurTileH + 6) * kBlurTileW];
+  const int tile = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
   const int l = tile_level[tile];
   const LevelGeom& L = G->lv[l];
   const int t = tile - L.tile_begin;
   const int x0 = (t % L.tiles_x) * kBlurTileW, y0 = (t / L.tiles_x) * kBlurTileH;
   const uint8_t* src = level_ptr(*G, B, img, l);
   uint8_t* dst = B.blur + (size_t)img * G->blur_bytes + L.boff;
-  const int w = L.w, h = L.h;
-  for (int q = threadIdx.x; q < (kBlurTileH + 6) * (kBlurTileW + 6); q += BS) {
-    const int ty = q / (kBlurTileW + 6), tx = q % (kBlurTileW + 6);
-    const int sy = reflect101(y0 + ty - 3, h), sx = reflect101(x0 + tx - 3, w);
-    tin[ty][tx] = src[(size_t)sy * w + sx];
+  const int w = L.w, h = L.h, bs = L.bstride;
+  const bool interior = x0 - 4 >= 0 && x0 + kBlurTileW + 4 <= w && y0 - 3 >= 0 && y0 + kBlurTileH + 3 <= h;
+  // input tile: rows y0-3 .. y0+H+2, cols x0-4 .. x0+W+3 (REFLECT_101 at the borders)
+  constexpr int TR = kBlurTileH + 6;
+  if (interior) {
+    // 70 rows x 36 dwords / 256 threads <= 10 loads per thread
+    window_to_lds<10>(src + (size_t)(y0 - 3) * w + (x0 - 4), w, TR, kBIn, tin, kBIn, tid, BS);
+  } else {
+    for (int q0 = 0; q0 < TR * kBIn; q0 += 8 * BS) {
+      uint8_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int q = q0 + tid + k * BS;
+        v[k] = 0;
+        if (q < TR * kBIn) {
+          const int ty = q / kBIn, tx = q - ty * kBIn;
+          v[k] = src[(size_t)reflect101(y0 + ty - 3, h) * w + reflect101(x0 + tx - 4, w)];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int q = q0 + tid + k * BS;
+        if (q < TR * kBIn) tin[q] = v[k];
+      }
+    }
   }
   __syncthreads();
   const int k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
-  for (int q = threadIdx.x; q < (kBlurTileH + 6) * kBlurTileW; q += BS) {
-    const int ty = q / kBlurTileW, tx = q % kBlurTileW;
-    const uint8_t* r = &tin[ty][tx];
-    trow[ty][tx] = k3 * r[3] + k2 * (r[2] + r[4]) + k1 * (r[1] + r[5]) + k0 * (r[0] + r[6]);
+  // row pass: 4 outputs per task from 3 aligned dwords
+  for (int q = tid; q < TR * (kBlurTileW / 4); q += BS) {
+    const int ty = q / (kBlurTileW / 4), g = q - ty * (kBlurTileW / 4);
+    const uint32_t* r32 = (const uint32_t*)&tin[ty * kBIn + 4 * g];
+    const uint32_t a = r32[0], b = r32[1], c = r32[2];
+    int p[12];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      p[i] = (a >> (8 * i)) & 255;
+      p[4 + i] = (b >> (8 * i)) & 255;
+      p[8 + i] = (c >> (8 * i)) & 255;
+    }
+    uint32_t o[2];
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      // output col 4g+j needs tile cols 4g+j+1 .. 4g+j+7
+      const int s0 = k3 * p[j + 4] + k2 * (p[j + 3] + p[j + 5]) + k1 * (p[j + 2] + p[j + 6]) + k0 * (p[j + 1] + p[j + 7]);
+      const int s1 = k3 * p[j + 5] + k2 * (p[j + 4] + p[j + 6]) + k1 * (p[j + 3] + p[j + 7]) + k0 * (p[j + 2] + p[j + 8]);
+      o[j >> 1] = (uint32_t)s0 | ((uint32_t)s1 << 16);
+    }
+    *(uint2*)&trow[ty * kBlurTileW + 4 * g] = make_uint2(o[0], o[1]);
   }
   __syncthreads();
+  // column pass: 4 columns x 8 rows per thread
+  const int g = tid & (kBlurTileW / 4 - 1);
+  const int rg = tid / (kBlurTileW / 4);
+  const int xg = x0 + 4 * g;
+  if (xg >= w) return;
   const int simd_w = w & ~3;
-  const int tx = threadIdx.x & 63;
-  const int x = x0 + tx;
-  if (x >= w) return;
-  for (int ty = threadIdx.x >> 6; ty < kBlurTileH; ty += BS / 64) {
-    const int y = y0 + ty;
+  int col[14][4];
+#pragma unroll
+  for (int r = 0; r < 14; r++) {
+    const uint2 v = *(const uint2*)&trow[(rg * 8 + r) * kBlurTileW + 4 * g];
+    col[r][0] = v.x & 0xFFFF;
+    col[r][1] = v.x >> 16;
+    col[r][2] = v.y & 0xFFFF;
+    col[r][3] = v.y >> 16;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int y = y0 + rg * 8 + r;
     if (y >= h) break;
-    const int acc = k3 * trow[ty + 3][tx] + k2 * (trow[ty + 2][tx] + trow[ty + 4][tx]) +
-                    k1 * (trow[ty + 1][tx] + trow[ty + 5][tx]) + k0 * (trow[ty][tx] + trow[ty + 6][tx]);
-    int v;
-    if (x < simd_w)
-      v = (int)__builtin_rintf((float)acc * (1.0f / 65536.0f));
-    else
-      v = (acc + (1 << 15)) >> 16;
-    dst[(size_t)y * w + x] = (uint8_t)min(max(v, 0), 255);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int acc = k3 * col[r + 3][j] + k2 * (col[r + 2][j] + col[r + 4][j]) + k1 * (col[r + 1][j] + col[r + 5][j]) +
+                      k0 * (col[r][j] + col[r + 6][j]);
+      int v;
+      if (xg + j < simd_w)
+        v = (int)__builtin_rintf((float)acc * (1.0f / 65536.0f));
+      else
+        v = (acc + (1 << 15)) >> 16;
+      packed |= (uint32_t)min(max(v, 0), 255) << (8 * j);
+    }
+    uint8_t* d = dst + (size_t)y * bs + xg;
+    if (xg + 4 <= w) {
+      *(uint32_t*)d = packed;
+    } else {
+      for (int j = 0; j < w - xg; j++) d[j] = (uint8_t)(packed >> (8 * j));
+    }
   }
 }
 
 // ------------------------------------------------------------------- FAST
-// One block per FAST cell window.  cv::FAST(window, th, nonmax) semantics
-// (OpenCV 3.2 FAST_t<16>): a pixel of the detection region is a corner at
-// threshold t iff >= 9 contiguous ring pixels are all > v+t or all < v-t;
-// its cornerScore<16> S satisfies corner_t <=> S >= t, so one score map serves
-// both thresholds.  NMS is strict against the 8 neighbours inside the region
-// (0 outside).  If nothing survives at iniThFAST the cell uses minThFAST
-// (src/ORBextractor.cc:892-900).  Survivors are written in row-major order.
-constexpr int kMaxCell = 64;  // wCell,hCell <= 60
+// One wavefront per FAST cell window (block = 1 wave, no block-level syncs).
+// cv::FAST(window, th, nonmax) semantics (OpenCV 3.2 FAST_t<16>): a pixel of
+// the detection region is a corner at threshold t iff >= 9 contiguous ring
+// pixels are all > v+t or all < v-t; its cornerScore<16> S satisfies
+// corner_t <=> S >= t, so one score map serves both thresholds.  NMS is strict
+// against the 8 neighbours inside the region (0 outside).  If nothing survives
+// at iniThFAST the cell uses minThFAST (src/ORBextractor.cc:892-900).
+// Survivors are written in row-major order.
+//
+//   1. window -> LDS tile (lanes = columns)
+//   2. compass quick test (two adjacent of ring pixels 0,4,8,12 beyond t) and
+//      ballot-compaction of passing pixels into a row-major list
+//   3. full segment test + score on the compacted list (all 64 lanes busy);
+//      corners compacted in place, score map S+1 in LDS
+//   4. NMS at iniThFAST -> count; 5. NMS at the chosen threshold -> ballot-ranked
+//      row-major writes
+constexpr int kMaxCell = 60;          // wCell,hCell <= 60 (checked on the host)
+constexpr int kTileS = 68;            // tile row stride (TW <= 66)
+constexpr int kMapS = 64;             // score-map row stride
 
-__device__ __forceinline__ int fast_score(const uint8_t* t, int ts, int tlo) {
+__device__ __forceinline__ int ring_score(const uint8_t* t, int tlo) {
+  // t points at the centre pixel inside the LDS tile (row stride kTileS)
   const int v = t[0];
   int p[16];
-  p[0] = t[3 * ts];
-  p[1] = t[3 * ts + 1];
-  p[2] = t[2 * ts + 2];
-  p[3] = t[ts + 3];
+  p[0] = t[3 * kTileS];
+  p[1] = t[3 * kTileS + 1];
+  p[2] = t[2 * kTileS + 2];
+  p[3] = t[kTileS + 3];
   p[4] = t[3];
-  p[5] = t[-ts + 3];
-  p[6] = t[-2 * ts + 2];
-  p[7] = t[-3 * ts + 1];
-  p[8] = t[-3 * ts];
-  p[9] = t[-3 * ts - 1];
-  p[10] = t[-2 * ts - 2];
-  p[11] = t[-ts - 3];
+  p[5] = t[-kTileS + 3];
+  p[6] = t[-2 * kTileS + 2];
+  p[7] = t[-3 * kTileS + 1];
+  p[8] = t[-3 * kTileS];
+  p[9] = t[-3 * kTileS - 1];
+  p[10] = t[-2 * kTileS - 2];
+  p[11] = t[-kTileS - 3];
   p[12] = t[-3];
-  p[13] = t[ts - 3];
-  p[14] = t[2 * ts - 2];
-  p[15] = t[3 * ts - 1];
+  p[13] = t[kTileS - 3];
+  p[14] = t[2 * kTileS - 2];
+  p[15] = t[3 * kTileS - 1];
   uint32_t dark = 0, bright = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -198,102 +316,144 @@ __device__ __forceinline__ int fast_score(const uint8_t* t, int ts, int tlo) {
     return r != 0;
   };
   if (!run9(dark) && !run9(bright)) return -1;
+  // cornerScore<16>: max over cyclic arcs of 9 of max(min d, -max d) - 1
   int d[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) d[k] = v - p[k];
+  int mn2[16], mx2[16], mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn2[k] = min(d[k], d[(k + 1) & 15]);
+    mx2[k] = max(d[k], d[(k + 1) & 15]);
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+  }
   int a0 = -1000, b0 = 1000;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    int mn = d[k], mx = d[k];
-#pragma unroll
-    for (int j = 1; j < 9; j++) {
-      mn = min(mn, d[(k + j) & 15]);
-      mx = max(mx, d[(k + j) & 15]);
-    }
-    a0 = max(a0, mn);
-    b0 = min(b0, mx);
+    const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+    const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+    a0 = max(a0, mn9);
+    b0 = min(b0, mx9);
   }
   return max(a0, -b0) - 1;
 }
 
-__global__ __launch_bounds__(BS) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int lane = threadIdx.x & 63;
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B) {
-  __shared__ uint8_t tile[(kMaxCell + 6) * (kMaxCell + 6)];
-  __shared__ int16_t sc[kMaxCell * kMaxCell];
-  __shared__ int wtot[BS / 64 + 1];
-  const int cell = blockIdx.x, img = blockIdx.y;
+  __shared__ uint8_t tile[(kMaxCell + 6) * kTileS];
+  __shared__ uint8_t smap[kMaxCell * kMapS];
+  __shared__ uint16_t list[kMaxCell * kMaxCell];
+  const int cell = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
   const CellInfo c = cells[cell];
-  const LevelGeom& L = G->lv[c.level];
-  const uint8_t* base = level_ptr(*G, B, img, c.level);
+  const int lw = G->lv[c.level].w;
+  const uint8_t* base = level_ptr(*G, B, img, c.level) + (size_t)(c.y0 - 3) * lw + (c.x0 - 3);
   const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TW = W + 6, TH = H + 6;
-  for (int q = threadIdx.x; q < TW * TH; q += BS) {
-    const int ty = q / TW, tx = q - ty * TW;
-    tile[q] = base[(size_t)(c.y0 - 3 + ty) * L.w + (c.x0 - 3 + tx)];
+  // (kMaxCell+6) rows x ceil((66+6)/4)+1 dwords / 64 lanes <= 22 loads per lane
+  window_to_lds<22>(base, lw, TH, TW, tile, kTileS, lane, 64);
+  {
+    uint32_t* m32 = (uint32_t*)smap;
+    for (int i = lane; i < H * kMapS / 4; i += 64) m32[i] = 0;
   }
   __syncthreads();
   const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255);
   const int tlo = min(ini, mint);
-  const int npx = W * H;
-  for (int q = threadIdx.x; q < npx; q += BS) {
-    const int y = q / W, x = q - y * W;
-    const int s = fast_score(&tile[(y + 3) * TW + x + 3], TW, tlo);
-    sc[q] = (int16_t)(s >= tlo ? s : -1);
+  const uint64_t lt = lanemask_lt();
+  // 2. compass quick test, row-major compaction
+  int n = 0;
+  for (int y = 0; y < H; y++) {
+    bool pass = false;
+    if (lane < W) {
+      const uint8_t* t = &tile[(y + 3) * kTileS + lane + 3];
+      const int v = t[0];
+      const int c0 = t[3 * kTileS], c4 = t[3], c8 = t[-3 * kTileS], c12 = t[-3];
+      const uint32_t dk = (uint32_t)(c0 < v - tlo) | (uint32_t)(c4 < v - tlo) << 1 |
+                          (uint32_t)(c8 < v - tlo) << 2 | (uint32_t)(c12 < v - tlo) << 3;
+      const uint32_t bk = (uint32_t)(c0 > v + tlo) | (uint32_t)(c4 > v + tlo) << 1 |
+                          (uint32_t)(c8 > v + tlo) << 2 | (uint32_t)(c12 > v + tlo) << 3;
+      const uint32_t dr = (dk >> 1) | ((dk & 1) << 3), br = (bk >> 1) | ((bk & 1) << 3);
+      pass = ((dk & dr) | (bk & br)) != 0;
+    }
+    const uint64_t m = __ballot(pass);
+    if (pass) list[n + __popcll(m & lt)] = (uint16_t)((y << 6) | lane);
+    n += __popcll(m);
   }
   __syncthreads();
-  auto kept = [&](int q, int t) -> bool {
-    const int s = sc[q];
-    if (s < t) return false;
-    const int y = q / W, x = q - y * W;
+  // 3. full segment test + score; corners compacted in place
+  int nc = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    int S = -1, pix = 0;
+    if (i < n) {
+      pix = list[i];
+      const int y = pix >> 6, x = pix & 63;
+      S = ring_score(&tile[(y + 3) * kTileS + x + 3], tlo);
+    }
+    const bool corner = S >= tlo;
+    const uint64_t m = __ballot(corner);
+    __syncthreads();
+    if (corner) {
+      list[nc + __popcll(m & lt)] = (uint16_t)pix;
+      smap[(pix >> 6) * kMapS + (pix & 63)] = (uint8_t)(S + 1);
+    }
+    nc += __popcll(m);
+  }
+  __syncthreads();
+  auto keep = [&](int pix, int thr) -> bool {  // thr = t + 1 in map units (S + 1)
+    const int y = pix >> 6, x = pix & 63;
+    const int s = smap[y * kMapS + x];
+    if (s < thr || s <= 1) return false;
+#pragma unroll
     for (int dy = -1; dy <= 1; dy++) {
       const int yy = y + dy;
       if (yy < 0 || yy >= H) continue;
+#pragma unroll
       for (int dx = -1; dx <= 1; dx++) {
         const int xx = x + dx;
         if ((dx == 0 && dy == 0) || xx < 0 || xx >= W) continue;
-        const int n = sc[yy * W + xx];
-        if (n >= t && !(s > n)) return false;
+        const int nv = smap[yy * kMapS + xx];
+        if (nv >= thr && nv >= s) return false;
       }
     }
     return true;
   };
-  int cnt_ini = 0;
-  for (int q = threadIdx.x; q < npx; q += BS) cnt_ini += kept(q, ini) ? 1 : 0;
-  cnt_ini = block_sum(cnt_ini);
-  const int t = cnt_ini > 0 ? ini : mint;
-  // row-major compaction: contiguous chunk per thread
-  const int chunk = (npx + BS - 1) / BS;
-  const int qb = threadIdx.x * chunk, qe = min(npx, qb + chunk);
-  int mine = 0;
-  for (int q = qb; q < qe; q++) mine += kept(q, t) ? 1 : 0;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int incl = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
+  // 4. survivors at iniThFAST
+  int cnt = 0;
+  for (int i0 = 0; i0 < nc; i0 += 64) {
+    const int i = i0 + lane;
+    const bool k = i < nc && keep(list[i], ini + 1);
+    cnt += __popcll(__ballot(k));
   }
-  if (lane == 63) wtot[wid] = incl;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int w = 0; w < BS / 64; w++) {
-      int v = wtot[w];
-      wtot[w] = s;
-      s += v;
-    }
-    wtot[BS / 64] = s;
-  }
-  __syncthreads();
-  int pos = wtot[wid] + incl - mine;
+  const int thr = (cnt > 0 ? ini : mint) + 1;
+  // 5. row-major writes at the chosen threshold
   uint32_t* out = B.cand + (size_t)img * G->cand_total + c.cand_off;
-  for (int q = qb; q < qe; q++) {
-    if (!kept(q, t)) continue;
-    const int y = q / W, x = q - y * W;
-    if (pos < c.cap)
-      out[pos] = ((uint32_t)sc[q] << 24) | ((uint32_t)(c.y0 + y) << 12) | (uint32_t)(c.x0 + x);
-    pos++;
+  int pos = 0;
+  for (int i0 = 0; i0 < nc; i0 += 64) {
+    const int i = i0 + lane;
+    int pix = 0;
+    bool k = false;
+    if (i < nc) {
+      pix = list[i];
+      k = keep(pix, thr);
+    }
+    const uint64_t m = __ballot(k);
+    if (k) {
+      const int p = pos + __popcll(m & lt);
+      const int y = pix >> 6, x = pix & 63;
+      if (p < c.cap)
+        out[p] = ((uint32_t)(smap[y * kMapS + x] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) | (uint32_t)(c.x0 + x);
+    }
+    pos += __popcll(m);
   }
-  if (threadIdx.x == 0) B.cell_count[(size_t)img * G->ncells + cell] = min(wtot[BS / 64], c.cap);
+  if (lane == 0) B.cell_count[(size_t)img * G->ncells + cell] = min(pos, c.cap);
 }
 
 // ----------------------------------------------------------------- octree
@@ -673,13 +833,18 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   if (lane < 62) {
     const int u = (lane % 31) - 15;
     const int au = u < 0 ? -u : u;
-    const int vb = lane < 31 ? -15 : 1, ve = lane < 31 ? 0 : 15;
-    for (int vv = vb; vv <= ve; vv++) {
+    const int vb = lane < 31 ? -15 : 1, nv = lane < 31 ? 16 : 15;
+    int I[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {  // all loads in flight before the sums
+      const int vv = vb + i;
       const int av = vv < 0 ? -vv : vv;
-      if (au > c_umax[av]) continue;
-      const int I = raw[(size_t)(y + vv) * w + (x + u)];
-      m10 += u * I;
-      m01 += vv * I;
+      I[i] = (i < nv && au <= c_umax[av]) ? raw[(ptrdiff_t)(y + vv) * w + (x + u)] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      m10 += u * I[i];
+      m01 += (vb + i) * I[i];
     }
   }
   m01 = wave_sum(m01);
@@ -690,7 +855,8 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   sincos_det(angle * factorPI, &sn, &cs);
   const float a = cs, b = sn;
   const uint8_t* blur = B.blur + (size_t)img * G->blur_bytes + L.boff;
-  const uint8_t* center = blur + (size_t)y * w + x;
+  const int bs = L.bstride;
+  const uint8_t* center = blur + (size_t)y * bs + x;
   int bits = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -702,7 +868,7 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
       const float px = (float)c_pattern[idx], py = (float)c_pattern[idx + 1];
       const int r = round_even(px * b + py * a);
       const int c = round_even(px * a - py * b);
-      t[e] = center[r * w + c];
+      t[e] = center[r * bs + c];
     }
     bits |= (t[0] < t[1]) << k;
   }
@@ -746,7 +912,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   }
   if (Gh.ncells > 0) {
     T->begin(st);
-    hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(BS), 0, st, Gd, cells, B);
+    hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(64), 0, st, Gd, cells, B);
     T->end(ST_FAST, st);
   } else {
     (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);

@@ -4,7 +4,7 @@
 // HBM layout per image (all u8, row-major, stride = level width):
 //   level 0            : the caller's input image itself (never copied)
 //   pyramid  (levels>=1): pyr  + img*pyr_bytes  + lv[l].off
-//   blurred  (all levels): blur + img*blur_bytes + lv[l].boff
+//   blurred  (all levels): blur + img*blur_bytes + lv[l].boff, row stride lv[l].bstride
 //   FAST candidates     : cand + img*cand_total + cells[c].cand_off   (u32 score<<24|y<<12|x)
 //   octree output       : oct  + img*oct_total  + lv[l].oct_off        (same packing, list order)
 #pragma once
@@ -21,7 +21,8 @@ constexpr int kEdgeThresholdHost = 19;  // EDGE_THRESHOLD, src/ORBextractor.cc:7
 struct LevelGeom {
   int w, h;
   long long off;    // offset of level in per-image pyramid buffer (levels >= 1)
-  long long boff;   // offset of level in per-image blurred buffer
+  long long boff;   // offset of level in per-image blurred buffer (256-B aligned)
+  int bstride;      // blurred row stride (multiple of 16 bytes)
   int minBX, minBY, maxBX, maxBY;  // FAST border box, src/ORBextractor.cc:829-832
   int cell_begin, cell_end;        // range in the cell table (row-major)
   int cand_begin, cand_cap;        // candidate slots of the level in the per-image buffer
@@ -60,7 +61,7 @@ struct ResizeY {
   int16_t b0, b1;
 };
 
-constexpr int kBlurTileW = 64, kBlurTileH = 16;
+constexpr int kBlurTileW = 128, kBlurTileH = 64;
 
 // Device pointers for one batch.
 struct BatchPtrs {
