@@ -278,29 +278,29 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
 //   4. NMS at iniThFAST -> count; 5. NMS at the chosen threshold -> ballot-ranked
 //      row-major writes
 constexpr int kMaxCell = 60;          // wCell,hCell <= 60 (checked on the host)
-constexpr int kTileS = 68;            // tile row stride (TW <= 66)
+constexpr int kTileMaxS = 79;         // LDS tile row stride in [76,79], == level stride (mod 4)
 constexpr int kMapS = 64;             // score-map row stride
 
-__device__ __forceinline__ int ring_score(const uint8_t* t, int tlo) {
-  // t points at the centre pixel inside the LDS tile (row stride kTileS)
+__device__ __forceinline__ int ring_score(const uint8_t* t, int S, int tlo) {
+  // t points at the centre pixel inside the LDS tile (row stride S)
   const int v = t[0];
   int p[16];
-  p[0] = t[3 * kTileS];
-  p[1] = t[3 * kTileS + 1];
-  p[2] = t[2 * kTileS + 2];
-  p[3] = t[kTileS + 3];
+  p[0] = t[3 * S];
+  p[1] = t[3 * S + 1];
+  p[2] = t[2 * S + 2];
+  p[3] = t[S + 3];
   p[4] = t[3];
-  p[5] = t[-kTileS + 3];
-  p[6] = t[-2 * kTileS + 2];
-  p[7] = t[-3 * kTileS + 1];
-  p[8] = t[-3 * kTileS];
-  p[9] = t[-3 * kTileS - 1];
-  p[10] = t[-2 * kTileS - 2];
-  p[11] = t[-kTileS - 3];
+  p[5] = t[-S + 3];
+  p[6] = t[-2 * S + 2];
+  p[7] = t[-3 * S + 1];
+  p[8] = t[-3 * S];
+  p[9] = t[-3 * S - 1];
+  p[10] = t[-2 * S - 2];
+  p[11] = t[-S - 3];
   p[12] = t[-3];
-  p[13] = t[kTileS - 3];
-  p[14] = t[2 * kTileS - 2];
-  p[15] = t[3 * kTileS - 1];
+  p[13] = t[S - 3];
+  p[14] = t[2 * S - 2];
+  p[15] = t[3 * S - 1];
   uint32_t dark = 0, bright = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -349,7 +349,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 
 __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B) {
-  __shared__ uint8_t tile[(kMaxCell + 6) * kTileS];
+  __shared__ __align__(16) uint8_t tile_raw[(kMaxCell + 6) * kTileMaxS + 8];
   __shared__ uint8_t smap[kMaxCell * kMapS];
   __shared__ uint16_t list[kMaxCell * kMaxCell];
   const int cell = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
@@ -357,8 +357,33 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const int lw = G->lv[c.level].w;
   const uint8_t* base = level_ptr(*G, B, img, c.level) + (size_t)(c.y0 - 3) * lw + (c.x0 - 3);
   const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TW = W + 6, TH = H + 6;
-  // (kMaxCell+6) rows x ceil((66+6)/4)+1 dwords / 64 lanes <= 22 loads per lane
-  window_to_lds<22>(base, lw, TH, TW, tile, kTileS, lane, 64);
+  // 1. window -> LDS.  With S == lw (mod 4) the aligned global dword j of row r
+  //    lands on an aligned LDS dword, so pixel (r, col) sits at r*S + s0 + col
+  //    for every row (s0 = alignment of the window's first byte).
+  const int S = 76 + ((lw - 76) & 3);
+  const uintptr_t a0 = (uintptr_t)base;
+  const int s0 = (int)(a0 & 3), wm = lw & 3;
+  {
+    const int rg = lane / 18, j = lane - rg * 18;  // 3 rows x 18 dwords per load instruction
+    uint32_t v[22];
+#pragma unroll
+    for (int k = 0; k < 22; k++) {
+      const int r = 3 * k + rg;
+      const int sr = (s0 + r * wm) & 3;
+      v[k] = 0;
+      if (rg < 3 && r < TH && 4 * j < sr + TW) {
+        const uintptr_t ar = a0 + (uintptr_t)r * lw;
+        v[k] = *((const uint32_t*)(ar & ~(uintptr_t)3) + j);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 22; k++) {
+      const int r = 3 * k + rg;
+      const int sr = (s0 + r * wm) & 3;
+      if (rg < 3 && r < TH && 4 * j < sr + TW) *(uint32_t*)&tile_raw[r * S + s0 - sr + 4 + 4 * j] = v[k];
+    }
+  }
+  const uint8_t* tile = tile_raw + 4 + s0;  // pixel (r, col) = tile[r*S + col]
   {
     uint32_t* m32 = (uint32_t*)smap;
     for (int i = lane; i < H * kMapS / 4; i += 64) m32[i] = 0;
@@ -367,42 +392,54 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255);
   const int tlo = min(ini, mint);
   const uint64_t lt = lanemask_lt();
-  // 2. compass quick test, row-major compaction
+  // 2. compass quick test, row-major compaction; rows_per = 2 when W <= 32
+  const int rows_per = W <= 32 ? 2 : 1;
+  const int ly = W <= 32 ? (lane >> 5) : 0, lx = W <= 32 ? (lane & 31) : lane;
   int n = 0;
-  for (int y = 0; y < H; y++) {
-    bool pass = false;
-    if (lane < W) {
-      const uint8_t* t = &tile[(y + 3) * kTileS + lane + 3];
-      const int v = t[0];
-      const int c0 = t[3 * kTileS], c4 = t[3], c8 = t[-3 * kTileS], c12 = t[-3];
-      const uint32_t dk = (uint32_t)(c0 < v - tlo) | (uint32_t)(c4 < v - tlo) << 1 |
-                          (uint32_t)(c8 < v - tlo) << 2 | (uint32_t)(c12 < v - tlo) << 3;
-      const uint32_t bk = (uint32_t)(c0 > v + tlo) | (uint32_t)(c4 > v + tlo) << 1 |
-                          (uint32_t)(c8 > v + tlo) << 2 | (uint32_t)(c12 > v + tlo) << 3;
-      const uint32_t dr = (dk >> 1) | ((dk & 1) << 3), br = (bk >> 1) | ((bk & 1) << 3);
-      pass = ((dk & dr) | (bk & br)) != 0;
+  constexpr int QU = 4;  // row groups per iteration: all their LDS reads in flight together
+  for (int y0r = 0; y0r < H; y0r += QU * rows_per) {
+    bool pass[QU];
+#pragma unroll
+    for (int u = 0; u < QU; u++) {
+      const int y = y0r + u * rows_per + ly;
+      pass[u] = false;
+      if (lx < W && y < H) {
+        const uint8_t* t = &tile[(y + 3) * S + lx + 3];
+        const int v = t[0];
+        const int c0 = t[3 * S], c4 = t[3], c8 = t[-3 * S], c12 = t[-3];
+        const uint32_t dk = (uint32_t)(c0 < v - tlo) | (uint32_t)(c4 < v - tlo) << 1 |
+                            (uint32_t)(c8 < v - tlo) << 2 | (uint32_t)(c12 < v - tlo) << 3;
+        const uint32_t bk = (uint32_t)(c0 > v + tlo) | (uint32_t)(c4 > v + tlo) << 1 |
+                            (uint32_t)(c8 > v + tlo) << 2 | (uint32_t)(c12 > v + tlo) << 3;
+        const uint32_t dr = (dk >> 1) | ((dk & 1) << 3), br = (bk >> 1) | ((bk & 1) << 3);
+        pass[u] = ((dk & dr) | (bk & br)) != 0;
+      }
     }
-    const uint64_t m = __ballot(pass);
-    if (pass) list[n + __popcll(m & lt)] = (uint16_t)((y << 6) | lane);
-    n += __popcll(m);
+#pragma unroll
+    for (int u = 0; u < QU; u++) {
+      const int y = y0r + u * rows_per + ly;
+      const uint64_t m = __ballot(pass[u]);
+      if (pass[u]) list[n + __popcll(m & lt)] = (uint16_t)((y << 6) | lx);
+      n += __popcll(m);
+    }
   }
   __syncthreads();
   // 3. full segment test + score; corners compacted in place
   int nc = 0;
   for (int i0 = 0; i0 < n; i0 += 64) {
     const int i = i0 + lane;
-    int S = -1, pix = 0;
+    int Sc = -1, pix = 0;
     if (i < n) {
       pix = list[i];
       const int y = pix >> 6, x = pix & 63;
-      S = ring_score(&tile[(y + 3) * kTileS + x + 3], tlo);
+      Sc = ring_score(&tile[(y + 3) * S + x + 3], S, tlo);
     }
-    const bool corner = S >= tlo;
+    const bool corner = Sc >= tlo;
     const uint64_t m = __ballot(corner);
     __syncthreads();
     if (corner) {
       list[nc + __popcll(m & lt)] = (uint16_t)pix;
-      smap[(pix >> 6) * kMapS + (pix & 63)] = (uint8_t)(S + 1);
+      smap[(pix >> 6) * kMapS + (pix & 63)] = (uint8_t)(Sc + 1);
     }
     nc += __popcll(m);
   }
@@ -830,16 +867,25 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   // IC_Angle: lanes 0..61 -> column u = lane%31-15, rows v in [-15,0] or [1,15]
   const uint8_t* raw = level_ptr(*G, B, img, l);
   int m01 = 0, m10 = 0;
-  if (lane < 62) {
-    const int u = (lane % 31) - 15;
+  {
+    // circle table in scalar registers; every load below is unconditional (the
+    // 31x31 box around a keypoint is always inside its level) and masked by
+    // multiplication, so all 16 loads are in flight together
+    int um[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) um[i] = c_umax[i];
+    const bool lo = lane < 31;
+    const int u = lane < 62 ? (lane % 31) - 15 : 0;
     const int au = u < 0 ? -u : u;
-    const int vb = lane < 31 ? -15 : 1, nv = lane < 31 ? 16 : 15;
+    const int vb = lo ? -15 : 1;
+    const uint8_t* col = raw + (ptrdiff_t)(y + vb) * w + (x + u);
     int I[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) {  // all loads in flight before the sums
-      const int vv = vb + i;
-      const int av = vv < 0 ? -vv : vv;
-      I[i] = (i < nv && au <= c_umax[av]) ? raw[(ptrdiff_t)(y + vv) * w + (x + u)] : 0;
+    for (int i = 0; i < 16; i++) {
+      const int lim = lo ? um[15 - i] : (i < 15 ? um[1 + i] : -1);
+      const int ok = (lane < 62 && au <= lim) ? 1 : 0;
+      const int r = i < 15 || lo ? i : 14;  // lanes >= 31 have 15 rows; row 15 re-reads row 14 (masked)
+      I[i] = (int)col[(ptrdiff_t)r * w] * ok;
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) {
