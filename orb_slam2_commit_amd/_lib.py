@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liborbx.so")
+LIB_PATH = os.environ.get("ORBX_LIB_OVERRIDE") or os.path.join(_HERE, "liborbx.so")  # override: A/B experiments only
 
 ORBX_OK = 0
 ORBX_ERR_ARG = -1

@@ -281,10 +281,11 @@ constexpr int kMaxCell = 60;          // wCell,hCell <= 60 (checked on the host)
 constexpr int kTileMaxS = 79;         // LDS tile row stride in [76,79], == level stride (mod 4)
 constexpr int kMapS = 64;             // score-map row stride
 
-__device__ __forceinline__ int ring_score(const uint8_t* t, int S, int tlo) {
-  // t points at the centre pixel inside the LDS tile (row stride S)
-  const int v = t[0];
-  int p[16];
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void ring_load(const uint8_t* t, int S, int p[16]) {
+  // t points at the centre pixel inside the LDS tile (row stride S); Bresenham
+  // circle of radius 3 in OpenCV's makeOffsets order
   p[0] = t[3 * S];
   p[1] = t[3 * S + 1];
   p[2] = t[2 * S + 2];
@@ -301,6 +302,13 @@ __device__ __forceinline__ int ring_score(const uint8_t* t, int S, int tlo) {
   p[13] = t[S - 3];
   p[14] = t[2 * S - 2];
   p[15] = t[3 * S - 1];
+}
+
+// Segment test: >= 9 contiguous ring pixels all < v-t or all > v+t.
+__device__ __forceinline__ bool ring_corner(const uint8_t* t, int S, int tlo) {
+  int p[16];
+  ring_load(t, S, p);
+  const int v = t[0];
   uint32_t dark = 0, bright = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -313,33 +321,34 @@ __device__ __forceinline__ int ring_score(const uint8_t* t, int S, int tlo) {
     r &= r >> 2;
     r &= r >> 4;
     r &= m >> 8;
-    return r != 0;
+    return r;
   };
-  if (!run9(dark) && !run9(bright)) return -1;
-  // cornerScore<16>: max over cyclic arcs of 9 of max(min d, -max d) - 1
-  int d[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) d[k] = v - p[k];
-  int mn2[16], mx2[16], mn4[16], mx4[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn2[k] = min(d[k], d[(k + 1) & 15]);
-    mx2[k] = max(d[k], d[(k + 1) & 15]);
-  }
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-  }
-  int a0 = -1000, b0 = 1000;
+  return (run9(dark) | run9(bright)) != 0;
+}
+
+// cornerScore<16>: max over the 16 cyclic arcs of 9 of max(min d, min -d) - 1,
+// d = centre - ring.  (d, -d) ride together in packed int16 lanes.
+__device__ __forceinline__ int ring_score(const uint8_t* t, int S) {
+  int p[16];
+  ring_load(t, S, p);
+  const int v = t[0];
+  short2v q[16], m2[16], m4[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-    const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-    a0 = max(a0, mn9);
-    b0 = min(b0, mx9);
+    const short d = (short)(v - p[k]);
+    q[k] = (short2v){d, (short)-d};
   }
-  return max(a0, -b0) - 1;
+#pragma unroll
+  for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(q[k], q[(k + 1) & 15]);
+#pragma unroll
+  for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+  short2v best = (short2v){(short)-1000, (short)-1000};
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const short2v m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), q[(k + 8) & 15]);
+    best = __builtin_elementwise_max(best, m9);
+  }
+  return max((int)best.x, (int)best.y) - 1;
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -424,24 +433,30 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     }
   }
   __syncthreads();
-  // 3. full segment test + score; corners compacted in place
+  // 3a. full segment test on the compass list; corners compacted in place
   int nc = 0;
   for (int i0 = 0; i0 < n; i0 += 64) {
     const int i = i0 + lane;
-    int Sc = -1, pix = 0;
+    int pix = 0;
+    bool corner = false;
     if (i < n) {
       pix = list[i];
-      const int y = pix >> 6, x = pix & 63;
-      Sc = ring_score(&tile[(y + 3) * S + x + 3], S, tlo);
+      corner = ring_corner(&tile[((pix >> 6) + 3) * S + (pix & 63) + 3], S, tlo);
     }
-    const bool corner = Sc >= tlo;
     const uint64_t m = __ballot(corner);
     __syncthreads();
-    if (corner) {
-      list[nc + __popcll(m & lt)] = (uint16_t)pix;
-      smap[(pix >> 6) * kMapS + (pix & 63)] = (uint8_t)(Sc + 1);
-    }
+    if (corner) list[nc + __popcll(m & lt)] = (uint16_t)pix;
     nc += __popcll(m);
+  }
+  __syncthreads();
+  // 3b. cornerScore on the corners only; score map holds S+1
+  for (int i0 = 0; i0 < nc; i0 += 64) {
+    const int i = i0 + lane;
+    if (i < nc) {
+      const int pix = list[i];
+      const int sc = ring_score(&tile[((pix >> 6) + 3) * S + (pix & 63) + 3], S);
+      smap[(pix >> 6) * kMapS + (pix & 63)] = (uint8_t)(sc + 1);
+    }
   }
   __syncthreads();
   auto keep = [&](int pix, int thr) -> bool {  // thr = t + 1 in map units (S + 1)
