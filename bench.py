@@ -94,14 +94,10 @@ def cpu_baseline(pairs, seconds):
 def main():
     args = parse()
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+    from orb_slam2_commit_amd import dist as odist
+    rank, local, world = odist.env_rank()
+    odist.init("nccl", rank, world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -110,7 +106,7 @@ def main():
 
     W, H, B = KITTI["width"], KITTI["height"], args.batch
     # synthetic frames: distinct seeds per rank (frame shards), tiled into the batch
-    pairs = [synth.stereo_pair(1000 * rank + s, W, H) for s in range(args.unique)]
+    pairs = [synth.stereo_pair(seed, W, H) for seed in odist.frame_seeds(rank, args.unique)]
     host = np.stack([pairs[f % len(pairs)][k] for f in range(B) for k in (0, 1)])
     images = torch.from_numpy(host).to(dev)
     ex = ORBextractor(KITTI["nfeatures"], 1.2, 8, 20, 7, device=local)
@@ -133,21 +129,16 @@ def main():
     L = _lib.lib()
     L.orbx_profile_reset(ex._h)
     L.orbx_profile_enable(ex._h, 1)
-    if world > 1:
-        dist.barrier()
+    odist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    odist.barrier()
     elapsed = time.perf_counter() - t0
     L.orbx_profile_enable(ex._h, 0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = odist.max_over_ranks(elapsed, dev)
 
     # per-stage live HIP-event timings on the stream the kernels ran on
     import ctypes as C
@@ -184,8 +175,7 @@ def main():
                         frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic,
                         algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4))
 
-    frames = B * args.steps * world
-    value = frames / elapsed
+    value = odist.job_throughput(B, args.steps, world, elapsed)
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -214,6 +204,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

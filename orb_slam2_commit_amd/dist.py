@@ -1,0 +1,49 @@
+"""Multi-GPU plumbing for the frame-sharded hot path.
+
+Extraction + stereo matching of a frame is a pure function of that frame, so
+frames shard across ranks with no data-path collective; the only
+communication is the benchmark's barrier and the max-over-ranks of the timed
+region (torch.distributed; backend "nccl" = RCCL on ROCm, "gloo" in CPU tests).
+"""
+import os
+
+
+def env_rank():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def init(backend, rank, world):
+    import torch.distributed as dist
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    return world > 1
+
+
+def frame_seeds(rank, n_unique):
+    """Distinct synthetic stereo scenes per rank (each rank owns its frame shard)."""
+    return [1000 * rank + s for s in range(n_unique)]
+
+
+def max_over_ranks(value, device=None):
+    """Max of a float over all ranks (the slowest rank defines the job time)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
+def job_throughput(frames_per_rank_per_step, steps, world, elapsed_max):
+    """Whole-job frames/s: every rank's frames over the slowest rank's time."""
+    return frames_per_rank_per_step * steps * world / elapsed_max

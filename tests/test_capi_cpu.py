@@ -1,0 +1,64 @@
+"""CPU checks of the C-ABI library: it loads, exports every declared entry
+point, and refuses (loudly) to run without a GPU -- no compute calls here."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "orb_slam2_commit_amd", "liborbx.so")
+
+
+def declared(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(orbx_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "orb_slam2_commit_amd", "csrc")])
+    from orb_slam2_commit_amd import _lib
+    return _lib.lib()
+
+
+def test_exports_every_declared_symbol(lib):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
+    exported = set(re.findall(r" T (orbx_\w+)", out))
+    for h in ("orbx.h", "orbx_debug.h"):
+        names = declared(h)
+        assert names, h
+        missing = [n for n in names if n not in exported]
+        assert not missing, (h, missing)
+
+
+def test_python_signatures_cover_abi(lib):
+    from orb_slam2_commit_amd import _lib
+    for h in ("orbx.h", "orbx_debug.h"):
+        for n in declared(h):
+            assert n in _lib.SIGNATURES, n
+
+
+def test_no_gpu_fails_loudly(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from orb_slam2_commit_amd import ORBextractor, OrbxError
+    assert lib.orbx_device_count() == 0
+    with pytest.raises(OrbxError) as e:
+        ORBextractor(1000, 1.2, 8, 20, 7)
+    assert e.value.code == -4
+
+
+def test_version(lib):
+    assert b"gfx950" in lib.orbx_version()
+
+
+def test_keypoint_layout():
+    import numpy as np
+    from orb_slam2_commit_amd import KEYPOINT_DTYPE
+    assert KEYPOINT_DTYPE.itemsize == 28  # cv::KeyPoint
+    assert [KEYPOINT_DTYPE.fields[f][1] for f in KEYPOINT_DTYPE.names] == [0, 4, 8, 12, 16, 20, 24]
+    assert np.dtype(KEYPOINT_DTYPE)

@@ -1,0 +1,54 @@
+"""world_size-2 gloo rehearsal of the multi-GPU bench path on CPU.
+
+Frames shard across ranks with no data-path collective; ranks meet only at the
+barrier and at the max-over-ranks of the timed region (orb_slam2_commit_amd/dist.py)."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from orb_slam2_commit_amd import dist as odist
+    import torch.distributed as dist
+    odist.init("gloo", rank, world)
+    odist.barrier()
+    elapsed = 1.0 + rank  # rank 1 is the slow one
+    m = odist.max_over_ranks(elapsed)
+    seeds = odist.frame_seeds(rank, 4)
+    q.put((rank, m, seeds, odist.job_throughput(8, 10, world, m)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_max_and_shards():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] == 2.0 for r in res)  # max over ranks
+    assert set(res[0][2]).isdisjoint(res[1][2])  # disjoint frame shards
+    assert res[0][3] == pytest.approx(8 * 10 * 2 / 2.0)
+
+
+def test_single_rank_noop():
+    from orb_slam2_commit_amd import dist as odist
+    assert odist.max_over_ranks(3.5) == 3.5
+    assert odist.job_throughput(128, 20, 1, 2.0) == 1280.0
