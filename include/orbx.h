@@ -20,6 +20,12 @@
  *   orbx_stereo_frames_device   extract(L)+extract(R)+ComputeStereoMatches for n stereo frames
  *   orbx_descriptor_distance_device
  *                               ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1844-1860, include/ORBmatcher.h:50
+ *   orbx_search_by_bow_kf_f     ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+ *                                                               src/ORBmatcher.cc:175-325, include/ORBmatcher.h:61
+ *   orbx_search_by_bow_kf_kf    ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)
+ *                                                               src/ORBmatcher.cc:589-736, include/ORBmatcher.h:62
+ *   orbx_search_by_bow_device   batch of the two above (one block per problem); ComputeThreeMaxima
+ *                               (src/ORBmatcher.cc:1797-1839) runs inside
  */
 #ifndef ORBX_H
 #define ORBX_H
@@ -108,6 +114,43 @@ orbx_status orbx_stereo_frames_device(orbx_extractor* h, int n_frames, const uin
 /* Batched ORBmatcher::DescriptorDistance on device: d_out[i] = popcount(a_i ^ b_i). */
 orbx_status orbx_descriptor_distance_device(const uint8_t* d_a, const uint8_t* d_b, int n, int32_t* d_out,
                                             void* stream);
+
+/* One side of SearchByBoW: n features (descriptors n x 32, keypoint angles),
+ * MapPoint validity valid[i] = (mvpMapPoints[i] && !isBad()) (NULL = all valid;
+ * ignored for the Frame side), and the DBoW2::FeatureVector as CSR: n_nodes
+ * ascending node ids, node_off[n_nodes+1], feat[] = feature indices of each
+ * node in vector order. */
+typedef struct {
+  int n;
+  const uint8_t* desc;
+  const float* angle;
+  const uint8_t* valid;
+  int n_nodes;
+  const uint32_t* node_id;
+  const int32_t* node_off;
+  const int32_t* feat;
+} orbx_bow_side;
+
+/* Host pointers in and out.  KF-F: match_f[f->n] = KF feature index matched to
+ * each frame feature (the reference stores KF MapPoint*), -1 otherwise.
+ * KF-KF: match12[kf1->n] = KF2 feature index or -1.  *nmatches = the return
+ * value of the reference.  nnratio/check_ori = ORBmatcher(nnratio, checkOri). */
+orbx_status orbx_search_by_bow_kf_f(const orbx_bow_side* kf, const orbx_bow_side* f, float nnratio, int check_ori,
+                                    int32_t* match_f, int* nmatches, int device);
+orbx_status orbx_search_by_bow_kf_kf(const orbx_bow_side* kf1, const orbx_bow_side* kf2, float nnratio,
+                                     int check_ori, int32_t* match12, int* nmatches, int device);
+
+/* Batched, device-resident: problems[] is a HOST array whose pointers are device
+ * pointers; mode 0 = KF-F, 1 = KF-KF.  Each problem writes match[] and *nmatches. */
+typedef struct {
+  orbx_bow_side a, b;
+  float nnratio;
+  int check_ori;
+  int mode;
+  int32_t* match;
+  int32_t* nmatches;
+} orbx_bow_problem;
+orbx_status orbx_search_by_bow_device(const orbx_bow_problem* problems, int n, void* stream);
 
 /* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
  * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel

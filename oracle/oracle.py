@@ -20,6 +20,11 @@ class Params(C.Structure):
                 ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
 
 
+class BowSide(C.Structure):
+    _fields_ = [("n", C.c_int), ("desc", C.c_void_p), ("angle", C.c_void_p), ("valid", C.c_void_p),
+                ("n_nodes", C.c_int), ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("feat", C.c_void_p)]
+
+
 _lib = None
 
 
@@ -47,6 +52,9 @@ def lib():
         L.oracle_hamming_pairs.argtypes = [P, P, C.c_int, P]
         L.oracle_stereo_match.argtypes = [C.POINTER(Params), P, P, C.c_int, P, P, C.c_int, P, P, P,
                                           C.c_float, C.c_float, P, P]
+        L.oracle_search_by_bow_kf_f.argtypes = [C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P]
+        L.oracle_search_by_bow_kf_kf.argtypes = [C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P]
+        L.oracle_three_maxima.argtypes = [P, C.c_int, P, P, P]
         _lib = L
     return _lib
 
@@ -155,3 +163,30 @@ def hamming_pairs(a, b):
     d = np.zeros(len(a), np.int32)
     lib().oracle_hamming_pairs(_p(a), _p(b), len(a), _p(d))
     return d
+
+
+def _bow_side(side):
+    arrs = dict(desc=np.ascontiguousarray(side["desc"], np.uint8),
+                angle=np.ascontiguousarray(side["angle"], np.float32),
+                valid=None if side.get("valid") is None else np.ascontiguousarray(side["valid"], np.uint8),
+                node_id=np.ascontiguousarray(side["node_id"], np.uint32),
+                node_off=np.ascontiguousarray(side["node_off"], np.int32),
+                feat=np.ascontiguousarray(side["feat"], np.int32))
+    return BowSide(len(arrs["desc"]), _p(arrs["desc"]), _p(arrs["angle"]), _p(arrs["valid"]), len(arrs["node_id"]),
+                   _p(arrs["node_id"]), _p(arrs["node_off"]), _p(arrs["feat"])), arrs
+
+
+def search_by_bow(side_a, side_b, nnratio=0.6, check_ori=True, kf_kf=False):
+    A, ka = _bow_side(side_a)
+    B, kb = _bow_side(side_b)
+    match = np.zeros(A.n if kf_kf else B.n, np.int32)
+    fn = lib().oracle_search_by_bow_kf_kf if kf_kf else lib().oracle_search_by_bow_kf_f
+    n = fn(C.byref(A), C.byref(B), C.c_float(nnratio), int(check_ori), _p(match))
+    return match, n
+
+
+def three_maxima(counts):
+    c = np.ascontiguousarray(counts, np.int32)
+    out = [np.zeros(1, np.int32) for _ in range(3)]
+    lib().oracle_three_maxima(_p(c), len(c), *[_p(o) for o in out])
+    return tuple(int(o[0]) for o in out)

@@ -824,3 +824,131 @@ int oracle_stereo_match(const oracle_params* p, const oracle_keypoint* kL, const
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ SearchByBoW
+namespace {
+
+const int kThLow = 50, kHistoLength = 30;  // src/ORBmatcher.cc:37-39
+
+// ORBmatcher::ComputeThreeMaxima, src/ORBmatcher.cc:1797-1839.
+void three_maxima(const int* h, int L, int& ind1, int& ind2, int& ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  for (int i = 0; i < L; i++) {
+    const int s = h[i];
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s;
+      ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) {
+    ind2 = -1;
+    ind3 = -1;
+  } else if (max3 < 0.1f * (float)max1) {
+    ind3 = -1;
+  }
+}
+
+int rot_bin(float angA, float angB) {
+  const float factor = 1.0f / kHistoLength;
+  float rot = angA - angB;
+  if (rot < 0.0) rot += 360.0f;
+  int bin = (int)std::round(rot * factor);
+  if (bin == kHistoLength) bin = 0;
+  return bin;
+}
+
+// Merge-walk of two FeatureVectors (std::map iteration with lower_bound jumps
+// visits exactly the common node ids in ascending order).
+template <class F>
+void for_common_nodes(const oracle_bow_side& a, const oracle_bow_side& b, F fn) {
+  int i = 0, j = 0;
+  while (i < a.n_nodes && j < b.n_nodes) {
+    if (a.node_id[i] == b.node_id[j]) {
+      fn(i, j);
+      i++;
+      j++;
+    } else if (a.node_id[i] < b.node_id[j]) {
+      i++;
+    } else {
+      j++;
+    }
+  }
+}
+
+int search_by_bow(const oracle_bow_side& A, const oracle_bow_side& B, float nnratio, bool checkOri, bool kfkf,
+                  int32_t* match, int nmatch_out) {
+  // match indexed by B feature (KF-F) or by A feature (KF-KF)
+  for (int i = 0; i < nmatch_out; i++) match[i] = -1;
+  std::vector<char> matchedB(B.n, 0);
+  std::vector<int> rotHist[kHistoLength];
+  int nmatches = 0;
+  for_common_nodes(A, B, [&](int ia, int jb) {
+    for (int pa = A.node_off[ia]; pa < A.node_off[ia + 1]; pa++) {
+      const int idxA = A.feat[pa];
+      if (A.valid && !A.valid[idxA]) continue;
+      int best1 = 256, bestIdx = -1, best2 = 256;
+      for (int pb = B.node_off[jb]; pb < B.node_off[jb + 1]; pb++) {
+        const int idxB = B.feat[pb];
+        if (matchedB[idxB]) continue;
+        if (kfkf && B.valid && !B.valid[idxB]) continue;
+        const int dist = descriptor_distance(A.desc + 32 * (size_t)idxA, B.desc + 32 * (size_t)idxB);
+        if (dist < best1) {
+          best2 = best1;
+          best1 = dist;
+          bestIdx = idxB;
+        } else if (dist < best2) {
+          best2 = dist;
+        }
+      }
+      const bool pass = kfkf ? best1 < kThLow : best1 <= kThLow;
+      if (!pass) continue;
+      if (!((float)best1 < nnratio * (float)best2)) continue;
+      matchedB[bestIdx] = 1;
+      const int out = kfkf ? idxA : bestIdx;
+      match[out] = kfkf ? bestIdx : idxA;
+      if (checkOri) rotHist[rot_bin(A.angle[idxA], B.angle[bestIdx])].push_back(out);
+      nmatches++;
+    }
+  });
+  if (checkOri) {
+    int counts[kHistoLength];
+    for (int i = 0; i < kHistoLength; i++) counts[i] = (int)rotHist[i].size();
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(counts, kHistoLength, ind1, ind2, ind3);
+    for (int i = 0; i < kHistoLength; i++) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (int o : rotHist[i]) {
+        match[o] = -1;
+        nmatches--;
+      }
+    }
+  }
+  return nmatches;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oracle_search_by_bow_kf_f(const oracle_bow_side* kf, const oracle_bow_side* f, float nnratio, int check_ori,
+                              int32_t* match_f) {
+  return search_by_bow(*kf, *f, nnratio, check_ori != 0, false, match_f, f->n);
+}
+
+int oracle_search_by_bow_kf_kf(const oracle_bow_side* kf1, const oracle_bow_side* kf2, float nnratio, int check_ori,
+                               int32_t* match12) {
+  return search_by_bow(*kf1, *kf2, nnratio, check_ori != 0, true, match12, kf1->n);
+}
+
+void oracle_three_maxima(const int* counts, int L, int* ind1, int* ind2, int* ind3) {
+  *ind1 = *ind2 = *ind3 = -1;
+  three_maxima(counts, L, *ind1, *ind2, *ind3);
+}
+
+}  // extern "C"

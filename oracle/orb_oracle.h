@@ -74,6 +74,30 @@ int oracle_stereo_match(const oracle_params* p,
                         const uint8_t* pyrL, const uint8_t* pyrR, const int* level_wh,
                         float bf, float baseline, float* uRight, float* depth);
 
+/* One side of SearchByBoW: descriptors, keypoint angles, MapPoint validity
+ * (NULL = all valid) and its DBoW2::FeatureVector as CSR (ascending node ids). */
+typedef struct {
+  int n;
+  const uint8_t* desc;
+  const float* angle;
+  const uint8_t* valid;
+  int n_nodes;
+  const uint32_t* node_id;
+  const int32_t* node_off;
+  const int32_t* feat;
+} oracle_bow_side;
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&), src/ORBmatcher.cc:175-325.
+ * match_f[f->n] = KF feature index matched to each frame feature, or -1. Returns nmatches. */
+int oracle_search_by_bow_kf_f(const oracle_bow_side* kf, const oracle_bow_side* f, float nnratio, int check_ori,
+                              int32_t* match_f);
+/* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&), src/ORBmatcher.cc:589-736.
+ * match12[kf1->n] = KF2 feature index or -1. Returns nmatches. */
+int oracle_search_by_bow_kf_kf(const oracle_bow_side* kf1, const oracle_bow_side* kf2, float nnratio, int check_ori,
+                               int32_t* match12);
+/* ORBmatcher::ComputeThreeMaxima, src/ORBmatcher.cc:1797-1839 (on bin counts). */
+void oracle_three_maxima(const int* counts, int L, int* ind1, int* ind2, int* ind3);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,16 @@ class ExtractorParams(C.Structure):
                 ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
 
 
+class BowSide(C.Structure):
+    _fields_ = [("n", C.c_int), ("desc", C.c_void_p), ("angle", C.c_void_p), ("valid", C.c_void_p),
+                ("n_nodes", C.c_int), ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("feat", C.c_void_p)]
+
+
+class BowProblem(C.Structure):
+    _fields_ = [("a", BowSide), ("b", BowSide), ("nnratio", C.c_float), ("check_ori", C.c_int), ("mode", C.c_int),
+                ("match", C.c_void_p), ("nmatches", C.c_void_p)]
+
+
 # Every entry point of include/orbx.h with its ctypes signature.
 P = C.c_void_p
 SIGNATURES = {
@@ -55,6 +65,11 @@ SIGNATURES = {
     "orbx_stereo_frames_device": ([P, C.c_int, P, C.c_int, C.c_int, C.c_size_t, P, P, P, C.c_int, C.c_float,
                                    C.c_float, P, P, P, P], C.c_int),
     "orbx_descriptor_distance_device": ([P, P, C.c_int, P, P], C.c_int),
+    "orbx_search_by_bow_kf_f": ([C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P,
+                                 C.POINTER(C.c_int), C.c_int], C.c_int),
+    "orbx_search_by_bow_kf_kf": ([C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P,
+                                  C.POINTER(C.c_int), C.c_int], C.c_int),
+    "orbx_search_by_bow_device": ([C.POINTER(BowProblem), C.c_int, P], C.c_int),
     "orbx_device_count": ([], C.c_int),
     "orbx_version": ([], C.c_char_p),
     "orbx_profile_enable": ([P, C.c_int], C.c_int),

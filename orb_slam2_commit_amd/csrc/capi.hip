@@ -21,6 +21,7 @@
 #include "orbx_internal.h"
 #include "orbx_stereo.h"
 #include "orbx_prof.h"
+#include "orbx_bow.h"
 
 namespace orbx {
 hipError_t upload_constants(const int* umax16, const int* gauss7);
@@ -641,6 +642,84 @@ orbx_status orbx_stereo_frames_device(orbx_extractor* h, int n_frames, const uin
   return run_stereo(h, h, n_frames, d_kps, d_desc, d_counts, 2 * kc, 2, d_kps + kc, d_desc + kc * 32, d_counts + 1,
                     2 * kc, 2, 2, 0, 2, 1, h->last_plan->G.max_kps, bf, baseline, d_uright, d_depth, kc,
                     d_nmatches, pick_stream(h, stream));
+}
+
+static orbx_status bow_host(const orbx_bow_side* A, const orbx_bow_side* B, float nnratio, int check_ori, int mode,
+                            int32_t* match, int* nmatches, int device) {
+  if (!A || !B || !match || !nmatches) return ORBX_ERR_ARG;
+  const int nout = mode ? A->n : B->n;
+  *nmatches = 0;
+  if (A->n > kMaxBowFeatures || B->n > kMaxBowFeatures || A->n < 0 || B->n < 0) return ORBX_ERR_CAPACITY;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_NODEV;
+  if (device < 0 || device >= ndev || hipSetDevice(device) != hipSuccess) return ORBX_ERR_ARG;
+  // one arena: both sides' arrays + outputs + the problem descriptor
+  auto side_bytes = [](const orbx_bow_side* s) {
+    return (size_t)s->n * 32 + (size_t)s->n * 4 + (size_t)s->n + (size_t)s->n_nodes * 4 +
+           (size_t)(s->n_nodes + 1) * 4 + (size_t)(s->n_nodes ? s->node_off[s->n_nodes] : 0) * 4 + 64;
+  };
+  const size_t bytes = side_bytes(A) + side_bytes(B) + (size_t)nout * 4 + 64 + sizeof(BowProblem) + 64;
+  std::vector<uint8_t> host(bytes, 0);
+  uint8_t* dbase = nullptr;
+  if (hipMalloc((void**)&dbase, bytes) != hipSuccess) return ORBX_ERR_HIP;
+  size_t off = 0;
+  auto put = [&](const void* src, size_t nbytes) -> void* {
+    off = (off + 15) & ~(size_t)15;
+    if (src && nbytes) std::memcpy(host.data() + off, src, nbytes);
+    void* d = dbase + off;
+    off += nbytes;
+    return d;
+  };
+  auto side = [&](const orbx_bow_side* s) {
+    orbx_bow_side d = *s;
+    const int nf = s->n_nodes ? s->node_off[s->n_nodes] : 0;
+    d.desc = (const uint8_t*)put(s->desc, (size_t)s->n * 32);
+    d.angle = (const float*)put(s->angle, (size_t)s->n * 4);
+    d.valid = s->valid ? (const uint8_t*)put(s->valid, (size_t)s->n) : nullptr;
+    d.node_id = (const uint32_t*)put(s->node_id, (size_t)s->n_nodes * 4);
+    d.node_off = (const int32_t*)put(s->node_off, (size_t)(s->n_nodes + 1) * 4);
+    d.feat = (const int32_t*)put(s->feat, (size_t)nf * 4);
+    return d;
+  };
+  BowProblem P;
+  P.a = side(A);
+  P.b = side(B);
+  P.nnratio = nnratio;
+  P.check_ori = check_ori;
+  P.mode = mode;
+  P.match = (int32_t*)put(nullptr, (size_t)nout * 4);
+  P.nmatches = (int32_t*)put(nullptr, 4);
+  BowProblem* dP = (BowProblem*)put(&P, sizeof(P));
+  hipError_t e = hipMemcpy(dbase, host.data(), off, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_search_by_bow(dP, 1, nullptr);
+  if (e == hipSuccess && nout) e = hipMemcpy(match, P.match, (size_t)nout * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(nmatches, P.nmatches, 4, hipMemcpyDeviceToHost);
+  (void)hipFree(dbase);
+  return hip_status(e);
+}
+
+orbx_status orbx_search_by_bow_kf_f(const orbx_bow_side* kf, const orbx_bow_side* f, float nnratio, int check_ori,
+                                    int32_t* match_f, int* nmatches, int device) {
+  return bow_host(kf, f, nnratio, check_ori, 0, match_f, nmatches, device);
+}
+
+orbx_status orbx_search_by_bow_kf_kf(const orbx_bow_side* kf1, const orbx_bow_side* kf2, float nnratio,
+                                     int check_ori, int32_t* match12, int* nmatches, int device) {
+  return bow_host(kf1, kf2, nnratio, check_ori, 1, match12, nmatches, device);
+}
+
+orbx_status orbx_search_by_bow_device(const orbx_bow_problem* problems, int n, void* stream) {
+  if (n < 0 || (n > 0 && !problems)) return ORBX_ERR_ARG;
+  if (n == 0) return ORBX_OK;
+  for (int i = 0; i < n; i++)
+    if (problems[i].a.n > kMaxBowFeatures || problems[i].b.n > kMaxBowFeatures) return ORBX_ERR_CAPACITY;
+  hipStream_t st = (hipStream_t)stream;
+  BowProblem* dP = nullptr;
+  if (hipMallocAsync((void**)&dP, sizeof(BowProblem) * n, st) != hipSuccess) return ORBX_ERR_HIP;
+  hipError_t e = hipMemcpyAsync(dP, problems, sizeof(BowProblem) * n, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = launch_search_by_bow(dP, n, st);
+  hipError_t e2 = hipFreeAsync(dP, st);
+  return hip_status(e != hipSuccess ? e : e2);
 }
 
 orbx_status orbx_profile_enable(orbx_extractor* h, int enable) {

@@ -164,12 +164,41 @@ def compute_stereo_matches(extractor_left, extractor_right, kps_left, desc_left,
     return uR, depth
 
 
+def bow_side(side):
+    """dict(desc, angle, valid, node_id, node_off, feat) -> (orbx_bow_side, keep-alive arrays)."""
+    arrs = dict(desc=np.ascontiguousarray(side["desc"], np.uint8),
+                angle=np.ascontiguousarray(side["angle"], np.float32),
+                valid=None if side.get("valid") is None else np.ascontiguousarray(side["valid"], np.uint8),
+                node_id=np.ascontiguousarray(side["node_id"], np.uint32),
+                node_off=np.ascontiguousarray(side["node_off"], np.int32),
+                feat=np.ascontiguousarray(side["feat"], np.int32))
+    s = _lib.BowSide(len(arrs["desc"]), ptr(arrs["desc"]), ptr(arrs["angle"]), ptr(arrs["valid"]),
+                     len(arrs["node_id"]), ptr(arrs["node_id"]), ptr(arrs["node_off"]), ptr(arrs["feat"]))
+    return s, arrs
+
+
 class ORBmatcher:
     """ORBmatcher(nnratio=0.6, checkOri=True) -- include/ORBmatcher.h:47."""
 
-    def __init__(self, nnratio=0.6, checkOri=True):
+    def __init__(self, nnratio=0.6, checkOri=True, device=0):
         self.mfNNratio = float(nnratio)
         self.mbCheckOrientation = bool(checkOri)
+        self.device = int(device)
+
+    def SearchByBoW(self, side_a, side_b, kf_kf=False):
+        """SearchByBoW(KeyFrame*, Frame&) (kf_kf=False) or SearchByBoW(KeyFrame*, KeyFrame*) (kf_kf=True).
+
+        Sides are dicts (desc, angle, valid, node_id, node_off, feat).  Returns (match, nmatches):
+        KF-F: match[i_frame] = KF feature index or -1; KF-KF: match[i_kf1] = KF2 feature index or -1."""
+        A, ka = bow_side(side_a)
+        B, kb = bow_side(side_b)
+        nout = A.n if kf_kf else B.n
+        match = np.zeros(nout, np.int32)
+        n = C.c_int(0)
+        fn = _lib.lib().orbx_search_by_bow_kf_kf if kf_kf else _lib.lib().orbx_search_by_bow_kf_f
+        check(fn(C.byref(A), C.byref(B), C.c_float(self.mfNNratio), int(self.mbCheckOrientation), ptr(match),
+                 C.byref(n), self.device), "orbx_search_by_bow")
+        return match, n.value
 
     @staticmethod
     def DescriptorDistance(a, b):

@@ -93,3 +93,41 @@ def stereo_pair(seed, width=1241, height=376, n_shapes=None, stress=False):
 
 def mono_image(seed, width=640, height=480):
     return stereo_pair(seed, width, height)[0]
+
+
+def bow_problem(seed, n_a=1500, n_b=1500, n_nodes=100, n_true=700, noise_bits=12, rot_deg=25.0, p_valid=0.8):
+    """Synthetic SearchByBoW inputs: two feature sets sharing n_true noisy correspondences.
+
+    Returns dict(a=..., b=...) of side dicts {desc, angle, valid, node_id, node_off, feat}.
+    Corresponding features share a FeatureVector node and differ by `noise_bits`
+    flipped descriptor bits and a global rotation of `rot_deg` (plus outliers),
+    which exercises the ratio test, the TH_LOW gate and the rotation histogram.
+    """
+    rng = np.random.default_rng(seed)
+    da = rng.integers(0, 256, (n_a, 32), dtype=np.uint8)
+    db = rng.integers(0, 256, (n_b, 32), dtype=np.uint8)
+    node_a = rng.integers(0, n_nodes, n_a)
+    node_b = rng.integers(0, n_nodes, n_b)
+    ang_a = rng.uniform(0, 360, n_a).astype(np.float32)
+    ang_b = rng.uniform(0, 360, n_b).astype(np.float32)
+    ia = rng.choice(n_a, n_true, replace=False)
+    ib = rng.choice(n_b, n_true, replace=False)
+    bits = np.unpackbits(da[ia], axis=1)
+    for r in range(n_true):
+        flip = rng.choice(256, int(rng.integers(0, noise_bits + 1)), replace=False)
+        bits[r, flip] ^= 1
+    db[ib] = np.packbits(bits, axis=1)
+    node_b[ib] = node_a[ia]
+    rot = np.where(rng.uniform(size=n_true) < 0.85, rot_deg, rng.uniform(0, 360, n_true))
+    ang_b[ib] = np.mod(ang_a[ia] - rot + rng.normal(0, 2, n_true), 360).astype(np.float32)
+    ids = np.sort(rng.choice(10 ** 6, n_nodes, replace=False)).astype(np.uint32)
+
+    def side(desc, ang, node):
+        order = np.argsort(node, kind="stable")  # feature indices grouped by node, ascending index inside
+        counts = np.bincount(node, minlength=n_nodes)
+        present = counts > 0
+        off = np.concatenate([[0], np.cumsum(counts[present])]).astype(np.int32)
+        return dict(desc=desc, angle=ang, valid=(rng.uniform(size=len(desc)) < p_valid).astype(np.uint8),
+                    node_id=ids[present], node_off=off, feat=order.astype(np.int32))
+
+    return dict(a=side(da, ang_a, node_a), b=side(db, ang_b, node_b))
