@@ -26,6 +26,9 @@
  *                                                               src/ORBmatcher.cc:589-736, include/ORBmatcher.h:62
  *   orbx_search_by_bow_device   batch of the two above (one block per problem); ComputeThreeMaxima
  *                               (src/ORBmatcher.cc:1797-1839) runs inside
+ *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
+ *                               (g2o graph build, optimize(5), outlier levels, optimize(10), vToErase;
+ *                               the Map mutex/recovery part stays on the caller's side)
  */
 #ifndef ORBX_H
 #define ORBX_H
@@ -151,6 +154,52 @@ typedef struct {
   int32_t* nmatches;
 } orbx_bow_problem;
 orbx_status orbx_search_by_bow_device(const orbx_bow_problem* problems, int n, void* stream);
+
+/* Optimizer::LocalBundleAdjustment on g2o semantics (BlockSolver_6_3 +
+ * LinearSolverEigen + Levenberg, Huber kernels, two phases), FP64 on the GPU.
+ * The caller gathers lLocalKeyFrames (not fixed unless mnId==0),
+ * lFixedCameras (fixed) and lLocalMapPoints with their observations exactly
+ * as src/Optimizer.cc:530-650 does, and writes back poses, points and erases
+ * the flagged observations under the map mutex (:817-885).
+ *   cameras: Tcw row-major 3x4 float, fixed flag, intrinsics fx,fy,cx,cy,bf
+ *   edges:   point, camera, obs (u, v, ur; ur < 0 -> monocular
+ *            EdgeSE3ProjectXYZ, else EdgeStereoSE3ProjectXYZ), invSigma2 */
+typedef struct {
+  int n_cams;
+  const float* Tcw;
+  const uint8_t* fixed;
+  const float* intr;
+  int n_points;
+  const float* Xw;
+  int n_edges;
+  const int32_t* edge_point;
+  const int32_t* edge_cam;
+  const float* obs;
+  const float* inv_sigma2;
+} orbx_ba_problem;
+
+typedef struct {
+  float* Tcw;             /* n_cams x 12 (Converter::toCvMat of the optimised SE3Quat) */
+  float* Xw;              /* n_points x 3 */
+  uint8_t* edge_outlier;  /* n_edges: observation to erase (vToErase, :817-847) */
+  double* Tcw_d;          /* optional FP64 copies (NULL to skip) */
+  double* Xw_d;
+  int iterations[2];      /* LM iterations run by optimize(5) and optimize(10) */
+  int trials;             /* LM inner trials in total */
+  double chi2[2];         /* active robust chi2 at the end of each phase */
+} orbx_ba_result;
+
+typedef struct orbx_ba orbx_ba;
+/* A solver handle keeps its device buffers and HIP stream across calls. */
+orbx_status orbx_ba_create(int device, orbx_ba** out);
+orbx_status orbx_ba_destroy(orbx_ba* h);
+/* *stop_flag != 0 (the reference's pbStopFlag / setForceStopFlag) is polled
+ * before the run and between LM trials. */
+orbx_status orbx_ba_run(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_result* result,
+                        const volatile int* stop_flag);
+/* One-shot form: create, run, destroy. */
+orbx_status orbx_local_ba(const orbx_ba_problem* problem, orbx_ba_result* result, const volatile int* stop_flag,
+                          int device);
 
 /* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
  * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel

@@ -25,6 +25,17 @@ class BowSide(C.Structure):
                 ("n_nodes", C.c_int), ("node_id", C.c_void_p), ("node_off", C.c_void_p), ("feat", C.c_void_p)]
 
 
+class BaProblem(C.Structure):
+    _fields_ = [("n_cams", C.c_int), ("Tcw", C.c_void_p), ("fixed", C.c_void_p), ("intr", C.c_void_p),
+                ("n_points", C.c_int), ("Xw", C.c_void_p), ("n_edges", C.c_int), ("edge_point", C.c_void_p),
+                ("edge_cam", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
+
+
+class BaResult(C.Structure):
+    _fields_ = [("Tcw", C.c_void_p), ("Xw", C.c_void_p), ("edge_outlier", C.c_void_p), ("Tcw_d", C.c_void_p),
+                ("Xw_d", C.c_void_p), ("iterations", C.c_int * 2), ("trials", C.c_int), ("chi2", C.c_double * 2)]
+
+
 _lib = None
 
 
@@ -55,6 +66,11 @@ def lib():
         L.oracle_search_by_bow_kf_f.argtypes = [C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P]
         L.oracle_search_by_bow_kf_kf.argtypes = [C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P]
         L.oracle_three_maxima.argtypes = [P, C.c_int, P, P, P]
+        L.oracle_local_ba.argtypes = [C.POINTER(BaProblem), C.POINTER(BaResult), P]
+        L.oracle_ba_edge_probe.argtypes = [P, P, P, P, C.c_int, P, P, P, P]
+        L.oracle_ba_edge_probe.restype = None
+        L.oracle_se3_exp_mul.argtypes = [P, P, P, P, P]
+        L.oracle_se3_exp_mul.restype = None
         _lib = L
     return _lib
 
@@ -190,3 +206,44 @@ def three_maxima(counts):
     out = [np.zeros(1, np.int32) for _ in range(3)]
     lib().oracle_three_maxima(_p(c), len(c), *[_p(o) for o in out])
     return tuple(int(o[0]) for o in out)
+
+
+BA_KEYS = ("Tcw", "fixed", "intr", "Xw", "edge_point", "edge_cam", "obs", "inv_sigma2")
+BA_DTYPES = dict(Tcw=np.float32, fixed=np.uint8, intr=np.float32, Xw=np.float32, edge_point=np.int32,
+                 edge_cam=np.int32, obs=np.float32, inv_sigma2=np.float32)
+
+
+def ba_arrays(prob):
+    return {k: np.ascontiguousarray(prob[k], BA_DTYPES[k]) for k in BA_KEYS}
+
+
+def ba_edge_probe(q, t, X, intr, stereo, obs):
+    """(err[3], A[3,3], B[3,6]) of one edge at an explicit state (rows beyond the edge dimension are 0)."""
+    d = lambda a, n: np.ascontiguousarray(np.asarray(a, np.float64).reshape(n))
+    q, t, X, intr, obs = d(q, 4), d(t, 3), d(X, 3), d(intr, 5), d(obs, 3)
+    err, A, B = np.zeros(3), np.zeros(9), np.zeros(18)
+    lib().oracle_ba_edge_probe(_p(q), _p(t), _p(X), _p(intr), int(stereo), _p(obs), _p(err), _p(A), _p(B))
+    return err, A.reshape(3, 3), B.reshape(3, 6)
+
+
+def se3_exp_mul(u, q, t):
+    """exp(u) * (q, t) -> (q', t'), q as (x, y, z, w)."""
+    d = lambda a, n: np.ascontiguousarray(np.asarray(a, np.float64).reshape(n))
+    u, q, t = d(u, 6), d(q, 4), d(t, 3)
+    qo, to = np.zeros(4), np.zeros(3)
+    lib().oracle_se3_exp_mul(_p(u), _p(q), _p(t), _p(qo), _p(to))
+    return qo, to
+
+
+def local_ba(prob, stop=False):
+    a = ba_arrays(prob)
+    nc, np_, ne = len(a["Tcw"]), len(a["Xw"]), len(a["edge_point"])
+    P = BaProblem(nc, _p(a["Tcw"]), _p(a["fixed"]), _p(a["intr"]), np_, _p(a["Xw"]), ne, _p(a["edge_point"]),
+                  _p(a["edge_cam"]), _p(a["obs"]), _p(a["inv_sigma2"]))
+    out = dict(Tcw=np.zeros((nc, 12), np.float32), Xw=np.zeros((np_, 3), np.float32),
+               edge_outlier=np.zeros(ne, np.uint8), Tcw_d=np.zeros((nc, 12)), Xw_d=np.zeros((np_, 3)))
+    R = BaResult(_p(out["Tcw"]), _p(out["Xw"]), _p(out["edge_outlier"]), _p(out["Tcw_d"]), _p(out["Xw_d"]))
+    flag = np.array([1 if stop else 0], np.int32)
+    lib().oracle_local_ba(C.byref(P), C.byref(R), _p(flag))
+    out.update(iterations=tuple(R.iterations), trials=R.trials, chi2=tuple(R.chi2))
+    return out

@@ -98,6 +98,47 @@ int oracle_search_by_bow_kf_kf(const oracle_bow_side* kf1, const oracle_bow_side
 /* ORBmatcher::ComputeThreeMaxima, src/ORBmatcher.cc:1797-1839 (on bin counts). */
 void oracle_three_maxima(const int* counts, int L, int* ind1, int* ind2, int* ind3);
 
+/* Optimizer::LocalBundleAdjustment (src/Optimizer.cc:530-885) on g2o semantics.
+ * Cameras: Tcw row-major 3x4 float (KeyFrame::GetPose), fixed flag (local KF
+ * with mnId==0 or fixed camera), intrinsics fx,fy,cx,cy,bf (float).  Points:
+ * world positions float.  Edges: point, camera, obs (u, v, ur; ur < 0 ->
+ * monocular EdgeSE3ProjectXYZ, else EdgeStereoSE3ProjectXYZ) and invSigma2 of
+ * the keypoint octave. */
+typedef struct {
+  int n_cams;
+  const float* Tcw;
+  const uint8_t* fixed;
+  const float* intr;
+  int n_points;
+  const float* Xw;
+  int n_edges;
+  const int32_t* edge_point;
+  const int32_t* edge_cam;
+  const float* obs;
+  const float* inv_sigma2;
+} oracle_ba_problem;
+
+typedef struct {
+  float* Tcw;             /* n_cams x 12 */
+  float* Xw;              /* n_points x 3 */
+  uint8_t* edge_outlier;  /* n_edges: (KF, MapPoint) pair to erase (:817-847) */
+  double* Tcw_d;          /* optional double copies (NULL to skip) */
+  double* Xw_d;
+  int iterations[2];      /* LM iterations of optimize(5) / optimize(10) */
+  int trials;             /* LM inner trials in total */
+  double chi2[2];         /* active robust chi2 at the end of each phase */
+} oracle_ba_result;
+
+int oracle_local_ba(const oracle_ba_problem* p, oracle_ba_result* r, const volatile int* stop_flag);
+
+/* Test probes: EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ computeError +
+ * linearizeOplus at (q xyzw, t, X); A = d err/d X (rows of 3), B = d err/d
+ * pose (rows of 6, pose update exp(u) * T, u = (omega, upsilon)). */
+void oracle_ba_edge_probe(const double q[4], const double t[3], const double X[3], const double intr[5], int stereo,
+                          const double obs[3], double err[3], double A[9], double B[18]);
+/* exp(u) * T (SE3Quat::exp, operator*, normalizeRotation). */
+void oracle_se3_exp_mul(const double u[6], const double q[4], const double t[3], double q_out[4], double t_out[3]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,17 @@ class BowProblem(C.Structure):
                 ("match", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
+class BaProblem(C.Structure):
+    _fields_ = [("n_cams", C.c_int), ("Tcw", C.c_void_p), ("fixed", C.c_void_p), ("intr", C.c_void_p),
+                ("n_points", C.c_int), ("Xw", C.c_void_p), ("n_edges", C.c_int), ("edge_point", C.c_void_p),
+                ("edge_cam", C.c_void_p), ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p)]
+
+
+class BaResult(C.Structure):
+    _fields_ = [("Tcw", C.c_void_p), ("Xw", C.c_void_p), ("edge_outlier", C.c_void_p), ("Tcw_d", C.c_void_p),
+                ("Xw_d", C.c_void_p), ("iterations", C.c_int * 2), ("trials", C.c_int), ("chi2", C.c_double * 2)]
+
+
 # Every entry point of include/orbx.h with its ctypes signature.
 P = C.c_void_p
 SIGNATURES = {
@@ -70,6 +81,10 @@ SIGNATURES = {
     "orbx_search_by_bow_kf_kf": ([C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P,
                                   C.POINTER(C.c_int), C.c_int], C.c_int),
     "orbx_search_by_bow_device": ([C.POINTER(BowProblem), C.c_int, P], C.c_int),
+    "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_ba_destroy": ([P], C.c_int),
+    "orbx_ba_run": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),
+    "orbx_local_ba": ([C.POINTER(BaProblem), C.POINTER(BaResult), P, C.c_int], C.c_int),
     "orbx_device_count": ([], C.c_int),
     "orbx_version": ([], C.c_char_p),
     "orbx_profile_enable": ([P, C.c_int], C.c_int),

@@ -10,6 +10,10 @@ Names, argument meaning and error behaviour follow the reference:
 * ``ORBmatcher.DescriptorDistance`` (src/ORBmatcher.cc:1844-1860), batched.
 * ``compute_stereo_matches`` == ``Frame::ComputeStereoMatches``
   (src/Frame.cc:547-788).
+* ``ORBmatcher.SearchByBoW`` (src/ORBmatcher.cc:175-325, 589-736).
+* ``Optimizer.LocalBundleAdjustment`` (src/Optimizer.cc:530-885) on an
+  explicit problem (cameras, points, observations) gathered like the
+  reference gathers it from the covisibility graph.
 
 Every result is computed by the HIP kernels; this module only moves bytes.
 """
@@ -216,3 +220,59 @@ class ORBmatcher:
               "orbx_descriptor_distance_device")
         d = out.cpu().numpy()
         return int(d[0]) if n == 1 else d
+
+
+def _ba_arrays(prob):
+    """Problem dict -> contiguous arrays in the orbx_ba_problem layout."""
+    nc = len(prob["Tcw"])
+    fixed = prob.get("fixed")
+    return dict(Tcw=np.ascontiguousarray(np.asarray(prob["Tcw"], np.float32).reshape(nc, 12)),
+                fixed=np.ascontiguousarray(np.zeros(nc, np.uint8) if fixed is None else fixed, np.uint8),
+                intr=np.ascontiguousarray(np.asarray(prob["intr"], np.float32).reshape(nc, 5)),
+                Xw=np.ascontiguousarray(np.asarray(prob["Xw"], np.float32).reshape(-1, 3)),
+                edge_point=np.ascontiguousarray(prob["edge_point"], np.int32),
+                edge_cam=np.ascontiguousarray(prob["edge_cam"], np.int32),
+                obs=np.ascontiguousarray(np.asarray(prob["obs"], np.float32).reshape(-1, 3)),
+                inv_sigma2=np.ascontiguousarray(prob["inv_sigma2"], np.float32))
+
+
+class Optimizer:
+    """Optimizer::LocalBundleAdjustment (include/Optimizer.h:46) on the GPU.
+
+    The solver handle keeps device buffers between calls (the local mapping
+    thread runs one LocalBA per new keyframe)."""
+
+    def __init__(self, device=0):
+        h = C.c_void_p()
+        check(_lib.lib().orbx_ba_create(int(device), C.byref(h)), "orbx_ba_create")
+        self._h = h
+        self.device = int(device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().orbx_ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def LocalBundleAdjustment(self, prob, stop=False):
+        """prob: dict(Tcw[n,12], fixed[n], intr[n,5] fx,fy,cx,cy,bf, Xw[m,3], edge_point, edge_cam,
+        obs[e,3] (u, v, ur; ur<0 mono), inv_sigma2[e]).  ``stop`` mirrors *pbStopFlag.
+
+        Returns dict(Tcw, Xw, edge_outlier, Tcw_d, Xw_d, iterations, trials, chi2)."""
+        a = _ba_arrays(prob)
+        nc, npt, ne = len(a["Tcw"]), len(a["Xw"]), len(a["edge_point"])
+        P = _lib.BaProblem(nc, ptr(a["Tcw"]), ptr(a["fixed"]), ptr(a["intr"]), npt, ptr(a["Xw"]), ne,
+                           ptr(a["edge_point"]), ptr(a["edge_cam"]), ptr(a["obs"]), ptr(a["inv_sigma2"]))
+        out = dict(Tcw=np.zeros((nc, 12), np.float32), Xw=np.zeros((npt, 3), np.float32),
+                   edge_outlier=np.zeros(ne, np.uint8), Tcw_d=np.zeros((nc, 12)), Xw_d=np.zeros((npt, 3)))
+        R = _lib.BaResult(ptr(out["Tcw"]), ptr(out["Xw"]), ptr(out["edge_outlier"]), ptr(out["Tcw_d"]),
+                          ptr(out["Xw_d"]))
+        flag = np.array([1 if stop else 0], np.int32)
+        check(_lib.lib().orbx_ba_run(self._h, C.byref(P), C.byref(R), ptr(flag)), "orbx_ba_run")
+        out.update(iterations=tuple(R.iterations), trials=R.trials, chi2=tuple(R.chi2))
+        return out

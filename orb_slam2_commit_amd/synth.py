@@ -131,3 +131,88 @@ def bow_problem(seed, n_a=1500, n_b=1500, n_nodes=100, n_true=700, noise_bits=12
                     node_id=ids[present], node_off=off, feat=order.astype(np.int32))
 
     return dict(a=side(da, ang_a, node_a), b=side(db, ang_b, node_b))
+
+
+def _rot_y(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def _rot_small(rng, sigma):
+    w = rng.normal(0, sigma, 3)
+    th = np.linalg.norm(w)
+    if th < 1e-12:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def localba_problem(seed=7, n_local=20, n_fixed=6, n_points=8000, obs_per_point=5, outlier_frac=0.05,
+                    fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, bf=386.1448, width=1241, height=376,
+                    th_depth=35.0, pose_noise=(0.01, 0.05), point_noise=0.1):
+    """KITTI-00-shaped LocalBundleAdjustment problem.
+
+    n_local keyframes along +z at 1 m spacing with +-2 deg yaw jitter, n_fixed
+    fixed keyframes behind them; n_points points observed by ~obs_per_point
+    keyframes each; stereo edge when depth < ThDepth*baseline, else monocular;
+    pixel noise sigma = 1.2^octave; outlier_frac of observations offset by 20 px;
+    initial poses perturbed by (0.01 rad, 0.05 m), points by 0.1 m."""
+    rng = np.random.default_rng(seed)
+    base = bf / fx
+    n_cams = n_local + n_fixed
+    Rwc, twc = [], []
+    for i in range(n_cams):
+        z = float(i) if i < n_local else -float(i - n_local + 1)
+        Rwc.append(_rot_y(np.deg2rad(rng.uniform(-2, 2))))
+        twc.append(np.array([rng.uniform(-0.2, 0.2), rng.uniform(-0.05, 0.05), z]))
+    Tcw_true = np.zeros((n_cams, 3, 4))
+    for i in range(n_cams):
+        R = Rwc[i].T
+        Tcw_true[i, :, :3] = R
+        Tcw_true[i, :, 3] = -R @ twc[i]
+    X = np.stack([rng.uniform(-15, 15, n_points), rng.uniform(-3, 2, n_points),
+                  rng.uniform(5, 80, n_points)], axis=1)
+    ep, ec, obs, isg = [], [], [], []
+    for p in range(n_points):
+        Pc = Tcw_true[:, :, :3] @ X[p] + Tcw_true[:, :, 3]
+        z = Pc[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = fx * Pc[:, 0] / z + cx
+            v = fy * Pc[:, 1] / z + cy
+        vis = np.where((z > 0.5) & (u > 20) & (u < width - 20) & (v > 20) & (v < height - 20))[0]
+        vis_local = vis[vis < n_local]
+        if len(vis_local) == 0:
+            continue
+        k = min(len(vis), int(rng.integers(obs_per_point - 1, obs_per_point + 2)))
+        chosen = set(rng.choice(vis, k, replace=False).tolist())
+        chosen.add(int(rng.choice(vis_local)))
+        for c in sorted(chosen):
+            octave = int(rng.integers(0, 8))
+            sigma = 1.2 ** octave
+            uu = u[c] + rng.normal(0, sigma)
+            vv = v[c] + rng.normal(0, sigma)
+            ur = -1.0
+            if z[c] < th_depth * base:
+                ur = uu - bf / z[c] + rng.normal(0, sigma * 0.5)
+            if rng.uniform() < outlier_frac:
+                uu += 20.0
+                if ur >= 0:
+                    ur += 20.0
+            ep.append(p)
+            ec.append(c)
+            obs.append((uu, vv, ur if ur >= 0 else -1.0))
+            isg.append(1.0 / (sigma * sigma))
+    Tcw = Tcw_true.copy()
+    for i in range(n_local):
+        dR = _rot_small(rng, pose_noise[0])
+        Tcw[i, :, :3] = dR @ Tcw[i, :, :3]
+        Tcw[i, :, 3] = dR @ Tcw[i, :, 3] + rng.normal(0, pose_noise[1], 3)
+    Xn = X + rng.normal(0, point_noise, X.shape)
+    intr = np.tile(np.array([fx, fy, cx, cy, bf], np.float32), (n_cams, 1))
+    fixed = np.zeros(n_cams, np.uint8)
+    fixed[n_local:] = 1
+    return dict(Tcw=Tcw.reshape(n_cams, 12).astype(np.float32), fixed=fixed, intr=intr,
+                Xw=Xn.astype(np.float32), edge_point=np.array(ep, np.int32), edge_cam=np.array(ec, np.int32),
+                obs=np.array(obs, np.float32), inv_sigma2=np.array(isg, np.float32),
+                Tcw_true=Tcw_true.reshape(n_cams, 12), Xw_true=X)
