@@ -23,6 +23,11 @@ enum {
 /* Returns the number of bytes the item occupies (copies min(cap, size)); <0 on error. */
 long long orbx_debug_copy(orbx_extractor* h, int what, int image, int arg, void* dst, size_t cap);
 
+/* Solve S x = b (N x N, N a multiple of 6) with the LocalBA reduced-system
+ * LDLT kernel; *ms = mean kernel time over reps launches.  ORBX_ERR_STATE on
+ * a zero pivot. */
+int orbx_debug_ldlt(const double* S, const double* b, int N, double* x, int reps, float* ms);
+
 #ifdef __cplusplus
 }
 #endif

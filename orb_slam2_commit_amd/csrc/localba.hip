@@ -20,6 +20,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -149,6 +152,8 @@ __device__ inline void inv3(const double m[9], double out[9]) {
 }
 
 // ------------------------------------------------------------ device state
+constexpr int LBS = 256;
+
 struct BaDev {
   int nc, np, ne;
   // cameras
@@ -190,26 +195,65 @@ struct BaDev {
   double* cmc;     // na*42: Hpp 36 + bp 6
   double* BD;      // na*18
   double* cf;      // na*6
-  double* chi;     // na (robust chi of the edge)
   // per active point
   double* Hll;     // npa*9
   double* bl;      // npa*3
   double* Dinv;    // npa*9
-  double* xl;      // npa*3
   double* dmax_p;  // npa
-  double* scale_p; // npa
   // per pose
   double* Hpp;     // nposes*36
   double* bp;      // nposes*6
   double* xp;      // nposes*6
   double* bs;      // nposes*6
   double* S;       // (6*nposes)^2
+  double* Sw;      // padded LDLT work matrix when it does not fit LDS
+  unsigned long long* dbg;  // optional phase timestamps (debug probe only)
   double* dmax_c;  // nposes
-  double* scale_c; // nposes
-  double* scal;    // scalars: [0] chi, [1] scale, [2] ok, [3] dmax
+  int* pos_pt;     // na: active point index of position k
+  double* part;    // grid-reduction block partials
+  unsigned* cnt;   // grid-reduction arrival counter (reset by the last block)
+  double* scal;    // scalars: [0] chi at iteration start, [1] chi after the trial, [2] solve ok, [3] max diag, [4] LM scale
 };
 
-constexpr int LBS = 256;
+// Fixed-order block sum of one double per thread (blockDim LBS); every thread gets the result.
+__device__ inline double block_sum1(double v, double* red /* LDS [LBS/64] */) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0;
+#pragma unroll
+  for (int w = 0; w < LBS / 64; w++) s += red[w];
+  __syncthreads();
+  return s;
+}
+
+// Grid-wide sum in a fixed order (block partials, then the last block to
+// arrive adds them in block order): run-to-run deterministic, one launch.
+// Must be reached by every thread of every block.
+__device__ inline void grid_sum(double v, double* part, unsigned* cnt, double* out) {
+  __shared__ double red[LBS / 64];
+  __shared__ int last;
+  const double bs = block_sum1(v, red);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(part) + blockIdx.x, __double_as_longlong(bs),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  double s = 0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += LBS)
+    s += __longlong_as_double(__hip_atomic_load(reinterpret_cast<unsigned long long*>(part) + b, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+  s = block_sum1(s, red);
+  if (threadIdx.x == 0) {
+    *out = s;
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 
 __device__ inline void edge_error(const BaDev& D, int e, double err[3], double& chi2) {
   const int c = D.ecam[e], p = D.ept[e];
@@ -251,29 +295,31 @@ __device__ inline void huber(double chi, double delta, float dsqr, double rho[3]
   }
 }
 
-__global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute) {
+__global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute, int dst) {
   const int k = blockIdx.x * LBS + threadIdx.x;
-  if (k >= D.na) return;
-  const int e = D.act[k];
-  double c2;
-  if (recompute) {
-    double err[3];
-    edge_error(D, e, err, c2);
-    D.eerr[3 * e] = err[0];
-    D.eerr[3 * e + 1] = err[1];
-    D.eerr[3 * e + 2] = err[2];
-  } else {
-    const double info = D.einfo[e];
-    c2 = 0;
-    for (int i = 0; i < (D.est[e] ? 3 : 2); i++) c2 += D.eerr[3 * e + i] * (info * D.eerr[3 * e + i]);
+  double chi = 0;
+  if (k < D.na) {
+    const int e = D.act[k];
+    double c2;
+    if (recompute) {
+      double err[3];
+      edge_error(D, e, err, c2);
+      D.eerr[3 * e] = err[0];
+      D.eerr[3 * e + 1] = err[1];
+      D.eerr[3 * e + 2] = err[2];
+    } else {
+      const double info = D.einfo[e];
+      c2 = 0;
+      for (int i = 0; i < (D.est[e] ? 3 : 2); i++) c2 += D.eerr[3 * e + i] * (info * D.eerr[3 * e + i]);
+    }
+    chi = c2;
+    if (D.erobust[e]) {
+      double rho[3];
+      huber(c2, D.edelta[e], D.edsqr[e], rho);
+      chi = rho[0];
+    }
   }
-  double chi = c2;
-  if (D.erobust[e]) {
-    double rho[3];
-    huber(c2, D.edelta[e], D.edsqr[e], rho);
-    chi = rho[0];
-  }
-  D.chi[k] = chi;
+  grid_sum(chi, D.part, D.cnt, D.scal + dst);
 }
 
 // Deterministic sum / max of n doubles into *out (one block).
@@ -417,27 +463,74 @@ __global__ __launch_bounds__(LBS) void k_ba_point_sum(BaDev D) {
   D.dmax_p[i] = fmax(fmax(fabs(h[0]), fabs(h[4])), fabs(h[8]));
 }
 
-// one block per pose; thread j < 42 sums component j over the pose's edges in order
-__global__ __launch_bounds__(64) void k_ba_cam_sum(BaDev D) {
-  const int ci = blockIdx.x, j = threadIdx.x;
-  __shared__ double dg[6];
-  if (j < 42) {
-    double s = 0;
-    for (int t = D.cam_off[ci]; t < D.cam_off[ci + 1]; t++) s += D.cmc[42 * (size_t)D.cam_pos[t] + j];
-    if (j < 36) D.Hpp[36 * ci + j] = s; else D.bp[6 * ci + (j - 36)] = s;
-    if (j < 36 && (j % 7) == 0) dg[j / 7] = fabs(s);
+// Fixed-order block sum of NV per-thread partials (shuffle tree, then the
+// waves' results in wave order): deterministic for a fixed launch shape.
+template <int NV>
+__device__ inline void block_sum_fixed(double (&v)[NV], double* red /* LDS [4*NV] */) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    double x = v[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    v[j] = x;
   }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < NV; j++) red[wv * NV + j] = v[j];
   __syncthreads();
-  if (j == 0) {
+}
+
+// Hpp, bp per pose: one 256-thread block per pose, thread t takes the pose's
+// edges t, t+256, ... ; only the upper triangle (21) + b (6) are summed.
+__global__ __launch_bounds__(256) void k_ba_cam_sum(BaDev D) {
+  __shared__ double red[4 * 27];
+  const int ci = blockIdx.x;
+  double v[27];
+#pragma unroll
+  for (int j = 0; j < 27; j++) v[j] = 0;
+  for (int t = D.cam_off[ci] + threadIdx.x; t < D.cam_off[ci + 1]; t += 256) {
+    const double* cm = D.cmc + 42 * (size_t)D.cam_pos[t];
+    int j = 0;
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+      for (int c = r; c < 6; c++) v[j++] += cm[6 * r + c];
+#pragma unroll
+    for (int r = 0; r < 6; r++) v[21 + r] += cm[36 + r];
+  }
+  block_sum_fixed<27>(v, red);
+  const int j = threadIdx.x;
+  if (j < 36) {
+    int r = j / 6, c = j % 6;
+    if (c < r) {
+      const int t = r;
+      r = c;
+      c = t;
+    }
+    const int u = r * 6 - (r * (r - 1)) / 2 + (c - r);  // upper-triangle index
+    const double s = ((red[u] + red[27 + u]) + red[54 + u]) + red[81 + u];
+    D.Hpp[36 * ci + j] = s;
+  } else if (j < 42) {
+    const int u = 21 + (j - 36);
+    D.bp[6 * ci + (j - 36)] = ((red[u] + red[27 + u]) + red[54 + u]) + red[81 + u];
+  } else if (j == 42) {
     double m = 0;
-    for (int r = 0; r < 6; r++) m = fmax(m, dg[r]);
+    for (int r = 0; r < 6; r++) {
+      const int u = r * 6 - (r * (r - 1)) / 2;
+      m = fmax(m, fabs(((red[u] + red[27 + u]) + red[54 + u]) + red[81 + u]));
+    }
     D.dmax_c[ci] = m;
   }
 }
 
+// One thread per active edge position: D = Hll + lambda I of its point,
+// Dinv (stored once per point), BD_e = Hpl_e Dinv, cf_e = Hpl_e Dinv bl.
 __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) {
-  const int i = blockIdx.x * LBS + threadIdx.x;
-  if (i >= D.npa) return;
+  const int k = blockIdx.x * LBS + threadIdx.x;
+  if (k == 0 && D.nposes == 0) D.scal[2] = 1.0;  // no reduced system to factor
+  if (k >= D.na) return;
+  const int i = D.pos_pt[k];
   double Dm[9];
   for (int j = 0; j < 9; j++) Dm[j] = D.Hll[9 * i + j];
   Dm[0] += lambda;
@@ -445,127 +538,306 @@ __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) 
   Dm[8] += lambda;
   double Di[9];
   inv3(Dm, Di);
-  for (int j = 0; j < 9; j++) D.Dinv[9 * i + j] = Di[j];
+  if (k == D.pt_off[i])
+    for (int j = 0; j < 9; j++) D.Dinv[9 * i + j] = Di[j];
+  if (D.chidx[D.ecam[D.act[k]]] < 0) return;
   const double b0 = D.bl[3 * i], b1 = D.bl[3 * i + 1], b2 = D.bl[3 * i + 2];
   double db[3];
   for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
-  for (int k = D.pt_off[i]; k < D.pt_off[i + 1]; k++) {
-    if (D.chidx[D.ecam[D.act[k]]] < 0) continue;
-    const double* B1 = D.Hpl + 18 * (size_t)k;
-    double* bd = D.BD + 18 * (size_t)k;
-    for (int r = 0; r < 6; r++) {
-      for (int c = 0; c < 3; c++) bd[3 * r + c] = B1[3 * r] * Di[c] + B1[3 * r + 1] * Di[3 + c] + B1[3 * r + 2] * Di[6 + c];
-      D.cf[6 * (size_t)k + r] = B1[3 * r] * db[0] + B1[3 * r + 1] * db[1] + B1[3 * r + 2] * db[2];
-    }
+  const double* B1 = D.Hpl + 18 * (size_t)k;
+  double* bd = D.BD + 18 * (size_t)k;
+  for (int r = 0; r < 6; r++) {
+    for (int c = 0; c < 3; c++) bd[3 * r + c] = B1[3 * r] * Di[c] + B1[3 * r + 1] * Di[3 + c] + B1[3 * r + 2] * Di[6 + c];
+    D.cf[6 * (size_t)k + r] = B1[3 * r] * db[0] + B1[3 * r + 1] * db[1] + B1[3 * r + 2] * db[2];
   }
 }
 
-// One wave per Hschur block (c1 <= c2): lanes take pairs lane, lane+64, ...;
-// every lane accumulates the 6x6 block, then a fixed shuffle tree sums lanes.
-__global__ __launch_bounds__(64) void k_ba_pairs(BaDev D, double lambda) {
-  const int b = blockIdx.x, lane = threadIdx.x;
+// One 256-thread block per Hschur block (c1 <= c2): threads take pairs t,
+// t+256, ...; each accumulates the 6x6 block, then a fixed-order block sum.
+__global__ __launch_bounds__(256) void k_ba_pairs(BaDev D, double lambda) {
+  __shared__ double red[4 * 36];
+  const int b = blockIdx.x;
   double acc[36];
+#pragma unroll
   for (int j = 0; j < 36; j++) acc[j] = 0;
-  for (int t = D.blk_off[b] + lane; t < D.blk_off[b + 1]; t += 64) {
+  for (int t = D.blk_off[b] + threadIdx.x; t < D.blk_off[b + 1]; t += 256) {
     const int2 pr = D.pairs[t];
     const double* bd = D.BD + 18 * (size_t)pr.x;
     const double* h2 = D.Hpl + 18 * (size_t)pr.y;
     double A[18], Bv[18];
+#pragma unroll
     for (int j = 0; j < 18; j++) {
       A[j] = bd[j];
       Bv[j] = h2[j];
     }
+#pragma unroll
     for (int r = 0; r < 6; r++)
+#pragma unroll
       for (int c = 0; c < 6; c++) acc[6 * r + c] += A[3 * r] * Bv[3 * c] + A[3 * r + 1] * Bv[3 * c + 1] + A[3 * r + 2] * Bv[3 * c + 2];
   }
-  for (int j = 0; j < 36; j++) {
-    double v = acc[j];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    acc[j] = v;
-  }
-  if (lane < 36) {
+  block_sum_fixed<36>(acc, red);
+  const int j = threadIdx.x;
+  if (j < 36) {
+    const double v = ((red[j] + red[36 + j]) + red[72 + j]) + red[108 + j];
     const int2 cc = D.blk_cc[b];
     const int N = 6 * D.nposes;
-    const int r = lane / 6, c = lane % 6;
-    double v = 0;
-#pragma unroll
-    for (int j = 0; j < 36; j++)
-      if (j == lane) v = acc[j];
-    double s;
+    const int r = j / 6, c = j % 6;
+    double sv;
     if (cc.x == cc.y) {
-      s = D.Hpp[36 * cc.x + lane] + (r == c ? lambda : 0.0) - v;
+      sv = D.Hpp[36 * cc.x + j] + (r == c ? lambda : 0.0) - v;
     } else {
-      s = -v;
-      D.S[(size_t)(6 * cc.y + c) * N + 6 * cc.x + r] = s;
+      sv = -v;
+      D.S[(size_t)(6 * cc.y + c) * N + 6 * cc.x + r] = sv;
     }
-    D.S[(size_t)(6 * cc.x + r) * N + 6 * cc.y + c] = s;
+    D.S[(size_t)(6 * cc.x + r) * N + 6 * cc.y + c] = sv;
   }
 }
 
-__global__ __launch_bounds__(64) void k_ba_cam_coef(BaDev D) {
-  const int ci = blockIdx.x, j = threadIdx.x;
-  if (j >= 6) return;
-  double s = 0;
-  for (int t = D.cam_off[ci]; t < D.cam_off[ci + 1]; t++) s += D.cf[6 * (size_t)D.cam_pos[t] + j];
-  D.bs[6 * ci + j] = D.bp[6 * ci + j] - s;
+__global__ __launch_bounds__(256) void k_ba_cam_coef(BaDev D) {
+  __shared__ double red[4 * 6];
+  const int ci = blockIdx.x;
+  double v[6] = {0, 0, 0, 0, 0, 0};
+  for (int t = D.cam_off[ci] + threadIdx.x; t < D.cam_off[ci + 1]; t += 256) {
+    const double* f = D.cf + 6 * (size_t)D.cam_pos[t];
+#pragma unroll
+    for (int r = 0; r < 6; r++) v[r] += f[r];
+  }
+  block_sum_fixed<6>(v, red);
+  const int j = threadIdx.x;
+  if (j < 6) D.bs[6 * ci + j] = D.bp[6 * ci + j] - (((red[j] + red[6 + j]) + red[12 + j]) + red[18 + j]);
+}
+
+__device__ inline double readlane_d(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, l);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kLdltMaxNp = 512;                 // padded size limit (y: 8 registers per lane)
+constexpr int kLdltLdsNp = 128;                 // largest padded size kept in LDS
+inline int ldlt_np(int N) { return (N + 15) & ~15; }
+inline size_t ldlt_smem_bytes(int N, bool lds) {
+  const size_t Np = ldlt_np(N);
+  return ((lds ? Np * (Np + 1) : 0) + Np * 17) * sizeof(double);
 }
 
 // Dense LDLT (no pivoting; fails on an exactly zero pivot like Eigen's
-// SimplicialLDLT) of the N x N reduced camera system, right-looking: per
-// column j, scale the column by 1/d_j then a rank-1 update of the trailing
-// lower triangle, all threads; then column-oriented triangular solves.
-// A lives in LDS when it fits, else in place in global memory.
-__global__ __launch_bounds__(1024) void k_ba_ldlt(BaDev D, int in_lds) {
+// SimplicialLDLT) of the N x N reduced camera system and the solve, blocked
+// by 16-column panels.  The matrix is padded to Np = 16k with an identity
+// block (decoupled, never a zero pivot).  Per panel:
+//   1. wave 0 factors the 16 x 16 diagonal block in registers (lane r = row
+//      r, column values broadcast with readlane);
+//   2. each row below it solves its 16 panel entries against L11 (one
+//      thread per row) and stores W = L D (in A) and L (in P);
+//   3. the trailing lower triangle is updated A22 -= W21 L21^T with FP64
+//      MFMA 16x16x4 tiles spread over the 16 waves.
+// Then L = W / D in place, and the two triangular solves run on wave 0 with
+// the vector in registers.  kLds: A in LDS (row stride Np+1), else in the
+// global scratch D.Sw (row stride Np).  A template parameter, not a runtime
+// select, so that LDS accesses are ds_* and not FLAT instructions.
+// L z = b, z /= D, L^T x = z on one wave; lane owns rows lane + 64 q held in
+// registers, broadcasts via readlane.  Loads are unconditional (clamped
+// rows) and the next column's values are fetched one step ahead.
+template <int NQ>
+__device__ inline void ldlt_solve_wave(const double* A, int ld, int N, int Np, const double* b, double* x) {
+  const int lane = threadIdx.x & 63;
+  double y[NQ];
+  int row[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    const int i = lane + 64 * q;
+    row[q] = i < Np ? i : Np - 1;
+    y[q] = i < N ? b[i] : 0.0;
+  }
+  double a[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; q++) a[q] = A[(size_t)row[q] * ld];
+  for (int k = 0; k < Np; k++) {
+    double an[NQ];
+    const int kn = k + 1 < Np ? k + 1 : k;
+#pragma unroll
+    for (int q = 0; q < NQ; q++) an[q] = A[(size_t)row[q] * ld + kn];
+    double yk = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+      if (q == (k >> 6)) yk = readlane_d(y[q], k & 63);
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const int i = lane + 64 * q;
+      const double t = y[q] - a[q] * yk;
+      y[q] = i > k ? t : y[q];
+      a[q] = an[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; q++) y[q] /= A[(size_t)row[q] * ld + row[q]];
+  // backward: row i of L (contiguous) against lanes k < i
+#pragma unroll
+  for (int q = 0; q < NQ; q++) a[q] = A[(size_t)(Np - 1) * ld + (lane + 64 * q < Np ? lane + 64 * q : 0)];
+  for (int i = Np - 1; i >= 0; i--) {
+    double an[NQ];
+    const int in = i > 0 ? i - 1 : 0;
+#pragma unroll
+    for (int q = 0; q < NQ; q++) an[q] = A[(size_t)in * ld + (lane + 64 * q < Np ? lane + 64 * q : 0)];
+    double xi = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+      if (q == (i >> 6)) xi = readlane_d(y[q], i & 63);
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const int k = lane + 64 * q;
+      const double t = y[q] - a[q] * xi;
+      y[q] = k < i ? t : y[q];
+      a[q] = an[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    const int i = lane + 64 * q;
+    if (i < N) x[i] = y[q];
+  }
+}
+
+#define LDLT_TS(idx)                                                  \
+  do {                                                                \
+    if (D.dbg && tid == 0 && (idx) < 64) D.dbg[idx] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+template <bool kLds>
+__global__ __launch_bounds__(1024) void k_ba_ldlt(BaDev D, int stage_limit) {
   extern __shared__ double sm[];
-  const int N = 6 * D.nposes, tid = threadIdx.x, nt = blockDim.x;
-  double* y = sm;
-  double* w = sm + N;
-  double* A = in_lds ? sm + 2 * N : D.S;
-  if (in_lds)
-    for (int i = tid; i < N * N; i += nt) A[i] = D.S[i];
-  for (int i = tid; i < N; i += nt) y[i] = D.bs[i];
+  __shared__ int fail;
+  __shared__ double Dinv_p[16];
+  const int N = 6 * D.nposes, Np = (N + 15) & ~15, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ld = kLds ? Np + 1 : Np;
+  double* A = kLds ? sm : D.Sw;
+  double* P = sm + (kLds ? (size_t)Np * ld : 0);  // Np x 16 (stride 17): L of the current panel
+  for (int i0 = 0; i0 < Np * Np; i0 += 4 * 1024) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int idx = i0 + u * 1024 + tid, r = idx / Np, c = idx - r * Np;
+      v[u] = (r < N && c < N) ? D.S[(size_t)r * N + c] : (r == c ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int idx = i0 + u * 1024 + tid, r = idx / Np, c = idx - r * Np;
+      if (idx < Np * Np) A[(size_t)r * ld + c] = v[u];
+    }
+  }
+  if (tid == 0) fail = 0;
   __syncthreads();
-  for (int j = 0; j < N; j++) {
-    const double d = A[(size_t)j * N + j];
-    if (d == 0.0) {  // uniform: every thread reads the same value
+  LDLT_TS(0);
+  if (stage_limit == 1) return;
+  for (int j0 = 0; j0 < Np; j0 += 16) {
+    if (wv == 0) {
+      const int r = lane & 15;
+      double row[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) row[c] = A[(size_t)(j0 + r) * ld + j0 + c];
+      bool bad = false;  // no early exit: the loops must unroll fully (constant register indices)
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const double d = readlane_d(row[c], c);
+        bad |= d == 0.0;
+        const double invd = 1.0 / d;
+#pragma unroll
+        for (int k = c + 1; k < 16; k++) {
+          const double lk = readlane_d(row[c], k) * invd;  // L[k][c]
+          if (r >= k) row[k] -= row[c] * lk;
+        }
+      }
+      if (bad) {
+        if (lane == 0) fail = 1;
+      } else if (lane < 16) {
+        const double dr = row[r < 16 ? r : 0];
+        double dd[16];
+#pragma unroll
+        for (int c = 0; c < 16; c++) dd[c] = readlane_d(row[c], c);
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+          if (c <= r) A[(size_t)(j0 + r) * ld + j0 + c] = row[c];
+          if (c < r) P[(j0 + r) * 17 + c] = row[c] / dd[c];
+        }
+        Dinv_p[r] = 1.0 / dr;
+      }
+    }
+    __syncthreads();
+    LDLT_TS(1 + 3 * (j0 >> 4));
+    if (fail) {
       if (tid == 0) D.scal[2] = 0.0;
       return;
     }
-    for (int i = j + 1 + tid; i < N; i += nt) {
-      const double a = A[(size_t)i * N + j];
-      w[i] = a;
-      A[(size_t)i * N + j] = a / d;
+    const int nrows = Np - j0 - 16;
+    for (int t = tid; t < nrows; t += 1024) {
+      const int i = j0 + 16 + t;
+      double w[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) w[c] = A[(size_t)i * ld + j0 + c];
+#pragma unroll
+      for (int c = 1; c < 16; c++)
+#pragma unroll
+        for (int m = 0; m < c; m++) w[c] -= w[m] * P[(j0 + c) * 17 + m];
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        A[(size_t)i * ld + j0 + c] = w[c];
+        P[i * 17 + c] = w[c] * Dinv_p[c];
+      }
     }
     __syncthreads();
-    const int M = N - j - 1;
-    for (int t = tid; t < M * M; t += nt) {
-      const int i = j + 1 + t / M, k = j + 1 + t % M;
-      if (k <= i) A[(size_t)i * N + k] -= A[(size_t)i * N + j] * w[k];
+    LDLT_TS(2 + 3 * (j0 >> 4));
+    const int m = nrows >> 4, T = m * (m + 1) / 2;
+    for (int t = wv; t < T; t += 16) {
+      int ti = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
+      while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+      while (ti * (ti + 1) / 2 > t) ti--;
+      const int tk = t - ti * (ti + 1) / 2;
+      const int R0 = j0 + 16 + 16 * ti, C0 = j0 + 16 + 16 * tk;
+      double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++) {
+        const double av = A[(size_t)(R0 + (lane & 15)) * ld + j0 + 4 * kk + (lane >> 4)];  // W[row][k]
+        const double bv = P[(C0 + (lane & 15)) * 17 + 4 * kk + (lane >> 4)];              // L[col][k]
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) {
+        const size_t o = (size_t)(R0 + (lane >> 4) + 4 * rr) * ld + C0 + (lane & 15);
+        A[o] -= acc[rr];
+      }
     }
     __syncthreads();
+    LDLT_TS(3 + 3 * (j0 >> 4));
   }
-  // L z = b
-  for (int i = 0; i < N; i++) {
-    const double yi = y[i];
-    for (int k = i + 1 + tid; k < N; k += nt) y[k] -= A[(size_t)k * N + i] * yi;
-    __syncthreads();
-  }
-  for (int i = tid; i < N; i += nt) y[i] /= A[(size_t)i * N + i];
+  if (stage_limit == 2) return;
+  for (int i = 1 + (tid >> 5); i < Np; i += 32)
+    for (int k = tid & 31; k < i; k += 32) A[(size_t)i * ld + k] /= A[(size_t)k * ld + k];
   __syncthreads();
-  // L^T x = z
-  for (int i = N - 1; i >= 0; i--) {
-    const double xi = y[i];
-    for (int k = tid; k < i; k += nt) y[k] -= A[(size_t)i * N + k] * xi;
-    __syncthreads();
+  LDLT_TS(60);
+  if (wv != 0 || stage_limit == 3) return;
+  switch ((Np + 63) >> 6) {
+    case 1: ldlt_solve_wave<1>(A, ld, N, Np, D.bs, D.xp); break;
+    case 2: ldlt_solve_wave<2>(A, ld, N, Np, D.bs, D.xp); break;
+    case 3: ldlt_solve_wave<3>(A, ld, N, Np, D.bs, D.xp); break;
+    case 4: ldlt_solve_wave<4>(A, ld, N, Np, D.bs, D.xp); break;
+    case 5: ldlt_solve_wave<5>(A, ld, N, Np, D.bs, D.xp); break;
+    case 6: ldlt_solve_wave<6>(A, ld, N, Np, D.bs, D.xp); break;
+    case 7: ldlt_solve_wave<7>(A, ld, N, Np, D.bs, D.xp); break;
+    default: ldlt_solve_wave<8>(A, ld, N, Np, D.bs, D.xp); break;
   }
-  for (int i = tid; i < N; i += nt) D.xp[i] = y[i];
-  if (tid == 0) D.scal[2] = 1.0;
+  if (lane == 0) D.scal[2] = 1.0;
+  LDLT_TS(61);
 }
 
-// back-substitution + update (push first) + LM scale terms
+// back-substitution + update (push first) + LM scale, skipped when the
+// solve failed (scal[2] == 0).  Threads: active points, then active poses.
 __global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
   const int i = blockIdx.x * LBS + threadIdx.x;
-  if (i < D.npa) {
+  const bool ok = D.scal[2] != 0.0;
+  double sc = 0;
+  if (ok && i < D.npa) {
     double c[3] = {D.bl[3 * i], D.bl[3 * i + 1], D.bl[3 * i + 2]};
     for (int k = D.pt_off[i]; k < D.pt_off[i + 1]; k++) {
       const int ci = D.chidx[D.ecam[D.act[k]]];
@@ -578,24 +850,19 @@ __global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
     double x[3];
     for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
     const int p = D.pt_id[i];
-    double sc = 0;
     for (int r = 0; r < 3; r++) {
       D.Xbak[3 * p + r] = D.X[3 * p + r];
       D.X[3 * p + r] += x[r];
-      D.xl[3 * i + r] = x[r];
       sc += x[r] * (lambda * x[r] + D.bl[3 * i + r]);
     }
-    D.scale_p[i] = sc;
-  } else if (i < D.npa + D.nposes) {
+  } else if (ok && i < D.npa + D.nposes) {
     const int pi = i - D.npa;
     const int c = D.pose_cam[pi];
     double u[6];
-    double sc = 0;
     for (int r = 0; r < 6; r++) {
       u[r] = D.xp[6 * pi + r];
       sc += u[r] * (lambda * u[r] + D.bp[6 * pi + r]);
     }
-    D.scale_c[pi] = sc;
     for (int r = 0; r < 4; r++) D.cbak[7 * c + r] = D.cq[4 * c + r];
     for (int r = 0; r < 3; r++) D.cbak[7 * c + 4 + r] = D.ct[3 * c + r];
     const SE3d E = se3_exp(u);
@@ -611,6 +878,7 @@ __global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
     D.cq[4 * c + 3] = nq.w;
     for (int r = 0; r < 3; r++) D.ct[3 * c + r] = E.t[r] + rt[r];
   }
+  grid_sum(sc, D.part, D.cnt, D.scal + 4);
 }
 
 __global__ __launch_bounds__(LBS) void k_ba_restore(BaDev D) {
@@ -694,12 +962,10 @@ struct DBuf {
 };
 
 struct Ctx {
-  DBuf<double> cq, ct, cbak, intr, X, Xbak, eobs, einfo, edelta, eerr, Hpl, ptc, cmc, BD, cf, chi, Hll, bl, Dinv, xl,
-      dmax_p, scale_p, Hpp, bp, xp, bs, S, scal;
-  DBuf<int> chidx, ept, ecam, act, pt_off, pt_id, cam_pos, cam_off, pose_cam, blk_off;
-  DBuf<int2> blk_cc, pairs;
-  DBuf<uint8_t> est, erobust, flag;
-  DBuf<float> edsqr, Tcw_out, Xw_out;
+  DBuf<double> cbak, Xbak, eerr, Hpl, ptc, cmc, BD, cf, Hll, bl, Dinv, dmax_p, Hpp, bp, xp, bs, S, Sw, scal, part;
+  DBuf<unsigned> cnt;
+  DBuf<uint8_t> flag;
+  DBuf<float> Tcw_out, Xw_out;
   DBuf<double> Tcw_d_out, Xw_d_out;
 };
 
@@ -708,98 +974,185 @@ struct Ctx {
     if ((x) != hipSuccess) return ORBX_ERR_HIP; \
   } while (0)
 
+// Pinned host staging buffer + one device arena: arrays are laid out with
+// take(), filled through host(), and sent with one async copy.
+struct Arena {
+  uint8_t* hbuf = nullptr;
+  uint8_t* dbuf = nullptr;
+  size_t cap = 0, off = 0;
+  ~Arena() {
+    if (hbuf) (void)hipHostFree(hbuf);
+    if (dbuf) (void)hipFree(dbuf);
+  }
+  hipError_t reserve(size_t bytes) {
+    off = 0;
+    if (bytes <= cap && hbuf) return hipSuccess;
+    if (hbuf) (void)hipHostFree(hbuf);
+    if (dbuf) (void)hipFree(dbuf);
+    hbuf = dbuf = nullptr;
+    cap = bytes + bytes / 4 + 4096;
+    hipError_t e = hipHostMalloc((void**)&hbuf, cap, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void**)&dbuf, cap);
+    if (e != hipSuccess) cap = 0;
+    return e;
+  }
+  template <class T>
+  T* take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T* d = reinterpret_cast<T*>(dbuf + off);
+    off += std::max<size_t>(n, 1) * sizeof(T);
+    return d;
+  }
+  template <class T>
+  T* host(T* d) {
+    return reinterpret_cast<T*>(hbuf + (reinterpret_cast<uint8_t*>(d) - dbuf));
+  }
+  template <class T>
+  T* put(const std::vector<T>& v) {
+    T* d = take<T>(v.size());
+    if (!v.empty()) std::memcpy(host(d), v.data(), v.size() * sizeof(T));
+    return d;
+  }
+  hipError_t upload(hipStream_t st) { return off ? hipMemcpyAsync(dbuf, hbuf, off, hipMemcpyHostToDevice, st) : hipSuccess; }
+};
+
+inline size_t arena_bytes(std::initializer_list<size_t> sizes) {
+  size_t t = 0;
+  for (size_t x : sizes) t += ((std::max<size_t>(x, 1) + 255) & ~(size_t)255);
+  return t + 256;
+}
+
 struct LocalBA {
   BaDev D{};
   Ctx c;  // device buffers, kept across calls (grow only)
+  Arena prob_arena, struct_arena;
   std::vector<int> e_pt, e_cam;
   std::vector<uint8_t> e_st, fixed;
   std::vector<uint8_t> level;  // 0/1 per edge
   int trials = 0;
+  // host scratch, reused across calls
+  std::vector<int> act, pos_pt, chidx, pose_cam, pt_off, pt_id, cam_off, cam_pos, blk_off, cnt, pcam, blk_map;
+  std::vector<int2> blk_cc, pairs;
 
   // Active set of a phase: SparseOptimizer::initializeOptimization(level) +
-  // buildIndexMapping; point-major positions, pose groups, Schur pair blocks.
-  orbx_status build_structure(int lvl) {
+  // buildIndexMapping; point-major positions (stable counting sort), pose
+  // groups, Schur pair blocks (c1 <= c2; pairs ordered by point).
+  orbx_status build_structure(int lvl, hipStream_t st) {
     const int nc = D.nc, np = D.np, ne = D.ne;
-    std::vector<int> act;
-    std::vector<char> cam_used(nc, 0), pt_used(np, 0);
-    std::vector<std::vector<int>> by_pt(np);
-    for (int e = 0; e < ne; e++) {
-      if (lvl >= 0 && level[e] != lvl) continue;
-      by_pt[e_pt[e]].push_back(e);
-      cam_used[e_cam[e]] = 1;
-      pt_used[e_pt[e]] = 1;
-    }
-    std::vector<int> chidx(nc, -1), pose_cam;
-    for (int c = 0; c < nc; c++)
-      if (cam_used[c] && !fixed[c]) {
+    auto on = [&](int e) { return lvl < 0 || level[e] == lvl; };
+    cnt.assign(np + 1, 0);
+    chidx.assign(nc, -1);
+    for (int e = 0; e < ne; e++)
+      if (on(e)) {
+        cnt[e_pt[e] + 1]++;
+        chidx[e_cam[e]] = 0;  // used
+      }
+    pose_cam.clear();
+    for (int c = 0; c < nc; c++) {
+      if (chidx[c] == 0 && !fixed[c]) {
         chidx[c] = (int)pose_cam.size();
         pose_cam.push_back(c);
+      } else {
+        chidx[c] = -1;
       }
+    }
     const int nposes = (int)pose_cam.size();
-    std::vector<int> pt_off(1, 0), pt_id;
+    pt_off.assign(1, 0);
+    pt_id.clear();
     for (int p = 0; p < np; p++) {
-      if (!pt_used[p]) continue;
-      for (int e : by_pt[p]) act.push_back(e);
-      pt_id.push_back(p);
-      pt_off.push_back((int)act.size());
+      const int n = cnt[p + 1];
+      cnt[p + 1] = cnt[p] + n;  // start of point p's positions
+      if (n) {
+        pt_id.push_back(p);
+        pt_off.push_back(cnt[p + 1]);
+      }
     }
-    const int na = (int)act.size(), npa = (int)pt_id.size();
-    std::vector<std::vector<int>> by_cam(nposes);
+    const int na = cnt[np], npa = (int)pt_id.size();
+    act.resize(na);
+    pos_pt.resize(na);
+    for (int e = 0; e < ne; e++)
+      if (on(e)) act[cnt[e_pt[e]]++] = e;  // stable: ascending edge order per point
+    for (int i = 0; i < npa; i++)
+      for (int k = pt_off[i]; k < pt_off[i + 1]; k++) pos_pt[k] = i;
+    // positions grouped by pose (stable)
+    pcam.resize(na);
+    cam_off.assign(nposes + 1, 0);
     for (int k = 0; k < na; k++) {
-      const int ci = chidx[e_cam[act[k]]];
-      if (ci >= 0) by_cam[ci].push_back(k);
+      pcam[k] = chidx[e_cam[act[k]]];
+      if (pcam[k] >= 0) cam_off[pcam[k] + 1]++;
     }
-    std::vector<int> cam_off(1, 0), cam_pos;
-    for (int ci = 0; ci < nposes; ci++) {
-      cam_pos.insert(cam_pos.end(), by_cam[ci].begin(), by_cam[ci].end());
-      cam_off.push_back((int)cam_pos.size());
+    for (int ci = 0; ci < nposes; ci++) cam_off[ci + 1] += cam_off[ci];
+    cam_pos.resize(cam_off[nposes]);
+    {
+      std::vector<int>& fill = cnt;  // reuse
+      fill.assign(cam_off.begin(), cam_off.end());
+      for (int k = 0; k < na; k++)
+        if (pcam[k] >= 0) cam_pos[fill[pcam[k]]++] = k;
     }
-    // pair blocks (c1 <= c2), pairs ordered by point then edge order
-    std::vector<std::vector<int2>> blk((size_t)nposes * nposes);
-    for (int i = 0; i < npa; i++) {
+    // pair blocks: count, compact (empty off-diagonal blocks dropped), scatter
+    blk_map.assign((size_t)nposes * nposes, 0);
+    for (int i = 0; i < npa; i++)
       for (int k1 = pt_off[i]; k1 < pt_off[i + 1]; k1++) {
-        const int c1 = chidx[e_cam[act[k1]]];
+        const int c1 = pcam[k1];
         if (c1 < 0) continue;
         for (int k2 = pt_off[i]; k2 < pt_off[i + 1]; k2++) {
-          const int c2 = chidx[e_cam[act[k2]]];
-          if (c2 < 0 || c2 < c1) continue;
-          blk[(size_t)c1 * nposes + c2].push_back(make_int2(k1, k2));
+          const int c2 = pcam[k2];
+          if (c2 >= c1) blk_map[(size_t)c1 * nposes + c2]++;
         }
       }
-    }
-    std::vector<int> blk_off(1, 0);
-    std::vector<int2> blk_cc, pairs;
+    blk_off.assign(1, 0);
+    blk_cc.clear();
     for (int c1 = 0; c1 < nposes; c1++)
       for (int c2 = c1; c2 < nposes; c2++) {
-        const auto& v = blk[(size_t)c1 * nposes + c2];
-        if (v.empty() && c1 != c2) continue;
-        pairs.insert(pairs.end(), v.begin(), v.end());
-        blk_off.push_back((int)pairs.size());
+        int& m = blk_map[(size_t)c1 * nposes + c2];
+        const int n = m;
+        if (n == 0 && c1 != c2) {
+          m = -1;
+          continue;
+        }
+        m = blk_off.back();  // write cursor of this block
+        blk_off.push_back(blk_off.back() + n);
         blk_cc.push_back(make_int2(c1, c2));
       }
-    BA_CHECK(c.act.put(act));
-    BA_CHECK(c.chidx.put(chidx));
-    BA_CHECK(c.pose_cam.put(pose_cam));
-    BA_CHECK(c.pt_off.put(pt_off));
-    BA_CHECK(c.pt_id.put(pt_id));
-    BA_CHECK(c.cam_off.put(cam_off));
-    BA_CHECK(c.cam_pos.put(cam_pos));
-    BA_CHECK(c.blk_off.put(blk_off));
-    BA_CHECK(c.blk_cc.put(blk_cc));
-    BA_CHECK(c.pairs.put(pairs));
+    pairs.resize(blk_off.back());
+    for (int i = 0; i < npa; i++)
+      for (int k1 = pt_off[i]; k1 < pt_off[i + 1]; k1++) {
+        const int c1 = pcam[k1];
+        if (c1 < 0) continue;
+        for (int k2 = pt_off[i]; k2 < pt_off[i + 1]; k2++) {
+          const int c2 = pcam[k2];
+          if (c2 >= c1) pairs[blk_map[(size_t)c1 * nposes + c2]++] = make_int2(k1, k2);
+        }
+      }
+    // one upload
+    const size_t nb = blk_cc.size();
+    hipError_t he = struct_arena.reserve(arena_bytes(
+        {4 * (size_t)na, 4 * (size_t)na, 4 * (size_t)nc, 4 * (size_t)nposes, 4 * (size_t)(npa + 1), 4 * (size_t)npa,
+         4 * (size_t)(nposes + 1), 4 * cam_pos.size(), 4 * (nb + 1), 8 * nb, 8 * pairs.size()}));
+    if (he != hipSuccess) return ORBX_ERR_HIP;
+    Arena& A = struct_arena;
+    D.act = A.put(act);
+    D.pos_pt = A.put(pos_pt);
+    D.chidx = A.put(chidx);
+    D.pose_cam = A.put(pose_cam);
+    D.pt_off = A.put(pt_off);
+    D.pt_id = A.put(pt_id);
+    D.cam_off = A.put(cam_off);
+    D.cam_pos = A.put(cam_pos);
+    D.blk_off = A.put(blk_off);
+    D.blk_cc = A.put(blk_cc);
+    D.pairs = A.put(pairs);
+    BA_CHECK(A.upload(st));
     const size_t N = 6 * (size_t)nposes;
     BA_CHECK(c.Hpl.alloc(18 * (size_t)na));
     BA_CHECK(c.ptc.alloc(12 * (size_t)na));
     BA_CHECK(c.cmc.alloc(42 * (size_t)na));
     BA_CHECK(c.BD.alloc(18 * (size_t)na));
     BA_CHECK(c.cf.alloc(6 * (size_t)na));
-    BA_CHECK(c.chi.alloc(na));
     BA_CHECK(c.Hll.alloc(9 * (size_t)npa));
     BA_CHECK(c.bl.alloc(3 * (size_t)npa));
     BA_CHECK(c.Dinv.alloc(9 * (size_t)npa));
-    BA_CHECK(c.xl.alloc(3 * (size_t)npa));
     BA_CHECK(c.dmax_p.alloc(npa + nposes));
-    BA_CHECK(c.scale_p.alloc(npa + nposes));
     BA_CHECK(c.Hpp.alloc(36 * (size_t)nposes));
     BA_CHECK(c.bp.alloc(N));
     BA_CHECK(c.xp.alloc(N));
@@ -808,29 +1161,15 @@ struct LocalBA {
     D.na = na;
     D.npa = npa;
     D.nposes = nposes;
-    D.nblk = (int)blk_cc.size();
-    D.act = c.act.p;
-    D.chidx = c.chidx.p;
-    D.pose_cam = c.pose_cam.p;
-    D.pt_off = c.pt_off.p;
-    D.pt_id = c.pt_id.p;
-    D.cam_off = c.cam_off.p;
-    D.cam_pos = c.cam_pos.p;
-    D.blk_off = c.blk_off.p;
-    D.blk_cc = c.blk_cc.p;
-    D.pairs = c.pairs.p;
+    D.nblk = (int)nb;
     D.Hpl = c.Hpl.p;
     D.ptc = c.ptc.p;
     D.cmc = c.cmc.p;
     D.BD = c.BD.p;
     D.cf = c.cf.p;
-    D.chi = c.chi.p;
     D.Hll = c.Hll.p;
     D.bl = c.bl.p;
     D.Dinv = c.Dinv.p;
-    D.xl = c.xl.p;
-    D.scale_p = c.scale_p.p;
-    D.scale_c = c.scale_p.p + npa;  // contiguous with the point terms for one reduction
     D.Hpp = c.Hpp.p;
     D.bp = c.bp.p;
     D.xp = c.xp.p;
@@ -841,77 +1180,74 @@ struct LocalBA {
     return ORBX_OK;
   }
 
-  hipError_t errors(hipStream_t st, int recompute = 1) {
-    if (D.na > 0) hipLaunchKernelGGL(k_ba_errors, dim3((D.na + LBS - 1) / LBS), dim3(LBS), 0, st, D, recompute);
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D.chi, D.na, D.scal + 0, 0);
+  hipError_t errors(hipStream_t st, int recompute, int dst) {
+    hipLaunchKernelGGL(k_ba_errors, dim3(std::max((D.na + LBS - 1) / LBS, 1)), dim3(LBS), 0, st, D, recompute, dst);
     return hipGetLastError();
   }
 
-  hipError_t read_scalars(double out[4], hipStream_t st) {
-    hipError_t e = hipMemcpyAsync(out, D.scal, 4 * sizeof(double), hipMemcpyDeviceToHost, st);
+  hipError_t read_scalars(double out[5], hipStream_t st) {
+    hipError_t e = hipMemcpyAsync(out, D.scal, 5 * sizeof(double), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     return e;
   }
 
-  // OptimizationAlgorithmLevenberg::solve (+ optimize loop); returns iterations
+  // SparseOptimizer::optimize + OptimizationAlgorithmLevenberg::solve.  One
+  // host readback per LM trial (plus one for lambda init per phase); the
+  // accept/reject logic runs on the host on exactly the reference's doubles.
   orbx_status optimize(int iterations, const volatile int* stop, hipStream_t st, int* iters, double* final_chi) {
     double lambda = 0, ni = 2;
     int nBad = 0;
     int it = 0;
     const size_t N = 6 * (size_t)D.nposes;
-    const int in_lds = (N * N + 2 * N) * sizeof(double) <= 160 * 1024;
-    const size_t ldlt_smem = (in_lds ? N * N + 2 * N : 2 * N) * sizeof(double);
-    if (ldlt_smem > 160 * 1024) return ORBX_ERR_SIZE;
-    if (hipFuncSetAttribute((const void*)k_ba_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldlt_smem) !=
-        hipSuccess)
+    if (ldlt_np((int)N) > kLdltMaxNp) return ORBX_ERR_SIZE;
+    const bool in_lds = ldlt_np((int)N) <= kLdltLdsNp;
+    const size_t ldlt_smem = ldlt_smem_bytes((int)N, in_lds);
+    if (!in_lds) {
+      BA_CHECK(c.Sw.alloc((size_t)ldlt_np((int)N) * ldlt_np((int)N)));
+      D.Sw = c.Sw.p;
+    }
+    if (hipFuncSetAttribute(in_lds ? (const void*)k_ba_ldlt<true> : (const void*)k_ba_ldlt<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldlt_smem) != hipSuccess)
       return ORBX_ERR_HIP;
-    const int gp = (D.npa + D.nposes + LBS - 1) / LBS;
-    double sc[4];
+    const int gp = std::max((D.npa + D.nposes + LBS - 1) / LBS, 1);
+    const int ga = std::max((D.na + LBS - 1) / LBS, 1);
+    double sc[5];
     for (int i = 0; i < iterations && !(stop && *stop); i++) {
-      BA_CHECK(errors(st));
-      if (D.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3((D.na + LBS - 1) / LBS), dim3(LBS), 0, st, D);
+      BA_CHECK(errors(st, 1, 0));  // computeActiveErrors; activeRobustChi2 -> scal[0]
+      if (D.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3(ga), dim3(LBS), 0, st, D);
       if (D.npa > 0) hipLaunchKernelGGL(k_ba_point_sum, dim3((D.npa + LBS - 1) / LBS), dim3(LBS), 0, st, D);
-      if (D.nposes > 0) hipLaunchKernelGGL(k_ba_cam_sum, dim3(D.nposes), dim3(64), 0, st, D);
-      if (i == 0) hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D.dmax_p, D.npa + D.nposes, D.scal + 3, 1);
+      if (D.nposes > 0) hipLaunchKernelGGL(k_ba_cam_sum, dim3(D.nposes), dim3(256), 0, st, D);
       BA_CHECK(hipGetLastError());
-      BA_CHECK(read_scalars(sc, st));
-      double currentChi = sc[0];
-      const double iniChi = currentChi;
       if (i == 0) {
+        hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D.dmax_p, D.npa + D.nposes, D.scal + 3, 1);
+        BA_CHECK(read_scalars(sc, st));
         lambda = 1e-5 * sc[3];  // computeLambdaInit: tau * max |H_jj|
         ni = 2;
         nBad = 0;
       }
+      double currentChi = 0, iniChi = 0;
       double rho = 0;
       int qmax = 0;
       do {
-        if (D.npa > 0) hipLaunchKernelGGL(k_ba_point_schur, dim3((D.npa + LBS - 1) / LBS), dim3(LBS), 0, st, D, lambda);
+        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, D, lambda);
         if (D.nposes > 0) {
           BA_CHECK(hipMemsetAsync(D.S, 0, N * N * sizeof(double), st));
-          hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk), dim3(64), 0, st, D, lambda);
-          hipLaunchKernelGGL(k_ba_cam_coef, dim3(D.nposes), dim3(64), 0, st, D);
-          hipLaunchKernelGGL(k_ba_ldlt, dim3(1), dim3(1024), ldlt_smem, st, D, in_lds);
-        } else {
-          const double one = 1.0;
-          BA_CHECK(hipMemcpyAsync(D.scal + 2, &one, sizeof(double), hipMemcpyHostToDevice, st));
+          hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk), dim3(256), 0, st, D, lambda);
+          hipLaunchKernelGGL(k_ba_cam_coef, dim3(D.nposes), dim3(256), 0, st, D);
+          if (in_lds)
+            hipLaunchKernelGGL(k_ba_ldlt<true>, dim3(1), dim3(1024), ldlt_smem, st, D, 99);
+          else
+            hipLaunchKernelGGL(k_ba_ldlt<false>, dim3(1), dim3(1024), ldlt_smem, st, D, 99);
         }
-        BA_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_ba_update, dim3(gp), dim3(LBS), 0, st, D, lambda);
+        BA_CHECK(errors(st, 1, 1));
         BA_CHECK(read_scalars(sc, st));
+        if (qmax == 0) currentChi = iniChi = sc[0];
         const bool ok2 = sc[2] != 0.0;
-        double tempChi, scale = 0;
         trials++;
-        if (ok2) {
-          hipLaunchKernelGGL(k_ba_update, dim3(std::max(gp, 1)), dim3(LBS), 0, st, D, lambda);
-          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D.scale_p, D.npa + D.nposes, D.scal + 1, 0);
-          BA_CHECK(errors(st));
-          BA_CHECK(read_scalars(sc, st));
-          tempChi = sc[0];
-          scale = sc[1];
-        } else {
-          BA_CHECK(errors(st));
-          tempChi = std::numeric_limits<double>::max();
-        }
+        const double tempChi = ok2 ? sc[1] : std::numeric_limits<double>::max();
         rho = currentChi - tempChi;
+        double scale = ok2 ? sc[4] : 0.0;
         scale += 1e-3;
         rho /= scale;
         if (rho > 0 && std::isfinite(tempChi)) {
@@ -924,7 +1260,7 @@ struct LocalBA {
         } else {
           lambda *= ni;
           ni *= 2;
-          if (ok2) hipLaunchKernelGGL(k_ba_restore, dim3(std::max(gp, 1)), dim3(LBS), 0, st, D);
+          if (ok2) hipLaunchKernelGGL(k_ba_restore, dim3(gp), dim3(LBS), 0, st, D);
           BA_CHECK(hipGetLastError());
         }
         qmax++;
@@ -938,7 +1274,7 @@ struct LocalBA {
       if (nBad >= 3) break;
     }
     *iters = it;
-    BA_CHECK(errors(st, 0));  // activeRobustChi2 of the stored errors
+    BA_CHECK(errors(st, 0, 0));  // activeRobustChi2 of the stored errors
     BA_CHECK(read_scalars(sc, st));
     if (final_chi) *final_chi = sc[0];
     return ORBX_OK;
@@ -949,79 +1285,108 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
                          hipStream_t st) {
   L.trials = 0;
   BaDev& D = L.D;
+  double host_build_ms = 0;
+  const auto t_start = std::chrono::steady_clock::now();
   Ctx& c = L.c;
   const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
   D.nc = nc;
   D.np = np;
   D.ne = ne;
-  // vertices: Converter::toSE3Quat (float -> double, Quaterniond(R), normalize)
-  std::vector<double> cq(4 * (size_t)nc), ct(3 * (size_t)nc), intr(5 * (size_t)nc), X(3 * (size_t)np);
-  L.fixed.assign(nc, 0);
-  for (int i = 0; i < nc; i++) {
-    const float* T = pb->Tcw + 12 * i;
-    const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
-    Quat q = mat2q(R);
-    qnormalize(q);
-    cq[4 * i] = q.x;
-    cq[4 * i + 1] = q.y;
-    cq[4 * i + 2] = q.z;
-    cq[4 * i + 3] = q.w;
-    ct[3 * i] = T[3];
-    ct[3 * i + 1] = T[7];
-    ct[3 * i + 2] = T[11];
-    for (int k = 0; k < 5; k++) intr[5 * i + k] = pb->intr[5 * i + k];
-    L.fixed[i] = pb->fixed ? pb->fixed[i] : 0;
-  }
-  for (int i = 0; i < 3 * np; i++) X[i] = pb->Xw[i];
+  for (int e = 0; e < ne; e++)
+    if (pb->edge_point[e] < 0 || pb->edge_point[e] >= np || pb->edge_cam[e] < 0 || pb->edge_cam[e] >= nc)
+      return ORBX_ERR_ARG;
   L.e_pt.assign(pb->edge_point, pb->edge_point + ne);
   L.e_cam.assign(pb->edge_cam, pb->edge_cam + ne);
-  for (int e = 0; e < ne; e++) {
-    if (L.e_pt[e] < 0 || L.e_pt[e] >= np || L.e_cam[e] < 0 || L.e_cam[e] >= nc) return ORBX_ERR_ARG;
-  }
-  std::vector<double> eobs(3 * (size_t)ne), einfo(ne), edelta(ne);
-  std::vector<float> edsqr(ne);
+  L.fixed.assign(nc, 0);
   L.e_st.resize(ne);
-  std::vector<uint8_t> erob(ne, 1);
-  const float thMono = std::sqrt(5.991f), thStereo = std::sqrt(7.815f);  // src/Optimizer.cc:653-654
-  for (int e = 0; e < ne; e++) {
-    L.e_st[e] = pb->obs[3 * e + 2] >= 0 ? 1 : 0;
-    for (int k = 0; k < 3; k++) eobs[3 * e + k] = pb->obs[3 * e + k];
-    einfo[e] = pb->inv_sigma2[e];
-    edelta[e] = L.e_st[e] ? thStereo : thMono;
-    edsqr[e] = (float)(edelta[e] * edelta[e]);
+  Arena& A = L.prob_arena;
+  if (A.reserve(arena_bytes({32 * (size_t)nc, 24 * (size_t)nc, 40 * (size_t)nc, 24 * (size_t)np, 4 * (size_t)ne,
+                             4 * (size_t)ne, (size_t)ne, 24 * (size_t)ne, 8 * (size_t)ne, 8 * (size_t)ne,
+                             4 * (size_t)ne, (size_t)ne})) != hipSuccess)
+    return ORBX_ERR_HIP;
+  double* cq = A.take<double>(4 * (size_t)nc);
+  double* ct = A.take<double>(3 * (size_t)nc);
+  double* intr = A.take<double>(5 * (size_t)nc);
+  double* X = A.take<double>(3 * (size_t)np);
+  int* ept = A.take<int>(ne);
+  int* ecam = A.take<int>(ne);
+  uint8_t* est = A.take<uint8_t>(ne);
+  double* eobs = A.take<double>(3 * (size_t)ne);
+  double* einfo = A.take<double>(ne);
+  double* edelta = A.take<double>(ne);
+  float* edsqr = A.take<float>(ne);
+  uint8_t* erob = A.take<uint8_t>(ne);
+  // vertices: Converter::toSE3Quat (float -> double, Quaterniond(R), normalize)
+  {
+    double* hq = A.host(cq);
+    double* ht = A.host(ct);
+    double* hi = A.host(intr);
+    for (int i = 0; i < nc; i++) {
+      const float* T = pb->Tcw + 12 * i;
+      const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+      Quat q = mat2q(R);
+      qnormalize(q);
+      hq[4 * i] = q.x;
+      hq[4 * i + 1] = q.y;
+      hq[4 * i + 2] = q.z;
+      hq[4 * i + 3] = q.w;
+      ht[3 * i] = T[3];
+      ht[3 * i + 1] = T[7];
+      ht[3 * i + 2] = T[11];
+      for (int k = 0; k < 5; k++) hi[5 * i + k] = pb->intr[5 * i + k];
+      L.fixed[i] = pb->fixed ? pb->fixed[i] : 0;
+    }
+    double* hx = A.host(X);
+    for (int i = 0; i < 3 * np; i++) hx[i] = pb->Xw[i];
+    if (ne) {
+      std::memcpy(A.host(ept), pb->edge_point, 4 * (size_t)ne);
+      std::memcpy(A.host(ecam), pb->edge_cam, 4 * (size_t)ne);
+    }
+    const float thMono = std::sqrt(5.991f), thStereo = std::sqrt(7.815f);  // src/Optimizer.cc:653-654
+    uint8_t* hs = A.host(est);
+    double* ho = A.host(eobs);
+    double* hinf = A.host(einfo);
+    double* hd = A.host(edelta);
+    float* hd2 = A.host(edsqr);
+    uint8_t* hr = A.host(erob);
+    for (int e = 0; e < ne; e++) {
+      L.e_st[e] = hs[e] = pb->obs[3 * e + 2] >= 0 ? 1 : 0;
+      for (int k = 0; k < 3; k++) ho[3 * e + k] = pb->obs[3 * e + k];
+      hinf[e] = pb->inv_sigma2[e];
+      hd[e] = hs[e] ? thStereo : thMono;
+      hd2[e] = (float)(hd[e] * hd[e]);
+      hr[e] = 1;
+    }
   }
-  BA_CHECK(c.cq.put(cq));
-  BA_CHECK(c.ct.put(ct));
+  BA_CHECK(A.upload(st));
   BA_CHECK(c.cbak.alloc(7 * (size_t)nc));
-  BA_CHECK(c.intr.put(intr));
-  BA_CHECK(c.X.put(X));
   BA_CHECK(c.Xbak.alloc(3 * (size_t)np));
-  BA_CHECK(c.ept.put(L.e_pt));
-  BA_CHECK(c.ecam.put(L.e_cam));
-  BA_CHECK(c.est.put(L.e_st));
-  BA_CHECK(c.eobs.put(eobs));
-  BA_CHECK(c.einfo.put(einfo));
-  BA_CHECK(c.edelta.put(edelta));
-  BA_CHECK(c.edsqr.put(edsqr));
-  BA_CHECK(c.erobust.put(erob));
   BA_CHECK(c.eerr.alloc(3 * (size_t)ne));
   BA_CHECK(hipMemsetAsync(c.eerr.p, 0, 3 * sizeof(double) * std::max(ne, 1), st));
   BA_CHECK(c.flag.alloc(ne));
-  BA_CHECK(c.scal.alloc(4));
-  D.cq = c.cq.p;
-  D.ct = c.ct.p;
+  BA_CHECK(c.scal.alloc(8));
+  // grid-reduction scratch: partials for the widest reducing launch, counter zeroed once
+  BA_CHECK(c.part.alloc((size_t)(ne + np + nc) / LBS + 16));
+  if (!c.cnt.p) {
+    BA_CHECK(c.cnt.alloc(1));
+    BA_CHECK(hipMemsetAsync(c.cnt.p, 0, sizeof(unsigned), st));
+  }
+  D.part = c.part.p;
+  D.cnt = c.cnt.p;
+  D.cq = cq;
+  D.ct = ct;
   D.cbak = c.cbak.p;
-  D.intr = c.intr.p;
-  D.X = c.X.p;
+  D.intr = intr;
+  D.X = X;
   D.Xbak = c.Xbak.p;
-  D.ept = c.ept.p;
-  D.ecam = c.ecam.p;
-  D.est = c.est.p;
-  D.eobs = c.eobs.p;
-  D.einfo = c.einfo.p;
-  D.edelta = c.edelta.p;
-  D.edsqr = c.edsqr.p;
-  D.erobust = c.erobust.p;
+  D.ept = ept;
+  D.ecam = ecam;
+  D.est = est;
+  D.eobs = eobs;
+  D.einfo = einfo;
+  D.edelta = edelta;
+  D.edsqr = edsqr;
+  D.erobust = erob;
   D.eerr = c.eerr.p;
   D.scal = c.scal.p;
   res->iterations[0] = res->iterations[1] = 0;
@@ -1032,7 +1397,10 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   if (!(stop && *stop)) {  // src/Optimizer.cc:749-751
     ran = true;
     L.level.assign(ne, 0);
-    orbx_status s = L.build_structure(-1);
+    const auto tb0 = std::chrono::steady_clock::now();
+    orbx_status s = L.build_structure(-1, st);
+    const auto tb1 = std::chrono::steady_clock::now();
+    host_build_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
     if (s != ORBX_OK) return s;
     s = L.optimize(5, stop, st, &res->iterations[0], &res->chi2[0]);
     if (s != ORBX_OK) return s;
@@ -1042,7 +1410,9 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       BA_CHECK(hipGetLastError());
       BA_CHECK(hipMemcpyAsync(L.level.data(), c.flag.p, ne, hipMemcpyDeviceToHost, st));
       BA_CHECK(hipStreamSynchronize(st));
-      s = L.build_structure(0);
+      const auto tb2 = std::chrono::steady_clock::now();
+      s = L.build_structure(0, st);
+      host_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb2).count();
       if (s != ORBX_OK) return s;
       s = L.optimize(10, stop, st, &res->iterations[1], &res->chi2[1]);
       if (s != ORBX_OK) return s;
@@ -1078,6 +1448,10 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   if (res->Tcw_d) BA_CHECK(hipMemcpyAsync(res->Tcw_d, c.Tcw_d_out.p, 12 * sizeof(double) * nc, hipMemcpyDeviceToHost, st));
   if (res->Xw_d) BA_CHECK(hipMemcpyAsync(res->Xw_d, c.Xw_d_out.p, 3 * sizeof(double) * np, hipMemcpyDeviceToHost, st));
   BA_CHECK(hipStreamSynchronize(st));
+  if (std::getenv("ORBX_BA_TRACE"))
+    std::fprintf(stderr, "[orbx_ba] total %.3f ms, host structure %.3f ms, iterations %d+%d, trials %d\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(),
+                 host_build_ms, res->iterations[0], res->iterations[1], res->trials);
   return ORBX_OK;
 }
 
@@ -1138,3 +1512,84 @@ orbx_status orbx_local_ba(const orbx_ba_problem* p, orbx_ba_result* r, const vol
 }
 
 }  // extern "C"
+
+// Debug/benchmark probe (include/orbx_debug.h): solve S x = b (N = 6 * nposes)
+// with the LocalBA LDLT kernel; ms = average kernel time over reps launches.
+extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* x, int reps, float* ms) {
+  if (!S || !b || !x || N <= 0 || N % 6 || reps < 1) return ORBX_ERR_ARG;
+  const int stage_limit = std::getenv("ORBX_LDLT_STAGE") ? std::atoi(std::getenv("ORBX_LDLT_STAGE")) : 99;
+  orbx::BaDev D{};
+  D.nposes = N / 6;
+  double *dS = nullptr, *dS0 = nullptr, *db = nullptr, *dx = nullptr, *dscal = nullptr;
+  const size_t nn = (size_t)N * N * sizeof(double);
+  hipEvent_t e0, e1;
+  hipError_t e = hipMalloc((void**)&dS, nn);
+  if (e == hipSuccess) e = hipMalloc((void**)&dS0, nn);
+  if (e == hipSuccess) e = hipMalloc((void**)&db, N * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&dx, N * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&dscal, 8 * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(dS0, S, nn, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(db, b, N * sizeof(double), hipMemcpyHostToDevice);
+  D.S = dS;
+  D.bs = db;
+  D.xp = dx;
+  D.scal = dscal;
+  unsigned long long* ddbg = nullptr;
+  const bool want_ts = std::getenv("ORBX_LDLT_TS") != nullptr;
+  if (e == hipSuccess && want_ts) {
+    e = hipMalloc((void**)&ddbg, 64 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(ddbg, 0, 64 * sizeof(unsigned long long));
+  }
+  D.dbg = ddbg;
+  if (orbx::ldlt_np(N) > orbx::kLdltMaxNp) e = hipErrorInvalidValue;
+  const bool in_lds = orbx::ldlt_np(N) <= orbx::kLdltLdsNp;
+  const size_t smem = orbx::ldlt_smem_bytes(N, in_lds);
+  double* dSw = nullptr;
+  if (e == hipSuccess && !in_lds) e = hipMalloc((void**)&dSw, (size_t)orbx::ldlt_np(N) * orbx::ldlt_np(N) * sizeof(double));
+  D.Sw = dSw;
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute(in_lds ? (const void*)orbx::k_ba_ldlt<true> : (const void*)orbx::k_ba_ldlt<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  float total = 0;
+  if (e == hipSuccess) {
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int r = 0; r < reps && e == hipSuccess; r++) {
+      e = hipMemcpy(dS, dS0, nn, hipMemcpyDeviceToDevice);
+      (void)hipEventRecord(e0, nullptr);
+      if (in_lds)
+        hipLaunchKernelGGL(orbx::k_ba_ldlt<true>, dim3(1), dim3(1024), smem, nullptr, D, stage_limit);
+      else
+        hipLaunchKernelGGL(orbx::k_ba_ldlt<false>, dim3(1), dim3(1024), smem, nullptr, D, stage_limit);
+      (void)hipEventRecord(e1, nullptr);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      float t = 0;
+      (void)hipEventElapsedTime(&t, e0, e1);
+      total += t;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  double ok = 0;
+  if (e == hipSuccess) e = hipMemcpy(x, dx, N * sizeof(double), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(&ok, dscal + 2, sizeof(double), hipMemcpyDeviceToHost);
+  if (ms) *ms = total / reps;
+  (void)hipFree(dS);
+  (void)hipFree(dS0);
+  (void)hipFree(db);
+  (void)hipFree(dx);
+  (void)hipFree(dscal);
+  if (dSw) (void)hipFree(dSw);
+  if (ddbg) {
+    unsigned long long ts[64];
+    if (hipMemcpy(ts, ddbg, sizeof(ts), hipMemcpyDeviceToHost) == hipSuccess) {
+      std::fprintf(stderr, "[ldlt ts N=%d] ", N);
+      for (int i = 1; i < 64; i++)
+        if (ts[i]) std::fprintf(stderr, "%d:%llu ", i, ts[i] - ts[0]);
+      std::fprintf(stderr, "\n");
+    }
+    (void)hipFree(ddbg);
+  }
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  return ok != 0.0 ? ORBX_OK : ORBX_ERR_STATE;
+}

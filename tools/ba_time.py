@@ -1,0 +1,27 @@
+"""Time Optimizer::LocalBundleAdjustment on the config-4 problem (GPU handle, repeated calls)."""
+import json
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+from orb_slam2_commit_amd import Optimizer, synth  # noqa: E402
+
+
+def main(reps=10):
+    P = synth.localba_problem(seed=7)
+    o = Optimizer(0)
+    r = o.LocalBundleAdjustment(P)  # warm-up (allocations, code load)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = o.LocalBundleAdjustment(P)
+    dt = (time.perf_counter() - t0) / reps
+    its = sum(r["iterations"])
+    print(json.dumps(dict(ms_per_call=dt * 1e3, iterations=r["iterations"], trials=r["trials"],
+                          iters_per_s=its / dt, trials_per_s=r["trials"] / dt,
+                          edges=int(len(P["edge_point"])))))
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10)
