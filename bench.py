@@ -1,9 +1,13 @@
-"""Benchmark: frames/sec ORB extract+match on KITTI-00-shaped stereo (BASELINE.json configs[1]).
+"""Benchmark: frames/sec ORB extract+match on KITTI-00-shaped stereo (BASELINE.json configs[1])
++ LocalBA iterations/sec on the KITTI-00 LocalBundleAdjustment problem (configs[3]).
 
 One "step" = one pass of the hot path over one batch of B synthetic stereo
 frames resident in HBM: ORB extraction of the 2B images (1241x376, 2000
 features, 8 levels x1.2, FAST 20/7) + Frame::ComputeStereoMatches of the B
-frames, all inside liborbx.so (orbx_stereo_frames_device).
+frames, all inside liborbx.so (orbx_stereo_frames_device).  `value` is that
+frames/s.  The LocalBA leg then runs Optimizer::LocalBundleAdjustment
+(orbx_ba_run) on a synthetic 20-KF / ~7.4k-point / ~43k-edge problem per rank,
+--ba-calls times, and reports LM iterations/s (whole job) under "localba".
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 
@@ -37,6 +41,7 @@ def parse():
     ap.add_argument("--unique", type=int, default=16, help="distinct synthetic stereo pairs tiled into the batch")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/profile.py); null if absent")
     return ap.parse_args()
@@ -89,6 +94,49 @@ def cpu_baseline(pairs, seconds):
     return dict(value=round(n / el, 3), unit="frames/s", cores=1, kind="port",
                 sample="%d KITTI-shaped stereo frames (extract L + extract R + stereo match), oracle/ C++ "
                        "restatement, 1 thread, %.1f s" % (n, el))
+
+
+def localba_leg(args, rank, world, dev, odist):
+    """Optimizer::LocalBundleAdjustment on the config-4 problem: whole-job LM iterations/s."""
+    import torch
+    from orb_slam2_commit_amd import Optimizer, synth
+    P = synth.localba_problem(seed=7 + 1000 * rank)
+    opt = Optimizer(dev.index)
+    r = opt.LocalBundleAdjustment(P)  # warm-up: allocations, code objects
+    odist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    its = 0
+    for _ in range(args.ba_calls):
+        r = opt.LocalBundleAdjustment(P)
+        its += sum(r["iterations"])
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    el = odist.max_over_ranks(time.perf_counter() - t0, dev)
+    its_all = odist.sum_over_ranks(float(its), dev)
+    opt.close()
+    out = dict(iters_per_s=round(its_all / el, 2), ms_per_call=round(el / args.ba_calls * 1e3, 3),
+               calls_per_gpu=args.ba_calls, iterations=list(r["iterations"]), trials=r["trials"],
+               problem=dict(keyframes=int(len(P["Tcw"])), fixed=int(np.sum(P["fixed"])),
+                            points=int(len(P["Xw"])), edges=int(len(P["edge_point"])),
+                            stereo_edges=int(np.sum(P["obs"][:, 2] >= 0))),
+               dtype="f64", scaling="weak", cpu_baseline=None)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        n, t0 = 0, time.perf_counter()
+        cits = 0
+        while True:
+            cr = oracle.local_ba(P)
+            cits += sum(cr["iterations"])
+            n += 1
+            cel = time.perf_counter() - t0
+            if cel >= 2.0 and n >= 2:
+                break
+        out["cpu_baseline"] = dict(value=round(cits / cel, 2), unit="LM iterations/s", cores=1, kind="port",
+                                   sample="%d LocalBA calls on the same problem, oracle/localba.cpp, 1 thread, "
+                                          "%.1f s" % (n, cel))
+    return out
 
 
 def main():
@@ -201,6 +249,9 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pairs, args.cpu_baseline_seconds)
+    if args.ba_calls > 0:
+        out["localba"] = localba_leg(args, rank, world, dev, odist)
+        out["localba_iters_per_s"] = out["localba"]["iters_per_s"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

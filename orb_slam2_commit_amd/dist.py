@@ -38,6 +38,17 @@ def max_over_ranks(value, device=None):
     return float(t.item())
 
 
+def sum_over_ranks(value, device=None):
+    """Sum of a float over all ranks (work done by the whole job)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():

@@ -27,7 +27,8 @@ def _worker(rank, world, port, q):
     elapsed = 1.0 + rank  # rank 1 is the slow one
     m = odist.max_over_ranks(elapsed)
     seeds = odist.frame_seeds(rank, 4)
-    q.put((rank, m, seeds, odist.job_throughput(8, 10, world, m)))
+    its = odist.sum_over_ranks(15.0 + rank)  # LocalBA leg: iterations summed over ranks
+    q.put((rank, m, seeds, odist.job_throughput(8, 10, world, m), its))
     dist.destroy_process_group()
 
 
@@ -46,9 +47,11 @@ def test_gloo_world2_max_and_shards():
     assert all(r[1] == 2.0 for r in res)  # max over ranks
     assert set(res[0][2]).isdisjoint(res[1][2])  # disjoint frame shards
     assert res[0][3] == pytest.approx(8 * 10 * 2 / 2.0)
+    assert all(r[4] == 31.0 for r in res)
 
 
 def test_single_rank_noop():
     from orb_slam2_commit_amd import dist as odist
     assert odist.max_over_ranks(3.5) == 3.5
+    assert odist.sum_over_ranks(3.5) == 3.5
     assert odist.job_throughput(128, 20, 1, 2.0) == 1280.0
