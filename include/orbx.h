@@ -26,6 +26,9 @@
  *                                                               src/ORBmatcher.cc:589-736, include/ORBmatcher.h:62
  *   orbx_search_by_bow_device   batch of the two above (one block per problem); ComputeThreeMaxima
  *                               (src/ORBmatcher.cc:1797-1839) runs inside
+ *   orbx_pnp_create             PnPsolver::PnPsolver + SetRansacParameters
+ *                                                               src/PnPsolver.cc:67-179, include/PnPsolver.h:66-70
+ *   orbx_pnp_iterate            PnPsolver::iterate              src/PnPsolver.cc:182-384, include/PnPsolver.h:74
  *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
  *                               (g2o graph build, optimize(5), outlier levels, optimize(10), vToErase;
  *                               the Map mutex/recovery part stays on the caller's side)
@@ -200,6 +203,43 @@ orbx_status orbx_ba_run(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_resu
 /* One-shot form: create, run, destroy. */
 orbx_status orbx_local_ba(const orbx_ba_problem* problem, orbx_ba_result* result, const volatile int* stop_flag,
                           int device);
+
+/* PnPsolver (src/PnPsolver.cc).  The caller gathers the correspondences
+ * exactly like the constructor (:67-125): for each frame keypoint i with a
+ * valid, non-bad MapPoint, p2d = mvKeysUn[i].pt, sigma2 = mvLevelSigma2[octave],
+ * p3d = MapPoint world position, and keeps i (mvKeyPointIndices) to map the
+ * returned inlier bytes back to frame indices. */
+typedef struct {
+  int n;
+  const float* p3d;    /* n x 3 */
+  const float* p2d;    /* n x 2 */
+  const float* sigma2; /* n */
+  float fx, fy, cx, cy;
+} orbx_pnp_problem;
+
+typedef struct { /* SetRansacParameters arguments (Tracking: 0.99, 10, 300, 4, 0.5, 5.991) */
+  double probability;
+  int min_inliers;
+  int max_iterations;
+  int min_set; /* 1..16 */
+  float epsilon;
+  float th2;
+} orbx_pnp_params;
+
+typedef struct orbx_pnp orbx_pnp;
+orbx_status orbx_pnp_create(const orbx_pnp_problem* problem, const orbx_pnp_params* params, int device,
+                            orbx_pnp** out);
+orbx_status orbx_pnp_destroy(orbx_pnp* h);
+/* Derived RANSAC parameters (mRansacMinInliers, mRansacMaxIts, mRansacEpsilon). */
+orbx_status orbx_pnp_get_params(const orbx_pnp* h, int* min_inliers, int* max_iterations, float* epsilon);
+/* iterate(nIterations, bNoMore, vbInliers, nInliers).  rand_vals: the next
+ * rand() outputs of the caller's stream (the reference draws
+ * DUtils::Random::RandomInt from the process rand()); supply at least
+ * min_set * max(maxIts - done, nIterations) values; *used = values consumed,
+ * so the caller advances its stream by exactly that.  *found = 1 when a pose
+ * (Tcw, row-major 4x4) is returned; inliers[n] = 1 per inlier correspondence. */
+orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_vals, int n_rand, int* used,
+                             int* no_more, float Tcw[16], uint8_t* inliers, int* n_inliers, int* found);
 
 /* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
  * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel

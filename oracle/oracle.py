@@ -71,6 +71,18 @@ def lib():
         L.oracle_ba_edge_probe.restype = None
         L.oracle_se3_exp_mul.argtypes = [P, P, P, P, P]
         L.oracle_se3_exp_mul.restype = None
+        L.oracle_pnp_create.argtypes = [C.c_int, P, P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_double,
+                                        C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+        L.oracle_pnp_create.restype = P
+        L.oracle_pnp_destroy.argtypes = [P]
+        L.oracle_pnp_destroy.restype = None
+        L.oracle_pnp_params.argtypes = [P, P, P, P]
+        L.oracle_pnp_params.restype = None
+        L.oracle_pnp_iterate.argtypes = [P, C.c_int, P, C.c_int, P, P, P, P, P]
+        L.oracle_epnp.argtypes = [P, P, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, P, P]
+        L.oracle_epnp.restype = C.c_double
+        L.oracle_svd.argtypes = [P, C.c_int, C.c_int, P, P, P]
+        L.oracle_svd.restype = None
         _lib = L
     return _lib
 
@@ -247,3 +259,57 @@ def local_ba(prob, stop=False):
     lib().oracle_local_ba(C.byref(P), C.byref(R), _p(flag))
     out.update(iterations=tuple(R.iterations), trials=R.trials, chi2=tuple(R.chi2))
     return out
+
+
+class PnPsolver:
+    """PnPsolver restatement (src/PnPsolver.cc): correspondences in gather order,
+    SetRansacParameters at creation (Tracking uses 0.99, 10, 300, 4, 0.5, 5.991)."""
+
+    def __init__(self, p3d, p2d, sigma2, fx, fy, cx, cy, probability=0.99, min_inliers=8, max_iterations=300,
+                 min_set=4, epsilon=0.4, th2=5.991):
+        self.p3d = np.ascontiguousarray(p3d, np.float32).reshape(-1, 3)
+        self.p2d = np.ascontiguousarray(p2d, np.float32).reshape(-1, 2)
+        self.sigma2 = np.ascontiguousarray(sigma2, np.float32)
+        self.n = len(self.p3d)
+        self._h = lib().oracle_pnp_create(self.n, _p(self.p3d), _p(self.p2d), _p(self.sigma2), float(fx), float(fy),
+                                          float(cx), float(cy), float(probability), int(min_inliers),
+                                          int(max_iterations), int(min_set), float(epsilon), float(th2))
+        a, b, c = C.c_int(), C.c_int(), C.c_float()
+        lib().oracle_pnp_params(self._h, C.byref(a), C.byref(b), C.byref(c))
+        self.min_inliers, self.max_its, self.epsilon = a.value, b.value, c.value
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oracle_pnp_destroy(self._h)
+            self._h = None
+
+    def iterate(self, n_iterations, rng):
+        """rng: object with take(k) -> rand() values; consumes exactly what the reference would.
+        Returns (Tcw[4,4] f32 or None, no_more, inliers[n] bool, n_inliers)."""
+        need = 4 * max(n_iterations, self.max_its) + 16
+        vals = np.asarray(rng.peek(need) if hasattr(rng, "peek") else rng.take(need), np.int32)
+        used, nm, ni = C.c_int(), C.c_int(), C.c_int()
+        T = np.zeros(16, np.float32)
+        inl = np.zeros(self.n, np.uint8)
+        rc = lib().oracle_pnp_iterate(self._h, int(n_iterations), _p(vals), len(vals), C.byref(used), C.byref(nm),
+                                      _p(T), _p(inl), C.byref(ni))
+        if hasattr(rng, "advance"):
+            rng.advance(used.value)
+        assert rc >= 0
+        return (T.reshape(4, 4) if rc == 1 else None), bool(nm.value), inl.astype(bool), ni.value, used.value
+
+
+def epnp(pws, us, fu, fv, uc, vc):
+    pws = np.ascontiguousarray(pws, np.float64).reshape(-1, 3)
+    us = np.ascontiguousarray(us, np.float64).reshape(-1, 2)
+    R, t = np.zeros(9), np.zeros(3)
+    err = lib().oracle_epnp(_p(pws), _p(us), len(pws), fu, fv, uc, vc, _p(R), _p(t))
+    return R.reshape(3, 3), t, err
+
+
+def svd(A):
+    A = np.ascontiguousarray(A, np.float64)
+    m, n = A.shape
+    Ut, w, Vt = np.zeros((n, m)), np.zeros(n), np.zeros((n, n))
+    lib().oracle_svd(_p(A), m, n, _p(Ut), _p(w), _p(Vt))
+    return Ut, w, Vt

@@ -139,6 +139,26 @@ void oracle_ba_edge_probe(const double q[4], const double t[3], const double X[3
 /* exp(u) * T (SE3Quat::exp, operator*, normalizeRotation). */
 void oracle_se3_exp_mul(const double u[6], const double q[4], const double t[3], double q_out[4], double t_out[3]);
 
+/* PnPsolver (src/PnPsolver.cc:67-1101).  Correspondences in ctor gather
+ * order; SetRansacParameters(probability, minInliers, maxIterations, minSet,
+ * epsilon, th2) applied at creation. */
+typedef struct oracle_pnp oracle_pnp;
+oracle_pnp* oracle_pnp_create(int n, const float* p3d, const float* p2d, const float* sigma2, float fx, float fy,
+                              float cx, float cy, double probability, int min_inliers, int max_iterations,
+                              int min_set, float epsilon, float th2);
+void oracle_pnp_destroy(oracle_pnp* h);
+void oracle_pnp_params(const oracle_pnp* h, int* min_inliers, int* max_its, float* epsilon);
+/* iterate(nIterations, bNoMore, vbInliers, nInliers) over caller rand() values
+ * (consumed count in *used); returns 1 if a pose is returned, 0 if not, -1
+ * if rand_vals ran out. */
+int oracle_pnp_iterate(oracle_pnp* h, int nIterations, const int32_t* rand_vals, int n_rand, int* used,
+                       int* bNoMore, float Tcw[16], uint8_t* inliers, int* nInliers);
+/* EPnP compute_pose probe; returns the reprojection error. */
+double oracle_epnp(const double* pws, const double* us, int n, double fu, double fv, double uc, double vc, double* R,
+                   double* t);
+/* cvSVD probe on an m x n matrix (m >= n): left vectors as rows, w, Vt. */
+void oracle_svd(const double* A, int m, int n, double* Ut, double* w, double* Vt);
+
 #ifdef __cplusplus
 }
 #endif

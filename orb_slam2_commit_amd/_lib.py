@@ -61,6 +61,16 @@ class BaResult(C.Structure):
                 ("Xw_d", C.c_void_p), ("iterations", C.c_int * 2), ("trials", C.c_int), ("chi2", C.c_double * 2)]
 
 
+class PnpProblem(C.Structure):
+    _fields_ = [("n", C.c_int), ("p3d", C.c_void_p), ("p2d", C.c_void_p), ("sigma2", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float)]
+
+
+class PnpParams(C.Structure):
+    _fields_ = [("probability", C.c_double), ("min_inliers", C.c_int), ("max_iterations", C.c_int),
+                ("min_set", C.c_int), ("epsilon", C.c_float), ("th2", C.c_float)]
+
+
 # Every entry point of include/orbx.h with its ctypes signature.
 P = C.c_void_p
 SIGNATURES = {
@@ -81,6 +91,11 @@ SIGNATURES = {
     "orbx_search_by_bow_kf_kf": ([C.POINTER(BowSide), C.POINTER(BowSide), C.c_float, C.c_int, P,
                                   C.POINTER(C.c_int), C.c_int], C.c_int),
     "orbx_search_by_bow_device": ([C.POINTER(BowProblem), C.c_int, P], C.c_int),
+    "orbx_pnp_create": ([C.POINTER(PnpProblem), C.POINTER(PnpParams), C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_pnp_destroy": ([P], C.c_int),
+    "orbx_pnp_get_params": ([P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)], C.c_int),
+    "orbx_pnp_iterate": ([P, C.c_int, P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), P, P,
+                          C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "orbx_ba_destroy": ([P], C.c_int),
     "orbx_ba_run": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),

@@ -276,3 +276,64 @@ class Optimizer:
         check(_lib.lib().orbx_ba_run(self._h, C.byref(P), C.byref(R), ptr(flag)), "orbx_ba_run")
         out.update(iterations=tuple(R.iterations), trials=R.trials, chi2=tuple(R.chi2))
         return out
+
+
+class PnPsolver:
+    """PnPsolver (include/PnPsolver.h:66-77) over orbx_pnp_*.
+
+    Correspondences are given in the constructor's gather order
+    (src/PnPsolver.cc:67-125): world points, undistorted keypoints and
+    mvLevelSigma2[octave] of the matched keypoints.  Like the reference the
+    constructor applies SetRansacParameters() with its defaults."""
+
+    def __init__(self, p3d, p2d, sigma2, fx, fy, cx, cy, device=0):
+        self.p3d = np.ascontiguousarray(p3d, np.float32).reshape(-1, 3)
+        self.p2d = np.ascontiguousarray(p2d, np.float32).reshape(-1, 2)
+        self.sigma2 = np.ascontiguousarray(sigma2, np.float32)
+        self.n = len(self.p3d)
+        self.intr = (float(fx), float(fy), float(cx), float(cy))
+        self.device = int(device)
+        self._h = None
+        self.SetRansacParameters()
+
+    def SetRansacParameters(self, probability=0.99, minInliers=8, maxIterations=300, minSet=4, epsilon=0.4,
+                            th2=5.991):
+        self.close()
+        prob = _lib.PnpProblem(self.n, ptr(self.p3d), ptr(self.p2d), ptr(self.sigma2), *self.intr)
+        prm = _lib.PnpParams(float(probability), int(minInliers), int(maxIterations), int(minSet), float(epsilon),
+                             float(th2))
+        h = C.c_void_p()
+        check(_lib.lib().orbx_pnp_create(C.byref(prob), C.byref(prm), self.device, C.byref(h)), "orbx_pnp_create")
+        self._h = h
+        self.min_set = int(minSet)
+        a, b, c = C.c_int(), C.c_int(), C.c_float()
+        check(_lib.lib().orbx_pnp_get_params(h, C.byref(a), C.byref(b), C.byref(c)), "orbx_pnp_get_params")
+        self.min_inliers, self.max_its, self.epsilon = a.value, b.value, c.value
+        self._done = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().orbx_pnp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def iterate(self, nIterations, rng):
+        """rng: a rand() stream with peek(k)/advance(k) (e.g. glibc_rand.GlibcRand(1), the
+        unseeded process rand() of the reference).  Returns (Tcw[4,4] or None, bNoMore,
+        vbInliers[n] bool, nInliers); the stream advances by exactly what was drawn."""
+        need = self.min_set * max(self.max_its - self._done, int(nIterations), 0)
+        vals = np.ascontiguousarray(rng.peek(need), np.int32) if need else np.zeros(0, np.int32)
+        used, nm, ni, found = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        T = np.zeros(16, np.float32)
+        inl = np.zeros(max(self.n, 1), np.uint8)
+        check(_lib.lib().orbx_pnp_iterate(self._h, int(nIterations), ptr(vals), len(vals), C.byref(used),
+                                          C.byref(nm), ptr(T), ptr(inl), C.byref(ni), C.byref(found)),
+              "orbx_pnp_iterate")
+        rng.advance(used.value)
+        self._done += used.value // self.min_set
+        return (T.reshape(4, 4) if found.value else None), bool(nm.value), inl[:self.n].astype(bool), ni.value

@@ -216,3 +216,36 @@ def localba_problem(seed=7, n_local=20, n_fixed=6, n_points=8000, obs_per_point=
                 Xw=Xn.astype(np.float32), edge_point=np.array(ep, np.int32), edge_cam=np.array(ec, np.int32),
                 obs=np.array(obs, np.float32), inv_sigma2=np.array(isg, np.float32),
                 Tcw_true=Tcw_true.reshape(n_cams, 12), Xw_true=X)
+
+
+EUROC = dict(fx=435.2047, fy=435.2047, cx=367.4517, cy=252.2009, bf=47.9064, width=752, height=480)
+
+
+def pnp_problem(seed=3, n=1200, outlier_frac=0.4, noise_px=1.0, z_range=(2.0, 20.0), scale_factor=1.2,
+                nlevels=8, intr=EUROC):
+    """PnP RANSAC problem: n 3D-2D matches, outlier_frac
+    of them with a random image position, the rest projected by a random true
+    pose plus sigma=noise_px pixel noise; octave per match -> sigma2 = sf^(2 octave).
+
+    Returns dict(p3d[n,3] f32, p2d[n,2] f32, sigma2[n] f32, fx, fy, cx, cy, R_true, t_true, outlier[n])."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, W, H = intr["fx"], intr["fy"], intr["cx"], intr["cy"], intr["width"], intr["height"]
+    ang = rng.normal(0, 0.3, 3)
+    th = np.linalg.norm(ang)
+    k = ang / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    R = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+    t = rng.normal(0, 1.0, 3)
+    z = rng.uniform(*z_range, n)
+    u = rng.uniform(0, W, n)
+    v = rng.uniform(0, H, n)
+    Pc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], axis=1)
+    Xw = (Pc - t) @ R  # R^T (Pc - t)
+    octave = rng.integers(0, nlevels, n)
+    sigma2 = (np.float32(scale_factor) ** (2 * octave)).astype(np.float32)
+    obs = np.stack([u, v], axis=1) + rng.normal(0, noise_px, (n, 2))
+    out = rng.random(n) < outlier_frac
+    obs[out] = np.stack([rng.uniform(0, W, out.sum()), rng.uniform(0, H, out.sum())], axis=1)
+    return dict(p3d=Xw.astype(np.float32), p2d=obs.astype(np.float32), sigma2=sigma2,
+                fx=np.float32(fx), fy=np.float32(fy), cx=np.float32(cx), cy=np.float32(cy),
+                R_true=R, t_true=t, outlier=out)
