@@ -241,6 +241,20 @@ orbx_status orbx_pnp_get_params(const orbx_pnp* h, int* min_inliers, int* max_it
 orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_vals, int n_rand, int* used,
                              int* no_more, float Tcw[16], uint8_t* inliers, int* n_inliers, int* found);
 
+/* glibc rand() (random_r TYPE_3) as a copyable stream: the reference's
+ * RandomInt draws from the unseeded process rand() (seed 1).  POD state, so
+ * a caller can snapshot it. */
+typedef struct {
+  uint32_t r[34];
+  int32_t i;
+} orbx_rand_state;
+void orbx_rand_seed(orbx_rand_state* s, uint32_t seed);
+int32_t orbx_rand_next(orbx_rand_state* s);
+/* iterate() drawing from *rng and advancing it by exactly the values the
+ * reference would consume. */
+orbx_status orbx_pnp_iterate_stream(orbx_pnp* h, int n_iterations, orbx_rand_state* rng, int* no_more,
+                                    float Tcw[16], uint8_t* inliers, int* n_inliers, int* found);
+
 /* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
  * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel
  * launch of the handle is bracketed by events on its stream.

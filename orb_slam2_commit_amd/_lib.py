@@ -71,6 +71,10 @@ class PnpParams(C.Structure):
                 ("min_set", C.c_int), ("epsilon", C.c_float), ("th2", C.c_float)]
 
 
+class RandState(C.Structure):
+    _fields_ = [("r", C.c_uint32 * 34), ("i", C.c_int32)]
+
+
 # Every entry point of include/orbx.h with its ctypes signature.
 P = C.c_void_p
 SIGNATURES = {
@@ -96,6 +100,10 @@ SIGNATURES = {
     "orbx_pnp_get_params": ([P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)], C.c_int),
     "orbx_pnp_iterate": ([P, C.c_int, P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), P, P,
                           C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
+    "orbx_pnp_iterate_stream": ([P, C.c_int, C.POINTER(RandState), C.POINTER(C.c_int), P, P, C.POINTER(C.c_int),
+                                 C.POINTER(C.c_int)], C.c_int),
+    "orbx_rand_seed": ([C.POINTER(RandState), C.c_uint32], None),
+    "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "orbx_ba_destroy": ([P], C.c_int),
     "orbx_ba_run": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),

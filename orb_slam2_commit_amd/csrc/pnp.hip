@@ -951,4 +951,45 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
   return ORBX_OK;
 }
 
+void orbx_rand_seed(orbx_rand_state* s, uint32_t seed) {
+  // glibc __srandom_r: r[0] = seed (0 -> 1), r[i] = 16807 r[i-1] mod (2^31 - 1) (Schrage),
+  // r[31..33] = r[0..2], then 310 outputs discarded
+  if (!s) return;
+  int32_t r[34];
+  r[0] = (int32_t)(seed == 0 ? 1 : seed);
+  for (int i = 1; i < 31; i++) {
+    const int32_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+    int32_t word = 16807 * lo - 2836 * hi;
+    if (word < 0) word += 2147483647;
+    r[i] = word;
+  }
+  for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+  for (int i = 0; i < 34; i++) s->r[i] = (uint32_t)r[i];
+  s->i = 34;
+  for (int k = 0; k < 310; k++) (void)orbx_rand_next(s);
+}
+
+int32_t orbx_rand_next(orbx_rand_state* s) {
+  const int i = s->i;
+  const uint32_t v = s->r[(i - 31) % 34] + s->r[(i - 3) % 34];
+  s->r[i % 34] = v;
+  s->i = i + 1 >= 34 * 1024 ? i + 1 - 34 * 1000 : i + 1;  // keep the index bounded (multiple of 34)
+  return (int32_t)(v >> 1);
+}
+
+orbx_status orbx_pnp_iterate_stream(orbx_pnp* h, int n_iterations, orbx_rand_state* rng, int* no_more, float Tcw[16],
+                                    uint8_t* inliers, int* n_inliers, int* found) {
+  if (!h || !rng) return ORBX_ERR_ARG;
+  const int need = h->min_set * std::max(std::max(h->max_its - h->iterations, n_iterations), 0);
+  orbx_rand_state peek = *rng;
+  std::vector<int32_t> vals(need);
+  for (int k = 0; k < need; k++) vals[k] = orbx_rand_next(&peek);
+  int used = 0;
+  const orbx_status st =
+      orbx_pnp_iterate(h, n_iterations, vals.data(), need, &used, no_more, Tcw, inliers, n_inliers, found);
+  if (st != ORBX_OK) return st;
+  for (int k = 0; k < used; k++) (void)orbx_rand_next(rng);
+  return ORBX_OK;
+}
+
 }  // extern "C"

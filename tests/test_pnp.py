@@ -188,3 +188,46 @@ def test_gpu_pnp_round_robin_candidates(gpu):
             assert g_gpu.peek(2) == g_ora.peek(2)
     for s in gsolv:
         s.close()
+
+
+def test_capi_rand_stream_matches_libc():
+    """orbx_rand_seed/next (host code in liborbx.so, no GPU needed) == glibc rand()."""
+    import ctypes as C
+    from orb_slam2_commit_amd import _lib
+    L = _lib.lib()
+    libc = C.CDLL("libc.so.6")
+    for seed in (1, 0, 99):
+        st = _lib.RandState()
+        L.orbx_rand_seed(C.byref(st), seed)
+        libc.srand(C.c_uint(seed))
+        assert [L.orbx_rand_next(C.byref(st)) for _ in range(36000)] == [libc.rand() for _ in range(36000)]
+    libc.srand(C.c_uint(1))
+
+
+@pytest.mark.gpu
+def test_gpu_pnp_stream_api_equals_values_api(gpu):
+    import ctypes as C
+    from orb_slam2_commit_amd import PnPsolver, _lib
+    P = synth.pnp_problem(seed=5, n=400, outlier_frac=0.45, noise_px=0.5)
+    a = PnPsolver(P["p3d"], P["p2d"], P["sigma2"], P["fx"], P["fy"], P["cx"], P["cy"])
+    a.SetRansacParameters(*TRACKING_PARAMS)
+    b = PnPsolver(P["p3d"], P["p2d"], P["sigma2"], P["fx"], P["fy"], P["cx"], P["cy"])
+    b.SetRansacParameters(*TRACKING_PARAMS)
+    g = GlibcRand(1)
+    st = _lib.RandState()
+    _lib.lib().orbx_rand_seed(C.byref(st), 1)
+    for _ in range(3):
+        Ta, nma, inla, nia = a.iterate(5, g)
+        nm, ni, found = C.c_int(), C.c_int(), C.c_int()
+        T = np.zeros(16, np.float32)
+        inl = np.zeros(a.n, np.uint8)
+        assert _lib.lib().orbx_pnp_iterate_stream(b._h, 5, C.byref(st), C.byref(nm), _lib.ptr(T), _lib.ptr(inl),
+                                                  C.byref(ni), C.byref(found)) == 0
+        assert bool(found.value) == (Ta is not None) and bool(nm.value) == nma and ni.value == nia
+        if Ta is not None:
+            np.testing.assert_array_equal(T.reshape(4, 4), Ta)
+            np.testing.assert_array_equal(inl.astype(bool), inla)
+        probe = _lib.RandState.from_buffer_copy(st)
+        assert _lib.lib().orbx_rand_next(C.byref(probe)) == g.peek(1)[0]
+    a.close()
+    b.close()

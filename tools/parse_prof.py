@@ -49,6 +49,10 @@ def main(prof_dir="gpurun_out/prof", tag="r01"):
         per_launch[k] = int(rb + wb)
         summary[k] = {"FETCH_SIZE_KiB_avg": fetch.get(k), "WRITE_SIZE_KiB_avg": write.get(k),
                       "read_bytes_corrected": int(rb), "write_bytes": int(wb)}
+    for extra in ("localba", "pnp"):
+        src = os.path.join(prof_dir, extra, "run_kernel_stats.csv")
+        if os.path.exists(src):
+            shutil.copy(src, os.path.join(out, "%s_%s_kernel_stats.csv" % (tag, extra)))
     json.dump(summary, open(os.path.join(out, "%s_pmc.json" % tag), "w"), indent=1)
     json.dump({"source": "%s_pmc.json" % tag, "per_launch_bytes": per_launch,
                "note": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per dispatch, averaged over dispatches"},
