@@ -119,25 +119,78 @@ __device__ __forceinline__ void window_to_lds(const uint8_t* base, size_t stride
 
 // ------------------------------------------------------------------ resize
 // cv::resize INTER_LINEAR 8U (OpenCV 3.2 fixed point, coefficient tables built
-// on the host exactly as resizeGeneric_ does).  One thread per output pixel.
+// on the host exactly as resizeGeneric_ does).  One block per 128x16 output
+// tile: the tile's coefficient entries go to LDS once, its source footprint
+// (rows sy0(first)..sy1(last), cols sx0(first)..sx1(last)) is staged with
+// aligned dword loads (all of a thread's loads issued before its LDS writes),
+// and each thread computes 8 consecutive outputs of one row from LDS.
 __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, const ResizeX* __restrict__ xt,
                                                const ResizeY* __restrict__ yt, BatchPtrs B, int l) {
+  extern __shared__ __align__(16) uint32_t rz_tin[];
+  __shared__ ResizeX sx[kRzTW];
+  __shared__ ResizeY sy[kRzTH];
+  __shared__ int rsh[kRzMaxRows];
   const LevelGeom& L = G->lv[l];
   const LevelGeom& S = G->lv[l - 1];
-  const int img = blockIdx.z;
-  const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (dx >= L.w || dy >= L.h) return;
+  const int img = blockIdx.z, tid = threadIdx.x;
+  const int ox0 = blockIdx.x * kRzTW, oy0 = blockIdx.y * kRzTH;
+  const int nx = min(kRzTW, L.w - ox0), ny = min(kRzTH, L.h - oy0);
+  if (tid < nx) sx[tid] = xt[L.xtab_off + ox0 + tid];
+  if (tid >= kRzTW && tid - kRzTW < ny) sy[tid - kRzTW] = yt[L.ytab_off + oy0 + tid - kRzTW];
+  __syncthreads();
   const uint8_t* src = level_ptr(*G, B, img, l - 1);
-  uint8_t* dst = B.pyr + (size_t)img * G->pyr_bytes + L.off;
-  const ResizeX X = xt[L.xtab_off + dx];
-  const ResizeY Y = yt[L.ytab_off + dy];
-  const uint8_t* r0 = src + (size_t)Y.sy0 * S.w;
-  const uint8_t* r1 = src + (size_t)Y.sy1 * S.w;
-  const int h0 = r0[X.sx0] * X.a0 + r0[X.sx1] * X.a1;
-  const int h1 = r1[X.sx0] * X.a0 + r1[X.sx1] * X.a1;
-  const int v = (((Y.b0 * (h0 >> 4)) >> 16) + ((Y.b1 * (h1 >> 4)) >> 16) + 2) >> 2;
-  dst[(size_t)dy * L.w + dx] = (uint8_t)v;
+  const uint8_t* src_end = src + (size_t)S.w * S.h;
+  const int cx0 = sx[0].sx0, span = sx[nx - 1].sx1 - cx0 + 1;
+  const int ry0 = sy[0].sy0, nrows = sy[ny - 1].sy1 - ry0 + 1;
+  const int dpr = G->rz_dpr;
+  const int total = nrows * dpr;
+  for (int q0 = 0; q0 < total; q0 += 8 * BS) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int q = q0 + k * BS + tid;
+      v[k] = 0;
+      if (q < total) {
+        const int r = q / dpr, j = q - r * dpr;
+        const uint8_t* a = src + (size_t)(ry0 + r) * S.w + cx0;
+        const int sh = (int)((uintptr_t)a & 3);
+        const uint8_t* d = a - sh + 4 * j;
+        if (4 * j < sh + span) {
+          if (d >= src && d + 4 <= src_end) {
+            v[k] = *(const uint32_t*)d;
+          } else {  // first/last dword of the level: byte loads inside it only
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+              if (d + b >= src && d + b < src_end) v[k] |= (uint32_t)d[b] << (8 * b);
+          }
+        }
+        if (j == 0) rsh[r] = sh;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int q = q0 + k * BS + tid;
+      if (q < total) rz_tin[q] = v[k];
+    }
+  }
+  __syncthreads();
+  const int r = tid >> 4, g = tid & 15;
+  if (r >= ny) return;
+  const ResizeY Y = sy[r];
+  const uint8_t* tin = (const uint8_t*)rz_tin;
+  const uint8_t* t0 = tin + (Y.sy0 - ry0) * 4 * dpr + rsh[Y.sy0 - ry0] - cx0;
+  const uint8_t* t1 = tin + (Y.sy1 - ry0) * 4 * dpr + rsh[Y.sy1 - ry0] - cx0;
+  uint8_t* dst = B.pyr + (size_t)img * G->pyr_bytes + L.off + (size_t)(oy0 + r) * L.w + ox0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int c = 8 * g + k;
+    if (c < nx) {
+      const ResizeX X = sx[c];
+      const int h0 = t0[X.sx0] * X.a0 + t0[X.sx1] * X.a1;
+      const int h1 = t1[X.sx0] * X.a0 + t1[X.sx1] * X.a1;
+      dst[c] = (uint8_t)((((Y.b0 * (h0 >> 4)) >> 16) + ((Y.b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+    }
+  }
 }
 
 // ----------------------------------------------------------------- blur
@@ -966,9 +1019,9 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
                                  int n_img, orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap,
                                  hipStream_t st, StageTimer* T) {
   for (int l = 1; l < Gh.nlevels; l++) {
-    dim3 grid((Gh.lv[l].w + 63) / 64, (Gh.lv[l].h + 3) / 4, n_img);
+    dim3 grid((Gh.lv[l].w + kRzTW - 1) / kRzTW, (Gh.lv[l].h + kRzTH - 1) / kRzTH, n_img);
     T->begin(st);
-    hipLaunchKernelGGL(k_resize, grid, dim3(BS), 0, st, Gd, xt, yt, B, l);
+    hipLaunchKernelGGL(k_resize, grid, dim3(BS), (size_t)Gh.rz_rows * Gh.rz_dpr * 4, st, Gd, xt, yt, B, l);
     T->end(ST_RESIZE, st);
   }
   if (Gh.ncells > 0) {

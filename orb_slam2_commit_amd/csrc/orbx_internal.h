@@ -44,7 +44,12 @@ struct Geometry {
   int ncells, cand_total, oct_total, max_kps, ntiles;
   int node_cap;   // octree LDS node capacity (max over levels, multiple of 64)
   int cell_cap;   // max cells in one level
+  int rz_rows;    // k_resize: max source rows staged per 128x16 output tile
+  int rz_dpr;     // k_resize: max source dwords per staged row
 };
+
+constexpr int kRzTW = 128, kRzTH = 16;  // k_resize output tile
+constexpr int kRzMaxRows = 64;
 
 struct CellInfo {
   int16_t level, pad;
