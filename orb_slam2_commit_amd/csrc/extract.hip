@@ -426,23 +426,26 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const uintptr_t a0 = (uintptr_t)base;
   const int s0 = (int)(a0 & 3), wm = lw & 3;
   {
-    const int rg = lane / 18, j = lane - rg * 18;  // 3 rows x 18 dwords per load instruction
-    uint32_t v[22];
+    // lanes = (row, dword) with dpr dwords per row; every load is issued before any LDS write
+    const int dpr = (TW + 6) / 4 + 1;
+    const int rpi = 64 / dpr, rg = lane / dpr, j = lane - rg * dpr;
+    constexpr int KMAX = (kMaxCell + 6 + 3) / 4 + 1;  // rows per lane at the smallest rpi (dpr <= 19 -> rpi >= 3)
+    uint32_t v[KMAX];
 #pragma unroll
-    for (int k = 0; k < 22; k++) {
-      const int r = 3 * k + rg;
+    for (int k = 0; k < KMAX; k++) {
+      const int r = rg + k * rpi;
       const int sr = (s0 + r * wm) & 3;
       v[k] = 0;
-      if (rg < 3 && r < TH && 4 * j < sr + TW) {
+      if (rg < rpi && r < TH && 4 * j < sr + TW) {
         const uintptr_t ar = a0 + (uintptr_t)r * lw;
         v[k] = *((const uint32_t*)(ar & ~(uintptr_t)3) + j);
       }
     }
 #pragma unroll
-    for (int k = 0; k < 22; k++) {
-      const int r = 3 * k + rg;
+    for (int k = 0; k < KMAX; k++) {
+      const int r = rg + k * rpi;
       const int sr = (s0 + r * wm) & 3;
-      if (rg < 3 && r < TH && 4 * j < sr + TW) *(uint32_t*)&tile_raw[r * S + s0 - sr + 4 + 4 * j] = v[k];
+      if (rg < rpi && r < TH && 4 * j < sr + TW) *(uint32_t*)&tile_raw[r * S + s0 - sr + 4 + 4 * j] = v[k];
     }
   }
   const uint8_t* tile = tile_raw + 4 + s0;  // pixel (r, col) = tile[r*S + col]
@@ -454,34 +457,40 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255);
   const int tlo = min(ini, mint);
   const uint64_t lt = lanemask_lt();
-  // 2. compass quick test, row-major compaction; rows_per = 2 when W <= 32
+  // 2. compass quick test, row-major compaction; rows_per = 2 when W <= 32.
+  //    Branchless: coordinates are clamped into the region and the validity
+  //    is a ballot, so the reads of all QU row groups are in flight together;
+  //    the 8 comparisons are wave masks combined with scalar 64-bit logic, and
+  //    the pass mask is the compaction ballot itself.
   const int rows_per = W <= 32 ? 2 : 1;
   const int ly = W <= 32 ? (lane >> 5) : 0, lx = W <= 32 ? (lane & 31) : lane;
+  const int lxc = min(lx, W - 1);
   int n = 0;
-  constexpr int QU = 4;  // row groups per iteration: all their LDS reads in flight together
+  constexpr int QU = 4;
   for (int y0r = 0; y0r < H; y0r += QU * rows_per) {
-    bool pass[QU];
+    int cv[QU], c0[QU], c4[QU], c8[QU], c12[QU];
 #pragma unroll
     for (int u = 0; u < QU; u++) {
-      const int y = y0r + u * rows_per + ly;
-      pass[u] = false;
-      if (lx < W && y < H) {
-        const uint8_t* t = &tile[(y + 3) * S + lx + 3];
-        const int v = t[0];
-        const int c0 = t[3 * S], c4 = t[3], c8 = t[-3 * S], c12 = t[-3];
-        const uint32_t dk = (uint32_t)(c0 < v - tlo) | (uint32_t)(c4 < v - tlo) << 1 |
-                            (uint32_t)(c8 < v - tlo) << 2 | (uint32_t)(c12 < v - tlo) << 3;
-        const uint32_t bk = (uint32_t)(c0 > v + tlo) | (uint32_t)(c4 > v + tlo) << 1 |
-                            (uint32_t)(c8 > v + tlo) << 2 | (uint32_t)(c12 > v + tlo) << 3;
-        const uint32_t dr = (dk >> 1) | ((dk & 1) << 3), br = (bk >> 1) | ((bk & 1) << 3);
-        pass[u] = ((dk & dr) | (bk & br)) != 0;
-      }
+      const int y = min(y0r + u * rows_per + ly, H - 1);
+      const uint8_t* t = &tile[(y + 3) * S + lxc + 3];
+      cv[u] = t[0];
+      c0[u] = t[3 * S];
+      c4[u] = t[3];
+      c8[u] = t[-3 * S];
+      c12[u] = t[-3];
     }
 #pragma unroll
     for (int u = 0; u < QU; u++) {
       const int y = y0r + u * rows_per + ly;
-      const uint64_t m = __ballot(pass[u]);
-      if (pass[u]) list[n + __popcll(m & lt)] = (uint16_t)((y << 6) | lx);
+      const int dlo = cv[u] - tlo, dhi = cv[u] + tlo;
+      const uint64_t k0 = __ballot(c0[u] < dlo), k4 = __ballot(c4[u] < dlo), k8 = __ballot(c8[u] < dlo),
+                     k12 = __ballot(c12[u] < dlo);
+      const uint64_t b0 = __ballot(c0[u] > dhi), b4 = __ballot(c4[u] > dhi), b8 = __ballot(c8[u] > dhi),
+                     b12 = __ballot(c12[u] > dhi);
+      const uint64_t ok = __ballot(lx < W && y < H);
+      const uint64_t m = (((k0 & k4) | (k4 & k8) | (k8 & k12) | (k12 & k0)) |
+                          ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0))) & ok;
+      if ((m >> lane) & 1) list[n + __popcll(m & lt)] = (uint16_t)((y << 6) | lx);
       n += __popcll(m);
     }
   }
