@@ -149,6 +149,7 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
   G.min_th = p.min_th_fast;
   long long pyr = 0, blur = 0;
   int cand = 0, oct = 0, ntiles = 0, node_cap = 64, cell_cap = 1;
+  int fast_wmax = 1, fast_hmax = 1;
   P.cells.clear();
   P.tile_level.clear();
   P.xt.clear();
@@ -195,6 +196,8 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
           if (c.x1 < c.x0 || c.y1 < c.y0) continue;
           const int cw = c.x1 - c.x0 + 1, ch = c.y1 - c.y0 + 1;
           if (cw > 60 || ch > 60) return ORBX_ERR_SIZE;  // k_fast LDS tile bound
+          fast_wmax = std::max(fast_wmax, cw);
+          fast_hmax = std::max(fast_hmax, ch);
           c.cap = ((cw + 1) / 2) * ((ch + 1) / 2);
           c.cand_off = cand;
           cand += c.cap;
@@ -258,6 +261,14 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
       }
     }
   }
+  // k_fast LDS layout for the largest cell: tile rows H+6 at stride <= sbase+3
+  // (window dwords land at byte s0 - sr + 4 + 4j <= 7 + 4*((W+12)/4 + 1)), score
+  // map H x maps, compass list W*H u16
+  G.fast_sbase = (fast_wmax + 6 + 18 + 3) & ~3;
+  G.fast_maps = (fast_wmax + 3) & ~3;
+  G.fast_tile_bytes = ((fast_hmax + 6) * (G.fast_sbase + 3) + 8 + 15) & ~15;
+  G.fast_map_bytes = (fast_hmax * G.fast_maps + 15) & ~15;
+  G.fast_smem = G.fast_tile_bytes + G.fast_map_bytes + 2 * fast_wmax * fast_hmax;
   // k_resize staging bound: source footprint of every 128x16 output tile
   G.rz_rows = 1;
   G.rz_dpr = 1;

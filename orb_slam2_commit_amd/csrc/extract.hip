@@ -331,8 +331,6 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
 //   4. NMS at iniThFAST -> count; 5. NMS at the chosen threshold -> ballot-ranked
 //      row-major writes
 constexpr int kMaxCell = 60;          // wCell,hCell <= 60 (checked on the host)
-constexpr int kTileMaxS = 79;         // LDS tile row stride in [76,79], == level stride (mod 4)
-constexpr int kMapS = 64;             // score-map row stride
 
 typedef short short2v __attribute__((ext_vector_type(2)));
 
@@ -409,11 +407,24 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+#ifndef FAST_STOP
+#define FAST_STOP 0
+#endif
+#define FAST_EXIT(nn, dep)                                                        \
+  if (FAST_STOP == (nn)) {                                                      \
+    const int dv = (dep);                                                       \
+    if (lane == 0) B.cell_count[(size_t)img * G->ncells + cell] = dv == 0x7fffffff ? 1 : 0; \
+    return;                                                                     \
+  }
 __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B) {
-  __shared__ __align__(16) uint8_t tile_raw[(kMaxCell + 6) * kTileMaxS + 8];
-  __shared__ uint8_t smap[kMaxCell * kMapS];
-  __shared__ uint16_t list[kMaxCell * kMaxCell];
+  // dynamic LDS sized by the plan's largest cell (G->fast_*): occupancy is what
+  // hides this kernel's LDS/ballot latency chains
+  extern __shared__ __align__(16) uint8_t fast_smem[];
+  uint8_t* tile_raw = fast_smem;
+  uint8_t* smap = fast_smem + G->fast_tile_bytes;
+  uint16_t* list = (uint16_t*)(fast_smem + G->fast_tile_bytes + G->fast_map_bytes);
+  const int kMapS = G->fast_maps;
   const int cell = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
   const CellInfo c = cells[cell];
   const int lw = G->lv[c.level].w;
@@ -422,7 +433,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   // 1. window -> LDS.  With S == lw (mod 4) the aligned global dword j of row r
   //    lands on an aligned LDS dword, so pixel (r, col) sits at r*S + s0 + col
   //    for every row (s0 = alignment of the window's first byte).
-  const int S = 76 + ((lw - 76) & 3);
+  const int S = G->fast_sbase + ((lw - G->fast_sbase) & 3);
   const uintptr_t a0 = (uintptr_t)base;
   const int s0 = (int)(a0 & 3), wm = lw & 3;
   {
@@ -454,6 +465,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     for (int i = lane; i < H * kMapS / 4; i += 64) m32[i] = 0;
   }
   __syncthreads();
+  FAST_EXIT(1, tile[lane])
   const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255);
   const int tlo = min(ini, mint);
   const uint64_t lt = lanemask_lt();
@@ -495,6 +507,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     }
   }
   __syncthreads();
+  FAST_EXIT(2, n + list[lane])
   // 3a. full segment test on the compass list; corners compacted in place
   int nc = 0;
   for (int i0 = 0; i0 < n; i0 += 64) {
@@ -511,6 +524,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     nc += __popcll(m);
   }
   __syncthreads();
+  FAST_EXIT(3, nc + list[lane])
   // 3b. cornerScore on the corners only; score map holds S+1
   for (int i0 = 0; i0 < nc; i0 += 64) {
     const int i = i0 + lane;
@@ -539,6 +553,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     }
     return true;
   };
+  FAST_EXIT(4, smap[lane] + smap[lane + 64] + smap[lane + 128] + nc)
   // 4. survivors at iniThFAST
   int cnt = 0;
   for (int i0 = 0; i0 < nc; i0 += 64) {
@@ -547,6 +562,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     cnt += __popcll(__ballot(k));
   }
   const int thr = (cnt > 0 ? ini : mint) + 1;
+  FAST_EXIT(5, thr)
   // 5. row-major writes at the chosen threshold
   uint32_t* out = B.cand + (size_t)img * G->cand_total + c.cand_off;
   int pos = 0;
@@ -1035,7 +1051,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   }
   if (Gh.ncells > 0) {
     T->begin(st);
-    hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(64), 0, st, Gd, cells, B);
+    hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(64), Gh.fast_smem, st, Gd, cells, B);
     T->end(ST_FAST, st);
   } else {
     (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
