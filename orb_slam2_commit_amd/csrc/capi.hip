@@ -265,9 +265,9 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
   // (window dwords land at byte s0 - sr + 4 + 4j <= 7 + 4*((W+12)/4 + 1)), score
   // map H x maps, compass list W*H u16
   G.fast_sbase = (fast_wmax + 6 + 18 + 3) & ~3;
-  G.fast_maps = (fast_wmax + 3) & ~3;
+  G.fast_maps = (fast_wmax + 2 + 3) & ~3;  // one zero column each side
   G.fast_tile_bytes = ((fast_hmax + 6) * (G.fast_sbase + 3) + 8 + 15) & ~15;
-  G.fast_map_bytes = (fast_hmax * G.fast_maps + 15) & ~15;
+  G.fast_map_bytes = ((fast_hmax + 2) * G.fast_maps + 15) & ~15;  // one zero row each side
   G.fast_smem = G.fast_tile_bytes + G.fast_map_bytes + 2 * fast_wmax * fast_hmax;
   // k_resize staging bound: source footprint of every 128x16 output tile
   G.rz_rows = 1;

@@ -462,7 +462,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const uint8_t* tile = tile_raw + 4 + s0;  // pixel (r, col) = tile[r*S + col]
   {
     uint32_t* m32 = (uint32_t*)smap;
-    for (int i = lane; i < H * kMapS / 4; i += 64) m32[i] = 0;
+    for (int i = lane; i < (H + 2) * kMapS / 4; i += 64) m32[i] = 0;  // zero border included
   }
   __syncthreads();
   FAST_EXIT(1, tile[lane])
@@ -531,34 +531,31 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     if (i < nc) {
       const int pix = list[i];
       const int sc = ring_score(&tile[((pix >> 6) + 3) * S + (pix & 63) + 3], S);
-      smap[(pix >> 6) * kMapS + (pix & 63)] = (uint8_t)(sc + 1);
+      smap[((pix >> 6) + 1) * kMapS + (pix & 63) + 1] = (uint8_t)(sc + 1);
     }
   }
   __syncthreads();
+  // strict NMS inside the region; the map's zero border stands for "outside"
   auto keep = [&](int pix, int thr) -> bool {  // thr = t + 1 in map units (S + 1)
-    const int y = pix >> 6, x = pix & 63;
-    const int s = smap[y * kMapS + x];
-    if (s < thr || s <= 1) return false;
-#pragma unroll
-    for (int dy = -1; dy <= 1; dy++) {
-      const int yy = y + dy;
-      if (yy < 0 || yy >= H) continue;
-#pragma unroll
-      for (int dx = -1; dx <= 1; dx++) {
-        const int xx = x + dx;
-        if ((dx == 0 && dy == 0) || xx < 0 || xx >= W) continue;
-        const int nv = smap[yy * kMapS + xx];
-        if (nv >= thr && nv >= s) return false;
-      }
-    }
-    return true;
+    const uint8_t* m = smap + ((pix >> 6) + 1) * kMapS + (pix & 63) + 1;
+    const int s = m[0];
+    const int n0 = m[-kMapS - 1], n1 = m[-kMapS], n2 = m[-kMapS + 1], n3 = m[-1], n4 = m[1], n5 = m[kMapS - 1],
+              n6 = m[kMapS], n7 = m[kMapS + 1];
+    auto beats = [&](int nv) { return nv >= thr && nv >= s; };
+    const bool lost = beats(n0) | beats(n1) | beats(n2) | beats(n3) | beats(n4) | beats(n5) | beats(n6) | beats(n7);
+    return s >= thr && s > 1 && !lost;
   };
-  FAST_EXIT(4, smap[lane] + smap[lane + 64] + smap[lane + 128] + nc)
-  // 4. survivors at iniThFAST
+  FAST_EXIT(4, smap[lane + kMapS + 1] + smap[lane + 64] + smap[lane + 128] + nc)
+  // 4. survivors at iniThFAST (verdict kept in bit 15 of the list entry)
   int cnt = 0;
   for (int i0 = 0; i0 < nc; i0 += 64) {
     const int i = i0 + lane;
-    const bool k = i < nc && keep(list[i], ini + 1);
+    bool k = false;
+    if (i < nc) {
+      const int pix = list[i];
+      k = keep(pix, ini + 1);
+      if (k) list[i] = (uint16_t)(pix | 0x8000);
+    }
     cnt += __popcll(__ballot(k));
   }
   const int thr = (cnt > 0 ? ini : mint) + 1;
@@ -571,15 +568,17 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     int pix = 0;
     bool k = false;
     if (i < nc) {
-      pix = list[i];
-      k = keep(pix, thr);
+      const int e = list[i];
+      pix = e & 0x7FFF;
+      k = cnt > 0 ? (e >> 15) != 0 : keep(pix, thr);  // at iniThFAST the verdict is already known
     }
     const uint64_t m = __ballot(k);
     if (k) {
       const int p = pos + __popcll(m & lt);
       const int y = pix >> 6, x = pix & 63;
       if (p < c.cap)
-        out[p] = ((uint32_t)(smap[y * kMapS + x] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) | (uint32_t)(c.x0 + x);
+        out[p] = ((uint32_t)(smap[(y + 1) * kMapS + x + 1] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) |
+                 (uint32_t)(c.x0 + x);
     }
     pos += __popcll(m);
   }
