@@ -318,6 +318,8 @@ struct orbx_extractor {
   DevBuf<int32_t> counts;
   // stereo scratch
   DevBuf<uint64_t> rkeys;
+  DevBuf<int2> rxi;
+  DevBuf<uint32_t> rtab;
   DevBuf<int> oct_start, sad;
   DevBuf<float> uR, depth;
   DevBuf<int32_t> nmatch, nbuf;
@@ -572,6 +574,8 @@ static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_fram
   auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
   chk(h->rkeys.ensure((size_t)n_frames * kMaxStereoKps));
   chk(h->oct_start.ensure((size_t)n_frames * (kMaxLevelsPlan + 1)));
+  chk(h->rxi.ensure((size_t)n_frames * kMaxStereoKps));
+  chk(h->rtab.ensure((size_t)n_frames * P->G.nlevels * std::max(P->G.height, 1)));
   chk(h->sad.ensure((size_t)n_frames * out_stride));
   if (e != hipSuccess) return ORBX_ERR_HIP;
   StereoArgs A;
@@ -605,6 +609,9 @@ static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_fram
   A.out_stride = out_stride;
   A.rkeys = h->rkeys.p;
   A.oct_start = h->oct_start.p;
+  A.rxi = h->rxi.p;
+  A.rtab = h->rtab.p;
+  A.rows = std::max(P->G.height, 1);
   A.nmatches = nmatches;
   return hip_status(launch_stereo(A, P->dG.p, n_frames, maxL, st, &h->timer));
 }

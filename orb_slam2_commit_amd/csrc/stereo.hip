@@ -23,8 +23,14 @@ constexpr int SBS = 256;
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
 
-__global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A) {
+// Sorts the right keypoints by (octave, y) and builds, per (octave, row Y), the
+// candidate range [start, end) of right keypoints whose band
+// [floor(y - 2 s_o), ceil(y + 2 s_o)] contains Y -- the reference's
+// vRowIndices[Y] (src/Frame.cc:572-590) split by octave, in iR order within
+// equal y.  Also writes (x, index) in sorted order for the match kernel.
+__global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometry* __restrict__ G) {
   __shared__ uint64_t keys[kMaxStereoKps];
+  __shared__ int ost[kMaxLevelsPlan + 1];
   const int f = blockIdx.x, tid = threadIdx.x;
   const int nR = min(A.nR[(size_t)f * A.n_stride_R], kMaxStereoKps);
   const orbx_keypoint* kR = A.kpR + (size_t)f * A.kR_stride;
@@ -55,7 +61,13 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A) {
     }
   }
   uint64_t* out = A.rkeys + (size_t)f * kMaxStereoKps;
-  for (int i = tid; i < nR; i += SBS) out[i] = keys[i];
+  int2* rxi = A.rxi + (size_t)f * kMaxStereoKps;
+  for (int i = tid; i < nR; i += SBS) {
+    const uint64_t k = keys[i];
+    out[i] = k;
+    const int idx = (int)(k & 0xFFF);
+    rxi[i] = make_int2(__float_as_int(kR[idx].x), idx);
+  }
   // octave starts
   int* os = A.oct_start + (size_t)f * (kMaxLevelsPlan + 1);
   for (int o = tid; o <= A.nlevels; o += SBS) {
@@ -65,32 +77,41 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A) {
       if ((int)(keys[mid] >> 44) < o) lo = mid + 1; else hi = mid;
     }
     os[o] = lo;
+    ost[o] = lo;
+  }
+  __syncthreads();
+  // row table: first with ceil(y + r) >= Y, then first (from there) with floor(y - r) > Y
+  uint32_t* tab = A.rtab + (size_t)f * A.nlevels * A.rows;
+  for (int e = tid; e < A.nlevels * A.rows; e += SBS) {
+    const int o = e / A.rows, Y = e - o * A.rows;
+    const float r = 2.0f * G->lv[o].scale;
+    const int lo = ost[o], hi = ost[o + 1];
+    int a = lo, b = hi;
+    while (a < b) {
+      const int m = (a + b) >> 1;
+      if ((int)__builtin_ceilf(__uint_as_float((uint32_t)(keys[m] >> 12)) + r) >= Y) b = m; else a = m + 1;
+    }
+    int c = a, d = hi;
+    while (c < d) {
+      const int m = (c + d) >> 1;
+      if ((int)__builtin_floorf(__uint_as_float((uint32_t)(keys[m] >> 12)) - r) > Y) d = m; else c = m + 1;
+    }
+    tab[e] = (uint32_t)a | ((uint32_t)c << 16);
   }
 }
 
 constexpr int kKpsPerBlock = 128;
 
+// No LDS: candidate ranges come from the row table, (x, index) pairs from the
+// sorted array, so occupancy is bounded by registers only.
 __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
-  __shared__ float ry[kMaxStereoKps];
-  __shared__ float rx[kMaxStereoKps];
-  __shared__ int16_t ridx[kMaxStereoKps];
-  __shared__ int ost[kMaxLevelsPlan + 1];
   const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
   const int base = blockIdx.x * kKpsPerBlock;
   if (base >= nL) return;
-  const int nR = min(A.nR[(size_t)f * A.n_stride_R], kMaxStereoKps);
   const orbx_keypoint* kR = A.kpR + (size_t)f * A.kR_stride;
-  const uint64_t* keys = A.rkeys + (size_t)f * kMaxStereoKps;
-  for (int i = tid; i < nR; i += SBS) {
-    const uint64_t k = keys[i];
-    const int idx = (int)(k & 0xFFF);
-    ry[i] = __uint_as_float((uint32_t)(k >> 12));
-    ridx[i] = (int16_t)idx;
-    rx[i] = kR[idx].x;
-  }
-  for (int o = tid; o <= G->nlevels; o += SBS) ost[o] = A.oct_start[(size_t)f * (kMaxLevelsPlan + 1) + o];
-  __syncthreads();
+  const int2* rxi = A.rxi + (size_t)f * kMaxStereoKps;
+  const uint32_t* tab = A.rtab + (size_t)f * A.nlevels * A.rows;
   const orbx_keypoint* kL = A.kpL + (size_t)f * A.kL_stride;
   const uint8_t* dL = A.dL + (size_t)f * A.kL_stride * 32;
   const uint8_t* dR = A.dR + (size_t)f * A.kR_stride * 32;
@@ -111,28 +132,17 @@ __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geomet
       *outS = -1;
     }
     if (maxU < 0) continue;
-    // candidate ranges per octave
+    // candidate ranges per octave (vRowIndices[vL], octaves levelL-1..levelL+1)
     int rb[3], re[3];
+#pragma unroll
     for (int q = 0; q < 3; q++) {
       rb[q] = re[q] = 0;
       const int o = levelL - 1 + q;
-      if (o < 0 || o >= nl) continue;
-      const float r = 2.0f * G->lv[o].scale;
-      int lo = ost[o], hi = ost[o + 1];
-      // first with ceil(y + r) >= Y
-      int a = lo, b = hi;
-      while (a < b) {
-        const int m = (a + b) >> 1;
-        if ((int)__builtin_ceilf(ry[m] + r) >= Y) b = m; else a = m + 1;
+      if (o >= 0 && o < nl && Y >= 0 && Y < A.rows) {
+        const uint32_t t = tab[(size_t)o * A.rows + Y];
+        rb[q] = (int)(t & 0xFFFF);
+        re[q] = (int)(t >> 16);
       }
-      // first (from a) with floor(y - r) > Y
-      int c = a, d = hi;
-      while (c < d) {
-        const int m = (c + d) >> 1;
-        if ((int)__builtin_floorf(ry[m] - r) > Y) d = m; else c = m + 1;
-      }
-      rb[q] = a;
-      re[q] = c;
     }
     const int n0 = re[0] - rb[0], n1 = re[1] - rb[1], n2 = re[2] - rb[2];
     const int K = n0 + n1 + n2;
@@ -144,9 +154,10 @@ __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geomet
     uint32_t best = 0xFFFFFFFFu;
     for (int j = lane; j < K; j += 64) {
       const int pos = j < n0 ? rb[0] + j : (j < n0 + n1 ? rb[1] + (j - n0) : rb[2] + (j - n0 - n1));
-      const float uR = rx[pos];
+      const int2 xi = rxi[pos];
+      const float uR = __int_as_float(xi.x);
       if (!(uR >= minU && uR <= maxU)) continue;
-      const int idx = ridx[pos];
+      const int idx = xi.y;
       const uint64_t* p = (const uint64_t*)(dR + (size_t)idx * 32);
       uint64_t rd[4] = {p[0], p[1], p[2], p[3]};
       const int dist = hamming256(ld, rd);
@@ -178,21 +189,38 @@ __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geomet
     const int lw = Lv.w;
     const int cy = (int)scaledvL, cxL = (int)scaleduL, cxR0 = (int)scaleduR0;
     int part = 0;
-    if (lane < 55) {
-      const int inc = lane % 11 - L;
-      const int g = lane / 11;
-      const int cL = imL[(size_t)cy * lw + cxL];
+    {
+      // lanes 0..54: inc = lane % 11, rows g, g+5, g+10 (g = lane / 11); branchless so that
+      // every patch load of the lane is in flight together (rows >= 11 clamped and masked)
+      const int ll = lane < 55 ? lane : 0;
+      const int inc = ll % 11 - L;
+      const int g = ll / 11;
       const int cx = cxR0 + inc;
+      const int cL = imL[(size_t)cy * lw + cxL];
       const int cR = imR[(size_t)cy * lw + cx];
-      for (int dy = g; dy < 2 * w + 1; dy += 5) {
+      int pv[3][2 * w + 1], qv[3][2 * w + 1];
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int dy = min(g + 5 * k, 2 * w);
         const uint8_t* pl = imL + (size_t)(cy - w + dy) * lw + cxL - w;
         const uint8_t* pr = imR + (size_t)(cy - w + dy) * lw + cx - w;
 #pragma unroll
         for (int dx = 0; dx < 2 * w + 1; dx++) {
-          const int a = (int)pl[dx] - cL, c = (int)pr[dx] - cR;
-          part += a > c ? a - c : c - a;
+          pv[k][dx] = pl[dx];
+          qv[k][dx] = pr[dx];
         }
       }
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        int rowsad = 0;
+#pragma unroll
+        for (int dx = 0; dx < 2 * w + 1; dx++) {
+          const int a = pv[k][dx] - cL, c = qv[k][dx] - cR;
+          rowsad += a > c ? a - c : c - a;
+        }
+        part += (g + 5 * k < 2 * w + 1) ? rowsad : 0;
+      }
+      if (lane >= 55) part = 0;
     }
     const int src = lane < 11 ? lane : 0;
     int sad = __shfl(part, src, 64) + __shfl(part, src + 11, 64) + __shfl(part, src + 22, 64) +
@@ -313,7 +341,7 @@ __global__ __launch_bounds__(SBS) void k_hamming(const uint8_t* __restrict__ a, 
 hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st,
                          StageTimer* T) {
   T->begin(st);
-  hipLaunchKernelGGL(k_stereo_prep, dim3(n_frames), dim3(SBS), 0, st, A);
+  hipLaunchKernelGGL(k_stereo_prep, dim3(n_frames), dim3(SBS), 0, st, A, Gd);
   T->end(ST_STEREO_PREP, st);
   const int nb = (maxL + kKpsPerBlock - 1) / kKpsPerBlock;
   T->begin(st);
