@@ -206,15 +206,17 @@ __device__ __forceinline__ int reflect101(int p, int n) {
   return p;
 }
 
-// Tile of kBlurTileW x kBlurTileH outputs per 256-thread block.  Input tile
-// col 0 = x0-4 so that every 4-output group reads 3 aligned LDS dwords; row
-// sums (<= 257*255 = 65535) are packed u16; outputs go out as aligned dwords
-// (blurred rows are padded to a 16-byte stride).
+// Tile of kBlurTileW x kBlurTileH (128 x 128) outputs per 256-thread block.
+// Input tile col 0 = x0-4 so that every 4-output group reads 3 aligned LDS
+// dwords.  Thread = 4 columns x a 16-row strip: row sums are computed straight
+// from the input tile into a 7-row register window that slides down the strip
+// (no row-sum buffer in LDS), outputs go out as aligned dwords (blurred rows
+// are padded to a 16-byte stride).
 constexpr int kBIn = kBlurTileW + 8;  // input tile row stride (bytes)
+constexpr int kBStrip = 16;           // output rows per thread
 __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
                                              BatchPtrs B) {
   __shared__ __align__(16) uint8_t tin[(kBlurTileH + 6) * kBIn];
-  __shared__ __align__(16) uint16_t trow[(kBlurTileH + 6) * kBlurTileW];
   const int tile = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
   const int l = tile_level[tile];
   const LevelGeom& L = G->lv[l];
@@ -227,8 +229,8 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
   // input tile: rows y0-3 .. y0+H+2, cols x0-4 .. x0+W+3 (REFLECT_101 at the borders)
   constexpr int TR = kBlurTileH + 6;
   if (interior) {
-    // 70 rows x 36 dwords / 256 threads <= 10 loads per thread
-    window_to_lds<10>(src + (size_t)(y0 - 3) * w + (x0 - 4), w, TR, kBIn, tin, kBIn, tid, BS);
+    // 134 rows x 36 dwords / 256 threads <= 19 loads per thread
+    window_to_lds<19>(src + (size_t)(y0 - 3) * w + (x0 - 4), w, TR, kBIn, tin, kBIn, tid, BS);
   } else {
     for (int q0 = 0; q0 < TR * kBIn; q0 += 8 * BS) {
       uint8_t v[8];
@@ -249,10 +251,13 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
     }
   }
   __syncthreads();
+  const int g = tid & (kBlurTileW / 4 - 1);
+  const int ys = (tid / (kBlurTileW / 4)) * kBStrip;  // strip's first output row in the tile
+  const int xg = x0 + 4 * g;
+  if (xg >= w || y0 + ys >= h) return;
   const int k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
-  // row pass: 4 outputs per task from 3 aligned dwords
-  for (int q = tid; q < TR * (kBlurTileW / 4); q += BS) {
-    const int ty = q / (kBlurTileW / 4), g = q - ty * (kBlurTileW / 4);
+  // row sums (<= 257*255) of output cols xg..xg+3 on tile row ty
+  auto rowsum = [&](int ty, int (&o)[4]) {
     const uint32_t* r32 = (const uint32_t*)&tin[ty * kBIn + 4 * g];
     const uint32_t a = r32[0], b = r32[1], c = r32[2];
     int p[12];
@@ -262,54 +267,39 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
       p[4 + i] = (b >> (8 * i)) & 255;
       p[8 + i] = (c >> (8 * i)) & 255;
     }
-    uint32_t o[2];
 #pragma unroll
-    for (int j = 0; j < 4; j += 2) {
-      // output col 4g+j needs tile cols 4g+j+1 .. 4g+j+7
-      const int s0 = k3 * p[j + 4] + k2 * (p[j + 3] + p[j + 5]) + k1 * (p[j + 2] + p[j + 6]) + k0 * (p[j + 1] + p[j + 7]);
-      const int s1 = k3 * p[j + 5] + k2 * (p[j + 4] + p[j + 6]) + k1 * (p[j + 3] + p[j + 7]) + k0 * (p[j + 2] + p[j + 8]);
-      o[j >> 1] = (uint32_t)s0 | ((uint32_t)s1 << 16);
-    }
-    *(uint2*)&trow[ty * kBlurTileW + 4 * g] = make_uint2(o[0], o[1]);
-  }
-  __syncthreads();
-  // column pass: 4 columns x 8 rows per thread
-  const int g = tid & (kBlurTileW / 4 - 1);
-  const int rg = tid / (kBlurTileW / 4);
-  const int xg = x0 + 4 * g;
-  if (xg >= w) return;
+    for (int j = 0; j < 4; j++)  // output col 4g+j needs tile cols 4g+j+1 .. 4g+j+7
+      o[j] = k3 * p[j + 4] + k2 * (p[j + 3] + p[j + 5]) + k1 * (p[j + 2] + p[j + 6]) + k0 * (p[j + 1] + p[j + 7]);
+  };
+  int win[7][4];
+#pragma unroll
+  for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
   const int simd_w = w & ~3;
-  int col[14][4];
 #pragma unroll
-  for (int r = 0; r < 14; r++) {
-    const uint2 v = *(const uint2*)&trow[(rg * 8 + r) * kBlurTileW + 4 * g];
-    col[r][0] = v.x & 0xFFFF;
-    col[r][1] = v.x >> 16;
-    col[r][2] = v.y & 0xFFFF;
-    col[r][3] = v.y >> 16;
-  }
+  for (int r = 0; r < kBStrip; r++) {
+    rowsum(ys + r + 6, win[6]);
+    const int y = y0 + ys + r;
+    if (y < h) {
+      uint32_t packed = 0;
 #pragma unroll
-  for (int r = 0; r < 8; r++) {
-    const int y = y0 + rg * 8 + r;
-    if (y >= h) break;
-    uint32_t packed = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int acc = k3 * col[r + 3][j] + k2 * (col[r + 2][j] + col[r + 4][j]) + k1 * (col[r + 1][j] + col[r + 5][j]) +
-                      k0 * (col[r][j] + col[r + 6][j]);
-      int v;
-      if (xg + j < simd_w)
-        v = (int)__builtin_rintf((float)acc * (1.0f / 65536.0f));
-      else
-        v = (acc + (1 << 15)) >> 16;
-      packed |= (uint32_t)min(max(v, 0), 255) << (8 * j);
+      for (int j = 0; j < 4; j++) {
+        const int acc = k3 * win[3][j] + k2 * (win[2][j] + win[4][j]) + k1 * (win[1][j] + win[5][j]) +
+                        k0 * (win[0][j] + win[6][j]);
+        // SSE2 groups: rint(acc / 2^16) (ties to even; acc >= 2^24 saturates either way); tail: (acc + 2^15) >> 16
+        const int v = (xg + j < simd_w) ? (acc + 0x7FFF + ((acc >> 16) & 1)) >> 16 : (acc + (1 << 15)) >> 16;
+        packed |= (uint32_t)min(v, 255) << (8 * j);
+      }
+      uint8_t* d = dst + (size_t)y * bs + xg;
+      if (xg + 4 <= w) {
+        *(uint32_t*)d = packed;
+      } else {
+        for (int j = 0; j < w - xg; j++) d[j] = (uint8_t)(packed >> (8 * j));
+      }
     }
-    uint8_t* d = dst + (size_t)y * bs + xg;
-    if (xg + 4 <= w) {
-      *(uint32_t*)d = packed;
-    } else {
-      for (int j = 0; j < w - xg; j++) d[j] = (uint8_t)(packed >> (8 * j));
-    }
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) win[i][j] = win[i + 1][j];
   }
 }
 

@@ -69,7 +69,7 @@ struct ResizeY {
   int16_t b0, b1;
 };
 
-constexpr int kBlurTileW = 128, kBlurTileH = 64;
+constexpr int kBlurTileW = 128, kBlurTileH = 128;
 
 // Device pointers for one batch.
 struct BatchPtrs {
