@@ -397,15 +397,6 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-#ifndef FAST_STOP
-#define FAST_STOP 0
-#endif
-#define FAST_EXIT(nn, dep)                                                        \
-  if (FAST_STOP == (nn)) {                                                      \
-    const int dv = (dep);                                                       \
-    if (lane == 0) B.cell_count[(size_t)img * G->ncells + cell] = dv == 0x7fffffff ? 1 : 0; \
-    return;                                                                     \
-  }
 __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B) {
   // dynamic LDS sized by the plan's largest cell (G->fast_*): occupancy is what
@@ -455,7 +446,6 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     for (int i = lane; i < (H + 2) * kMapS / 4; i += 64) m32[i] = 0;  // zero border included
   }
   __syncthreads();
-  FAST_EXIT(1, tile[lane])
   const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255);
   const int tlo = min(ini, mint);
   const uint64_t lt = lanemask_lt();
@@ -497,7 +487,6 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     }
   }
   __syncthreads();
-  FAST_EXIT(2, n + list[lane])
   // 3a. full segment test on the compass list; corners compacted in place
   int nc = 0;
   for (int i0 = 0; i0 < n; i0 += 64) {
@@ -514,7 +503,6 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     nc += __popcll(m);
   }
   __syncthreads();
-  FAST_EXIT(3, nc + list[lane])
   // 3b. cornerScore on the corners only; score map holds S+1
   for (int i0 = 0; i0 < nc; i0 += 64) {
     const int i = i0 + lane;
@@ -535,7 +523,6 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     const bool lost = beats(n0) | beats(n1) | beats(n2) | beats(n3) | beats(n4) | beats(n5) | beats(n6) | beats(n7);
     return s >= thr && s > 1 && !lost;
   };
-  FAST_EXIT(4, smap[lane + kMapS + 1] + smap[lane + 64] + smap[lane + 128] + nc)
   // 4. survivors at iniThFAST (verdict kept in bit 15 of the list entry)
   int cnt = 0;
   for (int i0 = 0; i0 < nc; i0 += 64) {
@@ -549,7 +536,6 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     cnt += __popcll(__ballot(k));
   }
   const int thr = (cnt > 0 ? ini : mint) + 1;
-  FAST_EXIT(5, thr)
   // 5. row-major writes at the chosen threshold
   uint32_t* out = B.cand + (size_t)img * G->cand_total + c.cand_off;
   int pos = 0;
