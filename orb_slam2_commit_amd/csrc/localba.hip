@@ -616,7 +616,7 @@ __device__ inline double readlane_d(double v, int l) {
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
-constexpr int kLdltMaxNp = 512;                 // padded size limit (y: 8 registers per lane)
+constexpr int kLdltMaxNp = 1024;                // padded size limit (panel buffer Np x 17 doubles in LDS)
 constexpr int kLdltLdsNp = 128;                 // largest padded size kept in LDS
 inline int ldlt_np(int N) { return (N + 15) & ~15; }
 inline size_t ldlt_smem_bytes(int N, bool lds) {
@@ -638,69 +638,6 @@ inline size_t ldlt_smem_bytes(int N, bool lds) {
 // the vector in registers.  kLds: A in LDS (row stride Np+1), else in the
 // global scratch D.Sw (row stride Np).  A template parameter, not a runtime
 // select, so that LDS accesses are ds_* and not FLAT instructions.
-// L z = b, z /= D, L^T x = z on one wave; lane owns rows lane + 64 q held in
-// registers, broadcasts via readlane.  Loads are unconditional (clamped
-// rows) and the next column's values are fetched one step ahead.
-template <int NQ>
-__device__ inline void ldlt_solve_wave(const double* A, int ld, int N, int Np, const double* b, double* x) {
-  const int lane = threadIdx.x & 63;
-  double y[NQ];
-  int row[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    const int i = lane + 64 * q;
-    row[q] = i < Np ? i : Np - 1;
-    y[q] = i < N ? b[i] : 0.0;
-  }
-  double a[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; q++) a[q] = A[(size_t)row[q] * ld];
-  for (int k = 0; k < Np; k++) {
-    double an[NQ];
-    const int kn = k + 1 < Np ? k + 1 : k;
-#pragma unroll
-    for (int q = 0; q < NQ; q++) an[q] = A[(size_t)row[q] * ld + kn];
-    double yk = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; q++)
-      if (q == (k >> 6)) yk = readlane_d(y[q], k & 63);
-#pragma unroll
-    for (int q = 0; q < NQ; q++) {
-      const int i = lane + 64 * q;
-      const double t = y[q] - a[q] * yk;
-      y[q] = i > k ? t : y[q];
-      a[q] = an[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < NQ; q++) y[q] /= A[(size_t)row[q] * ld + row[q]];
-  // backward: row i of L (contiguous) against lanes k < i
-#pragma unroll
-  for (int q = 0; q < NQ; q++) a[q] = A[(size_t)(Np - 1) * ld + (lane + 64 * q < Np ? lane + 64 * q : 0)];
-  for (int i = Np - 1; i >= 0; i--) {
-    double an[NQ];
-    const int in = i > 0 ? i - 1 : 0;
-#pragma unroll
-    for (int q = 0; q < NQ; q++) an[q] = A[(size_t)in * ld + (lane + 64 * q < Np ? lane + 64 * q : 0)];
-    double xi = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; q++)
-      if (q == (i >> 6)) xi = readlane_d(y[q], i & 63);
-#pragma unroll
-    for (int q = 0; q < NQ; q++) {
-      const int k = lane + 64 * q;
-      const double t = y[q] - a[q] * xi;
-      y[q] = k < i ? t : y[q];
-      a[q] = an[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    const int i = lane + 64 * q;
-    if (i < N) x[i] = y[q];
-  }
-}
-
 #define LDLT_TS(idx)                                                  \
   do {                                                                \
     if (D.dbg && tid == 0 && (idx) < 64) D.dbg[idx] = __builtin_amdgcn_s_memtime(); \
@@ -816,18 +753,63 @@ __global__ __launch_bounds__(1024) void k_ba_ldlt(BaDev D, int stage_limit) {
     for (int k = tid & 31; k < i; k += 32) A[(size_t)i * ld + k] /= A[(size_t)k * ld + k];
   __syncthreads();
   LDLT_TS(60);
-  if (wv != 0 || stage_limit == 3) return;
-  switch ((Np + 63) >> 6) {
-    case 1: ldlt_solve_wave<1>(A, ld, N, Np, D.bs, D.xp); break;
-    case 2: ldlt_solve_wave<2>(A, ld, N, Np, D.bs, D.xp); break;
-    case 3: ldlt_solve_wave<3>(A, ld, N, Np, D.bs, D.xp); break;
-    case 4: ldlt_solve_wave<4>(A, ld, N, Np, D.bs, D.xp); break;
-    case 5: ldlt_solve_wave<5>(A, ld, N, Np, D.bs, D.xp); break;
-    case 6: ldlt_solve_wave<6>(A, ld, N, Np, D.bs, D.xp); break;
-    case 7: ldlt_solve_wave<7>(A, ld, N, Np, D.bs, D.xp); break;
-    default: ldlt_solve_wave<8>(A, ld, N, Np, D.bs, D.xp); break;
+  if (stage_limit == 3) return;
+  // blocked triangular solves with the vector in LDS (the panel buffer P is
+  // free now): per 16-row panel wave 0 solves the small triangle in registers
+  // (readlane broadcasts), then every thread updates the remaining rows
+  double* yv = P;
+  for (int i = tid; i < Np; i += 1024) yv[i] = i < N ? D.bs[i] : 0.0;
+  __syncthreads();
+  for (int j0 = 0; j0 < Np; j0 += 16) {  // L z = b (unit lower)
+    if (wv == 0) {
+      const int r = lane & 15;
+      double Lr[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) Lr[c] = A[(size_t)(j0 + r) * ld + j0 + c];
+      double val = yv[j0 + r];
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const double zc = readlane_d(val, c);
+        if (r > c) val -= Lr[c] * zc;
+      }
+      if (lane < 16) yv[j0 + r] = val;
+    }
+    __syncthreads();
+    for (int i = j0 + 16 + tid; i < Np; i += 1024) {
+      double sacc = yv[i];
+#pragma unroll
+      for (int c = 0; c < 16; c++) sacc -= A[(size_t)i * ld + j0 + c] * yv[j0 + c];
+      yv[i] = sacc;
+    }
+    __syncthreads();
   }
-  if (lane == 0) D.scal[2] = 1.0;
+  for (int i = tid; i < Np; i += 1024) yv[i] /= A[(size_t)i * ld + i];
+  __syncthreads();
+  for (int j0 = Np - 16; j0 >= 0; j0 -= 16) {  // L^T x = z
+    if (wv == 0) {
+      const int r = lane & 15;
+      double Lc[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) Lc[c] = A[(size_t)(j0 + c) * ld + j0 + r];
+      double val = yv[j0 + r];
+#pragma unroll
+      for (int c = 15; c >= 0; c--) {
+        const double xc = readlane_d(val, c);
+        if (r < c) val -= Lc[c] * xc;
+      }
+      if (lane < 16) yv[j0 + r] = val;
+    }
+    __syncthreads();
+    for (int i = tid; i < j0; i += 1024) {
+      double sacc = yv[i];
+#pragma unroll
+      for (int c = 0; c < 16; c++) sacc -= A[(size_t)(j0 + c) * ld + i] * yv[j0 + c];
+      yv[i] = sacc;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < N; i += 1024) D.xp[i] = yv[i];
+  if (tid == 0) D.scal[2] = 1.0;
   LDLT_TS(61);
 }
 
@@ -1037,7 +1019,13 @@ struct LocalBA {
   // Active set of a phase: SparseOptimizer::initializeOptimization(level) +
   // buildIndexMapping; point-major positions (stable counting sort), pose
   // groups, Schur pair blocks (c1 <= c2; pairs ordered by point).
+  double t_struct[4] = {0, 0, 0, 0};  // host ms: index/CSR, pose groups, pair blocks, upload+alloc
   orbx_status build_structure(int lvl, hipStream_t st) {
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto T0 = now();
     const int nc = D.nc, np = D.np, ne = D.ne;
     auto on = [&](int e) { return lvl < 0 || level[e] == lvl; };
     cnt.assign(np + 1, 0);
@@ -1074,6 +1062,7 @@ struct LocalBA {
       if (on(e)) act[cnt[e_pt[e]]++] = e;  // stable: ascending edge order per point
     for (int i = 0; i < npa; i++)
       for (int k = pt_off[i]; k < pt_off[i + 1]; k++) pos_pt[k] = i;
+    const auto T1 = now();
     // positions grouped by pose (stable)
     pcam.resize(na);
     cam_off.assign(nposes + 1, 0);
@@ -1089,6 +1078,7 @@ struct LocalBA {
       for (int k = 0; k < na; k++)
         if (pcam[k] >= 0) cam_pos[fill[pcam[k]]++] = k;
     }
+    const auto T2 = now();
     // pair blocks: count, compact (empty off-diagonal blocks dropped), scatter
     blk_map.assign((size_t)nposes * nposes, 0);
     for (int i = 0; i < npa; i++)
@@ -1124,6 +1114,7 @@ struct LocalBA {
           if (c2 >= c1) pairs[blk_map[(size_t)c1 * nposes + c2]++] = make_int2(k1, k2);
         }
       }
+    const auto T3 = now();
     // one upload
     const size_t nb = blk_cc.size();
     hipError_t he = struct_arena.reserve(arena_bytes(
@@ -1177,6 +1168,11 @@ struct LocalBA {
     D.S = c.S.p;
     D.dmax_p = c.dmax_p.p;
     D.dmax_c = c.dmax_p.p + npa;  // contiguous: one max-reduction for lambda init
+    const auto T4 = now();
+    t_struct[0] += ms(T0, T1);
+    t_struct[1] += ms(T1, T2);
+    t_struct[2] += ms(T2, T3);
+    t_struct[3] += ms(T3, T4);
     return ORBX_OK;
   }
 
@@ -1284,6 +1280,7 @@ struct LocalBA {
 orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, const volatile int* stop,
                          hipStream_t st) {
   L.trials = 0;
+  for (double& t : L.t_struct) t = 0;
   BaDev& D = L.D;
   double host_build_ms = 0;
   const auto t_start = std::chrono::steady_clock::now();
@@ -1449,9 +1446,12 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   if (res->Xw_d) BA_CHECK(hipMemcpyAsync(res->Xw_d, c.Xw_d_out.p, 3 * sizeof(double) * np, hipMemcpyDeviceToHost, st));
   BA_CHECK(hipStreamSynchronize(st));
   if (std::getenv("ORBX_BA_TRACE"))
-    std::fprintf(stderr, "[orbx_ba] total %.3f ms, host structure %.3f ms, iterations %d+%d, trials %d\n",
+    std::fprintf(stderr,
+                 "[orbx_ba] total %.3f ms, host structure %.3f ms (index %.3f, poses %.3f, pairs %.3f, upload %.3f), "
+                 "iterations %d+%d, trials %d\n",
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(),
-                 host_build_ms, res->iterations[0], res->iterations[1], res->trials);
+                 host_build_ms, L.t_struct[0], L.t_struct[1], L.t_struct[2], L.t_struct[3], res->iterations[0],
+                 res->iterations[1], res->trials);
   return ORBX_OK;
 }
 
