@@ -8,15 +8,20 @@
 //   k_ba_linearize   linearizeOplus + constructQuadraticForm per active edge:
 //                    Hpl_e = B^T W A, point (Hll,bl) and pose (Hpp,bp) terms
 //   k_ba_point_sum   Hll, bl per point (fixed edge order)
-//   k_ba_cam_sum     Hpp, bp per pose (fixed edge order)
+//   k_ba_cam_sum     Hpp, bp per pose: chunk partials (pose lists split over blocks)
+//   k_ba_cam_fin     chunk partials -> Hpp, bp, max |Hpp_jj| (chunk order)
 //   per trial:
 //   k_ba_point_schur D = Hll + lambda I, Dinv (cofactor inverse), BD_e = Hpl_e Dinv, cf_e = Hpl_e Dinv bl
-//   k_ba_pairs       Hschur block (c1,c2) = [c1==c2](Hpp+lambda I) - sum_points BD_e1 Hpl_e2^T
-//                    (one wave per block, fixed lane partition + tree: deterministic)
-//   k_ba_cam_coef    bschur = bp - sum_e cf_e
+//   k_ba_pairs       chunk partials of sum_points BD_e1 Hpl_e2^T per Hschur block
+//                    (pairs from the per-phase k_ba_pair_table) and of sum_e cf_e per pose
+//   k_ba_schur_fin   S block (c1,c2) = [c1==c2](Hpp+lambda I) - pair sum; bschur = bp - sum cf
 //   k_ba_ldlt        dense LDLT of the reduced camera system in LDS, solve
-//   k_ba_backsub     x_l = Dinv (bl - sum_e Hpl_e^T x_p), X += x_l; T = exp(x_p) T; scale terms
-//   k_ba_errors      new chi -> host LM decision (one 3-double readback per trial)
+//   k_ba_update      x_l = Dinv (bl - sum_e Hpl_e^T x_p), X += x_l; T = exp(x_p) T; scale terms
+//   k_ba_errors      new chi -> host LM decision (one readback per trial; the host adds
+//                    the block partials of chi and scale in block order)
+// Every reduction has a fixed partition and order: results are run-to-run
+// identical, with no cross-block atomics (an agent-scope release/acquire per
+// block costs an L2 writeback/invalidate on the multi-XCD part).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -185,10 +190,10 @@ struct BaDev {
   int* cam_off;    // nposes+1
   int* pose_cam;   // nposes: camera id
   int nposes;
-  int* blk_off;    // nblk+1 over pair list
-  int2* blk_cc;    // nblk: (c1,c2) pose indices
-  int2* pairs;     // (k1,k2) positions
-  int nblk;
+  int* pcam;       // na: pose index of position k (-1: fixed camera)
+  int* boff;       // nblk+1: block b's slice of ptab (one slot per position of pose c1)
+  int* ptab;       // per (block, c1 position): first c2 partner k2 | more<<30, or -1
+  int nblk;        // nposes*(nposes+1)/2 upper-triangle Hschur blocks
   // per position
   double* Hpl;     // na*18 (6x3)
   double* ptc;     // na*12: Hll 9 + bl 3
@@ -210,15 +215,67 @@ struct BaDev {
   unsigned long long* dbg;  // optional phase timestamps (debug probe only)
   double* dmax_c;  // nposes
   int* pos_pt;     // na: active point index of position k
-  double* part;    // grid-reduction block partials
-  unsigned* cnt;   // grid-reduction arrival counter (reset by the last block)
+  double* gpart;   // chunk partials of the pose-list gathers (summed by the *_fin kernels)
+  int gsplit;      // chunks per pose list in the gather kernels
+  int nbe;         // k_ba_errors blocks; scal[8..] holds its block partials (2 slots), then k_ba_update's
   double* scal;    // scalars: [0] chi at iteration start, [1] chi after the trial, [2] solve ok, [3] max diag, [4] LM scale
 };
 
+// Cross-lane exchange with the partner lane for butterfly level O: xor 32 via
+// ds_bpermute, xor 16 via ds_swizzle, and the in-row levels through DPP (no
+// LDS traffic): row_mirror (i <-> 15-i), row_half_mirror (i <-> 7-i), quad
+// perms.  Each is an involution whose partner differs in bit O of the lane.
+template <int O>
+__device__ inline int xlane_i(int x) {
+  if constexpr (O == 32) return __shfl_xor(x, 32, 64);
+  else if constexpr (O == 16) return __builtin_amdgcn_ds_swizzle(x, (0x10 << 10) | 0x1F);
+  else if constexpr (O == 8) return __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false);
+  else if constexpr (O == 4) return __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);
+  else if constexpr (O == 2) return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);
+  else return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
+}
+template <int O>
+__device__ inline double xlane(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = xlane_i<O>((int)x), hi = xlane_i<O>((int)(x >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Butterfly sum of one double over the 64 lanes (every lane gets the total).
+template <int O = 32>
+__device__ inline double wave_sum(double v) {
+  v += xlane<O>(v);
+  if constexpr (O > 1) return wave_sum<O / 2>(v);
+  else return v;
+}
+
+// Reduce-scatter of M per-lane values over the wave by recursive halving: at
+// level O the lanes with bit O set keep the upper half and send the lower,
+// so only M/2 values cross lanes per level (M-1 exchanges in all instead of
+// 6M).  On exit w[0] of every lane is the wave total of value idx.
+template <int M, int O>
+__device__ inline void wave_reduce_scatter(double* w, int lane, int& idx) {
+  if constexpr (O > 0) {
+    const bool hi = (lane & O) != 0;
+    if constexpr (M > 1) {
+#pragma unroll
+      for (int i = 0; i < M / 2; i++) {
+        const double keep = hi ? w[M / 2 + i] : w[i];
+        const double send = hi ? w[i] : w[M / 2 + i];
+        w[i] = keep + xlane<O>(send);
+      }
+      if (hi) idx += M / 2;
+      wave_reduce_scatter<M / 2, O / 2>(w, lane, idx);
+    } else {
+      w[0] += xlane<O>(w[0]);
+      wave_reduce_scatter<1, O / 2>(w, lane, idx);
+    }
+  }
+}
+
 // Fixed-order block sum of one double per thread (blockDim LBS); every thread gets the result.
 __device__ inline double block_sum1(double v, double* red /* LDS [LBS/64] */) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   double s = 0;
@@ -228,32 +285,14 @@ __device__ inline double block_sum1(double v, double* red /* LDS [LBS/64] */) {
   return s;
 }
 
-// Grid-wide sum in a fixed order (block partials, then the last block to
-// arrive adds them in block order): run-to-run deterministic, one launch.
-// Must be reached by every thread of every block.
-__device__ inline void grid_sum(double v, double* part, unsigned* cnt, double* out) {
+// Block partial of a grid-wide sum: stored to out[blockIdx.x]; the host adds
+// the partials in block order after its one readback per LM trial (fixed
+// order, no cross-block synchronisation on the device).
+__device__ inline void block_partial(double v, double* out) {
   __shared__ double red[LBS / 64];
-  __shared__ int last;
   const double bs = block_sum1(v, red);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(part) + blockIdx.x, __double_as_longlong(bs),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  double s = 0;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += LBS)
-    s += __longlong_as_double(__hip_atomic_load(reinterpret_cast<unsigned long long*>(part) + b, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT));
-  s = block_sum1(s, red);
-  if (threadIdx.x == 0) {
-    *out = s;
-    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0) out[blockIdx.x] = bs;
 }
-
 
 __device__ inline void edge_error(const BaDev& D, int e, double err[3], double& chi2) {
   const int c = D.ecam[e], p = D.ept[e];
@@ -319,7 +358,7 @@ __global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute, int d
       chi = rho[0];
     }
   }
-  grid_sum(chi, D.part, D.cnt, D.scal + dst);
+  block_partial(chi, D.scal + 8 + dst * D.nbe);
 }
 
 // Deterministic sum / max of n doubles into *out (one block).
@@ -463,33 +502,54 @@ __global__ __launch_bounds__(LBS) void k_ba_point_sum(BaDev D) {
   D.dmax_p[i] = fmax(fmax(fabs(h[0]), fabs(h[4])), fabs(h[8]));
 }
 
-// Fixed-order block sum of NV per-thread partials (shuffle tree, then the
-// waves' results in wave order): deterministic for a fixed launch shape.
-template <int NV>
-__device__ inline void block_sum_fixed(double (&v)[NV], double* red /* LDS [4*NV] */) {
+// Fixed-order block sum of NV per-thread partials over a kGB-thread block
+// (shuffle tree per wave, then the waves' results summed in wave order by
+// thread j < NV): deterministic for a fixed launch shape.  Returns the NV
+// totals (in LDS, visible to the whole block).
+constexpr int kGB = 256;  // gather-block size (pose lists are split into chunks across blocks)
+constexpr int kGW = kGB / 64;
+constexpr int kPB = 256;
+template <int NV, int NW = kGW>
+__device__ inline const double* block_sum_fixed(double (&v)[NV], double* red /* LDS [(NW+1)*NV] */) {
+  static_assert(NV <= 64, "one value per lane after the reduce-scatter");
+  constexpr int P = NV <= 1 ? 1 : NV <= 2 ? 2 : NV <= 4 ? 4 : NV <= 8 ? 8 : NV <= 16 ? 16 : NV <= 32 ? 32 : 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double w[P];
 #pragma unroll
-  for (int j = 0; j < NV; j++) {
-    double x = v[j];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    v[j] = x;
-  }
-  if (lane == 0)
-#pragma unroll
-    for (int j = 0; j < NV; j++) red[wv * NV + j] = v[j];
+  for (int j = 0; j < P; j++) w[j] = j < NV ? v[j] : 0.0;
+  int idx = 0;
+  wave_reduce_scatter<P, 32>(w, lane, idx);
+  if (idx < NV && (lane & ((64 / P) - 1)) == 0) red[wv * NV + idx] = w[0];
   __syncthreads();
+  if (threadIdx.x < NV) {
+    double t = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) t += red[w * NV + threadIdx.x];
+    red[NW * NV + threadIdx.x] = t;
+  }
+  __syncthreads();
+  return red + NW * NV;
 }
 
-// Hpp, bp per pose: one 256-thread block per pose, thread t takes the pose's
-// edges t, t+256, ... ; only the upper triangle (21) + b (6) are summed.
-__global__ __launch_bounds__(256) void k_ba_cam_sum(BaDev D) {
-  __shared__ double red[4 * 27];
+// Chunk s of S of the range [lo, hi): [lo + n*s/S, lo + n*(s+1)/S).
+__device__ inline void chunk_range(int lo, int hi, int s, int S, int& a, int& b) {
+  const long long n = hi - lo;
+  a = lo + (int)(n * s / S);
+  b = lo + (int)(n * (s + 1) / S);
+}
+
+// Hpp, bp per pose: grid (pose, chunk); a chunk's threads take its positions
+// t, t+kGB, ... ; only the upper triangle (21) + b (6) are summed.  Chunk
+// partials -> gpart, summed in chunk order by k_ba_cam_fin.
+__global__ __launch_bounds__(kGB) void k_ba_cam_sum(BaDev D) {
+  __shared__ double red[(kGW + 1) * 27];
   const int ci = blockIdx.x;
   double v[27];
 #pragma unroll
   for (int j = 0; j < 27; j++) v[j] = 0;
-  for (int t = D.cam_off[ci] + threadIdx.x; t < D.cam_off[ci + 1]; t += 256) {
+  int lo, hi;
+  chunk_range(D.cam_off[ci], D.cam_off[ci + 1], blockIdx.y, gridDim.y, lo, hi);
+  for (int t = lo + threadIdx.x; t < hi; t += kGB) {
     const double* cm = D.cmc + 42 * (size_t)D.cam_pos[t];
     int j = 0;
 #pragma unroll
@@ -499,8 +559,20 @@ __global__ __launch_bounds__(256) void k_ba_cam_sum(BaDev D) {
 #pragma unroll
     for (int r = 0; r < 6; r++) v[21 + r] += cm[36 + r];
   }
-  block_sum_fixed<27>(v, red);
-  const int j = threadIdx.x;
+  const double* tot = block_sum_fixed<27>(v, red);
+  if (threadIdx.x < 27) D.gpart[((size_t)ci * gridDim.y + blockIdx.y) * 27 + threadIdx.x] = tot[threadIdx.x];
+}
+
+// One 64-thread block per pose: Hpp (symmetric), bp, max |Hpp_jj|.
+__global__ __launch_bounds__(64) void k_ba_cam_fin(BaDev D) {
+  __shared__ double tot[27];
+  const int ci = blockIdx.x, j = threadIdx.x, S = D.gsplit;
+  if (j < 27) {
+    double t = 0;
+    for (int c = 0; c < S; c++) t += D.gpart[((size_t)ci * S + c) * 27 + j];
+    tot[j] = t;
+  }
+  __syncthreads();
   if (j < 36) {
     int r = j / 6, c = j % 6;
     if (c < r) {
@@ -508,18 +580,12 @@ __global__ __launch_bounds__(256) void k_ba_cam_sum(BaDev D) {
       r = c;
       c = t;
     }
-    const int u = r * 6 - (r * (r - 1)) / 2 + (c - r);  // upper-triangle index
-    const double s = ((red[u] + red[27 + u]) + red[54 + u]) + red[81 + u];
-    D.Hpp[36 * ci + j] = s;
+    D.Hpp[36 * ci + j] = tot[r * 6 - (r * (r - 1)) / 2 + (c - r)];  // upper-triangle index
   } else if (j < 42) {
-    const int u = 21 + (j - 36);
-    D.bp[6 * ci + (j - 36)] = ((red[u] + red[27 + u]) + red[54 + u]) + red[81 + u];
+    D.bp[6 * ci + (j - 36)] = tot[21 + (j - 36)];
   } else if (j == 42) {
     double m = 0;
-    for (int r = 0; r < 6; r++) {
-      const int u = r * 6 - (r * (r - 1)) / 2;
-      m = fmax(m, fabs(((red[u] + red[27 + u]) + red[54 + u]) + red[81 + u]));
-    }
+    for (int r = 0; r < 6; r++) m = fmax(m, fabs(tot[r * 6 - (r * (r - 1)) / 2]));
     D.dmax_c[ci] = m;
   }
 }
@@ -540,7 +606,7 @@ __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) 
   inv3(Dm, Di);
   if (k == D.pt_off[i])
     for (int j = 0; j < 9; j++) D.Dinv[9 * i + j] = Di[j];
-  if (D.chidx[D.ecam[D.act[k]]] < 0) return;
+  if (D.pcam[k] < 0) return;
   const double b0 = D.bl[3 * i], b1 = D.bl[3 * i + 1], b2 = D.bl[3 * i + 2];
   double db[3];
   for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
@@ -552,59 +618,129 @@ __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) 
   }
 }
 
-// One 256-thread block per Hschur block (c1 <= c2): threads take pairs t,
-// t+256, ...; each accumulates the 6x6 block, then a fixed-order block sum.
-__global__ __launch_bounds__(256) void k_ba_pairs(BaDev D, double lambda) {
-  __shared__ double red[4 * 36];
-  const int b = blockIdx.x;
-  double acc[36];
+// Accumulates acc += BD_k1 Hpl_k2^T (6x3 * 3x6), one Hpl row at a time.
+__device__ inline void pair_acc(double acc[36], const double A[18], const double* __restrict__ h2) {
 #pragma unroll
-  for (int j = 0; j < 36; j++) acc[j] = 0;
-  for (int t = D.blk_off[b] + threadIdx.x; t < D.blk_off[b + 1]; t += 256) {
-    const int2 pr = D.pairs[t];
-    const double* bd = D.BD + 18 * (size_t)pr.x;
-    const double* h2 = D.Hpl + 18 * (size_t)pr.y;
-    double A[18], Bv[18];
+  for (int c = 0; c < 6; c++) {
+    const double b0 = h2[3 * c], b1 = h2[3 * c + 1], b2 = h2[3 * c + 2];
 #pragma unroll
-    for (int j = 0; j < 18; j++) {
-      A[j] = bd[j];
-      Bv[j] = h2[j];
-    }
-#pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-      for (int c = 0; c < 6; c++) acc[6 * r + c] += A[3 * r] * Bv[3 * c] + A[3 * r + 1] * Bv[3 * c + 1] + A[3 * r + 2] * Bv[3 * c + 2];
-  }
-  block_sum_fixed<36>(acc, red);
-  const int j = threadIdx.x;
-  if (j < 36) {
-    const double v = ((red[j] + red[36 + j]) + red[72 + j]) + red[108 + j];
-    const int2 cc = D.blk_cc[b];
-    const int N = 6 * D.nposes;
-    const int r = j / 6, c = j % 6;
-    double sv;
-    if (cc.x == cc.y) {
-      sv = D.Hpp[36 * cc.x + j] + (r == c ? lambda : 0.0) - v;
-    } else {
-      sv = -v;
-      D.S[(size_t)(6 * cc.y + c) * N + 6 * cc.x + r] = sv;
-    }
-    D.S[(size_t)(6 * cc.x + r) * N + 6 * cc.y + c] = sv;
+    for (int r = 0; r < 6; r++) acc[6 * r + c] += A[3 * r] * b0 + A[3 * r + 1] * b1 + A[3 * r + 2] * b2;
   }
 }
 
-__global__ __launch_bounds__(256) void k_ba_cam_coef(BaDev D) {
-  __shared__ double red[4 * 6];
-  const int ci = blockIdx.x;
-  double v[6] = {0, 0, 0, 0, 0, 0};
-  for (int t = D.cam_off[ci] + threadIdx.x; t < D.cam_off[ci + 1]; t += 256) {
-    const double* f = D.cf + 6 * (size_t)D.cam_pos[t];
-#pragma unroll
-    for (int r = 0; r < 6; r++) v[r] += f[r];
+__device__ inline int tri_decode(int b, int n, int& c1) {
+  c1 = 0;
+  while (b >= n - c1) {
+    b -= n - c1;
+    c1++;
   }
-  block_sum_fixed<6>(v, red);
-  const int j = threadIdx.x;
-  if (j < 6) D.bs[6 * ci + j] = D.bp[6 * ci + j] - (((red[j] + red[6 + j]) + red[12 + j]) + red[18 + j]);
+  return c1 + b;
+}
+
+// Once per phase (the structure is fixed across its LM trials): for Hschur
+// block (c1, c2) and each position k1 of pose c1 (ascending, i.e. point
+// order), the first position k2 of the same point on pose c2, flagged when
+// the point has more than one.
+__global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
+  int c1;
+  const int c2 = tri_decode(blockIdx.x, D.nposes, c1);
+  int lo, hi;
+  chunk_range(D.cam_off[c1], D.cam_off[c1 + 1], blockIdx.y, gridDim.y, lo, hi);
+  int* tab = D.ptab + D.boff[blockIdx.x] - D.cam_off[c1];
+  for (int t = lo + threadIdx.x; t < hi; t += kPB) {
+    const int i = D.pos_pt[D.cam_pos[t]];
+    const int s = D.pt_off[i], e = D.pt_off[i + 1];
+    int first = -1, more = 0;
+    for (int k2 = s; k2 < e; k2++)
+      if (D.pcam[k2] == c2) {
+        more |= first >= 0;
+        first = first < 0 ? k2 : first;
+      }
+    tab[t] = first < 0 ? -1 : (first | (more << 30));
+  }
+}
+
+// Grid (nblk + nposes, chunk).  Blocks b < nblk: Hschur block (c1 <= c2)
+// pair sum  sum BD_k1 Hpl_k2^T  over the pairs of k_ba_pair_table; thread t of
+// a chunk takes pose c1's positions t, t+kPB, ... (each thread's pairs in
+// (k1, k2) order).  Blocks b >= nblk: sum of cf over pose b - nblk's positions
+// (the Schur rhs correction).  Chunk partials -> gpart; k_ba_schur_fin sums
+// them in chunk order (deterministic).
+__global__ __launch_bounds__(kPB) void k_ba_pairs(BaDev D) {
+  __shared__ double red[(kPB / 64 + 1) * 36];
+  const int S = gridDim.y, s = blockIdx.y;
+  if ((int)blockIdx.x >= D.nblk) {
+    const int ci = blockIdx.x - D.nblk;
+    double v[6] = {0, 0, 0, 0, 0, 0};
+    int lo, hi;
+    chunk_range(D.cam_off[ci], D.cam_off[ci + 1], s, S, lo, hi);
+    for (int t = lo + threadIdx.x; t < hi; t += kPB) {
+      const double* f = D.cf + 6 * (size_t)D.cam_pos[t];
+#pragma unroll
+      for (int r = 0; r < 6; r++) v[r] += f[r];
+    }
+    const double* tot = block_sum_fixed<6, kPB / 64>(v, red);
+    if (threadIdx.x < 6)
+      D.gpart[(size_t)D.nblk * S * 36 + ((size_t)ci * S + s) * 6 + threadIdx.x] = tot[threadIdx.x];
+    return;
+  }
+  int c1;
+  const int c2 = tri_decode(blockIdx.x, D.nposes, c1);
+  double acc[36];
+#pragma unroll
+  for (int j = 0; j < 36; j++) acc[j] = 0;
+  int lo, hi;
+  chunk_range(D.cam_off[c1], D.cam_off[c1 + 1], s, S, lo, hi);
+  const int* tab = D.ptab + D.boff[blockIdx.x] - D.cam_off[c1];
+  for (int t = lo + threadIdx.x; t < hi; t += kPB) {
+    const int v = tab[t];
+    const int k1 = D.cam_pos[t];
+    if (v < 0) continue;
+    const int first = v & ((1 << 30) - 1);
+    double A[18];
+    const double* bd = D.BD + 18 * (size_t)k1;
+#pragma unroll
+    for (int j = 0; j < 18; j++) A[j] = bd[j];
+    pair_acc(acc, A, D.Hpl + 18 * (size_t)first);
+    if (v >> 30) {
+      const int e = D.pt_off[D.pos_pt[k1] + 1];
+      for (int k2 = first + 1; k2 < e; k2++)
+        if (D.pcam[k2] == c2) pair_acc(acc, A, D.Hpl + 18 * (size_t)k2);
+    }
+  }
+  const double* tot = block_sum_fixed<36, kPB / 64>(acc, red);
+  if (threadIdx.x < 36) D.gpart[((size_t)blockIdx.x * S + s) * 36 + threadIdx.x] = tot[threadIdx.x];
+}
+
+// Reduced system from the chunk partials: blocks b < nblk write Hschur block
+// (c1, c2) = [c1==c2](Hpp + lambda I) - pair sum (both triangles, so every
+// entry of S is written); blocks b >= nblk write bs = bp - sum cf.
+__global__ __launch_bounds__(64) void k_ba_schur_fin(BaDev D, double lambda) {
+  const int j = threadIdx.x, S = D.gsplit;
+  if ((int)blockIdx.x >= D.nblk) {
+    const int ci = blockIdx.x - D.nblk;
+    if (j < 6) {
+      double t = 0;
+      for (int c = 0; c < S; c++) t += D.gpart[(size_t)D.nblk * S * 36 + ((size_t)ci * S + c) * 6 + j];
+      D.bs[6 * ci + j] = D.bp[6 * ci + j] - t;
+    }
+    return;
+  }
+  if (j >= 36) return;
+  int c1;
+  const int c2 = tri_decode(blockIdx.x, D.nposes, c1);
+  double v = 0;
+  for (int c = 0; c < S; c++) v += D.gpart[((size_t)blockIdx.x * S + c) * 36 + j];
+  const int N = 6 * D.nposes;
+  const int r = j / 6, c = j % 6;
+  double sv;
+  if (c1 == c2) {
+    sv = D.Hpp[36 * c1 + j] + (r == c ? lambda : 0.0) - v;
+  } else {
+    sv = -v;
+    D.S[(size_t)(6 * c2 + c) * N + 6 * c1 + r] = sv;
+  }
+  D.S[(size_t)(6 * c1 + r) * N + 6 * c2 + c] = sv;
 }
 
 __device__ inline double readlane_d(double v, int l) {
@@ -822,7 +958,7 @@ __global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
   if (ok && i < D.npa) {
     double c[3] = {D.bl[3 * i], D.bl[3 * i + 1], D.bl[3 * i + 2]};
     for (int k = D.pt_off[i]; k < D.pt_off[i + 1]; k++) {
-      const int ci = D.chidx[D.ecam[D.act[k]]];
+      const int ci = D.pcam[k];
       if (ci < 0) continue;
       const double* B = D.Hpl + 18 * (size_t)k;
       for (int j = 0; j < 3; j++)
@@ -860,7 +996,7 @@ __global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
     D.cq[4 * c + 3] = nq.w;
     for (int r = 0; r < 3; r++) D.ct[3 * c + r] = E.t[r] + rt[r];
   }
-  grid_sum(sc, D.part, D.cnt, D.scal + 4);
+  block_partial(sc, D.scal + 8 + 2 * D.nbe);
 }
 
 __global__ __launch_bounds__(LBS) void k_ba_restore(BaDev D) {
@@ -944,8 +1080,9 @@ struct DBuf {
 };
 
 struct Ctx {
-  DBuf<double> cbak, Xbak, eerr, Hpl, ptc, cmc, BD, cf, Hll, bl, Dinv, dmax_p, Hpp, bp, xp, bs, S, Sw, scal, part;
-  DBuf<unsigned> cnt;
+  DBuf<double> cbak, Xbak, eerr, Hpl, ptc, cmc, BD, cf, Hll, bl, Dinv, dmax_p, Hpp, bp, xp, bs, S, Sw, scal, gpart;
+
+  DBuf<int> ptab;
   DBuf<uint8_t> flag;
   DBuf<float> Tcw_out, Xw_out;
   DBuf<double> Tcw_d_out, Xw_d_out;
@@ -1012,14 +1149,25 @@ struct LocalBA {
   std::vector<uint8_t> e_st, fixed;
   std::vector<uint8_t> level;  // 0/1 per edge
   int trials = 0;
+  int nbu = 1, n_rb = 8;           // k_ba_update blocks; doubles in the readback block
+  double* rb_host = nullptr;       // pinned readback block
+  int rb_cap = 0;
+  LocalBA() = default;
+  LocalBA(const LocalBA&) = delete;
+  LocalBA& operator=(const LocalBA&) = delete;
+  ~LocalBA() {
+    if (rb_host) (void)hipHostFree(rb_host);
+  }
   // host scratch, reused across calls
-  std::vector<int> act, pos_pt, chidx, pose_cam, pt_off, pt_id, cam_off, cam_pos, blk_off, cnt, pcam, blk_map;
-  std::vector<int2> blk_cc, pairs;
+  std::vector<int> act, pos_pt, chidx, pose_cam, pt_off, pt_id, cam_off, cam_pos, cnt, pcam, ccnt, boff;
 
   // Active set of a phase: SparseOptimizer::initializeOptimization(level) +
-  // buildIndexMapping; point-major positions (stable counting sort), pose
-  // groups, Schur pair blocks (c1 <= c2; pairs ordered by point).
-  double t_struct[4] = {0, 0, 0, 0};  // host ms: index/CSR, pose groups, pair blocks, upload+alloc
+  // buildIndexMapping; point-major positions, pose groups (positions
+  // ascending within each pose).  Edges arriving grouped by point (the
+  // reference adds them per MapPoint, Optimizer.cc:659-745) take the one-pass
+  // path; otherwise a stable counting sort by point.  Schur pairs are found on
+  // the device (k_ba_pairs), not listed here.
+  double t_struct[4] = {0, 0, 0, 0};  // host ms: index/CSR, pose groups, (unused), upload+alloc
   orbx_status build_structure(int lvl, hipStream_t st) {
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
@@ -1027,50 +1175,71 @@ struct LocalBA {
     };
     const auto T0 = now();
     const int nc = D.nc, np = D.np, ne = D.ne;
-    auto on = [&](int e) { return lvl < 0 || level[e] == lvl; };
-    cnt.assign(np + 1, 0);
-    chidx.assign(nc, -1);
-    for (int e = 0; e < ne; e++)
-      if (on(e)) {
-        cnt[e_pt[e] + 1]++;
-        chidx[e_cam[e]] = 0;  // used
+    const uint8_t* lv = level.data();
+    ccnt.assign(nc, 0);
+    int na = 0;
+    bool sorted = true;
+    for (int e = 0, last = -1; e < ne; e++)
+      if (lvl < 0 || lv[e] == lvl) {
+        ccnt[e_cam[e]]++;
+        na++;
+        sorted &= e_pt[e] >= last;
+        last = e_pt[e];
       }
+    chidx.assign(nc, -1);
     pose_cam.clear();
-    for (int c = 0; c < nc; c++) {
-      if (chidx[c] == 0 && !fixed[c]) {
+    cam_off.assign(1, 0);
+    for (int c = 0; c < nc; c++)
+      if (ccnt[c] && !fixed[c]) {
         chidx[c] = (int)pose_cam.size();
         pose_cam.push_back(c);
-      } else {
-        chidx[c] = -1;
+        cam_off.push_back(cam_off.back() + ccnt[c]);
       }
-    }
     const int nposes = (int)pose_cam.size();
-    pt_off.assign(1, 0);
-    pt_id.clear();
-    for (int p = 0; p < np; p++) {
-      const int n = cnt[p + 1];
-      cnt[p + 1] = cnt[p] + n;  // start of point p's positions
-      if (n) {
-        pt_id.push_back(p);
-        pt_off.push_back(cnt[p + 1]);
-      }
-    }
-    const int na = cnt[np], npa = (int)pt_id.size();
+    int maxc = 0;
+    for (int ci = 0; ci < nposes; ci++) maxc = std::max(maxc, cam_off[ci + 1] - cam_off[ci]);
+    const int gsplit = std::min(std::max((maxc + 2 * kGB - 1) / (2 * kGB), 1), 64);  // ~2 positions per thread
     act.resize(na);
     pos_pt.resize(na);
-    for (int e = 0; e < ne; e++)
-      if (on(e)) act[cnt[e_pt[e]]++] = e;  // stable: ascending edge order per point
-    for (int i = 0; i < npa; i++)
-      for (int k = pt_off[i]; k < pt_off[i + 1]; k++) pos_pt[k] = i;
-    const auto T1 = now();
-    // positions grouped by pose (stable)
     pcam.resize(na);
-    cam_off.assign(nposes + 1, 0);
-    for (int k = 0; k < na; k++) {
-      pcam[k] = chidx[e_cam[act[k]]];
-      if (pcam[k] >= 0) cam_off[pcam[k] + 1]++;
+    pt_off.clear();
+    pt_id.clear();
+    if (sorted) {
+      int k = 0;
+      for (int e = 0; e < ne; e++)
+        if (lvl < 0 || lv[e] == lvl) {
+          const int p = e_pt[e];
+          if (pt_id.empty() || pt_id.back() != p) {
+            pt_off.push_back(k);
+            pt_id.push_back(p);
+          }
+          act[k] = e;
+          pos_pt[k] = (int)pt_id.size() - 1;
+          pcam[k] = chidx[e_cam[e]];
+          k++;
+        }
+      pt_off.push_back(na);
+    } else {
+      cnt.assign(np + 1, 0);
+      for (int e = 0; e < ne; e++)
+        if (lvl < 0 || lv[e] == lvl) cnt[e_pt[e] + 1]++;
+      pt_off.push_back(0);
+      for (int p = 0; p < np; p++) {
+        const int n = cnt[p + 1];
+        cnt[p + 1] = cnt[p] + n;  // start of point p's positions
+        if (n) {
+          pt_id.push_back(p);
+          pt_off.push_back(cnt[p + 1]);
+        }
+      }
+      for (int e = 0; e < ne; e++)
+        if (lvl < 0 || lv[e] == lvl) act[cnt[e_pt[e]]++] = e;  // stable: ascending edge order per point
+      for (int i = 0; i < (int)pt_id.size(); i++)
+        for (int k = pt_off[i]; k < pt_off[i + 1]; k++) pos_pt[k] = i;
+      for (int k = 0; k < na; k++) pcam[k] = chidx[e_cam[act[k]]];
     }
-    for (int ci = 0; ci < nposes; ci++) cam_off[ci + 1] += cam_off[ci];
+    const int npa = (int)pt_id.size();
+    const auto T1 = now();
     cam_pos.resize(cam_off[nposes]);
     {
       std::vector<int>& fill = cnt;  // reuse
@@ -1079,47 +1248,15 @@ struct LocalBA {
         if (pcam[k] >= 0) cam_pos[fill[pcam[k]]++] = k;
     }
     const auto T2 = now();
-    // pair blocks: count, compact (empty off-diagonal blocks dropped), scatter
-    blk_map.assign((size_t)nposes * nposes, 0);
-    for (int i = 0; i < npa; i++)
-      for (int k1 = pt_off[i]; k1 < pt_off[i + 1]; k1++) {
-        const int c1 = pcam[k1];
-        if (c1 < 0) continue;
-        for (int k2 = pt_off[i]; k2 < pt_off[i + 1]; k2++) {
-          const int c2 = pcam[k2];
-          if (c2 >= c1) blk_map[(size_t)c1 * nposes + c2]++;
-        }
-      }
-    blk_off.assign(1, 0);
-    blk_cc.clear();
+    const auto T3 = T2;
+    boff.assign(1, 0);
     for (int c1 = 0; c1 < nposes; c1++)
-      for (int c2 = c1; c2 < nposes; c2++) {
-        int& m = blk_map[(size_t)c1 * nposes + c2];
-        const int n = m;
-        if (n == 0 && c1 != c2) {
-          m = -1;
-          continue;
-        }
-        m = blk_off.back();  // write cursor of this block
-        blk_off.push_back(blk_off.back() + n);
-        blk_cc.push_back(make_int2(c1, c2));
-      }
-    pairs.resize(blk_off.back());
-    for (int i = 0; i < npa; i++)
-      for (int k1 = pt_off[i]; k1 < pt_off[i + 1]; k1++) {
-        const int c1 = pcam[k1];
-        if (c1 < 0) continue;
-        for (int k2 = pt_off[i]; k2 < pt_off[i + 1]; k2++) {
-          const int c2 = pcam[k2];
-          if (c2 >= c1) pairs[blk_map[(size_t)c1 * nposes + c2]++] = make_int2(k1, k2);
-        }
-      }
-    const auto T3 = now();
+      for (int c2 = c1; c2 < nposes; c2++) boff.push_back(boff.back() + cam_off[c1 + 1] - cam_off[c1]);
     // one upload
-    const size_t nb = blk_cc.size();
-    hipError_t he = struct_arena.reserve(arena_bytes(
-        {4 * (size_t)na, 4 * (size_t)na, 4 * (size_t)nc, 4 * (size_t)nposes, 4 * (size_t)(npa + 1), 4 * (size_t)npa,
-         4 * (size_t)(nposes + 1), 4 * cam_pos.size(), 4 * (nb + 1), 8 * nb, 8 * pairs.size()}));
+    hipError_t he = struct_arena.reserve(arena_bytes({4 * (size_t)na, 4 * (size_t)na, 4 * (size_t)nc,
+                                                      4 * (size_t)nposes, 4 * (size_t)(npa + 1), 4 * (size_t)npa,
+                                                      4 * (size_t)(nposes + 1), 4 * cam_pos.size(), 4 * (size_t)na,
+                                                      4 * boff.size()}));
     if (he != hipSuccess) return ORBX_ERR_HIP;
     Arena& A = struct_arena;
     D.act = A.put(act);
@@ -1130,9 +1267,8 @@ struct LocalBA {
     D.pt_id = A.put(pt_id);
     D.cam_off = A.put(cam_off);
     D.cam_pos = A.put(cam_pos);
-    D.blk_off = A.put(blk_off);
-    D.blk_cc = A.put(blk_cc);
-    D.pairs = A.put(pairs);
+    D.pcam = A.put(pcam);
+    D.boff = A.put(boff);
     BA_CHECK(A.upload(st));
     const size_t N = 6 * (size_t)nposes;
     BA_CHECK(c.Hpl.alloc(18 * (size_t)na));
@@ -1152,7 +1288,27 @@ struct LocalBA {
     D.na = na;
     D.npa = npa;
     D.nposes = nposes;
-    D.nblk = (int)nb;
+    D.nblk = nposes * (nposes + 1) / 2;
+    D.gsplit = gsplit;
+    BA_CHECK(c.gpart.alloc((size_t)std::max(D.nblk * 36 + nposes * 6, nposes * 27) * gsplit));
+    D.gpart = c.gpart.p;
+    // readback block: scal[0..7], then errors partials (2 slots of nbe), then update partials
+    D.nbe = std::max((na + LBS - 1) / LBS, 1);
+    nbu = std::max((npa + nposes + LBS - 1) / LBS, 1);
+    n_rb = 8 + 2 * D.nbe + nbu;
+    BA_CHECK(c.scal.alloc(n_rb));
+    D.scal = c.scal.p;
+    if (rb_cap < n_rb) {
+      if (rb_host) (void)hipHostFree(rb_host);
+      rb_host = nullptr;
+      rb_cap = 0;
+      BA_CHECK(hipHostMalloc((void**)&rb_host, n_rb * sizeof(double), hipHostMallocDefault));
+      rb_cap = n_rb;
+    }
+    BA_CHECK(c.ptab.alloc(boff.back()));
+    D.ptab = c.ptab.p;
+    if (D.nblk > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk, gsplit), dim3(kPB), 0, st, D);
+    BA_CHECK(hipGetLastError());
     D.Hpl = c.Hpl.p;
     D.ptc = c.ptc.p;
     D.cmc = c.cmc.p;
@@ -1181,10 +1337,24 @@ struct LocalBA {
     return hipGetLastError();
   }
 
+  // One readback: out[2] ok flag, out[3] lambda-init max; out[0], out[1]
+  // (chi of the two error slots) and out[4] (LM scale) are the block
+  // partials added in block order.
   hipError_t read_scalars(double out[5], hipStream_t st) {
-    hipError_t e = hipMemcpyAsync(out, D.scal, 5 * sizeof(double), hipMemcpyDeviceToHost, st);
+    hipError_t e = hipMemcpyAsync(rb_host, D.scal, n_rb * sizeof(double), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    return e;
+    if (e != hipSuccess) return e;
+    out[2] = rb_host[2];
+    out[3] = rb_host[3];
+    const double* p = rb_host + 8;
+    double a = 0, b = 0, u = 0;
+    for (int i = 0; i < D.nbe; i++) a += p[i];
+    for (int i = 0; i < D.nbe; i++) b += p[D.nbe + i];
+    for (int i = 0; i < nbu; i++) u += p[2 * D.nbe + i];
+    out[0] = a;
+    out[1] = b;
+    out[4] = u;
+    return hipSuccess;
   }
 
   // SparseOptimizer::optimize + OptimizationAlgorithmLevenberg::solve.  One
@@ -1212,7 +1382,10 @@ struct LocalBA {
       BA_CHECK(errors(st, 1, 0));  // computeActiveErrors; activeRobustChi2 -> scal[0]
       if (D.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3(ga), dim3(LBS), 0, st, D);
       if (D.npa > 0) hipLaunchKernelGGL(k_ba_point_sum, dim3((D.npa + LBS - 1) / LBS), dim3(LBS), 0, st, D);
-      if (D.nposes > 0) hipLaunchKernelGGL(k_ba_cam_sum, dim3(D.nposes), dim3(256), 0, st, D);
+      if (D.nposes > 0) {
+        hipLaunchKernelGGL(k_ba_cam_sum, dim3(D.nposes, D.gsplit), dim3(kGB), 0, st, D);
+        hipLaunchKernelGGL(k_ba_cam_fin, dim3(D.nposes), dim3(64), 0, st, D);
+      }
       BA_CHECK(hipGetLastError());
       if (i == 0) {
         hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D.dmax_p, D.npa + D.nposes, D.scal + 3, 1);
@@ -1227,9 +1400,8 @@ struct LocalBA {
       do {
         hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, D, lambda);
         if (D.nposes > 0) {
-          BA_CHECK(hipMemsetAsync(D.S, 0, N * N * sizeof(double), st));
-          hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk), dim3(256), 0, st, D, lambda);
-          hipLaunchKernelGGL(k_ba_cam_coef, dim3(D.nposes), dim3(256), 0, st, D);
+          hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk + D.nposes, D.gsplit), dim3(kPB), 0, st, D);
+          hipLaunchKernelGGL(k_ba_schur_fin, dim3(D.nblk + D.nposes), dim3(64), 0, st, D, lambda);
           if (in_lds)
             hipLaunchKernelGGL(k_ba_ldlt<true>, dim3(1), dim3(1024), ldlt_smem, st, D, 99);
           else
@@ -1362,14 +1534,6 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   BA_CHECK(hipMemsetAsync(c.eerr.p, 0, 3 * sizeof(double) * std::max(ne, 1), st));
   BA_CHECK(c.flag.alloc(ne));
   BA_CHECK(c.scal.alloc(8));
-  // grid-reduction scratch: partials for the widest reducing launch, counter zeroed once
-  BA_CHECK(c.part.alloc((size_t)(ne + np + nc) / LBS + 16));
-  if (!c.cnt.p) {
-    BA_CHECK(c.cnt.alloc(1));
-    BA_CHECK(hipMemsetAsync(c.cnt.p, 0, sizeof(unsigned), st));
-  }
-  D.part = c.part.p;
-  D.cnt = c.cnt.p;
   D.cq = cq;
   D.ct = ct;
   D.cbak = c.cbak.p;

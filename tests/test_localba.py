@@ -174,7 +174,7 @@ def ba(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["config4", "small", "mono_only", "many_kfs", "no_outliers"])
+@pytest.mark.parametrize("case", ["config4", "small", "mono_only", "many_kfs", "no_outliers", "edges_shuffled"])
 def test_gpu_localba_matches_oracle(ba, case):
     if case == "config4":
         P = synth.localba_problem(seed=7)
@@ -184,6 +184,11 @@ def test_gpu_localba_matches_oracle(ba, case):
         P = small_problem(seed=5, th_depth=0.0)
     elif case == "many_kfs":  # 30 local KFs: reduced system 180x180 (does not fit LDS)
         P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
+    elif case == "edges_shuffled":  # edges not grouped by point: the counting-sort index path
+        P = dict(small_problem(seed=11))
+        perm = np.random.default_rng(0).permutation(len(P["edge_point"]))
+        for k in ("edge_point", "edge_cam", "obs", "inv_sigma2"):
+            P[k] = np.ascontiguousarray(np.asarray(P[k])[perm])
     else:
         P = small_problem(seed=6, outlier_frac=0.0)
     _compare(ba.LocalBundleAdjustment(P), oracle.local_ba(P))
