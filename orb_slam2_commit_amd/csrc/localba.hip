@@ -949,6 +949,229 @@ __global__ __launch_bounds__(1024) void k_ba_ldlt(BaDev D, int stage_limit) {
   LDLT_TS(61);
 }
 
+// ---- reduced camera system, small N: column-step LDLT with 4x4 tiles ----
+// Right-looking LDL^T of the augmented [S b; b^T .] with one barrier per
+// pivot (~780 cycles per pivot on gfx950, latency-bound: LDS round trip +
+// reciprocal + barrier; 60 us at N = 120 vs 71 us for the 16-wide blocked
+// kernel, whose in-wave panel factorisation is readlane/division bound).  Each thread owns TPT 4x4 tiles of the lower triangle in registers
+// (rows up to N, row N = rhs, padded to a multiple of 4).  At pivot j a tile
+// reads 4 + 4 entries of column j from LDS (two ds_read_b128 each) and does
+// 16 FMAs -- a quarter of the LDS traffic of one element per thread, which
+// is what bounds this loop.  After pivot j's update the owners of column
+// j+1 publish it (and 1/d_{j+1}) to LDS; nothing else is read from LDS.  The
+// augmented row ends as z = L^-1 b (columns are unscaled: entry (i,j) =
+// L_ij d_j), so the forward solve is free; wave 0 then applies D^-1 and the
+// backward L^T solve, prefetching column entries eight pivots at a time.  A
+// zero pivot fails the solve (scal[2] = 0) like the blocked kernel.
+//
+// LDS column j holds rows (j & ~3) .. Np4-1 at Lc[cbase(j) + i], 32-byte
+// aligned for every 4-row group.
+__host__ __device__ inline int ldlt_np4(int N) { return (N + 1 + 3) & ~3; }
+__host__ __device__ inline int ldlt_cstart(int j, int N) {  // sum_{c<j} (Np4 - (c & ~3))
+  const int q = j >> 2, r = j & 3;
+  return j * ldlt_np4(N) - (8 * q * (q - 1) + 4 * q * r);
+}
+__host__ __device__ inline int ldlt_cbase(int j, int N) { return ldlt_cstart(j, N) - (j & ~3); }
+inline int ldlt_col_tiles(int N) {
+  const int Tr = ldlt_np4(N) / 4, Tc = (N + 3) / 4;
+  return Tc * Tr - Tc * (Tc - 1) / 2;
+}
+inline size_t ldlt_col_smem(int N) { return (size_t)(ldlt_cstart(N, N) + N + 1) * sizeof(double); }
+constexpr size_t kLdltColMaxSmem = 160 * 1024 - 256;
+inline bool ldlt_col_fits(int N) { return ldlt_col_smem(N) <= kLdltColMaxSmem && ldlt_col_tiles(N) <= 2048; }
+
+typedef double double2_t __attribute__((ext_vector_type(2)));
+
+// 1/d by v_rcp_f64 + two Newton steps (full double accuracy, a third of the
+// latency of the IEEE division sequence -- it sits on the per-pivot path).
+__device__ inline double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Pivot j = 4m + U of k_ba_ldlt_col: rank-1 update of the active tiles from
+// column j, then the owners of column j+1 publish it and 1/d_{j+1}.
+template <int TPT, int U>
+__device__ __forceinline__ void ldlt_col_step(double* Lc, double* rinv, double (&a)[TPT][4][4], const int (&ti)[TPT],
+                                              const int (&tk)[TPT], int m, int N, int& fail) {
+  const int j = 4 * m + U;
+  if (j >= N) return;  // uniform
+  const double* cj = Lc + ldlt_cbase(j, N);
+  const double invd = rinv[j];
+#pragma unroll
+  for (int t = 0; t < TPT; t++) {
+    if (tk[t] >= m && !(tk[t] == m && U == 3)) {  // some column of the tile is > j
+      const double2_t* pr = reinterpret_cast<const double2_t*>(cj + 4 * ti[t]);
+      const double2_t* pk = reinterpret_cast<const double2_t*>(cj + 4 * tk[t]);
+      const double2_t r0 = pr[0], r1 = pr[1], k0 = pk[0], k1 = pk[1];
+      const double cr[4] = {r0.x, r0.y, r1.x, r1.y}, ckv[4] = {k0.x, k0.y, k1.x, k1.y};
+      double ck[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const bool live = (tk[t] > m || q > U) && 4 * tk[t] + q < N;
+        ck[q] = live ? ckv[q] * invd : 0.0;  // select: junk never propagates
+      }
+#pragma unroll
+      for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) a[t][p][q] -= cr[p] * ck[q];
+    }
+  }
+  constexpr int Q = (U + 1) & 3;  // column j+1 within its tile
+  const int mn = U == 3 ? m + 1 : m;
+  if (j + 1 < N) {
+#pragma unroll
+    for (int t = 0; t < TPT; t++) {
+      if (tk[t] == mn) {
+        double2_t* dst = reinterpret_cast<double2_t*>(Lc + ldlt_cbase(j + 1, N) + 4 * ti[t]);
+        dst[0] = double2_t{a[t][0][Q], a[t][1][Q]};
+        dst[1] = double2_t{a[t][2][Q], a[t][3][Q]};
+        if (ti[t] == tk[t]) {
+          const double dn = a[t][Q][Q];
+          rinv[j + 1] = rcp_nr(dn);
+          if (dn == 0.0) fail = 1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int TPT>
+__global__ __launch_bounds__(1024) void k_ba_ldlt_col(BaDev D) {
+  extern __shared__ __attribute__((aligned(16))) double Lc[];
+  __shared__ int fail;
+  const int N = 6 * D.nposes, tid = threadIdx.x;
+  const int Np4 = ldlt_np4(N), Tr = Np4 / 4, Tc = (N + 3) / 4;
+  const int ntiles = Tc * Tr - Tc * (Tc - 1) / 2;
+  double* rinv = Lc + ldlt_cstart(N, N);
+  double a[TPT][4][4];
+  int ti[TPT], tk[TPT];
+  if (tid == 0) fail = 0;
+#pragma unroll
+  for (int t = 0; t < TPT; t++) {
+    int x = tid + 1024 * t, k = 0;
+    ti[t] = 0;
+    tk[t] = -1;  // inactive
+    if (x < ntiles) {
+      while (x >= Tr - k) {  // column-major tile order
+        x -= Tr - k;
+        k++;
+      }
+      tk[t] = k;
+      ti[t] = k + x;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int i = 4 * ti[t] + p, kk = 4 * tk[t] + q;
+        double v = 0.0;
+        if (tk[t] >= 0 && kk < N) v = i < N ? D.S[(size_t)i * N + kk] : (i == N ? D.bs[kk] : 0.0);
+        a[t][p][q] = v;
+      }
+    if (tk[t] == 0) {
+#pragma unroll
+      for (int p = 0; p < 4; p++) Lc[ldlt_cbase(0, N) + 4 * ti[t] + p] = a[t][p][0];
+      if (ti[t] == 0) {
+        rinv[0] = rcp_nr(a[t][0][0]);
+        if (a[t][0][0] == 0.0) fail = 1;
+      }
+    }
+  }
+  __syncthreads();
+  for (int m = 0; 4 * m < N; m++) {  // pivots j = 4m + U, U unrolled so tile columns index statically
+    ldlt_col_step<TPT, 0>(Lc, rinv, a, ti, tk, m, N, fail);
+    ldlt_col_step<TPT, 1>(Lc, rinv, a, ti, tk, m, N, fail);
+    ldlt_col_step<TPT, 2>(Lc, rinv, a, ti, tk, m, N, fail);
+    ldlt_col_step<TPT, 3>(Lc, rinv, a, ti, tk, m, N, fail);
+  }
+  if (fail) {
+    if (tid == 0) D.scal[2] = 0.0;
+    return;
+  }
+  if (tid >= 64) return;
+  // y = D^-1 z; L^T x = y (x_k final at step k, rows i < k updated)
+  const int lane = tid;
+  double y[4], invd[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int i = lane + 64 * r;
+    invd[r] = 0.0;
+    y[r] = 0.0;
+    if (i < N) {
+      invd[r] = rinv[i];
+      y[r] = Lc[ldlt_cbase(i, N) + N] * invd[r];
+    }
+  }
+  int cb[4];  // column i's base; rows >= N clamp to a valid column (their Lv is zeroed)
+#pragma unroll
+  for (int r = 0; r < 4; r++) cb[r] = ldlt_cbase(min(lane + 64 * r, N - 1), N);
+  for (int kb = N - 1; kb >= 0; kb -= 8) {
+    double Lv[8][4];
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {  // branchless: all 32 LDS reads issue together
+        const int i = lane + 64 * r, k = kb - u;
+        const double v = Lc[cb[r] + (i < k ? k : min(i, N - 1))];  // always a finite L entry
+        Lv[u][r] = v * (i < k ? invd[r] : 0.0);  // L[k][i]; a multiply, so the load is unconditional
+      }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = kb - u;
+      if (k >= 0) {
+        const int rk = k >> 6;
+        const double yk = rk == 0 ? y[0] : rk == 1 ? y[1] : rk == 2 ? y[2] : y[3];
+        const double xk = readlane_d(yk, k & 63);
+#pragma unroll
+        for (int r = 0; r < 4; r++) y[r] -= Lv[u][r] * xk;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    if (lane + 64 * r < N) D.xp[lane + 64 * r] = y[r];
+  if (lane == 0) D.scal[2] = 1.0;
+}
+
+// Launch plan for the reduced system: the column-step kernel while the
+// packed factor fits LDS, else the 16-wide blocked kernel (LDS or global).
+struct LdltPlan {
+  int N = 0, tpt = 0;
+  bool col = false, in_lds = false;
+  size_t smem = 0;
+  hipError_t prepare(int n) {
+    N = n;
+    col = ldlt_col_fits(N) && !std::getenv("ORBX_LDLT_BLOCKED");
+    if (col) {
+      tpt = ldlt_col_tiles(N) <= 1024 ? 1 : 2;
+      smem = ldlt_col_smem(N);
+    } else {
+      in_lds = ldlt_np(N) <= kLdltLdsNp;
+      smem = ldlt_smem_bytes(N, in_lds);
+    }
+    return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  }
+  const void* kernel_ptr() const {
+    if (col) return tpt == 1 ? (const void*)k_ba_ldlt_col<1> : (const void*)k_ba_ldlt_col<2>;
+    return in_lds ? (const void*)k_ba_ldlt<true> : (const void*)k_ba_ldlt<false>;
+  }
+  void launch(const BaDev& D, hipStream_t st, int stage_limit = 99) const {
+    if (col) {
+      if (tpt == 1) hipLaunchKernelGGL(k_ba_ldlt_col<1>, dim3(1), dim3(1024), smem, st, D);
+      else hipLaunchKernelGGL(k_ba_ldlt_col<2>, dim3(1), dim3(1024), smem, st, D);
+    } else if (in_lds) {
+      hipLaunchKernelGGL(k_ba_ldlt<true>, dim3(1), dim3(1024), smem, st, D, stage_limit);
+    } else {
+      hipLaunchKernelGGL(k_ba_ldlt<false>, dim3(1), dim3(1024), smem, st, D, stage_limit);
+    }
+  }
+};
+
 // back-substitution + update (push first) + LM scale, skipped when the
 // solve failed (scal[2] == 0).  Threads: active points, then active poses.
 __global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
@@ -1366,15 +1589,12 @@ struct LocalBA {
     int it = 0;
     const size_t N = 6 * (size_t)D.nposes;
     if (ldlt_np((int)N) > kLdltMaxNp) return ORBX_ERR_SIZE;
-    const bool in_lds = ldlt_np((int)N) <= kLdltLdsNp;
-    const size_t ldlt_smem = ldlt_smem_bytes((int)N, in_lds);
-    if (!in_lds) {
+    LdltPlan ldlt;
+    BA_CHECK(ldlt.prepare((int)N));
+    if (!ldlt.col && !ldlt.in_lds) {
       BA_CHECK(c.Sw.alloc((size_t)ldlt_np((int)N) * ldlt_np((int)N)));
       D.Sw = c.Sw.p;
     }
-    if (hipFuncSetAttribute(in_lds ? (const void*)k_ba_ldlt<true> : (const void*)k_ba_ldlt<false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldlt_smem) != hipSuccess)
-      return ORBX_ERR_HIP;
     const int gp = std::max((D.npa + D.nposes + LBS - 1) / LBS, 1);
     const int ga = std::max((D.na + LBS - 1) / LBS, 1);
     double sc[5];
@@ -1402,10 +1622,7 @@ struct LocalBA {
         if (D.nposes > 0) {
           hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk + D.nposes, D.gsplit), dim3(kPB), 0, st, D);
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(D.nblk + D.nposes), dim3(64), 0, st, D, lambda);
-          if (in_lds)
-            hipLaunchKernelGGL(k_ba_ldlt<true>, dim3(1), dim3(1024), ldlt_smem, st, D, 99);
-          else
-            hipLaunchKernelGGL(k_ba_ldlt<false>, dim3(1), dim3(1024), ldlt_smem, st, D, 99);
+          ldlt.launch(D, st);
         }
         hipLaunchKernelGGL(k_ba_update, dim3(gp), dim3(LBS), 0, st, D, lambda);
         BA_CHECK(errors(st, 1, 1));
@@ -1706,14 +1923,12 @@ extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* 
   }
   D.dbg = ddbg;
   if (orbx::ldlt_np(N) > orbx::kLdltMaxNp) e = hipErrorInvalidValue;
-  const bool in_lds = orbx::ldlt_np(N) <= orbx::kLdltLdsNp;
-  const size_t smem = orbx::ldlt_smem_bytes(N, in_lds);
+  orbx::LdltPlan plan;
+  if (e == hipSuccess) e = plan.prepare(N);
   double* dSw = nullptr;
-  if (e == hipSuccess && !in_lds) e = hipMalloc((void**)&dSw, (size_t)orbx::ldlt_np(N) * orbx::ldlt_np(N) * sizeof(double));
+  if (e == hipSuccess && !plan.col && !plan.in_lds)
+    e = hipMalloc((void**)&dSw, (size_t)orbx::ldlt_np(N) * orbx::ldlt_np(N) * sizeof(double));
   D.Sw = dSw;
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute(in_lds ? (const void*)orbx::k_ba_ldlt<true> : (const void*)orbx::k_ba_ldlt<false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   float total = 0;
   if (e == hipSuccess) {
     (void)hipEventCreate(&e0);
@@ -1721,10 +1936,7 @@ extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* 
     for (int r = 0; r < reps && e == hipSuccess; r++) {
       e = hipMemcpy(dS, dS0, nn, hipMemcpyDeviceToDevice);
       (void)hipEventRecord(e0, nullptr);
-      if (in_lds)
-        hipLaunchKernelGGL(orbx::k_ba_ldlt<true>, dim3(1), dim3(1024), smem, nullptr, D, stage_limit);
-      else
-        hipLaunchKernelGGL(orbx::k_ba_ldlt<false>, dim3(1), dim3(1024), smem, nullptr, D, stage_limit);
+      plan.launch(D, nullptr, stage_limit);
       (void)hipEventRecord(e1, nullptr);
       if (e == hipSuccess) e = hipEventSynchronize(e1);
       float t = 0;
