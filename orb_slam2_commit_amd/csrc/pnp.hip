@@ -24,7 +24,9 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "../../include/orbx.h"
@@ -32,6 +34,11 @@
 namespace orbx {
 
 constexpr int kPnpMaxSet = 16;
+__device__ unsigned long long g_pnp_ts[32];
+#define PNP_TS(i) \
+  do {            \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_pnp_ts[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 struct PnpIn {
   const float* p3d;
@@ -56,144 +63,268 @@ __device__ inline void swap_d(double& a, double& b) {
   b = t;
 }
 
-// JacobiSVDImpl_<double> (see oracle/pnp.cpp): n rows of length m in At.
-__device__ void jacobi_svd(double* At, int astep, double* Wout, double* Vt, int vstep, int m, int n, int n1) {
-  const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
-  double W[16];
-  const int max_iter = m > 30 ? m : 30;
-  for (int i = 0; i < n; i++) {
-    double sd = 0;
-    for (int k = 0; k < m; k++) {
-      const double t = At[i * astep + k];
-      sd += t * t;
+// JacobiSVDImpl_<double> (see oracle/pnp.cpp) on N rows of length M in At
+// (row stride M), n1 = N.  Sizes are compile-time so the small systems live
+// in registers; kV = false skips the V rotations -- they never feed back into
+// At or W, so U and W are unchanged (EPnP's 12x12 SVD only reads Ut).
+// One Jacobi rotation of rows i < j (At row stride M, W the squared row
+// norms); returns false when the pair is already orthogonal (skipped).
+template <int M, int N, bool kV>
+__device__ __forceinline__ bool jacobi_rotate(double* At, double* W, double* Vt, int i, int j) {
+  const double eps = DBL_EPSILON * 10;
+  double* Ai = At + i * M;
+  double* Aj = At + j * M;
+  double a = W[i], p = 0, b = W[j];
+  double xi[M], xj[M];
+#pragma unroll
+  for (int k = 0; k < M; k++) {
+    xi[k] = Ai[k];
+    xj[k] = Aj[k];
+  }
+#pragma unroll
+  for (int k = 0; k < M; k++) p += xi[k] * xj[k];
+  if (fabs(p) <= eps * sqrt(a * b)) return false;
+  p *= 2;
+  const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+  double c, s;
+  if (beta < 0) {
+    const double delta = (gamma - beta) * 0.5;
+    s = sqrt(delta / gamma);
+    c = p / (gamma * s * 2);
+  } else {
+    c = sqrt((gamma + beta) / (gamma * 2));
+    s = p / (gamma * c * 2);
+  }
+  a = b = 0;
+#pragma unroll
+  for (int k = 0; k < M; k++) {
+    const double t0 = c * xi[k] + s * xj[k];
+    const double t1 = -s * xi[k] + c * xj[k];
+    Ai[k] = t0;
+    Aj[k] = t1;
+    a += t0 * t0;
+    b += t1 * t1;
+  }
+  W[i] = a;
+  W[j] = b;
+  if (kV) {
+    double* Vi = Vt + i * N;
+    double* Vj = Vt + j * N;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      const double t0 = c * Vi[k] + s * Vj[k];
+      const double t1 = -s * Vi[k] + c * Vj[k];
+      Vi[k] = t0;
+      Vj[k] = t1;
     }
-    W[i] = sd;
-    for (int k = 0; k < n; k++) Vt[i * vstep + k] = 0;
-    Vt[i * vstep + i] = 1;
   }
-  for (int iter = 0; iter < max_iter; iter++) {
-    bool changed = false;
-    for (int i = 0; i < n - 1; i++)
-      for (int j = i + 1; j < n; j++) {
-        double* Ai = At + i * astep;
-        double* Aj = At + j * astep;
-        double a = W[i], p = 0, b = W[j];
-        for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
-        if (fabs(p) <= eps * sqrt(a * b)) continue;
-        p *= 2;
-        const double beta = a - b, gamma = sqrt(p * p + beta * beta);
-        double c, s;
-        if (beta < 0) {
-          const double delta = (gamma - beta) * 0.5;
-          s = sqrt(delta / gamma);
-          c = p / (gamma * s * 2);
-        } else {
-          c = sqrt((gamma + beta) / (gamma * 2));
-          s = p / (gamma * c * 2);
-        }
-        a = b = 0;
-        for (int k = 0; k < m; k++) {
-          const double t0 = c * Ai[k] + s * Aj[k];
-          const double t1 = -s * Ai[k] + c * Aj[k];
-          Ai[k] = t0;
-          Aj[k] = t1;
-          a += t0 * t0;
-          b += t1 * t1;
-        }
-        W[i] = a;
-        W[j] = b;
-        changed = true;
-        double* Vi = Vt + i * vstep;
-        double* Vj = Vt + j * vstep;
-        for (int k = 0; k < n; k++) {
-          const double t0 = c * Vi[k] + s * Vj[k];
-          const double t1 = -s * Vi[k] + c * Vj[k];
-          Vi[k] = t0;
-          Vj[k] = t1;
-        }
-      }
-    if (!changed) break;
-  }
-  for (int i = 0; i < n; i++) {
+  return true;
+}
+
+// After the sweeps: singular values, descending sort (rows of At and Vt
+// swapped along), and the cv::RNG(0x12345678) completion of null rows.
+template <int M, int N, bool kV, bool kSmall>
+__device__ __forceinline__ void jacobi_tail(double* At, double* W, double* Wout, double* Vt) {
+  const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
     double sd = 0;
-    for (int k = 0; k < m; k++) {
-      const double t = At[i * astep + k];
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+      const double t = At[i * M + k];
       sd += t * t;
     }
     W[i] = sqrt(sd);
   }
-  for (int i = 0; i < n - 1; i++) {
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) {
     int j = i;
-    for (int k = i + 1; k < n; k++)
+#pragma unroll
+    for (int k = i + 1; k < N; k++)
       if (W[j] < W[k]) j = k;
     if (i != j) {
-      swap_d(W[i], W[j]);
-      for (int k = 0; k < m; k++) swap_d(At[i * astep + k], At[j * astep + k]);
-      for (int k = 0; k < n; k++) swap_d(Vt[i * vstep + k], Vt[j * vstep + k]);
+      if constexpr (kSmall) {  // W[j] with j runtime: select chains keep W in registers
+        double wj = W[i];
+#pragma unroll
+        for (int k = i + 1; k < N; k++)
+          if (k == j) wj = W[k];
+#pragma unroll
+        for (int k = i + 1; k < N; k++)
+          if (k == j) W[k] = W[i];
+        W[i] = wj;
+      } else {
+        swap_d(W[i], W[j]);
+      }
+#pragma unroll
+      for (int k = 0; k < M; k++) swap_d(At[i * M + k], At[j * M + k]);
+      if (kV) {
+#pragma unroll
+        for (int k = 0; k < N; k++) swap_d(Vt[i * N + k], Vt[j * N + k]);
+      }
     }
   }
-  for (int i = 0; i < n; i++) Wout[i] = W[i];
+  if (kSmall) {
+#pragma unroll
+    for (int i = 0; i < N; i++) Wout[i] = W[i];
+  }
   CvRng rng{0x12345678};
-  for (int i = 0; i < n1; i++) {
-    double sd = i < n ? W[i] : 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    double sd = W[i];
     for (int ii = 0; ii < 100 && sd <= minval; ii++) {
-      const double val0 = 1. / m;
-      for (int k = 0; k < m; k++) At[i * astep + k] = (rng.next() & 256) != 0 ? val0 : -val0;
+      const double val0 = 1. / M;
+#pragma unroll
+      for (int k = 0; k < M; k++) At[i * M + k] = (rng.next() & 256) != 0 ? val0 : -val0;
       for (int iter = 0; iter < 2; iter++)
         for (int j = 0; j < i; j++) {
           sd = 0;
-          for (int k = 0; k < m; k++) sd += At[i * astep + k] * At[j * astep + k];
+#pragma unroll
+          for (int k = 0; k < M; k++) sd += At[i * M + k] * At[j * M + k];
           double asum = 0;
-          for (int k = 0; k < m; k++) {
-            const double t = At[i * astep + k] - sd * At[j * astep + k];
-            At[i * astep + k] = t;
+#pragma unroll
+          for (int k = 0; k < M; k++) {
+            const double t = At[i * M + k] - sd * At[j * M + k];
+            At[i * M + k] = t;
             asum += fabs(t);
           }
           asum = asum > eps * 100 ? 1 / asum : 0;
-          for (int k = 0; k < m; k++) At[i * astep + k] *= asum;
+#pragma unroll
+          for (int k = 0; k < M; k++) At[i * M + k] *= asum;
         }
       sd = 0;
-      for (int k = 0; k < m; k++) {
-        const double t = At[i * astep + k];
+#pragma unroll
+      for (int k = 0; k < M; k++) {
+        const double t = At[i * M + k];
         sd += t * t;
       }
       sd = sqrt(sd);
     }
     const double s = sd > minval ? 1 / sd : 0.;
-    for (int k = 0; k < m; k++) At[i * astep + k] *= s;
+#pragma unroll
+    for (int k = 0; k < M; k++) At[i * M + k] *= s;
   }
 }
 
-// _SVDcompute, m >= n: left singular vectors as rows Ut (n x m), w, Vt.
-__device__ void svd_rows(const double* A, int m, int n, double* Ut, double* w, double* Vt) {
-  for (int i = 0; i < n; i++)
-    for (int k = 0; k < m; k++) Ut[i * m + k] = A[k * n + i];
-  jacobi_svd(Ut, m, w, Vt, n, m, n, n);
+// JacobiSVDImpl_<double> (see oracle/pnp.cpp) on N rows of length M in At
+// (row stride M), n1 = N, one thread.  Sizes are compile-time so the small
+// systems live in registers; kV = false skips the V rotations -- they never
+// feed back into At or W, so U and W are unchanged.
+template <int M, int N, bool kV>
+__device__ __forceinline__ void jacobi_svd(double* At, double* Wout, double* Vt) {
+  constexpr bool kSmall = N <= 6;  // else W works in Wout and the pair loops stay rolled
+  double Wreg[kSmall ? N : 1];
+  double* W = kSmall ? Wreg : Wout;
+  constexpr int max_iter = M > 30 ? M : 30;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    double sd = 0;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+      const double t = At[i * M + k];
+      sd += t * t;
+    }
+    W[i] = sd;
+    if (kV) {
+#pragma unroll
+      for (int k = 0; k < N; k++) Vt[i * N + k] = 0;
+      Vt[i * N + i] = 1;
+    }
+  }
+  for (int iter = 0; iter < max_iter; iter++) {
+    bool changed = false;
+    if constexpr (kSmall) {
+#pragma unroll
+      for (int i = 0; i < N - 1; i++)
+#pragma unroll
+        for (int j = i + 1; j < N; j++) changed |= jacobi_rotate<M, N, kV>(At, W, Vt, i, j);
+    } else {
+#pragma unroll 1
+      for (int i = 0; i < N - 1; i++)
+#pragma unroll 1
+        for (int j = i + 1; j < N; j++) changed |= jacobi_rotate<M, N, kV>(At, W, Vt, i, j);
+    }
+    if (!changed) break;
+  }
+  jacobi_tail<M, N, kV, kSmall>(At, W, Wout, Vt);
 }
 
-// SVBkSbImpl_ (b == nullptr: inverse)
-__device__ void svd_backsubst(const double* Ut, const double* w, const double* Vt, int m, int n, const double* b,
-                              double* x) {
-  const int nb = b ? 1 : m;
-  for (int i = 0; i < n * nb; i++) x[i] = 0;
+// The same SVD (no V) run by one wave on LDS data: rotation (i, j) only
+// touches rows i, j, and in the cyclic order each row's rotations come in
+// increasing i + j, so step t = i + j runs every pair (lane i, t - i) at once
+// -- disjoint rows, each row's rotations in the reference order, so the
+// result is bit-identical -- 2N-3 steps per sweep instead of N(N-1)/2.  The
+// sort and null-row completion stay on lane 0.
+template <int M, int N>
+__device__ __forceinline__ void jacobi_svd_wave(double* At, double* W) {
+  constexpr int max_iter = M > 30 ? M : 30;
+  const int lane = threadIdx.x & 63;
+  if (lane < N) {
+    double sd = 0;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+      const double t = At[lane * M + k];
+      sd += t * t;
+    }
+    W[lane] = sd;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS writes visible wave-wide
+  __builtin_amdgcn_wave_barrier();
+  for (int iter = 0; iter < max_iter; iter++) {
+    bool changed = false;
+    for (int t = 1; t <= 2 * N - 3; t++) {
+      const int j = t - lane;
+      if (lane < j && j < N) changed |= jacobi_rotate<M, N, false>(At, W, nullptr, lane, j);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (__ballot(changed) == 0) break;
+  }
+  if (lane == 0) jacobi_tail<M, N, false, false>(At, W, W, nullptr);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// _SVDcompute, m >= n: left singular vectors as rows Ut (n x m), w, Vt.
+template <int M, int N, bool kV = true>
+__device__ __forceinline__ void svd_rows(const double* A, double* Ut, double* w, double* Vt) {
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int k = 0; k < M; k++) Ut[i * M + k] = A[k * N + i];
+  jacobi_svd<M, N, kV>(Ut, w, Vt);
+}
+
+// SVBkSbImpl_ (kInv: b = identity, i.e. the inverse)
+template <int M, int N, bool kInv>
+__device__ __forceinline__ void svd_backsubst(const double* Ut, const double* w, const double* Vt, const double* b, double* x) {
+  constexpr int nb = kInv ? M : 1;
+#pragma unroll
+  for (int i = 0; i < N * nb; i++) x[i] = 0;
   double threshold = 0;
-  for (int i = 0; i < n; i++) threshold += w[i];
+#pragma unroll
+  for (int i = 0; i < N; i++) threshold += w[i];
   threshold *= DBL_EPSILON * 2;
-  double buffer[16];
-  for (int i = 0; i < n; i++) {
+#pragma unroll
+  for (int i = 0; i < N; i++) {
     double wi = w[i];
     if (fabs(wi) <= threshold) continue;
     wi = 1 / wi;
-    const double* u = Ut + i * m;
-    const double* v = Vt + i * n;
-    if (nb == 1) {
+    const double* u = Ut + i * M;
+    const double* v = Vt + i * N;
+    if (!kInv) {
       double s = 0;
-      for (int j = 0; j < m; j++) s += u[j] * b[j];
+#pragma unroll
+      for (int j = 0; j < M; j++) s += u[j] * b[j];
       s *= wi;
-      for (int j = 0; j < n; j++) x[j] = x[j] + s * v[j];
+#pragma unroll
+      for (int j = 0; j < N; j++) x[j] = x[j] + s * v[j];
     } else {
+      double buffer[nb];
+#pragma unroll
       for (int j = 0; j < nb; j++) buffer[j] = u[j] * wi;
-      for (int j = 0; j < n; j++)
+#pragma unroll
+      for (int j = 0; j < N; j++)
+#pragma unroll
         for (int k = 0; k < nb; k++) x[j * nb + k] += buffer[k] * v[j];
     }
   }
@@ -205,21 +336,23 @@ __device__ inline double dist2(const double* p1, const double* p2) {
 }
 
 // find_betas_approx_{1,2,3}, compute_L_6x10, compute_rho, gauss_newton, qr_solve
-__device__ void solve6(const double* L, int k, const double* rho, double* x) {
-  double ut[6 * 5], w[5], vt[25];
-  svd_rows(L, 6, k, ut, w, vt);
-  svd_backsubst(ut, w, vt, 6, k, rho, x);
+template <int K>
+__device__ __forceinline__ void solve6(const double* L, const double* rho, double* x) {
+  double ut[6 * K], w[K], vt[K * K];
+  svd_rows<6, K>(L, ut, w, vt);
+  svd_backsubst<6, K, false>(ut, w, vt, rho, x);
 }
 
-__device__ void find_betas_approx_1(const double* l_6x10, const double* rho, double* betas) {
+__device__ __forceinline__ void find_betas_approx_1(const double* l_6x10, const double* rho, double* betas) {
   double l_6x4[24], b4[4];
+#pragma unroll
   for (int i = 0; i < 6; i++) {
     l_6x4[4 * i] = l_6x10[10 * i];
     l_6x4[4 * i + 1] = l_6x10[10 * i + 1];
     l_6x4[4 * i + 2] = l_6x10[10 * i + 3];
     l_6x4[4 * i + 3] = l_6x10[10 * i + 6];
   }
-  solve6(l_6x4, 4, rho, b4);
+  solve6<4>(l_6x4, rho, b4);
   if (b4[0] < 0) {
     betas[0] = sqrt(-b4[0]);
     betas[1] = -b4[1] / betas[0];
@@ -233,11 +366,13 @@ __device__ void find_betas_approx_1(const double* l_6x10, const double* rho, dou
   }
 }
 
-__device__ void find_betas_approx_2(const double* l_6x10, const double* rho, double* betas) {
+__device__ __forceinline__ void find_betas_approx_2(const double* l_6x10, const double* rho, double* betas) {
   double l_6x3[18], b3[3];
+#pragma unroll
   for (int i = 0; i < 6; i++)
+#pragma unroll
     for (int j = 0; j < 3; j++) l_6x3[3 * i + j] = l_6x10[10 * i + j];
-  solve6(l_6x3, 3, rho, b3);
+  solve6<3>(l_6x3, rho, b3);
   if (b3[0] < 0) {
     betas[0] = sqrt(-b3[0]);
     betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
@@ -250,11 +385,13 @@ __device__ void find_betas_approx_2(const double* l_6x10, const double* rho, dou
   betas[3] = 0.0;
 }
 
-__device__ void find_betas_approx_3(const double* l_6x10, const double* rho, double* betas) {
+__device__ __forceinline__ void find_betas_approx_3(const double* l_6x10, const double* rho, double* betas) {
   double l_6x5[30], b5[5];
+#pragma unroll
   for (int i = 0; i < 6; i++)
+#pragma unroll
     for (int j = 0; j < 5; j++) l_6x5[5 * i + j] = l_6x10[10 * i + j];
-  solve6(l_6x5, 5, rho, b5);
+  solve6<5>(l_6x5, rho, b5);
   if (b5[0] < 0) {
     betas[0] = sqrt(-b5[0]);
     betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
@@ -267,15 +404,17 @@ __device__ void find_betas_approx_3(const double* l_6x10, const double* rho, dou
   betas[3] = 0.0;
 }
 
-__device__ void compute_L_6x10(const double* ut, double* l_6x10) {
-  const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+__device__ __forceinline__ void compute_L_6x10(const double* ut, double* l_6x10) {
   double dv[4][6][3];
+#pragma unroll
   for (int i = 0; i < 4; i++) {
+    const double* v = ut + 12 * (11 - i);
     int a = 0, b = 1;
+#pragma unroll
     for (int j = 0; j < 6; j++) {
-      dv[i][j][0] = v[i][3 * a] - v[i][3 * b];
-      dv[i][j][1] = v[i][3 * a + 1] - v[i][3 * b + 1];
-      dv[i][j][2] = v[i][3 * a + 2] - v[i][3 * b + 2];
+      dv[i][j][0] = v[3 * a] - v[3 * b];
+      dv[i][j][1] = v[3 * a + 1] - v[3 * b + 1];
+      dv[i][j][2] = v[3 * a + 2] - v[3 * b + 2];
       b++;
       if (b > 3) {
         a++;
@@ -283,6 +422,7 @@ __device__ void compute_L_6x10(const double* ut, double* l_6x10) {
       }
     }
   }
+#pragma unroll
   for (int i = 0; i < 6; i++) {
     double* row = l_6x10 + 10 * i;
     row[0] = dot3(dv[0][i], dv[0][i]);
@@ -298,80 +438,67 @@ __device__ void compute_L_6x10(const double* ut, double* l_6x10) {
   }
 }
 
-__device__ void qr_solve(double* A, double* b, double* X) {
-  const int nr = 6, nc = 4;
-  double A1[6], A2[6];
-  double* pA = A;
-  double* ppAkk = pA;
+// Householder QR solve of the 6x4 Gauss-Newton system (the reference's
+// qr_solve, pointer walks replaced by indices; same operation order).
+__device__ __forceinline__ void qr_solve(double* A, double* b, double* X) {
+  constexpr int nr = 6, nc = 4;
+  double A1[nc], A2[nc];
+#pragma unroll
   for (int k = 0; k < nc; k++) {
-    double* ppAik = ppAkk;
-    double eta = fabs(*ppAik);
+    // the reference's scan reads rows k .. nr-2 (its pointer advances after
+    // the read), so row nr-1 never enters eta -- kept as is
+    double eta = fabs(A[k * nc + k]);
+#pragma unroll
     for (int i = k + 1; i < nr; i++) {
-      const double elt = fabs(*ppAik);
+      const double elt = fabs(A[(i - 1) * nc + k]);
       if (eta < elt) eta = elt;
-      ppAik += nc;
     }
     if (eta == 0) return;
     double sum = 0.0;
     const double inv_eta = 1. / eta;
-    ppAik = ppAkk;
+#pragma unroll
     for (int i = k; i < nr; i++) {
-      *ppAik *= inv_eta;
-      sum += *ppAik * *ppAik;
-      ppAik += nc;
+      A[i * nc + k] *= inv_eta;
+      sum += A[i * nc + k] * A[i * nc + k];
     }
     double sigma = sqrt(sum);
-    if (*ppAkk < 0) sigma = -sigma;
-    *ppAkk += sigma;
-    A1[k] = sigma * *ppAkk;
+    if (A[k * nc + k] < 0) sigma = -sigma;
+    A[k * nc + k] += sigma;
+    A1[k] = sigma * A[k * nc + k];
     A2[k] = -eta * sigma;
+#pragma unroll
     for (int j = k + 1; j < nc; j++) {
-      double* p = ppAkk;
       double s = 0;
-      for (int i = k; i < nr; i++) {
-        s += *p * p[j - k];
-        p += nc;
-      }
+#pragma unroll
+      for (int i = k; i < nr; i++) s += A[i * nc + k] * A[i * nc + j];
       const double tau = s / A1[k];
-      p = ppAkk;
-      for (int i = k; i < nr; i++) {
-        p[j - k] -= tau * *p;
-        p += nc;
-      }
+#pragma unroll
+      for (int i = k; i < nr; i++) A[i * nc + j] -= tau * A[i * nc + k];
     }
-    ppAkk += nc + 1;
   }
-  double* ppAjj = pA;
+#pragma unroll
   for (int j = 0; j < nc; j++) {
-    double* ppAij = ppAjj;
     double tau = 0;
-    for (int i = j; i < nr; i++) {
-      tau += *ppAij * b[i];
-      ppAij += nc;
-    }
+#pragma unroll
+    for (int i = j; i < nr; i++) tau += A[i * nc + j] * b[i];
     tau /= A1[j];
-    ppAij = ppAjj;
-    for (int i = j; i < nr; i++) {
-      b[i] -= tau * *ppAij;
-      ppAij += nc;
-    }
-    ppAjj += nc + 1;
+#pragma unroll
+    for (int i = j; i < nr; i++) b[i] -= tau * A[i * nc + j];
   }
   X[nc - 1] = b[nc - 1] / A2[nc - 1];
+#pragma unroll
   for (int i = nc - 2; i >= 0; i--) {
-    double* ppAij = pA + i * nc + (i + 1);
     double s = 0;
-    for (int j = i + 1; j < nc; j++) {
-      s += *ppAij * X[j];
-      ppAij++;
-    }
+#pragma unroll
+    for (int j = i + 1; j < nc; j++) s += A[i * nc + j] * X[j];
     X[i] = (b[i] - s) / A2[i];
   }
 }
 
-__device__ void gauss_newton(const double* l_6x10, const double* rho, double betas[4]) {
+__device__ __forceinline__ void gauss_newton(const double* l_6x10, const double* rho, double betas[4]) {
   double a[24], b[6], x[4] = {0, 0, 0, 0};
   for (int k = 0; k < 5; k++) {
+#pragma unroll
     for (int i = 0; i < 6; i++) {
       const double* rowL = l_6x10 + i * 10;
       double* rowA = a + i * 4;
@@ -385,114 +512,163 @@ __device__ void gauss_newton(const double* l_6x10, const double* rho, double bet
                        rowL[9] * betas[3] * betas[3]);
     }
     qr_solve(a, b, x);
+#pragma unroll
     for (int i = 0; i < 4; i++) betas[i] += x[i];
   }
 }
 
-// ------------------------------------------------------------ EPnP on a group
-// Group = one thread (hypotheses) or one block (Refine).  Per-point work is
-// spread over the group; every reduction runs on one thread in point order.
-struct GroupThread {
-  __device__ int tid() const { return 0; }
-  __device__ int nt() const { return 1; }
-  __device__ void sync() const {}
-};
-struct GroupBlock {
-  __device__ int tid() const { return threadIdx.x; }
-  __device__ int nt() const { return blockDim.x; }
-  __device__ void sync() const { __syncthreads(); }
-};
+// ------------------------------------------------------------ EPnP on a block
+// One block computes one EPnP (a RANSAC hypothesis on its minimal set, or
+// Refine on the inlier set): per-point work is spread over the threads, every
+// reduction runs on thread 0 (or one thread per output) in point order, and
+// the SVDs run on thread 0 -- the reference's sequential order, so results
+// are bit-identical to the oracle.  The matrices live in LDS (EpnpSmall) and
+// so do the points when they fit (EpnpPts); M is never materialised: MtM
+// recomputes the entries of fill_M on the fly (same expressions).
 
 struct EpnpSmall {
-  double cws[4][3], ccs[4][3], ci[9], pw0tpw0[9], mtm[144], ut[144], vt[144], d[12];
+  double cws[4][3], ccs[4][3], ci[9], pw0tpw0[9], mtm[144], ut[144], d[12];
   double l_6x10[60], rho[6], betas[4][4], rep[4], Rs[4][3][3], ts[4][3];
   double pc0[3], pw0[3], abt[9];
   int flip;
 };
 
-struct EpnpWork {  // per-correspondence arrays (n entries)
-  double* alphas;  // 4n
-  double* pcs;     // 3n
-  double* M;       // 24n
-  double* tmp;     // n
+struct EpnpPts {   // per-correspondence arrays of one problem (n entries)
+  const float* pw;  // 3n
+  const float* uv;  // 2n
+  double* alphas;   // 4n
+  double* tmp;      // n
 };
 
-template <class G>
-__device__ void epnp_compute_pose(const G& g, const PnpIn& in, const int* idx, int n, EpnpSmall* S, EpnpWork W) {
-  const int tid = g.tid(), nt = g.nt();
-  auto pw = [&](int k, int j) { return (double)in.p3d[3 * idx[k] + j]; };
-  auto uv = [&](int k, int j) { return (double)in.p2d[2 * idx[k] + j]; };
+// s = ((0 + t(0)) + t(1)) + ... + t(n-1): the reference's sequential sum,
+// with the terms of each group of 8 computed (and loaded) independently so
+// their latencies overlap; only the additions form the chain.
+template <class F>
+__device__ __forceinline__ double seq_sum(int n, F term) {
+  double s = 0;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) t[u] = term(i + u);
+#pragma unroll
+    for (int u = 0; u < 8; u++) s += t[u];
+  }
+  for (; i < n; i++) s += term(i);
+  return s;
+}
+
+template <int NT>
+__device__ __forceinline__ void epnp_compute_pose(const PnpIn& in, const EpnpPts P, const int n, EpnpSmall* S) {
+  const int tid = threadIdx.x;
+  auto pw = [&](int k, int j) { return (double)P.pw[3 * k + j]; };
+  auto uv = [&](int k, int j) { return (double)P.uv[2 * k + j]; };
+  PNP_TS(0);
   // choose_control_points
-  if (tid == 0) {
-    S->cws[0][0] = S->cws[0][1] = S->cws[0][2] = 0;
-    for (int i = 0; i < n; i++)
-      for (int j = 0; j < 3; j++) S->cws[0][j] += pw(i, j);
-    for (int j = 0; j < 3; j++) S->cws[0][j] /= n;
+  if (tid < 3)  // the three coordinate sums are independent chains
+    S->cws[0][tid] = seq_sum(n, [&](int i) { return pw(i, tid); }) / n;
+  __syncthreads();
+  if (tid < 6) {
+    const int i = tid < 3 ? 0 : (tid < 5 ? 1 : 2), j = tid < 3 ? tid : (tid < 5 ? tid - 2 : 2);
+    const double ci0 = S->cws[0][i], cj0 = S->cws[0][j];
+    S->pw0tpw0[3 * i + j] = seq_sum(n, [&](int k) { return (pw(k, i) - ci0) * (pw(k, j) - cj0); });
   }
-  g.sync();
-  for (int e = tid; e < 6; e += nt) {
-    const int i = e < 3 ? 0 : (e < 5 ? 1 : 2), j = e < 3 ? e : (e < 5 ? e - 2 : 2);
-    double s = 0;
-    for (int k = 0; k < n; k++) s += (pw(k, i) - S->cws[0][i]) * (pw(k, j) - S->cws[0][j]);
-    S->pw0tpw0[3 * i + j] = s;
-  }
-  g.sync();
+  __syncthreads();
   if (tid == 0) {
-    double* P = S->pw0tpw0;
-    P[3] = P[1];
-    P[6] = P[2];
-    P[7] = P[5];
+    double P9[9];
+#pragma unroll
+    for (int e = 0; e < 9; e++) P9[e] = S->pw0tpw0[e];
+    P9[3] = P9[1];
+    P9[6] = P9[2];
+    P9[7] = P9[5];
     double uct[9], dc[3], vt[9];
-    svd_rows(P, 3, 3, uct, dc, vt);
+    svd_rows<3, 3>(P9, uct, dc, vt);
+#pragma unroll
     for (int i = 1; i < 4; i++) {
       const double k = sqrt(dc[i - 1] / n);
+#pragma unroll
       for (int j = 0; j < 3; j++) S->cws[i][j] = S->cws[0][j] + k * uct[3 * (i - 1) + j];
     }
-    double cc[9], ut[9], w[3];
+    double cc[9], ut[9], w[3], ci[9];
+#pragma unroll
     for (int i = 0; i < 3; i++)
+#pragma unroll
       for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = S->cws[j][i] - S->cws[0][i];
-    svd_rows(cc, 3, 3, ut, w, vt);
-    svd_backsubst(ut, w, vt, 3, 3, nullptr, S->ci);
+    svd_rows<3, 3>(cc, ut, w, vt);
+    svd_backsubst<3, 3, true>(ut, w, vt, nullptr, ci);
+#pragma unroll
+    for (int e = 0; e < 9; e++) S->ci[e] = ci[e];
   }
-  g.sync();
-  // compute_barycentric_coordinates + fill_M
-  for (int i = tid; i < n; i += nt) {
-    double* a = W.alphas + 4 * i;
-    const double* ci = S->ci;
+  __syncthreads();
+  PNP_TS(1);
+  // compute_barycentric_coordinates
+  for (int i = tid; i < n; i += NT) {
+    double ci[9];
+#pragma unroll
+    for (int e = 0; e < 9; e++) ci[e] = S->ci[e];
     const double p0 = pw(i, 0), p1 = pw(i, 1), p2 = pw(i, 2);
+    double a[4];
+#pragma unroll
     for (int j = 0; j < 3; j++)
       a[1 + j] = ci[3 * j] * (p0 - S->cws[0][0]) + ci[3 * j + 1] * (p1 - S->cws[0][1]) + ci[3 * j + 2] * (p2 - S->cws[0][2]);
     a[0] = 1.0f - a[1] - a[2] - a[3];
-    double* M1 = W.M + 24 * i;
-    double* M2 = M1 + 12;
-    const double u = uv(i, 0), v = uv(i, 1);
-    for (int q = 0; q < 4; q++) {
-      M1[3 * q] = a[q] * in.fu;
-      M1[3 * q + 1] = 0.0;
-      M1[3 * q + 2] = a[q] * (in.uc - u);
-      M2[3 * q] = 0.0;
-      M2[3 * q + 1] = a[q] * in.fv;
-      M2[3 * q + 2] = a[q] * (in.vc - v);
-    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) P.alphas[4 * i + j] = a[j];
   }
-  g.sync();
-  // MtM = M^T M (upper triangle sums over rows in order), mirrored
-  for (int e = tid; e < 78; e += nt) {
+  __syncthreads();
+  // MtM = M^T M, M = fill_M rows (2 per point, M1 then M2), upper triangle
+  // sums over rows in order, mirrored
+  for (int e = tid; e < 78; e += NT) {
     int i = 0, r = e;
     while (r >= 12 - i) {
       r -= 12 - i;
       i++;
     }
     const int j = i + r;
+    const int qi = i / 3, ci = i % 3, qj = j / 3, cj = j % 3;
+    // rows 2k (M1) and 2k+1 (M2) of point k, summed in row order; the fill_M
+    // entry of column c is selected branch-free (c % 3: fu / 0 / (uc - u))
+    // Branch-free: the factor is w_fu*fu + w_du*du with 0/1 weights, which is
+    // exactly fu, du or +-0 (a +-0 entry where fill_M holds +0 yields a +-0
+    // term, which never changes the sum).
+    const double i0 = ci == 0, i2 = ci == 2, j0 = cj == 0, j2 = cj == 2;
+    const double i1 = ci == 1, j1 = cj == 1;
     double s = 0;
-    for (int k = 0; k < 2 * n; k++) s += W.M[12 * k + i] * W.M[12 * k + j];
+    int k = 0;
+    for (; k + 4 <= n; k += 4) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const double ai = P.alphas[4 * (k + u) + qi], aj = P.alphas[4 * (k + u) + qj];
+        const double du = in.uc - uv(k + u, 0), dv = in.vc - uv(k + u, 1);
+        t[2 * u] = (ai * (i0 * in.fu + i2 * du)) * (aj * (j0 * in.fu + j2 * du));
+        t[2 * u + 1] = (ai * (i1 * in.fv + i2 * dv)) * (aj * (j1 * in.fv + j2 * dv));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) s += t[u];
+    }
+    for (; k < n; k++) {
+      const double ai = P.alphas[4 * k + qi], aj = P.alphas[4 * k + qj];
+      const double du = in.uc - uv(k, 0), dv = in.vc - uv(k, 1);
+      s += (ai * (i0 * in.fu + i2 * du)) * (aj * (j0 * in.fu + j2 * du));
+      s += (ai * (i1 * in.fv + i2 * dv)) * (aj * (j1 * in.fv + j2 * dv));
+    }
     S->mtm[12 * i + j] = s;
   }
-  g.sync();
+  __syncthreads();
+  PNP_TS(2);
+  if (tid < 64) {  // wave 0: Ut = MtM^T of the mirrored MtM, then the wave-parallel Jacobi
+    for (int e = tid; e < 144; e += 64) {
+      const int i = e / 12, k = e % 12;  // Ut[i][k] = MtM[k][i]; MtM[k][i] = upper (min, max)
+      S->ut[e] = S->mtm[12 * min(i, k) + max(i, k)];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    jacobi_svd_wave<12, 12>(S->ut, S->d);
+  }
+  __syncthreads();
+  PNP_TS(3);
   if (tid == 0) {
-    for (int i = 0; i < 12; i++)
-      for (int j = 0; j < i; j++) S->mtm[12 * i + j] = S->mtm[12 * j + i];
-    svd_rows(S->mtm, 12, 12, S->ut, S->d, S->vt);
     compute_L_6x10(S->ut, S->l_6x10);
     S->rho[0] = dist2(S->cws[0], S->cws[1]);
     S->rho[1] = dist2(S->cws[0], S->cws[2]);
@@ -501,70 +677,89 @@ __device__ void epnp_compute_pose(const G& g, const PnpIn& in, const int* idx, i
     S->rho[4] = dist2(S->cws[1], S->cws[3]);
     S->rho[5] = dist2(S->cws[2], S->cws[3]);
   }
-  g.sync();
+  __syncthreads();
   for (int ap = 1; ap <= 3; ap++) {
     if (tid == 0) {
-      double* betas = S->betas[ap];
-      if (ap == 1) find_betas_approx_1(S->l_6x10, S->rho, betas);
-      if (ap == 2) find_betas_approx_2(S->l_6x10, S->rho, betas);
-      if (ap == 3) find_betas_approx_3(S->l_6x10, S->rho, betas);
-      gauss_newton(S->l_6x10, S->rho, betas);
+      const double* l = S->l_6x10;
+      const double* rho = S->rho;
+      double betas[4];
+      if (ap == 1) find_betas_approx_1(l, rho, betas);
+      if (ap == 2) find_betas_approx_2(l, rho, betas);
+      if (ap == 3) find_betas_approx_3(l, rho, betas);
+      PNP_TS(4 + 4 * ap);
+      gauss_newton(l, rho, betas);
+      PNP_TS(5 + 4 * ap);
+#pragma unroll
+      for (int e = 0; e < 4; e++) S->betas[ap][e] = betas[e];
       // compute_ccs
-      for (int i = 0; i < 4; i++) S->ccs[i][0] = S->ccs[i][1] = S->ccs[i][2] = 0.0f;
+      double ccs[4][3];
+#pragma unroll
+      for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
+#pragma unroll
       for (int i = 0; i < 4; i++) {
         const double* v = S->ut + 12 * (11 - i);
+#pragma unroll
         for (int j = 0; j < 4; j++)
-          for (int k = 0; k < 3; k++) S->ccs[j][k] += betas[i] * v[3 * j + k];
+#pragma unroll
+          for (int k = 0; k < 3; k++) ccs[j][k] += betas[i] * v[3 * j + k];
       }
+      // solve_for_sign on point 0's compute_pcs value
+      const double* a0 = P.alphas;
+      const double z0 = a0[0] * ccs[0][2] + a0[1] * ccs[1][2] + a0[2] * ccs[2][2] + a0[3] * ccs[3][2];
+      const int flip = z0 < 0.0;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) S->ccs[i][j] = flip ? -ccs[i][j] : ccs[i][j];
     }
-    g.sync();
-    for (int i = tid; i < n; i += nt) {  // compute_pcs
-      const double* a = W.alphas + 4 * i;
-      double* pc = W.pcs + 3 * i;
-      for (int j = 0; j < 3; j++)
-        pc[j] = a[0] * S->ccs[0][j] + a[1] * S->ccs[1][j] + a[2] * S->ccs[2][j] + a[3] * S->ccs[3][j];
-    }
-    g.sync();
-    if (tid == 0) S->flip = W.pcs[2] < 0.0;  // solve_for_sign
-    g.sync();
-    if (S->flip) {
-      for (int i = tid; i < n; i += nt) {
-        W.pcs[3 * i] = -W.pcs[3 * i];
-        W.pcs[3 * i + 1] = -W.pcs[3 * i + 1];
-        W.pcs[3 * i + 2] = -W.pcs[3 * i + 2];
-      }
-      if (tid == 0)
-        for (int i = 0; i < 4; i++)
-          for (int j = 0; j < 3; j++) S->ccs[i][j] = -S->ccs[i][j];
-    }
-    g.sync();
+    __syncthreads();
+    // compute_pcs (after the sign flip: pcs of the negated ccs == negated pcs)
+    double ccs[4][3];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) ccs[q][j] = S->ccs[q][j];
+    auto pcs = [&](int i, int j) {
+      const double* a = P.alphas + 4 * i;
+      const double c0 = j == 0 ? ccs[0][0] : j == 1 ? ccs[0][1] : ccs[0][2];
+      const double c1 = j == 0 ? ccs[1][0] : j == 1 ? ccs[1][1] : ccs[1][2];
+      const double c2 = j == 0 ? ccs[2][0] : j == 1 ? ccs[2][1] : ccs[2][2];
+      const double c3 = j == 0 ? ccs[3][0] : j == 1 ? ccs[3][1] : ccs[3][2];
+      return a[0] * c0 + a[1] * c1 + a[2] * c2 + a[3] * c3;
+    };
     // estimate_R_and_t: centroid sums, then ABt sums, in point order
-    for (int e = tid; e < 6; e += nt) {
-      double s = 0;
-      for (int i = 0; i < n; i++) s += e < 3 ? W.pcs[3 * i + e] : pw(i, e - 3);
+    if (tid < 6) {
+      const int e = tid;
+      const double s = e < 3 ? seq_sum(n, [&](int i) { return pcs(i, e); }) : seq_sum(n, [&](int i) { return pw(i, e - 3); });
       if (e < 3)
         S->pc0[e] = s / n;
       else
         S->pw0[e - 3] = s / n;
     }
-    g.sync();
-    for (int e = tid; e < 9; e += nt) {
-      const int j = e / 3, c = e % 3;
-      double s = 0;
-      for (int i = 0; i < n; i++) s += (W.pcs[3 * i + j] - S->pc0[j]) * (pw(i, c) - S->pw0[c]);
-      S->abt[e] = s;
+    __syncthreads();
+    if (tid < 9) {
+      const int j = tid / 3, c = tid % 3;
+      const double pc0 = S->pc0[j], pw0 = S->pw0[c];
+      S->abt[tid] = seq_sum(n, [&](int i) { return (pcs(i, j) - pc0) * (pw(i, c) - pw0); });
     }
-    g.sync();
+    __syncthreads();
+    PNP_TS(6 + 4 * ap);
     if (tid == 0) {
-      double ut[9], w[3], vt[9], U[9], V[9];
-      svd_rows(S->abt, 3, 3, ut, w, vt);
+      double abt[9], ut[9], w[3], vt[9], U[9], V[9];
+#pragma unroll
+      for (int e = 0; e < 9; e++) abt[e] = S->abt[e];
+      svd_rows<3, 3>(abt, ut, w, vt);
+#pragma unroll
       for (int i = 0; i < 3; i++)
+#pragma unroll
         for (int k = 0; k < 3; k++) {
           U[3 * i + k] = ut[3 * k + i];
           V[3 * i + k] = vt[3 * k + i];
         }
-      double(*R)[3] = S->Rs[ap];
+      double R[3][3];
+#pragma unroll
       for (int i = 0; i < 3; i++)
+#pragma unroll
         for (int j = 0; j < 3; j++) R[i][j] = dot3(U + 3 * i, V + 3 * j);
       const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
                          R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
@@ -573,28 +768,36 @@ __device__ void epnp_compute_pose(const G& g, const PnpIn& in, const int* idx, i
         R[2][1] = -R[2][1];
         R[2][2] = -R[2][2];
       }
-      for (int r = 0; r < 3; r++) S->ts[ap][r] = S->pc0[r] - dot3(R[r], S->pw0);
+      const double pc0[3] = {S->pc0[0], S->pc0[1], S->pc0[2]}, pw0[3] = {S->pw0[0], S->pw0[1], S->pw0[2]};
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) S->Rs[ap][i][j] = R[i][j];
+#pragma unroll
+      for (int r = 0; r < 3; r++) S->ts[ap][r] = pc0[r] - dot3(R[r], pw0);
     }
-    g.sync();
-    for (int i = tid; i < n; i += nt) {  // reprojection_error terms
-      const double(*R)[3] = S->Rs[ap];
-      const double* t = S->ts[ap];
-      const double p[3] = {pw(i, 0), pw(i, 1), pw(i, 2)};
-      const double Xc = dot3(R[0], p) + t[0];
-      const double Yc = dot3(R[1], p) + t[1];
-      const double inv_Zc = 1.0 / (dot3(R[2], p) + t[2]);
-      const double ue = in.uc + in.fu * Xc * inv_Zc;
-      const double ve = in.vc + in.fv * Yc * inv_Zc;
-      const double u = uv(i, 0), v = uv(i, 1);
-      W.tmp[i] = sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+    __syncthreads();
+    {
+      double R[9], t[3];
+#pragma unroll
+      for (int e = 0; e < 9; e++) R[e] = S->Rs[ap][e / 3][e % 3];
+#pragma unroll
+      for (int e = 0; e < 3; e++) t[e] = S->ts[ap][e];
+      for (int i = tid; i < n; i += NT) {  // reprojection_error terms
+        const double p[3] = {pw(i, 0), pw(i, 1), pw(i, 2)};
+        const double Xc = dot3(R, p) + t[0];
+        const double Yc = dot3(R + 3, p) + t[1];
+        const double inv_Zc = 1.0 / (dot3(R + 6, p) + t[2]);
+        const double ue = in.uc + in.fu * Xc * inv_Zc;
+        const double ve = in.vc + in.fv * Yc * inv_Zc;
+        const double u = uv(i, 0), v = uv(i, 1);
+        P.tmp[i] = sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+      }
     }
-    g.sync();
-    if (tid == 0) {
-      double sum2 = 0.0;
-      for (int i = 0; i < n; i++) sum2 += W.tmp[i];
-      S->rep[ap] = sum2 / n;
-    }
-    g.sync();
+    __syncthreads();
+    if (tid == 0) S->rep[ap] = seq_sum(n, [&](int i) { return P.tmp[i]; }) / n;
+    __syncthreads();
+    PNP_TS(7 + 4 * ap);
   }
   if (tid == 0) {
     int N = 1;
@@ -602,7 +805,7 @@ __device__ void epnp_compute_pose(const G& g, const PnpIn& in, const int* idx, i
     if (S->rep[3] < S->rep[N]) N = 3;
     S->rep[0] = (double)N;
   }
-  g.sync();
+  __syncthreads();
 }
 
 // CheckInliers (:352-384) of one point
@@ -620,20 +823,32 @@ __device__ inline bool check_inlier(const PnpIn& in, const double* R, const doub
 }
 
 // ------------------------------------------------------------ kernels
-// pose record per hypothesis: R (9, row-major) + t (3)
-__global__ __launch_bounds__(64) void k_pnp_hyp(PnpIn in, const int* __restrict__ sets, int set_size, int n_hyp,
-                                                double* __restrict__ poses, double* __restrict__ work) {
-  const int h = blockIdx.x * 64 + threadIdx.x;
-  if (h >= n_hyp) return;
-  EpnpSmall S;
-  double* w = work + (size_t)h * (32 * kPnpMaxSet);
-  EpnpWork W{w, w + 4 * kPnpMaxSet, w + 7 * kPnpMaxSet, w + 31 * kPnpMaxSet};
-  epnp_compute_pose(GroupThread{}, in, sets + (size_t)h * set_size, set_size, &S, W);
-  const int b = (int)S.rep[0];
-  double* P = poses + 12 * (size_t)h;
-  for (int i = 0; i < 3; i++) {
-    for (int j = 0; j < 3; j++) P[3 * i + j] = S.Rs[b][i][j];
-    P[9 + i] = S.ts[b][i];
+constexpr int kHypThreads = 64;
+constexpr int kRefThreads = 256;
+constexpr int kRefineLdsPts = 2048;  // Refine stages up to this many inliers in LDS
+constexpr size_t kRefinePtBytes = 3 * 4 + 2 * 4 + 4 * 8 + 8;
+
+// One 64-thread block per hypothesis: its minimal set staged in LDS, EPnP,
+// pose record R (9, row-major) + t (3).
+__global__ __launch_bounds__(kHypThreads) void k_pnp_hyp(PnpIn in, const int* __restrict__ sets, int set_size,
+                                                         double* __restrict__ poses) {
+  __shared__ EpnpSmall S;
+  __shared__ float spw[3 * kPnpMaxSet], suv[2 * kPnpMaxSet];
+  __shared__ double salpha[4 * kPnpMaxSet], stmp[kPnpMaxSet];
+  const int h = blockIdx.x, tid = threadIdx.x;
+  const int* idx = sets + (size_t)h * set_size;
+  if (tid < set_size) {
+    const int i = idx[tid];
+#pragma unroll
+    for (int j = 0; j < 3; j++) spw[3 * tid + j] = in.p3d[3 * i + j];
+    suv[2 * tid] = in.p2d[2 * i];
+    suv[2 * tid + 1] = in.p2d[2 * i + 1];
+  }
+  __syncthreads();
+  epnp_compute_pose<kHypThreads>(in, EpnpPts{spw, suv, salpha, stmp}, set_size, &S);
+  if (tid < 12) {
+    const int b = (int)S.rep[0];
+    poses[12 * (size_t)h + tid] = tid < 9 ? S.Rs[b][tid / 3][tid % 3] : S.ts[b][tid - 9];
   }
 }
 
@@ -659,12 +874,17 @@ __global__ __launch_bounds__(256) void k_pnp_check(PnpIn in, const double* __res
 }
 
 // Refine(): EPnP on the inliers of `best` (ascending index), then CheckInliers.
-// out: [0..8] R, [9..11] t; *count; mask_out.
-__global__ __launch_bounds__(256) void k_pnp_refine(PnpIn in, const uint8_t* __restrict__ best, int* __restrict__ idx,
-                                                    double* __restrict__ work, double* __restrict__ out,
-                                                    uint8_t* __restrict__ mask_out, int* __restrict__ count) {
+// The inliers are compacted in order and staged in LDS (dynamic: kLds, up to
+// kRefineLdsPts) or in the global work buffer.  out: [0..8] R, [9..11] t;
+// *count; mask_out.
+template <bool kLds>
+__global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint8_t* __restrict__ best,
+                                                            int* __restrict__ idx, double* __restrict__ work,
+                                                            double* __restrict__ out, uint8_t* __restrict__ mask_out,
+                                                            int* __restrict__ count) {
   __shared__ EpnpSmall S;
   __shared__ int wsum[4], base;
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
   const int tid = threadIdx.x;
   // ordered compaction of the best inlier set
   if (tid == 0) base = 0;
@@ -685,8 +905,20 @@ __global__ __launch_bounds__(256) void k_pnp_refine(PnpIn in, const uint8_t* __r
     __syncthreads();
   }
   const int n = base;
-  EpnpWork W{work, work + 4 * (size_t)in.N, work + 7 * (size_t)in.N, work + 31 * (size_t)in.N};
-  epnp_compute_pose(GroupBlock{}, in, idx, n, &S, W);
+  const int cap = kLds ? kRefineLdsPts : in.N;
+  double* alphas = kLds ? dyn : work;
+  double* tmp = alphas + 4 * (size_t)cap;
+  float* spw = reinterpret_cast<float*>(tmp + cap);
+  float* suv = spw + 3 * (size_t)cap;
+  for (int k = tid; k < n; k += kRefThreads) {
+    const int i = idx[k];
+#pragma unroll
+    for (int j = 0; j < 3; j++) spw[3 * k + j] = in.p3d[3 * i + j];
+    suv[2 * k] = in.p2d[2 * i];
+    suv[2 * k + 1] = in.p2d[2 * i + 1];
+  }
+  __syncthreads();
+  epnp_compute_pose<kRefThreads>(in, EpnpPts{spw, suv, alphas, tmp}, n, &S);
   const int b = (int)S.rep[0];
   double R[9], t[3];
   for (int i = 0; i < 3; i++) {
@@ -694,7 +926,7 @@ __global__ __launch_bounds__(256) void k_pnp_refine(PnpIn in, const uint8_t* __r
     t[i] = S.ts[b][i];
   }
   int c = 0;
-  for (int i = tid; i < in.N; i += 256) {
+  for (int i = tid; i < in.N; i += kRefThreads) {
     const bool ok = check_inlier(in, R, t, i);
     mask_out[i] = ok;
     c += ok;
@@ -713,6 +945,48 @@ __global__ __launch_bounds__(256) void k_pnp_refine(PnpIn in, const uint8_t* __r
 }  // namespace orbx
 
 // ------------------------------------------------------------------ host / C ABI
+// One stream and one pinned readback block per device, shared by every
+// solver (the reference creates a PnPsolver per relocalisation candidate, so
+// creation must be cheap); each solver owns one stream-ordered allocation
+// (hipMallocAsync) holding all of its arrays.
+namespace {
+
+struct PnpDevice {
+  std::once_flag once;
+  hipError_t init_err = hipSuccess;
+  hipStream_t st = nullptr;
+  std::mutex mu;  // serialises iterate() calls that share the stream and readback block
+  void* pinned = nullptr;
+  size_t pinned_cap = 0;
+  hipError_t pinned_reserve(size_t bytes) {
+    if (bytes <= pinned_cap) return hipSuccess;
+    if (pinned) (void)hipHostFree(pinned);
+    pinned = nullptr;
+    pinned_cap = 0;
+    hipError_t e = hipHostMalloc(&pinned, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) pinned_cap = bytes;
+    return e;
+  }
+};
+PnpDevice g_pnp_dev[64];
+
+hipError_t pnp_device_init(int device) {
+  PnpDevice& d = g_pnp_dev[device];
+  std::call_once(d.once, [&] {
+    d.init_err = hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking);
+    if (d.init_err == hipSuccess)
+      d.init_err = hipFuncSetAttribute((const void*)orbx::k_pnp_refine<true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(orbx::kRefineLdsPts * orbx::kRefinePtBytes));
+    if (d.init_err == hipSuccess) d.init_err = d.pinned_reserve(1 << 16);
+  });
+  return d.init_err;
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
 struct orbx_pnp {
   int device = 0;
   hipStream_t st = nullptr;
@@ -721,36 +995,62 @@ struct orbx_pnp {
   double prob;
   int min_inliers, max_its, min_set;
   float epsilon;
-  // device: correspondences, per-hypothesis buffers, refine buffers
+  // device (one allocation): correspondences, refine buffers, per-hypothesis buffers
+  uint8_t* d_mem = nullptr;
   float *d_p3d = nullptr, *d_p2d = nullptr, *d_maxerr = nullptr;
-  int* d_sets = nullptr;
-  double* d_poses = nullptr;
-  double* d_hwork = nullptr;
-  uint8_t* d_masks = nullptr;
-  int* d_counts = nullptr;
   uint8_t *d_best = nullptr, *d_refmask = nullptr;
   int* d_idx = nullptr;
   double* d_rwork = nullptr;
-  double* d_rout = nullptr;
-  int* d_rcount = nullptr;
+  double* d_res = nullptr;  // refine result: R t (12) + count; best pose (12)
+  int* d_sets = nullptr;
+  double* d_poses = nullptr;
+  uint8_t* d_masks = nullptr;
+  int* d_counts = nullptr;
   int cap_hyp = 0;
   // iterate() state
   int iterations = 0, best_inliers = 0;
+  bool best_pose_on_host = false;
   float best_Tcw[16];
   bool refine_valid = false;  // Refine() of the current best set already known to fail
   orbx::PnpIn in() const {
     return orbx::PnpIn{d_p3d, d_p2d, d_maxerr, N, fu, fv, uc, vc};
   }
+  // lays the arrays out in d_mem for cap hypotheses; returns the byte size
+  size_t layout(int cap, uint8_t* base) {
+    const size_t nn = std::max(N, 1);
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+      uint8_t* p = base ? base + o : nullptr;
+      o += align256(bytes);
+      return p;
+    };
+    d_p3d = (float*)take(12 * nn);
+    d_p2d = (float*)take(8 * nn);
+    d_maxerr = (float*)take(4 * nn);
+    d_best = take(nn);
+    d_refmask = take(nn);
+    d_idx = (int*)take(4 * nn);
+    d_rwork = (double*)take(60 * nn);  // global-fallback refine: alphas 4n, tmp n (double), pw 3n, uv 2n (float)
+    d_res = (double*)take(8 * 32);
+    d_sets = (int*)take(sizeof(int) * (size_t)cap * orbx::kPnpMaxSet);
+    d_poses = (double*)take(sizeof(double) * 12 * (size_t)cap);
+    d_masks = take((size_t)cap * nn);
+    d_counts = (int*)take(sizeof(int) * (size_t)cap);
+    return o;
+  }
+  hipError_t alloc(int cap) {  // (re)allocates d_mem; the correspondences are re-uploaded by the caller
+    if (d_mem) (void)hipFreeAsync(d_mem, st);
+    d_mem = nullptr;
+    const size_t bytes = layout(cap, nullptr);
+    hipError_t e = hipMallocAsync((void**)&d_mem, bytes, st);
+    if (e != hipSuccess) return e;
+    layout(cap, d_mem);
+    cap_hyp = cap;
+    return hipSuccess;
+  }
 };
 
 namespace {
-
-void free_pnp(orbx_pnp* h) {
-  void* ptrs[] = {h->d_p3d,  h->d_p2d,     h->d_maxerr, h->d_sets,  h->d_poses, h->d_hwork, h->d_masks,
-                  h->d_counts, h->d_best, h->d_refmask, h->d_idx,   h->d_rwork, h->d_rout,  h->d_rcount};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
-}
 
 void pose_to_Tcw(const double* P, float T[16]) {  // Rcw/tcw convertTo(CV_32F) into eye(4)
   for (int i = 0; i < 16; i++) T[i] = (i % 5 == 0) ? 1.f : 0.f;
@@ -775,11 +1075,13 @@ orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* pr
   *out = nullptr;
   int nd = 0;
   if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return ORBX_ERR_NODEV;
-  if (device < 0 || device >= nd) return ORBX_ERR_ARG;
+  if (device < 0 || device >= nd || device >= 64) return ORBX_ERR_ARG;
   if (hipSetDevice(device) != hipSuccess) return ORBX_ERR_HIP;
+  if (pnp_device_init(device) != hipSuccess) return ORBX_ERR_HIP;
   orbx_pnp* h = new (std::nothrow) orbx_pnp();
   if (!h) return ORBX_ERR_HIP;
   h->device = device;
+  h->st = g_pnp_dev[device].st;
   const int n = p->n;
   h->N = n;
   h->fu = p->fx;
@@ -803,29 +1105,23 @@ orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* pr
   else
     nIterations = (int)std::ceil(std::log(1 - h->prob) / std::log(1 - std::pow(h->epsilon, 3)));
   h->max_its = std::max(1, std::min(nIterations, h->max_its));
-  std::vector<float> maxerr(n);
-  for (int i = 0; i < n; i++) maxerr[i] = p->sigma2[i] * prm->th2;
-  const size_t nn = std::max(n, 1);
-  hipError_t e = hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_p3d, 12 * nn);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_p2d, 8 * nn);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_maxerr, 4 * nn);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_best, nn);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_refmask, nn);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_idx, 4 * nn);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_rwork, 32 * 8 * nn);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_rout, 12 * 8);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->d_rcount, 4);
-  if (e == hipSuccess && n > 0) e = hipMemcpy(h->d_p3d, p->p3d, 12 * (size_t)n, hipMemcpyHostToDevice);
-  if (e == hipSuccess && n > 0) e = hipMemcpy(h->d_p2d, p->p2d, 8 * (size_t)n, hipMemcpyHostToDevice);
-  if (e == hipSuccess && n > 0) e = hipMemcpy(h->d_maxerr, maxerr.data(), 4 * (size_t)n, hipMemcpyHostToDevice);
+  for (int i = 0; i < 16; i++) h->best_Tcw[i] = 0;
+  hipError_t e = h->alloc(std::max(h->max_its, 8));
+  if (e == hipSuccess && n > 0) {
+    // one upload: p3d | p2d | maxerr are consecutive in the layout
+    std::vector<uint8_t> stage((uint8_t*)h->d_best - (uint8_t*)h->d_p3d);
+    std::memcpy(stage.data(), p->p3d, 12 * (size_t)n);
+    std::memcpy(stage.data() + ((uint8_t*)h->d_p2d - (uint8_t*)h->d_p3d), p->p2d, 8 * (size_t)n);
+    float* me = (float*)(stage.data() + ((uint8_t*)h->d_maxerr - (uint8_t*)h->d_p3d));
+    for (int i = 0; i < n; i++) me[i] = p->sigma2[i] * prm->th2;
+    e = hipMemcpyAsync(h->d_p3d, stage.data(), stage.size(), hipMemcpyHostToDevice, h->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->st);  // stage is pageable and local
+  }
   if (e != hipSuccess) {
-    free_pnp(h);
-    if (h->st) (void)hipStreamDestroy(h->st);
+    if (h->d_mem) (void)hipFreeAsync(h->d_mem, h->st);
     delete h;
     return ORBX_ERR_HIP;
   }
-  for (int i = 0; i < 16; i++) h->best_Tcw[i] = 0;
   *out = h;
   return ORBX_OK;
 }
@@ -833,8 +1129,7 @@ orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* pr
 orbx_status orbx_pnp_destroy(orbx_pnp* h) {
   if (!h) return ORBX_ERR_ARG;
   (void)hipSetDevice(h->device);
-  free_pnp(h);
-  if (h->st) (void)hipStreamDestroy(h->st);
+  if (h->d_mem) (void)hipFreeAsync(h->d_mem, h->st);
   delete h;
   return ORBX_OK;
 }
@@ -866,8 +1161,27 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
   const int H = std::max(h->max_its - h->iterations, n_iterations);
   if (H <= 0) return ORBX_OK;
   if ((long long)H * ms > n_rand) return ORBX_ERR_CAPACITY;
+  PnpDevice& dev = g_pnp_dev[h->device];
+  std::lock_guard<std::mutex> lock(dev.mu);
+  const size_t pin_bytes = std::max(sizeof(int) * (size_t)H * ms, sizeof(int) * (size_t)H) + 8 * 32;
+  PNP_CHECK(dev.pinned_reserve(pin_bytes));
+  if (H > h->cap_hyp) {  // keeps the correspondences: copy them over to the new block
+    uint8_t* old = h->d_mem;
+    const size_t keep = (uint8_t*)h->d_best - (uint8_t*)h->d_p3d;
+    const size_t best_off = (uint8_t*)h->d_best - old, res_off = (uint8_t*)h->d_res - old;
+    h->d_mem = nullptr;
+    const size_t bytes = h->layout(H, nullptr);
+    PNP_CHECK(hipMallocAsync((void**)&h->d_mem, bytes, h->st));
+    h->layout(H, h->d_mem);
+    h->cap_hyp = H;
+    PNP_CHECK(hipMemcpyAsync(h->d_p3d, old, keep, hipMemcpyDeviceToDevice, h->st));
+    PNP_CHECK(hipMemcpyAsync(h->d_best, old + best_off, std::max(N, 1), hipMemcpyDeviceToDevice, h->st));
+    PNP_CHECK(hipMemcpyAsync(h->d_res, old + res_off, 8 * 32, hipMemcpyDeviceToDevice, h->st));
+    PNP_CHECK(hipFreeAsync(old, h->st));
+  }
   // DUtils::Random::RandomInt(0, size-1) on the rand() stream + swap-remove
-  std::vector<int> sets((size_t)H * ms), avail(N);
+  int* sets = (int*)dev.pinned;
+  std::vector<int> avail(N);
   for (int k = 0; k < H; k++) {
     for (int i = 0; i < N; i++) avail[i] = i;
     int size = N;
@@ -878,61 +1192,62 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
       size--;
     }
   }
-  if (H > h->cap_hyp) {
-    if (h->d_sets) (void)hipFree(h->d_sets);
-    if (h->d_poses) (void)hipFree(h->d_poses);
-    if (h->d_hwork) (void)hipFree(h->d_hwork);
-    if (h->d_masks) (void)hipFree(h->d_masks);
-    if (h->d_counts) (void)hipFree(h->d_counts);
-    h->d_sets = nullptr;
-    h->d_poses = h->d_hwork = nullptr;
-    h->d_masks = nullptr;
-    h->d_counts = nullptr;
-    h->cap_hyp = 0;
-    PNP_CHECK(hipMalloc((void**)&h->d_sets, sizeof(int) * (size_t)H * orbx::kPnpMaxSet));
-    PNP_CHECK(hipMalloc((void**)&h->d_poses, sizeof(double) * 12 * (size_t)H));
-    PNP_CHECK(hipMalloc((void**)&h->d_hwork, sizeof(double) * 32 * orbx::kPnpMaxSet * (size_t)H));
-    PNP_CHECK(hipMalloc((void**)&h->d_masks, (size_t)H * std::max(N, 1)));
-    PNP_CHECK(hipMalloc((void**)&h->d_counts, sizeof(int) * (size_t)H));
-    h->cap_hyp = H;
-  }
   hipStream_t st = h->st;
-  PNP_CHECK(hipMemcpyAsync(h->d_sets, sets.data(), sizeof(int) * sets.size(), hipMemcpyHostToDevice, st));
+  PNP_CHECK(hipMemcpyAsync(h->d_sets, sets, sizeof(int) * (size_t)H * ms, hipMemcpyHostToDevice, st));
   const orbx::PnpIn in = h->in();
-  hipLaunchKernelGGL(orbx::k_pnp_hyp, dim3((H + 63) / 64), dim3(64), 0, st, in, h->d_sets, ms, H, h->d_poses,
-                     h->d_hwork);
+  hipLaunchKernelGGL(orbx::k_pnp_hyp, dim3(H), dim3(orbx::kHypThreads), 0, st, in, h->d_sets, ms, h->d_poses);
   hipLaunchKernelGGL(orbx::k_pnp_check, dim3(H), dim3(256), 0, st, in, h->d_poses, h->d_masks, h->d_counts);
   PNP_CHECK(hipGetLastError());
-  std::vector<int> counts(H);
-  PNP_CHECK(hipMemcpyAsync(counts.data(), h->d_counts, sizeof(int) * H, hipMemcpyDeviceToHost, st));
+  int* counts = (int*)dev.pinned;  // the sets were consumed by the copy above (stream order)
+  PNP_CHECK(hipMemcpyAsync(counts, h->d_counts, sizeof(int) * H, hipMemcpyDeviceToHost, st));
   PNP_CHECK(hipStreamSynchronize(st));
+  if (std::getenv("ORBX_PNP_TS")) {
+    unsigned long long ts[32];
+    if (hipMemcpyFromSymbol(ts, HIP_SYMBOL(orbx::g_pnp_ts), sizeof(ts)) == hipSuccess) {
+      std::fprintf(stderr, "[pnp ts]");
+      for (int i = 1; i < 20; i++) std::fprintf(stderr, " %d:%llu", i, ts[i] - ts[0]);
+      std::fprintf(stderr, "\n");
+    }
+  }
+  double* res = (double*)((uint8_t*)dev.pinned + align256(sizeof(int) * (size_t)H));
   int cur = 0;
   for (int k = 0; k < H && (h->iterations < h->max_its || cur < n_iterations); k++) {
     cur++;
     h->iterations++;
     *used += ms;
     if (counts[k] < h->min_inliers) continue;
-    if (counts[k] > h->best_inliers) {
+    if (counts[k] > h->best_inliers) {  // new best: mask + pose stay on the device
       h->best_inliers = counts[k];
       PNP_CHECK(hipMemcpyAsync(h->d_best, h->d_masks + (size_t)k * N, N, hipMemcpyDeviceToDevice, st));
-      double P[12];
-      PNP_CHECK(hipMemcpyAsync(P, h->d_poses + 12 * (size_t)k, sizeof(P), hipMemcpyDeviceToHost, st));
-      PNP_CHECK(hipStreamSynchronize(st));
-      pose_to_Tcw(P, h->best_Tcw);
+      PNP_CHECK(hipMemcpyAsync(h->d_res + 16, h->d_poses + 12 * (size_t)k, 12 * sizeof(double),
+                               hipMemcpyDeviceToDevice, st));
+      h->best_pose_on_host = false;
       h->refine_valid = false;
     }
     if (h->refine_valid) continue;  // same best set: Refine() fails again
-    hipLaunchKernelGGL(orbx::k_pnp_refine, dim3(1), dim3(256), 0, st, in, h->d_best, h->d_idx, h->d_rwork,
-                       h->d_rout, h->d_refmask, h->d_rcount);
+    if (N <= orbx::kRefineLdsPts)
+      hipLaunchKernelGGL(orbx::k_pnp_refine<true>, dim3(1), dim3(orbx::kRefThreads),
+                         orbx::kRefineLdsPts * orbx::kRefinePtBytes, st, in, h->d_best, h->d_idx, h->d_rwork,
+                         h->d_res, h->d_refmask, (int*)(h->d_res + 12));
+    else
+      hipLaunchKernelGGL(orbx::k_pnp_refine<false>, dim3(1), dim3(orbx::kRefThreads), 0, st, in, h->d_best, h->d_idx,
+                         h->d_rwork, h->d_res, h->d_refmask, (int*)(h->d_res + 12));
     PNP_CHECK(hipGetLastError());
-    int rc = 0;
-    double P[12];
-    PNP_CHECK(hipMemcpyAsync(&rc, h->d_rcount, sizeof(int), hipMemcpyDeviceToHost, st));
-    PNP_CHECK(hipMemcpyAsync(P, h->d_rout, sizeof(P), hipMemcpyDeviceToHost, st));
+    PNP_CHECK(hipMemcpyAsync(res, h->d_res, 13 * sizeof(double), hipMemcpyDeviceToHost, st));
     PNP_CHECK(hipStreamSynchronize(st));
+    if (std::getenv("ORBX_PNP_TS")) {
+      unsigned long long ts[32];
+      if (hipMemcpyFromSymbol(ts, HIP_SYMBOL(orbx::g_pnp_ts), sizeof(ts)) == hipSuccess) {
+        std::fprintf(stderr, "[pnp refine ts]");
+        for (int i = 1; i < 20; i++) std::fprintf(stderr, " %d:%llu", i, ts[i] - ts[0]);
+        std::fprintf(stderr, "\n");
+      }
+    }
+    const int rc = *(const int*)(res + 12);
     if (rc > h->min_inliers) {
-      PNP_CHECK(hipMemcpy(inliers, h->d_refmask, N, hipMemcpyDeviceToHost));
-      pose_to_Tcw(P, Tcw);
+      PNP_CHECK(hipMemcpyAsync(inliers, h->d_refmask, N, hipMemcpyDeviceToHost, st));
+      PNP_CHECK(hipStreamSynchronize(st));
+      pose_to_Tcw(res, Tcw);
       *n_inliers = rc;
       *found = 1;
       return ORBX_OK;
@@ -942,7 +1257,10 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
   if (h->iterations >= h->max_its) {
     *no_more = 1;
     if (h->best_inliers >= h->min_inliers) {
-      PNP_CHECK(hipMemcpy(inliers, h->d_best, N, hipMemcpyDeviceToHost));
+      PNP_CHECK(hipMemcpyAsync(res, h->d_res + 16, 12 * sizeof(double), hipMemcpyDeviceToHost, st));
+      PNP_CHECK(hipMemcpyAsync(inliers, h->d_best, N, hipMemcpyDeviceToHost, st));
+      PNP_CHECK(hipStreamSynchronize(st));
+      pose_to_Tcw(res, h->best_Tcw);
       std::memcpy(Tcw, h->best_Tcw, sizeof(float) * 16);
       *n_inliers = h->best_inliers;
       *found = 1;
