@@ -1,14 +1,14 @@
 // pnp.hip -- PnPsolver (src/PnPsolver.cc:67-1101) on the GPU: RANSAC
 // hypotheses evaluated in parallel, resolved in the reference's order.
 //
-//   k_pnp_hyp     one thread per hypothesis: EPnP compute_pose on its
-//                 minimal set (DUtils::Random::RandomInt + swap-remove
+//   k_pnp_hyp     one 256-thread block per hypothesis: EPnP compute_pose on
+//                 its minimal set (DUtils::Random::RandomInt + swap-remove
 //                 sampling replayed on the host from the caller's rand()
-//                 values)
+//                 values), everything in LDS
 //   k_pnp_check   one block per hypothesis: CheckInliers (float/double mix
 //                 exactly as :352-384) -> inlier bytes + count
 //   k_pnp_refine  one block: Refine() (:303-349) = EPnP on every inlier of
-//                 the best hypothesis + CheckInliers
+//                 the best hypothesis (staged in LDS) + CheckInliers
 // The host walks hypotheses in order (best = first strict maximum, Refine at
 // each hypothesis reaching minInliers, return on the first successful
 // Refine), which is iterate() (:182-301) including its
@@ -17,7 +17,11 @@
 // EPnP and the OpenCV 3.2 helpers it calls (cvMulTransposed, Jacobi cvSVD,
 // cvInvert/cvSolve through SVBkSb) use only IEEE + - * / sqrt in the same
 // order as the oracle, with every reduction sequential in the reference's
-// order, so poses and masks are bit-identical to the CPU restatement.
+// order, so poses and masks are bit-identical to the CPU restatement.  The
+// parallelism is only where it cannot change a bit: per-point terms, the
+// 12x12 Jacobi's independent rotations (wavefront schedule), the three
+// independent beta approximations (one wave each), and loads/terms of the
+// sequential sums computed ahead of the additions.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,11 +38,7 @@
 namespace orbx {
 
 constexpr int kPnpMaxSet = 16;
-__device__ unsigned long long g_pnp_ts[32];
-#define PNP_TS(i) \
-  do {            \
-    if (threadIdx.x == 0 && blockIdx.x == 0) g_pnp_ts[i] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
+
 
 struct PnpIn {
   const float* p3d;
@@ -529,15 +529,14 @@ __device__ __forceinline__ void gauss_newton(const double* l_6x10, const double*
 struct EpnpSmall {
   double cws[4][3], ccs[4][3], ci[9], pw0tpw0[9], mtm[144], ut[144], d[12];
   double l_6x10[60], rho[6], betas[4][4], rep[4], Rs[4][3][3], ts[4][3];
-  double pc0[3], pw0[3], abt[9];
-  int flip;
+  double pw0[3], ccs_ap[4][4][3], pc0_ap[4][3], abt_ap[4][9];
 };
 
 struct EpnpPts {   // per-correspondence arrays of one problem (n entries)
   const float* pw;  // 3n
   const float* uv;  // 2n
   double* alphas;   // 4n
-  double* tmp;      // n
+  double* tmp;      // 3n: pcs (compute_pcs), later the reprojection errors
 };
 
 // s = ((0 + t(0)) + t(1)) + ... + t(n-1): the reference's sequential sum,
@@ -563,7 +562,6 @@ __device__ __forceinline__ void epnp_compute_pose(const PnpIn& in, const EpnpPts
   const int tid = threadIdx.x;
   auto pw = [&](int k, int j) { return (double)P.pw[3 * k + j]; };
   auto uv = [&](int k, int j) { return (double)P.uv[2 * k + j]; };
-  PNP_TS(0);
   // choose_control_points
   if (tid < 3)  // the three coordinate sums are independent chains
     S->cws[0][tid] = seq_sum(n, [&](int i) { return pw(i, tid); }) / n;
@@ -600,7 +598,6 @@ __device__ __forceinline__ void epnp_compute_pose(const PnpIn& in, const EpnpPts
     for (int e = 0; e < 9; e++) S->ci[e] = ci[e];
   }
   __syncthreads();
-  PNP_TS(1);
   // compute_barycentric_coordinates
   for (int i = tid; i < n; i += NT) {
     double ci[9];
@@ -656,7 +653,6 @@ __device__ __forceinline__ void epnp_compute_pose(const PnpIn& in, const EpnpPts
     S->mtm[12 * i + j] = s;
   }
   __syncthreads();
-  PNP_TS(2);
   if (tid < 64) {  // wave 0: Ut = MtM^T of the mirrored MtM, then the wave-parallel Jacobi
     for (int e = tid; e < 144; e += 64) {
       const int i = e / 12, k = e % 12;  // Ut[i][k] = MtM[k][i]; MtM[k][i] = upper (min, max)
@@ -667,7 +663,6 @@ __device__ __forceinline__ void epnp_compute_pose(const PnpIn& in, const EpnpPts
     jacobi_svd_wave<12, 12>(S->ut, S->d);
   }
   __syncthreads();
-  PNP_TS(3);
   if (tid == 0) {
     compute_L_6x10(S->ut, S->l_6x10);
     S->rho[0] = dist2(S->cws[0], S->cws[1]);
@@ -678,127 +673,128 @@ __device__ __forceinline__ void epnp_compute_pose(const PnpIn& in, const EpnpPts
     S->rho[5] = dist2(S->cws[2], S->cws[3]);
   }
   __syncthreads();
-  for (int ap = 1; ap <= 3; ap++) {
-    if (tid == 0) {
-      const double* l = S->l_6x10;
-      const double* rho = S->rho;
-      double betas[4];
-      if (ap == 1) find_betas_approx_1(l, rho, betas);
-      if (ap == 2) find_betas_approx_2(l, rho, betas);
-      if (ap == 3) find_betas_approx_3(l, rho, betas);
-      PNP_TS(4 + 4 * ap);
-      gauss_newton(l, rho, betas);
-      PNP_TS(5 + 4 * ap);
+  // estimate_R_and_t's pw0 is the same for every approximation: once
+  if (tid < 3) S->pw0[tid] = seq_sum(n, [&](int i) { return pw(i, tid); }) / n;
+  __syncthreads();
+  // The three beta approximations are independent: with >= 3 waves, wave w
+  // runs approximation w+1 (its own ccs/pc0/abt/error scratch), so their
+  // serial FP64 chains overlap; each keeps the reference's operation order.
+  const int wv = tid >> 6, lane = tid & 63;
+  constexpr bool kApPar = NT >= 192;
+  auto wave_sync = [] {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+  };
+  if (kApPar ? wv < 3 : wv == 0) {
+    for (int ap = kApPar ? wv + 1 : 1; ap <= (kApPar ? wv + 1 : 3); ap++) {
+      double* ccs_s = &S->ccs_ap[ap][0][0];
+      if (lane == 0) {
+        const double* l = S->l_6x10;
+        const double* rho = S->rho;
+        double betas[4];
+        if (ap == 1) find_betas_approx_1(l, rho, betas);
+        if (ap == 2) find_betas_approx_2(l, rho, betas);
+        if (ap == 3) find_betas_approx_3(l, rho, betas);
+        gauss_newton(l, rho, betas);
 #pragma unroll
-      for (int e = 0; e < 4; e++) S->betas[ap][e] = betas[e];
-      // compute_ccs
-      double ccs[4][3];
+        for (int e = 0; e < 4; e++) S->betas[ap][e] = betas[e];
+        // compute_ccs
+        double ccs[4][3];
 #pragma unroll
-      for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
+        for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const double* v = S->ut + 12 * (11 - i);
+        for (int i = 0; i < 4; i++) {
+          const double* v = S->ut + 12 * (11 - i);
 #pragma unroll
-        for (int j = 0; j < 4; j++)
+          for (int j = 0; j < 4; j++)
 #pragma unroll
-          for (int k = 0; k < 3; k++) ccs[j][k] += betas[i] * v[3 * j + k];
-      }
-      // solve_for_sign on point 0's compute_pcs value
-      const double* a0 = P.alphas;
-      const double z0 = a0[0] * ccs[0][2] + a0[1] * ccs[1][2] + a0[2] * ccs[2][2] + a0[3] * ccs[3][2];
-      const int flip = z0 < 0.0;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) S->ccs[i][j] = flip ? -ccs[i][j] : ccs[i][j];
-    }
-    __syncthreads();
-    // compute_pcs (after the sign flip: pcs of the negated ccs == negated pcs)
-    double ccs[4][3];
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) ccs[q][j] = S->ccs[q][j];
-    auto pcs = [&](int i, int j) {
-      const double* a = P.alphas + 4 * i;
-      const double c0 = j == 0 ? ccs[0][0] : j == 1 ? ccs[0][1] : ccs[0][2];
-      const double c1 = j == 0 ? ccs[1][0] : j == 1 ? ccs[1][1] : ccs[1][2];
-      const double c2 = j == 0 ? ccs[2][0] : j == 1 ? ccs[2][1] : ccs[2][2];
-      const double c3 = j == 0 ? ccs[3][0] : j == 1 ? ccs[3][1] : ccs[3][2];
-      return a[0] * c0 + a[1] * c1 + a[2] * c2 + a[3] * c3;
-    };
-    // estimate_R_and_t: centroid sums, then ABt sums, in point order
-    if (tid < 6) {
-      const int e = tid;
-      const double s = e < 3 ? seq_sum(n, [&](int i) { return pcs(i, e); }) : seq_sum(n, [&](int i) { return pw(i, e - 3); });
-      if (e < 3)
-        S->pc0[e] = s / n;
-      else
-        S->pw0[e - 3] = s / n;
-    }
-    __syncthreads();
-    if (tid < 9) {
-      const int j = tid / 3, c = tid % 3;
-      const double pc0 = S->pc0[j], pw0 = S->pw0[c];
-      S->abt[tid] = seq_sum(n, [&](int i) { return (pcs(i, j) - pc0) * (pw(i, c) - pw0); });
-    }
-    __syncthreads();
-    PNP_TS(6 + 4 * ap);
-    if (tid == 0) {
-      double abt[9], ut[9], w[3], vt[9], U[9], V[9];
-#pragma unroll
-      for (int e = 0; e < 9; e++) abt[e] = S->abt[e];
-      svd_rows<3, 3>(abt, ut, w, vt);
-#pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          U[3 * i + k] = ut[3 * k + i];
-          V[3 * i + k] = vt[3 * k + i];
+            for (int k = 0; k < 3; k++) ccs[j][k] += betas[i] * v[3 * j + k];
         }
-      double R[3][3];
+        // solve_for_sign on point 0's compute_pcs value; the flipped pcs are
+        // the pcs of the negated ccs, exactly
+        const double* a0 = P.alphas;
+        const double z0 = a0[0] * ccs[0][2] + a0[1] * ccs[1][2] + a0[2] * ccs[2][2] + a0[3] * ccs[3][2];
+        const int flip = z0 < 0.0;
 #pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) R[i][j] = dot3(U + 3 * i, V + 3 * j);
-      const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
-                         R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
-      if (det < 0) {
-        R[2][0] = -R[2][0];
-        R[2][1] = -R[2][1];
-        R[2][2] = -R[2][2];
+        for (int e = 0; e < 12; e++) ccs_s[e] = flip ? -ccs[e / 3][e % 3] : ccs[e / 3][e % 3];
       }
-      const double pc0[3] = {S->pc0[0], S->pc0[1], S->pc0[2]}, pw0[3] = {S->pw0[0], S->pw0[1], S->pw0[2]};
+      wave_sync();
+      // compute_pcs on the fly: pcs(i, j) from the point's alphas
+      double cj[4] = {0, 0, 0, 0};
+      const int jl = lane < 3 ? lane : (lane < 12 ? (lane - 3) / 3 : 0);
 #pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) S->Rs[ap][i][j] = R[i][j];
-#pragma unroll
-      for (int r = 0; r < 3; r++) S->ts[ap][r] = pc0[r] - dot3(R[r], pw0);
-    }
-    __syncthreads();
-    {
-      double R[9], t[3];
-#pragma unroll
-      for (int e = 0; e < 9; e++) R[e] = S->Rs[ap][e / 3][e % 3];
-#pragma unroll
-      for (int e = 0; e < 3; e++) t[e] = S->ts[ap][e];
-      for (int i = tid; i < n; i += NT) {  // reprojection_error terms
-        const double p[3] = {pw(i, 0), pw(i, 1), pw(i, 2)};
-        const double Xc = dot3(R, p) + t[0];
-        const double Yc = dot3(R + 3, p) + t[1];
-        const double inv_Zc = 1.0 / (dot3(R + 6, p) + t[2]);
-        const double ue = in.uc + in.fu * Xc * inv_Zc;
-        const double ve = in.vc + in.fv * Yc * inv_Zc;
-        const double u = uv(i, 0), v = uv(i, 1);
-        P.tmp[i] = sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+      for (int q = 0; q < 4; q++) cj[q] = ccs_s[3 * q + jl];
+      auto pcs = [&](int i) {
+        const double* a = P.alphas + 4 * i;
+        return a[0] * cj[0] + a[1] * cj[1] + a[2] * cj[2] + a[3] * cj[3];
+      };
+      // estimate_R_and_t: centroid sums (lanes 0-2), then ABt sums (lanes 3-11), in point order
+      if (lane < 3) S->pc0_ap[ap][lane] = seq_sum(n, pcs) / n;
+      wave_sync();
+      if (lane >= 3 && lane < 12) {
+        const int c = (lane - 3) % 3;
+        const double pc0 = S->pc0_ap[ap][jl], pw0 = S->pw0[c];
+        S->abt_ap[ap][lane - 3] = seq_sum(n, [&](int i) { return (pcs(i) - pc0) * (pw(i, c) - pw0); });
       }
+      wave_sync();
+      if (lane == 0) {
+        double abt[9], ut[9], w[3], vt[9], U[9], V[9];
+#pragma unroll
+        for (int e = 0; e < 9; e++) abt[e] = S->abt_ap[ap][e];
+        svd_rows<3, 3>(abt, ut, w, vt);
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int k = 0; k < 3; k++) {
+            U[3 * i + k] = ut[3 * k + i];
+            V[3 * i + k] = vt[3 * k + i];
+          }
+        double R[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++) R[i][j] = dot3(U + 3 * i, V + 3 * j);
+        const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
+                           R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
+        if (det < 0) {
+          R[2][0] = -R[2][0];
+          R[2][1] = -R[2][1];
+          R[2][2] = -R[2][2];
+        }
+        const double pc0[3] = {S->pc0_ap[ap][0], S->pc0_ap[ap][1], S->pc0_ap[ap][2]};
+        const double pw0[3] = {S->pw0[0], S->pw0[1], S->pw0[2]};
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++) S->Rs[ap][i][j] = R[i][j];
+#pragma unroll
+        for (int r = 0; r < 3; r++) S->ts[ap][r] = pc0[r] - dot3(R[r], pw0);
+      }
+      wave_sync();
+      double* err = P.tmp + (size_t)(ap - 1) * n;
+      {
+        double R[9], t[3];
+#pragma unroll
+        for (int e = 0; e < 9; e++) R[e] = S->Rs[ap][e / 3][e % 3];
+#pragma unroll
+        for (int e = 0; e < 3; e++) t[e] = S->ts[ap][e];
+        for (int i = lane; i < n; i += (kApPar ? 64 : NT)) {  // reprojection_error terms
+          const double p[3] = {pw(i, 0), pw(i, 1), pw(i, 2)};
+          const double Xc = dot3(R, p) + t[0];
+          const double Yc = dot3(R + 3, p) + t[1];
+          const double inv_Zc = 1.0 / (dot3(R + 6, p) + t[2]);
+          const double ue = in.uc + in.fu * Xc * inv_Zc;
+          const double ve = in.vc + in.fv * Yc * inv_Zc;
+          const double u = uv(i, 0), v = uv(i, 1);
+          err[i] = sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+        }
+      }
+      wave_sync();
+      if (lane == 0) S->rep[ap] = seq_sum(n, [&](int i) { return err[i]; }) / n;
+      wave_sync();
     }
-    __syncthreads();
-    if (tid == 0) S->rep[ap] = seq_sum(n, [&](int i) { return P.tmp[i]; }) / n;
-    __syncthreads();
-    PNP_TS(7 + 4 * ap);
   }
+  __syncthreads();
   if (tid == 0) {
     int N = 1;
     if (S->rep[2] < S->rep[1]) N = 2;
@@ -823,10 +819,10 @@ __device__ inline bool check_inlier(const PnpIn& in, const double* R, const doub
 }
 
 // ------------------------------------------------------------ kernels
-constexpr int kHypThreads = 64;
+constexpr int kHypThreads = 256;  // 4 waves: the beta approximations run one per wave
 constexpr int kRefThreads = 256;
-constexpr int kRefineLdsPts = 2048;  // Refine stages up to this many inliers in LDS
-constexpr size_t kRefinePtBytes = 3 * 4 + 2 * 4 + 4 * 8 + 8;
+constexpr int kRefineLdsPts = 2000;  // Refine stages up to this many inliers in LDS
+constexpr size_t kRefinePtBytes = 4 * 8 + 3 * 8 + 3 * 4 + 2 * 4;  // alphas, pcs/errors, pw, uv
 
 // One 64-thread block per hypothesis: its minimal set staged in LDS, EPnP,
 // pose record R (9, row-major) + t (3).
@@ -834,7 +830,7 @@ __global__ __launch_bounds__(kHypThreads) void k_pnp_hyp(PnpIn in, const int* __
                                                          double* __restrict__ poses) {
   __shared__ EpnpSmall S;
   __shared__ float spw[3 * kPnpMaxSet], suv[2 * kPnpMaxSet];
-  __shared__ double salpha[4 * kPnpMaxSet], stmp[kPnpMaxSet];
+  __shared__ double salpha[4 * kPnpMaxSet], stmp[3 * kPnpMaxSet];
   const int h = blockIdx.x, tid = threadIdx.x;
   const int* idx = sets + (size_t)h * set_size;
   if (tid < set_size) {
@@ -908,7 +904,7 @@ __global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint
   const int cap = kLds ? kRefineLdsPts : in.N;
   double* alphas = kLds ? dyn : work;
   double* tmp = alphas + 4 * (size_t)cap;
-  float* spw = reinterpret_cast<float*>(tmp + cap);
+  float* spw = reinterpret_cast<float*>(tmp + 3 * (size_t)cap);
   float* suv = spw + 3 * (size_t)cap;
   for (int k = tid; k < n; k += kRefThreads) {
     const int i = idx[k];
@@ -1009,7 +1005,6 @@ struct orbx_pnp {
   int cap_hyp = 0;
   // iterate() state
   int iterations = 0, best_inliers = 0;
-  bool best_pose_on_host = false;
   float best_Tcw[16];
   bool refine_valid = false;  // Refine() of the current best set already known to fail
   orbx::PnpIn in() const {
@@ -1030,7 +1025,7 @@ struct orbx_pnp {
     d_best = take(nn);
     d_refmask = take(nn);
     d_idx = (int*)take(4 * nn);
-    d_rwork = (double*)take(60 * nn);  // global-fallback refine: alphas 4n, tmp n (double), pw 3n, uv 2n (float)
+    d_rwork = (double*)take(orbx::kRefinePtBytes * nn);  // global-fallback refine: same per-point layout
     d_res = (double*)take(8 * 32);
     d_sets = (int*)take(sizeof(int) * (size_t)cap * orbx::kPnpMaxSet);
     d_poses = (double*)take(sizeof(double) * 12 * (size_t)cap);
@@ -1201,14 +1196,6 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
   int* counts = (int*)dev.pinned;  // the sets were consumed by the copy above (stream order)
   PNP_CHECK(hipMemcpyAsync(counts, h->d_counts, sizeof(int) * H, hipMemcpyDeviceToHost, st));
   PNP_CHECK(hipStreamSynchronize(st));
-  if (std::getenv("ORBX_PNP_TS")) {
-    unsigned long long ts[32];
-    if (hipMemcpyFromSymbol(ts, HIP_SYMBOL(orbx::g_pnp_ts), sizeof(ts)) == hipSuccess) {
-      std::fprintf(stderr, "[pnp ts]");
-      for (int i = 1; i < 20; i++) std::fprintf(stderr, " %d:%llu", i, ts[i] - ts[0]);
-      std::fprintf(stderr, "\n");
-    }
-  }
   double* res = (double*)((uint8_t*)dev.pinned + align256(sizeof(int) * (size_t)H));
   int cur = 0;
   for (int k = 0; k < H && (h->iterations < h->max_its || cur < n_iterations); k++) {
@@ -1221,11 +1208,10 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
       PNP_CHECK(hipMemcpyAsync(h->d_best, h->d_masks + (size_t)k * N, N, hipMemcpyDeviceToDevice, st));
       PNP_CHECK(hipMemcpyAsync(h->d_res + 16, h->d_poses + 12 * (size_t)k, 12 * sizeof(double),
                                hipMemcpyDeviceToDevice, st));
-      h->best_pose_on_host = false;
       h->refine_valid = false;
     }
     if (h->refine_valid) continue;  // same best set: Refine() fails again
-    if (N <= orbx::kRefineLdsPts)
+    if (h->best_inliers <= orbx::kRefineLdsPts)  // the refined set is the best mask
       hipLaunchKernelGGL(orbx::k_pnp_refine<true>, dim3(1), dim3(orbx::kRefThreads),
                          orbx::kRefineLdsPts * orbx::kRefinePtBytes, st, in, h->d_best, h->d_idx, h->d_rwork,
                          h->d_res, h->d_refmask, (int*)(h->d_res + 12));
@@ -1235,14 +1221,6 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
     PNP_CHECK(hipGetLastError());
     PNP_CHECK(hipMemcpyAsync(res, h->d_res, 13 * sizeof(double), hipMemcpyDeviceToHost, st));
     PNP_CHECK(hipStreamSynchronize(st));
-    if (std::getenv("ORBX_PNP_TS")) {
-      unsigned long long ts[32];
-      if (hipMemcpyFromSymbol(ts, HIP_SYMBOL(orbx::g_pnp_ts), sizeof(ts)) == hipSuccess) {
-        std::fprintf(stderr, "[pnp refine ts]");
-        for (int i = 1; i < 20; i++) std::fprintf(stderr, " %d:%llu", i, ts[i] - ts[0]);
-        std::fprintf(stderr, "\n");
-      }
-    }
     const int rc = *(const int*)(res + 12);
     if (rc > h->min_inliers) {
       PNP_CHECK(hipMemcpyAsync(inliers, h->d_refmask, N, hipMemcpyDeviceToHost, st));

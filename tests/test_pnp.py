@@ -92,6 +92,7 @@ PNP_CASES = {  # (n, outlier_frac, noise_px, seed): outcome exercised
     "small_60": (60, 0.3, 0.5, 7),
     "small_40": (40, 0.2, 0.3, 8),
     "heavy_outliers": (300, 0.5, 0.5, 10),
+    "refine_global": (2600, 0.1, 0.5, 11),  # > 2000 inliers: Refine's global-memory staging path
 }
 
 
