@@ -132,8 +132,9 @@ __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, c
   __shared__ int rsh[kRzMaxRows];
   const LevelGeom& L = G->lv[l];
   const LevelGeom& S = G->lv[l - 1];
-  const int img = blockIdx.z, tid = threadIdx.x;
-  const int ox0 = blockIdx.x * kRzTW, oy0 = blockIdx.y * kRzTH;
+  const int3 bi = xcd_block3();
+  const int img = bi.z, tid = threadIdx.x;
+  const int ox0 = bi.x * kRzTW, oy0 = bi.y * kRzTH;
   const int nx = min(kRzTW, L.w - ox0), ny = min(kRzTH, L.h - oy0);
   if (tid < nx) sx[tid] = xt[L.xtab_off + ox0 + tid];
   if (tid >= kRzTW && tid - kRzTW < ny) sy[tid - kRzTW] = yt[L.ytab_off + oy0 + tid - kRzTW];
@@ -217,7 +218,8 @@ constexpr int kBStrip = 16;           // output rows per thread
 __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
                                              BatchPtrs B) {
   __shared__ __align__(16) uint8_t tin[(kBlurTileH + 6) * kBIn];
-  const int tile = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const int2 bi = xcd_block2();
+  const int tile = bi.x, img = bi.y, tid = threadIdx.x;
   const int l = tile_level[tile];
   const LevelGeom& L = G->lv[l];
   const int t = tile - L.tile_begin;
@@ -406,7 +408,8 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   uint8_t* smap = fast_smem + G->fast_tile_bytes;
   uint16_t* list = (uint16_t*)(fast_smem + G->fast_tile_bytes + G->fast_map_bytes);
   const int kMapS = G->fast_maps;
-  const int cell = blockIdx.x, img = blockIdx.y, lane = threadIdx.x;
+  const int2 bi = xcd_block2();
+  const int cell = bi.x, img = bi.y, lane = threadIdx.x;
   const CellInfo c = cells[cell];
   const int lw = G->lv[c.level].w;
   const uint8_t* base = level_ptr(*G, B, img, c.level) + (size_t)(c.y0 - 3) * lw + (c.x0 - 3);
@@ -916,15 +919,16 @@ __global__ __launch_bounds__(BS) void k_octree(const Geometry* __restrict__ G, c
 __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                  int32_t* __restrict__ counts, int kp_cap) {
-  const int img = blockIdx.y;
+  const int2 bi = xcd_block2();
+  const int img = bi.y;
   const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * (BS / 64) + (threadIdx.x >> 6);
+  const int i = bi.x * (BS / 64) + (threadIdx.x >> 6);
   const int nl = G->nlevels;
   int pre[kMaxLevelsPlan + 1];
   pre[0] = 0;
   for (int l = 0; l < nl; l++) pre[l + 1] = pre[l] + B.oct_count[(size_t)img * nl + l];
   const int total = pre[nl];
-  if (blockIdx.x == 0 && threadIdx.x == 0) counts[img] = total;
+  if (bi.x == 0 && threadIdx.x == 0) counts[img] = total;
   if (i >= total) return;
   int l = 0;
   while (pre[l + 1] <= i) l++;

@@ -14,6 +14,30 @@ constexpr int kEdgeThreshold = 19;  // EDGE_THRESHOLD, src/ORBextractor.cc:74
 constexpr int kMaxLevels = 16;
 
 // cvRound (SSE2 cvtss2si): round half to even.
+// XCD-aware block order.  MI355X deals blocks round-robin over its 8 XCDs,
+// each with a private L2, so neighbouring blocks -- cells, tiles, keypoints
+// that read overlapping image rows -- would each pull the shared lines into a
+// different L2.  xcd_block maps the hardware linear block id so that the
+// blocks sharing an XCD take one contiguous range of the logical grid.
+// Bijective for any grid size (q + 1 blocks for the first total % 8 groups);
+// affects speed only, never results.
+__device__ __forceinline__ int xcd_block(int hw, int total) {
+  const int x = hw & 7, i = hw >> 3, q = total >> 3, r = total & 7;
+  return x * q + min(x, r) + i;
+}
+// logical (x, y) of a 2-D grid, x fastest
+__device__ __forceinline__ int2 xcd_block2() {
+  const int gx = gridDim.x;
+  const int l = xcd_block(blockIdx.x + gx * blockIdx.y, gx * gridDim.y);
+  return make_int2(l % gx, l / gx);
+}
+// logical (x, y, z) of a 3-D grid, x fastest
+__device__ __forceinline__ int3 xcd_block3() {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int l = xcd_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  return make_int3(l % gx, (l / gx) % gy, l / (gx * gy));
+}
+
 __device__ __forceinline__ int round_even(float v) { return (int)__builtin_rintf(v); }
 
 // fastAtan2 (OpenCV 3.2 core): degrees in [0,360).

@@ -105,9 +105,10 @@ constexpr int kKpsPerBlock = 128;
 // No LDS: candidate ranges come from the row table, (x, index) pairs from the
 // sorted array, so occupancy is bounded by registers only.
 __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
-  const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int2 bi = xcd_block2();
+  const int f = bi.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
-  const int base = blockIdx.x * kKpsPerBlock;
+  const int base = bi.x * kKpsPerBlock;
   if (base >= nL) return;
   const orbx_keypoint* kR = A.kpR + (size_t)f * A.kR_stride;
   const int2* rxi = A.rxi + (size_t)f * kMaxStereoKps;
