@@ -258,25 +258,27 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
   const int xg = x0 + 4 * g;
   if (xg >= w || y0 + ys >= h) return;
   const int k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
+  // horizontal taps as byte dot products (exact integers, weights < 256):
+  // output col j of the group needs tile bytes j+1..j+7 of the 12 bytes
+  // [a b c]; lo = bytes j+1..j+4 (k0 k1 k2 k3), hi = bytes j+5..j+8 (k2 k1 k0 0)
+  const uint32_t wlo = (uint32_t)k0 | (uint32_t)k1 << 8 | (uint32_t)k2 << 16 | (uint32_t)k3 << 24;
+  const uint32_t whi = (uint32_t)k2 | (uint32_t)k1 << 8 | (uint32_t)k0 << 16;
   // row sums (<= 257*255) of output cols xg..xg+3 on tile row ty
   auto rowsum = [&](int ty, int (&o)[4]) {
     const uint32_t* r32 = (const uint32_t*)&tin[ty * kBIn + 4 * g];
     const uint32_t a = r32[0], b = r32[1], c = r32[2];
-    int p[12];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      p[i] = (a >> (8 * i)) & 255;
-      p[4 + i] = (b >> (8 * i)) & 255;
-      p[8 + i] = (c >> (8 * i)) & 255;
+    for (int j = 0; j < 4; j++) {
+      const uint32_t lo = j < 3 ? __builtin_amdgcn_alignbyte(b, a, j + 1) : b;
+      const uint32_t hi = j < 3 ? __builtin_amdgcn_alignbyte(c, b, j + 1) : c;
+      o[j] = (int)__builtin_amdgcn_udot4(lo, wlo, __builtin_amdgcn_udot4(hi, whi, 0u, false), false);
     }
-#pragma unroll
-    for (int j = 0; j < 4; j++)  // output col 4g+j needs tile cols 4g+j+1 .. 4g+j+7
-      o[j] = k3 * p[j + 4] + k2 * (p[j + 3] + p[j + 5]) + k1 * (p[j + 2] + p[j + 6]) + k0 * (p[j + 1] + p[j + 7]);
   };
   int win[7][4];
 #pragma unroll
   for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
   const int simd_w = w & ~3;
+  const bool all_simd = xg + 3 < simd_w;  // the whole group takes the SSE2 rounding
 #pragma unroll
   for (int r = 0; r < kBStrip; r++) {
     rowsum(ys + r + 6, win[6]);
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
         const int acc = k3 * win[3][j] + k2 * (win[2][j] + win[4][j]) + k1 * (win[1][j] + win[5][j]) +
                         k0 * (win[0][j] + win[6][j]);
         // SSE2 groups: rint(acc / 2^16) (ties to even; acc >= 2^24 saturates either way); tail: (acc + 2^15) >> 16
-        const int v = (xg + j < simd_w) ? (acc + 0x7FFF + ((acc >> 16) & 1)) >> 16 : (acc + (1 << 15)) >> 16;
+        const int v = (all_simd || xg + j < simd_w) ? (acc + 0x7FFF + ((acc >> 16) & 1)) >> 16 : (acc + (1 << 15)) >> 16;
         packed |= (uint32_t)min(v, 255) << (8 * j);
       }
       uint8_t* d = dst + (size_t)y * bs + xg;
