@@ -29,6 +29,10 @@
  *   orbx_pnp_create             PnPsolver::PnPsolver + SetRansacParameters
  *                                                               src/PnPsolver.cc:67-179, include/PnPsolver.h:66-70
  *   orbx_pnp_iterate            PnPsolver::iterate              src/PnPsolver.cc:182-384, include/PnPsolver.h:74
+ *   orbx_voc_load_text          TemplatedVocabulary::loadFromTextFile (ORBVocabulary)
+ *                                                               Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1420
+ *   orbx_voc_transform          TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
+ *                                                               :1125-1196, 1218-1259 (Frame::ComputeBoW src/Frame.cc:462-469)
  *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
  *                               (g2o graph build, optimize(5), outlier levels, optimize(10), vToErase;
  *                               the Map mutex/recovery part stays on the caller's side)
@@ -157,6 +161,29 @@ typedef struct {
   int32_t* nmatches;
 } orbx_bow_problem;
 orbx_status orbx_search_by_bow_device(const orbx_bow_problem* problems, int n, void* stream);
+
+/* DBoW2 vocabulary (ORBVocabulary = TemplatedVocabulary<FORB::TDescriptor, FORB>)
+ * from the text format of loadFromTextFile: header "k L scoring weighting",
+ * then one line per node "parent isLeaf d0..d31 weight" in node-id order.  A
+ * blank line ends the node list.  The tree lives on `device`. */
+typedef struct orbx_voc orbx_voc;
+orbx_status orbx_voc_load_text(const char* text, size_t len, int device, orbx_voc** out);
+orbx_status orbx_voc_destroy(orbx_voc* v);
+/* info = {k, L, scoring, weighting, n_nodes (incl. root), n_words} */
+orbx_status orbx_voc_info(const orbx_voc* v, int32_t info[6]);
+/* transform(features, BowVector, FeatureVector, levelsup) for n_sets descriptor
+ * sets in one call: set s = rows set_off[s] .. set_off[s+1]-1 of desc (32 B
+ * each, set_off[0] = 0, at most 8192 rows per set).  Host pointers.  Per set s:
+ *   BowVector     n_bow[s] entries at bow_words/bow_values + set_off[s], word ids
+ *                 ascending (std::map order), values after the vocabulary's
+ *                 weighting/normalisation;
+ *   FeatureVector n_fv[s] nodes at fv_nodes + set_off[s] (ascending), the
+ *                 features of node j at fv_feat[set_off[s] + fv_off[set_off[s] + s + j]
+ *                 .. + fv_off[set_off[s] + s + j + 1]) as indices within the set,
+ *                 ascending -- the CSR that orbx_bow_side takes. */
+orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* set_off, int n_sets, int levelsup,
+                               uint32_t* bow_words, double* bow_values, int32_t* n_bow, uint32_t* fv_nodes,
+                               int32_t* fv_off, int32_t* fv_feat, int32_t* n_fv);
 
 /* Optimizer::LocalBundleAdjustment on g2o semantics (BlockSolver_6_3 +
  * LinearSolverEigen + Levenberg, Huber kernels, two phases), FP64 on the GPU.

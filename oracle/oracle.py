@@ -83,6 +83,13 @@ def lib():
         L.oracle_epnp.restype = C.c_double
         L.oracle_svd.argtypes = [P, C.c_int, C.c_int, P, P, P]
         L.oracle_svd.restype = None
+        L.oracle_voc_load.argtypes = [C.c_char_p, C.c_long]
+        L.oracle_voc_load.restype = P
+        L.oracle_voc_free.argtypes = [P]
+        L.oracle_voc_free.restype = None
+        L.oracle_voc_info.argtypes = [P, P]
+        L.oracle_voc_info.restype = None
+        L.oracle_voc_transform.argtypes = [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -313,3 +320,39 @@ def svd(A):
     Ut, w, Vt = np.zeros((n, m)), np.zeros(n), np.zeros((n, n))
     lib().oracle_svd(_p(A), m, n, _p(Ut), _p(w), _p(Vt))
     return Ut, w, Vt
+
+
+class Vocabulary:
+    """DBoW2 TemplatedVocabulary (text format) + transform -- oracle/voc.cpp."""
+
+    def __init__(self, text):
+        raw = text.encode() if isinstance(text, str) else bytes(text)
+        self._h = lib().oracle_voc_load(raw, len(raw))
+        if not self._h:
+            raise ValueError("vocabulary text rejected")
+        info = np.zeros(6, np.int32)
+        lib().oracle_voc_info(self._h, _p(info))
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = (int(x) for x in info)
+
+    def transform(self, desc, levelsup=4):
+        """-> (bow_words, bow_values, fv_nodes, fv_off, fv_feat) in std::map order."""
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(desc)
+        w = np.zeros(max(n, 1), np.int32)
+        v = np.zeros(max(n, 1), np.float64)
+        fn = np.zeros(max(n, 1), np.int32)
+        fo = np.zeros(max(n, 1) + 1, np.int32)
+        ff = np.zeros(max(n, 1), np.int32)
+        nb, nf = C.c_int(), C.c_int()
+        rc = lib().oracle_voc_transform(self._h, _p(desc), n, int(levelsup), _p(w), _p(v), C.byref(nb), _p(fn),
+                                        _p(fo), _p(ff), C.byref(nf))
+        if rc != 0:
+            return (np.zeros(0, np.int32), np.zeros(0), np.zeros(0, np.int32), np.zeros(1, np.int32),
+                    np.zeros(0, np.int32))
+        k = nf.value
+        return w[:nb.value], v[:nb.value], fn[:k], fo[:k + 1], ff[:fo[k]]
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().oracle_voc_free(self._h)
+            self._h = None

@@ -102,6 +102,10 @@ SIGNATURES = {
                           C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
     "orbx_pnp_iterate_stream": ([P, C.c_int, C.POINTER(RandState), C.POINTER(C.c_int), P, P, C.POINTER(C.c_int),
                                  C.POINTER(C.c_int)], C.c_int),
+    "orbx_voc_load_text": ([C.c_char_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_voc_destroy": ([P], C.c_int),
+    "orbx_voc_info": ([P, P], C.c_int),
+    "orbx_voc_transform": ([P, P, P, C.c_int, C.c_int, P, P, P, P, P, P, P], C.c_int),
     "orbx_rand_seed": ([C.POINTER(RandState), C.c_uint32], None),
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),

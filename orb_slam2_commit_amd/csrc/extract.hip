@@ -524,8 +524,8 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     const int s = m[0];
     const int n0 = m[-kMapS - 1], n1 = m[-kMapS], n2 = m[-kMapS + 1], n3 = m[-1], n4 = m[1], n5 = m[kMapS - 1],
               n6 = m[kMapS], n7 = m[kMapS + 1];
-    auto beats = [&](int nv) { return nv >= thr && nv >= s; };
-    const bool lost = beats(n0) | beats(n1) | beats(n2) | beats(n3) | beats(n4) | beats(n5) | beats(n6) | beats(n7);
+    auto beats = [&](int nv) -> int { return nv >= thr && nv >= s; };  // int: branch-free OR below
+    const bool lost = (beats(n0) | beats(n1) | beats(n2) | beats(n3) | beats(n4) | beats(n5) | beats(n6) | beats(n7)) != 0;
     return s >= thr && s > 1 && !lost;
   };
   // 4. survivors at iniThFAST (verdict kept in bit 15 of the list entry)

@@ -337,3 +337,66 @@ class PnPsolver:
         rng.advance(used.value)
         self._done += used.value // self.min_set
         return (T.reshape(4, 4) if found.value else None), bool(nm.value), inl[:self.n].astype(bool), ni.value
+
+
+class ORBVocabulary:
+    """DBoW2 TemplatedVocabulary<FORB> (include/ORBVocabulary.h) on the GPU:
+    loadFromTextFile (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1420) and
+    transform(features, BowVector, FeatureVector, levelsup) (:1125-1196) over liborbx.so."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self._h = None
+
+    def loadFromText(self, text):
+        """The text of a vocabulary file (ORBvoc.txt format).  Returns True like the reference."""
+        self.close()
+        raw = text.encode() if isinstance(text, str) else bytes(text)
+        h = C.c_void_p()
+        check(_lib.lib().orbx_voc_load_text(raw, len(raw), self.device, C.byref(h)), "orbx_voc_load_text")
+        self._h = h
+        info = np.zeros(6, np.int32)
+        check(_lib.lib().orbx_voc_info(h, ptr(info)), "orbx_voc_info")
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = (int(x) for x in info)
+        return True
+
+    def loadFromTextFile(self, path):
+        with open(path, "rb") as f:
+            return self.loadFromText(f.read())
+
+    def transform_sets(self, desc_sets, levelsup=4):
+        """Batch form: list of (n_i, 32) uint8 descriptor arrays -> list of
+        (bow_words, bow_values, fv_nodes, fv_off, fv_feat) per set (std::map order)."""
+        sets = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in desc_sets]
+        off = np.zeros(len(sets) + 1, np.int32)
+        off[1:] = np.cumsum([len(d) for d in sets])
+        total = int(off[-1])
+        desc = np.concatenate(sets) if total else np.zeros((1, 32), np.uint8)
+        m = max(total, 1)
+        bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
+        fn, fo, ff = np.zeros(m, np.uint32), np.zeros(m + len(sets), np.int32), np.zeros(m, np.int32)
+        nb, nf = np.zeros(len(sets), np.int32), np.zeros(len(sets), np.int32)
+        check(_lib.lib().orbx_voc_transform(self._h, ptr(desc), ptr(off), len(sets), int(levelsup), ptr(bw), ptr(bv),
+                                            ptr(nb), ptr(fn), ptr(fo), ptr(ff), ptr(nf)), "orbx_voc_transform")
+        out = []
+        for s in range(len(sets)):
+            o, b, q = int(off[s]), int(nb[s]), int(nf[s])
+            foff = fo[o + s:o + s + q + 1].copy()
+            out.append((bw[o:o + b].copy(), bv[o:o + b].copy(), fn[o:o + q].copy(), foff,
+                        ff[o:o + int(foff[-1] if q else 0)].copy()))
+        return out
+
+    def transform(self, desc, levelsup=4):
+        """(BowVector as (words, values), FeatureVector as CSR (nodes, off, feat))."""
+        return self.transform_sets([desc], levelsup)[0]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().orbx_voc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -249,3 +249,67 @@ def pnp_problem(seed=3, n=1200, outlier_frac=0.4, noise_px=1.0, z_range=(2.0, 20
     return dict(p3d=Xw.astype(np.float32), p2d=obs.astype(np.float32), sigma2=sigma2,
                 fx=np.float32(fx), fy=np.float32(fy), cx=np.float32(cx), cy=np.float32(cy),
                 R_true=R, t_true=t, outlier=out)
+
+
+def vocabulary(seed=5, k=10, L=4, scoring=0, weighting=0, flip_p=0.22, p_short=0.05, p_stop=0.03):
+    """Synthetic DBoW2 vocabulary in the text format of TemplatedVocabulary::saveToTextFile
+    (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1429-1455): header `k L scoring weighting`,
+    then one line per node in node-id order: `parent isLeaf d0 .. d31 weight`.  Node ids follow
+    DBoW2's HKmeansStep creation order (siblings consecutive, then depth first).  A child's
+    descriptor is its parent's with each bit flipped with probability flip_p; some branches end
+    early (fewer than k children, leaves above level L), some words are stopped (weight 0).
+    Returns (text, node descriptors [n,32] u8, leaf flags) -- ORBvoc.txt is not in the image."""
+    rng = np.random.default_rng(seed)
+    desc = [np.zeros(32, np.uint8)]
+    parent = [-1]
+    depth = [0]
+    children = [[]]
+
+    def make_children(nid):
+        kk = k if rng.random() > 0.15 else int(rng.integers(1, k + 1))
+        ids = []
+        for _ in range(kk):
+            bits = np.unpackbits(desc[nid]) if nid else rng.integers(0, 2, 256).astype(np.uint8)
+            flip = (rng.random(256) < (flip_p if nid else 0.5)).astype(np.uint8)
+            d = np.packbits(bits ^ flip)
+            desc.append(d)
+            parent.append(nid)
+            depth.append(depth[nid] + 1)
+            children.append([])
+            ids.append(len(desc) - 1)
+        children[nid].extend(ids)
+        for c in ids:
+            if depth[c] < L and not (depth[c] >= 2 and rng.random() < p_short):
+                make_children(c)
+
+    make_children(0)
+    lines = [f"{k} {L}  {scoring} {weighting}"]
+    leaf = np.zeros(len(desc), bool)
+    for nid in range(1, len(desc)):
+        is_leaf = not children[nid]
+        leaf[nid] = is_leaf
+        w = 0.0
+        if is_leaf and rng.random() > p_stop:
+            w = float(rng.uniform(0.2, 6.0))
+        lines.append(f"{parent[nid]} {1 if is_leaf else 0} " + " ".join(str(int(x)) for x in desc[nid]) +
+                     f" {w!r}")
+    return "\n".join(lines) + "\n", np.array(desc), leaf
+
+
+def voc_descriptors(seed, voc_desc, leaf, n=800, noise_bits=24, p_random=0.15, p_dup=0.1):
+    """Descriptors near random vocabulary leaves (noise_bits flipped), some uniform random, some
+    exact duplicates of earlier ones (same word twice)."""
+    rng = np.random.default_rng(seed)
+    leaves = np.flatnonzero(leaf)
+    out = np.zeros((n, 32), np.uint8)
+    for i in range(n):
+        r = rng.random()
+        if i and r < p_dup:
+            out[i] = out[rng.integers(0, i)]
+        elif r < p_dup + p_random:
+            out[i] = rng.integers(0, 256, 32, dtype=np.uint8)
+        else:
+            bits = np.unpackbits(voc_desc[rng.choice(leaves)])
+            bits[rng.choice(256, noise_bits, replace=False)] ^= 1
+            out[i] = np.packbits(bits)
+    return out
