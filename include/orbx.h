@@ -33,6 +33,9 @@
  *                                                               Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1420
  *   orbx_voc_transform          TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
  *                                                               :1125-1196, 1218-1259 (Frame::ComputeBoW src/Frame.cc:462-469)
+ *   orbx_search_by_projection   ORBmatcher::SearchByProjection x3 (+ Frame::isInFrustum, GetFeaturesInArea)
+ *                                                               src/ORBmatcher.cc:46-142, 1489-1795, include/ORBmatcher.h:64-95
+ *   orbx_search_by_projection_device   batch of the above (one block per problem)
  *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
  *                               (g2o graph build, optimize(5), outlier levels, optimize(10), vToErase;
  *                               the Map mutex/recovery part stays on the caller's side)
@@ -281,6 +284,82 @@ int32_t orbx_rand_next(orbx_rand_state* s);
  * reference would consume. */
 orbx_status orbx_pnp_iterate_stream(orbx_pnp* h, int n_iterations, orbx_rand_state* rng, int* no_more,
                                     float Tcw[16], uint8_t* inliers, int* n_inliers, int* found);
+
+/* ORBmatcher::SearchByProjection -- the three overloads run on every tracked
+ * frame -- with Frame::AssignFeaturesToGrid / GetFeaturesInArea
+ * (src/Frame.cc:254-271, 388-453) and, for the local map, Frame::isInFrustum
+ * (src/Frame.cc:315-375) fused in front:
+ *   ORBX_PROJ_LOCAL      SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+ *                                                   src/ORBmatcher.cc:46-142, include/ORBmatcher.h:64
+ *                        (frustum = 1: Tracking::SearchLocalPoints' isInFrustum(pMP, 0.5)
+ *                        loop first, src/Tracking.cc:1427-1443)
+ *   ORBX_PROJ_LAST_FRAME SearchByProjection(Frame&, const Frame&, th, bMono)
+ *                                                   src/ORBmatcher.cc:1489-1646, include/ORBmatcher.h:76
+ *   ORBX_PROJ_KEYFRAME   SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+ *                                                   src/ORBmatcher.cc:1648-1795, include/ORBmatcher.h:95
+ * The current Frame (orbx_proj_frame) and the projected MapPoints are SoA
+ * arrays the caller gathers from its object graph; the Frame's mvpMapPoints
+ * on entry is summarised per feature as occ[i]: 0 NULL, 1 a MapPoint with
+ * Observations() == 0, 2 a MapPoint with Observations() > 0. */
+#define ORBX_GRID_COLS 64 /* FRAME_GRID_COLS, include/Frame.h:39 */
+#define ORBX_GRID_ROWS 48 /* FRAME_GRID_ROWS, include/Frame.h:38 */
+#define ORBX_PROJ_LOCAL 0
+#define ORBX_PROJ_LAST_FRAME 1
+#define ORBX_PROJ_KEYFRAME 2
+#define ORBX_PROJ_MAX_FEATURES 8192 /* Frame::N per problem */
+
+typedef struct {
+  int n;                           /* N */
+  const orbx_keypoint* keys_un;    /* mvKeysUn (pt, octave, angle) */
+  const uint8_t* desc;             /* mDescriptors, n x 32 */
+  const float* u_right;            /* mvuRight, NULL = monocular (all -1) */
+  const int8_t* occ;               /* mvpMapPoints on entry (see above), NULL = all NULL */
+  float min_x, max_x, min_y, max_y;/* mnMinX, mnMaxX, mnMinY, mnMaxY */
+  float grid_inv_w, grid_inv_h;    /* mfGridElementWidthInv, mfGridElementHeightInv */
+  int nlevels;                     /* mnScaleLevels (<= 16) */
+  float scale_factors[16];         /* mvScaleFactors */
+  float log_scale_factor;          /* mfLogScaleFactor */
+  float fx, fy, cx, cy, bf, b;     /* fx, fy, cx, cy, mbf, mb */
+  float Tcw[16];                   /* mTcw, row-major 4x4 */
+} orbx_proj_frame;
+
+typedef struct {
+  int kind;                 /* ORBX_PROJ_* */
+  int frustum;              /* LOCAL: 1 = compute track[]/track_level[] by isInFrustum first */
+  orbx_proj_frame f;
+  int n_points;
+  const uint8_t* desc;      /* MapPoint::GetDescriptor(), n_points x 32 */
+  const uint8_t* flags;     /* bit0 = the point takes part (LOCAL: mbTrackInView && !isBad(), or with
+                               frustum: mnLastFrameSeen != mnId && !isBad(); LAST_FRAME: pMP &&
+                               !mvbOutlier[i]; KEYFRAME: pMP && !isBad() && !sAlreadyFound.count(pMP));
+                               bit1 = Observations() > 0 */
+  const float* pos;         /* GetWorldPos(), n_points x 3 (frustum, LAST_FRAME, KEYFRAME) */
+  const float* normal;      /* GetNormal(), n_points x 3 (frustum) */
+  const float* dist_minmax; /* mfMinDistance, mfMaxDistance, n_points x 2 (frustum, KEYFRAME) */
+  const float* angle;       /* LastFrame.mvKeysUn[i].angle / pKF->mvKeysUn[i].angle (LAST_FRAME, KEYFRAME) */
+  const int32_t* octave;    /* LastFrame.mvKeys[i].octave (LAST_FRAME) */
+  float* track;             /* LOCAL, n_points x 4: mTrackProjX, mTrackProjY, mTrackProjXR, mTrackViewCos
+                               (input, or output when frustum) */
+  int32_t* track_level;     /* LOCAL: mnTrackScaleLevel (input; with frustum output, -1 = not in view) */
+  float th;                 /* th */
+  float nnratio;            /* ORBmatcher mfNNratio (LOCAL) */
+  float view_cos_limit;     /* isInFrustum viewingCosLimit (0.5 in SearchLocalPoints) */
+  int check_ori;            /* ORBmatcher mbCheckOrientation (LAST_FRAME, KEYFRAME) */
+  int mono;                 /* bMono (LAST_FRAME) */
+  int orb_dist;             /* ORBdist (KEYFRAME) */
+  float last_Tcw[16];       /* LastFrame.mTcw (LAST_FRAME) */
+  int32_t* frame_out;       /* f.n: the Frame's mvpMapPoints on return: -1 unchanged by this call,
+                               -2 set to NULL by the rotation check, k >= 0 = point k */
+  int32_t* point_match;     /* n_points: feature index point k was assigned to (before the
+                               rotation check), -1 none */
+  int32_t* nmatches;        /* the reference's return value */
+} orbx_proj_problem;
+
+/* One problem; every pointer in *p is a HOST pointer (outputs are written back). */
+orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int device);
+/* Batched, device-resident: problems[] is a HOST array whose pointers are
+ * device pointers; one launch for the whole batch, stream-ordered. */
+orbx_status orbx_search_by_projection_device(const orbx_proj_problem* problems, int n, void* stream);
 
 /* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
  * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel

@@ -36,6 +36,24 @@ class BaResult(C.Structure):
                 ("Xw_d", C.c_void_p), ("iterations", C.c_int * 2), ("trials", C.c_int), ("chi2", C.c_double * 2)]
 
 
+class ProjFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
+                ("occ", C.c_void_p)] + [(k, C.c_float) for k in ("min_x", "max_x", "min_y", "max_y", "grid_inv_w",
+                                                                 "grid_inv_h")] + \
+               [("nlevels", C.c_int), ("scale_factors", C.c_float * 16)] + \
+               [(k, C.c_float) for k in ("log_scale_factor", "fx", "fy", "cx", "cy", "bf", "b")] + \
+               [("Tcw", C.c_float * 16)]
+
+
+class ProjProblem(C.Structure):
+    _fields_ = [("kind", C.c_int), ("frustum", C.c_int), ("f", ProjFrame), ("n_points", C.c_int)] + \
+               [(k, C.c_void_p) for k in ("desc", "flags", "pos", "normal", "dist_minmax", "angle", "octave",
+                                          "track", "track_level")] + \
+               [("th", C.c_float), ("nnratio", C.c_float), ("view_cos_limit", C.c_float), ("check_ori", C.c_int),
+                ("mono", C.c_int), ("orb_dist", C.c_int), ("last_Tcw", C.c_float * 16)] + \
+               [(k, C.c_void_p) for k in ("frame_out", "point_match", "nmatches")]
+
+
 _lib = None
 
 
@@ -90,6 +108,12 @@ def lib():
         L.oracle_voc_info.argtypes = [P, P]
         L.oracle_voc_info.restype = None
         L.oracle_voc_transform.argtypes = [P, P, C.c_int, C.c_int, P, P, P, P, P, P, P]
+        L.oracle_search_by_projection.argtypes = [C.POINTER(ProjProblem)]
+        L.oracle_log_det.argtypes = [C.c_float]
+        L.oracle_log_det.restype = C.c_float
+        L.oracle_predict_scale.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int]
+        L.oracle_features_in_area.argtypes = [C.POINTER(ProjFrame), C.c_float, C.c_float, C.c_float, C.c_int,
+                                              C.c_int, P, C.c_int]
         _lib = L
     return _lib
 
@@ -356,3 +380,73 @@ class Vocabulary:
         if getattr(self, "_h", None):
             lib().oracle_voc_free(self._h)
             self._h = None
+
+
+# ------------------------------------------------------------ SearchByProjection
+def _proj_frame(fr):
+    keep = dict(keys=np.ascontiguousarray(fr["keys_un"], KEYPOINT_DTYPE), desc=np.ascontiguousarray(fr["desc"], np.uint8),
+                ur=None if fr.get("u_right") is None else np.ascontiguousarray(fr["u_right"], np.float32),
+                occ=None if fr.get("occ") is None else np.ascontiguousarray(fr["occ"], np.int8))
+    f = ProjFrame()
+    f.n = len(keep["keys"])
+    f.keys_un, f.desc, f.u_right, f.occ = _p(keep["keys"]), _p(keep["desc"]), _p(keep["ur"]), _p(keep["occ"])
+    for k in ("min_x", "max_x", "min_y", "max_y", "grid_inv_w", "grid_inv_h", "log_scale_factor", "fx", "fy", "cx",
+              "cy", "bf", "b"):
+        setattr(f, k, float(fr[k]))
+    f.nlevels = int(fr["nlevels"])
+    for i in range(f.nlevels):
+        f.scale_factors[i] = float(fr["scale_factors"][i])
+    T = np.asarray(fr["Tcw"], np.float32).reshape(16)
+    for i in range(16):
+        f.Tcw[i] = float(T[i])
+    return f, keep
+
+
+def search_by_projection(frame, points, kind, th, nnratio=0.6, check_ori=True, mono=False, orb_dist=100,
+                         last_Tcw=None, frustum=False, view_cos_limit=0.5):
+    """Sequential reference of the three SearchByProjection overloads.  Returns dict(nmatches,
+    frame_out, point_match[, track, track_level])."""
+    f, keep = _proj_frame(frame)
+    n = len(points["desc"])
+    arr = {}
+    for k, dt, shape in (("desc", np.uint8, (n, 32)), ("flags", np.uint8, (n,)), ("pos", np.float32, (n, 3)),
+                         ("normal", np.float32, (n, 3)), ("dist_minmax", np.float32, (n, 2)),
+                         ("angle", np.float32, (n,)), ("octave", np.int32, (n,))):
+        arr[k] = None if points.get(k) is None else np.ascontiguousarray(points[k], dt).reshape(shape)
+    if kind == 0 and not frustum:
+        track = np.ascontiguousarray(points["track"], np.float32).copy()
+        level = np.ascontiguousarray(points["track_level"], np.int32).copy()
+    else:
+        track, level = np.zeros((n, 4), np.float32), np.zeros(n, np.int32)
+    out = dict(frame_out=np.zeros(f.n, np.int32), point_match=np.zeros(n, np.int32), nmatches=np.zeros(1, np.int32))
+    p = ProjProblem()
+    p.kind, p.frustum, p.f, p.n_points = kind, int(bool(frustum)), f, n
+    for k in ("desc", "flags", "pos", "normal", "dist_minmax", "angle", "octave"):
+        setattr(p, k, _p(arr[k]))
+    p.track, p.track_level = _p(track), _p(level)
+    p.th, p.nnratio, p.view_cos_limit = th, nnratio, view_cos_limit
+    p.check_ori, p.mono, p.orb_dist = int(bool(check_ori)), int(bool(mono)), int(orb_dist)
+    L = np.eye(4, dtype=np.float32).reshape(16) if last_Tcw is None else np.asarray(last_Tcw, np.float32).reshape(16)
+    for i in range(16):
+        p.last_Tcw[i] = float(L[i])
+    p.frame_out, p.point_match, p.nmatches = _p(out["frame_out"]), _p(out["point_match"]), _p(out["nmatches"])
+    nm = lib().oracle_search_by_projection(C.byref(p))
+    out["nmatches"] = int(nm)
+    if kind == 0:
+        out["track"], out["track_level"] = track, level
+    return out
+
+
+def features_in_area(frame, x, y, r, min_level=-1, max_level=-1):
+    f, keep = _proj_frame(frame)
+    buf = np.zeros(max(1, f.n), np.int32)
+    k = lib().oracle_features_in_area(C.byref(f), x, y, r, min_level, max_level, _p(buf), len(buf))
+    return buf[:k]
+
+
+def log_det(x):
+    return lib().oracle_log_det(float(x))
+
+
+def predict_scale(max_distance, dist, log_sf, nlevels):
+    return lib().oracle_predict_scale(float(max_distance), float(dist), float(log_sf), int(nlevels))

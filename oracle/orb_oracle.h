@@ -159,6 +159,50 @@ double oracle_epnp(const double* pws, const double* us, int n, double fu, double
 /* cvSVD probe on an m x n matrix (m >= n): left vectors as rows, w, Vt. */
 void oracle_svd(const double* A, int m, int n, double* Ut, double* w, double* Vt);
 
+/* SearchByProjection (src/ORBmatcher.cc:46-142, 1489-1646, 1648-1795); layout
+ * identical to orbx_proj_frame / orbx_proj_problem in include/orbx.h. */
+typedef struct {
+  int n;
+  const oracle_keypoint* keys_un;
+  const uint8_t* desc;
+  const float* u_right;
+  const int8_t* occ;
+  float min_x, max_x, min_y, max_y;
+  float grid_inv_w, grid_inv_h;
+  int nlevels;
+  float scale_factors[16];
+  float log_scale_factor;
+  float fx, fy, cx, cy, bf, b;
+  float Tcw[16];
+} oracle_proj_frame;
+
+typedef struct {
+  int kind, frustum;
+  oracle_proj_frame f;
+  int n_points;
+  const uint8_t* desc;
+  const uint8_t* flags;
+  const float* pos;
+  const float* normal;
+  const float* dist_minmax;
+  const float* angle;
+  const int32_t* octave;
+  float* track;
+  int32_t* track_level;
+  float th, nnratio, view_cos_limit;
+  int check_ori, mono, orb_dist;
+  float last_Tcw[16];
+  int32_t* frame_out;
+  int32_t* point_match;
+  int32_t* nmatches;
+} oracle_proj_problem;
+
+int oracle_search_by_projection(const oracle_proj_problem* p);
+float oracle_log_det(float x);
+int oracle_predict_scale(float max_distance, float dist, float log_sf, int nlevels);
+int oracle_features_in_area(const oracle_proj_frame* f, float x, float y, float r, int minLevel, int maxLevel,
+                            int32_t* out, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,25 @@ class PnpParams(C.Structure):
                 ("min_set", C.c_int), ("epsilon", C.c_float), ("th2", C.c_float)]
 
 
+class ProjFrame(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
+                ("occ", C.c_void_p), ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
+                ("max_y", C.c_float), ("grid_inv_w", C.c_float), ("grid_inv_h", C.c_float), ("nlevels", C.c_int),
+                ("scale_factors", C.c_float * 16), ("log_scale_factor", C.c_float), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float), ("b", C.c_float),
+                ("Tcw", C.c_float * 16)]
+
+
+class ProjProblem(C.Structure):
+    _fields_ = [("kind", C.c_int), ("frustum", C.c_int), ("f", ProjFrame), ("n_points", C.c_int),
+                ("desc", C.c_void_p), ("flags", C.c_void_p), ("pos", C.c_void_p), ("normal", C.c_void_p),
+                ("dist_minmax", C.c_void_p), ("angle", C.c_void_p), ("octave", C.c_void_p), ("track", C.c_void_p),
+                ("track_level", C.c_void_p), ("th", C.c_float), ("nnratio", C.c_float),
+                ("view_cos_limit", C.c_float), ("check_ori", C.c_int), ("mono", C.c_int), ("orb_dist", C.c_int),
+                ("last_Tcw", C.c_float * 16), ("frame_out", C.c_void_p), ("point_match", C.c_void_p),
+                ("nmatches", C.c_void_p)]
+
+
 class RandState(C.Structure):
     _fields_ = [("r", C.c_uint32 * 34), ("i", C.c_int32)]
 
@@ -106,6 +125,8 @@ SIGNATURES = {
     "orbx_voc_destroy": ([P], C.c_int),
     "orbx_voc_info": ([P, P], C.c_int),
     "orbx_voc_transform": ([P, P, P, C.c_int, C.c_int, P, P, P, P, P, P, P], C.c_int),
+    "orbx_search_by_projection": ([C.POINTER(ProjProblem), C.c_int], C.c_int),
+    "orbx_search_by_projection_device": ([C.POINTER(ProjProblem), C.c_int, P], C.c_int),
     "orbx_rand_seed": ([C.POINTER(RandState), C.c_uint32], None),
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),

@@ -1,0 +1,602 @@
+// projection.hip -- ORBmatcher::SearchByProjection, the three overloads run on
+// every tracked frame (src/ORBmatcher.cc:46-142 local map, :1489-1646 last
+// frame, :1648-1795 keyframe), with Frame::AssignFeaturesToGrid /
+// GetFeaturesInArea (src/Frame.cc:254-271, 388-453) and, for the local map,
+// Frame::isInFrustum (src/Frame.cc:315-375) fused in front.  One block per
+// problem (a Frame plus the MapPoints projected into it), batched.
+//
+// The reference walks the MapPoints in order and each match it makes can
+// hide a feature from every later MapPoint ("already has a MapPoint with
+// observations", :90-92 / :1574-1576 / :1732-1733).  Point k's result is a
+// function of the matches of points j < k only, so the sequential answer is
+// the unique fixed point of
+//     match_k = search(k, taken_k),  taken_k(f) = occ(f) || first_writer(f) < k
+// where first_writer(f) is the smallest blocking point matched to f.  The
+// block evaluates every point in parallel against the previous sweep's
+// first_writer table and repeats until no match changes: after sweep s the
+// first s points are final, so the loop ends, and an unchanged sweep is the
+// fixed point -- bit-identical to the sequential scan, usually in 2-3 sweeps.
+//
+// Grid: the reference's 64x48 cells hold feature indices in ascending order
+// and GetFeaturesInArea enumerates (cell x, cell y, index).  Sorting the keys
+// (x*48 + y) << 13 | index makes that enumeration order the sorted position,
+// and for one x the cells y0..y1 are one contiguous range.  Best/second-best
+// with the reference's "first candidate wins" ties is then a min over 32-bit
+// keys dist << 16 | position.
+//
+// Roofline: per candidate ~52 B (descriptor 32, keypoint x/y/octave 12,
+// mvuRight 4, occ 1) from L2-resident frame arrays; per point 32 B descriptor
+// + 16-40 B of geometry.  Latency-bound per block (a few hundred dependent
+// loads per point group), so the batch is the unit of throughput.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstring>
+#include <vector>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+#include "orbx_proj.h"
+
+namespace orbx {
+
+constexpr int PBS = 1024;         // threads per problem block
+constexpr int kGroup = 16;        // lanes per MapPoint
+constexpr int kCells = ORBX_GRID_COLS * ORBX_GRID_ROWS;
+constexpr int kMaxF = ORBX_PROJ_MAX_FEATURES;  // 8192 = 2^13
+constexpr int kThHigh = 100;
+
+// Deterministic natural log rounded to float (same operation sequence as the
+// oracle's log_det): frexp, 2*atanh series to s^25.
+__device__ float log_det(float xf) {
+  if (!(xf > 0.0f)) return xf == 0.0f ? -__builtin_inff() : __builtin_nanf("");
+  if (__builtin_isinf(xf)) return __builtin_inff();
+  int e;
+  double m = __builtin_frexp((double)xf, &e);
+  if (m < 0.70710678118654752440) {
+    m = m * 2.0;
+    e -= 1;
+  }
+  const double s = (m - 1.0) / (m + 1.0);
+  const double s2 = s * s;
+  double p = 1.0 / 25.0;
+#pragma unroll
+  for (int k = 23; k >= 1; k -= 2) p = p * s2 + 1.0 / (double)k;
+  const double lm = 2.0 * s * p;
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  return (float)((double)e * ln2_hi + ((double)e * ln2_lo + lm));
+}
+
+// MapPoint::PredictScale(dist, Frame*), src/MapPoint.cc:424-440
+__device__ int predict_scale(float max_distance, float dist, float log_sf, int nlevels) {
+  const float ratio = max_distance / dist;
+  const float q = log_det(ratio) / log_sf;
+  int n;
+  if (q != q) n = 0;
+  else if (q > 1e6f) n = nlevels - 1;
+  else if (q < -1e6f) n = 0;
+  else n = (int)__builtin_ceilf(q);
+  if (n < 0) n = 0;
+  else if (n >= nlevels) n = nlevels - 1;
+  return n;
+}
+
+// cv::gemm 32F (double accumulation, one rounding): R*X + t and -R^T t
+__device__ __forceinline__ void mat3x1(const float* T, const float* X, float* out) {
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    double s = (double)T[4 * r + 0] * X[0];
+    s = s + (double)T[4 * r + 1] * X[1];
+    s = s + (double)T[4 * r + 2] * X[2];
+    out[r] = (float)(s + (double)T[4 * r + 3]);
+  }
+}
+__device__ __forceinline__ void camera_centre(const float* T, float* Ow) {
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    double s = (double)T[c] * T[3];
+    s = s + (double)T[4 + c] * T[7];
+    s = s + (double)T[8 + c] * T[11];
+    Ow[c] = (float)(-s);
+  }
+}
+__device__ __forceinline__ float norm3(const float* v) {
+  double s = (double)v[0] * v[0];
+  s = s + (double)v[1] * v[1];
+  s = s + (double)v[2] * v[2];
+  return (float)__builtin_sqrt(s);
+}
+
+__device__ __forceinline__ int rot_bin(float a, float b) {
+  float rot = a - b;
+  if (rot < 0.0) rot += 360.0f;
+  int bin = (int)__builtin_roundf(rot * (1.0f / 30));
+  if (bin == 30) bin = 0;
+  return bin;
+}
+
+// The per-point search window (everything the reference derives before its
+// candidate loop).
+struct Query {
+  bool active;
+  float x, y, r;      // GetFeaturesInArea centre and half-size
+  int min_level, max_level;
+  float ur, ur_th;    // stereo check |ur - mvuRight| > ur_th (ur_th < 0: no check)
+  int th;             // accept bestDist <= th
+};
+
+__device__ Query setup_query(const ProjProblem& P, int i, const float* Ow, bool fwd, bool bwd) {
+  Query q;
+  q.active = false;
+  const orbx_proj_frame& F = P.f;
+  const uint8_t fl = P.flags[i];
+  if (P.kind == ORBX_PROJ_LOCAL) {
+    const int lvl = P.track_level[i];
+    if (P.frustum ? lvl < 0 : !(fl & 1)) return q;
+    if (lvl < 0 || lvl >= F.nlevels) return q;
+    const float* tr = P.track + 4 * i;
+    float r = tr[3] > 0.998f ? 2.5f : 4.0f;  // RadiusByViewingCos, src/ORBmatcher.cc:145-151
+    if (P.th != 1.0f) r *= P.th;
+    q.r = r * F.scale_factors[lvl];
+    q.x = tr[0];
+    q.y = tr[1];
+    q.min_level = lvl - 1;
+    q.max_level = lvl;
+    q.ur = tr[2];
+    q.ur_th = q.r;
+    q.th = kThHigh;
+    q.active = true;
+    return q;
+  }
+  if (!(fl & 1)) return q;
+  const float* X = P.pos + 3 * i;
+  float c[3];
+  mat3x1(F.Tcw, X, c);
+  const float invzc = (float)(1.0 / (double)c[2]);
+  if (P.kind == ORBX_PROJ_LAST_FRAME && invzc < 0) return q;
+  const float u = F.fx * c[0] * invzc + F.cx;
+  const float v = F.fy * c[1] * invzc + F.cy;
+  if (u != u || v != v) return q;  // 0 * inf: undefined in the reference
+  if (u < F.min_x || u > F.max_x) return q;
+  if (v < F.min_y || v > F.max_y) return q;
+  q.x = u;
+  q.y = v;
+  if (P.kind == ORBX_PROJ_LAST_FRAME) {
+    const int o = P.octave[i];
+    if (o < 0 || o >= F.nlevels) return q;
+    q.r = P.th * F.scale_factors[o];
+    if (fwd) {
+      q.min_level = o;
+      q.max_level = -1;
+    } else if (bwd) {
+      q.min_level = 0;
+      q.max_level = o;
+    } else {
+      q.min_level = o - 1;
+      q.max_level = o + 1;
+    }
+    q.ur = u - F.bf * invzc;
+    q.ur_th = q.r;
+    q.th = kThHigh;
+  } else {
+    const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+    const float d3 = norm3(PO);
+    const float dmin = P.dist_minmax[2 * i], dmax = P.dist_minmax[2 * i + 1];
+    if (d3 < 0.8f * dmin || d3 > 1.2f * dmax) return q;
+    const int lvl = predict_scale(dmax, d3, F.log_scale_factor, F.nlevels);
+    q.r = P.th * F.scale_factors[lvl];
+    q.min_level = lvl - 1;
+    q.max_level = lvl + 1;
+    q.ur_th = -1.0f;
+    q.th = P.orb_dist;
+  }
+  q.active = true;
+  return q;
+}
+
+__device__ __forceinline__ uint32_t group_min(uint32_t v) {
+#pragma unroll
+  for (int o = kGroup / 2; o > 0; o >>= 1) {
+    const uint32_t w = __shfl_xor(v, o, kGroup);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem* __restrict__ probs) {
+  __shared__ uint32_t s_keys[kMaxF];  // grid sort keys, then first-writer / final occupant table
+  __shared__ uint16_t s_pos[kMaxF];   // sorted position -> feature index
+  __shared__ int s_start[kCells + 1];
+  __shared__ int s_hist[32];
+  __shared__ int s_sel[3];
+  __shared__ int s_changed, s_count, s_drop;
+  const ProjProblem& P = probs[blockIdx.x];
+  const orbx_proj_frame& F = P.f;
+  const int tid = threadIdx.x;
+  const int nF = F.n, nP = P.n_points;
+  int* s_fw = (int*)s_keys;
+
+  // ---- Frame::AssignFeaturesToGrid as a sort of (cell << 13 | index) ----
+  int nsort = 1;
+  while (nsort < nF) nsort <<= 1;
+  for (int i = tid; i < nsort; i += PBS) {
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < nF) {
+      const orbx_keypoint kp = F.keys_un[i];
+      const int px = (int)__builtin_roundf((kp.x - F.min_x) * F.grid_inv_w);
+      const int py = (int)__builtin_roundf((kp.y - F.min_y) * F.grid_inv_h);
+      if (px >= 0 && px < ORBX_GRID_COLS && py >= 0 && py < ORBX_GRID_ROWS)
+        key = ((uint32_t)(px * ORBX_GRID_ROWS + py) << 13) | (uint32_t)i;
+    }
+    s_keys[i] = key;
+  }
+  __syncthreads();
+  for (int k = 2; k <= nsort; k <<= 1) {  // bitonic sort, ascending
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < (nsort >> 1); t += PBS) {
+        const int lo = 2 * t - (t & (j - 1));
+        const int hi = lo + j;
+        const uint32_t a = s_keys[lo], b = s_keys[hi];
+        const bool up = (lo & k) == 0;
+        if ((a > b) == up) {
+          s_keys[lo] = b;
+          s_keys[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int c = tid; c <= kCells; c += PBS) {  // s_start[c] = lower_bound(c << 13)
+    const uint32_t target = (uint32_t)c << 13;
+    int lo = 0, hi = nsort;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (s_keys[m] < target) lo = m + 1; else hi = m;
+    }
+    s_start[c] = lo;
+  }
+  for (int i = tid; i < nF; i += PBS) s_pos[i] = (uint16_t)(s_keys[i] & 0x1FFF);
+  if (tid < 32) s_hist[tid] = 0;
+  __syncthreads();
+
+  float Ow[3];
+  camera_centre(F.Tcw, Ow);
+  bool fwd = false, bwd = false;
+  if (P.kind == ORBX_PROJ_LAST_FRAME) {
+    float tlc[3];
+    mat3x1(P.last_Tcw, Ow, tlc);  // twc = Ow
+    fwd = tlc[2] > F.b && !P.mono;
+    bwd = -tlc[2] > F.b && !P.mono;
+  }
+
+  // ---- Tracking::SearchLocalPoints: isInFrustum(pMP, limit) for every point ----
+  if (P.kind == ORBX_PROJ_LOCAL && P.frustum) {
+    for (int i = tid; i < nP; i += PBS) {
+      int lvl = -1;
+      float* tr = P.track + 4 * i;
+      if (P.flags[i] & 1) {
+        const float* X = P.pos + 3 * i;
+        float c[3];
+        mat3x1(F.Tcw, X, c);
+        if (!(c[2] < 0.0f)) {
+          const float invz = 1.0f / c[2];
+          const float u = F.fx * c[0] * invz + F.cx;
+          const float v = F.fy * c[1] * invz + F.cy;
+          if (!(u < F.min_x || u > F.max_x) && !(v < F.min_y || v > F.max_y) && u == u && v == v) {
+            const float dmin = P.dist_minmax[2 * i], dmax = P.dist_minmax[2 * i + 1];
+            const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+            const float dist = norm3(PO);
+            if (!(dist < 0.8f * dmin || dist > 1.2f * dmax)) {
+              const float* Pn = P.normal + 3 * i;
+              double dot = (double)PO[0] * Pn[0];
+              dot = dot + (double)PO[1] * Pn[1];
+              dot = dot + (double)PO[2] * Pn[2];
+              const float vc = (float)(dot / dist);
+              if (!(vc < P.view_cos_limit)) {
+                lvl = predict_scale(dmax, dist, F.log_scale_factor, F.nlevels);
+                tr[0] = u;
+                tr[1] = v;
+                tr[2] = u - F.bf * invz;
+                tr[3] = vc;
+              }
+            }
+          }
+        }
+      }
+      P.track_level[i] = lvl;
+    }
+    __threadfence_block();
+  }
+  for (int i = tid; i < nF; i += PBS) s_fw[i] = INT_MAX;
+  __syncthreads();
+
+  // ---- sweeps to the sequential fixed point ----
+  const int g = tid / kGroup, gl = tid % kGroup;
+  constexpr int kGroups = PBS / kGroup;
+  const bool local = P.kind == ORBX_PROJ_LOCAL;
+  const bool kf = P.kind == ORBX_PROJ_KEYFRAME;
+  for (int sweep = 0; sweep <= nP + 1; sweep++) {
+    if (tid == 0) s_changed = 0;
+    __syncthreads();
+    int changed = 0;
+    for (int i = g; i < nP; i += kGroups) {
+      const Query q = setup_query(P, i, Ow, fwd, bwd);
+      int m = -1;
+      if (q.active) {
+        uint64_t dq[4];
+        {
+          const uint64_t* d = (const uint64_t*)(P.desc + (size_t)i * 32);
+          dq[0] = d[0]; dq[1] = d[1]; dq[2] = d[2]; dq[3] = d[3];
+        }
+        uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+        int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+        {  // Frame::GetFeaturesInArea cell range, src/Frame.cc:395-413
+          x0 = max(0, (int)__builtin_floorf((q.x - F.min_x - q.r) * F.grid_inv_w));
+          x1 = min(ORBX_GRID_COLS - 1, (int)__builtin_ceilf((q.x - F.min_x + q.r) * F.grid_inv_w));
+          y0 = max(0, (int)__builtin_floorf((q.y - F.min_y - q.r) * F.grid_inv_h));
+          y1 = min(ORBX_GRID_ROWS - 1, (int)__builtin_ceilf((q.y - F.min_y + q.r) * F.grid_inv_h));
+          if (x0 >= ORBX_GRID_COLS || x1 < 0 || y0 >= ORBX_GRID_ROWS || y1 < 0) x1 = x0 - 1;
+        }
+        const bool check = q.min_level > 0 || q.max_level >= 0;
+        for (int ix = x0; ix <= x1; ix++) {
+          const int c0 = ix * ORBX_GRID_ROWS;
+          const int pend = s_start[c0 + y1 + 1];
+          for (int p = s_start[c0 + y0] + gl; p < pend; p += kGroup) {
+            const int idx = s_pos[p];
+            const orbx_keypoint& kp = F.keys_un[idx];
+            const int oct = kp.octave;
+            if (check && (oct < q.min_level || (q.max_level >= 0 && oct > q.max_level))) continue;
+            const float dx = kp.x - q.x, dy = kp.y - q.y;
+            if (!(__builtin_fabsf(dx) < q.r && __builtin_fabsf(dy) < q.r)) continue;
+            const int o = F.occ ? F.occ[idx] : 0;
+            if ((kf ? o != 0 : o == 2) || s_fw[idx] < i) continue;
+            if (q.ur_th >= 0.0f && F.u_right) {
+              const float urf = F.u_right[idx];
+              if (urf > 0 && __builtin_fabsf(q.ur - urf) > q.ur_th) continue;
+            }
+            const uint64_t* d = (const uint64_t*)(F.desc + (size_t)idx * 32);
+            const uint64_t x[4] = {d[0], d[1], d[2], d[3]};
+            const uint32_t key = ((uint32_t)hamming256(dq, x) << 16) | (uint32_t)p;
+            if (key < m1) {
+              m2 = m1;
+              m1 = key;
+            } else if (key < m2) {
+              m2 = key;
+            }
+          }
+        }
+        const uint32_t b1 = group_min(m1);
+        const uint32_t b2 = group_min(m1 == b1 ? m2 : m1);
+        if (b1 != 0xFFFFFFFFu) {
+          const int d1 = (int)(b1 >> 16);
+          if (d1 <= q.th) {
+            const int i1 = s_pos[b1 & 0xFFFF];
+            bool ok = true;
+            if (local) {  // ratio only when best and second share a level, src/ORBmatcher.cc:127-131
+              const int l1 = F.keys_un[i1].octave;
+              const int l2 = b2 == 0xFFFFFFFFu ? -1 : F.keys_un[s_pos[b2 & 0xFFFF]].octave;
+              const int d2 = b2 == 0xFFFFFFFFu ? 256 : (int)(b2 >> 16);
+              if (l1 == l2 && (float)d1 > P.nnratio * (float)d2) ok = false;
+            }
+            if (ok) m = i1;
+          }
+        }
+      }
+      if (gl == 0) {
+        if (sweep == 0 || P.point_match[i] != m) changed = 1;
+        P.point_match[i] = m;
+      }
+    }
+    if (changed) s_changed = 1;
+    __threadfence_block();
+    __syncthreads();
+    if (!s_changed) break;
+    // first blocking writer per feature from this sweep's matches
+    for (int f = tid; f < nF; f += PBS) s_fw[f] = INT_MAX;
+    __syncthreads();
+    for (int i = tid; i < nP; i += PBS) {
+      const int m = P.point_match[i];
+      if (m >= 0 && (kf || (P.flags[i] & 2))) atomicMin(&s_fw[m], i);
+    }
+    __syncthreads();
+  }
+
+  // ---- final occupant (last writer), rotation consistency, count ----
+  for (int f = tid; f < nF; f += PBS) s_fw[f] = -1;
+  if (tid == 0) {
+    s_count = 0;
+    s_drop = 0;
+  }
+  __syncthreads();
+  const bool rot = !local && P.check_ori;
+  int cnt = 0;
+  for (int i = tid; i < nP; i += PBS) {
+    const int m = P.point_match[i];
+    if (m < 0) continue;
+    cnt++;
+    atomicMax(&s_fw[m], i);
+    if (rot) atomicAdd(&s_hist[rot_bin(P.angle[i], F.keys_un[m].angle)], 1);
+  }
+  atomicAdd(&s_count, cnt);
+  __syncthreads();
+  if (rot && tid == 0) {  // ComputeThreeMaxima, src/ORBmatcher.cc:1797-1839
+    int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+    for (int b = 0; b < 30; b++) {
+      const int s = s_hist[b];
+      if (s > m1) {
+        m3 = m2; m2 = m1; m1 = s;
+        i3 = i2; i2 = i1; i1 = b;
+      } else if (s > m2) {
+        m3 = m2; m2 = s;
+        i3 = i2; i2 = b;
+      } else if (s > m3) {
+        m3 = s;
+        i3 = b;
+      }
+    }
+    if (m2 < 0.1f * (float)m1) {
+      i2 = -1;
+      i3 = -1;
+    } else if (m3 < 0.1f * (float)m1) {
+      i3 = -1;
+    }
+    s_sel[0] = i1;
+    s_sel[1] = i2;
+    s_sel[2] = i3;
+  }
+  __syncthreads();
+  if (rot) {
+    int drop = 0;
+    for (int i = tid; i < nP; i += PBS) {
+      const int m = P.point_match[i];
+      if (m < 0) continue;
+      const int b = rot_bin(P.angle[i], F.keys_un[m].angle);
+      if (b != s_sel[0] && b != s_sel[1] && b != s_sel[2]) {
+        s_fw[m] = -2;  // mvpMapPoints[bestIdx2] = NULL
+        drop++;
+      }
+    }
+    atomicAdd(&s_drop, drop);
+    __syncthreads();
+  }
+  for (int f = tid; f < nF; f += PBS) P.frame_out[f] = s_fw[f];
+  if (tid == 0) *P.nmatches = s_count - s_drop;
+}
+
+hipError_t launch_search_by_projection(const ProjProblem* d_probs, int n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_search_by_projection, dim3(n), dim3(PBS), 0, st, d_probs);
+  return hipGetLastError();
+}
+
+}  // namespace orbx
+
+// ------------------------------------------------------------------ C ABI
+namespace {
+
+orbx_status proj_status(hipError_t e) { return e == hipSuccess ? ORBX_OK : ORBX_ERR_HIP; }
+
+// Host-side argument checks shared by both entry points (the kernel assumes them).
+orbx_status proj_check(const orbx_proj_problem& p, bool host) {
+  if (p.kind < ORBX_PROJ_LOCAL || p.kind > ORBX_PROJ_KEYFRAME) return ORBX_ERR_ARG;
+  if (p.f.n < 0 || p.n_points < 0) return ORBX_ERR_ARG;
+  if (p.f.n > ORBX_PROJ_MAX_FEATURES) return ORBX_ERR_CAPACITY;
+  if (p.f.nlevels < 1 || p.f.nlevels > 16) return ORBX_ERR_ARG;
+  if (!p.frame_out || !p.point_match || !p.nmatches) return ORBX_ERR_ARG;
+  if (p.f.n > 0 && (!p.f.keys_un || !p.f.desc)) return ORBX_ERR_ARG;
+  if (p.n_points > 0) {
+    if (!p.desc || !p.flags) return ORBX_ERR_ARG;
+    switch (p.kind) {
+      case ORBX_PROJ_LOCAL:
+        if (!p.track || !p.track_level) return ORBX_ERR_ARG;
+        if (p.frustum && (!p.pos || !p.normal || !p.dist_minmax)) return ORBX_ERR_ARG;
+        if (host && !p.frustum)
+          for (int i = 0; i < p.n_points; i++)
+            if ((p.flags[i] & 1) && (p.track_level[i] < 0 || p.track_level[i] >= p.f.nlevels)) return ORBX_ERR_ARG;
+        break;
+      case ORBX_PROJ_LAST_FRAME:
+        if (!p.pos || !p.octave || (p.check_ori && !p.angle)) return ORBX_ERR_ARG;
+        if (host)
+          for (int i = 0; i < p.n_points; i++)
+            if ((p.flags[i] & 1) && (p.octave[i] < 0 || p.octave[i] >= p.f.nlevels)) return ORBX_ERR_ARG;
+        break;
+      default:
+        if (!p.pos || !p.dist_minmax || (p.check_ori && !p.angle)) return ORBX_ERR_ARG;
+    }
+  }
+  return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int device) {
+  if (!p) return ORBX_ERR_ARG;
+  const orbx_status chk = proj_check(*p, true);
+  if (chk != ORBX_OK) return chk;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_NODEV;
+  if (device < 0 || device >= ndev || hipSetDevice(device) != hipSuccess) return ORBX_ERR_ARG;
+  const size_t nF = (size_t)p->f.n, nP = (size_t)p->n_points;
+  const bool local = p->kind == ORBX_PROJ_LOCAL;
+  // one arena: inputs, outputs, problem descriptor
+  std::vector<uint8_t> host;
+  size_t off = 0;
+  struct Item { const void* src; size_t bytes; size_t at; };
+  std::vector<Item> items;
+  auto reserve = [&](const void* src, size_t bytes) -> size_t {
+    off = (off + 255) & ~(size_t)255;
+    items.push_back({src, bytes, off});
+    const size_t at = off;
+    off += bytes;
+    return at;
+  };
+  const size_t a_keys = reserve(p->f.keys_un, nF * sizeof(orbx_keypoint));
+  const size_t a_fdesc = reserve(p->f.desc, nF * 32);
+  const size_t a_ur = p->f.u_right ? reserve(p->f.u_right, nF * 4) : 0;
+  const size_t a_occ = p->f.occ ? reserve(p->f.occ, nF) : 0;
+  const size_t a_desc = reserve(p->desc, nP * 32);
+  const size_t a_flags = reserve(p->flags, nP);
+  const size_t a_pos = p->pos ? reserve(p->pos, nP * 12) : 0;
+  const size_t a_nrm = p->normal ? reserve(p->normal, nP * 12) : 0;
+  const size_t a_dmm = p->dist_minmax ? reserve(p->dist_minmax, nP * 8) : 0;
+  const size_t a_ang = p->angle ? reserve(p->angle, nP * 4) : 0;
+  const size_t a_oct = p->octave ? reserve(p->octave, nP * 4) : 0;
+  const size_t a_trk = local ? reserve(p->frustum ? nullptr : p->track, nP * 16) : 0;
+  const size_t a_lvl = local ? reserve(p->frustum ? nullptr : p->track_level, nP * 4) : 0;
+  const size_t a_fout = reserve(nullptr, nF * 4);
+  const size_t a_pm = reserve(nullptr, nP * 4);
+  const size_t a_nm = reserve(nullptr, 4);
+  const size_t a_prob = reserve(nullptr, sizeof(orbx_proj_problem));
+  host.assign(off, 0);
+  for (const Item& it : items)
+    if (it.src && it.bytes) std::memcpy(host.data() + it.at, it.src, it.bytes);
+  uint8_t* d = nullptr;
+  if (hipMalloc((void**)&d, off) != hipSuccess) return ORBX_ERR_HIP;
+  orbx_proj_problem q = *p;
+  q.f.keys_un = (const orbx_keypoint*)(d + a_keys);
+  q.f.desc = d + a_fdesc;
+  q.f.u_right = p->f.u_right ? (const float*)(d + a_ur) : nullptr;
+  q.f.occ = p->f.occ ? (const int8_t*)(d + a_occ) : nullptr;
+  q.desc = d + a_desc;
+  q.flags = d + a_flags;
+  q.pos = p->pos ? (const float*)(d + a_pos) : nullptr;
+  q.normal = p->normal ? (const float*)(d + a_nrm) : nullptr;
+  q.dist_minmax = p->dist_minmax ? (const float*)(d + a_dmm) : nullptr;
+  q.angle = p->angle ? (const float*)(d + a_ang) : nullptr;
+  q.octave = p->octave ? (const int32_t*)(d + a_oct) : nullptr;
+  q.track = local ? (float*)(d + a_trk) : nullptr;
+  q.track_level = local ? (int32_t*)(d + a_lvl) : nullptr;
+  q.frame_out = (int32_t*)(d + a_fout);
+  q.point_match = (int32_t*)(d + a_pm);
+  q.nmatches = (int32_t*)(d + a_nm);
+  std::memcpy(host.data() + a_prob, &q, sizeof(q));
+  hipError_t e = hipMemcpy(d, host.data(), off, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = orbx::launch_search_by_projection((const orbx::ProjProblem*)(d + a_prob), 1, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(host.data(), d, off, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return proj_status(e);
+  if (nF) std::memcpy(p->frame_out, host.data() + a_fout, nF * 4);
+  if (nP) std::memcpy(p->point_match, host.data() + a_pm, nP * 4);
+  std::memcpy(p->nmatches, host.data() + a_nm, 4);
+  if (local && p->frustum && nP) {
+    std::memcpy(p->track, host.data() + a_trk, nP * 16);
+    std::memcpy(p->track_level, host.data() + a_lvl, nP * 4);
+  }
+  return ORBX_OK;
+}
+
+extern "C" orbx_status orbx_search_by_projection_device(const orbx_proj_problem* problems, int n, void* stream) {
+  if (n < 0 || (n > 0 && !problems)) return ORBX_ERR_ARG;
+  if (n == 0) return ORBX_OK;
+  for (int i = 0; i < n; i++) {
+    const orbx_status s = proj_check(problems[i], false);
+    if (s != ORBX_OK) return s;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  orbx::ProjProblem* dP = nullptr;
+  if (hipMallocAsync((void**)&dP, sizeof(orbx::ProjProblem) * n, st) != hipSuccess) return ORBX_ERR_HIP;
+  hipError_t e = hipMemcpyAsync(dP, problems, sizeof(orbx::ProjProblem) * n, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = orbx::launch_search_by_projection(dP, n, st);
+  const hipError_t e2 = hipFreeAsync(dP, st);
+  return proj_status(e != hipSuccess ? e : e2);
+}

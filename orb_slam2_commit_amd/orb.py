@@ -204,6 +204,34 @@ class ORBmatcher:
                  C.byref(n), self.device), "orbx_search_by_bow")
         return match, n.value
 
+    def SearchByProjection(self, F, vpMapPoints, th=3.0, frustum=False, viewingCosLimit=0.5):
+        """SearchByProjection(Frame&, const vector<MapPoint*>&, th) -- src/ORBmatcher.cc:46-142.
+
+        F: frame dict (synth.projection_frame layout); vpMapPoints: points dict with the track
+        fields (track = mTrackProjX/Y/XR/ViewCos, track_level) or, with frustum=True, the
+        isInFrustum inputs (pos, normal, dist_minmax) of Tracking::SearchLocalPoints.  Returns
+        (nmatches, frame_out, point_match[, track, track_level]); frame_out[i] = point now held by
+        feature i, -1 unchanged."""
+        o = _run_projection(self, F, vpMapPoints, PROJ_LOCAL, th=th, frustum=frustum,
+                            view_cos_limit=viewingCosLimit)
+        res = (int(o["nmatches"][0]), o["frame_out"], o["point_match"])
+        return res + ((o["track"], o["track_level"]) if frustum else ())
+
+    def SearchByProjectionLastFrame(self, CurrentFrame, LastFramePoints, LastTcw, th, bMono):
+        """SearchByProjection(Frame&, const Frame&, th, bMono) -- src/ORBmatcher.cc:1489-1646.
+        LastFramePoints: the last frame's MapPoints (pos, desc, octave, angle, flags bit0 =
+        pMP && !mvbOutlier, bit1 = Observations() > 0).  frame_out[i] = -2 where the rotation
+        check reset the feature to NULL."""
+        o = _run_projection(self, CurrentFrame, LastFramePoints, PROJ_LAST_FRAME, th=th, mono=bMono,
+                            last_Tcw=LastTcw)
+        return int(o["nmatches"][0]), o["frame_out"], o["point_match"]
+
+    def SearchByProjectionKeyFrame(self, CurrentFrame, KFPoints, th, ORBdist):
+        """SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>& sAlreadyFound, th, ORBdist) --
+        src/ORBmatcher.cc:1648-1795.  KFPoints flags bit0 = pMP && !isBad() && not already found."""
+        o = _run_projection(self, CurrentFrame, KFPoints, PROJ_KEYFRAME, th=th, orb_dist=ORBdist)
+        return int(o["nmatches"][0]), o["frame_out"], o["point_match"]
+
     @staticmethod
     def DescriptorDistance(a, b):
         """Hamming distance of 32-byte descriptors; a, b: [32] or [n,32] uint8 (computed on the GPU)."""
@@ -220,6 +248,84 @@ class ORBmatcher:
               "orbx_descriptor_distance_device")
         d = out.cpu().numpy()
         return int(d[0]) if n == 1 else d
+
+
+PROJ_LOCAL, PROJ_LAST_FRAME, PROJ_KEYFRAME = 0, 1, 2
+
+
+def _f32(x):
+    return np.ascontiguousarray(x, np.float32)
+
+
+def proj_problem(frame, points, kind, th, nnratio=0.6, check_ori=True, mono=False, orb_dist=100, last_Tcw=None,
+                 frustum=False, view_cos_limit=0.5, outputs=None):
+    """Fill an orbx_proj_problem from a frame dict and a points dict (synth.projection_frame /
+    projection_points layout).  Arrays may be host numpy arrays (for orbx_search_by_projection) or
+    device tensors (for orbx_search_by_projection_device); the caller keeps them alive.  `outputs`
+    = dict(frame_out, point_match, nmatches[, track, track_level]); numpy arrays are allocated when
+    absent.  Returns (problem, outputs)."""
+    n, npnt = len(frame["desc"]), len(points["desc"])
+    if outputs is None:
+        outputs = dict(frame_out=np.zeros(n, np.int32), point_match=np.zeros(npnt, np.int32),
+                       nmatches=np.zeros(1, np.int32))
+        if kind == PROJ_LOCAL:
+            outputs["track"] = (np.zeros((npnt, 4), np.float32) if frustum
+                                else np.ascontiguousarray(points["track"], np.float32))
+            outputs["track_level"] = (np.zeros(npnt, np.int32) if frustum
+                                      else np.ascontiguousarray(points["track_level"], np.int32))
+    f = _lib.ProjFrame()
+    f.n = n
+    f.keys_un, f.desc = ptr(frame["keys_un"]), ptr(frame["desc"])
+    f.u_right = ptr(frame.get("u_right"))
+    f.occ = ptr(frame.get("occ"))
+    for k in ("min_x", "max_x", "min_y", "max_y", "grid_inv_w", "grid_inv_h", "log_scale_factor", "fx", "fy",
+              "cx", "cy", "bf", "b"):
+        setattr(f, k, float(frame[k]))
+    f.nlevels = int(frame["nlevels"])
+    sf = np.zeros(16, np.float32)
+    sf[:f.nlevels] = frame["scale_factors"][:f.nlevels]
+    f.scale_factors[:] = sf.tolist()
+    f.Tcw[:] = _f32(frame["Tcw"]).reshape(16).tolist()
+    p = _lib.ProjProblem()
+    p.kind, p.frustum, p.f, p.n_points = int(kind), int(bool(frustum)), f, npnt
+    p.desc, p.flags = ptr(points["desc"]), ptr(points["flags"])
+    for k in ("pos", "normal", "dist_minmax", "angle", "octave"):
+        setattr(p, k, ptr(points.get(k)))
+    p.track = ptr(outputs.get("track"))
+    p.track_level = ptr(outputs.get("track_level"))
+    p.th, p.nnratio, p.view_cos_limit = float(th), float(nnratio), float(view_cos_limit)
+    p.check_ori, p.mono, p.orb_dist = int(bool(check_ori)), int(bool(mono)), int(orb_dist)
+    p.last_Tcw[:] = (_f32(last_Tcw).reshape(16) if last_Tcw is not None else np.eye(4, dtype=np.float32).reshape(16)).tolist()
+    p.frame_out, p.point_match, p.nmatches = (ptr(outputs["frame_out"]), ptr(outputs["point_match"]),
+                                              ptr(outputs["nmatches"]))
+    return p, outputs
+
+
+def _host_points(points):
+    out = dict(points)
+    for k, dt in (("desc", np.uint8), ("flags", np.uint8), ("pos", np.float32), ("normal", np.float32),
+                  ("dist_minmax", np.float32), ("angle", np.float32), ("octave", np.int32)):
+        if points.get(k) is not None:
+            out[k] = np.ascontiguousarray(points[k], dt)
+    return out
+
+
+def _host_frame(frame):
+    out = dict(frame)
+    out["keys_un"] = np.ascontiguousarray(frame["keys_un"], KEYPOINT_DTYPE)
+    out["desc"] = np.ascontiguousarray(frame["desc"], np.uint8)
+    if frame.get("u_right") is not None:
+        out["u_right"] = np.ascontiguousarray(frame["u_right"], np.float32)
+    if frame.get("occ") is not None:
+        out["occ"] = np.ascontiguousarray(frame["occ"], np.int8)
+    return out
+
+
+def _run_projection(matcher, frame, points, kind, **kw):
+    fr, pts = _host_frame(frame), _host_points(points)
+    p, out = proj_problem(fr, pts, kind, nnratio=matcher.mfNNratio, check_ori=matcher.mbCheckOrientation, **kw)
+    check(_lib.lib().orbx_search_by_projection(C.byref(p), matcher.device), "orbx_search_by_projection")
+    return out
 
 
 def _ba_arrays(prob):

@@ -313,3 +313,130 @@ def voc_descriptors(seed, voc_desc, leaf, n=800, noise_bits=24, p_random=0.15, p
             bits[rng.choice(256, noise_bits, replace=False)] ^= 1
             out[i] = np.packbits(bits)
     return out
+
+
+# --------------------------------------------------------------- SearchByProjection
+KITTI_K = dict(fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, bf=386.1448)
+_LEVEL_SHARE = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+
+
+def scale_factors(scale_factor=1.2, nlevels=8):
+    """mvScaleFactor as the ORBextractor ctor builds it (float, x double)."""
+    s = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        s.append(np.float32(np.float64(s[-1]) * scale_factor))
+    return np.array(s, np.float32)
+
+
+def _flip_bits(rng, desc, nbits):
+    out = desc.copy()
+    for k in range(len(out)):
+        if nbits[k] > 0:
+            pos = rng.choice(256, size=int(nbits[k]), replace=False)
+            bits = np.unpackbits(out[k])
+            bits[pos] ^= 1
+            out[k] = np.packbits(bits)
+    return out
+
+
+def _pose(rng, rot_sigma=0.05, t_sigma=0.5):
+    R = _rot_small(rng, rot_sigma)
+    t = rng.normal(0, t_sigma, 3)
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    return T.astype(np.float32)
+
+
+def projection_frame(seed, width=1241, height=376, n=2000, p_stereo=0.6, p_occ=(0.05, 0.10), cell_crowd=0.0):
+    """A current Frame for SearchByProjection: keypoints (mvKeysUn), descriptors,
+    mvuRight, mvpMapPoints occupancy, image bounds, grid and KITTI intrinsics.
+    cell_crowd > 0 piles that fraction of the keypoints into a few small spots
+    (many features per grid cell)."""
+    rng = np.random.default_rng(seed)
+    from ._lib import KEYPOINT_DTYPE
+    keys = np.zeros(n, KEYPOINT_DTYPE)
+    keys["x"] = rng.uniform(0, width - 1, n).astype(np.float32)
+    keys["y"] = rng.uniform(0, height - 1, n).astype(np.float32)
+    if cell_crowd > 0:
+        m = rng.random(n) < cell_crowd
+        spots = rng.uniform([0, 0], [width - 1, height - 1], size=(4, 2))
+        pick = rng.integers(0, 4, m.sum())
+        keys["x"][m] = np.clip(spots[pick, 0] + rng.normal(0, 3, m.sum()), 0, width - 1)
+        keys["y"][m] = np.clip(spots[pick, 1] + rng.normal(0, 3, m.sum()), 0, height - 1)
+    keys["octave"] = rng.choice(8, size=n, p=_LEVEL_SHARE / _LEVEL_SHARE.sum())
+    keys["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    keys["size"] = 31
+    keys["response"] = rng.uniform(7, 80, n).astype(np.float32)
+    keys["class_id"] = -1
+    desc = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    u_right = np.full(n, -1.0, np.float32)
+    st = rng.random(n) < p_stereo
+    u_right[st] = (keys["x"][st] - rng.uniform(1, 60, st.sum())).astype(np.float32)
+    r = rng.random(n)
+    occ = np.zeros(n, np.int8)
+    occ[r < p_occ[0] + p_occ[1]] = 2
+    occ[r < p_occ[0]] = 1
+    sf = scale_factors()
+    K = KITTI_K
+    Tcw = _pose(rng)
+    return dict(keys_un=keys, desc=desc, u_right=u_right, occ=occ, min_x=np.float32(0), max_x=np.float32(width),
+                min_y=np.float32(0), max_y=np.float32(height),
+                grid_inv_w=np.float32(64) / np.float32(width), grid_inv_h=np.float32(48) / np.float32(height),
+                nlevels=8, scale_factors=sf, log_scale_factor=np.float32(np.log(np.float32(1.2))),
+                fx=np.float32(K["fx"]), fy=np.float32(K["fy"]), cx=np.float32(K["cx"]), cy=np.float32(K["cy"]),
+                bf=np.float32(K["bf"]), b=np.float32(K["bf"] / K["fx"]), Tcw=Tcw)
+
+
+def projection_points(seed, frame, kind, n_points=3000, pool=0.5, noise_px=1.5, max_flip=70, p_random=0.15,
+                      p_take=0.9, p_obs=0.75, rot_sigma=8.0, p_rot_random=0.2):
+    """MapPoints projected into `frame`.  Each point is built from a frame
+    keypoint (drawn with repetition from a pool of pool*N keypoints, so several
+    points compete for one feature): world position back-projected at a random
+    depth with pixel noise, descriptor = the keypoint's with U[0,max_flip] bits
+    flipped (p_random: a random descriptor), source angle near the keypoint's.
+    kind 0 (local map) also gets isInFrustum inputs (normal, distances) and
+    precomputed track fields; kind 1 the last-frame octaves; kind 2 distances."""
+    rng = np.random.default_rng(seed)
+    keys, n = frame["keys_un"], len(frame["keys_un"])
+    pool_idx = rng.choice(n, size=max(1, int(pool * n)), replace=False)
+    src = pool_idx[rng.integers(0, len(pool_idx), n_points)]
+    T = frame["Tcw"].astype(np.float64)
+    R, t = T[:3, :3], T[:3, 3]
+    Ow = -R.T @ t
+    fx, fy, cx, cy = (float(frame[k]) for k in ("fx", "fy", "cx", "cy"))
+    z = rng.uniform(2.0, 40.0, n_points)
+    u = keys["x"][src] + rng.normal(0, noise_px, n_points)
+    v = keys["y"][src] + rng.normal(0, noise_px, n_points)
+    Xc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    Xw = (Xc - t) @ R  # R^T (Xc - t)
+    nb = rng.integers(0, max_flip + 1, n_points)
+    desc = _flip_bits(rng, frame["desc"][src], nb)
+    rnd = rng.random(n_points) < p_random
+    desc[rnd] = rng.integers(0, 256, size=(rnd.sum(), 32), dtype=np.uint8)
+    flags = ((rng.random(n_points) < p_take).astype(np.uint8) | ((rng.random(n_points) < p_obs).astype(np.uint8) << 1))
+    ang = (keys["angle"][src] + rng.normal(0, rot_sigma, n_points)) % 360.0
+    rr = rng.random(n_points) < p_rot_random
+    ang[rr] = rng.uniform(0, 360, rr.sum())
+    sf = frame["scale_factors"].astype(np.float64)
+    oct_ = np.clip(keys["octave"][src] + rng.integers(-1, 2, n_points), 0, 7).astype(np.int32)
+    dist = np.linalg.norm(Xw - Ow, axis=1)
+    dmax = dist * sf[oct_] * rng.uniform(0.9, 1.1, n_points)
+    dmin = dmax / sf[7]
+    far = rng.random(n_points) < 0.05
+    dmax[far] *= 0.3
+    pts = dict(kind=kind, desc=desc, flags=flags, pos=Xw.astype(np.float32),
+               dist_minmax=np.stack([dmin, dmax], 1).astype(np.float32), angle=ang.astype(np.float32),
+               octave=oct_)
+    if kind == 0:
+        nrm = (Xw - Ow) / dist[:, None] + rng.normal(0, 0.3, (n_points, 3))
+        nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+        pts["normal"] = nrm.astype(np.float32)
+        track = np.zeros((n_points, 4), np.float32)
+        track[:, 0] = u
+        track[:, 1] = v
+        track[:, 2] = u - float(frame["bf"]) / z
+        track[:, 3] = np.where(rng.random(n_points) < 0.5, 0.9995, 0.99)
+        pts["track"] = track
+        pts["track_level"] = oct_.copy()
+    return pts
