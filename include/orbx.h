@@ -36,6 +36,8 @@
  *   orbx_search_by_projection   ORBmatcher::SearchByProjection x3 (+ Frame::isInFrustum, GetFeaturesInArea)
  *                                                               src/ORBmatcher.cc:46-142, 1489-1795, include/ORBmatcher.h:64-95
  *   orbx_search_by_projection_device   batch of the above (one block per problem)
+ *   orbx_pose_optimization     Optimizer::PoseOptimization     src/Optimizer.cc:287-528, include/Optimizer.h:71
+ *   orbx_pose_optimization_device      batch of the above (one block per frame)
  *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
  *                               (g2o graph build, optimize(5), outlier levels, optimize(10), vToErase;
  *                               the Map mutex/recovery part stays on the caller's side)
@@ -360,6 +362,32 @@ orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int device);
 /* Batched, device-resident: problems[] is a HOST array whose pointers are
  * device pointers; one launch for the whole batch, stream-ordered. */
 orbx_status orbx_search_by_projection_device(const orbx_proj_problem* problems, int n, void* stream);
+
+/* Optimizer::PoseOptimization(Frame*) -- src/Optimizer.cc:287-528, include/Optimizer.h:71:
+ * one SE3 vertex, EdgeSE3ProjectXYZOnlyPose (monocular) / EdgeStereoSE3ProjectXYZOnlyPose
+ * (mvuRight >= 0) edges with Huber kernels, four rounds of optimize(10) restarting from
+ * mTcw, outlier levels between rounds, kernels dropped after round 2.  The caller gathers
+ * one edge per feature with a MapPoint, in feature order (the reference's edge insertion
+ * order), exactly as src/Optimizer.cc:318-410 does, and writes back pFrame->SetPose(Tcw_out)
+ * and mvbOutlier[feature of edge k] = outlier[k]. */
+typedef struct {
+  int n;                    /* edges = nInitialCorrespondences */
+  const float* obs;         /* n x 3: mvKeysUn[i].pt.x, .y, mvuRight[i] (< 0: monocular edge) */
+  const float* Xw;          /* n x 3: MapPoint::GetWorldPos() */
+  const float* inv_sigma2;  /* n: mvInvLevelSigma2[mvKeysUn[i].octave] */
+  float fx, fy, cx, cy, bf; /* Frame fx, fy, cx, cy, mbf */
+  float Tcw[16];            /* pFrame->mTcw on entry, row-major */
+  float* Tcw_out;           /* 16: the optimised pose (Converter::toCvMat) */
+  uint8_t* outlier;         /* n: mvbOutlier of each edge's feature on return */
+  int32_t* ngood;           /* the return value nInitialCorrespondences - nBad */
+  int32_t* iterations;      /* optional [4]: LM iterations run by each round's optimize(10) */
+} orbx_pose_problem;
+
+/* One problem, HOST pointers. */
+orbx_status orbx_pose_optimization(const orbx_pose_problem* p, int device);
+/* Batched, device-resident: problems[] is a HOST array whose pointers are device
+ * pointers; one block per problem runs all four rounds on the GPU (no host round trips). */
+orbx_status orbx_pose_optimization_device(const orbx_pose_problem* problems, int n, void* stream);
 
 /* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
  * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel

@@ -54,6 +54,12 @@ class ProjProblem(C.Structure):
                [(k, C.c_void_p) for k in ("frame_out", "point_match", "nmatches")]
 
 
+class PoseProblem(C.Structure):
+    _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p)] + \
+               [(k, C.c_float) for k in ("fx", "fy", "cx", "cy", "bf")] + \
+               [("Tcw", C.c_float * 16)] + [(k, C.c_void_p) for k in ("Tcw_out", "outlier", "ngood", "iterations")]
+
+
 _lib = None
 
 
@@ -114,6 +120,10 @@ def lib():
         L.oracle_predict_scale.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int]
         L.oracle_features_in_area.argtypes = [C.POINTER(ProjFrame), C.c_float, C.c_float, C.c_float, C.c_int,
                                               C.c_int, P, C.c_int]
+        L.oracle_pose_optimization.argtypes = [C.POINTER(PoseProblem)]
+        L.oracle_pose_edge_probe.argtypes = [P, P, P, P, C.c_int, P, P, P]
+        L.oracle_pose_edge_probe.restype = None
+        L.oracle_ldlt6.argtypes = [P, P, P]
         _lib = L
     return _lib
 
@@ -450,3 +460,42 @@ def log_det(x):
 
 def predict_scale(max_distance, dist, log_sf, nlevels):
     return lib().oracle_predict_scale(float(max_distance), float(dist), float(log_sf), int(nlevels))
+
+
+# ------------------------------------------------------------ PoseOptimization
+def pose_optimization(prob):
+    """Optimizer::PoseOptimization on a dict(obs[n,3], Xw[n,3], inv_sigma2[n], fx, fy, cx, cy, bf, Tcw[4,4]).
+    Returns dict(Tcw[4,4] f32, outlier[n] u8, ngood, iterations[4])."""
+    obs = np.ascontiguousarray(prob["obs"], np.float32).reshape(-1, 3)
+    X = np.ascontiguousarray(prob["Xw"], np.float32).reshape(-1, 3)
+    s2 = np.ascontiguousarray(prob["inv_sigma2"], np.float32)
+    n = len(obs)
+    out = dict(Tcw=np.zeros((4, 4), np.float32), outlier=np.zeros(max(n, 1), np.uint8), ngood=np.zeros(1, np.int32),
+               iterations=np.zeros(4, np.int32))
+    p = PoseProblem()
+    p.n, p.obs, p.Xw, p.inv_sigma2 = n, _p(obs), _p(X), _p(s2)
+    for k in ("fx", "fy", "cx", "cy", "bf"):
+        setattr(p, k, float(prob[k]))
+    T = np.asarray(prob["Tcw"], np.float32).reshape(16)
+    for i in range(16):
+        p.Tcw[i] = float(T[i])
+    p.Tcw_out, p.outlier, p.ngood, p.iterations = _p(out["Tcw"]), _p(out["outlier"]), _p(out["ngood"]), _p(out["iterations"])
+    lib().oracle_pose_optimization(C.byref(p))
+    out["outlier"] = out["outlier"][:n]
+    out["ngood"] = int(out["ngood"][0])
+    return out
+
+
+def pose_edge_probe(q, t, X, intr, stereo, obs):
+    err, J = np.zeros(3), np.zeros(18)
+    a = [np.ascontiguousarray(v, np.float64) for v in (q, t, X, intr, obs)]
+    lib().oracle_pose_edge_probe(_p(a[0]), _p(a[1]), _p(a[2]), _p(a[3]), int(stereo), _p(a[4]), _p(err), _p(J))
+    return err, J.reshape(3, 6)
+
+
+def ldlt6(H, b):
+    H = np.ascontiguousarray(H, np.float64).reshape(36)
+    b = np.ascontiguousarray(b, np.float64)
+    x = np.zeros(6)
+    ok = lib().oracle_ldlt6(_p(H), _p(b), _p(x))
+    return bool(ok), x

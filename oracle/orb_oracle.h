@@ -198,6 +198,25 @@ typedef struct {
 } oracle_proj_problem;
 
 int oracle_search_by_projection(const oracle_proj_problem* p);
+
+/* Optimizer::PoseOptimization (src/Optimizer.cc:287-528); layout identical to
+ * orbx_pose_problem in include/orbx.h. */
+typedef struct {
+  int n;
+  const float* obs;
+  const float* Xw;
+  const float* inv_sigma2;
+  float fx, fy, cx, cy, bf;
+  float Tcw[16];
+  float* Tcw_out;
+  uint8_t* outlier;
+  int32_t* ngood;
+  int32_t* iterations;
+} oracle_pose_problem;
+int oracle_pose_optimization(const oracle_pose_problem* p);
+void oracle_pose_edge_probe(const double q[4], const double t[3], const double X[3], const double intr[5], int stereo,
+                            const double obs[3], double err[3], double J[18]);
+int oracle_ldlt6(const double* H, const double* b, double* x);
 float oracle_log_det(float x);
 int oracle_predict_scale(float max_distance, float dist, float log_sf, int nlevels);
 int oracle_features_in_area(const oracle_proj_frame* f, float x, float y, float r, int minLevel, int maxLevel,

@@ -90,6 +90,13 @@ class ProjProblem(C.Structure):
                 ("nmatches", C.c_void_p)]
 
 
+class PoseProblem(C.Structure):
+    _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("Tcw", C.c_float * 16), ("Tcw_out", C.c_void_p), ("outlier", C.c_void_p), ("ngood", C.c_void_p),
+                ("iterations", C.c_void_p)]
+
+
 class RandState(C.Structure):
     _fields_ = [("r", C.c_uint32 * 34), ("i", C.c_int32)]
 
@@ -127,6 +134,8 @@ SIGNATURES = {
     "orbx_voc_transform": ([P, P, P, C.c_int, C.c_int, P, P, P, P, P, P, P], C.c_int),
     "orbx_search_by_projection": ([C.POINTER(ProjProblem), C.c_int], C.c_int),
     "orbx_search_by_projection_device": ([C.POINTER(ProjProblem), C.c_int, P], C.c_int),
+    "orbx_pose_optimization": ([C.POINTER(PoseProblem), C.c_int], C.c_int),
+    "orbx_pose_optimization_device": ([C.POINTER(PoseProblem), C.c_int, P], C.c_int),
     "orbx_rand_seed": ([C.POINTER(RandState), C.c_uint32], None),
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),

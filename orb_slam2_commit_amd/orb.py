@@ -365,6 +365,19 @@ class Optimizer:
         except Exception:
             pass
 
+    def PoseOptimization(self, frame):
+        """Optimizer::PoseOptimization(Frame*) -- src/Optimizer.cc:287-528.  frame: dict(obs[n,3]
+        (u, v, ur; ur < 0 = monocular), Xw[n,3], inv_sigma2[n], fx, fy, cx, cy, bf, Tcw[4,4]) with
+        one row per feature that has a MapPoint, in feature order.  Returns (nGood, Tcw[4,4],
+        outlier[n] (mvbOutlier), iterations[4])."""
+        pr = dict(frame)
+        pr["obs"] = np.ascontiguousarray(frame["obs"], np.float32).reshape(-1, 3)
+        pr["Xw"] = np.ascontiguousarray(frame["Xw"], np.float32).reshape(-1, 3)
+        pr["inv_sigma2"] = np.ascontiguousarray(frame["inv_sigma2"], np.float32)
+        p, out = pose_problem_struct(pr)
+        check(_lib.lib().orbx_pose_optimization(C.byref(p), self.device), "orbx_pose_optimization")
+        return int(out["ngood"][0]), out["Tcw_out"], out["outlier"][:len(pr["obs"])], out["iterations"]
+
     def LocalBundleAdjustment(self, prob, stop=False):
         """prob: dict(Tcw[n,12], fixed[n], intr[n,5] fx,fy,cx,cy,bf, Xw[m,3], edge_point, edge_cam,
         obs[e,3] (u, v, ur; ur<0 mono), inv_sigma2[e]).  ``stop`` mirrors *pbStopFlag.
@@ -382,6 +395,24 @@ class Optimizer:
         check(_lib.lib().orbx_ba_run(self._h, C.byref(P), C.byref(R), ptr(flag)), "orbx_ba_run")
         out.update(iterations=tuple(R.iterations), trials=R.trials, chi2=tuple(R.chi2))
         return out
+
+
+def pose_problem_struct(prob, outputs=None):
+    """orbx_pose_problem from a dict (host numpy or device tensors); outputs allocated on the host
+    when absent.  Returns (struct, outputs)."""
+    n = len(prob["obs"])
+    if outputs is None:
+        outputs = dict(Tcw_out=np.zeros((4, 4), np.float32), outlier=np.zeros(max(n, 1), np.uint8),
+                       ngood=np.zeros(1, np.int32), iterations=np.zeros(4, np.int32))
+    p = _lib.PoseProblem()
+    p.n = n
+    p.obs, p.Xw, p.inv_sigma2 = ptr(prob["obs"]), ptr(prob["Xw"]), ptr(prob["inv_sigma2"])
+    for k in ("fx", "fy", "cx", "cy", "bf"):
+        setattr(p, k, float(prob[k]))
+    p.Tcw[:] = _f32(prob["Tcw"]).reshape(16).tolist()
+    p.Tcw_out, p.outlier, p.ngood = ptr(outputs["Tcw_out"]), ptr(outputs["outlier"]), ptr(outputs["ngood"])
+    p.iterations = ptr(outputs.get("iterations"))
+    return p, outputs
 
 
 class PnPsolver:

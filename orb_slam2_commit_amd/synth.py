@@ -440,3 +440,40 @@ def projection_points(seed, frame, kind, n_points=3000, pool=0.5, noise_px=1.5, 
         pts["track"] = track
         pts["track_level"] = oct_.copy()
     return pts
+
+
+# --------------------------------------------------------------- PoseOptimization
+def pose_problem(seed, n=1000, p_stereo=0.6, outlier_frac=0.1, rot_sigma=0.01, t_sigma=0.05, width=1241,
+                 height=376, scale_factor=1.2, nlevels=8):
+    """A frame's PoseOptimization input: n MapPoint matches (feature order), KITTI intrinsics,
+    observations with pixel noise sigma = scale[octave], stereo ur for p_stereo of them, a
+    fraction of gross outliers (+/-20..60 px), and the initial Tcw perturbed from the truth."""
+    rng = np.random.default_rng(seed)
+    K = KITTI_K
+    sf = scale_factors(scale_factor, nlevels).astype(np.float64)
+    Ttrue = _pose(rng, 0.05, 0.5).astype(np.float64)
+    u = rng.uniform(5, width - 5, n)
+    v = rng.uniform(5, height - 5, n)
+    z = rng.uniform(2.0, 40.0, n)
+    Xc = np.stack([(u - K["cx"]) * z / K["fx"], (v - K["cy"]) * z / K["fy"], z], 1)
+    R, t = Ttrue[:3, :3], Ttrue[:3, 3]
+    Xw = (Xc - t) @ R
+    octv = rng.choice(nlevels, size=n, p=_LEVEL_SHARE[:nlevels] / _LEVEL_SHARE[:nlevels].sum())
+    sig = sf[octv]
+    obs = np.zeros((n, 3))
+    obs[:, 0] = u + rng.normal(0, 1, n) * sig
+    obs[:, 1] = v + rng.normal(0, 1, n) * sig
+    st = rng.random(n) < p_stereo
+    obs[:, 2] = np.where(st, u - K["bf"] / z + rng.normal(0, 1, n) * sig, -1.0)
+    bad = rng.random(n) < outlier_frac
+    off = rng.uniform(20, 60, (bad.sum(), 2)) * rng.choice([-1, 1], (bad.sum(), 2))
+    obs[bad, 0] += off[:, 0]
+    obs[bad, 1] += off[:, 1]
+    obs[bad & st, 2] += off[st[bad], 0]
+    T0 = Ttrue.copy()
+    T0[:3, :3] = _rot_small(rng, rot_sigma) @ R
+    T0[:3, 3] = t + rng.normal(0, t_sigma, 3)
+    inv_s2 = (1.0 / (sig * sig)).astype(np.float32)
+    return dict(obs=obs.astype(np.float32), Xw=Xw.astype(np.float32), inv_sigma2=inv_s2, fx=np.float32(K["fx"]),
+                fy=np.float32(K["fy"]), cx=np.float32(K["cx"]), cy=np.float32(K["cy"]), bf=np.float32(K["bf"]),
+                Tcw=T0.astype(np.float32), Ttrue=Ttrue.astype(np.float32), is_outlier=bad)
