@@ -36,6 +36,7 @@
  *   orbx_search_by_projection   ORBmatcher::SearchByProjection x3 (+ Frame::isInFrustum, GetFeaturesInArea)
  *                                                               src/ORBmatcher.cc:46-142, 1489-1795, include/ORBmatcher.h:64-95
  *   orbx_search_by_projection_device   batch of the above (one block per problem)
+ *   orbx_search_for_triangulation  ORBmatcher::SearchForTriangulation src/ORBmatcher.cc:738-925, include/ORBmatcher.h:134
  *   orbx_pose_optimization     Optimizer::PoseOptimization     src/Optimizer.cc:287-528, include/Optimizer.h:71
  *   orbx_pose_optimization_device      batch of the above (one block per frame)
  *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
@@ -299,6 +300,12 @@ orbx_status orbx_pnp_iterate_stream(orbx_pnp* h, int n_iterations, orbx_rand_sta
  *                                                   src/ORBmatcher.cc:1489-1646, include/ORBmatcher.h:76
  *   ORBX_PROJ_KEYFRAME   SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
  *                                                   src/ORBmatcher.cc:1648-1795, include/ORBmatcher.h:95
+ *   ORBX_PROJ_FUSE       the matching half of Fuse(KeyFrame*, const vector<MapPoint*>&, th)
+ *                                                   src/ORBmatcher.cc:944-1054, include/ORBmatcher.h:148
+ *                        (f = the KeyFrame, bounds = its int mnMinX.. as float; point_match[k] =
+ *                        bestIdx when bestDist <= TH_LOW, *nmatches = nFused.  The caller then
+ *                        applies Replace/AddObservation in point order, :1057-1086, re-querying
+ *                        any later point whose descriptor a Replace recomputed)
  * The current Frame (orbx_proj_frame) and the projected MapPoints are SoA
  * arrays the caller gathers from its object graph; the Frame's mvpMapPoints
  * on entry is summarised per feature as occ[i]: 0 NULL, 1 a MapPoint with
@@ -308,6 +315,7 @@ orbx_status orbx_pnp_iterate_stream(orbx_pnp* h, int n_iterations, orbx_rand_sta
 #define ORBX_PROJ_LOCAL 0
 #define ORBX_PROJ_LAST_FRAME 1
 #define ORBX_PROJ_KEYFRAME 2
+#define ORBX_PROJ_FUSE 3
 #define ORBX_PROJ_MAX_FEATURES 8192 /* Frame::N per problem */
 
 typedef struct {
@@ -320,6 +328,7 @@ typedef struct {
   float grid_inv_w, grid_inv_h;    /* mfGridElementWidthInv, mfGridElementHeightInv */
   int nlevels;                     /* mnScaleLevels (<= 16) */
   float scale_factors[16];         /* mvScaleFactors */
+  float inv_level_sigma2[16];      /* mvInvLevelSigma2 (FUSE) */
   float log_scale_factor;          /* mfLogScaleFactor */
   float fx, fy, cx, cy, bf, b;     /* fx, fy, cx, cy, mbf, mb */
   float Tcw[16];                   /* mTcw, row-major 4x4 */
@@ -333,11 +342,12 @@ typedef struct {
   const uint8_t* desc;      /* MapPoint::GetDescriptor(), n_points x 32 */
   const uint8_t* flags;     /* bit0 = the point takes part (LOCAL: mbTrackInView && !isBad(), or with
                                frustum: mnLastFrameSeen != mnId && !isBad(); LAST_FRAME: pMP &&
-                               !mvbOutlier[i]; KEYFRAME: pMP && !isBad() && !sAlreadyFound.count(pMP));
+                               !mvbOutlier[i]; KEYFRAME: pMP && !isBad() && !sAlreadyFound.count(pMP);
+                               FUSE: pMP && !isBad() && !IsInKeyFrame(pKF));
                                bit1 = Observations() > 0 */
-  const float* pos;         /* GetWorldPos(), n_points x 3 (frustum, LAST_FRAME, KEYFRAME) */
-  const float* normal;      /* GetNormal(), n_points x 3 (frustum) */
-  const float* dist_minmax; /* mfMinDistance, mfMaxDistance, n_points x 2 (frustum, KEYFRAME) */
+  const float* pos;         /* GetWorldPos(), n_points x 3 (frustum, LAST_FRAME, KEYFRAME, FUSE) */
+  const float* normal;      /* GetNormal(), n_points x 3 (frustum, FUSE) */
+  const float* dist_minmax; /* mfMinDistance, mfMaxDistance, n_points x 2 (frustum, KEYFRAME, FUSE) */
   const float* angle;       /* LastFrame.mvKeysUn[i].angle / pKF->mvKeysUn[i].angle (LAST_FRAME, KEYFRAME) */
   const int32_t* octave;    /* LastFrame.mvKeys[i].octave (LAST_FRAME) */
   float* track;             /* LOCAL, n_points x 4: mTrackProjX, mTrackProjY, mTrackProjXR, mTrackViewCos
@@ -362,6 +372,43 @@ orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int device);
 /* Batched, device-resident: problems[] is a HOST array whose pointers are
  * device pointers; one launch for the whole batch, stream-ordered. */
 orbx_status orbx_search_by_projection_device(const orbx_proj_problem* problems, int n, void* stream);
+
+/* ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12,
+ * vector<pair<size_t,size_t>>&, bOnlyStereo) -- src/ORBmatcher.cc:738-925,
+ * include/ORBmatcher.h:134 (caller LocalMapping::CreateNewMapPoints,
+ * src/LocalMapping.cc:363).  Each KeyFrame: mvKeysUn, descriptors, mvuRight
+ * (NULL = monocular), has_mp[i] = (GetMapPoint(i) != NULL) and its
+ * FeatureVector as CSR (as orbx_bow_side).  match12[i] = KF2 index matched to
+ * KF1 feature i after the rotation check (-1 none): vMatchedPairs is
+ * {(i, match12[i]) : match12[i] >= 0} in ascending i. */
+typedef struct {
+  int n;
+  const orbx_keypoint* keys_un;
+  const uint8_t* desc;
+  const float* u_right;
+  const uint8_t* has_mp;
+  int n_nodes;
+  const uint32_t* node_id;
+  const int32_t* node_off;
+  const int32_t* feat;
+} orbx_tri_kf;
+
+typedef struct {
+  orbx_tri_kf kf1, kf2;
+  float F12[9];             /* row-major 3x3 (LocalMapping::ComputeF12) */
+  float C1w[3];             /* pKF1->GetCameraCenter() */
+  float T2w[16];            /* pKF2 Tcw, row-major */
+  float fx, fy, cx, cy;     /* pKF2 intrinsics */
+  float scale_factors2[16]; /* pKF2->mvScaleFactors */
+  float level_sigma2_2[16]; /* pKF2->mvLevelSigma2 */
+  int only_stereo;          /* bOnlyStereo */
+  int check_ori;            /* ORBmatcher mbCheckOrientation */
+  int32_t* match12;         /* kf1.n */
+  int32_t* nmatches;        /* return value */
+} orbx_tri_problem;
+
+orbx_status orbx_search_for_triangulation(const orbx_tri_problem* p, int device); /* host pointers */
+orbx_status orbx_search_for_triangulation_device(const orbx_tri_problem* problems, int n, void* stream);
 
 /* Optimizer::PoseOptimization(Frame*) -- src/Optimizer.cc:287-528, include/Optimizer.h:71:
  * one SE3 vertex, EdgeSE3ProjectXYZOnlyPose (monocular) / EdgeStereoSE3ProjectXYZOnlyPose

@@ -40,7 +40,7 @@ class ProjFrame(C.Structure):
     _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
                 ("occ", C.c_void_p)] + [(k, C.c_float) for k in ("min_x", "max_x", "min_y", "max_y", "grid_inv_w",
                                                                  "grid_inv_h")] + \
-               [("nlevels", C.c_int), ("scale_factors", C.c_float * 16)] + \
+               [("nlevels", C.c_int), ("scale_factors", C.c_float * 16), ("inv_level_sigma2", C.c_float * 16)] + \
                [(k, C.c_float) for k in ("log_scale_factor", "fx", "fy", "cx", "cy", "bf", "b")] + \
                [("Tcw", C.c_float * 16)]
 
@@ -58,6 +58,19 @@ class PoseProblem(C.Structure):
     _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p)] + \
                [(k, C.c_float) for k in ("fx", "fy", "cx", "cy", "bf")] + \
                [("Tcw", C.c_float * 16)] + [(k, C.c_void_p) for k in ("Tcw_out", "outlier", "ngood", "iterations")]
+
+
+class TriKF(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
+                ("has_mp", C.c_void_p), ("n_nodes", C.c_int), ("node_id", C.c_void_p), ("node_off", C.c_void_p),
+                ("feat", C.c_void_p)]
+
+
+class TriProblem(C.Structure):
+    _fields_ = [("kf1", TriKF), ("kf2", TriKF), ("F12", C.c_float * 9), ("C1w", C.c_float * 3),
+                ("T2w", C.c_float * 16)] + [(k, C.c_float) for k in ("fx", "fy", "cx", "cy")] + \
+               [("scale_factors2", C.c_float * 16), ("level_sigma2_2", C.c_float * 16), ("only_stereo", C.c_int),
+                ("check_ori", C.c_int), ("match12", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
 _lib = None
@@ -124,6 +137,7 @@ def lib():
         L.oracle_pose_edge_probe.argtypes = [P, P, P, P, C.c_int, P, P, P]
         L.oracle_pose_edge_probe.restype = None
         L.oracle_ldlt6.argtypes = [P, P, P]
+        L.oracle_search_for_triangulation.argtypes = [C.POINTER(TriProblem)]
         _lib = L
     return _lib
 
@@ -404,8 +418,11 @@ def _proj_frame(fr):
               "cy", "bf", "b"):
         setattr(f, k, float(fr[k]))
     f.nlevels = int(fr["nlevels"])
+    isg = fr.get("inv_level_sigma2")
     for i in range(f.nlevels):
         f.scale_factors[i] = float(fr["scale_factors"][i])
+        s = np.float32(fr["scale_factors"][i])
+        f.inv_level_sigma2[i] = float(isg[i]) if isg is not None else float(np.float32(1.0) / np.float32(s * s))
     T = np.asarray(fr["Tcw"], np.float32).reshape(16)
     for i in range(16):
         f.Tcw[i] = float(T[i])
@@ -499,3 +516,40 @@ def ldlt6(H, b):
     x = np.zeros(6)
     ok = lib().oracle_ldlt6(_p(H), _p(b), _p(x))
     return bool(ok), x
+
+
+# ------------------------------------------------------------ SearchForTriangulation
+def search_for_triangulation(prob, only_stereo=False, check_ori=True):
+    """prob: dict(kf1, kf2, F12, C1w, T2w, fx, fy, cx, cy, scale_factors2, level_sigma2_2); each kf a dict
+    (keys_un, desc, u_right, has_mp, node_id, node_off, feat).  Returns (nmatches, match12)."""
+    keep = []
+
+    def kf(d):
+        a = dict(keys=np.ascontiguousarray(d["keys_un"], KEYPOINT_DTYPE), desc=np.ascontiguousarray(d["desc"], np.uint8),
+                 ur=None if d.get("u_right") is None else np.ascontiguousarray(d["u_right"], np.float32),
+                 mp=None if d.get("has_mp") is None else np.ascontiguousarray(d["has_mp"], np.uint8),
+                 nid=np.ascontiguousarray(d["node_id"], np.uint32), noff=np.ascontiguousarray(d["node_off"], np.int32),
+                 feat=np.ascontiguousarray(d["feat"], np.int32))
+        keep.append(a)
+        k = TriKF()
+        k.n, k.keys_un, k.desc, k.u_right, k.has_mp = len(a["keys"]), _p(a["keys"]), _p(a["desc"]), _p(a["ur"]), _p(a["mp"])
+        k.n_nodes, k.node_id, k.node_off, k.feat = len(a["nid"]), _p(a["nid"]), _p(a["noff"]), _p(a["feat"])
+        return k
+
+    p = TriProblem()
+    p.kf1, p.kf2 = kf(prob["kf1"]), kf(prob["kf2"])
+    for name, n in (("F12", 9), ("C1w", 3), ("T2w", 16)):
+        v = np.asarray(prob[name], np.float32).reshape(n)
+        for i in range(n):
+            getattr(p, name)[i] = float(v[i])
+    for k in ("fx", "fy", "cx", "cy"):
+        setattr(p, k, float(prob[k]))
+    for i in range(len(prob["scale_factors2"])):
+        p.scale_factors2[i] = float(prob["scale_factors2"][i])
+        p.level_sigma2_2[i] = float(prob["level_sigma2_2"][i])
+    p.only_stereo, p.check_ori = int(bool(only_stereo)), int(bool(check_ori))
+    m = np.zeros(max(1, p.kf1.n), np.int32)
+    nm = np.zeros(1, np.int32)
+    p.match12, p.nmatches = _p(m), _p(nm)
+    lib().oracle_search_for_triangulation(C.byref(p))
+    return int(nm[0]), m[:p.kf1.n]

@@ -171,6 +171,7 @@ typedef struct {
   float grid_inv_w, grid_inv_h;
   int nlevels;
   float scale_factors[16];
+  float inv_level_sigma2[16];
   float log_scale_factor;
   float fx, fy, cx, cy, bf, b;
   float Tcw[16];
@@ -214,6 +215,33 @@ typedef struct {
   int32_t* iterations;
 } oracle_pose_problem;
 int oracle_pose_optimization(const oracle_pose_problem* p);
+
+/* ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:738-925); layout
+ * identical to orbx_tri_problem in include/orbx.h. */
+typedef struct {
+  int n;
+  const oracle_keypoint* keys_un;
+  const uint8_t* desc;
+  const float* u_right;
+  const uint8_t* has_mp;
+  int n_nodes;
+  const uint32_t* node_id;
+  const int32_t* node_off;
+  const int32_t* feat;
+} oracle_tri_kf;
+typedef struct {
+  oracle_tri_kf kf1, kf2;
+  float F12[9];
+  float C1w[3];
+  float T2w[16];
+  float fx, fy, cx, cy;
+  float scale_factors2[16];
+  float level_sigma2_2[16];
+  int only_stereo, check_ori;
+  int32_t* match12;
+  int32_t* nmatches;
+} oracle_tri_problem;
+int oracle_search_for_triangulation(const oracle_tri_problem* p);
 void oracle_pose_edge_probe(const double q[4], const double t[3], const double X[3], const double intr[5], int stereo,
                             const double obs[3], double err[3], double J[18]);
 int oracle_ldlt6(const double* H, const double* b, double* x);

@@ -12,6 +12,7 @@
 //   ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)        src/ORBmatcher.cc:46-142
 //   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)      src/ORBmatcher.cc:1489-1646
 //   ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist)  src/ORBmatcher.cc:1648-1795
+//   ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th), matching half     src/ORBmatcher.cc:944-1054
 //
 // OpenCV arithmetic restated (parity vs the genuine library is unpinned; the
 // reference ships no fixture for any of this):
@@ -416,6 +417,74 @@ int keyframe(const oracle_proj_problem& P) {
   return finish_rotation(P, occ, rotHist, nmatches);
 }
 
+// The matching half of Fuse(KeyFrame*, const vector<MapPoint*>&, th),
+// src/ORBmatcher.cc:944-1054 (KeyFrame::IsInImage :749-752, GetFeaturesInArea
+// src/KeyFrame.cc:708-747 without level filter).  nFused counts every point
+// with bestDist <= TH_LOW (:1057-1087 increments it whatever the merge does).
+int fuse(const oracle_proj_problem& P) {
+  const oracle_proj_frame& F = P.f;
+  Frame fr(F);
+  Occupancy occ(F);
+  float Ow[3];
+  camera_centre(F.Tcw, Ow);
+  int nFused = 0;
+  for (int i = 0; i < P.n_points; i++) {
+    P.point_match[i] = -1;
+    if (!(P.flags[i] & 1)) continue;  // !pMP || isBad() || IsInKeyFrame(pKF)
+    const float* X = P.pos + 3 * i;
+    float c[3];
+    mat3x1(F.Tcw, X, c);
+    if (c[2] < 0.0f) continue;
+    const float invz = 1 / c[2];
+    const float x = c[0] * invz, y = c[1] * invz;
+    const float u = F.fx * x + F.cx, v = F.fy * y + F.cy;
+    if (!(u >= F.min_x && u < F.max_x && v >= F.min_y && v < F.max_y)) continue;  // IsInImage
+    const float ur = u - F.bf * invz;
+    const float maxDistance = 1.2f * P.dist_minmax[2 * i + 1], minDistance = 0.8f * P.dist_minmax[2 * i];
+    const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+    const float dist3D = norm3(PO);
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    const float* Pn = P.normal + 3 * i;
+    double dot = (double)PO[0] * Pn[0];
+    dot = dot + (double)PO[1] * Pn[1];
+    dot = dot + (double)PO[2] * Pn[2];
+    if (dot < 0.5 * dist3D) continue;
+    const int nPredictedLevel = predict_scale(P.dist_minmax[2 * i + 1], dist3D, F.log_scale_factor, F.nlevels);
+    const float radius = P.th * F.scale_factors[nPredictedLevel];
+    const std::vector<int> cand = fr.area(u, v, radius);
+    if (cand.empty()) continue;
+    const uint8_t* dMP = P.desc + 32 * (size_t)i;
+    int bestDist = 256, bestIdx = -1;
+    for (int idx : cand) {
+      const oracle_keypoint& kp = F.keys_un[idx];
+      const int kpLevel = kp.octave;
+      if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+      const float isg = F.inv_level_sigma2[kpLevel];
+      if (fr.ur(idx) >= 0) {
+        const float ex = u - kp.x, ey = v - kp.y, er = ur - fr.ur(idx);
+        const float e2 = ex * ex + ey * ey + er * er;
+        if (e2 * isg > 7.8) continue;
+      } else {
+        const float ex = u - kp.x, ey = v - kp.y;
+        const float e2 = ex * ex + ey * ey;
+        if (e2 * isg > 5.99) continue;
+      }
+      const int dist = hamming(dMP, F.desc + 32 * (size_t)idx);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= 50) {  // TH_LOW
+      P.point_match[i] = bestIdx;
+      occ.who[bestIdx] = i;
+      nFused++;
+    }
+  }
+  write_out(P, occ);
+  return nFused;
+}
+
 }  // namespace
 
 extern "C" {
@@ -426,6 +495,7 @@ int oracle_search_by_projection(const oracle_proj_problem* P) {
     case 0: return local_map(*P);
     case 1: return last_frame(*P);
     case 2: return keyframe(*P);
+    case 3: return fuse(*P);
     default: return -1;
   }
 }

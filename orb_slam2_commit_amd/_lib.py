@@ -75,7 +75,8 @@ class ProjFrame(C.Structure):
     _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
                 ("occ", C.c_void_p), ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
                 ("max_y", C.c_float), ("grid_inv_w", C.c_float), ("grid_inv_h", C.c_float), ("nlevels", C.c_int),
-                ("scale_factors", C.c_float * 16), ("log_scale_factor", C.c_float), ("fx", C.c_float),
+                ("scale_factors", C.c_float * 16), ("inv_level_sigma2", C.c_float * 16),
+                ("log_scale_factor", C.c_float), ("fx", C.c_float),
                 ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float), ("b", C.c_float),
                 ("Tcw", C.c_float * 16)]
 
@@ -95,6 +96,19 @@ class PoseProblem(C.Structure):
                 ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
                 ("Tcw", C.c_float * 16), ("Tcw_out", C.c_void_p), ("outlier", C.c_void_p), ("ngood", C.c_void_p),
                 ("iterations", C.c_void_p)]
+
+
+class TriKF(C.Structure):
+    _fields_ = [("n", C.c_int), ("keys_un", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
+                ("has_mp", C.c_void_p), ("n_nodes", C.c_int), ("node_id", C.c_void_p), ("node_off", C.c_void_p),
+                ("feat", C.c_void_p)]
+
+
+class TriProblem(C.Structure):
+    _fields_ = [("kf1", TriKF), ("kf2", TriKF), ("F12", C.c_float * 9), ("C1w", C.c_float * 3),
+                ("T2w", C.c_float * 16), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("scale_factors2", C.c_float * 16), ("level_sigma2_2", C.c_float * 16), ("only_stereo", C.c_int),
+                ("check_ori", C.c_int), ("match12", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
 class RandState(C.Structure):
@@ -136,6 +150,8 @@ SIGNATURES = {
     "orbx_search_by_projection_device": ([C.POINTER(ProjProblem), C.c_int, P], C.c_int),
     "orbx_pose_optimization": ([C.POINTER(PoseProblem), C.c_int], C.c_int),
     "orbx_pose_optimization_device": ([C.POINTER(PoseProblem), C.c_int, P], C.c_int),
+    "orbx_search_for_triangulation": ([C.POINTER(TriProblem), C.c_int], C.c_int),
+    "orbx_search_for_triangulation_device": ([C.POINTER(TriProblem), C.c_int, P], C.c_int),
     "orbx_rand_seed": ([C.POINTER(RandState), C.c_uint32], None),
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),

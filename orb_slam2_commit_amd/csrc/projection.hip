@@ -1,6 +1,7 @@
 // projection.hip -- ORBmatcher::SearchByProjection, the three overloads run on
 // every tracked frame (src/ORBmatcher.cc:46-142 local map, :1489-1646 last
-// frame, :1648-1795 keyframe), with Frame::AssignFeaturesToGrid /
+// frame, :1648-1795 keyframe) and the matching half of Fuse (:944-1054), with
+// Frame::AssignFeaturesToGrid /
 // GetFeaturesInArea (src/Frame.cc:254-271, 388-453) and, for the local map,
 // Frame::isInFrustum (src/Frame.cc:315-375) fused in front.  One block per
 // problem (a Frame plus the MapPoints projected into it), batched.
@@ -121,7 +122,7 @@ struct Query {
   bool active;
   float x, y, r;      // GetFeaturesInArea centre and half-size
   int min_level, max_level;
-  float ur, ur_th;    // stereo check |ur - mvuRight| > ur_th (ur_th < 0: no check)
+  float ur, ur_th;    // stereo check |ur - mvuRight| > ur_th (ur_th < 0: no check); FUSE: ur
   int th;             // accept bestDist <= th
 };
 
@@ -152,6 +153,33 @@ __device__ Query setup_query(const ProjProblem& P, int i, const float* Ow, bool 
   const float* X = P.pos + 3 * i;
   float c[3];
   mat3x1(F.Tcw, X, c);
+  if (P.kind == ORBX_PROJ_FUSE) {  // src/ORBmatcher.cc:960-1006
+    if (c[2] < 0.0f) return q;
+    const float invz = 1 / c[2];
+    const float x = c[0] * invz, y = c[1] * invz;
+    const float u = F.fx * x + F.cx, v = F.fy * y + F.cy;
+    if (!(u >= F.min_x && u < F.max_x && v >= F.min_y && v < F.max_y)) return q;  // KeyFrame::IsInImage
+    const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+    const float d3 = norm3(PO);
+    const float dmin = P.dist_minmax[2 * i], dmax = P.dist_minmax[2 * i + 1];
+    if (d3 < 0.8f * dmin || d3 > 1.2f * dmax) return q;
+    const float* Pn = P.normal + 3 * i;
+    double dot = (double)PO[0] * Pn[0];
+    dot = dot + (double)PO[1] * Pn[1];
+    dot = dot + (double)PO[2] * Pn[2];
+    if (dot < 0.5 * d3) return q;
+    const int lvl = predict_scale(dmax, d3, F.log_scale_factor, F.nlevels);
+    q.r = P.th * F.scale_factors[lvl];
+    q.x = u;
+    q.y = v;
+    q.min_level = lvl - 1;  // the candidate loop's kpLevel window (:1015-1016)
+    q.max_level = lvl;
+    q.ur = u - F.bf * invz;
+    q.ur_th = -1.0f;
+    q.th = 50;  // TH_LOW
+    q.active = true;
+    return q;
+  }
   const float invzc = (float)(1.0 / (double)c[2]);
   if (P.kind == ORBX_PROJ_LAST_FRAME && invzc < 0) return q;
   const float u = F.fx * c[0] * invzc + F.cx;
@@ -315,6 +343,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   constexpr int kGroups = PBS / kGroup;
   const bool local = P.kind == ORBX_PROJ_LOCAL;
   const bool kf = P.kind == ORBX_PROJ_KEYFRAME;
+  const bool fuse = P.kind == ORBX_PROJ_FUSE;  // no "already matched" state: one sweep
   for (int sweep = 0; sweep <= nP + 1; sweep++) {
     if (tid == 0) s_changed = 0;
     __syncthreads();
@@ -348,8 +377,22 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
             if (check && (oct < q.min_level || (q.max_level >= 0 && oct > q.max_level))) continue;
             const float dx = kp.x - q.x, dy = kp.y - q.y;
             if (!(__builtin_fabsf(dx) < q.r && __builtin_fabsf(dy) < q.r)) continue;
-            const int o = F.occ ? F.occ[idx] : 0;
-            if ((kf ? o != 0 : o == 2) || s_fw[idx] < i) continue;
+            if (fuse) {  // reprojection error gate, src/ORBmatcher.cc:1018-1042
+              const float isg = F.inv_level_sigma2[oct];
+              const float urf = F.u_right ? F.u_right[idx] : -1.0f;
+              const float ex = q.x - kp.x, ey = q.y - kp.y;
+              if (urf >= 0) {
+                const float er = q.ur - urf;
+                const float e2 = ex * ex + ey * ey + er * er;
+                if (e2 * isg > 7.8) continue;
+              } else {
+                const float e2 = ex * ex + ey * ey;
+                if (e2 * isg > 5.99) continue;
+              }
+            } else {
+              const int o = F.occ ? F.occ[idx] : 0;
+              if ((kf ? o != 0 : o == 2) || s_fw[idx] < i) continue;
+            }
             if (q.ur_th >= 0.0f && F.u_right) {
               const float urf = F.u_right[idx];
               if (urf > 0 && __builtin_fabsf(q.ur - urf) > q.ur_th) continue;
@@ -390,7 +433,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
     if (changed) s_changed = 1;
     __threadfence_block();
     __syncthreads();
-    if (!s_changed) break;
+    if (!s_changed || fuse) break;
     // first blocking writer per feature from this sweep's matches
     for (int f = tid; f < nF; f += PBS) s_fw[f] = INT_MAX;
     __syncthreads();
@@ -408,7 +451,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
     s_drop = 0;
   }
   __syncthreads();
-  const bool rot = !local && P.check_ori;
+  const bool rot = !local && !fuse && P.check_ori;
   int cnt = 0;
   for (int i = tid; i < nP; i += PBS) {
     const int m = P.point_match[i];
@@ -478,7 +521,7 @@ orbx_status proj_status(hipError_t e) { return e == hipSuccess ? ORBX_OK : ORBX_
 
 // Host-side argument checks shared by both entry points (the kernel assumes them).
 orbx_status proj_check(const orbx_proj_problem& p, bool host) {
-  if (p.kind < ORBX_PROJ_LOCAL || p.kind > ORBX_PROJ_KEYFRAME) return ORBX_ERR_ARG;
+  if (p.kind < ORBX_PROJ_LOCAL || p.kind > ORBX_PROJ_FUSE) return ORBX_ERR_ARG;
   if (p.f.n < 0 || p.n_points < 0) return ORBX_ERR_ARG;
   if (p.f.n > ORBX_PROJ_MAX_FEATURES) return ORBX_ERR_CAPACITY;
   if (p.f.nlevels < 1 || p.f.nlevels > 16) return ORBX_ERR_ARG;
@@ -499,6 +542,9 @@ orbx_status proj_check(const orbx_proj_problem& p, bool host) {
         if (host)
           for (int i = 0; i < p.n_points; i++)
             if ((p.flags[i] & 1) && (p.octave[i] < 0 || p.octave[i] >= p.f.nlevels)) return ORBX_ERR_ARG;
+        break;
+      case ORBX_PROJ_FUSE:
+        if (!p.pos || !p.normal || !p.dist_minmax) return ORBX_ERR_ARG;
         break;
       default:
         if (!p.pos || !p.dist_minmax || (p.check_ori && !p.angle)) return ORBX_ERR_ARG;

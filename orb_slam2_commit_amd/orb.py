@@ -232,6 +232,29 @@ class ORBmatcher:
         o = _run_projection(self, CurrentFrame, KFPoints, PROJ_KEYFRAME, th=th, orb_dist=ORBdist)
         return int(o["nmatches"][0]), o["frame_out"], o["point_match"]
 
+    def Fuse(self, pKF, vpMapPoints, th=3.0):
+        """The matching half of Fuse(KeyFrame*, const vector<MapPoint*>&, th) --
+        src/ORBmatcher.cc:944-1054.  pKF: frame dict of the KeyFrame (bounds = its int mnMinX..);
+        vpMapPoints: points dict (pos, normal, dist_minmax, desc, flags bit0 = pMP && !isBad() &&
+        !IsInKeyFrame(pKF)).  Returns (nFused, bestIdx[n_points] (-1 = no fuse)); the caller applies
+        Replace / AddObservation in point order (:1057-1086)."""
+        o = _run_projection(self, pKF, vpMapPoints, PROJ_FUSE, th=th)
+        return int(o["nmatches"][0]), o["point_match"]
+
+    def SearchForTriangulation(self, prob, bOnlyStereo=False):
+        """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) --
+        src/ORBmatcher.cc:738-925.  prob: dict(kf1, kf2 (keys_un, desc, u_right, has_mp, node_id,
+        node_off, feat), F12[3,3], C1w[3], T2w[4,4], fx, fy, cx, cy (pKF2), scale_factors2,
+        level_sigma2_2).  Returns (nmatches, vMatchedPairs as an [m,2] int array)."""
+        p, keep = tri_problem(prob, bOnlyStereo, self.mbCheckOrientation)
+        m12 = np.zeros(max(1, p.kf1.n), np.int32)
+        nm = np.zeros(1, np.int32)
+        p.match12, p.nmatches = ptr(m12), ptr(nm)
+        check(_lib.lib().orbx_search_for_triangulation(C.byref(p), self.device), "orbx_search_for_triangulation")
+        m12 = m12[:p.kf1.n]
+        i = np.nonzero(m12 >= 0)[0]
+        return int(nm[0]), np.stack([i, m12[i]], 1).astype(np.int64)
+
     @staticmethod
     def DescriptorDistance(a, b):
         """Hamming distance of 32-byte descriptors; a, b: [32] or [n,32] uint8 (computed on the GPU)."""
@@ -250,7 +273,7 @@ class ORBmatcher:
         return int(d[0]) if n == 1 else d
 
 
-PROJ_LOCAL, PROJ_LAST_FRAME, PROJ_KEYFRAME = 0, 1, 2
+PROJ_LOCAL, PROJ_LAST_FRAME, PROJ_KEYFRAME, PROJ_FUSE = 0, 1, 2, 3
 
 
 def _f32(x):
@@ -285,6 +308,12 @@ def proj_problem(frame, points, kind, th, nnratio=0.6, check_ori=True, mono=Fals
     sf = np.zeros(16, np.float32)
     sf[:f.nlevels] = frame["scale_factors"][:f.nlevels]
     f.scale_factors[:] = sf.tolist()
+    isg = np.zeros(16, np.float32)
+    if frame.get("inv_level_sigma2") is not None:
+        isg[:f.nlevels] = frame["inv_level_sigma2"][:f.nlevels]
+    else:  # mvInvLevelSigma2 = 1 / (s*s) in float (ORBextractor ctor)
+        isg[:f.nlevels] = np.float32(1.0) / (sf[:f.nlevels] * sf[:f.nlevels])
+    f.inv_level_sigma2[:] = isg.tolist()
     f.Tcw[:] = _f32(frame["Tcw"]).reshape(16).tolist()
     p = _lib.ProjProblem()
     p.kind, p.frustum, p.f, p.n_points = int(kind), int(bool(frustum)), f, npnt
@@ -326,6 +355,47 @@ def _run_projection(matcher, frame, points, kind, **kw):
     p, out = proj_problem(fr, pts, kind, nnratio=matcher.mfNNratio, check_ori=matcher.mbCheckOrientation, **kw)
     check(_lib.lib().orbx_search_by_projection(C.byref(p), matcher.device), "orbx_search_by_projection")
     return out
+
+
+def tri_problem(prob, only_stereo=False, check_ori=True):
+    """orbx_tri_problem from a dict whose arrays are host numpy arrays or device tensors (the caller
+    keeps them alive; numpy inputs are made contiguous here and returned in `keep`).  match12 and
+    nmatches are left for the caller to point at its outputs."""
+    keep = []
+
+    def arr(x, dt):
+        if x is None or not isinstance(x, np.ndarray):
+            return x
+        a = np.ascontiguousarray(x, dt)
+        keep.append(a)
+        return a
+
+    def kf(d):
+        k = _lib.TriKF()
+        keys = arr(d["keys_un"], KEYPOINT_DTYPE)
+        k.n = len(d["desc"])
+        k.keys_un, k.desc = ptr(keys), ptr(arr(d["desc"], np.uint8))
+        k.u_right, k.has_mp = ptr(arr(d.get("u_right"), np.float32)), ptr(arr(d.get("has_mp"), np.uint8))
+        k.n_nodes = len(d["node_id"])
+        k.node_id, k.node_off = ptr(arr(d["node_id"], np.uint32)), ptr(arr(d["node_off"], np.int32))
+        k.feat = ptr(arr(d["feat"], np.int32))
+        return k
+
+    p = _lib.TriProblem()
+    p.kf1, p.kf2 = kf(prob["kf1"]), kf(prob["kf2"])
+    p.F12[:] = _f32(prob["F12"]).reshape(9).tolist()
+    p.C1w[:] = _f32(prob["C1w"]).reshape(3).tolist()
+    p.T2w[:] = _f32(prob["T2w"]).reshape(16).tolist()
+    for k in ("fx", "fy", "cx", "cy"):
+        setattr(p, k, float(prob[k]))
+    sf = np.zeros(16, np.float32)
+    sg = np.zeros(16, np.float32)
+    nl = len(prob["scale_factors2"])
+    sf[:nl], sg[:nl] = prob["scale_factors2"], prob["level_sigma2_2"]
+    p.scale_factors2[:] = sf.tolist()
+    p.level_sigma2_2[:] = sg.tolist()
+    p.only_stereo, p.check_ori = int(bool(only_stereo)), int(bool(check_ori))
+    return p, keep
 
 
 def _ba_arrays(prob):

@@ -395,8 +395,8 @@ def projection_points(seed, frame, kind, n_points=3000, pool=0.5, noise_px=1.5, 
     points compete for one feature): world position back-projected at a random
     depth with pixel noise, descriptor = the keypoint's with U[0,max_flip] bits
     flipped (p_random: a random descriptor), source angle near the keypoint's.
-    kind 0 (local map) also gets isInFrustum inputs (normal, distances) and
-    precomputed track fields; kind 1 the last-frame octaves; kind 2 distances."""
+    Every kind gets world positions, normals, distance bounds, octaves and angles;
+    kind 0 (local map) also the precomputed track fields."""
     rng = np.random.default_rng(seed)
     keys, n = frame["keys_un"], len(frame["keys_un"])
     pool_idx = rng.choice(n, size=max(1, int(pool * n)), replace=False)
@@ -428,10 +428,10 @@ def projection_points(seed, frame, kind, n_points=3000, pool=0.5, noise_px=1.5, 
     pts = dict(kind=kind, desc=desc, flags=flags, pos=Xw.astype(np.float32),
                dist_minmax=np.stack([dmin, dmax], 1).astype(np.float32), angle=ang.astype(np.float32),
                octave=oct_)
+    nrm = (Xw - Ow) / dist[:, None] + rng.normal(0, 0.3, (n_points, 3))
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    pts["normal"] = nrm.astype(np.float32)
     if kind == 0:
-        nrm = (Xw - Ow) / dist[:, None] + rng.normal(0, 0.3, (n_points, 3))
-        nrm /= np.linalg.norm(nrm, axis=1)[:, None]
-        pts["normal"] = nrm.astype(np.float32)
         track = np.zeros((n_points, 4), np.float32)
         track[:, 0] = u
         track[:, 1] = v
@@ -477,3 +477,71 @@ def pose_problem(seed, n=1000, p_stereo=0.6, outlier_frac=0.1, rot_sigma=0.01, t
     return dict(obs=obs.astype(np.float32), Xw=Xw.astype(np.float32), inv_sigma2=inv_s2, fx=np.float32(K["fx"]),
                 fy=np.float32(K["fy"]), cx=np.float32(K["cx"]), cy=np.float32(K["cy"]), bf=np.float32(K["bf"]),
                 Tcw=T0.astype(np.float32), Ttrue=Ttrue.astype(np.float32), is_outlier=bad)
+
+
+# --------------------------------------------------------------- SearchForTriangulation
+def triangulation_problem(seed, n1=1500, n2=1500, n_true=700, n_nodes=100, noise_bits=20, p_mp=0.35,
+                          p_stereo=0.6, baseline=(0.8, 0.0, 0.3), width=1241, height=376):
+    """Two KeyFrames observing a shared scene: n_true features of KF1 have a true correspondence in
+    KF2 (same FeatureVector node, descriptor with noise bits flipped, pixel noise), the rest are
+    random.  F12 = K^-T [t12]x R12 K^-1 as LocalMapping::ComputeF12 (src/LocalMapping.cc:672-690)."""
+    rng = np.random.default_rng(seed)
+    K = KITTI_K
+    Km = np.array([[K["fx"], 0, K["cx"]], [0, K["fy"], K["cy"]], [0, 0, 1]])
+    T1 = _pose(rng, 0.02, 0.2).astype(np.float64)
+    T2 = T1.copy()
+    T2[:3, :3] = _rot_small(rng, 0.03) @ T1[:3, :3]
+    T2[:3, 3] = T1[:3, 3] - T2[:3, :3] @ np.array(baseline, np.float64) @ np.eye(3)
+    from ._lib import KEYPOINT_DTYPE
+
+    def keys(n):
+        k = np.zeros(n, KEYPOINT_DTYPE)
+        k["x"] = rng.uniform(0, width - 1, n)
+        k["y"] = rng.uniform(0, height - 1, n)
+        k["octave"] = rng.choice(8, size=n, p=_LEVEL_SHARE / _LEVEL_SHARE.sum())
+        k["angle"] = rng.uniform(0, 360, n)
+        k["size"] = 31
+        k["class_id"] = -1
+        return k
+
+    k1, k2 = keys(n1), keys(n2)
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    d2 = rng.integers(0, 256, (n2, 32), dtype=np.uint8)
+    node1 = rng.integers(0, n_nodes, n1)
+    node2 = rng.integers(0, n_nodes, n2)
+    i1 = rng.choice(n1, n_true, replace=False)
+    i2 = rng.choice(n2, n_true, replace=False)
+    # true 3D points seen by KF1 at its keypoints, reprojected into KF2
+    z = rng.uniform(3, 40, n_true)
+    Xc1 = np.stack([(k1["x"][i1] - K["cx"]) * z / K["fx"], (k1["y"][i1] - K["cy"]) * z / K["fy"], z], 1)
+    Xw = (Xc1 - T1[:3, 3]) @ T1[:3, :3]
+    Xc2 = Xw @ T2[:3, :3].T + T2[:3, 3]
+    u2 = K["fx"] * Xc2[:, 0] / Xc2[:, 2] + K["cx"] + rng.normal(0, 0.7, n_true)
+    v2 = K["fy"] * Xc2[:, 1] / Xc2[:, 2] + K["cy"] + rng.normal(0, 0.7, n_true)
+    k2["x"][i2], k2["y"][i2] = u2, v2
+    k2["octave"][i2] = k1["octave"][i1]
+    k2["angle"][i2] = np.mod(k1["angle"][i1] - 10 + rng.normal(0, 3, n_true), 360)
+    d2[i2] = _flip_bits(rng, d1[i1], rng.integers(0, noise_bits + 1, n_true))
+    node2[i2] = node1[i1]
+    ids = np.sort(rng.choice(10 ** 6, n_nodes, replace=False)).astype(np.uint32)
+
+    def side(kp, desc, node):
+        order = np.argsort(node, kind="stable")
+        counts = np.bincount(node, minlength=n_nodes)
+        present = counts > 0
+        off = np.concatenate([[0], np.cumsum(counts[present])]).astype(np.int32)
+        n = len(kp)
+        ur = np.where(rng.random(n) < p_stereo, kp["x"] - rng.uniform(1, 60, n), -1.0).astype(np.float32)
+        return dict(keys_un=kp, desc=desc, u_right=ur, has_mp=(rng.random(n) < p_mp).astype(np.uint8),
+                    node_id=ids[present], node_off=off, feat=order.astype(np.int32))
+
+    R1, t1, R2, t2 = T1[:3, :3], T1[:3, 3], T2[:3, :3], T2[:3, 3]
+    R12 = R1 @ R2.T
+    t12 = -R1 @ R2.T @ t2 + t1
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    F12 = np.linalg.inv(Km).T @ tx @ R12 @ np.linalg.inv(Km)
+    sf = scale_factors()
+    return dict(kf1=side(k1, d1, node1), kf2=side(k2, d2, node2), F12=F12.astype(np.float32),
+                C1w=(-R1.T @ t1).astype(np.float32), T2w=T2.astype(np.float32), fx=np.float32(K["fx"]),
+                fy=np.float32(K["fy"]), cx=np.float32(K["cx"]), cy=np.float32(K["cy"]), scale_factors2=sf,
+                level_sigma2_2=(sf * sf).astype(np.float32), true_pairs=(i1, i2))

@@ -173,6 +173,56 @@ def py_search(fr, pts, kind, th, nnratio=0.6, check_ori=True, mono=False, orb_di
                 continue
             level[i] = _predict(dmax, d, fr["log_scale_factor"], fr["nlevels"])
             track[i] = [u, v, f32(u - f32(bf * invz)), vc]
+    if kind == 3:  # Fuse matching half, src/ORBmatcher.cc:944-1054
+        isg = [f32(f32(1.0) / f32(s_ * s_)) for s_ in sf]
+        for i in range(npnt):
+            if not (pts["flags"][i] & 1):
+                continue
+            X = pts["pos"][i]
+            c = _mat3x1(T, X)
+            if c[2] < 0:
+                continue
+            invz = f32(f32(1.0) / c[2])
+            u = f32(f32(fx * f32(c[0] * invz)) + cx)
+            v = f32(f32(fy * f32(c[1] * invz)) + cy)
+            if not (u >= fr["min_x"] and u < fr["max_x"] and v >= fr["min_y"] and v < fr["max_y"]):
+                continue
+            urp = f32(u - f32(bf * invz))
+            PO = [f32(X[j] - Ow[j]) for j in range(3)]
+            d3 = _norm3(PO)
+            dmin, dmax = pts["dist_minmax"][i]
+            if d3 < f32(f32(0.8) * dmin) or d3 > f32(f32(1.2) * dmax):
+                continue
+            Pn = pts["normal"][i]
+            dot = (float(PO[0]) * float(Pn[0]) + float(PO[1]) * float(Pn[1])) + float(PO[2]) * float(Pn[2])
+            if dot < 0.5 * float(d3):
+                continue
+            lv = _predict(dmax, d3, fr["log_scale_factor"], fr["nlevels"])
+            rad = f32(f32(th) * sf[lv])
+            bd, bi = 256, -1
+            for idx in F.area(u, v, rad):
+                kl = int(keys["octave"][idx])
+                if kl < lv - 1 or kl > lv:
+                    continue
+                ex, ey = f32(u - keys["x"][idx]), f32(v - keys["y"][idx])
+                if ur is not None and ur[idx] >= 0:
+                    er = f32(urp - ur[idx])
+                    e2 = f32(f32(f32(ex * ex) + f32(ey * ey)) + f32(er * er))
+                    if float(f32(e2 * isg[kl])) > 7.8:
+                        continue
+                else:
+                    e2 = f32(f32(ex * ex) + f32(ey * ey))
+                    if float(f32(e2 * isg[kl])) > 5.99:
+                        continue
+                d = _ham(pts["desc"][i], fr["desc"][idx])
+                if d < bd:
+                    bd, bi = d, idx
+            if bd <= 50:
+                pm[i] = bi
+                who[bi] = i
+                nm += 1
+        fo = np.array([w if w >= 0 else -1 for w in who], np.int32)
+        return dict(nmatches=nm, frame_out=fo, point_match=np.array(pm, np.int32))
     if kind == 1:
         tlc = _mat3x1(np.asarray(last_Tcw, np.float32), Ow)
         fwd = tlc[2] > fr["b"] and not mono
@@ -274,6 +324,8 @@ def py_search(fr, pts, kind, th, nnratio=0.6, check_ori=True, mono=False, orb_di
 
 
 def _kw(kind, fr, variant=0):
+    if kind == 3:
+        return [dict(th=3.0), dict(th=1.0), dict(th=5.0), dict(th=3.0)][variant % 4]
     if kind == 0:
         return [dict(th=1.0, nnratio=0.8), dict(th=3.0, nnratio=0.8), dict(th=5.0, nnratio=0.8, frustum=True),
                 dict(th=1.0, nnratio=0.8, frustum=True)][variant % 4]
@@ -299,7 +351,7 @@ def _same(a, b, kind, frustum=False):
 
 
 # ------------------------------------------------------------------ CPU: oracle pinned
-@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_oracle_vs_python_restatement(kind, variant):
     fr = synth.projection_frame(10 + variant, n=400, width=300, height=200)
@@ -369,13 +421,19 @@ def _gpu(fr, pts, kind, **kw):
         return out
     if kind == 1:
         r = m.SearchByProjectionLastFrame(fr, pts, kw["last_Tcw"], kw["th"], kw.get("mono", False))
+    elif kind == 3:
+        nf, bi = m.Fuse(fr, pts, kw["th"])
+        fo = np.full(len(fr["keys_un"]), -1, np.int32)
+        for i in np.nonzero(bi >= 0)[0]:
+            fo[bi[i]] = i
+        return dict(nmatches=nf, frame_out=fo, point_match=bi)
     else:
         r = m.SearchByProjectionKeyFrame(fr, pts, kw["th"], kw["orb_dist"])
     return dict(nmatches=r[0], frame_out=r[1], point_match=r[2])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_gpu_projection_kitti(gpu, kind, variant):
     fr = synth.projection_frame(100 + variant, n=2000)
@@ -437,11 +495,11 @@ def test_gpu_projection_device_batch(gpu):
     from orb_slam2_commit_amd.orb import proj_problem
 
     probs, keep, refs = [], [], []
-    for b in range(12):
-        kind = b % 3
+    for b in range(16):
+        kind = b % 4
         fr = synth.projection_frame(300 + b, n=1500 + 37 * b)
         pts = synth.projection_points(400 + b, fr, kind, n_points=2000)
-        kw = _kw(kind, fr, b // 3)
+        kw = _kw(kind, fr, b // 4)
         refs.append((kind, kw, oracle.search_by_projection(fr, pts, kind, **kw)))
         dfr = dict(fr)
         for k in ("keys_un", "desc", "u_right", "occ"):
