@@ -39,6 +39,8 @@
  *   orbx_search_for_triangulation  ORBmatcher::SearchForTriangulation src/ORBmatcher.cc:738-925, include/ORBmatcher.h:134
  *   orbx_pose_optimization     Optimizer::PoseOptimization     src/Optimizer.cc:287-528, include/Optimizer.h:71
  *   orbx_pose_optimization_device      batch of the above (one block per frame)
+ *   orbx_distinctive_descriptors[_device]  MapPoint::ComputeDistinctiveDescriptors src/MapPoint.cc:249-320
+ *   orbx_undistort_keypoints[_device]      Frame::UndistortKeyPoints src/Frame.cc:471-506 (cv::undistortPoints)
  *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
  *                               (g2o graph build, optimize(5), outlier levels, optimize(10), vToErase;
  *                               the Map mutex/recovery part stays on the caller's side)
@@ -435,6 +437,34 @@ orbx_status orbx_pose_optimization(const orbx_pose_problem* p, int device);
 /* Batched, device-resident: problems[] is a HOST array whose pointers are device
  * pointers; one block per problem runs all four rounds on the GPU (no host round trips). */
 orbx_status orbx_pose_optimization_device(const orbx_pose_problem* problems, int n, void* stream);
+
+/* MapPoint::ComputeDistinctiveDescriptors() -- src/MapPoint.cc:249-320, include/MapPoint.h:83,
+ * for a batch of MapPoints.  Point p's observed descriptors (pKF->mDescriptors.row(idx) for
+ * each (pKF, idx) of mObservations in map order, bad KeyFrames skipped, :270-276) are rows
+ * obs_off[p] .. obs_off[p+1]-1 of desc (32 B each; at most 65535 per point).  best[p] =
+ * BestIdx within that list (-1: no observation, mDescriptor unchanged); out_desc (optional,
+ * n_points x 32) = the new mDescriptor. */
+orbx_status orbx_distinctive_descriptors(const uint8_t* desc, const int32_t* obs_off, int n_points, int32_t* best,
+                                         uint8_t* out_desc, int device); /* host pointers */
+orbx_status orbx_distinctive_descriptors_device(const uint8_t* desc, const int32_t* obs_off, int n_points,
+                                                int32_t* best, uint8_t* out_desc, void* stream);
+
+/* Frame::UndistortKeyPoints() -- src/Frame.cc:471-506, include/Frame.h:174 (cv::undistortPoints
+ * with P = K) and the corner pass of Frame::ComputeImageBounds (:508-537, four keypoints at the
+ * image corners).  K = mK row-major (float), dist = mDistCoef (k1, k2, p1, p2[, k3]). */
+typedef struct {
+  float K[9];
+  float dist[5];
+  int n_dist; /* 4 or 5 */
+} orbx_camera;
+
+orbx_status orbx_undistort_keypoints(const orbx_keypoint* keys, int n, const orbx_camera* cam,
+                                     orbx_keypoint* keys_un, int device); /* host pointers */
+/* Frame batch, device pointers: frame f's keypoints are keys[frame_off[f] .. frame_off[f+1]),
+ * at most max_keys each; cams[n_frames] is device-resident. */
+orbx_status orbx_undistort_keypoints_device(const orbx_keypoint* keys, const int32_t* frame_off, int n_frames,
+                                            int max_keys, const orbx_camera* cams, orbx_keypoint* keys_un,
+                                            void* stream);
 
 /* Per-stage HIP-event timers (the g2o G2OBatchStatistics analogue,
  * Thirdparty/g2o/g2o/core/batch_stats.h:38-79).  When enabled, every kernel

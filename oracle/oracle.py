@@ -138,6 +138,12 @@ def lib():
         L.oracle_pose_edge_probe.restype = None
         L.oracle_ldlt6.argtypes = [P, P, P]
         L.oracle_search_for_triangulation.argtypes = [C.POINTER(TriProblem)]
+        L.oracle_distinctive_descriptors.argtypes = [P, P, C.c_int, P, P]
+        L.oracle_distinctive_descriptors.restype = None
+        L.oracle_undistort_point.argtypes = [P, P, C.c_int, C.c_float, C.c_float, P, P]
+        L.oracle_undistort_point.restype = None
+        L.oracle_undistort_keypoints.argtypes = [P, C.c_int, P, P, C.c_int, P]
+        L.oracle_undistort_keypoints.restype = None
         _lib = L
     return _lib
 
@@ -553,3 +559,34 @@ def search_for_triangulation(prob, only_stereo=False, check_ori=True):
     p.match12, p.nmatches = _p(m), _p(nm)
     lib().oracle_search_for_triangulation(C.byref(p))
     return int(nm[0]), m[:p.kf1.n]
+
+
+# ------------------------------------------------------------ ComputeDistinctiveDescriptors / UndistortKeyPoints
+def distinctive_descriptors(desc, obs_off):
+    """MapPoint::ComputeDistinctiveDescriptors over a batch: desc[obs_off[p]:obs_off[p+1]] are point p's
+    observed descriptors.  Returns (best[n_points] int32 (-1: no observation), chosen[n_points,32] u8)."""
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    off = np.ascontiguousarray(obs_off, np.int32)
+    n = len(off) - 1
+    best = np.zeros(max(n, 1), np.int32)
+    out = np.zeros((max(n, 1), 32), np.uint8)
+    lib().oracle_distinctive_descriptors(_p(desc), _p(off), n, _p(best), _p(out))
+    return best[:n], out[:n]
+
+
+def undistort_keypoints(keys, K, dist):
+    """Frame::UndistortKeyPoints: keys (KEYPOINT_DTYPE), K float 3x3, dist = mDistCoef (4 or 5)."""
+    keys = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    Kf = np.ascontiguousarray(K, np.float32).reshape(9)
+    d = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    out = np.zeros(max(len(keys), 1), KEYPOINT_DTYPE)
+    lib().oracle_undistort_keypoints(_p(keys), len(keys), _p(Kf), _p(d), len(d), _p(out))
+    return out[:len(keys)]
+
+
+def undistort_point(K, dist, x, y):
+    Kf = np.ascontiguousarray(K, np.float32).reshape(9)
+    d = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    xo, yo = C.c_float(), C.c_float()
+    lib().oracle_undistort_point(_p(Kf), _p(d), len(d), C.c_float(x), C.c_float(y), C.byref(xo), C.byref(yo))
+    return np.float32(xo.value), np.float32(yo.value)

@@ -242,6 +242,14 @@ typedef struct {
   int32_t* nmatches;
 } oracle_tri_problem;
 int oracle_search_for_triangulation(const oracle_tri_problem* p);
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:249-320), batched:
+ * point p's observed descriptors are desc[obs_off[p] .. obs_off[p+1]). */
+void oracle_distinctive_descriptors(const uint8_t* desc, const int32_t* obs_off, int n_points, int32_t* best,
+                                    uint8_t* out_desc);
+/* Frame::UndistortKeyPoints (src/Frame.cc:471-506) via cvUndistortPoints (OpenCV 3.2). */
+void oracle_undistort_point(const float K[9], const float* dist, int n_dist, float x, float y, float* xo, float* yo);
+void oracle_undistort_keypoints(const oracle_keypoint* keys, int n, const float K[9], const float* dist, int n_dist,
+                                oracle_keypoint* keys_un);
 void oracle_pose_edge_probe(const double q[4], const double t[3], const double X[3], const double intr[5], int stereo,
                             const double obs[3], double err[3], double J[18]);
 int oracle_ldlt6(const double* H, const double* b, double* x);

@@ -111,6 +111,10 @@ class TriProblem(C.Structure):
                 ("check_ori", C.c_int), ("match12", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
+class Camera(C.Structure):
+    _fields_ = [("K", C.c_float * 9), ("dist", C.c_float * 5), ("n_dist", C.c_int)]
+
+
 class RandState(C.Structure):
     _fields_ = [("r", C.c_uint32 * 34), ("i", C.c_int32)]
 
@@ -152,7 +156,11 @@ SIGNATURES = {
     "orbx_pose_optimization_device": ([C.POINTER(PoseProblem), C.c_int, P], C.c_int),
     "orbx_search_for_triangulation": ([C.POINTER(TriProblem), C.c_int], C.c_int),
     "orbx_search_for_triangulation_device": ([C.POINTER(TriProblem), C.c_int, P], C.c_int),
-    "orbx_rand_seed": ([C.POINTER(RandState), C.c_uint32], None),
+    "orbx_distinctive_descriptors": ([P, P, C.c_int, P, P, C.c_int], C.c_int),
+    "orbx_distinctive_descriptors_device": ([P, P, C.c_int, P, P, P], C.c_int),
+    "orbx_undistort_keypoints": ([P, C.c_int, C.POINTER(Camera), P, C.c_int], C.c_int),
+    "orbx_undistort_keypoints_device": ([P, P, C.c_int, C.c_int, P, P, P], C.c_int),
+    "orbx_rand_seed":([C.POINTER(RandState), C.c_uint32], None),
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "orbx_ba_destroy": ([P], C.c_int),

@@ -168,6 +168,54 @@ def compute_stereo_matches(extractor_left, extractor_right, kps_left, desc_left,
     return uR, depth
 
 
+def compute_distinctive_descriptors(desc, obs_off, device=0):
+    """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:249-320) for a batch of MapPoints:
+    desc[obs_off[p]:obs_off[p+1]] are point p's observed descriptors in mObservations order.
+    Returns (best[n_points] int32, -1 where a point has no observation; mDescriptor[n_points, 32])."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    off = np.ascontiguousarray(obs_off, np.int32)
+    n = len(off) - 1
+    best = np.zeros(max(n, 1), np.int32)
+    out = np.zeros((max(n, 1), 32), np.uint8)
+    check(_lib.lib().orbx_distinctive_descriptors(ptr(d), ptr(off), n, ptr(best), ptr(out), int(device)),
+          "orbx_distinctive_descriptors")
+    return best[:n], out[:n]
+
+
+def camera(K, dist_coef):
+    """orbx_camera from mK (3x3) and mDistCoef (4 or 5 coefficients)."""
+    d = np.asarray(dist_coef, np.float32).reshape(-1)
+    cam = _lib.Camera()
+    cam.K[:] = _f32(K).reshape(9).tolist()
+    dd = np.zeros(5, np.float32)
+    dd[:len(d)] = d
+    cam.dist[:] = dd.tolist()
+    cam.n_dist = len(d)
+    return cam
+
+
+def undistort_keypoints(keys, K, dist_coef, device=0):
+    """Frame::UndistortKeyPoints (src/Frame.cc:471-506): mvKeysUn from mvKeys, mK and mDistCoef."""
+    k = np.ascontiguousarray(keys, KEYPOINT_DTYPE)
+    out = np.zeros(max(len(k), 1), KEYPOINT_DTYPE)
+    cam = camera(K, dist_coef)
+    check(_lib.lib().orbx_undistort_keypoints(ptr(k), len(k), C.byref(cam), ptr(out), int(device)),
+          "orbx_undistort_keypoints")
+    return out[:len(k)]
+
+
+def compute_image_bounds(cols, rows, K, dist_coef, device=0):
+    """Frame::ComputeImageBounds (src/Frame.cc:508-537): (mnMinX, mnMaxX, mnMinY, mnMaxY)."""
+    if float(np.float32(np.asarray(dist_coef, np.float32).reshape(-1)[0])) == 0.0:
+        return 0.0, float(cols), 0.0, float(rows)
+    c = np.zeros(4, KEYPOINT_DTYPE)
+    c["x"] = [0.0, cols, 0.0, cols]
+    c["y"] = [0.0, 0.0, rows, rows]
+    u = undistort_keypoints(c, K, dist_coef, device)
+    return (float(min(u["x"][0], u["x"][2])), float(max(u["x"][1], u["x"][3])),
+            float(min(u["y"][0], u["y"][1])), float(max(u["y"][2], u["y"][3])))
+
+
 def bow_side(side):
     """dict(desc, angle, valid, node_id, node_off, feat) -> (orbx_bow_side, keep-alive arrays)."""
     arrs = dict(desc=np.ascontiguousarray(side["desc"], np.uint8),
