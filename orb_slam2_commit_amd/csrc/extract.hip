@@ -19,7 +19,7 @@
 
 namespace orbx {
 
-__constant__ int8_t c_pattern[1024] = {
+__constant__ float c_pattern_f[1024] = {  // bit_pattern_31_ as floats (exact small integers)
 #include "brief_pattern_31.inc"
 };
 __constant__ int c_umax[16];
@@ -918,33 +918,91 @@ __global__ __launch_bounds__(BS) void k_octree(const Geometry* __restrict__ G, c
 // One wave per keypoint: IC_Angle on the raw level (src/ORBextractor.cc:77-105),
 // computeOrbDescriptor on the blurred level (:110-152), then the keypoint
 // record in level-major output order with pt *= mvScaleFactor[l] (:1201-1207).
+// Sum over the 64 lanes (all active), returned wave-uniform: DPP row_shr 1/2/4/8
+// prefix sums leave each 16-lane row's total in its last lane, then four readlanes.
+// (Integer adds: the order is immaterial.)
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+  return __builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31) + __builtin_amdgcn_readlane(v, 47) +
+         __builtin_amdgcn_readlane(v, 63);
+}
+
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+// describe's staged blurred patch: rotated bit_pattern_31_ points stay within
+// radius 18.39, so |row|, |col| <= 18 after cvRound
+constexpr int kPatchR = 18;
+constexpr int kPatchRows = 2 * kPatchR + 1;            // 37
+constexpr int kPatchDw = (3 + 2 * kPatchR + 1 + 3) / 4;  // 11 dwords: up to 3 bytes of alignment slack
+constexpr int kPatchIt = (kPatchRows * kPatchDw + 63) / 64;
+
+// One wave per keypoint: IC_Angle on the raw level (src/ORBextractor.cc:77-105),
+// computeOrbDescriptor on the blurred level (:110-152), then the keypoint
+// record in level-major output order with pt *= mvScaleFactor[l] (:1201-1207).
+// The keypoint index is wave-uniform (readfirstlane), so the level lookup and
+// the octree entry are scalar loads and every image access is a uniform base
+// plus a 32-bit lane offset.
 __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                  int32_t* __restrict__ counts, int kp_cap) {
+  // rBRIEF pattern as floats, once per block; each wave's 37 x 37 blurred patch
+  // (rows y-18..y+18, dword-aligned columns from (x-18) & ~3) staged with
+  // coalesced dword loads, so the 512 rotated samples are LDS gathers rather
+  // than ~30 cache lines per global gather instruction
+  __shared__ float4 s_pat[256];
+  __shared__ uint32_t s_patch[BS / 64][kPatchRows * kPatchDw];
   const int2 bi = xcd_block2();
   const int img = bi.y;
-  const int lane = threadIdx.x & 63;
-  const int i = bi.x * (BS / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  s_pat[threadIdx.x] = reinterpret_cast<const float4*>(c_pattern_f)[threadIdx.x];
+  __syncthreads();
+  const int i = __builtin_amdgcn_readfirstlane(bi.x * (BS / 64) + wv);
   const int nl = G->nlevels;
-  int pre[kMaxLevelsPlan + 1];
-  pre[0] = 0;
-  for (int l = 0; l < nl; l++) pre[l + 1] = pre[l] + B.oct_count[(size_t)img * nl + l];
-  const int total = pre[nl];
+  // level of keypoint i: per-level counts as independent scalar loads, then an
+  // unrolled scan in scalar registers (no dependent load chain, no indexing)
+  const int* oc = B.oct_count + (size_t)img * nl;
+  int cnt[kMaxLevelsPlan];
+#pragma unroll
+  for (int ll = 0; ll < kMaxLevelsPlan; ll++) cnt[ll] = ll < nl ? oc[ll] : 0;
+  int total = 0, l = 0, first = 0;
+#pragma unroll
+  for (int ll = 0; ll < kMaxLevelsPlan; ll++) {
+    if (i >= total) {  // last level whose start is <= i
+      l = ll;
+      first = total;
+    }
+    total += cnt[ll];
+  }
   if (bi.x == 0 && threadIdx.x == 0) counts[img] = total;
-  if (i >= total) return;
-  int l = 0;
-  while (pre[l + 1] <= i) l++;
+  if (i >= total) return;  // wave-uniform: the DPP sums below see a full wave
   const LevelGeom& L = G->lv[l];
-  const uint32_t v = B.oct[(size_t)img * G->oct_total + L.oct_off + (i - pre[l])];
+  const uint32_t v = B.oct[(size_t)img * G->oct_total + L.oct_off + (i - first)];
   const int x = v & 0xFFF, y = (v >> 12) & 0xFFF, score = v >> 24;
   const int w = L.w;
+  const uint8_t* blur = B.blur + (size_t)img * G->blur_bytes + L.boff;  // uniform
+  const int bs = L.bstride;
+  const int x0 = (x - kPatchR) & ~3;  // x - 18 >= 1: keypoints sit >= 19 px inside the level
+  uint32_t pv[kPatchIt];
+  {
+    const uint8_t* pb = blur + (size_t)(y - kPatchR) * bs + x0;  // 4-byte aligned (16-byte row stride)
+#pragma unroll
+    for (int k = 0; k < kPatchIt; k++) {
+      const int q = lane + 64 * k, r = q / kPatchDw, j = q - r * kPatchDw;
+      pv[k] = q < kPatchRows * kPatchDw ? *reinterpret_cast<const uint32_t*>(pb + (uint32_t)(r * bs + 4 * j)) : 0u;
+    }
+  }
   // IC_Angle: lanes 0..61 -> column u = lane%31-15, rows v in [-15,0] or [1,15]
   const uint8_t* raw = level_ptr(*G, B, img, l);
   int m01 = 0, m10 = 0;
   {
     // circle table in scalar registers; every load below is unconditional (the
     // 31x31 box around a keypoint is always inside its level) and masked by
-    // multiplication, so all 16 loads are in flight together
+    // multiplication, so all 16 loads are in flight together.  Row i of the
+    // top half is (y-15+i), of the bottom half (y+1+i): a uniform row base plus
+    // the lane's column offset (bottom lanes +16 rows).
     int um[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) um[i] = c_umax[i];
@@ -952,14 +1010,16 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
     const int u = lane < 62 ? (lane % 31) - 15 : 0;
     const int au = u < 0 ? -u : u;
     const int vb = lo ? -15 : 1;
-    const uint8_t* col = raw + (ptrdiff_t)(y + vb) * w + (x + u);
+    const uint8_t* top = raw + (size_t)(y - 15) * w + x;  // uniform
+    const uint32_t o = (uint32_t)(u + 15) + (lo ? 0u : 16u * (uint32_t)w);
+    const uint32_t o15 = lo ? o : o - (uint32_t)w;  // the bottom half has 15 rows: row 15 re-reads row 14 (masked)
     int I[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int lim = lo ? um[15 - i] : (i < 15 ? um[1 + i] : -1);
       const int ok = (lane < 62 && au <= lim) ? 1 : 0;
-      const int r = i < 15 || lo ? i : 14;  // lanes >= 31 have 15 rows; row 15 re-reads row 14 (masked)
-      I[i] = (int)col[(ptrdiff_t)r * w] * ok;
+      const uint8_t* rowp = top - 15 + (size_t)i * w;
+      I[i] = (int)rowp[i < 15 ? o : o15] * ok;
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) {
@@ -967,32 +1027,48 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
       m01 += (vb + i) * I[i];
     }
   }
-  m01 = wave_sum(m01);
-  m10 = wave_sum(m10);
+  m01 = wave_sum_dpp(m01);
+  m10 = wave_sum_dpp(m10);
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float sn, cs;
   sincos_det(angle * factorPI, &sn, &cs);
   const float a = cs, b = sn;
-  const uint8_t* blur = B.blur + (size_t)img * G->blur_bytes + L.boff;
-  const int bs = L.bstride;
-  const uint8_t* center = blur + (size_t)y * bs + x;
+#pragma unroll
+  for (int k = 0; k < kPatchIt; k++)
+    if (lane + 64 * k < kPatchRows * kPatchDw) s_patch[wv][lane + 64 * k] = pv[k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint8_t* patch = reinterpret_cast<const uint8_t*>(s_patch[wv]);
+  constexpr int PS = 4 * kPatchDw;  // patch row stride (bytes)
+  // Rotated pattern point (px, py) -> pixel (y + r, x + c) with
+  //   r = cvRound(px*b + py*a), c = cvRound(px*a - py*b)    (src/ORBextractor.cc:119-125)
+  // Both coordinates ride in packed-f32 lanes.  Each sum is rounded exactly as
+  // the scalar expression (products, then the add / subtract); adding 1.5*2^23
+  // rounds it to an integer half-to-even (|sum| < 2^22), leaving 0x4B400000 + r
+  // in the bits.  A 24-bit mad on the raw bits ((0x400000 + r) * bs, low 24 bits
+  // sign-extended) plus the uniform correction gives the 32-bit pixel offset.
+  const float2v ba = {b, a}, ab = {a, b}, magic = {12582912.0f, 12582912.0f};
+  const uint32_t corr = (uint32_t)(kPatchR * PS + (x - x0)) - (0x400000u * (uint32_t)PS + 0x4B400000u);
   int bits = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int pair = lane * 4 + k;  // bit (pair & 7) of byte pair >> 3
+    const float4 pp = s_pat[pair];  // points 2*pair, 2*pair + 1
     int t[2];
 #pragma unroll
     for (int e = 0; e < 2; e++) {
-      const int idx = 4 * pair + 2 * e;
-      const float px = (float)c_pattern[idx], py = (float)c_pattern[idx + 1];
-      const int r = round_even(px * b + py * a);
-      const int c = round_even(px * a - py * b);
-      t[e] = center[r * bs + c];
+      const float px = e ? pp.z : pp.x, py = e ? pp.w : pp.y;
+      const float2v P = (float2v){px, px} * ba;  // {px*b, px*a}
+      const float2v Q = (float2v){py, -py} * ab;  // {py*a, -(py*b)}: negation is exact
+      const float2v M = (P + Q) + magic;
+      const uint32_t mr = __float_as_uint(M.x), mc = __float_as_uint(M.y);
+      t[e] = patch[(uint32_t)__mul24((int)mr, PS) + mc + corr];
     }
     bits |= (t[0] < t[1]) << k;
   }
-  const int other = __shfl_xor(bits, 1, 64);
+  const int other = __builtin_amdgcn_mov_dpp(bits, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]: lane ^ 1
   uint8_t* d = desc + ((size_t)img * kp_cap + i) * 32;
   if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(bits | (other << 4));
   if (lane == 0) {
