@@ -101,10 +101,14 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometr
 }
 
 constexpr int kKpsPerBlock = 128;
+// SAD staging per wave: 11 rows x (4 left + 6 right) dwords
+constexpr int kSadDwL = 4, kSadDwR = 6, kSadDw = kSadDwL + kSadDwR;
+constexpr int kSadIt = (11 * kSadDw + 63) / 64;
 
 // No LDS: candidate ranges come from the row table, (x, index) pairs from the
 // sorted array, so occupancy is bounded by registers only.
 __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
+  __shared__ uint32_t s_sad[SBS / 64][11 * kSadDw];
   const int2 bi = xcd_block2();
   const int f = bi.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
@@ -189,26 +193,56 @@ __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geomet
     const uint8_t* imR = level_ptr(*G, A.BR, rimg, levelL);
     const int lw = Lv.w;
     const int cy = (int)scaledvL, cxL = (int)scaleduL, cxR0 = (int)scaleduR0;
+    // Stage the 11x11 left patch (columns cxL-5..cxL+5) and the 11x21 right
+    // strip (cxR0-10..cxR0+10) of rows cy-5..cy+5 in this wave's LDS slot:
+    // aligned dword loads, each row keeping its byte shift (rows are packed at
+    // the level width), dwords wholly past a row's bytes not loaded.
+    uint32_t* sp = s_sad[wid];
+    const uint8_t* rowL0 = imL + (size_t)(cy - w) * lw + (cxL - w);
+    const uint8_t* rowR0 = imR + (size_t)(cy - w) * lw + (cxR0 - 2 * w);
+    {
+      uint32_t sv[kSadIt];
+#pragma unroll
+      for (int k = 0; k < kSadIt; k++) {
+        const int q = lane + 64 * k, r = q / kSadDw, j = q - r * kSadDw;
+        const bool left = j < kSadDwL;
+        const uintptr_t a = (uintptr_t)((left ? rowL0 : rowR0) + (size_t)r * lw);
+        const int jj = left ? j : j - kSadDwL, need = left ? 2 * w + 1 : 4 * w + 1;
+        sv[k] = 0;
+        if (q < (2 * w + 1) * kSadDw && 4 * jj < (int)(a & 3) + need) sv[k] = *((const uint32_t*)(a & ~(uintptr_t)3) + jj);
+      }
+#pragma unroll
+      for (int k = 0; k < kSadIt; k++)
+        if (lane + 64 * k < (2 * w + 1) * kSadDw) sp[lane + 64 * k] = sv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(sp);
     int part = 0;
     {
-      // lanes 0..54: inc = lane % 11, rows g, g+5, g+10 (g = lane / 11); branchless so that
-      // every patch load of the lane is in flight together (rows >= 11 clamped and masked)
+      // lanes 0..54: inc = lane % 11, rows g, g+5, g+10 (g = lane / 11); rows >= 11
+      // clamped and masked
       const int ll = lane < 55 ? lane : 0;
       const int inc = ll % 11 - L;
       const int g = ll / 11;
-      const int cx = cxR0 + inc;
-      const int cL = imL[(size_t)cy * lw + cxL];
-      const int cR = imR[(size_t)cy * lw + cx];
+      const uint32_t aL0 = (uint32_t)(uintptr_t)rowL0, aR0 = (uint32_t)(uintptr_t)rowR0;
+      auto lpix = [&](int dy, int dx) -> int {
+        return sb[4 * kSadDw * dy + ((aL0 + (uint32_t)(dy * lw)) & 3) + dx];
+      };
+      auto rpix = [&](int dy, int dx) -> int {  // strip column dx
+        return sb[4 * (kSadDw * dy + kSadDwL) + ((aR0 + (uint32_t)(dy * lw)) & 3) + dx];
+      };
+      const int cL = lpix(w, w);
+      const int cR = rpix(w, inc + 2 * w);
       int pv[3][2 * w + 1], qv[3][2 * w + 1];
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         const int dy = min(g + 5 * k, 2 * w);
-        const uint8_t* pl = imL + (size_t)(cy - w + dy) * lw + cxL - w;
-        const uint8_t* pr = imR + (size_t)(cy - w + dy) * lw + cx - w;
 #pragma unroll
         for (int dx = 0; dx < 2 * w + 1; dx++) {
-          pv[k][dx] = pl[dx];
-          qv[k][dx] = pr[dx];
+          pv[k][dx] = lpix(dy, dx);
+          qv[k][dx] = rpix(dy, inc + w + dx);
         }
       }
 #pragma unroll
