@@ -100,7 +100,9 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometr
   }
 }
 
-constexpr int kKpsPerBlock = 128;
+// 16 left keypoints per 4-wave block (4 per wave): 128 per block left the
+// waves walking 32 keypoints each in series (0.39 ms/step; 16: 0.29 ms)
+constexpr int kKpsPerBlock = 16;
 // SAD staging per wave: 11 rows x (4 left + 6 right) dwords
 constexpr int kSadDwL = 4, kSadDwR = 6, kSadDw = kSadDwL + kSadDwR;
 constexpr int kSadIt = (11 * kSadDw + 63) / 64;
