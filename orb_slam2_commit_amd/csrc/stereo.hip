@@ -28,7 +28,10 @@ __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); 
 // [floor(y - 2 s_o), ceil(y + 2 s_o)] contains Y -- the reference's
 // vRowIndices[Y] (src/Frame.cc:572-590) split by octave, in iR order within
 // equal y.  Also writes (x, index) in sorted order for the match kernel.
-__global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometry* __restrict__ G) {
+// one 1024-thread block per frame: the bitonic stages and the per-(octave,row)
+// binary searches are the serial part, spread over 4x the threads of SBS
+constexpr int PBS = 1024;
+__global__ __launch_bounds__(PBS) void k_stereo_prep(StereoArgs A, const Geometry* __restrict__ G) {
   __shared__ uint64_t keys[kMaxStereoKps];
   __shared__ int ost[kMaxLevelsPlan + 1];
   const int f = blockIdx.x, tid = threadIdx.x;
@@ -36,7 +39,7 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometr
   const orbx_keypoint* kR = A.kpR + (size_t)f * A.kR_stride;
   int P2 = 2;
   while (P2 < nR) P2 <<= 1;
-  for (int i = tid; i < P2; i += SBS) {
+  for (int i = tid; i < P2; i += PBS) {
     uint64_t k = ~0ull;
     if (i < nR) {
       const orbx_keypoint kp = kR[i];
@@ -47,7 +50,7 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometr
   __syncthreads();
   for (int size = 2; size <= P2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < P2 / 2; i += SBS) {
+      for (int i = tid; i < P2 / 2; i += PBS) {
         const int lo = 2 * i - (i & (stride - 1));
         const int hi = lo + stride;
         const bool asc = (lo & size) == 0;
@@ -62,7 +65,7 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometr
   }
   uint64_t* out = A.rkeys + (size_t)f * kMaxStereoKps;
   int2* rxi = A.rxi + (size_t)f * kMaxStereoKps;
-  for (int i = tid; i < nR; i += SBS) {
+  for (int i = tid; i < nR; i += PBS) {
     const uint64_t k = keys[i];
     out[i] = k;
     const int idx = (int)(k & 0xFFF);
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometr
   }
   // octave starts
   int* os = A.oct_start + (size_t)f * (kMaxLevelsPlan + 1);
-  for (int o = tid; o <= A.nlevels; o += SBS) {
+  for (int o = tid; o <= A.nlevels; o += PBS) {
     int lo = 0, hi = nR;  // first i with octave >= o
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(SBS) void k_stereo_prep(StereoArgs A, const Geometr
   __syncthreads();
   // row table: first with ceil(y + r) >= Y, then first (from there) with floor(y - r) > Y
   uint32_t* tab = A.rtab + (size_t)f * A.nlevels * A.rows;
-  for (int e = tid; e < A.nlevels * A.rows; e += SBS) {
+  for (int e = tid; e < A.nlevels * A.rows; e += PBS) {
     const int o = e / A.rows, Y = e - o * A.rows;
     const float r = 2.0f * G->lv[o].scale;
     const int lo = ost[o], hi = ost[o + 1];
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(SBS) void k_hamming(const uint8_t* __restrict__ a, 
 hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st,
                          StageTimer* T) {
   T->begin(st);
-  hipLaunchKernelGGL(k_stereo_prep, dim3(n_frames), dim3(SBS), 0, st, A, Gd);
+  hipLaunchKernelGGL(k_stereo_prep, dim3(n_frames), dim3(PBS), 0, st, A, Gd);
   T->end(ST_STEREO_PREP, st);
   const int nb = (maxL + kKpsPerBlock - 1) / kKpsPerBlock;
   T->begin(st);
