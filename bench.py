@@ -37,8 +37,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="stereo frames per step per GPU")
-    ap.add_argument("--unique", type=int, default=16, help="distinct synthetic stereo pairs tiled into the batch")
+    ap.add_argument("--batch", type=int, default=256, help="stereo frames per step per GPU")
+    ap.add_argument("--unique", type=int, default=16, help="seeded synthetic stereo scenes per rank (slots are distinct rolls of them)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
@@ -155,7 +155,10 @@ def main():
     W, H, B = KITTI["width"], KITTI["height"], args.batch
     # synthetic frames: distinct seeds per rank (frame shards), tiled into the batch
     pairs = [synth.stereo_pair(seed, W, H) for seed in odist.frame_seeds(rank, args.unique)]
-    host = np.stack([pairs[f % len(pairs)][k] for f in range(B) for k in (0, 1)])
+    # every batch slot distinct: slot f is pair f % U rolled horizontally by 53 * (f // U) px
+    # (L and R alike, so the disparity field is kept), so no two slots share bytes in HBM
+    U = len(pairs)
+    host = np.stack([np.roll(pairs[f % U][k], 53 * (f // U), axis=1) for f in range(B) for k in (0, 1)])
     images = torch.from_numpy(host).to(dev)
     ex = ORBextractor(KITTI["nfeatures"], 1.2, 8, 20, 7, device=local)
     cap = ex.max_keypoints(W, H)
@@ -236,7 +239,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded stereo scenes, %d distinct pairs per rank tiled into the batch)" % args.unique,
+        "data": "synthetic (%d seeded stereo scenes per rank, each batch slot a distinct horizontal roll of one)" % args.unique,
         "config": {"workload": "KITTI-00 stereo 1241x376, 2000 features, extract L+R + ComputeStereoMatches",
                    "batch_frames_per_gpu": B, "global_batch_frames": B * world, "nlevels": 8,
                    "scale_factor": 1.2, "fast_th": [20, 7], "parallelism": "frame-sharded x%d" % world},
