@@ -234,21 +234,38 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
     // 134 rows x 36 dwords / 256 threads <= 19 loads per thread
     window_to_lds<19>(src + (size_t)(y0 - 3) * w + (x0 - 4), w, TR, kBIn, tin, kBIn, tid, BS);
   } else {
-    for (int q0 = 0; q0 < TR * kBIn; q0 += 8 * BS) {
-      uint8_t v[8];
+    // border tile (every tile of the small levels): one LDS dword per item; the
+    // source row is reflected once, a dword wholly inside the row is built from
+    // two aligned source dwords (alignbyte), only the <= 2 edge dwords of a row
+    // go byte by byte through REFLECT_101
+    constexpr int DW = kBIn / 4;
+    uint32_t* tin32 = reinterpret_cast<uint32_t*>(tin);
+    for (int q0 = 0; q0 < TR * DW; q0 += 8 * BS) {
+      uint32_t v[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int q = q0 + tid + k * BS;
         v[k] = 0;
-        if (q < TR * kBIn) {
-          const int ty = q / kBIn, tx = q - ty * kBIn;
-          v[k] = src[(size_t)reflect101(y0 + ty - 3, h) * w + reflect101(x0 + tx - 4, w)];
+        if (q < TR * DW) {
+          const int ty = q / DW, jd = q - ty * DW;
+          const uint8_t* row = src + (size_t)__umul24(reflect101(y0 + ty - 3, h), w);
+          const int sx = x0 - 4 + 4 * jd;
+          if (sx >= 0 && sx + 4 <= w) {
+            const uintptr_t a = (uintptr_t)(row + sx);
+            const uint32_t* pa = (const uint32_t*)(a & ~(uintptr_t)3);
+            const int sh = (int)(a & 3);
+            // pa[1] holds byte a+3 (inside the row) whenever sh != 0: same page
+            v[k] = sh ? __builtin_amdgcn_alignbyte(pa[1], pa[0], sh) : pa[0];
+          } else {
+#pragma unroll
+            for (int b = 0; b < 4; b++) v[k] |= (uint32_t)row[reflect101(sx + b, w)] << (8 * b);
+          }
         }
       }
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int q = q0 + tid + k * BS;
-        if (q < TR * kBIn) tin[q] = v[k];
+        if (q < TR * DW) tin32[q] = v[k];
       }
     }
   }
@@ -287,8 +304,9 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
       uint32_t packed = 0;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const int acc = k3 * win[3][j] + k2 * (win[2][j] + win[4][j]) + k1 * (win[1][j] + win[5][j]) +
-                        k0 * (win[0][j] + win[6][j]);
+        // 24-bit multiplies (v_mad_u32_u24, full rate): row sums <= 257*255, pair sums < 2^17, weights < 256
+        const int acc = (int)(__umul24(k3, win[3][j]) + __umul24(k2, win[2][j] + win[4][j]) +
+                              __umul24(k1, win[1][j] + win[5][j]) + __umul24(k0, win[0][j] + win[6][j]));
         // SSE2 groups: rint(acc / 2^16) (ties to even; acc >= 2^24 saturates either way); tail: (acc + 2^15) >> 16
         const int v = (all_simd || xg + j < simd_w) ? (acc + 0x7FFF + ((acc >> 16) & 1)) >> 16 : (acc + (1 << 15)) >> 16;
         packed |= (uint32_t)min(v, 255) << (8 * j);
@@ -431,18 +449,18 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
       const int r = rg + k * rpi;
-      const int sr = (s0 + r * wm) & 3;
+      const int sr = (s0 + __mul24(r, wm)) & 3;
       v[k] = 0;
       if (rg < rpi && r < TH && 4 * j < sr + TW) {
-        const uintptr_t ar = a0 + (uintptr_t)r * lw;
+        const uintptr_t ar = a0 + (uintptr_t)__umul24(r, lw);
         v[k] = *((const uint32_t*)(ar & ~(uintptr_t)3) + j);
       }
     }
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
       const int r = rg + k * rpi;
-      const int sr = (s0 + r * wm) & 3;
-      if (rg < rpi && r < TH && 4 * j < sr + TW) *(uint32_t*)&tile_raw[r * S + s0 - sr + 4 + 4 * j] = v[k];
+      const int sr = (s0 + __mul24(r, wm)) & 3;
+      if (rg < rpi && r < TH && 4 * j < sr + TW) *(uint32_t*)&tile_raw[__mul24(r, S) + s0 - sr + 4 + 4 * j] = v[k];
     }
   }
   const uint8_t* tile = tile_raw + 4 + s0;  // pixel (r, col) = tile[r*S + col]
@@ -469,7 +487,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
 #pragma unroll
     for (int u = 0; u < QU; u++) {
       const int y = min(y0r + u * rows_per + ly, H - 1);
-      const uint8_t* t = &tile[(y + 3) * S + lxc + 3];
+      const uint8_t* t = &tile[__mul24(y + 3, S) + lxc + 3];
       cv[u] = t[0];
       c0[u] = t[3 * S];
       c4[u] = t[3];
@@ -500,7 +518,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     bool corner = false;
     if (i < n) {
       pix = list[i];
-      corner = ring_corner(&tile[((pix >> 6) + 3) * S + (pix & 63) + 3], S, tlo);
+      corner = ring_corner(&tile[__mul24((pix >> 6) + 3, S) + (pix & 63) + 3], S, tlo);
     }
     const uint64_t m = __ballot(corner);
     __syncthreads();
@@ -513,14 +531,14 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     const int i = i0 + lane;
     if (i < nc) {
       const int pix = list[i];
-      const int sc = ring_score(&tile[((pix >> 6) + 3) * S + (pix & 63) + 3], S);
-      smap[((pix >> 6) + 1) * kMapS + (pix & 63) + 1] = (uint8_t)(sc + 1);
+      const int sc = ring_score(&tile[__mul24((pix >> 6) + 3, S) + (pix & 63) + 3], S);
+      smap[__mul24((pix >> 6) + 1, kMapS) + (pix & 63) + 1] = (uint8_t)(sc + 1);
     }
   }
   __syncthreads();
   // strict NMS inside the region; the map's zero border stands for "outside"
   auto keep = [&](int pix, int thr) -> bool {  // thr = t + 1 in map units (S + 1)
-    const uint8_t* m = smap + ((pix >> 6) + 1) * kMapS + (pix & 63) + 1;
+    const uint8_t* m = smap + __mul24((pix >> 6) + 1, kMapS) + (pix & 63) + 1;
     const int s = m[0];
     const int n0 = m[-kMapS - 1], n1 = m[-kMapS], n2 = m[-kMapS + 1], n3 = m[-1], n4 = m[1], n5 = m[kMapS - 1],
               n6 = m[kMapS], n7 = m[kMapS + 1];
@@ -558,7 +576,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
       const int p = pos + __popcll(m & lt);
       const int y = pix >> 6, x = pix & 63;
       if (p < c.cap)
-        out[p] = ((uint32_t)(smap[(y + 1) * kMapS + x + 1] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) |
+        out[p] = ((uint32_t)(smap[__mul24(y + 1, kMapS) + x + 1] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) |
                  (uint32_t)(c.x0 + x);
     }
     pos += __popcll(m);
