@@ -145,7 +145,10 @@ def main():
 
     from orb_slam2_commit_amd import dist as odist
     rank, local, world = odist.env_rank()
-    odist.init("nccl", rank, world)
+    # RCCL ("nccl") over xGMI; ORBX_DIST_BACKEND=gloo rehearses the multi-rank flow on a box with
+    # fewer GPUs than ranks (ranks then wrap onto the available devices; collectives on CPU tensors)
+    odist.init(os.environ.get("ORBX_DIST_BACKEND", "nccl"), rank, world)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -27,12 +27,19 @@ def frame_seeds(rank, n_unique):
     return [1000 * rank + s for s in range(n_unique)]
 
 
+def _coll_device(device):
+    """Collective tensors live on the GPU for RCCL, on the CPU for gloo."""
+    import torch.distributed as dist
+    return None if dist.get_backend() == "gloo" else device
+
+
 def max_over_ranks(value, device=None):
     """Max of a float over all ranks (the slowest rank defines the job time)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
+    device = _coll_device(device)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -44,6 +51,7 @@ def sum_over_ranks(value, device=None):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
+    device = _coll_device(device)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
