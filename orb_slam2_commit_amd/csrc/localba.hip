@@ -1375,11 +1375,44 @@ struct LocalBA {
   int nbu = 1, n_rb = 8;           // k_ba_update blocks; doubles in the readback block
   double* rb_host = nullptr;       // pinned readback block
   int rb_cap = 0;
+  hipEvent_t rb_ev = nullptr;      // recorded after the readback copy (the wait skips later work)
+  // Two sets of the linearisation outputs the LM trial reads.  While the host
+  // waits for a trial's readback, the next iteration's linearisation at the
+  // trial state is already running into the other set; an accepted trial (the
+  // common case) then starts its next iteration on that set, a rejected one
+  // keeps the current set untouched.
+  struct LinSet {
+    double *Hpl, *Hll, *bl, *dmax_p, *Hpp, *bp;
+  };
+  LinSet lin[2] = {};
+  int lin_cur = 0;
+  DBuf<double> Hpl2, Hll2, bl2, dmax2, Hpp2, bp2;
   LocalBA() = default;
   LocalBA(const LocalBA&) = delete;
   LocalBA& operator=(const LocalBA&) = delete;
   ~LocalBA() {
     if (rb_host) (void)hipHostFree(rb_host);
+    if (rb_ev) (void)hipEventDestroy(rb_ev);
+  }
+  static void use_lin(BaDev& D, const LinSet& L) {
+    D.Hpl = L.Hpl;
+    D.Hll = L.Hll;
+    D.bl = L.bl;
+    D.Hpp = L.Hpp;
+    D.bp = L.bp;
+    D.dmax_p = L.dmax_p;
+    D.dmax_c = L.dmax_p + D.npa;  // contiguous: one max-reduction for lambda init
+  }
+  // computeActiveErrors is not repeated: the errors/chi stored by the trial
+  // (recompute, slot 1) are the ones at the state being linearised
+  void linearize(const BaDev& Dl, hipStream_t st) {
+    const int ga = std::max((Dl.na + LBS - 1) / LBS, 1);
+    if (Dl.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3(ga), dim3(LBS), 0, st, Dl);
+    if (Dl.npa > 0) hipLaunchKernelGGL(k_ba_point_sum, dim3((Dl.npa + LBS - 1) / LBS), dim3(LBS), 0, st, Dl);
+    if (Dl.nposes > 0) {
+      hipLaunchKernelGGL(k_ba_cam_sum, dim3(Dl.nposes, Dl.gsplit), dim3(kGB), 0, st, Dl);
+      hipLaunchKernelGGL(k_ba_cam_fin, dim3(Dl.nposes), dim3(64), 0, st, Dl);
+    }
   }
   // host scratch, reused across calls
   std::vector<int> act, pos_pt, chidx, pose_cam, pt_off, pt_id, cam_off, cam_pos, cnt, pcam, ccnt, boff;
@@ -1505,6 +1538,13 @@ struct LocalBA {
     BA_CHECK(c.dmax_p.alloc(npa + nposes));
     BA_CHECK(c.Hpp.alloc(36 * (size_t)nposes));
     BA_CHECK(c.bp.alloc(N));
+    BA_CHECK(Hpl2.alloc(18 * (size_t)na));
+    BA_CHECK(Hll2.alloc(9 * (size_t)npa));
+    BA_CHECK(bl2.alloc(3 * (size_t)npa));
+    BA_CHECK(dmax2.alloc(npa + nposes));
+    BA_CHECK(Hpp2.alloc(36 * (size_t)nposes));
+    BA_CHECK(bp2.alloc(N));
+    if (!rb_ev) BA_CHECK(hipEventCreateWithFlags(&rb_ev, hipEventDisableTiming));
     BA_CHECK(c.xp.alloc(N));
     BA_CHECK(c.bs.alloc(N));
     BA_CHECK(c.S.alloc(N * N));
@@ -1532,21 +1572,18 @@ struct LocalBA {
     D.ptab = c.ptab.p;
     if (D.nblk > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk, gsplit), dim3(kPB), 0, st, D);
     BA_CHECK(hipGetLastError());
-    D.Hpl = c.Hpl.p;
     D.ptc = c.ptc.p;
     D.cmc = c.cmc.p;
     D.BD = c.BD.p;
     D.cf = c.cf.p;
-    D.Hll = c.Hll.p;
-    D.bl = c.bl.p;
     D.Dinv = c.Dinv.p;
-    D.Hpp = c.Hpp.p;
-    D.bp = c.bp.p;
     D.xp = c.xp.p;
     D.bs = c.bs.p;
     D.S = c.S.p;
-    D.dmax_p = c.dmax_p.p;
-    D.dmax_c = c.dmax_p.p + npa;  // contiguous: one max-reduction for lambda init
+    lin[0] = LinSet{c.Hpl.p, c.Hll.p, c.bl.p, c.dmax_p.p, c.Hpp.p, c.bp.p};
+    lin[1] = LinSet{Hpl2.p, Hll2.p, bl2.p, dmax2.p, Hpp2.p, bp2.p};
+    lin_cur = 0;
+    use_lin(D, lin[0]);
     const auto T4 = now();
     t_struct[0] += ms(T0, T1);
     t_struct[1] += ms(T1, T2);
@@ -1564,8 +1601,16 @@ struct LocalBA {
   // (chi of the two error slots) and out[4] (LM scale) are the block
   // partials added in block order.
   hipError_t read_scalars(double out[5], hipStream_t st) {
+    hipError_t e = start_read(st);
+    return e == hipSuccess ? finish_read(out) : e;
+  }
+  hipError_t start_read(hipStream_t st) {
     hipError_t e = hipMemcpyAsync(rb_host, D.scal, n_rb * sizeof(double), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipEventRecord(rb_ev, st);
+    return e;
+  }
+  hipError_t finish_read(double out[5]) {
+    hipError_t e = hipEventSynchronize(rb_ev);
     if (e != hipSuccess) return e;
     out[2] = rb_host[2];
     out[3] = rb_host[3];
@@ -1598,14 +1643,19 @@ struct LocalBA {
     const int gp = std::max((D.npa + D.nposes + LBS - 1) / LBS, 1);
     const int ga = std::max((D.na + LBS - 1) / LBS, 1);
     double sc[5];
+    const bool spec_on = std::getenv("ORBX_BA_NO_SPEC") == nullptr;  // A/B switch
+    bool spec_ready = false;  // the other LinSet holds the linearisation at the current state
+    double spec_chi = 0;      // its chi (the accepted trial's)
     for (int i = 0; i < iterations && !(stop && *stop); i++) {
-      BA_CHECK(errors(st, 1, 0));  // computeActiveErrors; activeRobustChi2 -> scal[0]
-      if (D.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3(ga), dim3(LBS), 0, st, D);
-      if (D.npa > 0) hipLaunchKernelGGL(k_ba_point_sum, dim3((D.npa + LBS - 1) / LBS), dim3(LBS), 0, st, D);
-      if (D.nposes > 0) {
-        hipLaunchKernelGGL(k_ba_cam_sum, dim3(D.nposes, D.gsplit), dim3(kGB), 0, st, D);
-        hipLaunchKernelGGL(k_ba_cam_fin, dim3(D.nposes), dim3(64), 0, st, D);
+      const bool from_spec = spec_ready;
+      if (from_spec) {
+        lin_cur ^= 1;
+        use_lin(D, lin[lin_cur]);
+      } else {
+        BA_CHECK(errors(st, 1, 0));  // computeActiveErrors; activeRobustChi2 -> scal[0]
+        linearize(D, st);
       }
+      spec_ready = false;
       BA_CHECK(hipGetLastError());
       if (i == 0) {
         hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D.dmax_p, D.npa + D.nposes, D.scal + 3, 1);
@@ -1626,8 +1676,17 @@ struct LocalBA {
         }
         hipLaunchKernelGGL(k_ba_update, dim3(gp), dim3(LBS), 0, st, D, lambda);
         BA_CHECK(errors(st, 1, 1));
-        BA_CHECK(read_scalars(sc, st));
-        if (qmax == 0) currentChi = iniChi = sc[0];
+        BA_CHECK(start_read(st));
+        bool launched = false;
+        if (spec_on && i + 1 < iterations) {  // next iteration's linearisation at the trial state
+          BaDev Ds = D;
+          use_lin(Ds, lin[lin_cur ^ 1]);
+          linearize(Ds, st);
+          BA_CHECK(hipGetLastError());
+          launched = true;
+        }
+        BA_CHECK(finish_read(sc));
+        if (qmax == 0) currentChi = iniChi = from_spec ? spec_chi : sc[0];
         const bool ok2 = sc[2] != 0.0;
         trials++;
         const double tempChi = ok2 ? sc[1] : std::numeric_limits<double>::max();
@@ -1642,9 +1701,12 @@ struct LocalBA {
           lambda *= scaleFactor;
           ni = 2;
           currentChi = tempChi;
+          spec_ready = launched;
+          spec_chi = tempChi;
         } else {
           lambda *= ni;
           ni *= 2;
+          spec_ready = false;
           if (ok2) hipLaunchKernelGGL(k_ba_restore, dim3(gp), dim3(LBS), 0, st, D);
           BA_CHECK(hipGetLastError());
         }

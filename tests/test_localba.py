@@ -208,6 +208,21 @@ def test_gpu_localba_stop_and_degenerate(ba):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed,kw", [(7, {}), (10, {}), (8, dict(n_local=30, n_fixed=4, n_points=4000))])
+def test_gpu_localba_speculative_linearization_bit_identical(ba, seed, kw, monkeypatch):
+    """Linearising the next iteration into the second buffer set while the host reads a
+    trial back (default) gives bit-identical poses, points, outlier flags and LM counts
+    to the in-line path (ORBX_BA_NO_SPEC=1)."""
+    P = synth.localba_problem(seed=seed, **kw)
+    a = ba.LocalBundleAdjustment(P)
+    monkeypatch.setenv("ORBX_BA_NO_SPEC", "1")
+    b = ba.LocalBundleAdjustment(P)
+    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
+    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+
+
+@pytest.mark.gpu
 def test_gpu_localba_repeatable(ba):
     P = small_problem(seed=10)
     a = ba.LocalBundleAdjustment(P)
