@@ -199,6 +199,8 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
           fast_wmax = std::max(fast_wmax, cw);
           fast_hmax = std::max(fast_hmax, ch);
           c.cap = ((cw + 1) / 2) * ((ch + 1) / 2);
+          c.lw = L.w;
+          c.loff = (int)L.off;
           c.cand_off = cand;
           cand += c.cap;
           P.cells.push_back(c);

@@ -433,8 +433,9 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const int2 bi = xcd_block2();
   const int cell = bi.x, img = bi.y, lane = threadIdx.x;
   const CellInfo c = cells[cell];
-  const int lw = G->lv[c.level].w;
-  const uint8_t* base = level_ptr(*G, B, img, c.level) + (size_t)(c.y0 - 3) * lw + (c.x0 - 3);
+  const int lw = c.lw;
+  const uint8_t* lvl = c.level == 0 ? B.in + (size_t)img * B.in_pitch : B.pyr + (size_t)img * G->pyr_bytes + c.loff;
+  const uint8_t* base = lvl + (size_t)(c.y0 - 3) * lw + (c.x0 - 3);
   const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TW = W + 6, TH = H + 6;
   // 1. window -> LDS.  With S == lw (mod 4) the aligned global dword j of row r
   //    lands on an aligned LDS dword, so pixel (r, col) sits at r*S + s0 + col

@@ -58,6 +58,9 @@ struct CellInfo {
   int16_t level, pad;
   int16_t x0, y0, x1, y1;  // FAST detection region (inclusive, level coordinates)
   int cand_off, cap;
+  int lw, loff;  // the level's width and byte offset in an image's pyramid block (level > 0):
+                 // k_fast finds its window from this one record, no dependent geometry load
+  int pad2;
 };
 
 struct ResizeX {  // horizontal tap of one output column
