@@ -229,6 +229,14 @@ def main():
                         frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic,
                         algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4))
 
+    # every stage against the same HBM roofline (algorithmic bytes / average launch time)
+    stage_hbm = {}
+    for k, (ms_tot, nl) in stages.items():
+        nb = algorithmic_bytes(k, 2 * B, B, P, kps_per_img, acc_per_frame, cand_per_img)
+        if nb:
+            gbs = nb / (ms_tot / nl / 1e3) / 1e9
+            stage_hbm[k] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
     value = odist.job_throughput(B, args.steps, world, elapsed)
     out = {
         "metric": METRIC,
@@ -248,6 +256,7 @@ def main():
                    "scale_factor": 1.2, "fast_th": [20, 7], "parallelism": "frame-sharded x%d" % world},
         "roofline": roofline,
         "stage_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()},
+        "stage_hbm": stage_hbm,
         "keypoints_per_image": round(kps_per_img, 1),
         "stereo_matches_per_frame": round(acc_per_frame, 1),
         "localba_iters_per_s": None,
