@@ -9,11 +9,11 @@
  * reference's ORBextractor (shared mvImagePyramid).
  *
  * Entry point -> reference interface it replaces:
- *   orbx_extractor_create       ORBextractor::ORBextractor      src/ORBextractor.cc:416-490, include/ORBextractor.h:77
+ *   orbx_extractor_create       ORBextractor::ORBextractor      src/ORBextractor.cc:416-490, include/ORBextractor.h:61
  *   orbx_extractor_scale_tables GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
  *                               GetInverseScaleSigmaSquares     include/ORBextractor.h:85-103
- *   orbx_extractor_get_levels   GetLevels                       include/ORBextractor.h:82
- *   orbx_extract                ORBextractor::operator()        src/ORBextractor.cc:1138-1211, include/ORBextractor.h:78-79
+ *   orbx_extractor_get_levels   GetLevels                       include/ORBextractor.h:81
+ *   orbx_extract                ORBextractor::operator()        src/ORBextractor.cc:1138-1211, include/ORBextractor.h:77-78
  *   orbx_pyramid_level          public mvImagePyramid[level]    include/ORBextractor.h:104 (read at src/Frame.cc:556,681,694,700)
  *   orbx_extract_batch_device   frame-batch form of operator() (one launch per stage for n images)
  *   orbx_stereo_match           Frame::ComputeStereoMatches     src/Frame.cc:547-788, include/Frame.h:111
@@ -21,14 +21,14 @@
  *   orbx_descriptor_distance_device
  *                               ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1844-1860, include/ORBmatcher.h:50
  *   orbx_search_by_bow_kf_f     ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
- *                                                               src/ORBmatcher.cc:175-325, include/ORBmatcher.h:61
+ *                                                               src/ORBmatcher.cc:175-325, include/ORBmatcher.h:114
  *   orbx_search_by_bow_kf_kf    ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)
- *                                                               src/ORBmatcher.cc:589-736, include/ORBmatcher.h:62
+ *                                                               src/ORBmatcher.cc:589-736, include/ORBmatcher.h:116
  *   orbx_search_by_bow_device   batch of the two above (one block per problem); ComputeThreeMaxima
  *                               (src/ORBmatcher.cc:1797-1839) runs inside
  *   orbx_pnp_create             PnPsolver::PnPsolver + SetRansacParameters
- *                                                               src/PnPsolver.cc:67-179, include/PnPsolver.h:66-70
- *   orbx_pnp_iterate            PnPsolver::iterate              src/PnPsolver.cc:182-384, include/PnPsolver.h:74
+ *                                                               src/PnPsolver.cc:67-179, include/PnPsolver.h:66,71
+ *   orbx_pnp_iterate            PnPsolver::iterate              src/PnPsolver.cc:182-384, include/PnPsolver.h:77
  *   orbx_voc_load_text          TemplatedVocabulary::loadFromTextFile (ORBVocabulary)
  *                                                               Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1420
  *   orbx_voc_transform          TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
@@ -41,7 +41,7 @@
  *   orbx_pose_optimization_device      batch of the above (one block per frame)
  *   orbx_distinctive_descriptors[_device]  MapPoint::ComputeDistinctiveDescriptors src/MapPoint.cc:249-320
  *   orbx_undistort_keypoints[_device]      Frame::UndistortKeyPoints src/Frame.cc:471-506 (cv::undistortPoints)
- *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:46
+ *   orbx_local_ba / orbx_ba_*   Optimizer::LocalBundleAdjustment src/Optimizer.cc:530-885, include/Optimizer.h:61
  *                               (g2o graph build, optimize(5), outlier levels, optimize(10), vToErase;
  *                               the Map mutex/recovery part stays on the caller's side)
  */
@@ -113,8 +113,11 @@ orbx_status orbx_extract_batch_device(orbx_extractor* h, int n_images, const uin
                                       int32_t* d_counts, int kp_capacity, void* stream);
 
 /* Drop-in Frame::ComputeStereoMatches: host keypoints/descriptors, pyramids
- * from the last extraction of `left` and `right` (image 0 of each).  bf =
- * baseline*fx (mbf), baseline = mb.  Writes uRight[nL], depth[nL] (-1 = no match). */
+ * from the last extraction of `left` and `right`.  bf = baseline*fx (mbf),
+ * baseline = mb.  Writes uRight[nL], depth[nL] (-1 = no match).
+ * The last call on each handle must be orbx_extract and kpsL/kpsR must be the
+ * keypoints it returned (checked by count and fingerprint): otherwise the
+ * pyramid no longer belongs to them and ORBX_ERR_STATE is returned. */
 orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const orbx_keypoint* kpsL,
                               const uint8_t* descL, int nL, const orbx_keypoint* kpsR, const uint8_t* descR,
                               int nR, float bf, float baseline, float* uRight, float* depth);

@@ -96,6 +96,12 @@ def lib():
         L.oracle_cosf.restype = C.c_float
         L.oracle_sinf.argtypes = [C.c_float]
         L.oracle_sinf.restype = C.c_float
+        L.oracle_set_trig_mode.argtypes = [C.c_int]
+        L.oracle_set_trig_mode.restype = None
+        L.oracle_trig_census.argtypes = [C.c_float, C.c_float, C.c_int, P]
+        L.oracle_trig_census.restype = None
+        L.oracle_trig_pattern_census.argtypes = [C.c_float, C.c_float, C.c_int, P, P, C.c_int]
+        L.oracle_trig_pattern_census.restype = None
         L.oracle_descriptor_distance.argtypes = [P, P]
         L.oracle_hamming_pairs.argtypes = [P, P, C.c_int, P]
         L.oracle_stereo_match.argtypes = [C.POINTER(Params), P, P, C.c_int, P, P, C.c_int, P, P, P,
@@ -150,6 +156,27 @@ def lib():
 
 def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def set_trig_mode(mode):
+    """0: sincos_det (default, shared with the GPU); 1: host libm cosf/sinf (src/ORBextractor.cc:117)."""
+    lib().oracle_set_trig_mode(int(mode))
+
+
+def trig_census(lo, hi, step=1):
+    """(#cos mismatches, #sin mismatches, #floats) of libm vs sincos_det over floats in [lo, hi]."""
+    out = np.zeros(3, np.int64)
+    lib().oracle_trig_census(float(lo), float(hi), int(step), out.ctypes.data)
+    return tuple(int(v) for v in out)
+
+
+def trig_pattern_census(lo, hi, step=1, cap=4096):
+    """(#angles with a libm/sincos_det difference, #of those whose rotated BRIEF pattern changes, #floats,
+    the pattern-changing angles)."""
+    out = np.zeros(3, np.int64)
+    ang = np.zeros(cap, np.float32)
+    lib().oracle_trig_pattern_census(float(lo), float(hi), int(step), out.ctypes.data, ang.ctypes.data, cap)
+    return int(out[0]), int(out[1]), int(out[2]), ang[:min(int(out[1]), cap)].copy()
 
 
 def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7):

@@ -482,12 +482,21 @@ float ic_angle(const Img& im, float px, float py, const std::vector<int>& umax) 
   return fast_atan2((float)m01, (float)m10);
 }
 
+// Trig used for the keypoint rotation.  0 (default, shared with the GPU): sincos_det.
+// 1: the host libm's float cos/sin, literally what src/ORBextractor.cc:117 calls
+// (`(float)cos(angle)` with `using namespace std` on a float -> std::cos(float) -> cosf).
+// Only the libm-divergence census test (tests/test_oracle_kat.py) sets 1.
+static int g_trig_mode = 0;
+
 // computeOrbDescriptor, src/ORBextractor.cc:110-152.
 void orb_descriptor(const Img& blurred, const Kp& kp, uint8_t* desc) {
   const float factorPI = (float)(M_PI / 180.f);
   float angle = kp.angle * factorPI;
   float a, b;
-  {
+  if (g_trig_mode == 1) {
+    a = std::cos(angle);
+    b = std::sin(angle);
+  } else {
     float s, c;
     sincos_det(angle, &s, &c);
     a = c;
@@ -698,6 +707,64 @@ int oracle_fast_score(const uint8_t* img, size_t stride, int x, int y) {
 float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
 float oracle_cosf(float x) { float s, c; sincos_det(x, &s, &c); return c; }
 float oracle_sinf(float x) { float s, c; sincos_det(x, &s, &c); return s; }
+
+void oracle_set_trig_mode(int mode) { g_trig_mode = mode; }
+
+// Census over every float in [lo, hi] with bit pattern index step `step`: how many inputs
+// give libm cosf/sinf != sincos_det (out[0] cos, out[1] sin, out[2] floats visited).
+void oracle_trig_census(float lo, float hi, int step, long long* out) {
+  uint32_t a, b;
+  std::memcpy(&a, &lo, 4);
+  std::memcpy(&b, &hi, 4);
+  long long dc = 0, ds = 0, n = 0;
+  for (uint64_t u = a; u <= b; u += (uint64_t)step) {
+    uint32_t w = (uint32_t)u;
+    float x;
+    std::memcpy(&x, &w, 4);
+    float s, c;
+    sincos_det(x, &s, &c);
+    float lc = std::cos(x), ls = std::sin(x);
+    dc += std::memcmp(&lc, &c, 4) != 0;
+    ds += std::memcmp(&ls, &s, 4) != 0;
+    n++;
+  }
+  out[0] = dc;
+  out[1] = ds;
+  out[2] = n;
+}
+
+// For every float angle (radians) in [lo, hi] with index step `step` whose libm cosf/sinf differ from
+// sincos_det, whether any of the 512 rotated pattern offsets cvRound(x*b + y*a), cvRound(x*a - y*b)
+// (src/ORBextractor.cc:119-125) changes.  out[0] angles with a trig difference, out[1] angles whose
+// rotated pattern differs, out[2] floats visited.
+void oracle_trig_pattern_census(float lo, float hi, int step, long long* out, float* angles, int cap) {
+  uint32_t a0, b0;
+  std::memcpy(&a0, &lo, 4);
+  std::memcpy(&b0, &hi, 4);
+  long long nt = 0, np = 0, n = 0;
+  for (uint64_t u = a0; u <= b0; u += (uint64_t)step) {
+    uint32_t w = (uint32_t)u;
+    float ang;
+    std::memcpy(&ang, &w, 4);
+    n++;
+    float s, c;
+    sincos_det(ang, &s, &c);
+    const float la = std::cos(ang), lb = std::sin(ang);
+    if (la == c && lb == s) continue;
+    nt++;
+    bool diff = false;
+    for (int idx = 0; idx < 1024 && !diff; idx += 2) {
+      const float x = (float)kPattern[idx], y = (float)kPattern[idx + 1];
+      diff = round_even(x * s + y * c) != round_even(x * lb + y * la) ||
+             round_even(x * c - y * s) != round_even(x * la - y * lb);
+    }
+    if (diff && angles && np < cap) angles[np] = ang;
+    np += diff;
+  }
+  out[0] = nt;
+  out[1] = np;
+  out[2] = n;
+}
 
 int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
 

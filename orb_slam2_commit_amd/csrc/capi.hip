@@ -333,6 +333,11 @@ struct orbx_extractor {
   const uint8_t* last_in = nullptr;
   size_t last_pitch = 0;
   int last_n = 0;
+  // fingerprint of the keypoints the last host-API orbx_extract returned: orbx_stereo_match only
+  // reads this handle's pyramid for exactly those keypoints (a batch extraction clears it)
+  bool last_host = false;
+  int last_fp_n = 0;
+  uint64_t last_fp = 0;
 };
 
 namespace {
@@ -418,10 +423,20 @@ orbx_status run_extract(orbx_extractor* h, Plan* P, int n, const uint8_t* d_in, 
   h->last_in = d_in;
   h->last_pitch = pitch;
   h->last_n = n;
+  h->last_host = false;  // orbx_extract sets it again after its readback
   return ORBX_OK;
 }
 
 hipStream_t pick_stream(orbx_extractor* h, void* s) { return s ? (hipStream_t)s : h->stream; }
+
+// 64-bit FNV-1a over the keypoint records, one 32-bit word per step (28-B records are word multiples)
+uint64_t keypoint_fingerprint(const orbx_keypoint* k, int n) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(k);
+  uint64_t h = 1469598103934665603ull ^ (uint64_t)n;
+  const size_t nw = (size_t)n * (sizeof(orbx_keypoint) / 4);
+  for (size_t i = 0; i < nw; i++) h = (h ^ w[i]) * 1099511628211ull;
+  return h;
+}
 
 bool params_ok(const orbx_extractor_params* p) {
   return p && p->nlevels >= 1 && p->nlevels <= kMaxLevelsPlan && p->scale_factor > 0.f && p->nfeatures >= 0;
@@ -523,12 +538,22 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
   if (e != hipSuccess) return ORBX_ERR_HIP;
   *n = cnt;
   if (cnt > cap) return ORBX_ERR_CAPACITY;
+  std::vector<orbx_keypoint> own;
+  orbx_keypoint* kdst = kps;
+  if (!kdst && cnt > 0) {
+    own.resize(cnt);
+    kdst = own.data();
+  }
   if (cnt > 0) {
-    if (kps) chk(hipMemcpyAsync(kps, h->kps.p, sizeof(orbx_keypoint) * cnt, hipMemcpyDeviceToHost, st));
+    chk(hipMemcpyAsync(kdst, h->kps.p, sizeof(orbx_keypoint) * cnt, hipMemcpyDeviceToHost, st));
     if (desc) chk(hipMemcpyAsync(desc, h->desc.p, (size_t)32 * cnt, hipMemcpyDeviceToHost, st));
     chk(hipStreamSynchronize(st));
   }
-  return hip_status(e);
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  h->last_host = true;
+  h->last_fp_n = cnt;
+  h->last_fp = keypoint_fingerprint(kdst, cnt);
+  return ORBX_OK;
 }
 
 orbx_status orbx_pyramid_level(orbx_extractor* h, int image, int level, uint8_t* dst, size_t dst_stride,
@@ -624,6 +649,13 @@ orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const
   if (!left || !right || !uRight || !depth || nL < 0 || nR < 0) return ORBX_ERR_ARG;
   if ((nL > 0 && (!kpsL || !descL)) || (nR > 0 && (!kpsR || !descR))) return ORBX_ERR_ARG;
   if (!left->last_plan || !right->last_plan) return ORBX_ERR_STATE;
+  // the pyramids must belong to the supplied keypoints: each handle's last call was orbx_extract and
+  // returned exactly these keypoints (src/Frame.cc:556,681 read mpORBextractorLeft/Right->mvImagePyramid
+  // of the extraction that produced mvKeys/mvKeysRight)
+  if (!left->last_host || !right->last_host || nL != left->last_fp_n || nR != right->last_fp_n ||
+      (nL > 0 && keypoint_fingerprint(kpsL, nL) != left->last_fp) ||
+      (nR > 0 && keypoint_fingerprint(kpsR, nR) != right->last_fp))
+    return ORBX_ERR_STATE;
   if (left->last_plan->G.width != right->last_plan->G.width ||
       left->last_plan->G.height != right->last_plan->G.height || left->device != right->device)
     return ORBX_ERR_ARG;

@@ -1,0 +1,175 @@
+"""Config-5 sequence pipeline (BASELINE.json configs[4]).
+
+One synthetic KITTI stereo sequence per rank (KITTI 00..07 -> rank 0..7): the rank
+extracts and stereo-matches its frames in device batches (the reference's per-frame
+unit is the stereo Frame constructor, src/Frame.cc:62-123, driven by the sequence
+loop of Examples/Stereo/stereo_kitti.cc:68-124), runs Optimizer::LocalBundleAdjustment
+on its own map (replicas: one problem per rank), and then the ranks exchange results
+with ONE all-gather each:
+
+* per-frame records: a rank's batch of B frames is a single byte arena
+  (``FrameRecords``) whose sections are exactly the buffers the extraction writes --
+  keypoints (cv::KeyPoint layout, 28 B), descriptors (32 B), per-image counts,
+  uRight / depth (f32) padded to the keypoint capacity, per-frame match counts -- so
+  the all-gather moves the arena as it lies in HBM (no packing kernel);
+* per-rank LocalBA summaries (``ba_summary``): LM iterations per phase, trials,
+  final chi2 per phase, outlier count and the optimised poses (FP64).
+
+torch.distributed backend "nccl" is RCCL over xGMI (device tensors); "gloo" moves
+CPU tensors (CPU tests, and the one-GPU multi-rank rehearsal).
+"""
+import numpy as np
+
+KP_BYTES = 28
+DESC_BYTES = 32
+_ALIGN = 256
+
+
+def _align(n):
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class FrameRecords:
+    """Byte layout of one rank's batch of ``n_frames`` stereo frames (capacity ``cap`` keypoints
+    per image).  Sections (each 256-B aligned), image 2f = left and 2f+1 = right of frame f:
+
+        kps    (2B, cap, 28) u8    desc  (2B, cap, 32) u8    counts (2B,) i32
+        uR     (B, cap) f32        depth (B, cap) f32        nmatch (B,) i32
+    """
+
+    SECTIONS = ("kps", "desc", "counts", "uR", "depth", "nmatch")
+
+    def __init__(self, n_frames, cap):
+        self.n_frames = int(n_frames)
+        self.cap = int(cap)
+        B, c = self.n_frames, self.cap
+        sizes = dict(kps=2 * B * c * KP_BYTES, desc=2 * B * c * DESC_BYTES, counts=2 * B * 4, uR=B * c * 4,
+                     depth=B * c * 4, nmatch=B * 4)
+        self.offsets = {}
+        off = 0
+        for k in self.SECTIONS:
+            self.offsets[k] = off
+            off = _align(off + sizes[k])
+        self.sizes = sizes
+        self.nbytes = off
+
+    def frame_bytes(self):
+        """Bytes one frame contributes to the record (its slices of every section)."""
+        return self.nbytes / self.n_frames
+
+    # ---- views over an arena (numpy array or torch tensor of nbytes uint8)
+    def views(self, arena):
+        B, c = self.n_frames, self.cap
+        shapes = dict(kps=((2 * B, c, KP_BYTES), "u8"), desc=((2 * B, c, DESC_BYTES), "u8"),
+                      counts=((2 * B,), "i32"), uR=((B, c), "f32"), depth=((B, c), "f32"), nmatch=((B,), "i32"))
+        out = {}
+        for k in self.SECTIONS:
+            o, n = self.offsets[k], self.sizes[k]
+            shape, dt = shapes[k]
+            out[k] = _typed(arena[o:o + n], dt).reshape(shape)
+        return out
+
+    def unpack(self, arena):
+        """Valid entries of every frame as host numpy: list of dicts (kpsL, descL, kpsR, descR, uR, depth,
+        nmatch); uR/depth hold the left keypoints' results."""
+        v = self.views(arena)
+        v = {k: (t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)) for k, t in v.items()}
+        frames = []
+        for f in range(self.n_frames):
+            nL, nR = int(v["counts"][2 * f]), int(v["counts"][2 * f + 1])
+            frames.append(dict(kpsL=v["kps"][2 * f, :nL].copy(), descL=v["desc"][2 * f, :nL].copy(),
+                               kpsR=v["kps"][2 * f + 1, :nR].copy(), descR=v["desc"][2 * f + 1, :nR].copy(),
+                               uR=v["uR"][f, :nL].copy(), depth=v["depth"][f, :nL].copy(),
+                               nmatch=int(v["nmatch"][f])))
+        return frames
+
+
+def _typed(a, dt):
+    if hasattr(a, "view") and not isinstance(a, np.ndarray):  # torch tensor
+        import torch
+        return a.view({"u8": torch.uint8, "i32": torch.int32, "f32": torch.float32}[dt])
+    return a.view({"u8": np.uint8, "i32": np.int32, "f32": np.float32}[dt])
+
+
+def new_arena(layout, device):
+    """Zeroed record arena on `device`; the padding beyond each image's count stays zero, so two
+    runs of the same frames give byte-identical arenas."""
+    import torch
+    return torch.zeros(layout.nbytes, dtype=torch.uint8, device=device)
+
+
+class SequenceShard:
+    """One rank's share of config 5: extract + stereo-match its sequence's frames batch by batch into
+    a FrameRecords arena (orbx_stereo_frames_device writes straight into the arena's sections)."""
+
+    def __init__(self, extractor, n_frames, width, height, bf, baseline, device):
+        self.ex = extractor
+        self.layout = FrameRecords(n_frames, extractor.max_keypoints(width, height))
+        self.arena = new_arena(self.layout, device)
+        self.v = self.layout.views(self.arena)
+        self.bf, self.baseline = float(bf), float(baseline)
+
+    def step(self, images, stream=None, clear=True):
+        """images: (2B, H, W) u8 device tensor ordered L0,R0,L1,R1,...  clear=True zeroes the arena first
+        (canonical padding: the records of a batch do not depend on the previous batch)."""
+        if clear:
+            self.arena.zero_()
+        v = self.v
+        self.ex.stereo_frames_device(images, v["kps"], v["desc"], v["counts"], self.bf, self.baseline, v["uR"],
+                                     v["depth"], v["nmatch"], stream)
+
+
+# ------------------------------------------------------------------ LocalBA summary record
+def ba_summary(result, n_cams):
+    """Fixed-size FP64 record of one LocalBundleAdjustment call: [iterations phase 1, phase 2, trials,
+    chi2 phase 1, chi2 phase 2, outlier edges, n_cams, Tcw (n_cams x 12, row-major 3x4)]."""
+    its = list(result["iterations"]) + [0, 0]
+    chi = list(result.get("chi2", (0.0, 0.0))) + [0.0, 0.0]
+    head = [its[0], its[1], result["trials"], chi[0], chi[1], float(np.sum(result["edge_outlier"])), n_cams]
+    T = np.asarray(result["Tcw_d"], np.float64).reshape(-1)
+    return np.concatenate([np.asarray(head, np.float64), T[:12 * n_cams]])
+
+
+def parse_ba_summary(rec):
+    rec = np.asarray(rec, np.float64)
+    n = int(rec[6])
+    return dict(iterations=(int(rec[0]), int(rec[1])), trials=int(rec[2]), chi2=(rec[3], rec[4]),
+                outliers=int(rec[5]), Tcw=rec[7:7 + 12 * n].reshape(n, 12))
+
+
+# ------------------------------------------------------------------ collectives
+def all_gather_bytes(t):
+    """All-gather a 1-D tensor over the process group: returns (world, n) with row r = rank r's tensor.
+    nccl (RCCL over xGMI): device tensors, one all_gather_into_tensor; gloo: CPU tensors.  Without an
+    initialised group (one rank) the result is the tensor itself as one row."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return t.reshape(1, -1)
+    world = dist.get_world_size()
+    if dist.get_backend() == "gloo":
+        src = t.detach().cpu().contiguous()
+        out = [torch.empty_like(src) for _ in range(world)]
+        dist.all_gather(out, src)
+        return torch.stack(out)
+    out = torch.empty((world, t.numel()), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous())
+    return out
+
+
+def gather_sequence_results(shard_arena, ba_record, device=None):
+    """The config-5 exchange: every rank's frame-record arena and LocalBA summary to every rank."""
+    import torch
+    recs = all_gather_bytes(shard_arena)
+    ba = torch.as_tensor(np.asarray(ba_record, np.float64))
+    if device is not None and _backend() != "gloo":
+        ba = ba.to(device)
+    bas = all_gather_bytes(ba)
+    return recs, bas.cpu().numpy()
+
+
+def _backend():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_backend()
+    return None

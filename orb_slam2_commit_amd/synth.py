@@ -91,6 +91,22 @@ def stereo_pair(seed, width=1241, height=376, n_shapes=None, stress=False):
             np.clip(np.rint(right), 0, 255).astype(np.uint8))
 
 
+def sequence_seeds(seq, n_unique):
+    """Seeds of the n_unique distinct stereo scenes of synthetic sequence `seq` (KITTI 00..07 -> 0..7)."""
+    return [1000 * seq + s for s in range(n_unique)]
+
+
+def stereo_batch(seq, n_frames, n_unique=16, width=1241, height=376, pairs=None):
+    """Frames of synthetic sequence `seq` as one (2*n_frames, height, width) u8 array ordered
+    L0,R0,L1,R1,... (the orbx_stereo_frames_device layout).  Frame f is scene f % U rolled
+    horizontally by 53*(f // U) px (left and right alike, so the disparity field is kept): no two
+    frames share bytes.  This is exactly the bench.py batch."""
+    if pairs is None:
+        pairs = [stereo_pair(s, width, height) for s in sequence_seeds(seq, n_unique)]
+    U = len(pairs)
+    return np.stack([np.roll(pairs[f % U][k], 53 * (f // U), axis=1) for f in range(n_frames) for k in (0, 1)])
+
+
 def mono_image(seed, width=640, height=480):
     return stereo_pair(seed, width, height)[0]
 
@@ -150,7 +166,7 @@ def _rot_small(rng, sigma):
 
 def localba_problem(seed=7, n_local=20, n_fixed=6, n_points=8000, obs_per_point=5, outlier_frac=0.05,
                     fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, bf=386.1448, width=1241, height=376,
-                    th_depth=35.0, pose_noise=(0.01, 0.05), point_noise=0.1):
+                    th_depth=35.0, pose_noise=(0.01, 0.05), point_noise=0.1, z_range=(5.0, 80.0), pixel_noise=1.0):
     """KITTI-00-shaped LocalBundleAdjustment problem.
 
     n_local keyframes along +z at 1 m spacing with +-2 deg yaw jitter, n_fixed
@@ -172,7 +188,7 @@ def localba_problem(seed=7, n_local=20, n_fixed=6, n_points=8000, obs_per_point=
         Tcw_true[i, :, :3] = R
         Tcw_true[i, :, 3] = -R @ twc[i]
     X = np.stack([rng.uniform(-15, 15, n_points), rng.uniform(-3, 2, n_points),
-                  rng.uniform(5, 80, n_points)], axis=1)
+                  rng.uniform(z_range[0], z_range[1], n_points)], axis=1)
     ep, ec, obs, isg = [], [], [], []
     for p in range(n_points):
         Pc = Tcw_true[:, :, :3] @ X[p] + Tcw_true[:, :, 3]
@@ -190,11 +206,11 @@ def localba_problem(seed=7, n_local=20, n_fixed=6, n_points=8000, obs_per_point=
         for c in sorted(chosen):
             octave = int(rng.integers(0, 8))
             sigma = 1.2 ** octave
-            uu = u[c] + rng.normal(0, sigma)
-            vv = v[c] + rng.normal(0, sigma)
+            uu = u[c] + rng.normal(0, sigma * pixel_noise)
+            vv = v[c] + rng.normal(0, sigma * pixel_noise)
             ur = -1.0
             if z[c] < th_depth * base:
-                ur = uu - bf / z[c] + rng.normal(0, sigma * 0.5)
+                ur = uu - bf / z[c] + rng.normal(0, sigma * 0.5 * pixel_noise)
             if rng.uniform() < outlier_frac:
                 uu += 20.0
                 if ur >= 0:

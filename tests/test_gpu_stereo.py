@@ -66,3 +66,39 @@ def test_descriptor_distance(gpu):
     assert np.array_equal(d, oracle.hamming_pairs(a, b))
     assert (d[:10] == 0).all() and (d[10:20] == 256).all()
     assert ORBmatcher.DescriptorDistance(a[0], b[0]) == int(oracle.hamming_pairs(a[:1], b[:1])[0])
+
+
+def test_bench_batch_slots_match_oracle(gpu):
+    """The bench's exact timed batch (B = 256 frames = 512 KITTI images, bench.py / synth.stereo_batch):
+    the first, a middle and the last slot against the oracle -- L and R keypoints, descriptors, uR,
+    depth and the match count (large-batch pyramid / candidate / output offsets)."""
+    import torch
+    B = 256
+    host = synth.stereo_batch(0, B)
+    ex = ORBextractor(2000, 1.2, 8, 20, 7)
+    cap = ex.max_keypoints(1241, 376)
+    d = torch.from_numpy(host).to(gpu)
+    kps = torch.zeros((2 * B, cap, 28), dtype=torch.uint8, device=gpu)
+    desc = torch.zeros((2 * B, cap, 32), dtype=torch.uint8, device=gpu)
+    cnt = torch.zeros(2 * B, dtype=torch.int32, device=gpu)
+    uR = torch.zeros((B, cap), dtype=torch.float32, device=gpu)
+    dep = torch.zeros((B, cap), dtype=torch.float32, device=gpu)
+    nm = torch.zeros(B, dtype=torch.int32, device=gpu)
+    ex.stereo_frames_device(d, kps, desc, cnt, KITTI_BF, KITTI_BF / KITTI_FX, uR, dep, nm,
+                            torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+    uR, dep, nm = uR.cpu().numpy(), dep.cpu().numpy(), nm.cpu().numpy()
+    p = oracle.params(2000, 1.2, 8, 20, 7)
+    for f in (0, 1, B // 2 - 1, B // 2, B - 1):
+        o = [oracle.extract(p, host[2 * f + k]) for k in (0, 1)]
+        for k in (0, 1):
+            n = int(cnt[2 * f + k])
+            assert n == len(o[k].keypoints), (f, k)
+            assert kps[2 * f + k, :n].tobytes() == o[k].keypoints.tobytes(), (f, k)
+            assert np.array_equal(desc[2 * f + k, :n], o[k].descriptors), (f, k)
+        ouR, odep = oracle.stereo_match(p, o[0], o[1], KITTI_BF, KITTI_BF / KITTI_FX)
+        nL = int(cnt[2 * f])
+        assert np.array_equal(uR[f, :nL].view(np.uint32), ouR.view(np.uint32)), f
+        assert np.array_equal(dep[f, :nL].view(np.uint32), odep.view(np.uint32)), f
+        assert int(nm[f]) == int((ouR >= 0).sum()), f

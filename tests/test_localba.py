@@ -165,6 +165,35 @@ def _compare(r_gpu, r_ora, tol=PARITY_TOL):
     np.testing.assert_array_equal(r_gpu["edge_outlier"], r_ora["edge_outlier"])
 
 
+# Problems whose LM runs reject trials (near points, large perturbations: Gauss-Newton overshoots)
+# or stop early on the ORB-SLAM2 _nBad rule -- the accept path alone never reaches either.
+REJECT_CASES = {
+    # 10 rejected trials over 15 iterations (phase 2 runs its 10)
+    "rejects_a": dict(seed=1, n_local=10, n_fixed=2, n_points=4000, obs_per_point=4, pose_noise=(0.1, 0.5),
+                      point_noise=1.0, z_range=(1.5, 6.0)),
+    # 10 rejected trials; phase 2 ends after 7 iterations
+    "rejects_b": dict(seed=5, n_local=6, n_fixed=2, n_points=600, obs_per_point=4, pose_noise=(0.1, 0.5),
+                      point_noise=1.0, z_range=(1.0, 4.0)),
+    # no rejection; phase 2 stops after 5 iterations (3 low-improvement iterations: _nBad)
+    "nbad_stop": dict(seed=4, n_local=6, n_fixed=2, n_points=600, obs_per_point=4, pose_noise=(0.05, 0.3),
+                      point_noise=0.5, z_range=(1.0, 6.0)),
+}
+
+
+def reject_problem(name):
+    return synth.localba_problem(**REJECT_CASES[name])
+
+
+@pytest.mark.parametrize("name", sorted(REJECT_CASES))
+def test_oracle_reject_cases_exercise_lm_rules(name):
+    r = oracle.local_ba(reject_problem(name))
+    its = list(r["iterations"])
+    if name.startswith("rejects"):
+        assert r["trials"] > sum(its), (its, r["trials"])
+    else:
+        assert r["trials"] == sum(its) and its[1] < 10, (its, r["trials"])
+
+
 @pytest.fixture(scope="module")
 def ba(gpu):
     from orb_slam2_commit_amd import Optimizer
@@ -215,6 +244,22 @@ def test_gpu_localba_speculative_linearization_bit_identical(ba, seed, kw, monke
     to the in-line path (ORBX_BA_NO_SPEC=1)."""
     P = synth.localba_problem(seed=seed, **kw)
     a = ba.LocalBundleAdjustment(P)
+    monkeypatch.setenv("ORBX_BA_NO_SPEC", "1")
+    b = ba.LocalBundleAdjustment(P)
+    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
+    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(REJECT_CASES))
+def test_gpu_localba_rejections_match_oracle(ba, name, monkeypatch):
+    """Rejected trials (pop + lambda *= ni, with a speculative linearisation launched on the
+    trial state that is then discarded) and the _nBad early stop: GPU = oracle, and the
+    speculative path = the in-line path (ORBX_BA_NO_SPEC=1) bit for bit."""
+    P = reject_problem(name)
+    a = ba.LocalBundleAdjustment(P)
+    _compare(a, oracle.local_ba(P))
     monkeypatch.setenv("ORBX_BA_NO_SPEC", "1")
     b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw_d", "Xw_d", "edge_outlier"):
