@@ -1,25 +1,36 @@
 """Benchmark: frames/sec ORB extract+match on KITTI-00-shaped stereo (BASELINE.json configs[1])
-+ LocalBA iterations/sec on the KITTI-00 LocalBundleAdjustment problem (configs[3]).
++ LocalBA iterations/sec on the KITTI-00 LocalBundleAdjustment problem (configs[3])
++ the config-5 sequence pipeline with its RCCL all-gather (configs[4]).
 
 One "step" = one pass of the hot path over one batch of B synthetic stereo
 frames resident in HBM: ORB extraction of the 2B images (1241x376, 2000
 features, 8 levels x1.2, FAST 20/7) + Frame::ComputeStereoMatches of the B
 frames, all inside liborbx.so (orbx_stereo_frames_device).  `value` is that
-frames/s.  The LocalBA leg then runs Optimizer::LocalBundleAdjustment
-(orbx_ba_run) on a synthetic 20-KF / ~7.4k-point / ~43k-edge problem per rank,
---ba-calls times, and reports LM iterations/s (whole job) under "localba".
+frames/s, from an un-instrumented loop (HIP events between steps only); the
+per-stage split and the roofline come from a second, profiled pass.
+
+Legs after the headline loop:
+  localba   Optimizer::LocalBundleAdjustment (orbx_ba_run) on the config-4 problem
+            per rank, --ba-calls times: LM iterations/s (whole job) + its roofline.
+  config5   one synthetic sequence per rank: extract+match of --pipeline-steps
+            batches into the frame-record arena, LocalBA on the rank's map, then
+            ONE all-gather of the records + LocalBA summaries (RCCL over xGMI);
+            compute and all-gather timed separately.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 
 For N>1 the driver launches one rank per GPU with torch.distributed.run;
-frames shard across ranks with no data-path collective ("weak" scaling), the
-timed region is bracketed by barrier + synchronize and the max over ranks is
-reported.  Rank 0 prints ONE JSON line.
+frames shard across ranks with no data-path collective in the headline loop
+("weak" scaling), the timed region is bracketed by barrier + synchronize and
+the max over ranks is reported.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
+import threading
 import time
 
 import numpy as np
@@ -29,7 +40,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec ORB extract+match (2k kp) + LocalBA iters/sec, KITTI-00 stereo"
 KITTI = dict(width=1241, height=376, nfeatures=2000, fx=718.856, bf=386.1448)
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured float4 copy)
 
 
 def parse():
@@ -39,11 +50,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="stereo frames per step per GPU")
     ap.add_argument("--unique", type=int, default=16, help="seeded synthetic stereo scenes per rank (slots are distinct rolls of them)")
+    ap.add_argument("--profile-steps", type=int, default=5, help="steps of the second, per-stage profiled pass")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
+    ap.add_argument("--pipeline-steps", type=int, default=3, help="config-5 batches per rank (0: skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (tools/profile.py); null if absent")
+                    help="PMC-derived HBM bytes per launch (tools/profile.sh + tools/parse_prof.py); null if absent")
     return ap.parse_args()
 
 
@@ -54,7 +67,7 @@ def level_sizes(w, h, inv_scales):
 
 
 def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, cand_per_img):
-    """Algorithmic HBM bytes of one launch of `stage` over the batch (DESIGN.md §Roofline)."""
+    """Algorithmic HBM bytes of one launch of `stage` over the batch (DESIGN.md §3/§5)."""
     sP = sum(P)
     if stage == "k_resize":  # per launch average over the 7 level launches: read P_{l-1} + write P_l
         return n_img * sum(P[l - 1] + P[l] for l in range(1, len(P))) / (len(P) - 1)
@@ -75,28 +88,133 @@ def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, can
     return None
 
 
-def cpu_baseline(pairs, seconds):
-    """Single-thread CPU restatement (oracle/) on a bounded sample of the same workload."""
+def pct(xs, q):
+    return float(np.percentile(np.asarray(xs, np.float64), q))
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle = checker)
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    return dict(cpu_model=model, nproc=os.cpu_count(), cpus_allowed=len(aff) or None), aff
+
+
+def native_oracle():
+    """Compile the oracle sources with -O3 -march=native -ffp-contract=off for THIS host into a temp dir
+    (SURVEY §8d baseline flags; the committed build is -O2 and portable).  Returns (path, flags) or
+    (None, reason)."""
+    src = os.path.join(ROOT, "oracle")
+    srcs = ["orb_oracle.cpp", "localba.cpp", "pnp.cpp", "voc.cpp", "projection.cpp", "poseopt.cpp",
+            "triangulation.cpp", "mapping.cpp"]
+    if not all(os.path.exists(os.path.join(src, s)) for s in srcs):
+        return None, "oracle sources absent"
+    flags = ["-O3", "-march=native", "-std=c++17", "-fPIC", "-ffp-contract=off"]
+    d = tempfile.mkdtemp(prefix="orbx_oracle_native_")
+    try:
+        procs = [subprocess.Popen(["g++"] + flags + ["-c", os.path.join(src, s), "-o", os.path.join(d, s + ".o")],
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE) for s in srcs]
+        if any(p.wait(timeout=300) != 0 for p in procs):
+            return None, "native oracle compile failed"
+        out = os.path.join(d, "liborb_oracle_native.so")
+        subprocess.check_call(["g++", "-shared", "-o", out] + [os.path.join(d, s + ".o") for s in srcs])
+        return out, " ".join(flags)
+    except Exception as e:  # noqa: BLE001 -- the baseline is reported, never fatal
+        return None, "native oracle build error: %s" % e
+
+
+def load_oracle():
+    path, flags = native_oracle()
+    if path:
+        os.environ["ORBX_ORACLE_LIB"] = path
+    else:
+        flags = "-O2 -ffp-contract=off (committed oracle/build; %s)" % flags
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    return oracle, flags
+
+
+def cpu_baseline(oracle, flags, pairs, seconds, cpus):
+    """oracle/ C++ restatement on a bounded sample of the same workload: 1 thread pinned to one core
+    (median/p90 per frame), plus the reference's 2-thread form (L and R extraction concurrently on two
+    cores, src/Frame.cc:80-84, then stereo matching)."""
     p = oracle.params(KITTI["nfeatures"], 1.2, 8, 20, 7)
     bf, fx = KITTI["bf"], KITTI["fx"]
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        L, R = pairs[n % len(pairs)]
-        oL, oR = oracle.extract(p, L), oracle.extract(p, R)
-        oracle.stereo_match(p, oL, oR, bf, bf / fx)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 3:
-            break
-    return dict(value=round(n / el, 3), unit="frames/s", cores=1, kind="port",
-                sample="%d KITTI-shaped stereo frames (extract L + extract R + stereo match), oracle/ C++ "
-                       "restatement, 1 thread, %.1f s" % (n, el))
+    old = os.sched_getaffinity(0) if hasattr(os, "sched_setaffinity") else None
+    c0 = cpus[0] if cpus else 0
+    c1 = cpus[1] if len(cpus) > 1 else c0
+    try:
+        if old is not None:
+            os.sched_setaffinity(0, {c0})
+        L, R = pairs[0]
+        oracle.stereo_match(p, oracle.extract(p, L), oracle.extract(p, R), bf, bf / fx)  # warm-up
+        times = []
+        t_start = time.perf_counter()
+        n = 0
+        while True:
+            L, R = pairs[n % len(pairs)]
+            t0 = time.perf_counter()
+            oL, oR = oracle.extract(p, L), oracle.extract(p, R)
+            oracle.stereo_match(p, oL, oR, bf, bf / fx)
+            times.append(time.perf_counter() - t0)
+            n += 1
+            if time.perf_counter() - t_start >= seconds and n >= 3:
+                break
+        el = sum(times)
+        one = dict(value=round(n / el, 3), unit="frames/s", cores=1, kind="port",
+                   median_ms=round(pct(times, 50) * 1e3, 2), p90_ms=round(pct(times, 90) * 1e3, 2),
+                   sample="%d KITTI-shaped stereo frames (extract L + extract R + stereo match), oracle/ C++ "
+                          "restatement built %s, 1 thread pinned to cpu %d, %.1f s" % (n, flags, c0, el))
+        # 2-thread L/R (ctypes releases the GIL inside the oracle calls)
+        res = [None, None]
+
+        def ext(k, img, cpu):
+            if old is not None:
+                os.sched_setaffinity(0, {cpu})
+            res[k] = oracle.extract(p, img)
+
+        times2 = []
+        n2 = 0
+        t_start = time.perf_counter()
+        while True:
+            L, R = pairs[n2 % len(pairs)]
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=ext, args=(0, L, c0)), threading.Thread(target=ext, args=(1, R, c1))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            oracle.stereo_match(p, res[0], res[1], bf, bf / fx)
+            times2.append(time.perf_counter() - t0)
+            n2 += 1
+            if time.perf_counter() - t_start >= seconds / 2 and n2 >= 3:
+                break
+        one["two_thread"] = dict(value=round(n2 / sum(times2), 3), unit="frames/s", cores=2,
+                                 median_ms=round(pct(times2, 50) * 1e3, 2), p90_ms=round(pct(times2, 90) * 1e3, 2),
+                                 sample="%d frames, L and R extraction on two threads pinned to cpus %d,%d "
+                                        "(src/Frame.cc:80-84), then stereo match" % (n2, c0, c1))
+        return one
+    finally:
+        if old is not None:
+            os.sched_setaffinity(0, old)
 
 
-def localba_leg(args, rank, world, dev, odist):
+# ------------------------------------------------------------------ LocalBA leg
+def localba_bytes_per_iteration(P):
+    """E*512 + M*360 + (6K)^2*16 algorithmic bytes per LM outer iteration."""
+    E = len(P["edge_point"])
+    M = len(P["Xw"])
+    K = int(len(P["fixed"]) - np.sum(P["fixed"]))
+    return E * 512 + M * 360 + (6 * K) ** 2 * 16
+
+
+def localba_leg(args, rank, world, dev, odist, oracle_mod=None, flags=None, cpus=None):
     """Optimizer::LocalBundleAdjustment on the config-4 problem: whole-job LM iterations/s."""
     import torch
     from orb_slam2_commit_amd import Optimizer, synth
@@ -107,36 +225,111 @@ def localba_leg(args, rank, world, dev, odist):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     its = 0
+    call_ms = []
     for _ in range(args.ba_calls):
-        r = opt.LocalBundleAdjustment(P)
+        c0 = time.perf_counter()
+        r = opt.LocalBundleAdjustment(P)  # returns after its final readback (host-synchronous)
+        call_ms.append((time.perf_counter() - c0) * 1e3)
         its += sum(r["iterations"])
     torch.cuda.synchronize(dev)
     odist.barrier()
-    el = odist.max_over_ranks(time.perf_counter() - t0, dev)
+    el_local = time.perf_counter() - t0
+    el = odist.max_over_ranks(el_local, dev)
     its_all = odist.sum_over_ranks(float(its), dev)
     opt.close()
+    bpi = localba_bytes_per_iteration(P)
+    it_s_local = its / el_local
+    achieved = bpi * it_s_local / 1e9
     out = dict(iters_per_s=round(its_all / el, 2), ms_per_call=round(el / args.ba_calls * 1e3, 3),
+               median_ms_per_call=round(pct(call_ms, 50), 3), p90_ms_per_call=round(pct(call_ms, 90), 3),
                calls_per_gpu=args.ba_calls, iterations=list(r["iterations"]), trials=r["trials"],
                problem=dict(keyframes=int(len(P["Tcw"])), fixed=int(np.sum(P["fixed"])),
                             points=int(len(P["Xw"])), edges=int(len(P["edge_point"])),
                             stereo_edges=int(np.sum(P["obs"][:, 2] >= 0))),
+               roofline=dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                             frac=round(achieved / HBM_PEAK_GBS, 5), traffic=None,
+                             algorithmic_bytes_per_iteration=int(bpi),
+                             note="SURVEY 8d bytes per LM iteration (E*512 + M*360 + (6K)^2*16) x iterations/s "
+                                  "of this rank; the trial is a chain of ~12 dependent small launches "
+                                  "(latency-bound; per-kernel split in profiles/*localba_kernel_stats.csv)"),
                dtype="f64", scaling="weak", cpu_baseline=None)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        n, t0 = 0, time.perf_counter()
-        cits = 0
-        while True:
-            cr = oracle.local_ba(P)
-            cits += sum(cr["iterations"])
-            n += 1
-            cel = time.perf_counter() - t0
-            if cel >= 2.0 and n >= 2:
-                break
+    if rank == 0 and world == 1 and oracle_mod is not None:
+        old = os.sched_getaffinity(0) if hasattr(os, "sched_setaffinity") else None
+        try:
+            if old is not None and cpus:
+                os.sched_setaffinity(0, {cpus[0]})
+            n, cits, ct = 0, 0, []
+            t0 = time.perf_counter()
+            while True:
+                c0 = time.perf_counter()
+                cr = oracle_mod.local_ba(P)
+                ct.append(time.perf_counter() - c0)
+                cits += sum(cr["iterations"])
+                n += 1
+                if time.perf_counter() - t0 >= 3.0 and n >= 3:
+                    break
+        finally:
+            if old is not None:
+                os.sched_setaffinity(0, old)
+        cel = sum(ct)
         out["cpu_baseline"] = dict(value=round(cits / cel, 2), unit="LM iterations/s", cores=1, kind="port",
-                                   sample="%d LocalBA calls on the same problem, oracle/localba.cpp, 1 thread, "
-                                          "%.1f s" % (n, cel))
+                                   median_ms_per_call=round(pct(ct, 50) * 1e3, 2),
+                                   p90_ms_per_call=round(pct(ct, 90) * 1e3, 2),
+                                   sample="%d LocalBA calls on the same problem, oracle/localba.cpp built %s, "
+                                          "1 thread pinned, %.1f s" % (n, flags, cel))
     return out
+
+
+# ------------------------------------------------------------------ config-5 leg
+def config5_leg(args, rank, world, dev, odist, ex, images, stream):
+    """One sequence per rank: extract+match `pipeline_steps` batches into the frame-record arena, LocalBA
+    on the rank's map, then one all-gather of records + LocalBA summaries.  Compute and all-gather timed
+    separately (each bracketed by barrier + synchronize, max over ranks)."""
+    import torch
+    from orb_slam2_commit_amd import Optimizer, pipeline, synth
+    W, H, B = KITTI["width"], KITTI["height"], args.batch
+    sh = pipeline.SequenceShard(ex, B, W, H, KITTI["bf"], KITTI["bf"] / KITTI["fx"], dev)
+    P = synth.localba_problem(seed=7 + 1000 * rank)
+    opt = Optimizer(dev.index)
+    sh.step(images, stream)  # warm-up
+    rec = pipeline.ba_summary(opt.LocalBundleAdjustment(P), len(P["Tcw"]))
+    recs, _ = sh.gather(rec)  # warm-up of the collective
+    del recs
+    odist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.pipeline_steps):
+        sh.step(images, stream)
+    rec = pipeline.ba_summary(opt.LocalBundleAdjustment(P), len(P["Tcw"]))
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    t_compute = odist.max_over_ranks(time.perf_counter() - t0, dev)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    recs, bas = sh.gather(rec)
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    t_gather = odist.max_over_ranks(time.perf_counter() - t1, dev)
+    opt.close()
+    # every rank checks that its own slot of the gathered records is its arena, byte for byte
+    own_ok = bool(torch.equal(recs[rank].to(sh.arena.device), sh.arena)) and bool(
+        np.array_equal(bas[rank], rec))
+    ok_all = odist.sum_over_ranks(1.0 if own_ok else 0.0, dev) == world
+    nbytes = sh.layout.nbytes
+    frames = B * args.pipeline_steps * world
+    backend = pipeline._backend() or "none (1 rank)"
+    return dict(sequences=world, frames_per_sequence=B * args.pipeline_steps, batch_frames=B,
+                extract_match_localba_s=round(t_compute, 5),
+                allgather_ms=round(t_gather * 1e3, 3), allgather_backend=backend,
+                record_bytes_per_rank=int(nbytes), record_bytes_per_frame=int(sh.layout.frame_bytes()),
+                allgather_bytes_received_per_rank=int(nbytes * (world - 1)),
+                allgather_algbw_GBps=round(nbytes * (world - 1) / t_gather / 1e9, 2) if world > 1 else None,
+                frames_per_s_compute=round(frames / t_compute, 2),
+                frames_per_s_with_allgather=round(frames / (t_compute + t_gather), 2),
+                localba_summary_ranks=[pipeline.parse_ba_summary(b)["iterations"] for b in bas],
+                gathered_slots_match=ok_all,
+                note="the all-gather carries the LAST batch's records (the one-consumer exchange, SURVEY 8e); "
+                     "records of earlier batches are consumed in place")
 
 
 def main():
@@ -145,23 +338,25 @@ def main():
 
     from orb_slam2_commit_amd import dist as odist
     rank, local, world = odist.env_rank()
-    # RCCL ("nccl") over xGMI; ORBX_DIST_BACKEND=gloo rehearses the multi-rank flow on a box with
-    # fewer GPUs than ranks (ranks then wrap onto the available devices; collectives on CPU tensors)
-    odist.init(os.environ.get("ORBX_DIST_BACKEND", "nccl"), rank, world)
-    local = local % max(torch.cuda.device_count(), 1)
+    backend = os.environ.get("ORBX_DIST_BACKEND", "nccl")
+    odist.init(backend, rank, world)
+    ndev = torch.cuda.device_count()
+    if backend == "gloo":
+        # one-GPU rehearsal of the multi-rank flow: ranks wrap onto the available devices
+        local = local % max(ndev, 1)
+    elif local >= ndev:
+        raise SystemExit("LOCAL_RANK %d but only %d GPU(s): one rank per GPU under RCCL" % (local, ndev))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    devices_used = world if backend != "gloo" else min(world, max(ndev, 1))  # distinct GPUs in use
 
     from orb_slam2_commit_amd import ORBextractor, synth
     from orb_slam2_commit_amd import _lib
 
     W, H, B = KITTI["width"], KITTI["height"], args.batch
-    # synthetic frames: distinct seeds per rank (frame shards), tiled into the batch
-    pairs = [synth.stereo_pair(seed, W, H) for seed in odist.frame_seeds(rank, args.unique)]
-    # every batch slot distinct: slot f is pair f % U rolled horizontally by 53 * (f // U) px
-    # (L and R alike, so the disparity field is kept), so no two slots share bytes in HBM
-    U = len(pairs)
-    host = np.stack([np.roll(pairs[f % U][k], 53 * (f // U), axis=1) for f in range(B) for k in (0, 1)])
+    # synthetic frames: sequence = rank (distinct seeds per rank: frame shards); every slot distinct
+    pairs = [synth.stereo_pair(s, W, H) for s in synth.sequence_seeds(rank, args.unique)]
+    host = synth.stereo_batch(rank, B, pairs=pairs)
     images = torch.from_numpy(host).to(dev)
     ex = ORBextractor(KITTI["nfeatures"], 1.2, 8, 20, 7, device=local)
     cap = ex.max_keypoints(W, H)
@@ -171,7 +366,11 @@ def main():
     uR = torch.empty((B, cap), dtype=torch.float32, device=dev)
     depth = torch.empty((B, cap), dtype=torch.float32, device=dev)
     nmatch = torch.zeros(B, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # one dedicated stream for the whole run: the library launches on it (the legacy null stream would be
+    # replaced by the handle's own stream), and the step events / torch ops are ordered with the kernels
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    torch.cuda.synchronize(dev)
     bf, baseline = KITTI["bf"], KITTI["bf"] / KITTI["fx"]
 
     def step():
@@ -181,20 +380,28 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     L = _lib.lib()
-    L.orbx_profile_reset(ex._h)
-    L.orbx_profile_enable(ex._h, 1)
+
+    # ---- headline: un-instrumented timed loop (events between steps only, on the launch stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     odist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    ev[0].record(stream)
+    for i in range(args.steps):
         step()
+        ev[i + 1].record(stream)
     torch.cuda.synchronize(dev)
     odist.barrier()
-    elapsed = time.perf_counter() - t0
-    L.orbx_profile_enable(ex._h, 0)
-    elapsed = odist.max_over_ranks(elapsed, dev)
+    elapsed = odist.max_over_ranks(time.perf_counter() - t0, dev)
+    step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
 
-    # per-stage live HIP-event timings on the stream the kernels ran on
+    # ---- second pass: per-stage HIP events (orbx_profile_*, recorded on the kernels' stream)
+    L.orbx_profile_reset(ex._h)
+    L.orbx_profile_enable(ex._h, 1)
+    for _ in range(args.profile_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    L.orbx_profile_enable(ex._h, 0)
     import ctypes as C
     stages = {}
     for s in range(L.orbx_profile_read(ex._h, -1, None, None, None)):
@@ -206,27 +413,29 @@ def main():
     nm = nmatch.cpu().numpy()
     kps_per_img = float(cnt.mean())
     acc_per_frame = float(nm.mean())  # surviving matches (lower bound of SAD refinements)
-    # candidates per image (FAST survivors) from the last batch
-    ncand = L.orbx_debug_copy(ex._h, 2, 0, 0, None, 0) // 4
+    ncand = L.orbx_debug_copy(ex._h, 2, 0, 0, None, 0) // 4  # FAST survivors per cell of the last batch
     cc = np.zeros(ncand, np.int32)
     L.orbx_debug_copy(ex._h, 2, 0, 0, _lib.ptr(cc), cc.nbytes)
     cand_per_img = float(cc.sum())
     P = [w * h for (w, h) in level_sizes(W, H, ex.GetInverseScaleFactors())]
     dom = max(stages, key=lambda k: stages[k][0]) if stages else None
+    traffic_all, traffic_src = {}, None
+    if os.path.exists(args.traffic):
+        try:
+            tj = json.load(open(args.traffic))
+            traffic_all = tj.get("per_launch_bytes", {})
+            traffic_src = dict(file=os.path.relpath(args.traffic, ROOT), head=tj.get("head"), batch=tj.get("batch"))
+        except Exception:
+            traffic_all = {}
     roofline = None
     if dom:
         ms_tot, nl = stages[dom]
         avg_s = ms_tot / nl / 1e3
         nbytes = algorithmic_bytes(dom, 2 * B, B, P, kps_per_img, acc_per_frame, cand_per_img)
         achieved = nbytes / avg_s / 1e9
-        traffic = None
-        if os.path.exists(args.traffic):
-            try:
-                traffic = json.load(open(args.traffic)).get("per_launch_bytes", {}).get(dom)
-            except Exception:
-                traffic = None
         roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic,
+                        frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic_all.get(dom),
+                        traffic_source=traffic_src,
                         algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4))
 
     # every stage against the same HBM roofline (algorithmic bytes / average launch time)
@@ -235,9 +444,11 @@ def main():
         nb = algorithmic_bytes(k, 2 * B, B, P, kps_per_img, acc_per_frame, cand_per_img)
         if nb:
             gbs = nb / (ms_tot / nl / 1e3) / 1e9
-            stage_hbm[k] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+            stage_hbm[k] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                            "traffic_per_launch": traffic_all.get(k), "algorithmic_per_launch": int(nb)}
 
     value = odist.job_throughput(B, args.steps, world, elapsed)
+    info, cpus = host_info()
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -246,6 +457,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "median_ms_per_step": round(pct(step_ms, 50), 4),
+        "p90_ms_per_step": round(pct(step_ms, 90), 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -253,20 +466,26 @@ def main():
         "data": "synthetic (%d seeded stereo scenes per rank, each batch slot a distinct horizontal roll of one)" % args.unique,
         "config": {"workload": "KITTI-00 stereo 1241x376, 2000 features, extract L+R + ComputeStereoMatches",
                    "batch_frames_per_gpu": B, "global_batch_frames": B * world, "nlevels": 8,
-                   "scale_factor": 1.2, "fast_th": [20, 7], "parallelism": "frame-sharded x%d" % world},
+                   "scale_factor": 1.2, "fast_th": [20, 7], "parallelism": "frame-sharded x%d" % world,
+                   "devices_used": devices_used, "dist_backend": backend if world > 1 else None},
         "roofline": roofline,
-        "stage_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items()},
+        "stage_ms_per_step": {k: round(v[0] / args.profile_steps, 4) for k, v in stages.items()},
         "stage_hbm": stage_hbm,
         "keypoints_per_image": round(kps_per_img, 1),
         "stereo_matches_per_frame": round(acc_per_frame, 1),
         "localba_iters_per_s": None,
+        "host": info,
         "cpu_baseline": None,
     }
+    oracle_mod, flags = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pairs, args.cpu_baseline_seconds)
+        oracle_mod, flags = load_oracle()
+        out["cpu_baseline"] = cpu_baseline(oracle_mod, flags, pairs, args.cpu_baseline_seconds, cpus)
     if args.ba_calls > 0:
-        out["localba"] = localba_leg(args, rank, world, dev, odist)
+        out["localba"] = localba_leg(args, rank, world, dev, odist, oracle_mod, flags, cpus)
         out["localba_iters_per_s"] = out["localba"]["iters_per_s"]
+    if args.pipeline_steps > 0:
+        out["config5"] = config5_leg(args, rank, world, dev, odist, ex, images, stream)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -9,7 +9,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "liborb_oracle.so")
+# ORBX_ORACLE_LIB: an alternative build of the same sources (bench.py's cpu_baseline leg compiles one
+# with -O3 -march=native on the host it runs on)
+_LIB_PATH = os.environ.get("ORBX_ORACLE_LIB") or os.path.join(_HERE, "build", "liborb_oracle.so")
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])

@@ -108,15 +108,33 @@ class SequenceShard:
         self.arena = new_arena(self.layout, device)
         self.v = self.layout.views(self.arena)
         self.bf, self.baseline = float(bf), float(baseline)
+        import torch
+        self.stream = torch.cuda.Stream(device)
 
     def step(self, images, stream=None, clear=True):
         """images: (2B, H, W) u8 device tensor ordered L0,R0,L1,R1,...  clear=True zeroes the arena first
-        (canonical padding: the records of a batch do not depend on the previous batch)."""
+        (canonical padding: the records of a batch do not depend on the previous batch).  The zeroing and
+        the extraction are ordered on ONE stream: `stream` (a torch.cuda.Stream other than the legacy null
+        stream, which the library would replace by its handle's own stream) or the shard's own."""
+        import torch
+        if stream is None or getattr(stream, "cuda_stream", 0) == 0:
+            stream = self.stream
+        self.last_stream = stream
         if clear:
-            self.arena.zero_()
+            with torch.cuda.stream(stream):
+                self.arena.zero_()
         v = self.v
         self.ex.stereo_frames_device(images, v["kps"], v["desc"], v["counts"], self.bf, self.baseline, v["uR"],
                                      v["depth"], v["nmatch"], stream)
+
+
+    def gather(self, ba_record):
+        """The config-5 exchange for this shard: the collective is ordered after the shard's last step
+        (the current stream waits for the step's stream)."""
+        import torch
+        if getattr(self, "last_stream", None) is not None:
+            torch.cuda.current_stream(self.arena.device).wait_stream(self.last_stream)
+        return gather_sequence_results(self.arena, ba_record, self.arena.device)
 
 
 # ------------------------------------------------------------------ LocalBA summary record

@@ -155,7 +155,7 @@ def _gpu_worker(rank, world, port, q):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     sh = _gpu_records(rank, dev)
-    recs, bas = pipeline.gather_sequence_results(sh.arena, _gpu_ba(rank, dev), dev)
+    recs, bas = sh.gather(_gpu_ba(rank, dev))
     q.put((rank, recs.cpu().numpy().tobytes(), bas.tobytes()))
     dist.destroy_process_group()
 
