@@ -263,13 +263,13 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
       }
     }
   }
-  // k_fast LDS layout for the largest cell: tile rows H+6 at stride <= sbase+3
-  // (window dwords land at byte s0 - sr + 4 + 4j <= 7 + 4*((W+12)/4 + 1)), score
-  // map H x maps, compass list W*H u16
-  G.fast_sbase = (fast_wmax + 6 + 18 + 3) & ~3;
-  G.fast_maps = (fast_wmax + 2 + 3) & ~3;  // one zero column each side
-  G.fast_tile_bytes = ((fast_hmax + 6) * (G.fast_sbase + 3) + 8 + 15) & ~15;
-  G.fast_map_bytes = ((fast_hmax + 2) * G.fast_maps + 15) & ~15;  // one zero row each side
+  // k_fast LDS layout for the largest cell: window tile of H+6 rows plus the compass
+  // slack (rows up to H+12 are read for out-of-region lanes) at stride S, score map
+  // (H+2) x S (one zero row/column each side), compass list W*H u16
+  G.fast_s = fast_wmax + 6 <= 48 ? 48 : 80;
+  G.fast_rp = fast_wmax <= 32 ? 2 : 1;
+  G.fast_tile_bytes = (fast_hmax + 13) * G.fast_s;
+  G.fast_map_bytes = (fast_hmax + 2) * G.fast_s;
   G.fast_smem = G.fast_tile_bytes + G.fast_map_bytes + 2 * fast_wmax * fast_hmax;
   // k_resize staging bound: source footprint of every 128x16 output tile
   G.rz_rows = 1;

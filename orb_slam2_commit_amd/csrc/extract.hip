@@ -337,214 +337,174 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
 // at iniThFAST the cell uses minThFAST (src/ORBextractor.cc:892-900).
 // Survivors are written in row-major order.
 //
-//   1. window -> LDS tile (lanes = columns)
-//   2. compass quick test (two adjacent of ring pixels 0,4,8,12 beyond t) and
-//      ballot-compaction of passing pixels into a row-major list
-//   3. full segment test + score on the compacted list (all 64 lanes busy);
-//      corners compacted in place, score map S+1 in LDS
+// The kernel is VALU-issue-bound, so every phase is shaped for few vector
+// instructions per pixel:
+//   1. window -> LDS: 16-B buffer loads at the (unaligned) row positions land on
+//      16-B aligned LDS rows of compile-time stride S, so every ring / map
+//      access below is an LDS read with an immediate offset (no address VALU);
+//   2. compass quick test (two adjacent of ring pixels 0,4,8,12 beyond t) on
+//      per-lane booleans (v_cmp + SALU lane-mask logic), survivors compacted as
+//      tile offsets e = y*S + x (the 7x7 neighbourhood's top-left);
+//   3. cornerScore and the corner test in ONE pass on the compacted list:
+//      ring pixel p is packed as the f16 pair (1024+p, 1279-p) (one v_mad_i32_i24:
+//      bits 0x6400+p / 0x64FF-p), the 9-arc maximum of both halves is two rounds
+//      of v_pk_maximum3_f16 and the minimum over the 16 arcs three rounds of
+//      v_pk_minimum3_f16, giving (min_k max_arc p, 255 - max_k min_arc p), so
+//      S+1 = max(v - min_k max_arc p, max_k min_arc p - v) (= cornerScore<16> + 1)
+//      and corner_t <=> S+1 > t; corners are compacted in place, the map holds S+1;
 //   4. NMS at iniThFAST -> count; 5. NMS at the chosen threshold -> ballot-ranked
-//      row-major writes
-constexpr int kMaxCell = 60;          // wCell,hCell <= 60 (checked on the host)
+//      row-major writes.
+constexpr int kMaxCell = 60;  // wCell,hCell <= 60 (checked on the host)
 
-typedef short short2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ void ring_load(const uint8_t* t, int S, int p[16]) {
-  // t points at the centre pixel inside the LDS tile (row stride S); Bresenham
-  // circle of radius 3 in OpenCV's makeOffsets order
-  p[0] = t[3 * S];
-  p[1] = t[3 * S + 1];
-  p[2] = t[2 * S + 2];
-  p[3] = t[S + 3];
-  p[4] = t[3];
-  p[5] = t[-S + 3];
-  p[6] = t[-2 * S + 2];
-  p[7] = t[-3 * S + 1];
-  p[8] = t[-3 * S];
-  p[9] = t[-3 * S - 1];
-  p[10] = t[-2 * S - 2];
-  p[11] = t[-S - 3];
-  p[12] = t[-3];
-  p[13] = t[S - 3];
-  p[14] = t[2 * S - 2];
-  p[15] = t[3 * S - 1];
+__device__ __forceinline__ uint32_t pk_max3_f16(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_min3_f16(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
 }
 
-// Segment test: >= 9 contiguous ring pixels all < v-t or all > v+t.
-__device__ __forceinline__ bool ring_corner(const uint8_t* t, int S, int tlo) {
-  int p[16];
-  ring_load(t, S, p);
-  const int v = t[0];
-  uint32_t dark = 0, bright = 0;
+// cornerScore<16> + 1 of the pixel whose 7x7 neighbourhood starts at t (row stride S): the
+// ring in OpenCV's makeOffsets order, offsets relative to the top-left (centre at 3S+3)
+template <int S>
+__device__ __forceinline__ int ring_score1(const uint8_t* t) {
+  constexpr int o[16] = {6 * S + 3, 6 * S + 4, 5 * S + 5, 4 * S + 6, 3 * S + 6, 2 * S + 6, S + 5, 4,
+                         3,         2,         S + 1,     2 * S,     3 * S,     4 * S,     5 * S + 1, 6 * S + 2};
+  const int v = t[3 * S + 3];
+  uint32_t P[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    dark |= (uint32_t)(p[k] < v - tlo) << k;
-    bright |= (uint32_t)(p[k] > v + tlo) << k;
-  }
-  auto run9 = [](uint32_t m) {
-    m |= m << 16;
-    uint32_t r = m & (m >> 1);
-    r &= r >> 2;
-    r &= r >> 4;
-    r &= m >> 8;
-    return r;
-  };
-  return (run9(dark) | run9(bright)) != 0;
+  for (int k = 0; k < 16; k++) P[k] = (uint32_t)((int)t[o[k]] * -65535 + 0x64FF6400);  // (0x64FF-p)<<16 | 0x6400+p
+  uint32_t M3[16], M9[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) M3[k] = pk_max3_f16(P[k], P[(k + 1) & 15], P[(k + 2) & 15]);
+#pragma unroll
+  for (int k = 0; k < 16; k++) M9[k] = pk_max3_f16(M3[k], M3[(k + 3) & 15], M3[(k + 6) & 15]);
+  const uint32_t a0 = pk_min3_f16(M9[0], M9[1], M9[2]), a1 = pk_min3_f16(M9[3], M9[4], M9[5]),
+                 a2 = pk_min3_f16(M9[6], M9[7], M9[8]), a3 = pk_min3_f16(M9[9], M9[10], M9[11]),
+                 a4 = pk_min3_f16(M9[12], M9[13], M9[14]);
+  const uint32_t R = pk_min3_f16(pk_min3_f16(a0, a1, a2), pk_min3_f16(a3, a4, M9[15]), M9[15]);
+  const int a = (v + 0x6400) - (int)(R & 0xFFFF);  // v - min_k max_arc p
+  const int b = (0x64FF - v) - (int)(R >> 16);     // max_k min_arc p - v
+  return max(a, b);
 }
 
-// cornerScore<16>: max over the 16 cyclic arcs of 9 of max(min d, min -d) - 1,
-// d = centre - ring.  (d, -d) ride together in packed int16 lanes.
-__device__ __forceinline__ int ring_score(const uint8_t* t, int S) {
-  int p[16];
-  ring_load(t, S, p);
-  const int v = t[0];
-  short2v q[16], m2[16], m4[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const short d = (short)(v - p[k]);
-    q[k] = (short2v){d, (short)-d};
-  }
-#pragma unroll
-  for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(q[k], q[(k + 1) & 15]);
-#pragma unroll
-  for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-  short2v best = (short2v){(short)-1000, (short)-1000};
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const short2v m9 = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]), q[(k + 8) & 15]);
-    best = __builtin_elementwise_max(best, m9);
-  }
-  return max((int)best.x, (int)best.y) - 1;
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ uint64_t lanemask_lt() {
-  const int lane = threadIdx.x & 63;
-  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
-}
-
+// S: LDS row stride of the window tile and the score map (multiple of 16, >= window width);
+// RP: region rows per compass instruction (2 when the widest cell fits 32 lanes)
+template <int S, int RP>
 __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B) {
-  // dynamic LDS sized by the plan's largest cell (G->fast_*): occupancy is what
-  // hides this kernel's LDS/ballot latency chains
+  // dynamic LDS sized by the plan's largest cell (G->fast_*)
   extern __shared__ __align__(16) uint8_t fast_smem[];
-  uint8_t* tile_raw = fast_smem;
+  uint8_t* tile = fast_smem;
   uint8_t* smap = fast_smem + G->fast_tile_bytes;
   uint16_t* list = (uint16_t*)(fast_smem + G->fast_tile_bytes + G->fast_map_bytes);
-  const int kMapS = G->fast_maps;
+  const int map_bytes = G->fast_map_bytes;
   const int2 bi = xcd_block2();
   const int cell = bi.x, img = bi.y, lane = threadIdx.x;
   const CellInfo c = cells[cell];
   const int lw = c.lw;
   const uint8_t* lvl = c.level == 0 ? B.in + (size_t)img * B.in_pitch : B.pyr + (size_t)img * G->pyr_bytes + c.loff;
   const uint8_t* base = lvl + (size_t)(c.y0 - 3) * lw + (c.x0 - 3);
-  const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TW = W + 6, TH = H + 6;
-  // 1. window -> LDS.  With S == lw (mod 4) the aligned global dword j of row r
-  //    lands on an aligned LDS dword, so pixel (r, col) sits at r*S + s0 + col
-  //    for every row (s0 = alignment of the window's first byte).
-  const int S = G->fast_sbase + ((lw - G->fast_sbase) & 3);
-  const uintptr_t a0 = (uintptr_t)base;
-  const int s0 = (int)(a0 & 3), wm = lw & 3;
+  const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TH = H + 6;
+  // 1. window -> LDS: lane = (row, 16-B chunk); window pixel (r, col) lands at tile[r*S + col]
   {
-    // lanes = (row, dword) with dpr dwords per row; every load is issued before any LDS write
-    const int dpr = (TW + 6) / 4 + 1;
-    const int rpi = 64 / dpr, rg = lane / dpr, j = lane - rg * dpr;
-    constexpr int KMAX = (kMaxCell + 6 + 3) / 4 + 1;  // rows per lane at the smallest rpi (dpr <= 19 -> rpi >= 3)
-    uint32_t v[KMAX];
+    constexpr int CPR = S / 16, RPI = 64 / CPR;
+    constexpr int KMAX = (kMaxCell + 6 + RPI - 1) / RPI;
+    const int lr = lane / CPR, lj = lane - lr * CPR;
+    const bool lane_ok = lr < RPI;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, TH * lw + S, 0x00020000);
+    uint32_t v[KMAX][4];
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
-      const int r = rg + k * rpi;
-      const int sr = (s0 + __mul24(r, wm)) & 3;
-      v[k] = 0;
-      if (rg < rpi && r < TH && 4 * j < sr + TW) {
-        const uintptr_t ar = a0 + (uintptr_t)__umul24(r, lw);
-        v[k] = *((const uint32_t*)(ar & ~(uintptr_t)3) + j);
+      const int r = k * RPI + lr;
+      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0;
+      if (k * RPI < TH && lane_ok && r < TH) {
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, r * lw + 16 * lj, 0, 0);
+        v[k][0] = q[0];
+        v[k][1] = q[1];
+        v[k][2] = q[2];
+        v[k][3] = q[3];
       }
     }
+    // zero the score map (its border row/column stands for "outside the region")
+    for (int i = lane * 16; i < map_bytes; i += 64 * 16) *(uint4*)(smap + i) = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
-      const int r = rg + k * rpi;
-      const int sr = (s0 + __mul24(r, wm)) & 3;
-      if (rg < rpi && r < TH && 4 * j < sr + TW) *(uint32_t*)&tile_raw[__mul24(r, S) + s0 - sr + 4 + 4 * j] = v[k];
+      const int r = k * RPI + lr;
+      if (k * RPI < TH && lane_ok && r < TH)
+        *(uint4*)(tile + r * S + 16 * lj) = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
     }
-  }
-  const uint8_t* tile = tile_raw + 4 + s0;  // pixel (r, col) = tile[r*S + col]
-  {
-    uint32_t* m32 = (uint32_t*)smap;
-    for (int i = lane; i < (H + 2) * kMapS / 4; i += 64) m32[i] = 0;  // zero border included
   }
   __syncthreads();
   const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255);
   const int tlo = min(ini, mint);
-  const uint64_t lt = lanemask_lt();
-  // 2. compass quick test, row-major compaction; rows_per = 2 when W <= 32.
-  //    Branchless: coordinates are clamped into the region and the validity
-  //    is a ballot, so the reads of all QU row groups are in flight together;
-  //    the 8 comparisons are wave masks combined with scalar 64-bit logic, and
-  //    the pass mask is the compaction ballot itself.
-  const int rows_per = W <= 32 ? 2 : 1;
-  const int ly = W <= 32 ? (lane >> 5) : 0, lx = W <= 32 ? (lane & 31) : lane;
-  const int lxc = min(lx, W - 1);
+  // 2. compass quick test, row-major compaction of tile offsets
+  const int ly = RP == 2 ? (lane >> 5) : 0, lx = RP == 2 ? (lane & 31) : lane;
+  const uint64_t col_ok = __ballot(lx < W);
   int n = 0;
-  constexpr int QU = 4;
-  for (int y0r = 0; y0r < H; y0r += QU * rows_per) {
+  constexpr int QU = 8 / RP;
+  for (int y0r = 0; y0r < H; y0r += QU * RP) {
+    const int eb = (y0r + ly) * S + lx;
     int cv[QU], c0[QU], c4[QU], c8[QU], c12[QU];
 #pragma unroll
     for (int u = 0; u < QU; u++) {
-      const int y = min(y0r + u * rows_per + ly, H - 1);
-      const uint8_t* t = &tile[__mul24(y + 3, S) + lxc + 3];
-      cv[u] = t[0];
-      c0[u] = t[3 * S];
-      c4[u] = t[3];
-      c8[u] = t[-3 * S];
-      c12[u] = t[-3];
+      const uint8_t* t = tile + eb + u * RP * S;
+      cv[u] = t[3 * S + 3];
+      c0[u] = t[6 * S + 3];
+      c4[u] = t[3 * S + 6];
+      c8[u] = t[3];
+      c12[u] = t[3 * S];
     }
 #pragma unroll
     for (int u = 0; u < QU; u++) {
-      const int y = y0r + u * rows_per + ly;
+      // the eight comparisons are lane masks (v_cmp -> SGPR pairs), combined with scalar logic
       const int dlo = cv[u] - tlo, dhi = cv[u] + tlo;
       const uint64_t k0 = __ballot(c0[u] < dlo), k4 = __ballot(c4[u] < dlo), k8 = __ballot(c8[u] < dlo),
                      k12 = __ballot(c12[u] < dlo);
       const uint64_t b0 = __ballot(c0[u] > dhi), b4 = __ballot(c4[u] > dhi), b8 = __ballot(c8[u] > dhi),
                      b12 = __ballot(c12[u] > dhi);
-      const uint64_t ok = __ballot(lx < W && y < H);
       const uint64_t m = (((k0 & k4) | (k4 & k8) | (k8 & k12) | (k12 & k0)) |
-                          ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0))) & ok;
-      if ((m >> lane) & 1) list[n + __popcll(m & lt)] = (uint16_t)((y << 6) | lx);
+                          ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0))) &
+                         col_ok & __ballot(y0r + u * RP + ly < H);
+      if (__builtin_amdgcn_inverse_ballot_w64(m)) list[n + lane_rank(m)] = (uint16_t)(eb + u * RP * S);
       n += __popcll(m);
     }
   }
   __syncthreads();
-  // 3a. full segment test on the compass list; corners compacted in place
+  // 3. cornerScore + corner test at min(ini, min) on the compass list; corners compacted in place
   int nc = 0;
   for (int i0 = 0; i0 < n; i0 += 64) {
     const int i = i0 + lane;
-    int pix = 0;
+    int e = 0, sc1 = 0;
     bool corner = false;
     if (i < n) {
-      pix = list[i];
-      corner = ring_corner(&tile[__mul24((pix >> 6) + 3, S) + (pix & 63) + 3], S, tlo);
+      e = list[i];
+      sc1 = ring_score1<S>(tile + e);
+      corner = sc1 > tlo;
     }
     const uint64_t m = __ballot(corner);
     __syncthreads();
-    if (corner) list[nc + __popcll(m & lt)] = (uint16_t)pix;
+    if (corner) {
+      list[nc + lane_rank(m)] = (uint16_t)e;
+      smap[e + S + 1] = (uint8_t)sc1;
+    }
     nc += __popcll(m);
   }
   __syncthreads();
-  // 3b. cornerScore on the corners only; score map holds S+1
-  for (int i0 = 0; i0 < nc; i0 += 64) {
-    const int i = i0 + lane;
-    if (i < nc) {
-      const int pix = list[i];
-      const int sc = ring_score(&tile[__mul24((pix >> 6) + 3, S) + (pix & 63) + 3], S);
-      smap[__mul24((pix >> 6) + 1, kMapS) + (pix & 63) + 1] = (uint8_t)(sc + 1);
-    }
-  }
-  __syncthreads();
   // strict NMS inside the region; the map's zero border stands for "outside"
-  auto keep = [&](int pix, int thr) -> bool {  // thr = t + 1 in map units (S + 1)
-    const uint8_t* m = smap + __mul24((pix >> 6) + 1, kMapS) + (pix & 63) + 1;
-    const int s = m[0];
-    const int n0 = m[-kMapS - 1], n1 = m[-kMapS], n2 = m[-kMapS + 1], n3 = m[-1], n4 = m[1], n5 = m[kMapS - 1],
-              n6 = m[kMapS], n7 = m[kMapS + 1];
+  auto keep = [&](int e, int thr) -> bool {  // thr = t + 1 in map units (S + 1)
+    const uint8_t* m = smap + e;              // centre at m[S + 1]
+    const int s = m[S + 1];
+    const int n0 = m[0], n1 = m[1], n2 = m[2], n3 = m[S], n4 = m[S + 2], n5 = m[2 * S], n6 = m[2 * S + 1],
+              n7 = m[2 * S + 2];
     auto beats = [&](int nv) -> int { return nv >= thr && nv >= s; };  // int: branch-free OR below
     const bool lost = (beats(n0) | beats(n1) | beats(n2) | beats(n3) | beats(n4) | beats(n5) | beats(n6) | beats(n7)) != 0;
     return s >= thr && s > 1 && !lost;
@@ -555,9 +515,9 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     const int i = i0 + lane;
     bool k = false;
     if (i < nc) {
-      const int pix = list[i];
-      k = keep(pix, ini + 1);
-      if (k) list[i] = (uint16_t)(pix | 0x8000);
+      const int e = list[i];
+      k = keep(e, ini + 1);
+      if (k) list[i] = (uint16_t)(e | 0x8000);
     }
     cnt += __popcll(__ballot(k));
   }
@@ -567,20 +527,19 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   int pos = 0;
   for (int i0 = 0; i0 < nc; i0 += 64) {
     const int i = i0 + lane;
-    int pix = 0;
+    int e = 0;
     bool k = false;
     if (i < nc) {
-      const int e = list[i];
-      pix = e & 0x7FFF;
-      k = cnt > 0 ? (e >> 15) != 0 : keep(pix, thr);  // at iniThFAST the verdict is already known
+      const int le = list[i];
+      e = le & 0x7FFF;
+      k = cnt > 0 ? (le >> 15) != 0 : keep(e, thr);  // at iniThFAST the verdict is already known
     }
     const uint64_t m = __ballot(k);
     if (k) {
-      const int p = pos + __popcll(m & lt);
-      const int y = pix >> 6, x = pix & 63;
+      const int p = pos + lane_rank(m);
+      const int y = e / S, x = e - y * S;
       if (p < c.cap)
-        out[p] = ((uint32_t)(smap[__mul24(y + 1, kMapS) + x + 1] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) |
-                 (uint32_t)(c.x0 + x);
+        out[p] = ((uint32_t)(smap[e + S + 1] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) | (uint32_t)(c.x0 + x);
     }
     pos += __popcll(m);
   }
@@ -1134,7 +1093,8 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   }
   if (Gh.ncells > 0) {
     T->begin(st);
-    hipLaunchKernelGGL(k_fast, dim3(Gh.ncells, n_img), dim3(64), Gh.fast_smem, st, Gd, cells, B);
+    auto kf = Gh.fast_s == 48 ? (Gh.fast_rp == 2 ? k_fast<48, 2> : k_fast<48, 1>) : k_fast<80, 1>;
+    hipLaunchKernelGGL(kf, dim3(Gh.ncells, n_img), dim3(64), Gh.fast_smem, st, Gd, cells, B);
     T->end(ST_FAST, st);
   } else {
     (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);

@@ -44,8 +44,8 @@ struct Geometry {
   int ncells, cand_total, oct_total, max_kps, ntiles;
   int node_cap;   // octree LDS node capacity (max over levels, multiple of 64)
   int cell_cap;   // max cells in one level
-  int fast_sbase;  // k_fast: LDS tile row stride base (multiple of 4; stride = base + ((lw - base) & 3))
-  int fast_maps;   // k_fast: score-map row stride
+  int fast_s;      // k_fast: LDS row stride of the window tile and the score map (48 or 80)
+  int fast_rp;     // k_fast: region rows per compass instruction (2 when every cell is <= 32 wide)
   int fast_tile_bytes, fast_map_bytes, fast_smem;  // k_fast dynamic LDS layout (sized by the largest cell)
   int rz_rows;    // k_resize: max source rows staged per 128x16 output tile
   int rz_dpr;     // k_resize: max source dwords per staged row
