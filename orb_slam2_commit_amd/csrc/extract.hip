@@ -200,7 +200,7 @@ __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, c
 // GaussianBlur(7x7, sigma=2, BORDER_REFLECT_101), OpenCV 3.2 8U fixed point:
 // integer kernel {k0..k6} (x256), exact integer row+column sums, then
 // rint(acc/65536) on SIMD column groups (x < w&~3) and (acc+2^15)>>16 on the
-// scalar tail; saturate to u8.  64x16 output tile per block, staged in LDS.
+// scalar tail; saturate to u8.  128x128 output tile per block, staged in LDS.
 __constant__ int c_gauss[7];
 
 __device__ __forceinline__ int reflect101(int p, int n) {
@@ -211,15 +211,20 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 
 // Tile of kBlurTileW x kBlurTileH (128 x 128) outputs per 256-thread block.
 // Input tile col 0 = x0-4 so that every 4-output group reads 3 aligned LDS
-// dwords.  Thread = 4 columns x a 16-row strip: row sums are computed straight
-// from the input tile into a 7-row register window that slides down the strip
-// (no row-sum buffer in LDS), outputs go out as aligned dwords (blurred rows
-// are padded to a 16-byte stride).
-constexpr int kBIn = kBlurTileW + 8;  // input tile row stride (bytes)
-constexpr int kBStrip = 16;           // output rows per thread
-__global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
+// dwords.  The tile arrives as 16-B buffer loads at the (unaligned) source row
+// positions, stored to 16-B aligned LDS rows (rows reflected per row index;
+// the <= 3 reflected columns each side are patched from LDS afterwards).
+// Thread = 4 columns x a 16-row strip: row sums (byte dot products) go into a
+// 7-row register window that slides down the strip; the column taps are exact
+// f32 FMAs on the row sums with the weights pre-scaled by 2^-16 (every partial
+// sum is an integer multiple of 2^-16 below 2^8, exact in f32), so
+// v_rndne_f32 is rint(acc/65536) and v_cvt_pk_u8_f32 packs the byte.
+constexpr int kBIn = kBlurTileW + 16;  // input tile row stride (bytes, 16-B multiple)
+constexpr int kBStrip = 16;            // output rows per thread
+__global__ __launch_bounds__(BS, 8) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
                                              BatchPtrs B) {
-  __shared__ __align__(16) uint8_t tin[(kBlurTileH + 6) * kBIn];
+  constexpr int TR = kBlurTileH + 6;
+  __shared__ __align__(16) uint8_t tin[(TR + 1) * kBIn];
   const int2 bi = xcd_block2();
   const int tile = bi.x, img = bi.y, tid = threadIdx.x;
   const int l = tile_level[tile];
@@ -229,45 +234,69 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
   const uint8_t* src = level_ptr(*G, B, img, l);
   uint8_t* dst = B.blur + (size_t)img * G->blur_bytes + L.boff;
   const int w = L.w, h = L.h, bs = L.bstride;
-  const bool interior = x0 - 4 >= 0 && x0 + kBlurTileW + 4 <= w && y0 - 3 >= 0 && y0 + kBlurTileH + 3 <= h;
-  // input tile: rows y0-3 .. y0+H+2, cols x0-4 .. x0+W+3 (REFLECT_101 at the borders)
-  constexpr int TR = kBlurTileH + 6;
-  if (interior) {
-    // 134 rows x 36 dwords / 256 threads <= 19 loads per thread
-    window_to_lds<19>(src + (size_t)(y0 - 3) * w + (x0 - 4), w, TR, kBIn, tin, kBIn, tid, BS);
-  } else {
-    // border tile (every tile of the small levels): one LDS dword per item; the
-    // source row is reflected once, a dword wholly inside the row is built from
-    // two aligned source dwords (alignbyte), only the <= 2 edge dwords of a row
-    // go byte by byte through REFLECT_101
-    constexpr int DW = kBIn / 4;
-    uint32_t* tin32 = reinterpret_cast<uint32_t*>(tin);
-    for (int q0 = 0; q0 < TR * DW; q0 += 8 * BS) {
-      uint32_t v[8];
+  // input tile rows y0-3 .. y0+H+2 (REFLECT_101), cols x0-4 .. x0+W+11
+  {
+    constexpr int CPR = kBIn / 16, NQ = TR * CPR, KQ = (NQ + BS - 1) / BS;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, w * h, 0x00020000);
+    uint32_t v[KQ][4];
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int q = q0 + tid + k * BS;
-        v[k] = 0;
-        if (q < TR * DW) {
-          const int ty = q / DW, jd = q - ty * DW;
-          const uint8_t* row = src + (size_t)__umul24(reflect101(y0 + ty - 3, h), w);
-          const int sx = x0 - 4 + 4 * jd;
-          if (sx >= 0 && sx + 4 <= w) {
-            const uintptr_t a = (uintptr_t)(row + sx);
-            const uint32_t* pa = (const uint32_t*)(a & ~(uintptr_t)3);
-            const int sh = (int)(a & 3);
-            // pa[1] holds byte a+3 (inside the row) whenever sh != 0: same page
-            v[k] = sh ? __builtin_amdgcn_alignbyte(pa[1], pa[0], sh) : pa[0];
-          } else {
+    for (int k = 0; k < KQ; k++) {
+      const int q = k * BS + tid;
+      const int ty = q / CPR, j = q - ty * CPR;
+      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0;
+      if (q < NQ) {
+        const int sy = reflect101(y0 - 3 + ty, h);
+        const int o = sy * w + x0 - 4 + 16 * j;
+        if (o >= 0 && o + 16 <= w * h) {
+          const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+          v[k][0] = r[0];
+          v[k][1] = r[1];
+          v[k][2] = r[2];
+          v[k][3] = r[3];
+        } else {
+          // a chunk straddling the level's first or last byte (a range check covers the whole
+          // 16-B access): byte loads, each range-checked on its own (outside -> 0, patched below)
 #pragma unroll
-            for (int b = 0; b < 4; b++) v[k] |= (uint32_t)row[reflect101(sx + b, w)] << (8 * b);
-          }
+          for (int b = 0; b < 16; b++)
+            v[k][b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + b, 0, 0) << (8 * (b & 3));
         }
       }
+    }
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int q = q0 + tid + k * BS;
-        if (q < TR * DW) tin32[q] = v[k];
+    for (int k = 0; k < KQ; k++) {
+      const int q = k * BS + tid;
+      const int ty = q / CPR, j = q - ty * CPR;
+      if (q < NQ) *(uint4*)&tin[ty * kBIn + 16 * j] = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
+    }
+  }
+  const bool left = x0 < 3, right = x0 + kBlurTileW + 3 > w;
+  if (left || right) {
+    // patch the reflected columns x in [-3, -1] and [w, w+2] of every tile row (read after a barrier:
+    // the source columns are inside the row and were stored by other threads)
+    __syncthreads();
+    // two-phase (read all, then write) so no patched byte feeds another patch
+    const int nfix = TR * 6;
+    uint8_t vals[(TR * 6 + BS - 1) / BS];
+#pragma unroll
+    for (int k = 0; k < (TR * 6 + BS - 1) / BS; k++) {
+      const int q = k * BS + tid;
+      vals[k] = 0;
+      if (q < nfix) {
+        const int ty = q / 6, s = q - ty * 6;
+        const int x = s < 3 ? -3 + s : w + (s - 3);
+        const int c = x - (x0 - 4);
+        if (c >= 0 && c < kBIn && (s < 3 ? left : right)) vals[k] = tin[ty * kBIn + reflect101(x, w) - (x0 - 4)];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < (TR * 6 + BS - 1) / BS; k++) {
+      const int q = k * BS + tid;
+      if (q < nfix) {
+        const int ty = q / 6, s = q - ty * 6;
+        const int x = s < 3 ? -3 + s : w + (s - 3);
+        const int c = x - (x0 - 4);
+        if (c >= 0 && c < kBIn && (s < 3 ? left : right)) tin[ty * kBIn + c] = vals[k];
       }
     }
   }
@@ -282,18 +311,20 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
   // [a b c]; lo = bytes j+1..j+4 (k0 k1 k2 k3), hi = bytes j+5..j+8 (k2 k1 k0 0)
   const uint32_t wlo = (uint32_t)k0 | (uint32_t)k1 << 8 | (uint32_t)k2 << 16 | (uint32_t)k3 << 24;
   const uint32_t whi = (uint32_t)k2 | (uint32_t)k1 << 8 | (uint32_t)k0 << 16;
-  // row sums (<= 257*255) of output cols xg..xg+3 on tile row ty
-  auto rowsum = [&](int ty, int (&o)[4]) {
+  const float f0 = (float)k0 * (1.f / 65536.f), f1 = (float)k1 * (1.f / 65536.f), f2 = (float)k2 * (1.f / 65536.f),
+              f3 = (float)k3 * (1.f / 65536.f);
+  // row sums (<= 257*255, exact in f32) of output cols xg..xg+3 on tile row ty
+  auto rowsum = [&](int ty, float (&o)[4]) {
     const uint32_t* r32 = (const uint32_t*)&tin[ty * kBIn + 4 * g];
     const uint32_t a = r32[0], b = r32[1], c = r32[2];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const uint32_t lo = j < 3 ? __builtin_amdgcn_alignbyte(b, a, j + 1) : b;
       const uint32_t hi = j < 3 ? __builtin_amdgcn_alignbyte(c, b, j + 1) : c;
-      o[j] = (int)__builtin_amdgcn_udot4(lo, wlo, __builtin_amdgcn_udot4(hi, whi, 0u, false), false);
+      o[j] = (float)__builtin_amdgcn_udot4(lo, wlo, __builtin_amdgcn_udot4(hi, whi, 0u, false), false);
     }
   };
-  int win[7][4];
+  float win[7][4];
 #pragma unroll
   for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
   const int simd_w = w & ~3;
@@ -306,12 +337,19 @@ __global__ __launch_bounds__(BS) void k_blur(const Geometry* __restrict__ G, con
       uint32_t packed = 0;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        // 24-bit multiplies (v_mad_u32_u24, full rate): row sums <= 257*255, pair sums < 2^17, weights < 256
-        const int acc = (int)(__umul24(k3, win[3][j]) + __umul24(k2, win[2][j] + win[4][j]) +
-                              __umul24(k1, win[1][j] + win[5][j]) + __umul24(k0, win[0][j] + win[6][j]));
-        // SSE2 groups: rint(acc / 2^16) (ties to even; acc >= 2^24 saturates either way); tail: (acc + 2^15) >> 16
-        const int v = (all_simd || xg + j < simd_w) ? (acc + 0x7FFF + ((acc >> 16) & 1)) >> 16 : (acc + (1 << 15)) >> 16;
-        packed |= (uint32_t)min(v, 255) << (8 * j);
+        // acc / 2^16 exactly (integer sums below 2^24 scaled by a power of two)
+        const float acc = __builtin_fmaf(f3, win[3][j],
+                                         __builtin_fmaf(f2, win[2][j] + win[4][j],
+                                                        __builtin_fmaf(f1, win[1][j] + win[5][j],
+                                                                       f0 * (win[0][j] + win[6][j]))));
+        float v;
+        if (all_simd || xg + j < simd_w) {
+          v = __builtin_rintf(acc);  // SSE2 groups: rint(acc / 2^16), ties to even
+        } else {
+          const int ai = (int)(acc * 65536.f);  // scalar tail: (acc + 2^15) >> 16
+          v = (float)((ai + (1 << 15)) >> 16);
+        }
+        packed = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(v, 0.f, 255.f), j, packed);
       }
       uint8_t* d = dst + (size_t)y * bs + xg;
       if (xg + 4 <= w) {
