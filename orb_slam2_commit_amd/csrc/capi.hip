@@ -273,7 +273,7 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
   G.fast_smem = G.fast_tile_bytes + G.fast_map_bytes + 2 * fast_wmax * fast_hmax;
   // k_resize staging bound: source footprint of every 128x16 output tile
   G.rz_rows = 1;
-  G.rz_dpr = 1;
+  G.rz_stride = 16;
   for (int l = 1; l < G.nlevels; l++) {
     const LevelGeom& L = G.lv[l];
     for (int oy = 0; oy < L.h; oy += kRzTH) {
@@ -282,10 +282,10 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
     }
     for (int ox = 0; ox < L.w; ox += kRzTW) {
       const int span = P.xt[L.xtab_off + std::min(ox + kRzTW, L.w) - 1].sx1 - P.xt[L.xtab_off + ox].sx0 + 1;
-      G.rz_dpr = std::max(G.rz_dpr, (3 + span + 3) / 4);
+      G.rz_stride = std::max(G.rz_stride, (span + 15) / 16 * 16);
     }
   }
-  if (G.rz_rows > kRzMaxRows || (size_t)G.rz_rows * G.rz_dpr * 4 > 64 * 1024) return ORBX_ERR_SIZE;
+  if (G.rz_rows > kRzMaxRows || (size_t)G.rz_rows * (G.rz_stride + 2 * kRzTW) > 64 * 1024) return ORBX_ERR_SIZE;
   G.pyr_bytes = (pyr + 255) & ~255LL;
   G.blur_bytes = (blur + 255) & ~255LL;
   G.ncells = (int)P.cells.size();

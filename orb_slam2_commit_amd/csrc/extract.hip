@@ -122,76 +122,99 @@ __device__ __forceinline__ void window_to_lds(const uint8_t* base, size_t stride
 // ------------------------------------------------------------------ resize
 // cv::resize INTER_LINEAR 8U (OpenCV 3.2 fixed point, coefficient tables built
 // on the host exactly as resizeGeneric_ does).  One block per 128x16 output
-// tile: the tile's coefficient entries go to LDS once, its source footprint
-// (rows sy0(first)..sy1(last), cols sx0(first)..sx1(last)) is staged with
-// aligned dword loads (all of a thread's loads issued before its LDS writes),
-// and each thread computes 8 consecutive outputs of one row from LDS.
+// tile, in three LDS phases:
+//   1. the tile's source footprint (rows sy0(first)..sy1(last), cols
+//      sx0(first)..sx1(last)) arrives as 16-B buffer loads at the unaligned row
+//      positions, stored to 16-B aligned LDS rows (byte loads only for a chunk
+//      straddling the level's last byte);
+//   2. the horizontal pass once per footprint row and output column:
+//      (S[sx0]*a0 + S[sx1]*a1) >> 4 as int16 (shared by the <= 2 output rows that
+//      read each source row);
+//   3. the vertical pass for 4 output columns per item:
+//      ((b0*h0)>>16 + (b1*h1)>>16 + 2) >> 2 with v_mul_hi_u32(b<<16, h), packed
+//      into one dword store.
 __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, const ResizeX* __restrict__ xt,
                                                const ResizeY* __restrict__ yt, BatchPtrs B, int l) {
-  extern __shared__ __align__(16) uint32_t rz_tin[];
-  __shared__ ResizeX sx[kRzTW];
-  __shared__ ResizeY sy[kRzTH];
-  __shared__ int rsh[kRzMaxRows];
+  extern __shared__ __align__(16) uint8_t rz_smem[];
   const LevelGeom& L = G->lv[l];
   const LevelGeom& S = G->lv[l - 1];
   const int3 bi = xcd_block3();
   const int img = bi.z, tid = threadIdx.x;
   const int ox0 = bi.x * kRzTW, oy0 = bi.y * kRzTH;
   const int nx = min(kRzTW, L.w - ox0), ny = min(kRzTH, L.h - oy0);
-  if (tid < nx) sx[tid] = xt[L.xtab_off + ox0 + tid];
-  if (tid >= kRzTW && tid - kRzTW < ny) sy[tid - kRzTW] = yt[L.ytab_off + oy0 + tid - kRzTW];
-  __syncthreads();
+  const ResizeX* X = xt + L.xtab_off + ox0;
+  const ResizeY* Y = yt + L.ytab_off + oy0;
+  const int cx0 = X[0].sx0, span = X[nx - 1].sx1 - cx0 + 1;
+  const int ry0 = Y[0].sy0, nrows = Y[ny - 1].sy1 - ry0 + 1;
+  const int stride = G->rz_stride;
+  uint8_t* tin = rz_smem;
+  int16_t* hb = (int16_t*)(rz_smem + G->rz_rows * stride);  // [rows][kRzTW]
   const uint8_t* src = level_ptr(*G, B, img, l - 1);
-  const uint8_t* src_end = src + (size_t)S.w * S.h;
-  const int cx0 = sx[0].sx0, span = sx[nx - 1].sx1 - cx0 + 1;
-  const int ry0 = sy[0].sy0, nrows = sy[ny - 1].sy1 - ry0 + 1;
-  const int dpr = G->rz_dpr;
-  const int total = nrows * dpr;
-  for (int q0 = 0; q0 < total; q0 += 8 * BS) {
-    uint32_t v[8];
+  const int swh = S.w * S.h;
+  // 1. footprint -> LDS
+  {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, swh, 0x00020000);
+    const int nch = (span + 15) >> 4, total = nrows * nch;
+    for (int q = tid; q < total; q += BS) {
+      const int r = q / nch, c = q - r * nch;
+      const int o = (ry0 + r) * S.w + cx0 + 16 * c;
+      uint32_t v0, v1, v2, v3;
+      if (o + 16 <= swh) {
+        const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+        v0 = t[0];
+        v1 = t[1];
+        v2 = t[2];
+        v3 = t[3];
+      } else {  // last bytes of the level: byte loads, each range-checked (outside -> 0, never used)
+        uint32_t w4[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int q = q0 + k * BS + tid;
-      v[k] = 0;
-      if (q < total) {
-        const int r = q / dpr, j = q - r * dpr;
-        const uint8_t* a = src + (size_t)(ry0 + r) * S.w + cx0;
-        const int sh = (int)((uintptr_t)a & 3);
-        const uint8_t* d = a - sh + 4 * j;
-        if (4 * j < sh + span) {
-          if (d >= src && d + 4 <= src_end) {
-            v[k] = *(const uint32_t*)d;
-          } else {  // first/last dword of the level: byte loads inside it only
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-              if (d + b >= src && d + b < src_end) v[k] |= (uint32_t)d[b] << (8 * b);
-          }
-        }
-        if (j == 0) rsh[r] = sh;
+        for (int b = 0; b < 16; b++)
+          w4[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + b, 0, 0) << (8 * (b & 3));
+        v0 = w4[0];
+        v1 = w4[1];
+        v2 = w4[2];
+        v3 = w4[3];
       }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int q = q0 + k * BS + tid;
-      if (q < total) rz_tin[q] = v[k];
+      *(uint4*)&tin[r * stride + 16 * c] = make_uint4(v0, v1, v2, v3);
     }
   }
   __syncthreads();
-  const int r = tid >> 4, g = tid & 15;
-  if (r >= ny) return;
-  const ResizeY Y = sy[r];
-  const uint8_t* tin = (const uint8_t*)rz_tin;
-  const uint8_t* t0 = tin + (Y.sy0 - ry0) * 4 * dpr + rsh[Y.sy0 - ry0] - cx0;
-  const uint8_t* t1 = tin + (Y.sy1 - ry0) * 4 * dpr + rsh[Y.sy1 - ry0] - cx0;
-  uint8_t* dst = B.pyr + (size_t)img * G->pyr_bytes + L.off + (size_t)(oy0 + r) * L.w + ox0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const int c = 8 * g + k;
+  // 2. horizontal pass: thread = one output column, rows strided by BS / kRzTW
+  {
+    const int c = tid & (kRzTW - 1);
     if (c < nx) {
-      const ResizeX X = sx[c];
-      const int h0 = t0[X.sx0] * X.a0 + t0[X.sx1] * X.a1;
-      const int h1 = t1[X.sx0] * X.a0 + t1[X.sx1] * X.a1;
-      dst[c] = (uint8_t)((((Y.b0 * (h0 >> 4)) >> 16) + ((Y.b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+      const ResizeX x = X[c];
+      const int s0 = x.sx0 - cx0, s1 = x.sx1 - cx0, a0 = x.a0, a1 = x.a1;
+      for (int r = tid / kRzTW; r < nrows; r += BS / kRzTW) {
+        const uint8_t* t = tin + r * stride;
+        hb[r * kRzTW + c] = (int16_t)((t[s0] * a0 + t[s1] * a1) >> 4);
+      }
+    }
+  }
+  __syncthreads();
+  // 3. vertical pass: item = (output row, group of 4 columns)
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(B.pyr + (size_t)img * G->pyr_bytes + L.off), (short)0, L.w * L.h, 0x00020000);
+  for (int it = tid; it < ny * (kRzTW / 4); it += BS) {
+    const int i = it / (kRzTW / 4), g = it - i * (kRzTW / 4);
+    if (4 * g >= nx) continue;
+    const ResizeY y = Y[i];
+    const uint32_t B0 = (uint32_t)y.b0 << 16, B1 = (uint32_t)y.b1 << 16;
+    const uint2 p0 = *(const uint2*)&hb[(y.sy0 - ry0) * kRzTW + 4 * g];
+    const uint2 p1 = *(const uint2*)&hb[(y.sy1 - ry0) * kRzTW + 4 * g];
+    const uint32_t h0[4] = {p0.x & 0xFFFF, p0.x >> 16, p0.y & 0xFFFF, p0.y >> 16};
+    const uint32_t h1[4] = {p1.x & 0xFFFF, p1.x >> 16, p1.y & 0xFFFF, p1.y >> 16};
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t v = (__umulhi(B0, h0[j]) + __umulhi(B1, h1[j]) + 2) >> 2;
+      packed |= v << (8 * j);
+    }
+    const int o = (oy0 + i) * L.w + ox0 + 4 * g;
+    if (4 * g + 4 <= nx) {
+      __builtin_amdgcn_raw_buffer_store_b32(packed, rd, o, 0, 0);
+    } else {
+      for (int j = 0; j < nx - 4 * g; j++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(packed >> (8 * j)), rd, o + j, 0, 0);
     }
   }
 }
@@ -1126,7 +1149,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   for (int l = 1; l < Gh.nlevels; l++) {
     dim3 grid((Gh.lv[l].w + kRzTW - 1) / kRzTW, (Gh.lv[l].h + kRzTH - 1) / kRzTH, n_img);
     T->begin(st);
-    hipLaunchKernelGGL(k_resize, grid, dim3(BS), (size_t)Gh.rz_rows * Gh.rz_dpr * 4, st, Gd, xt, yt, B, l);
+    hipLaunchKernelGGL(k_resize, grid, dim3(BS), (size_t)Gh.rz_rows * (Gh.rz_stride + 2 * kRzTW), st, Gd, xt, yt, B, l);
     T->end(ST_RESIZE, st);
   }
   if (Gh.ncells > 0) {

@@ -48,10 +48,10 @@ struct Geometry {
   int fast_rp;     // k_fast: region rows per compass instruction (2 when every cell is <= 32 wide)
   int fast_tile_bytes, fast_map_bytes, fast_smem;  // k_fast dynamic LDS layout (sized by the largest cell)
   int rz_rows;    // k_resize: max source rows staged per 128x16 output tile
-  int rz_dpr;     // k_resize: max source dwords per staged row
+  int rz_stride;  // k_resize: LDS row stride of the staged footprint (16-B chunks covering the widest span)
 };
 
-constexpr int kRzTW = 128, kRzTH = 16;  // k_resize output tile
+constexpr int kRzTW = 128, kRzTH = 32;  // k_resize output tile
 constexpr int kRzMaxRows = 64;
 
 struct CellInfo {
