@@ -21,7 +21,8 @@ from collections import defaultdict
 
 def short(name):
     n = name.split("(")[0]
-    return n.split("::")[-1]
+    n = n.split("::")[-1]
+    return n.split("<")[0] if n.startswith("k_") else n
 
 
 def pmc(path, counter):
@@ -33,7 +34,7 @@ def pmc(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
-def main(prof_dir="gpurun_out/prof", tag="r01"):
+def main(prof_dir="gpurun_out/prof", tag="r01", batch="256"):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.path.join(root, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -54,7 +55,10 @@ def main(prof_dir="gpurun_out/prof", tag="r01"):
         if os.path.exists(src):
             shutil.copy(src, os.path.join(out, "%s_%s_kernel_stats.csv" % (tag, extra)))
     json.dump(summary, open(os.path.join(out, "%s_pmc.json" % tag), "w"), indent=1)
-    json.dump({"source": "%s_pmc.json" % tag, "per_launch_bytes": per_launch,
+    import subprocess
+    head = subprocess.run(["git", "-C", root, "rev-parse", "--short", "HEAD"], capture_output=True,
+                          text=True).stdout.strip() or None
+    json.dump({"source": "%s_pmc.json" % tag, "head": head, "batch": int(batch), "per_launch_bytes": per_launch,
                "note": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per dispatch, averaged over dispatches"},
               open(os.path.join(out, "traffic.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
