@@ -49,6 +49,9 @@
 #define ORBX_H
 #include <stddef.h>
 #include <stdint.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -238,6 +241,10 @@ orbx_status orbx_ba_destroy(orbx_ba* h);
  * before the run and between LM trials. */
 orbx_status orbx_ba_run(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_result* result,
                         const volatile int* stop_flag);
+/* The same with the reference's own flag type: LocalBundleAdjustment(KeyFrame*, bool* pbStopFlag, Map*)
+ * (include/Optimizer.h:61), set from LocalMapping::InterruptBA on another thread. */
+orbx_status orbx_ba_run_bool(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_result* result,
+                             const volatile bool* stop_flag);
 /* One-shot form: create, run, destroy. */
 orbx_status orbx_local_ba(const orbx_ba_problem* problem, orbx_ba_result* result, const volatile int* stop_flag,
                           int device);

@@ -29,7 +29,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
                                  const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B, int n_img,
                                  orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t st,
                                  StageTimer* T);
-size_t octree_smem_host(int NC, int cell_cap);
+size_t octree_smem_host(int NC, int cell_cap, int kcap);
 hipError_t octree_set_smem_limit(size_t bytes);
 }  // namespace orbx
 
@@ -296,7 +296,21 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
   G.node_cap = node_cap;
   G.cell_cap = cell_cap;
   if (node_cap > 8192) return ORBX_ERR_SIZE;
-  if (octree_smem_host(node_cap, cell_cap) > 160 * 1024 - 1024) return ORBX_ERR_SIZE;
+  if (octree_smem_host(node_cap, cell_cap, 0) > 160 * 1024 - 1024) return ORBX_ERR_SIZE;
+  // octree candidate slots in LDS: fill the block up to 50 KB with the kernel's static LDS (three
+  // 512-thread blocks must fit the CU's 160 KB -- the VGPR limit allows three; at 53 KB the
+  // allocation granularity left two and the kernel ran 15 % slower), at least 1024, never more
+  // than a level can hold
+  {
+    int max_lv_cand = 1;
+    for (int l = 0; l < p.nlevels; l++) max_lv_cand = std::max(max_lv_cand, G.lv[l].cand_cap);
+    const long long base = (long long)octree_smem_host(node_cap, cell_cap, 0);
+    long long kc = (50 * 1024 - 512 - base) / 6;
+    kc = std::max(kc, 1024LL) & ~63LL;
+    kc = std::min(kc, (long long)(max_lv_cand + 63) / 64 * 64);
+    while (kc > 64 && (long long)octree_smem_host(node_cap, cell_cap, (int)kc) > 160 * 1024 - 1024) kc -= 64;
+    G.oct_kcap = (int)kc;
+  }
   return ORBX_OK;
 }
 
@@ -311,7 +325,7 @@ struct orbx_extractor {
   // batch buffers
   int batch_cap = 0;
   long long bytes_pyr = 0, bytes_blur = 0, n_cand = 0, n_oct = 0, n_cells = 0;
-  DevBuf<uint8_t> pyr, blur, kdig;
+  DevBuf<uint8_t> pyr, blur;
   DevBuf<uint32_t> cand, kpos, oct;
   DevBuf<int> cell_count, knode, oct_count;
   // host-API staging
@@ -321,6 +335,7 @@ struct orbx_extractor {
   // stereo scratch
   DevBuf<uint64_t> rkeys;
   DevBuf<int2> rxi;
+  DevBuf<uint4> rdesc;
   DevBuf<uint32_t> rtab;
   DevBuf<int> oct_start, sad;
   DevBuf<float> uR, depth;
@@ -371,7 +386,7 @@ orbx_status get_plan(orbx_extractor* h, int W, int H, Plan** out) {
   if (e == hipSuccess && !P->yt.empty())
     e = hipMemcpy(P->dyt.p, P->yt.data(), P->yt.size() * sizeof(ResizeY), hipMemcpyHostToDevice);
   if (e != hipSuccess) return ORBX_ERR_HIP;
-  e = octree_set_smem_limit(octree_smem_host(P->G.node_cap, P->G.cell_cap));
+  e = octree_set_smem_limit(octree_smem_host(P->G.node_cap, P->G.cell_cap, P->G.oct_kcap));
   if (e != hipSuccess) return ORBX_ERR_HIP;
   *out = P.get();
   h->plans[key] = std::move(P);
@@ -387,7 +402,6 @@ orbx_status ensure_batch(orbx_extractor* h, const Plan& P, int n) {
   chk(h->cand.ensure((size_t)G.cand_total * n));
   chk(h->kpos.ensure((size_t)G.cand_total * n));
   chk(h->knode.ensure((size_t)G.cand_total * n));
-  chk(h->kdig.ensure((size_t)G.cand_total * n));
   chk(h->cell_count.ensure((size_t)std::max(G.ncells, 1) * n));
   chk(h->oct.ensure((size_t)G.oct_total * n));
   chk(h->oct_count.ensure((size_t)G.nlevels * n));
@@ -404,7 +418,6 @@ BatchPtrs batch_ptrs(orbx_extractor* h, const uint8_t* in, size_t pitch) {
   B.cell_count = h->cell_count.p;
   B.kpos = h->kpos.p;
   B.knode = h->knode.p;
-  B.kdig = h->kdig.p;
   B.oct = h->oct.p;
   B.oct_count = h->oct_count.p;
   return B;
@@ -602,6 +615,7 @@ static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_fram
   chk(h->rkeys.ensure((size_t)n_frames * kMaxStereoKps));
   chk(h->oct_start.ensure((size_t)n_frames * (kMaxLevelsPlan + 1)));
   chk(h->rxi.ensure((size_t)n_frames * kMaxStereoKps));
+  chk(h->rdesc.ensure((size_t)n_frames * kMaxStereoKps * 2));
   chk(h->rtab.ensure((size_t)n_frames * P->G.nlevels * std::max(P->G.height, 1)));
   chk(h->sad.ensure((size_t)n_frames * out_stride));
   if (e != hipSuccess) return ORBX_ERR_HIP;
@@ -637,6 +651,7 @@ static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_fram
   A.rkeys = h->rkeys.p;
   A.oct_start = h->oct_start.p;
   A.rxi = h->rxi.p;
+  A.rdesc = h->rdesc.p;
   A.rtab = h->rtab.p;
   A.rows = std::max(P->G.height, 1);
   A.nmatches = nmatches;

@@ -28,41 +28,45 @@ constexpr int BS = 256;
 
 // ---------------------------------------------------------------- block scan
 // Exclusive scan of a[0..n) in LDS (in place); returns the total. All NT threads call.
-template <int NT>
-__device__ int block_exclusive_scan(int* a, int n) {
-  __shared__ int wsum[NT / 64 + 1];
+// Two barriers: after the wave totals are published every thread adds up the
+// NT/64 totals below its own wave itself (no serial pass + second barrier);
+// the trailing barrier orders the in-place writes before any other reader.
+template <int NT, class T>
+__device__ T block_scan_excl(T* a, int n) {
+  __shared__ T wsum[NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int chunk = (n + NT - 1) / NT;
   const int b = tid * chunk, e = min(n, b + chunk);
-  int local = 0;
+  T local = 0;
   for (int i = b; i < e; i++) local += a[i];
-  int incl = local;
+  T incl = local;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    int v = __shfl_up(incl, o, 64);
+    const T v = __shfl_up(incl, o, 64);
     if (lane >= o) incl += v;
   }
   if (lane == 63) wsum[wid] = incl;
   __syncthreads();
-  if (tid == 0) {
-    int s = 0;
-    for (int w = 0; w < NT / 64; w++) {
-      int t = wsum[w];
-      wsum[w] = s;
-      s += t;
-    }
-    wsum[NT / 64] = s;
+  T before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; w++) {
+    const T t = wsum[w];
+    before += w < wid ? t : 0;
+    total += t;
   }
-  __syncthreads();
-  int run = wsum[wid] + incl - local;
+  T run = before + incl - local;
   for (int i = b; i < e; i++) {
-    int v = a[i];
+    const T v = a[i];
     a[i] = run;
     run += v;
   }
-  const int total = wsum[NT / 64];
   __syncthreads();
   return total;
+}
+
+template <int NT>
+__device__ int block_exclusive_scan(int* a, int n) {
+  return block_scan_excl<NT, int>(a, n);
 }
 
 template <int NT>
@@ -630,6 +634,8 @@ struct OctSmem {
   uint64_t* key;   // [NP2] (also best)
   int* cpre;       // [cell_cap+1]
   int* ctrl;       // [8]
+  uint32_t* kp;    // [kcap] candidate positions
+  uint16_t* kn;    // [kcap] candidate node | digit << 14
 };
 
 __host__ __device__ inline int next_pow2(int v) {
@@ -638,7 +644,7 @@ __host__ __device__ inline int next_pow2(int v) {
   return p;
 }
 
-__host__ __device__ inline size_t octree_smem_bytes(int NC, int cell_cap) {
+__host__ __device__ inline size_t octree_smem_bytes(int NC, int cell_cap, int kcap) {
   const int NP2 = next_pow2(NC);
   size_t b = 0;
   b += 2 * 4 * NC * sizeof(int16_t);
@@ -651,6 +657,7 @@ __host__ __device__ inline size_t octree_smem_bytes(int NC, int cell_cap) {
   b += (size_t)NP2 * sizeof(uint64_t);
   b += (cell_cap + 1) * sizeof(int);
   b += 8 * sizeof(int);
+  b += (size_t)kcap * (sizeof(uint32_t) + sizeof(uint16_t));
   return b;
 }
 
@@ -677,7 +684,46 @@ __device__ __forceinline__ void bitonic_sort_desc(uint64_t* k, int n) {
   }
 }
 
-__global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
+// Per-candidate state across the split rounds: the packed position (score<<24 |
+// y<<12 | x, level-relative) and node | child digit<<14.  The first G->oct_kcap
+// candidates of a level live in LDS for the whole kernel (sized on the host so
+// the block still fits three per CU); only a level with more candidates keeps
+// the rest in the global kpos/knode scratch.  Every round walks all candidates
+// of the level, so keeping them out of memory removes the per-round L2/HBM
+// round trips (counter traffic 240 -> ~100 MB per 512 images).
+struct OctCands {
+  uint32_t* lpos;
+  uint16_t* lnd;
+  int kcap;
+  uint32_t* gpos;
+  uint32_t* gnd;
+  __device__ __forceinline__ uint32_t pos(int k) const { return k < kcap ? lpos[k] : gpos[k]; }
+  __device__ __forceinline__ uint32_t nd(int k) const { return k < kcap ? (uint32_t)lnd[k] : gnd[k]; }
+  __device__ __forceinline__ void set(int k, uint32_t p, uint32_t n) const {
+    if (k < kcap) {
+      lpos[k] = p;
+      lnd[k] = (uint16_t)n;
+    } else {
+      gpos[k] = p;
+      gnd[k] = n;
+    }
+  }
+  __device__ __forceinline__ void set_nd(int k, uint32_t n) const {
+    if (k < kcap) lnd[k] = (uint16_t)n; else gnd[k] = n;
+  }
+};
+
+template <class F>
+__device__ __forceinline__ void oct_cands(int T, const OctCands& c, F f) {
+  for (int k = threadIdx.x; k < T; k += OBS) {
+    const uint32_t n0 = c.nd(k);
+    uint32_t n = n0;
+    f(k, c.pos(k), n);
+    if (n != n0) c.set_nd(k, n);
+  }
+}
+
+__global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k_octree(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                                BatchPtrs B) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int l = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
@@ -701,14 +747,14 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
     p = (unsigned char*)(((uintptr_t)p + 7) & ~(uintptr_t)7);
     s.key = (uint64_t*)p; p += (size_t)NP2 * 8;
     s.cpre = (int*)p; p += (G->cell_cap + 1) * 4;
-    s.ctrl = (int*)p;
+    s.ctrl = (int*)p; p += 8 * 4;
+    s.kp = (uint32_t*)p; p += (size_t)G->oct_kcap * 4;
+    s.kn = (uint16_t*)p;
   }
   uint32_t* oct_out = B.oct + (size_t)img * G->oct_total + L.oct_off;
   int* oct_cnt = B.oct_count + (size_t)img * G->nlevels + l;
   const size_t kbase = (size_t)img * G->cand_total + L.cand_begin;
-  uint32_t* kpos = B.kpos + kbase;
-  int* knode = B.knode + kbase;
-  uint8_t* kdig = B.kdig + kbase;
+  OctCands oc{s.kp, s.kn, G->oct_kcap, B.kpos + kbase, (uint32_t*)B.knode + kbase};
 
   // 1. candidates of this level in vToDistributeKeys order (cells row-major)
   const int ncl = L.cell_end - L.cell_begin;
@@ -726,7 +772,7 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
   for (int i = tid; i < nIni; i += OBS) s.ccnt[i] = 0;
   __syncthreads();
   const uint32_t* cand = B.cand + (size_t)img * G->cand_total;
-  for (int k = tid; k < T; k += OBS) {
+  auto load_cand = [&](int k, uint32_t& pos, uint32_t& nd) {
     int lo = 0, hi = ncl - 1;  // last c with cpre[c] <= k
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -735,11 +781,16 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
     const CellInfo& ci = cells[L.cell_begin + lo];
     const uint32_t v = cand[ci.cand_off + (k - s.cpre[lo])];
     const int xr = (int)(v & 0xFFF) - minBX, yr = (int)((v >> 12) & 0xFFF) - minBY;
-    kpos[k] = (v & 0xFF000000u) | ((uint32_t)yr << 12) | (uint32_t)xr;
+    pos = (v & 0xFF000000u) | ((uint32_t)yr << 12) | (uint32_t)xr;
     int root = (int)((float)xr / hX);
     root = min(max(root, 0), nIni - 1);
-    knode[k] = root;
+    nd = (uint32_t)root;
     atomicAdd(&s.ccnt[root], 1);
+  };
+  for (int k = tid; k < T; k += OBS) {
+    uint32_t pos, nd;
+    load_cand(k, pos, nd);
+    oc.set(k, pos, nd);
   }
   __syncthreads();
   // 2. roots -> list (empty roots erased, src/ORBextractor.cc:604-615)
@@ -759,7 +810,11 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
     }
   }
   __syncthreads();
-  for (int k = tid; k < T; k += OBS) knode[k] = s.nidx[knode[k]];
+  oct_cands(T, oc, [&](int, uint32_t, uint32_t& nd) { nd = (uint32_t)s.nidx[nd]; });
+  // child counters of the next round are cleared by the pass that precedes that
+  // round's opening barrier (here, and after each round's remap): one barrier
+  // per round fewer than a separate clear
+  for (int i = tid; i < S * 4; i += OBS) s.ccnt[i] = 0;
   int cur = 0;
   int seqBase = nIni;
   int phase = 1;
@@ -767,40 +822,42 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
   for (int round = 0; round < 256; round++) {
     __syncthreads();
     const int nb = cur ^ 1;
-    for (int i = tid; i < S * 4; i += OBS) s.ccnt[i] = 0;
-    __syncthreads();
     // kp pass A: child digit of every keypoint whose node splits (count > 1)
-    for (int k = tid; k < T; k += OBS) {
-      const int n = knode[k];
+    oct_cands(T, oc, [&](int, uint32_t v, uint32_t& nd) {
+      const int n = (int)(nd & 0x3FFF);
       if ((s.cnt + cur * NC)[n] > 1) {
         const int nx0 = (s.x0 + cur * NC)[n], ny0 = (s.y0 + cur * NC)[n];
         const int hx = (int)__builtin_ceilf((float)((s.x1 + cur * NC)[n] - nx0) / 2);
         const int hy = (int)__builtin_ceilf((float)((s.y1 + cur * NC)[n] - ny0) / 2);
-        const uint32_t v = kpos[k];
         const float fx = (float)(int)(v & 0xFFF), fy = (float)(int)((v >> 12) & 0xFFF);
         const int d = (fx < (float)(nx0 + hx) ? 0 : 1) + (fy < (float)(ny0 + hy) ? 0 : 2);
-        kdig[k] = (uint8_t)d;
+        nd = (uint32_t)n | ((uint32_t)d << 14);
         atomicAdd(&s.ccnt[n * 4 + d], 1);
       }
-    }
+    });
     __syncthreads();
     int C, Snew;
     if (phase == 1) {
-      // split every node with > 1 keypoint, in list order
-      if (tid == 0) s.ctrl[0] = 0;
+      // split every node with > 1 keypoint, in list order.  One scan of packed
+      // (children | kept << 16 | expandable children << 32) gives each node its
+      // child and kept positions and the round's totals.
       for (int i = tid; i < S; i += OBS) {
         const bool split = (s.cnt + cur * NC)[i] > 1;
-        int nc = 0;
+        uint64_t v = split ? 0 : (1ull << 16);
         if (split)
-          for (int d = 0; d < 4; d++) nc += s.ccnt[i * 4 + d] > 0;
-        s.sa[i] = nc;
-        s.sb[i] = split ? 0 : 1;
+          for (int d = 0; d < 4; d++) {
+            const int cc = s.ccnt[i * 4 + d];
+            v += (cc > 0 ? 1ull : 0ull) + (cc > 1 ? (1ull << 32) : 0ull);
+          }
+        s.key[i] = v;
       }
       __syncthreads();
-      C = block_exclusive_scan<OBS>(s.sa, S);
-      const int Sg = block_exclusive_scan<OBS>(s.sb, S);
-      int nexp = 0;
+      const uint64_t tot = block_scan_excl<OBS, uint64_t>(s.key, S);
+      C = (int)(tot & 0xFFFF);
+      const int Sg = (int)((tot >> 16) & 0xFFFF);
+      const int nexp = (int)(tot >> 32);
       for (int i = tid; i < S; i += OBS) {
+        const uint64_t pre = s.key[i];
         if ((s.cnt + cur * NC)[i] > 1) {
           const int nx0 = (s.x0 + cur * NC)[i], ny0 = (s.y0 + cur * NC)[i], nx1 = (s.x1 + cur * NC)[i], ny1 = (s.y1 + cur * NC)[i];
           const int hx = (int)__builtin_ceilf((float)(nx1 - nx0) / 2);
@@ -809,7 +866,7 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
           for (int d = 0; d < 4; d++) {
             const int cc = s.ccnt[i * 4 + d];
             if (cc == 0) continue;
-            const int p = s.sa[i] + rank++;
+            const int p = (int)(pre & 0xFFFF) + rank++;
             const int ni = C - 1 - p;
             (s.x0 + nb * NC)[ni] = (int16_t)((d & 1) ? nx0 + hx : nx0);
             (s.x1 + nb * NC)[ni] = (int16_t)((d & 1) ? nx1 : nx0 + hx);
@@ -818,10 +875,9 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
             (s.cnt + nb * NC)[ni] = cc;
             (s.seq + nb * NC)[ni] = seqBase + p;
             s.cidx[i * 4 + d] = (int16_t)ni;
-            nexp += cc > 1;
           }
         } else {
-          const int ni = C + s.sb[i];
+          const int ni = C + (int)((pre >> 16) & 0xFFFF);
           (s.x0 + nb * NC)[ni] = (s.x0 + cur * NC)[i];
           (s.x1 + nb * NC)[ni] = (s.x1 + cur * NC)[i];
           (s.y0 + nb * NC)[ni] = (s.y0 + cur * NC)[i];
@@ -831,12 +887,13 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
           s.nidx[i] = (int16_t)ni;
         }
       }
-      nexp = block_sum<OBS>(nexp);
-      for (int k = tid; k < T; k += OBS) {
-        const int n = knode[k];
-        knode[k] = (s.cnt + cur * NC)[n] > 1 ? s.cidx[n * 4 + kdig[k]] : s.nidx[n];
-      }
+      __syncthreads();  // children / cidx / nidx written before the candidates remap
+      oct_cands(T, oc, [&](int, uint32_t, uint32_t& nd) {
+        const int n = (int)(nd & 0x3FFF);
+        nd = (uint32_t)((s.cnt + cur * NC)[n] > 1 ? s.cidx[n * 4 + (nd >> 14)] : s.nidx[n]);
+      });
       Snew = C + Sg;
+      for (int i = tid; i < Snew * 4; i += OBS) s.ccnt[i] = 0;
       seqBase += C;
       const bool finish = Snew >= N || Snew == S;
       S = Snew;
@@ -926,13 +983,13 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
         s.nidx[i] = (int16_t)ni;
       }
       __syncthreads();
-      for (int k = tid; k < T; k += OBS) {
-        const int n = knode[k];
-        // processed nodes' slots were overwritten? no: nidx[n]==-2 only for processed
-        const int ni = s.nidx[n];
-        knode[k] = ni == -2 ? s.cidx[n * 4 + kdig[k]] : ni;
-      }
+      oct_cands(T, oc, [&](int, uint32_t, uint32_t& nd) {
+        const int n = (int)(nd & 0x3FFF);
+        const int ni = s.nidx[n];  // -2: n was split this round
+        nd = (uint32_t)(ni == -2 ? s.cidx[n * 4 + (nd >> 14)] : ni);
+      });
       Snew = C + rest;
+      for (int i = tid; i < Snew * 4; i += OBS) s.ccnt[i] = 0;
       seqBase += C;
       const bool finish = Snew >= N || Snew == S;
       S = Snew;
@@ -944,13 +1001,12 @@ __global__ __launch_bounds__(OBS) void k_octree(const Geometry* __restrict__ G, 
   // 3. best response per node: max score, then lowest candidate index
   for (int i = tid; i < S; i += OBS) s.key[i] = 0;
   __syncthreads();
-  for (int k = tid; k < T; k += OBS) {
-    const uint32_t v = kpos[k];
+  oct_cands(T, oc, [&](int k, uint32_t v, uint32_t& nd) {
     const uint32_t x = (v & 0xFFF) + minBX, y = ((v >> 12) & 0xFFF) + minBY;
     const uint64_t key = ((uint64_t)(v >> 24) << 56) | ((uint64_t)(0xFFFFFFu - (uint32_t)k) << 24) |
                          (uint64_t)((y << 12) | x);
-    atomicMax((unsigned long long*)&s.key[knode[k]], (unsigned long long)key);
-  }
+    atomicMax((unsigned long long*)&s.key[nd & 0x3FFF], (unsigned long long)key);
+  });
   __syncthreads();
   const int nout = min(S, L.oct_cap);
   for (int i = tid; i < nout; i += OBS) {
@@ -1164,7 +1220,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
   T->end(ST_BLUR, st);
   if (Gh.ncells > 0) {
-    const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap);
+    const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap, Gh.oct_kcap);
     T->begin(st);
     hipLaunchKernelGGL(k_octree, dim3(Gh.nlevels, n_img), dim3(OBS), smem, st, Gd, cells, B);
     T->end(ST_OCTREE, st);
@@ -1176,7 +1232,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   return hipGetLastError();
 }
 
-size_t octree_smem_host(int NC, int cell_cap) { return octree_smem_bytes(NC, cell_cap); }
+size_t octree_smem_host(int NC, int cell_cap, int kcap) { return octree_smem_bytes(NC, cell_cap, kcap); }
 
 hipError_t octree_set_smem_limit(size_t bytes) {
   return hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

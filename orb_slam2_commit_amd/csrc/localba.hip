@@ -38,6 +38,15 @@
 
 namespace orbx {
 
+// The reference's pbStopFlag (bool*, src/Optimizer.cc:530, set by LocalMapping::InterruptBA) or an
+// int mirror of it; polled before the run and between LM trials (SparseOptimizer::terminate()).
+struct StopFlag {
+  const volatile int* i = nullptr;
+  const volatile bool* b = nullptr;
+  bool operator()() const { return (i && *i) || (b && *b); }
+};
+
+
 // ------------------------------------------------------------ SE3 numerics
 struct Quat {
   double x, y, z, w;
@@ -1628,7 +1637,7 @@ struct LocalBA {
   // SparseOptimizer::optimize + OptimizationAlgorithmLevenberg::solve.  One
   // host readback per LM trial (plus one for lambda init per phase); the
   // accept/reject logic runs on the host on exactly the reference's doubles.
-  orbx_status optimize(int iterations, const volatile int* stop, hipStream_t st, int* iters, double* final_chi) {
+  orbx_status optimize(int iterations, const StopFlag& stop, hipStream_t st, int* iters, double* final_chi) {
     double lambda = 0, ni = 2;
     int nBad = 0;
     int it = 0;
@@ -1646,7 +1655,7 @@ struct LocalBA {
     const bool spec_on = std::getenv("ORBX_BA_NO_SPEC") == nullptr;  // A/B switch
     bool spec_ready = false;  // the other LinSet holds the linearisation at the current state
     double spec_chi = 0;      // its chi (the accepted trial's)
-    for (int i = 0; i < iterations && !(stop && *stop); i++) {
+    for (int i = 0; i < iterations && !(stop()); i++) {
       const bool from_spec = spec_ready;
       if (from_spec) {
         lin_cur ^= 1;
@@ -1711,7 +1720,7 @@ struct LocalBA {
           BA_CHECK(hipGetLastError());
         }
         qmax++;
-      } while (rho < 0 && qmax < 10 && !(stop && *stop));
+      } while (rho < 0 && qmax < 10 && !(stop()));
       ++it;
       if (qmax == 10 || rho == 0) break;
       if ((iniChi - currentChi) * 1e3 < iniChi)
@@ -1728,7 +1737,7 @@ struct LocalBA {
   }
 };
 
-orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, const volatile int* stop,
+orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, const StopFlag& stop,
                          hipStream_t st) {
   L.trials = 0;
   for (double& t : L.t_struct) t = 0;
@@ -1834,7 +1843,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   res->chi2[0] = res->chi2[1] = 0;
   const int ge = (ne + LBS - 1) / LBS;
   bool ran = false;
-  if (!(stop && *stop)) {  // src/Optimizer.cc:749-751
+  if (!(stop())) {  // src/Optimizer.cc:749-751
     ran = true;
     L.level.assign(ne, 0);
     const auto tb0 = std::chrono::steady_clock::now();
@@ -1844,7 +1853,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
     if (s != ORBX_OK) return s;
     s = L.optimize(5, stop, st, &res->iterations[0], &res->chi2[0]);
     if (s != ORBX_OK) return s;
-    if (!(stop && *stop)) {
+    if (!(stop())) {
       // :764-802 level-1 outliers, drop robust kernels
       if (ne > 0) hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 1);
       BA_CHECK(hipGetLastError());
@@ -1942,7 +1951,22 @@ orbx_status orbx_ba_run(orbx_ba* h, const orbx_ba_problem* p, orbx_ba_result* r,
   if (p->n_edges > 0 && (!p->edge_point || !p->edge_cam || !p->obs || !p->inv_sigma2 || !r->edge_outlier))
     return ORBX_ERR_ARG;
   if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
-  return orbx::run_local_ba(h->L, p, r, stop_flag, h->st);
+  orbx::StopFlag f;
+  f.i = stop_flag;
+  return orbx::run_local_ba(h->L, p, r, f, h->st);
+}
+
+orbx_status orbx_ba_run_bool(orbx_ba* h, const orbx_ba_problem* p, orbx_ba_result* r, const volatile bool* stop_flag) {
+  if (!h || !p || !r) return ORBX_ERR_ARG;
+  if (p->n_cams < 0 || p->n_points < 0 || p->n_edges < 0) return ORBX_ERR_ARG;
+  if (p->n_cams > 0 && (!p->Tcw || !p->intr || !r->Tcw)) return ORBX_ERR_ARG;
+  if (p->n_points > 0 && (!p->Xw || !r->Xw)) return ORBX_ERR_ARG;
+  if (p->n_edges > 0 && (!p->edge_point || !p->edge_cam || !p->obs || !p->inv_sigma2 || !r->edge_outlier))
+    return ORBX_ERR_ARG;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  orbx::StopFlag f;
+  f.b = stop_flag;
+  return orbx::run_local_ba(h->L, p, r, f, h->st);
 }
 
 orbx_status orbx_local_ba(const orbx_ba_problem* p, orbx_ba_result* r, const volatile int* stop_flag, int device) {

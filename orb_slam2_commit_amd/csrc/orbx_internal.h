@@ -44,6 +44,7 @@ struct Geometry {
   int ncells, cand_total, oct_total, max_kps, ntiles;
   int node_cap;   // octree LDS node capacity (max over levels, multiple of 64)
   int cell_cap;   // max cells in one level
+  int oct_kcap;   // octree: candidates of a level kept in LDS (the rest in global scratch)
   int fast_s;      // k_fast: LDS row stride of the window tile and the score map (48 or 80)
   int fast_rp;     // k_fast: region rows per compass instruction (2 when every cell is <= 32 wide)
   int fast_tile_bytes, fast_map_bytes, fast_smem;  // k_fast dynamic LDS layout (sized by the largest cell)
@@ -84,7 +85,6 @@ struct BatchPtrs {
   int* cell_count;
   uint32_t* kpos;   // octree scratch
   int* knode;
-  uint8_t* kdig;
   uint32_t* oct;
   int* oct_count;
 };

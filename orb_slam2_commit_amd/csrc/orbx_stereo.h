@@ -30,6 +30,7 @@ struct StereoArgs {
   uint64_t* rkeys;  // [n_frames * kMaxStereoKps]
   int* oct_start;   // [n_frames * (kMaxLevelsPlan+1)]
   int2* rxi;        // [n_frames * kMaxStereoKps]: (float bits of x, index) in (octave, y) order
+  uint4* rdesc;     // [n_frames * kMaxStereoKps * 2]: right descriptors in the same sorted order
   uint32_t* rtab;   // [n_frames * nlevels * rows]: candidate range start | end << 16 per (octave, row)
   int rows;         // rows of the row table = level-0 image height (vRowIndices size)
   int32_t* nmatches;

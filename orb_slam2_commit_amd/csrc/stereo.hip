@@ -71,6 +71,13 @@ __global__ __launch_bounds__(PBS) void k_stereo_prep(StereoArgs A, const Geometr
     const int idx = (int)(k & 0xFFF);
     rxi[i] = make_int2(__float_as_int(kR[idx].x), idx);
   }
+  // descriptors in sorted order, so the match kernel loads a candidate's
+  // descriptor beside its (x, index) instead of after it
+  {
+    const uint4* dR = (const uint4*)(A.dR + (size_t)f * A.kR_stride * 32);
+    uint4* rd = A.rdesc + (size_t)f * kMaxStereoKps * 2;
+    for (int e = tid; e < 2 * nR; e += PBS) rd[e] = dR[2 * (int)(keys[e >> 1] & 0xFFF) + (e & 1)];
+  }
   // octave starts
   int* os = A.oct_start + (size_t)f * (kMaxLevelsPlan + 1);
   for (int o = tid; o <= A.nlevels; o += PBS) {
@@ -119,12 +126,11 @@ __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geomet
   const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
   const int base = bi.x * kKpsPerBlock;
   if (base >= nL) return;
-  const orbx_keypoint* kR = A.kpR + (size_t)f * A.kR_stride;
   const int2* rxi = A.rxi + (size_t)f * kMaxStereoKps;
+  const uint4* rdR = A.rdesc + (size_t)f * kMaxStereoKps * 2;
   const uint32_t* tab = A.rtab + (size_t)f * A.nlevels * A.rows;
   const orbx_keypoint* kL = A.kpL + (size_t)f * A.kL_stride;
   const uint8_t* dL = A.dL + (size_t)f * A.kL_stride * 32;
-  const uint8_t* dR = A.dR + (size_t)f * A.kR_stride * 32;
   const int limg = f * A.l_step + A.l_off, rimg = f * A.r_step + A.r_off;
   const int nl = G->nlevels;
   for (int iL = base + wid; iL < min(nL, base + kKpsPerBlock); iL += SBS / 64) {
@@ -161,26 +167,32 @@ __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geomet
       const uint64_t* p = (const uint64_t*)(dL + (size_t)iL * 32);
       ld[0] = p[0]; ld[1] = p[1]; ld[2] = p[2]; ld[3] = p[3];
     }
+    // candidate (x, index) and descriptor loads are independent (both in sorted
+    // order); the winner's x travels with its key, so no kR[bestIdxR] load follows
     uint32_t best = 0xFFFFFFFFu;
+    float bestX = 0.f;
     for (int j = lane; j < K; j += 64) {
       const int pos = j < n0 ? rb[0] + j : (j < n0 + n1 ? rb[1] + (j - n0) : rb[2] + (j - n0 - n1));
       const int2 xi = rxi[pos];
+      const uint4 r0 = rdR[2 * pos], r1 = rdR[2 * pos + 1];
       const float uR = __int_as_float(xi.x);
       if (!(uR >= minU && uR <= maxU)) continue;
-      const int idx = xi.y;
-      const uint64_t* p = (const uint64_t*)(dR + (size_t)idx * 32);
-      uint64_t rd[4] = {p[0], p[1], p[2], p[3]};
+      const uint64_t rd[4] = {(uint64_t)r0.x | ((uint64_t)r0.y << 32), (uint64_t)r0.z | ((uint64_t)r0.w << 32),
+                              (uint64_t)r1.x | ((uint64_t)r1.y << 32), (uint64_t)r1.z | ((uint64_t)r1.w << 32)};
       const int dist = hamming256(ld, rd);
-      const uint32_t key = ((uint32_t)dist << 12) | (uint32_t)idx;
-      best = key < best ? key : best;
+      const uint32_t key = ((uint32_t)dist << 12) | (uint32_t)xi.y;
+      if (key < best) {
+        best = key;
+        bestX = uR;
+      }
     }
-    best = wave_min_u32(best);
-    const int bestDist = best == 0xFFFFFFFFu ? 100 : (int)(best >> 12);
+    const uint32_t wbest = wave_min_u32(best);
+    const int bestDist = wbest == 0xFFFFFFFFu ? 100 : (int)(wbest >> 12);
     if (bestDist >= 75) continue;  // thOrbDist = (TH_HIGH+TH_LOW)/2 (also < TH_HIGH)
-    const int bestIdxR = (int)(best & 0xFFF);
     // SAD refinement on the unblurred level kpL.octave
     const LevelGeom& Lv = G->lv[levelL];
-    const float uR0 = kR[bestIdxR].x;
+    const int owner = __builtin_ctzll(__ballot(best == wbest));
+    const float uR0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bestX), owner));
     const float sf = A.inv_scale[levelL];
     const float scaleduL = __builtin_roundf(kp.x * sf);
     const float scaledvL = __builtin_roundf(kp.y * sf);

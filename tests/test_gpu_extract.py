@@ -92,13 +92,14 @@ def test_extract_bitexact(gpu, name, seed, w, h, nf):
     assert lv.sum() == len(kps)
 
 
-@pytest.mark.parametrize("seed", [10, 11])
-def test_extract_stress_noise(gpu, seed):
-    """i.i.d. uniform noise: dense FAST responses, heavy octree phase 2."""
-    img = _image(seed, 640, 480, stress=True)
-    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+@pytest.mark.parametrize("seed,w,h,nf", [(10, 640, 480, 1000), (11, 640, 480, 1000), (12, 1241, 376, 2000)])
+def test_extract_stress_noise(gpu, seed, w, h, nf):
+    """i.i.d. uniform noise: dense FAST responses, heavy octree phase 2; levels 0-2 hold more
+    candidates than k_octree keeps in LDS (Geometry::oct_kcap), so the global spill path runs."""
+    img = _image(seed, w, h, stress=True)
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
     kps, desc = ex(img)
-    ref = oracle.extract(oracle.params(1000, 1.2, 8, 20, 7), img)
+    ref = oracle.extract(oracle.params(nf, 1.2, 8, 20, 7), img)
     assert np.array_equal(kps.view(np.uint8), ref.keypoints.view(np.uint8))
     assert np.array_equal(desc, ref.descriptors)
 
