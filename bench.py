@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=3, help="config-5 batches per rank (0: skip)")
+    ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r02_sq_counters.json"),
+                    help="SQ counter summary (tools/pmc_kernel.sh + tools/sq_summary.py) for issue fractions")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/profile.sh + tools/parse_prof.py); null if absent")
     return ap.parse_args()
@@ -427,6 +429,15 @@ def main():
             traffic_src = dict(file=os.path.relpath(args.traffic, ROOT), head=tj.get("head"), batch=tj.get("batch"))
         except Exception:
             traffic_all = {}
+    # issue fractions of the same kernels from the committed SQ counter profile (PMC cannot run live)
+    sq_all, sq_src = {}, None
+    if os.path.exists(args.sq):
+        try:
+            sj = json.load(open(args.sq))
+            sq_all = sj.get("kernels", {})
+            sq_src = os.path.relpath(args.sq, ROOT)
+        except Exception:
+            sq_all = {}
     roofline = None
     if dom:
         ms_tot, nl = stages[dom]
@@ -437,6 +448,10 @@ def main():
                         frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic_all.get(dom),
                         traffic_source=traffic_src,
                         algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4))
+        if dom in sq_all:
+            roofline.update(valu_issue_frac=sq_all[dom].get("valu_issue_frac"),
+                            salu_issue_frac=sq_all[dom].get("salu_issue_frac"),
+                            wait_over_active=sq_all[dom].get("wait_over_active"), sq_source=sq_src)
 
     # every stage against the same HBM roofline (algorithmic bytes / average launch time)
     stage_hbm = {}
@@ -445,7 +460,8 @@ def main():
         if nb:
             gbs = nb / (ms_tot / nl / 1e3) / 1e9
             stage_hbm[k] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                            "traffic_per_launch": traffic_all.get(k), "algorithmic_per_launch": int(nb)}
+                            "traffic_per_launch": traffic_all.get(k), "algorithmic_per_launch": int(nb),
+                            "valu_issue_frac": sq_all.get(k, {}).get("valu_issue_frac")}
 
     value = odist.job_throughput(B, args.steps, world, elapsed)
     info, cpus = host_info()
