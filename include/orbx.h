@@ -300,6 +300,31 @@ int32_t orbx_rand_next(orbx_rand_state* s);
 orbx_status orbx_pnp_iterate_stream(orbx_pnp* h, int n_iterations, orbx_rand_state* rng, int* no_more,
                                     float Tcw[16], uint8_t* inliers, int* n_inliers, int* found);
 
+/* Several solvers per call.  Per solver: */
+typedef struct {
+  int no_more;    /* bNoMore */
+  int found;      /* a pose was returned */
+  int n_inliers;  /* nInliers */
+  int used;       /* rand() values this call drew for the solver */
+  float Tcw[16];  /* row-major 4x4 when found */
+} orbx_pnp_result;
+/* Tracking::Relocalization's candidate loop (src/Tracking.cc:1738-1757): iterate(n_iterations)
+ * on solvers[0], solvers[1], ... in order, all drawing from the one stream *rng, stopping after
+ * the first solver that returns a pose (*stopped = its index, n when none did).  Exactly the
+ * calls the reference makes, so the solvers' state and *rng advance as they would; solvers
+ * after *stopped are untouched (their results zeroed).  One hypothesis launch and one check
+ * launch span all solvers (a solver that returns no pose consumes all of its iterations, so
+ * where each one starts in the stream is known up front).  inliers[s] (may be NULL, or any
+ * entry NULL): solvers[s]->n bytes, written when results[s].found.  Same device for all. */
+orbx_status orbx_pnp_iterate_candidates(orbx_pnp* const* solvers, int n, int n_iterations, orbx_rand_state* rng,
+                                        orbx_pnp_result* results, uint8_t* const* inliers, int* stopped);
+/* Independent solvers, each with its own rand() stream rngs[s] (distinct pointers), e.g. one
+ * relocalising frame per sequence of a multi-sequence batch: iterate(n_iterations) on every
+ * solver, results as above; hypotheses, inlier checks and Refine() calls of all solvers are
+ * batched into shared launches. */
+orbx_status orbx_pnp_iterate_many(orbx_pnp* const* solvers, int n, int n_iterations, orbx_rand_state* const* rngs,
+                                  orbx_pnp_result* results, uint8_t* const* inliers);
+
 /* ORBmatcher::SearchByProjection -- the three overloads run on every tracked
  * frame -- with Frame::AssignFeaturesToGrid / GetFeaturesInArea
  * (src/Frame.cc:254-271, 388-453) and, for the local map, Frame::isInFrustum

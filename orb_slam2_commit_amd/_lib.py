@@ -119,6 +119,11 @@ class RandState(C.Structure):
     _fields_ = [("r", C.c_uint32 * 34), ("i", C.c_int32)]
 
 
+class PnpResult(C.Structure):
+    _fields_ = [("no_more", C.c_int), ("found", C.c_int), ("n_inliers", C.c_int), ("used", C.c_int),
+                ("Tcw", C.c_float * 16)]
+
+
 # Every entry point of include/orbx.h with its ctypes signature.
 P = C.c_void_p
 SIGNATURES = {
@@ -160,6 +165,8 @@ SIGNATURES = {
     "orbx_distinctive_descriptors_device": ([P, P, C.c_int, P, P, P], C.c_int),
     "orbx_undistort_keypoints": ([P, C.c_int, C.POINTER(Camera), P, C.c_int], C.c_int),
     "orbx_undistort_keypoints_device": ([P, P, C.c_int, C.c_int, P, P, P], C.c_int),
+    "orbx_pnp_iterate_candidates": ([P, C.c_int, C.c_int, C.POINTER(RandState), P, P, C.POINTER(C.c_int)], C.c_int),
+    "orbx_pnp_iterate_many": ([P, C.c_int, C.c_int, P, P, P], C.c_int),
     "orbx_rand_seed":([C.POINTER(RandState), C.c_uint32], None),
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),

@@ -1049,8 +1049,8 @@ __device__ __forceinline__ void ldlt_col_step(double* Lc, double* rinv, double (
   __syncthreads();
 }
 
-template <int TPT>
-__global__ __launch_bounds__(1024) void k_ba_ldlt_col(BaDev D) {
+template <int TPT, int NT>
+__global__ __launch_bounds__(NT) void k_ba_ldlt_col(BaDev D) {
   extern __shared__ __attribute__((aligned(16))) double Lc[];
   __shared__ int fail;
   const int N = 6 * D.nposes, tid = threadIdx.x;
@@ -1062,7 +1062,7 @@ __global__ __launch_bounds__(1024) void k_ba_ldlt_col(BaDev D) {
   if (tid == 0) fail = 0;
 #pragma unroll
   for (int t = 0; t < TPT; t++) {
-    int x = tid + 1024 * t, k = 0;
+    int x = tid + NT * t, k = 0;
     ti[t] = 0;
     tk[t] = -1;  // inactive
     if (x < ntiles) {
@@ -1150,14 +1150,23 @@ __global__ __launch_bounds__(1024) void k_ba_ldlt_col(BaDev D) {
 // Launch plan for the reduced system: the column-step kernel while the
 // packed factor fits LDS, else the 16-wide blocked kernel (LDS or global).
 struct LdltPlan {
-  int N = 0, tpt = 0;
+  int N = 0, tpt = 0, nt = 1024;
   bool col = false, in_lds = false;
   size_t smem = 0;
   hipError_t prepare(int n) {
     N = n;
     col = ldlt_col_fits(N) && !std::getenv("ORBX_LDLT_BLOCKED");
     if (col) {
-      tpt = ldlt_col_tiles(N) <= 1024 ? 1 : 2;
+      const char* e = std::getenv("ORBX_LDLT_NT");  // A/B: threads of the column-step kernel
+      nt = e ? std::atoi(e) : 1024;
+      if (nt != 256 && nt != 512) nt = 1024;
+      const int tiles = ldlt_col_tiles(N);
+      tpt = (tiles + nt - 1) / nt;
+      if (tpt > 8 || (nt == 1024 && tpt > 2) || (nt == 512 && tpt > 4)) {
+        nt = 1024;
+        tpt = tiles <= 1024 ? 1 : 2;
+      }
+      tpt = tpt <= 1 ? 1 : tpt <= 2 ? 2 : tpt <= 4 ? 4 : 8;
       smem = ldlt_col_smem(N);
     } else {
       in_lds = ldlt_np(N) <= kLdltLdsNp;
@@ -1166,13 +1175,20 @@ struct LdltPlan {
     return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   }
   const void* kernel_ptr() const {
-    if (col) return tpt == 1 ? (const void*)k_ba_ldlt_col<1> : (const void*)k_ba_ldlt_col<2>;
+    if (col) {
+      if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col<1, 1024> : (const void*)k_ba_ldlt_col<2, 1024>;
+      if (nt == 512)
+        return tpt == 1 ? (const void*)k_ba_ldlt_col<1, 512>
+                        : tpt == 2 ? (const void*)k_ba_ldlt_col<2, 512> : (const void*)k_ba_ldlt_col<4, 512>;
+      return tpt <= 2 ? (const void*)k_ba_ldlt_col<2, 256>
+                      : tpt == 4 ? (const void*)k_ba_ldlt_col<4, 256> : (const void*)k_ba_ldlt_col<8, 256>;
+    }
     return in_lds ? (const void*)k_ba_ldlt<true> : (const void*)k_ba_ldlt<false>;
   }
   void launch(const BaDev& D, hipStream_t st, int stage_limit = 99) const {
     if (col) {
-      if (tpt == 1) hipLaunchKernelGGL(k_ba_ldlt_col<1>, dim3(1), dim3(1024), smem, st, D);
-      else hipLaunchKernelGGL(k_ba_ldlt_col<2>, dim3(1), dim3(1024), smem, st, D);
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(BaDev)>(const_cast<void*>(kernel_ptr())), dim3(1), dim3(nt),
+                         smem, st, D);
     } else if (in_lds) {
       hipLaunchKernelGGL(k_ba_ldlt<true>, dim3(1), dim3(1024), smem, st, D, stage_limit);
     } else {

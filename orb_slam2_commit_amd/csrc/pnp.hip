@@ -824,15 +824,14 @@ constexpr int kRefThreads = 256;
 constexpr int kRefineLdsPts = 2000;  // Refine stages up to this many inliers in LDS
 constexpr size_t kRefinePtBytes = 4 * 8 + 3 * 8 + 3 * 4 + 2 * 4;  // alphas, pcs/errors, pw, uv
 
-// One 64-thread block per hypothesis: its minimal set staged in LDS, EPnP,
-// pose record R (9, row-major) + t (3).
-__global__ __launch_bounds__(kHypThreads) void k_pnp_hyp(PnpIn in, const int* __restrict__ sets, int set_size,
-                                                         double* __restrict__ poses) {
+// One block per hypothesis: its minimal set staged in LDS, EPnP, pose record
+// R (9, row-major) + t (3).
+__device__ __forceinline__ void pnp_hyp_body(const PnpIn& in, const int* __restrict__ idx, int set_size,
+                                             double* __restrict__ pose) {
   __shared__ EpnpSmall S;
   __shared__ float spw[3 * kPnpMaxSet], suv[2 * kPnpMaxSet];
   __shared__ double salpha[4 * kPnpMaxSet], stmp[3 * kPnpMaxSet];
-  const int h = blockIdx.x, tid = threadIdx.x;
-  const int* idx = sets + (size_t)h * set_size;
+  const int tid = threadIdx.x;
   if (tid < set_size) {
     const int i = idx[tid];
 #pragma unroll
@@ -844,20 +843,24 @@ __global__ __launch_bounds__(kHypThreads) void k_pnp_hyp(PnpIn in, const int* __
   epnp_compute_pose<kHypThreads>(in, EpnpPts{spw, suv, salpha, stmp}, set_size, &S);
   if (tid < 12) {
     const int b = (int)S.rep[0];
-    poses[12 * (size_t)h + tid] = tid < 9 ? S.Rs[b][tid / 3][tid % 3] : S.ts[b][tid - 9];
+    pose[tid] = tid < 9 ? S.Rs[b][tid / 3][tid % 3] : S.ts[b][tid - 9];
   }
 }
 
-__global__ __launch_bounds__(256) void k_pnp_check(PnpIn in, const double* __restrict__ poses,
-                                                   uint8_t* __restrict__ masks, int* __restrict__ counts) {
-  __shared__ int red[4];
+__global__ __launch_bounds__(kHypThreads) void k_pnp_hyp(PnpIn in, const int* __restrict__ sets, int set_size,
+                                                         double* __restrict__ poses) {
   const int h = blockIdx.x;
-  const double* P = poses + 12 * (size_t)h;
+  pnp_hyp_body(in, sets + (size_t)h * set_size, set_size, poses + 12 * (size_t)h);
+}
+
+// CheckInliers (src/PnPsolver.cc:352-384) of one hypothesis -> mask + count.
+__device__ __forceinline__ void pnp_check_body(const PnpIn& in, const double* __restrict__ P,
+                                               uint8_t* __restrict__ m, int* __restrict__ count) {
+  __shared__ int red[4];
   double R[9], t[3];
   for (int i = 0; i < 9; i++) R[i] = P[i];
   for (int i = 0; i < 3; i++) t[i] = P[9 + i];
   int c = 0;
-  uint8_t* m = masks + (size_t)h * in.N;
   for (int i = threadIdx.x; i < in.N; i += 256) {
     const bool ok = check_inlier(in, R, t, i);
     m[i] = ok;
@@ -866,28 +869,68 @@ __global__ __launch_bounds__(256) void k_pnp_check(PnpIn in, const double* __res
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) counts[h] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) *count = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void k_pnp_check(PnpIn in, const double* __restrict__ poses,
+                                                   uint8_t* __restrict__ masks, int* __restrict__ counts) {
+  const int h = blockIdx.x;
+  pnp_check_body(in, poses + 12 * (size_t)h, masks + (size_t)h * in.N, counts + h);
+}
+
+// Many solvers in one launch (orbx_pnp_iterate_candidates / _many): grid (hypotheses
+// of the largest job, jobs); job j runs its hypotheses h0 .. h0+H-1 (their minimal
+// sets at sets[(h0 + h) * set_size], results at index h0 + h of its own arrays).
+struct PnpHypJob {
+  PnpIn in;
+  const int* sets;
+  double* poses;
+  uint8_t* masks;
+  int* counts;
+  int h0, H, set_size;
+};
+
+__global__ __launch_bounds__(kHypThreads) void k_pnp_hyp_many(const PnpHypJob* __restrict__ jobs) {
+  const PnpHypJob& J = jobs[blockIdx.y];
+  if ((int)blockIdx.x >= J.H) return;  // block-uniform
+  const int h = J.h0 + blockIdx.x;
+  pnp_hyp_body(J.in, J.sets + (size_t)h * J.set_size, J.set_size, J.poses + 12 * (size_t)h);
+}
+
+__global__ __launch_bounds__(256) void k_pnp_check_many(const PnpHypJob* __restrict__ jobs) {
+  const PnpHypJob& J = jobs[blockIdx.y];
+  if ((int)blockIdx.x >= J.H) return;
+  const int h = J.h0 + blockIdx.x;
+  pnp_check_body(J.in, J.poses + 12 * (size_t)h, J.masks + (size_t)h * J.in.N, J.counts + h);
 }
 
 // Refine(): EPnP on the inliers of `best` (ascending index), then CheckInliers.
 // The inliers are compacted in order and staged in LDS (dynamic: kLds, up to
 // kRefineLdsPts) or in the global work buffer.  out: [0..8] R, [9..11] t;
 // *count; mask_out.
+struct PnpRefJob {
+  PnpIn in;
+  const uint8_t* best;
+  int* idx;
+  double* work;
+  double* out;
+  uint8_t* mask_out;
+  int* count;
+};
+
 template <bool kLds>
-__global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint8_t* __restrict__ best,
-                                                            int* __restrict__ idx, double* __restrict__ work,
-                                                            double* __restrict__ out, uint8_t* __restrict__ mask_out,
-                                                            int* __restrict__ count) {
+__device__ __forceinline__ void pnp_refine_body(const PnpRefJob& J) {
   __shared__ EpnpSmall S;
   __shared__ int wsum[4], base;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
+  const PnpIn& in = J.in;
   const int tid = threadIdx.x;
   // ordered compaction of the best inlier set
   if (tid == 0) base = 0;
   __syncthreads();
   for (int i0 = 0; i0 < in.N; i0 += 256) {
     const int i = i0 + tid;
-    const int f = (i < in.N && best[i]) ? 1 : 0;
+    const int f = (i < in.N && J.best[i]) ? 1 : 0;
     const unsigned long long bal = __ballot(f);
     const int lane = tid & 63, wv = tid >> 6;
     const int pre = __popcll(bal & ((1ull << lane) - 1));
@@ -895,19 +938,19 @@ __global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint
     __syncthreads();
     int off = base;
     for (int w = 0; w < wv; w++) off += wsum[w];
-    if (f) idx[off + pre] = i;
+    if (f) J.idx[off + pre] = i;
     __syncthreads();
     if (tid == 0) base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
   }
   const int n = base;
   const int cap = kLds ? kRefineLdsPts : in.N;
-  double* alphas = kLds ? dyn : work;
+  double* alphas = kLds ? dyn : J.work;
   double* tmp = alphas + 4 * (size_t)cap;
   float* spw = reinterpret_cast<float*>(tmp + 3 * (size_t)cap);
   float* suv = spw + 3 * (size_t)cap;
   for (int k = tid; k < n; k += kRefThreads) {
-    const int i = idx[k];
+    const int i = J.idx[k];
 #pragma unroll
     for (int j = 0; j < 3; j++) spw[3 * k + j] = in.p3d[3 * i + j];
     suv[2 * k] = in.p2d[2 * i];
@@ -924,7 +967,7 @@ __global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint
   int c = 0;
   for (int i = tid; i < in.N; i += kRefThreads) {
     const bool ok = check_inlier(in, R, t, i);
-    mask_out[i] = ok;
+    J.mask_out[i] = ok;
     c += ok;
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
@@ -932,10 +975,24 @@ __global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint
   if ((tid & 63) == 0) wsum[tid >> 6] = c;
   __syncthreads();
   if (tid == 0) {
-    *count = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    for (int i = 0; i < 9; i++) out[i] = R[i];
-    for (int i = 0; i < 3; i++) out[9 + i] = t[i];
+    *J.count = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    for (int i = 0; i < 9; i++) J.out[i] = R[i];
+    for (int i = 0; i < 3; i++) J.out[9 + i] = t[i];
   }
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint8_t* __restrict__ best,
+                                                            int* __restrict__ idx, double* __restrict__ work,
+                                                            double* __restrict__ out, uint8_t* __restrict__ mask_out,
+                                                            int* __restrict__ count) {
+  pnp_refine_body<kLds>(PnpRefJob{in, best, idx, work, out, mask_out, count});
+}
+
+// one block per job
+template <bool kLds>
+__global__ __launch_bounds__(kRefThreads) void k_pnp_refine_many(const PnpRefJob* __restrict__ jobs) {
+  pnp_refine_body<kLds>(jobs[blockIdx.x]);
 }
 
 }  // namespace orbx
@@ -954,6 +1011,17 @@ struct PnpDevice {
   std::mutex mu;  // serialises iterate() calls that share the stream and readback block
   void* pinned = nullptr;
   size_t pinned_cap = 0;
+  void* dstage = nullptr;  // device staging of the batched calls: job records, minimal sets, counts
+  size_t dstage_cap = 0;
+  hipError_t dstage_reserve(size_t bytes) {
+    if (bytes <= dstage_cap) return hipSuccess;
+    if (dstage) (void)hipFree(dstage);
+    dstage = nullptr;
+    dstage_cap = 0;
+    hipError_t e = hipMalloc(&dstage, bytes);
+    if (e == hipSuccess) dstage_cap = bytes;
+    return e;
+  }
   hipError_t pinned_reserve(size_t bytes) {
     if (bytes <= pinned_cap) return hipSuccess;
     if (pinned) (void)hipHostFree(pinned);
@@ -972,6 +1040,10 @@ hipError_t pnp_device_init(int device) {
     d.init_err = hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking);
     if (d.init_err == hipSuccess)
       d.init_err = hipFuncSetAttribute((const void*)orbx::k_pnp_refine<true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(orbx::kRefineLdsPts * orbx::kRefinePtBytes));
+    if (d.init_err == hipSuccess)
+      d.init_err = hipFuncSetAttribute((const void*)orbx::k_pnp_refine_many<true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)(orbx::kRefineLdsPts * orbx::kRefinePtBytes));
     if (d.init_err == hipSuccess) d.init_err = d.pinned_reserve(1 << 16);
@@ -1032,6 +1104,24 @@ struct orbx_pnp {
     d_masks = take((size_t)cap * nn);
     d_counts = (int*)take(sizeof(int) * (size_t)cap);
     return o;
+  }
+  // grows the per-hypothesis buffers to H, keeping correspondences, best mask and results
+  hipError_t ensure_cap(int H) {
+    if (H <= cap_hyp) return hipSuccess;
+    uint8_t* old = d_mem;
+    const size_t keep = (uint8_t*)d_best - (uint8_t*)d_p3d;
+    const size_t best_off = (uint8_t*)d_best - old, res_off = (uint8_t*)d_res - old;
+    d_mem = nullptr;
+    const size_t bytes = layout(H, nullptr);
+    hipError_t e = hipMallocAsync((void**)&d_mem, bytes, st);
+    if (e != hipSuccess) return e;
+    layout(H, d_mem);
+    cap_hyp = H;
+    if ((e = hipMemcpyAsync(d_p3d, old, keep, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(d_best, old + best_off, std::max(N, 1), hipMemcpyDeviceToDevice, st)) != hipSuccess)
+      return e;
+    if ((e = hipMemcpyAsync(d_res, old + res_off, 8 * 32, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+    return hipFreeAsync(old, st);
   }
   hipError_t alloc(int cap) {  // (re)allocates d_mem; the correspondences are re-uploaded by the caller
     if (d_mem) (void)hipFreeAsync(d_mem, st);
@@ -1160,20 +1250,7 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
   std::lock_guard<std::mutex> lock(dev.mu);
   const size_t pin_bytes = std::max(sizeof(int) * (size_t)H * ms, sizeof(int) * (size_t)H) + 8 * 32;
   PNP_CHECK(dev.pinned_reserve(pin_bytes));
-  if (H > h->cap_hyp) {  // keeps the correspondences: copy them over to the new block
-    uint8_t* old = h->d_mem;
-    const size_t keep = (uint8_t*)h->d_best - (uint8_t*)h->d_p3d;
-    const size_t best_off = (uint8_t*)h->d_best - old, res_off = (uint8_t*)h->d_res - old;
-    h->d_mem = nullptr;
-    const size_t bytes = h->layout(H, nullptr);
-    PNP_CHECK(hipMallocAsync((void**)&h->d_mem, bytes, h->st));
-    h->layout(H, h->d_mem);
-    h->cap_hyp = H;
-    PNP_CHECK(hipMemcpyAsync(h->d_p3d, old, keep, hipMemcpyDeviceToDevice, h->st));
-    PNP_CHECK(hipMemcpyAsync(h->d_best, old + best_off, std::max(N, 1), hipMemcpyDeviceToDevice, h->st));
-    PNP_CHECK(hipMemcpyAsync(h->d_res, old + res_off, 8 * 32, hipMemcpyDeviceToDevice, h->st));
-    PNP_CHECK(hipFreeAsync(old, h->st));
-  }
+  PNP_CHECK(h->ensure_cap(H));  // keeps the correspondences
   // DUtils::Random::RandomInt(0, size-1) on the rand() stream + swap-remove
   int* sets = (int*)dev.pinned;
   std::vector<int> avail(N);
@@ -1243,6 +1320,359 @@ orbx_status orbx_pnp_iterate(orbx_pnp* h, int n_iterations, const int32_t* rand_
       *n_inliers = h->best_inliers;
       *found = 1;
     }
+  }
+  return ORBX_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- many solvers
+// The walk of PnPsolver::iterate (the loop above) over several solvers at once.
+// Hypotheses are computed a chunk at a time for every solver that needs them
+// (one k_pnp_hyp_many + one k_pnp_check_many launch per round, minimal sets and
+// job records in one upload, counts in one readback), each solver's walk runs on
+// the host exactly as in orbx_pnp_iterate, and the Refine() calls the walks ask
+// for in the same round go out as one k_pnp_refine_many launch.
+namespace {
+
+struct PnpRun {
+  orbx_pnp* h = nullptr;
+  const int32_t* rv = nullptr;  // rand values this call may consume (H * min_set)
+  int H = 0;                    // hypotheses this call may run
+  int k = 0;                    // next hypothesis to walk
+  int launched = 0;             // hypotheses [0, launched) have counts
+  int cur = 0, used = 0;
+  bool eligible = true, done = false, pending = false;
+  std::vector<int> counts;
+  orbx_pnp_result* out = nullptr;
+  uint8_t* inliers = nullptr;
+};
+
+constexpr int kPnpFirstChunk = 16;  // RANSAC at ~60 % inliers usually stops within its first hypotheses
+
+orbx_status pnp_begin(PnpRun& r, int n_iterations) {
+  orbx_pnp* h = r.h;
+  r.out->no_more = r.out->found = r.out->n_inliers = r.out->used = 0;
+  if (h->N < h->min_inliers) {
+    r.out->no_more = 1;
+    r.done = true;
+    return ORBX_OK;
+  }
+  r.H = std::max(h->max_its - h->iterations, n_iterations);
+  if (r.H <= 0) {
+    r.H = 0;
+    r.done = true;
+    return ORBX_OK;
+  }
+  r.counts.assign(r.H, 0);
+  return h->ensure_cap(r.H) == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+}
+
+// hypotheses [launched, launched + c) of every run in `rs` with c > 0
+orbx_status pnp_launch_chunks(PnpDevice& dev, hipStream_t st, std::vector<std::pair<PnpRun*, int>>& rs) {
+  if (rs.empty()) return ORBX_OK;
+  const size_t nj = rs.size();
+  size_t nsets = 0, ncounts = 0;
+  int maxc = 0;
+  for (auto& q : rs) {
+    nsets += (size_t)q.second * q.first->h->min_set;
+    ncounts += q.second;
+    maxc = std::max(maxc, q.second);
+  }
+  const size_t off_sets = align256(nj * sizeof(orbx::PnpHypJob));
+  const size_t off_counts = off_sets + align256(nsets * sizeof(int));
+  const size_t bytes = off_counts + align256(ncounts * sizeof(int));
+  PNP_CHECK(dev.pinned_reserve(bytes));
+  PNP_CHECK(dev.dstage_reserve(bytes));
+  uint8_t* hp = (uint8_t*)dev.pinned;
+  uint8_t* dp = (uint8_t*)dev.dstage;
+  orbx::PnpHypJob* jobs = (orbx::PnpHypJob*)hp;
+  int* sets = (int*)(hp + off_sets);
+  size_t so = 0, co = 0;
+  for (size_t j = 0; j < nj; j++) {
+    PnpRun& r = *rs[j].first;
+    orbx_pnp* h = r.h;
+    const int c = rs[j].second, ms = h->min_set, N = h->N, h0 = r.launched;
+    // DUtils::Random::RandomInt(0, size-1) on the rand() stream + swap-remove (src/PnPsolver.cc:214-229)
+    std::vector<int> avail(N);
+    for (int k = 0; k < c; k++) {
+      for (int i = 0; i < N; i++) avail[i] = i;
+      int size = N;
+      for (int i = 0; i < ms; i++) {
+        const int32_t v = r.rv[(size_t)(h0 + k) * ms + i];
+        const int randi = (int)(((double)v / ((double)RAND_MAX + 1.0)) * size);
+        sets[so + (size_t)k * ms + i] = avail[randi];
+        avail[randi] = avail[size - 1];
+        size--;
+      }
+    }
+    orbx::PnpHypJob& J = jobs[j];
+    J.in = h->in();
+    J.sets = (const int*)(dp + off_sets) + so - (size_t)h0 * ms;  // indexed by absolute hypothesis
+    J.poses = h->d_poses;
+    J.masks = h->d_masks;
+    J.counts = (int*)(dp + off_counts) + co - h0;
+    J.h0 = h0;
+    J.H = c;
+    J.set_size = ms;
+    so += (size_t)c * ms;
+    co += c;
+  }
+  PNP_CHECK(hipMemcpyAsync(dp, hp, off_counts, hipMemcpyHostToDevice, st));
+  const orbx::PnpHypJob* dj = (const orbx::PnpHypJob*)dp;
+  hipLaunchKernelGGL(orbx::k_pnp_hyp_many, dim3(maxc, nj), dim3(orbx::kHypThreads), 0, st, dj);
+  hipLaunchKernelGGL(orbx::k_pnp_check_many, dim3(maxc, nj), dim3(256), 0, st, dj);
+  PNP_CHECK(hipGetLastError());
+  int* hc = (int*)(hp + off_counts);
+  PNP_CHECK(hipMemcpyAsync(hc, dp + off_counts, ncounts * sizeof(int), hipMemcpyDeviceToHost, st));
+  PNP_CHECK(hipStreamSynchronize(st));
+  co = 0;
+  for (auto& q : rs) {
+    PnpRun& r = *q.first;
+    for (int k = 0; k < q.second; k++) r.counts[r.launched + k] = hc[co + k];
+    co += q.second;
+    r.launched += q.second;
+  }
+  return ORBX_OK;
+}
+
+// the walk of orbx_pnp_iterate from hypothesis r.k: stops at a Refine() request,
+// at the end of the launched hypotheses, or at the end of the call
+orbx_status pnp_walk(PnpRun& r, hipStream_t st) {
+  orbx_pnp* h = r.h;
+  const int N = h->N;
+  while (!r.pending && r.k < r.launched) {
+    const int k = r.k++;
+    r.cur++;
+    h->iterations++;
+    r.used += h->min_set;
+    if (r.counts[k] < h->min_inliers) continue;
+    if (r.counts[k] > h->best_inliers) {  // new best: mask + pose stay on the device
+      h->best_inliers = r.counts[k];
+      PNP_CHECK(hipMemcpyAsync(h->d_best, h->d_masks + (size_t)k * N, N, hipMemcpyDeviceToDevice, st));
+      PNP_CHECK(hipMemcpyAsync(h->d_res + 16, h->d_poses + 12 * (size_t)k, 12 * sizeof(double),
+                               hipMemcpyDeviceToDevice, st));
+      h->refine_valid = false;
+    }
+    if (h->refine_valid) continue;  // same best set: Refine() fails again
+    r.pending = true;
+  }
+  return ORBX_OK;
+}
+
+// the end of iterate() once all H hypotheses were walked without a refined pose
+orbx_status pnp_finish(PnpRun& r, hipStream_t st, std::vector<double>& pose_scratch) {
+  orbx_pnp* h = r.h;
+  r.done = true;
+  if (h->iterations >= h->max_its) {
+    r.out->no_more = 1;
+    if (h->best_inliers >= h->min_inliers) {
+      PNP_CHECK(hipMemcpyAsync(pose_scratch.data(), h->d_res + 16, 12 * sizeof(double), hipMemcpyDeviceToHost, st));
+      if (r.inliers) PNP_CHECK(hipMemcpyAsync(r.inliers, h->d_best, h->N, hipMemcpyDeviceToHost, st));
+      PNP_CHECK(hipStreamSynchronize(st));
+      pose_to_Tcw(pose_scratch.data(), h->best_Tcw);
+      std::memcpy(r.out->Tcw, h->best_Tcw, sizeof(float) * 16);
+      r.out->n_inliers = h->best_inliers;
+      r.out->found = 1;
+    }
+  }
+  return ORBX_OK;
+}
+
+orbx_status pnp_refine_round(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*>& pend) {
+  if (pend.empty()) return ORBX_OK;
+  const size_t nj = pend.size();
+  const size_t off_res = align256(nj * sizeof(orbx::PnpRefJob));
+  const size_t bytes = off_res + nj * 16 * sizeof(double);
+  PNP_CHECK(dev.pinned_reserve(bytes));
+  PNP_CHECK(dev.dstage_reserve(bytes));
+  uint8_t* hp = (uint8_t*)dev.pinned;
+  uint8_t* dp = (uint8_t*)dev.dstage;
+  orbx::PnpRefJob* jobs = (orbx::PnpRefJob*)hp;
+  // LDS-staged jobs first, then the (rare) jobs whose best set exceeds the LDS stage
+  std::vector<PnpRun*> order;
+  for (PnpRun* r : pend)
+    if (r->h->best_inliers <= orbx::kRefineLdsPts) order.push_back(r);
+  const int n_lds = (int)order.size();
+  for (PnpRun* r : pend)
+    if (r->h->best_inliers > orbx::kRefineLdsPts) order.push_back(r);
+  for (size_t j = 0; j < nj; j++) {
+    orbx_pnp* h = order[j]->h;
+    jobs[j] = orbx::PnpRefJob{h->in(), h->d_best, h->d_idx, h->d_rwork, h->d_res, h->d_refmask,
+                              (int*)(h->d_res + 12)};
+  }
+  PNP_CHECK(hipMemcpyAsync(dp, hp, nj * sizeof(orbx::PnpRefJob), hipMemcpyHostToDevice, st));
+  const orbx::PnpRefJob* dj = (const orbx::PnpRefJob*)dp;
+  if (n_lds > 0)
+    hipLaunchKernelGGL(orbx::k_pnp_refine_many<true>, dim3(n_lds), dim3(orbx::kRefThreads),
+                       orbx::kRefineLdsPts * orbx::kRefinePtBytes, st, dj);
+  if ((int)nj > n_lds)
+    hipLaunchKernelGGL(orbx::k_pnp_refine_many<false>, dim3((int)nj - n_lds), dim3(orbx::kRefThreads), 0, st,
+                       dj + n_lds);
+  PNP_CHECK(hipGetLastError());
+  double* res = (double*)(hp + off_res);
+  for (size_t j = 0; j < nj; j++)
+    PNP_CHECK(hipMemcpyAsync(res + 16 * j, order[j]->h->d_res, 13 * sizeof(double), hipMemcpyDeviceToHost, st));
+  PNP_CHECK(hipStreamSynchronize(st));
+  for (size_t j = 0; j < nj; j++) {
+    PnpRun& r = *order[j];
+    orbx_pnp* h = r.h;
+    r.pending = false;
+    const int rc = *(const int*)(res + 16 * j + 12);
+    if (rc > h->min_inliers) {  // Refine() succeeded: the call returns mRefinedTcw
+      if (r.inliers) PNP_CHECK(hipMemcpyAsync(r.inliers, h->d_refmask, h->N, hipMemcpyDeviceToHost, st));
+      pose_to_Tcw(res + 16 * j, r.out->Tcw);
+      r.out->n_inliers = rc;
+      r.out->found = 1;
+      r.done = true;
+    } else {
+      h->refine_valid = true;
+    }
+  }
+  PNP_CHECK(hipStreamSynchronize(st));
+  return ORBX_OK;
+}
+
+// shared: all runs draw from one stream in order and the call stops at the first run
+// that returns a pose (Tracking::Relocalization's candidate loop); otherwise the runs
+// are independent and all of them complete.
+orbx_status pnp_run_many(std::vector<PnpRun>& runs, bool shared, int* stopped) {
+  if (runs.empty()) return ORBX_OK;
+  const int device = runs[0].h->device;
+  PnpDevice& dev = g_pnp_dev[device];
+  hipStream_t st = dev.st;
+  std::vector<double> pose_scratch(16);
+  const int nr = (int)runs.size();
+  int active = 0;  // shared mode: the run whose walk is committed
+  bool first_round = true;
+  if (stopped) *stopped = nr;
+  while (true) {
+    if (shared) {
+      while (active < nr && runs[active].done) {
+        if (runs[active].out->found) break;
+        active++;
+      }
+      if (active >= nr || runs[active].out->found) {
+        if (stopped && active < nr) *stopped = active;
+        break;
+      }
+    }
+    // 1. hypotheses: every eligible run whose walk reached the end of its launched ones
+    std::vector<std::pair<PnpRun*, int>> chunk;
+    for (int i = 0; i < nr; i++) {
+      PnpRun& r = runs[i];
+      const bool eligible = shared ? (first_round || i == active) : true;
+      if (!eligible || r.done || r.pending || r.k < r.launched || r.launched >= r.H) continue;
+      const int c = std::min(r.H - r.launched, std::max(kPnpFirstChunk, r.launched));  // 16, 16, 32, 64, ...
+      chunk.push_back({&r, c});
+    }
+    first_round = false;
+    orbx_status s = pnp_launch_chunks(dev, st, chunk);
+    if (s != ORBX_OK) return s;
+    // 2. walks (shared: only the committed run)
+    std::vector<PnpRun*> pend;
+    for (int i = 0; i < nr; i++) {
+      PnpRun& r = runs[i];
+      if (r.done || (shared && i != active)) continue;
+      if ((s = pnp_walk(r, st)) != ORBX_OK) return s;
+      if (r.pending)
+        pend.push_back(&r);
+      else if (r.k >= r.H && (s = pnp_finish(r, st, pose_scratch)) != ORBX_OK)
+        return s;
+    }
+    // 3. the Refine() calls of this round
+    if ((s = pnp_refine_round(dev, st, pend)) != ORBX_OK) return s;
+    for (PnpRun* r : pend)
+      if (!r->done && r->k >= r->H && (s = pnp_finish(*r, st, pose_scratch)) != ORBX_OK) return s;
+    bool all_done = true;
+    for (int i = 0; i < nr; i++) all_done = all_done && runs[i].done;
+    if (!shared && all_done) break;
+    if (shared && all_done) {
+      // fall through to the stop scan at the top
+    }
+  }
+  return ORBX_OK;
+}
+
+orbx_status pnp_check_solvers(orbx_pnp* const* solvers, int n, const orbx_pnp_result* results) {
+  if (n < 0 || (n > 0 && (!solvers || !results))) return ORBX_ERR_ARG;
+  for (int i = 0; i < n; i++) {
+    if (!solvers[i]) return ORBX_ERR_ARG;
+    if (solvers[i]->device != solvers[0]->device) return ORBX_ERR_ARG;
+    for (int j = 0; j < i; j++)
+      if (solvers[j] == solvers[i]) return ORBX_ERR_ARG;  // one walk per solver and call
+  }
+  return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+orbx_status orbx_pnp_iterate_candidates(orbx_pnp* const* solvers, int n, int n_iterations, orbx_rand_state* rng,
+                                        orbx_pnp_result* results, uint8_t* const* inliers, int* stopped) {
+  orbx_status s = pnp_check_solvers(solvers, n, results);
+  if (s != ORBX_OK || !rng || !stopped) return s != ORBX_OK ? s : ORBX_ERR_ARG;
+  *stopped = n;
+  if (n == 0) return ORBX_OK;
+  if (hipSetDevice(solvers[0]->device) != hipSuccess) return ORBX_ERR_HIP;
+  std::lock_guard<std::mutex> lock(g_pnp_dev[solvers[0]->device].mu);
+  std::vector<PnpRun> runs(n);
+  size_t total = 0;
+  for (int i = 0; i < n; i++) {
+    runs[i].h = solvers[i];
+    runs[i].out = &results[i];
+    runs[i].inliers = inliers ? inliers[i] : nullptr;
+    if ((s = pnp_begin(runs[i], n_iterations)) != ORBX_OK) return s;
+    total += (size_t)runs[i].H * solvers[i]->min_set;
+  }
+  // run i draws from where run i-1 would end without a pose (all of its hypotheses)
+  orbx_rand_state peek = *rng;
+  std::vector<int32_t> vals(std::max(total, (size_t)1));
+  for (size_t k = 0; k < total; k++) vals[k] = orbx_rand_next(&peek);
+  size_t o = 0;
+  for (int i = 0; i < n; i++) {
+    runs[i].rv = vals.data() + o;
+    o += (size_t)runs[i].H * solvers[i]->min_set;
+  }
+  if ((s = pnp_run_many(runs, true, stopped)) != ORBX_OK) return s;
+  for (int i = 0; i < n; i++) results[i].used = runs[i].used;
+  size_t used = 0;
+  for (int i = 0; i < n && i <= *stopped; i++) used += runs[i].used;
+  for (size_t k = 0; k < used; k++) (void)orbx_rand_next(rng);
+  return ORBX_OK;
+}
+
+orbx_status orbx_pnp_iterate_many(orbx_pnp* const* solvers, int n, int n_iterations, orbx_rand_state* const* rngs,
+                                  orbx_pnp_result* results, uint8_t* const* inliers) {
+  orbx_status s = pnp_check_solvers(solvers, n, results);
+  if (s != ORBX_OK) return s;
+  if (n == 0) return ORBX_OK;
+  if (!rngs) return ORBX_ERR_ARG;
+  for (int i = 0; i < n; i++) {
+    if (!rngs[i]) return ORBX_ERR_ARG;
+    for (int j = 0; j < i; j++)
+      if (rngs[j] == rngs[i]) return ORBX_ERR_ARG;  // independent streams only (shared: _candidates)
+  }
+  if (hipSetDevice(solvers[0]->device) != hipSuccess) return ORBX_ERR_HIP;
+  std::lock_guard<std::mutex> lock(g_pnp_dev[solvers[0]->device].mu);
+  std::vector<PnpRun> runs(n);
+  std::vector<std::vector<int32_t>> vals(n);
+  for (int i = 0; i < n; i++) {
+    runs[i].h = solvers[i];
+    runs[i].out = &results[i];
+    runs[i].inliers = inliers ? inliers[i] : nullptr;
+    if ((s = pnp_begin(runs[i], n_iterations)) != ORBX_OK) return s;
+    const size_t need = (size_t)runs[i].H * solvers[i]->min_set;
+    orbx_rand_state peek = *rngs[i];
+    vals[i].resize(std::max(need, (size_t)1));
+    for (size_t k = 0; k < need; k++) vals[i][k] = orbx_rand_next(&peek);
+    runs[i].rv = vals[i].data();
+  }
+  if ((s = pnp_run_many(runs, false, nullptr)) != ORBX_OK) return s;
+  for (int i = 0; i < n; i++) {
+    results[i].used = runs[i].used;
+    for (int k = 0; k < runs[i].used; k++) (void)orbx_rand_next(rngs[i]);
   }
   return ORBX_OK;
 }

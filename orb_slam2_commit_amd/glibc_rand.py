@@ -57,3 +57,10 @@ class GlibcRand:
     def advance(self, n):
         for _ in range(n):
             self._next_word()
+
+    def state_words(self):
+        """The 34 most recent words, oldest first (orbx_rand_state.r with i = 34)."""
+        return list(self._r[-34:])
+
+    def set_state_words(self, words):
+        self._r = [int(w) & 0xFFFFFFFF for w in words][-34:]

@@ -594,6 +594,63 @@ class PnPsolver:
         return (T.reshape(4, 4) if found.value else None), bool(nm.value), inl[:self.n].astype(bool), ni.value
 
 
+def _rand_state(rng):
+    st = _lib.RandState()
+    w = rng.state_words()
+    for k in range(34):
+        st.r[k] = w[k]
+    st.i = 34
+    return st
+
+
+def _rand_restore(rng, st):
+    i = st.i
+    rng.set_state_words([st.r[(i - 34 + k) % 34] for k in range(34)])
+
+
+def _pnp_outputs(solvers, res, inl):
+    out = []
+    for s, r, b in zip(solvers, res, inl):
+        s._done += r.used // s.min_set
+        T = np.ctypeslib.as_array(r.Tcw).reshape(4, 4).copy() if r.found else None
+        out.append((T, bool(r.no_more), b[:s.n].astype(bool), int(r.n_inliers)))
+    return out
+
+
+def pnp_iterate_candidates(solvers, nIterations, rng):
+    """Tracking::Relocalization's candidate loop (src/Tracking.cc:1738-1757) in one call:
+    solvers[0].iterate(n), solvers[1].iterate(n), ... on the shared stream `rng` (GlibcRand),
+    stopping after the first that returns a pose.  Returns (stopped, [(Tcw|None, bNoMore,
+    vbInliers, nInliers)] for solvers[0..stopped]); rng advances by exactly what was drawn."""
+    n = len(solvers)
+    hs = (C.c_void_p * max(n, 1))(*[s._h for s in solvers])
+    res = (_lib.PnpResult * max(n, 1))()
+    inl = [np.zeros(max(s.n, 1), np.uint8) for s in solvers]
+    ip = (C.c_void_p * max(n, 1))(*[ptr(b) for b in inl])
+    st = _rand_state(rng)
+    stopped = C.c_int()
+    check(_lib.lib().orbx_pnp_iterate_candidates(hs, n, int(nIterations), C.byref(st), res, ip, C.byref(stopped)),
+          "orbx_pnp_iterate_candidates")
+    _rand_restore(rng, st)
+    k = min(stopped.value + 1, n)
+    return stopped.value, _pnp_outputs(solvers[:k], res[:k], inl[:k])
+
+
+def pnp_iterate_many(solvers, nIterations, rngs):
+    """iterate(n) on independent solvers, rngs[i] its own GlibcRand stream; one batched call."""
+    n = len(solvers)
+    hs = (C.c_void_p * max(n, 1))(*[s._h for s in solvers])
+    res = (_lib.PnpResult * max(n, 1))()
+    inl = [np.zeros(max(s.n, 1), np.uint8) for s in solvers]
+    ip = (C.c_void_p * max(n, 1))(*[ptr(b) for b in inl])
+    sts = [_rand_state(r) for r in rngs]
+    sp = (C.c_void_p * max(n, 1))(*[C.addressof(x) for x in sts])
+    check(_lib.lib().orbx_pnp_iterate_many(hs, n, int(nIterations), sp, res, ip), "orbx_pnp_iterate_many")
+    for r, x in zip(rngs, sts):
+        _rand_restore(r, x)
+    return _pnp_outputs(solvers, res[:n], inl)
+
+
 class ORBVocabulary:
     """DBoW2 TemplatedVocabulary<FORB> (include/ORBVocabulary.h) on the GPU:
     loadFromTextFile (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1420) and

@@ -232,3 +232,108 @@ def test_gpu_pnp_stream_api_equals_values_api(gpu):
         assert _lib.lib().orbx_rand_next(C.byref(probe)) == g.peek(1)[0]
     a.close()
     b.close()
+
+
+def _gpu_solver(P):
+    from orb_slam2_commit_amd import PnPsolver
+    s = PnPsolver(P["p3d"], P["p2d"], P["sigma2"], P["fx"], P["fy"], P["cx"], P["cy"])
+    s.SetRansacParameters(*TRACKING_PARAMS)
+    return s
+
+
+def _oracle_solver(P):
+    return oracle.PnPsolver(P["p3d"], P["p2d"], P["sigma2"], P["fx"], P["fy"], P["cx"], P["cy"], *TRACKING_PARAMS)
+
+
+# candidate sets for Tracking::Relocalization's loop: pure outliers (no pose: all hypotheses
+# consumed), too few matches (bNoMore at once, nothing drawn), then good candidates
+RELOC_SETS = {
+    "first_good": [("good", 31)],
+    "after_failures": [("bad", 41), ("few", 42), ("bad", 43), ("good", 44), ("good", 45)],
+    "none_good": [("bad", 51), ("few", 52), ("bad", 53)],
+    "heavy_outliers": [("bad", 61), ("hard", 62), ("good", 63)],
+}
+
+
+def _reloc_problem(kind, seed):
+    if kind == "good":
+        return synth.pnp_problem(seed=seed, n=600, outlier_frac=0.4, noise_px=0.5)
+    if kind == "hard":  # 45 % outliers: 55 % inliers is just above minInliers (epsilon 0.5 -> N/2)
+        return synth.pnp_problem(seed=seed, n=500, outlier_frac=0.45, noise_px=0.5)
+    if kind == "few":  # N < mRansacMinInliers (10): iterate returns bNoMore without drawing
+        return synth.pnp_problem(seed=seed, n=8, outlier_frac=0.0, noise_px=0.5)
+    return synth.pnp_problem(seed=seed, n=300, outlier_frac=1.0, noise_px=0.5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(RELOC_SETS))
+def test_gpu_pnp_iterate_candidates_equals_reference_loop(gpu, name):
+    """One batched call == the reference's candidate loop of iterate(5) calls on one rand() stream:
+    same stopping candidate, pose bits, inliers, bNoMore flags and stream position; then the loop
+    continues from the candidate after it (as Relocalization does when PoseOptimization rejects)."""
+    from orb_slam2_commit_amd.orb import pnp_iterate_candidates
+    probs = [_reloc_problem(k, s) for k, s in RELOC_SETS[name]]
+    gs = [_gpu_solver(P) for P in probs]
+    os_ = [_oracle_solver(P) for P in probs]
+    g_gpu, g_ora = GlibcRand(1), GlibcRand(1)
+    start = 0
+    for _ in range(2):  # two passes of the candidate loop
+        if start >= len(probs):
+            break
+        stopped, res = pnp_iterate_candidates(gs[start:], 5, g_gpu)
+        # reference loop on the oracle
+        ostop = len(probs) - start
+        for j, s in enumerate(os_[start:]):
+            To, nmo, inlo, nio, usedo = s.iterate(5, g_ora)
+            Tg, nmg, inlg, nig = res[j]
+            assert (To is None) == (Tg is None) and nmo == nmg and nio == nig, (name, start + j)
+            if To is not None:
+                np.testing.assert_array_equal(Tg, To)
+                np.testing.assert_array_equal(inlg, inlo)
+                ostop = j
+                break
+        assert stopped == ostop, (stopped, ostop)
+        assert g_gpu.peek(8) == g_ora.peek(8)
+        start += stopped + 1
+    for s in gs:
+        s.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pnp_iterate_many_independent_streams(gpu):
+    """Independent solvers (one per sequence, each with its own rand() stream), three rounds of
+    iterate(5): every solver equals its own sequential oracle run, bit for bit."""
+    from orb_slam2_commit_amd.orb import pnp_iterate_many
+    kinds = ["good", "bad", "few", "hard", "good", "good", "bad", "good"]
+    probs = [_reloc_problem(k, 70 + i) for i, k in enumerate(kinds)]
+    gs = [_gpu_solver(P) for P in probs]
+    os_ = [_oracle_solver(P) for P in probs]
+    g_gpu = [GlibcRand(1 + i) for i in range(len(probs))]
+    g_ora = [GlibcRand(1 + i) for i in range(len(probs))]
+    for _ in range(3):
+        res = pnp_iterate_many(gs, 5, g_gpu)
+        for i, s in enumerate(os_):
+            To, nmo, inlo, nio, usedo = s.iterate(5, g_ora[i])
+            Tg, nmg, inlg, nig = res[i]
+            assert (To is None) == (Tg is None) and nmo == nmg and nio == nig, (i, kinds[i])
+            if To is not None:
+                np.testing.assert_array_equal(Tg, To)
+                np.testing.assert_array_equal(inlg, inlo)
+            assert g_gpu[i].peek(4) == g_ora[i].peek(4), i
+    for s in gs:
+        s.close()
+
+
+def test_rand_state_bridge_round_trip():
+    """GlibcRand <-> orbx_rand_state (host code of liborbx.so, no GPU)."""
+    import ctypes as C
+    from orb_slam2_commit_amd import _lib
+    from orb_slam2_commit_amd.orb import _rand_restore, _rand_state
+    g = GlibcRand(7)
+    g.advance(123)
+    st = _rand_state(g)
+    ref = GlibcRand(7)
+    ref.advance(123)
+    assert [_lib.lib().orbx_rand_next(C.byref(st)) for _ in range(100)] == ref.take(100)
+    _rand_restore(g, st)
+    assert g.take(50) == ref.take(50)
