@@ -10,6 +10,8 @@ frames/s, from an un-instrumented loop (HIP events between steps only); the
 per-stage split and the roofline come from a second, profiled pass.
 
 Legs after the headline loop:
+  config3   EuRoC-shaped stereo + PnP RANSAC per frame (configs[2]): extract+match of a frame batch
+            (one frame per synthetic sequence) and one batched orbx_pnp_iterate_many over their solvers.
   localba   Optimizer::LocalBundleAdjustment (orbx_ba_run) on the config-4 problem
             per rank, --ba-calls times: LM iterations/s (whole job) + its roofline.
   config5   one synthetic sequence per rank: extract+match of --pipeline-steps
@@ -55,6 +57,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=3, help="config-5 batches per rank (0: skip)")
+    ap.add_argument("--c3-steps", type=int, default=3, help="config-3 (EuRoC + PnP RANSAC) steps per rank (0: skip)")
+    ap.add_argument("--c3-batch", type=int, default=128, help="config-3 frames (sequences) per step per GPU")
     ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r02_sq_counters.json"),
                     help="SQ counter summary (tools/pmc_kernel.sh + tools/sq_summary.py) for issue fractions")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -282,6 +286,101 @@ def localba_leg(args, rank, world, dev, odist, oracle_mod=None, flags=None, cpus
     return out
 
 
+# ------------------------------------------------------------------ config-3 leg
+def config3_leg(args, rank, world, dev, odist, stream, oracle_mod=None, flags=None, cpus=None):
+    """EuRoC MH_01-shaped stereo (752x480, 1200 features) + PnP RANSAC per frame (BASELINE configs[2]):
+    a step = extract L+R + stereo match of B3 frames (one per synthetic sequence, device batch) and, per
+    frame, a fresh PnPsolver (1,200 matches, 40 % outliers, Tracking's (0.99,10,300,4,0.5,5.991)) run by
+    iterate(5) on that sequence's own rand() stream -- all B3 solvers in one orbx_pnp_iterate_many call.
+    Returns whole-job frames/s (+ the split) and a single-core oracle baseline of the same unit."""
+    import torch
+    from orb_slam2_commit_amd import ORBextractor, PnPsolver, synth
+    from orb_slam2_commit_amd.glibc_rand import GlibcRand
+    from orb_slam2_commit_amd.orb import pnp_iterate_many
+    E = synth.EUROC
+    W, H, B3, NF = E["width"], E["height"], args.c3_batch, 1200
+    pairs = [synth.stereo_pair(s, W, H) for s in synth.sequence_seeds(100 + rank, 8)]
+    host = synth.stereo_batch(100 + rank, B3, width=W, height=H, pairs=pairs)
+    images = torch.from_numpy(host).to(dev)
+    ex = ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
+    cap = ex.max_keypoints(W, H)
+    kps = torch.empty((2 * B3, cap, 28), dtype=torch.uint8, device=dev)
+    desc = torch.empty((2 * B3, cap, 32), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(2 * B3, dtype=torch.int32, device=dev)
+    uR = torch.empty((B3, cap), dtype=torch.float32, device=dev)
+    depth = torch.empty((B3, cap), dtype=torch.float32, device=dev)
+    nmatch = torch.zeros(B3, dtype=torch.int32, device=dev)
+    bf, baseline = E["bf"], E["bf"] / E["fx"]
+    probs = [synth.pnp_problem(seed=3000 * (rank + 1) + f, n=1200, outlier_frac=0.4) for f in range(B3)]
+    rngs = [GlibcRand(1 + f + 1000 * rank) for f in range(B3)]  # one process rand() per sequence
+    prm = (0.99, 10, 300, 4, 0.5, 5.991)
+
+    def step():
+        ex.stereo_frames_device(images, kps, desc, counts, bf, baseline, uR, depth, nmatch, stream)
+        t_e = time.perf_counter()
+        solvers = PnPsolver.create_many(probs, *prm, device=dev.index)  # a new PnPsolver per frame
+        t_c = time.perf_counter()
+        res = pnp_iterate_many(solvers, 5, rngs)
+        t_r = time.perf_counter()
+        for sv in solvers:
+            sv.close()
+        return res, t_c - t_e, t_r - t_c
+
+    step()
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    t0 = time.perf_counter()
+    found, t_create, t_ransac = 0, 0.0, 0.0
+    for _ in range(args.c3_steps):
+        res, tc, tr = step()
+        found += sum(1 for r in res if r[0] is not None)
+        t_create += tc
+        t_ransac += tr
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    el = odist.max_over_ranks(time.perf_counter() - t0, dev)
+    frames = B3 * args.c3_steps * world
+    out = dict(frames_per_s=round(frames / el, 2), ms_per_step=round(el / args.c3_steps * 1e3, 3),
+               batch_frames_per_gpu=B3, steps=args.c3_steps,
+               ms_per_step_solver_create=round(t_create / args.c3_steps * 1e3, 3),
+               ms_per_step_ransac=round(t_ransac / args.c3_steps * 1e3, 3),
+               poses_found_frac=round(found / (B3 * args.c3_steps), 4),
+               keypoints_per_image=round(float(counts.float().mean()), 1),
+               config=dict(workload="EuRoC MH_01 stereo 752x480, 1200 features, extract L+R + ComputeStereoMatches "
+                                    "+ PnPsolver RANSAC (1200 matches, 40% outliers) per frame",
+                           rand_streams="one glibc rand() stream per frame slot (independent sequences)"),
+               data="synthetic (seeded stereo scenes, seeded PnP correspondence sets)", cpu_baseline=None)
+    if rank == 0 and world == 1 and oracle_mod is not None:
+        p = oracle_mod.params(NF, 1.2, 8, 20, 7)
+        old = os.sched_getaffinity(0) if hasattr(os, "sched_setaffinity") else None
+        try:
+            if old is not None and cpus:
+                os.sched_setaffinity(0, {cpus[0]})
+            g = GlibcRand(1)
+            n, ct = 0, []
+            t0 = time.perf_counter()
+            while True:
+                L, R = pairs[n % len(pairs)]
+                P = probs[n % len(probs)]
+                c0 = time.perf_counter()
+                oL, oR = oracle_mod.extract(p, L), oracle_mod.extract(p, R)
+                oracle_mod.stereo_match(p, oL, oR, bf, baseline)
+                sv = oracle_mod.PnPsolver(P["p3d"], P["p2d"], P["sigma2"], P["fx"], P["fy"], P["cx"], P["cy"], *prm)
+                sv.iterate(5, g)
+                ct.append(time.perf_counter() - c0)
+                n += 1
+                if time.perf_counter() - t0 >= max(2.0, args.cpu_baseline_seconds / 3) and n >= 3:
+                    break
+        finally:
+            if old is not None:
+                os.sched_setaffinity(0, old)
+        out["cpu_baseline"] = dict(value=round(n / sum(ct), 3), unit="frames/s", cores=1, kind="port",
+                                   median_ms=round(pct(ct, 50) * 1e3, 2), p90_ms=round(pct(ct, 90) * 1e3, 2),
+                                   sample="%d EuRoC-shaped frames (extract L+R + stereo match + PnP RANSAC), "
+                                          "oracle built %s, 1 thread pinned" % (n, flags))
+    return out
+
+
 # ------------------------------------------------------------------ config-5 leg
 def config5_leg(args, rank, world, dev, odist, ex, images, stream):
     """One sequence per rank: extract+match `pipeline_steps` batches into the frame-record arena, LocalBA
@@ -502,6 +601,8 @@ def main():
         out["localba_iters_per_s"] = out["localba"]["iters_per_s"]
     if args.pipeline_steps > 0:
         out["config5"] = config5_leg(args, rank, world, dev, odist, ex, images, stream)
+    if args.c3_steps > 0:
+        out["config3"] = config3_leg(args, rank, world, dev, odist, stream, oracle_mod, flags, cpus)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -274,6 +274,11 @@ typedef struct { /* SetRansacParameters arguments (Tracking: 0.99, 10, 300, 4, 0
 typedef struct orbx_pnp orbx_pnp;
 orbx_status orbx_pnp_create(const orbx_pnp_problem* problem, const orbx_pnp_params* params, int device,
                             orbx_pnp** out);
+/* n solvers at once (one per relocalisation candidate, or one per frame of a batch): the same as n
+ * orbx_pnp_create calls with one parameter set, the correspondences in one upload.  out[n]; each
+ * solver is released with orbx_pnp_destroy. */
+orbx_status orbx_pnp_create_many(const orbx_pnp_problem* problems, int n, const orbx_pnp_params* params, int device,
+                                 orbx_pnp** out);
 orbx_status orbx_pnp_destroy(orbx_pnp* h);
 /* Derived RANSAC parameters (mRansacMinInliers, mRansacMaxIts, mRansacEpsilon). */
 orbx_status orbx_pnp_get_params(const orbx_pnp* h, int* min_inliers, int* max_iterations, float* epsilon);

@@ -826,6 +826,7 @@ constexpr size_t kRefinePtBytes = 4 * 8 + 3 * 8 + 3 * 4 + 2 * 4;  // alphas, pcs
 
 // One block per hypothesis: its minimal set staged in LDS, EPnP, pose record
 // R (9, row-major) + t (3).
+template <int NT>
 __device__ __forceinline__ void pnp_hyp_body(const PnpIn& in, const int* __restrict__ idx, int set_size,
                                              double* __restrict__ pose) {
   __shared__ EpnpSmall S;
@@ -840,7 +841,7 @@ __device__ __forceinline__ void pnp_hyp_body(const PnpIn& in, const int* __restr
     suv[2 * tid + 1] = in.p2d[2 * i + 1];
   }
   __syncthreads();
-  epnp_compute_pose<kHypThreads>(in, EpnpPts{spw, suv, salpha, stmp}, set_size, &S);
+  epnp_compute_pose<NT>(in, EpnpPts{spw, suv, salpha, stmp}, set_size, &S);
   if (tid < 12) {
     const int b = (int)S.rep[0];
     pose[tid] = tid < 9 ? S.Rs[b][tid / 3][tid % 3] : S.ts[b][tid - 9];
@@ -850,7 +851,7 @@ __device__ __forceinline__ void pnp_hyp_body(const PnpIn& in, const int* __restr
 __global__ __launch_bounds__(kHypThreads) void k_pnp_hyp(PnpIn in, const int* __restrict__ sets, int set_size,
                                                          double* __restrict__ poses) {
   const int h = blockIdx.x;
-  pnp_hyp_body(in, sets + (size_t)h * set_size, set_size, poses + 12 * (size_t)h);
+  pnp_hyp_body<kHypThreads>(in, sets + (size_t)h * set_size, set_size, poses + 12 * (size_t)h);
 }
 
 // CheckInliers (src/PnPsolver.cc:352-384) of one hypothesis -> mask + count.
@@ -890,11 +891,15 @@ struct PnpHypJob {
   int h0, H, set_size;
 };
 
-__global__ __launch_bounds__(kHypThreads) void k_pnp_hyp_many(const PnpHypJob* __restrict__ jobs) {
+// throughput form: one wave per hypothesis (the three beta approximations in series on it), so
+// four hypotheses share a CU where the 4-wave latency form (whose VGPR budget allows one
+// block per CU) runs one
+constexpr int kHypManyThreads = 64;
+__global__ __launch_bounds__(kHypManyThreads) void k_pnp_hyp_many(const PnpHypJob* __restrict__ jobs) {
   const PnpHypJob& J = jobs[blockIdx.y];
   if ((int)blockIdx.x >= J.H) return;  // block-uniform
   const int h = J.h0 + blockIdx.x;
-  pnp_hyp_body(J.in, J.sets + (size_t)h * J.set_size, J.set_size, J.poses + 12 * (size_t)h);
+  pnp_hyp_body<kHypManyThreads>(J.in, J.sets + (size_t)h * J.set_size, J.set_size, J.poses + 12 * (size_t)h);
 }
 
 __global__ __launch_bounds__(256) void k_pnp_check_many(const PnpHypJob* __restrict__ jobs) {
@@ -993,6 +998,17 @@ __global__ __launch_bounds__(kRefThreads) void k_pnp_refine(PnpIn in, const uint
 template <bool kLds>
 __global__ __launch_bounds__(kRefThreads) void k_pnp_refine_many(const PnpRefJob* __restrict__ jobs) {
   pnp_refine_body<kLds>(jobs[blockIdx.x]);
+}
+
+// byte ranges of several solvers' buffers into one staging block (one readback for all)
+struct PnpGatherJob {
+  const uint8_t* src;
+  uint8_t* dst;
+  int n;
+};
+__global__ __launch_bounds__(256) void k_pnp_gather(const PnpGatherJob* __restrict__ jobs) {
+  const PnpGatherJob J = jobs[blockIdx.x];
+  for (int i = threadIdx.x; i < J.n; i += 256) J.dst[i] = J.src[i];
 }
 
 }  // namespace orbx
@@ -1154,17 +1170,29 @@ void pose_to_Tcw(const double* P, float T[16]) {  // Rcw/tcw convertTo(CV_32F) i
 
 extern "C" {
 
-orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* prm, int device, orbx_pnp** out) {
-  if (!p || !prm || !out || p->n < 0 || (p->n > 0 && (!p->p3d || !p->p2d || !p->sigma2))) return ORBX_ERR_ARG;
+}  // extern "C"
+
+namespace {
+
+orbx_status pnp_check_problem(const orbx_pnp_problem* p, const orbx_pnp_params* prm) {
+  if (!p || !prm || p->n < 0 || (p->n > 0 && (!p->p3d || !p->p2d || !p->sigma2))) return ORBX_ERR_ARG;
   if (prm->min_set < 1 || prm->min_set > orbx::kPnpMaxSet) return ORBX_ERR_ARG;
-  *out = nullptr;
+  return ORBX_OK;
+}
+
+orbx_status pnp_device_check(int device) {
   int nd = 0;
   if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return ORBX_ERR_NODEV;
   if (device < 0 || device >= nd || device >= 64) return ORBX_ERR_ARG;
   if (hipSetDevice(device) != hipSuccess) return ORBX_ERR_HIP;
   if (pnp_device_init(device) != hipSuccess) return ORBX_ERR_HIP;
+  return ORBX_OK;
+}
+
+// PnPsolver ctor + SetRansacParameters (src/PnPsolver.cc:67-179) without the upload
+orbx_pnp* pnp_new(const orbx_pnp_problem* p, const orbx_pnp_params* prm, int device) {
   orbx_pnp* h = new (std::nothrow) orbx_pnp();
-  if (!h) return ORBX_ERR_HIP;
+  if (!h) return nullptr;
   h->device = device;
   h->st = g_pnp_dev[device].st;
   const int n = p->n;
@@ -1173,7 +1201,6 @@ orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* pr
   h->fv = p->fy;
   h->uc = p->cx;
   h->vc = p->cy;
-  // SetRansacParameters (src/PnPsolver.cc:136-179)
   h->prob = prm->probability;
   h->min_inliers = prm->min_inliers;
   h->max_its = prm->max_iterations;
@@ -1191,14 +1218,35 @@ orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* pr
     nIterations = (int)std::ceil(std::log(1 - h->prob) / std::log(1 - std::pow(h->epsilon, 3)));
   h->max_its = std::max(1, std::min(nIterations, h->max_its));
   for (int i = 0; i < 16; i++) h->best_Tcw[i] = 0;
+  return h;
+}
+
+// p3d | p2d | maxerr (= sigma2 * th2) of one solver, laid out as in its device block
+void pnp_stage_problem(const orbx_pnp* h, const orbx_pnp_problem* p, const orbx_pnp_params* prm, uint8_t* dst) {
+  const int n = p->n;
+  std::memcpy(dst, p->p3d, 12 * (size_t)n);
+  std::memcpy(dst + ((uint8_t*)h->d_p2d - (uint8_t*)h->d_p3d), p->p2d, 8 * (size_t)n);
+  float* me = (float*)(dst + ((uint8_t*)h->d_maxerr - (uint8_t*)h->d_p3d));
+  for (int i = 0; i < n; i++) me[i] = p->sigma2[i] * prm->th2;
+}
+
+}  // namespace
+
+extern "C" {
+
+orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* prm, int device, orbx_pnp** out) {
+  orbx_status s = pnp_check_problem(p, prm);
+  if (s != ORBX_OK || !out) return s != ORBX_OK ? s : ORBX_ERR_ARG;
+  *out = nullptr;
+  if ((s = pnp_device_check(device)) != ORBX_OK) return s;
+  orbx_pnp* h = pnp_new(p, prm, device);
+  if (!h) return ORBX_ERR_HIP;
+  const int n = p->n;
   hipError_t e = h->alloc(std::max(h->max_its, 8));
   if (e == hipSuccess && n > 0) {
     // one upload: p3d | p2d | maxerr are consecutive in the layout
     std::vector<uint8_t> stage((uint8_t*)h->d_best - (uint8_t*)h->d_p3d);
-    std::memcpy(stage.data(), p->p3d, 12 * (size_t)n);
-    std::memcpy(stage.data() + ((uint8_t*)h->d_p2d - (uint8_t*)h->d_p3d), p->p2d, 8 * (size_t)n);
-    float* me = (float*)(stage.data() + ((uint8_t*)h->d_maxerr - (uint8_t*)h->d_p3d));
-    for (int i = 0; i < n; i++) me[i] = p->sigma2[i] * prm->th2;
+    pnp_stage_problem(h, p, prm, stage.data());
     e = hipMemcpyAsync(h->d_p3d, stage.data(), stage.size(), hipMemcpyHostToDevice, h->st);
     if (e == hipSuccess) e = hipStreamSynchronize(h->st);  // stage is pageable and local
   }
@@ -1208,6 +1256,58 @@ orbx_status orbx_pnp_create(const orbx_pnp_problem* p, const orbx_pnp_params* pr
     return ORBX_ERR_HIP;
   }
   *out = h;
+  return ORBX_OK;
+}
+
+orbx_status orbx_pnp_create_many(const orbx_pnp_problem* problems, int n, const orbx_pnp_params* prm, int device,
+                                 orbx_pnp** out) {
+  if (n < 0 || (n > 0 && (!problems || !out))) return ORBX_ERR_ARG;
+  for (int i = 0; i < n; i++) {
+    const orbx_status s = pnp_check_problem(&problems[i], prm);
+    if (s != ORBX_OK) return s;
+    out[i] = nullptr;
+  }
+  if (n == 0) return ORBX_OK;
+  orbx_status s = pnp_device_check(device);
+  if (s != ORBX_OK) return s;
+  PnpDevice& dev = g_pnp_dev[device];
+  std::lock_guard<std::mutex> lock(dev.mu);
+  std::vector<orbx_pnp*> hs(n, nullptr);
+  auto fail = [&](orbx_status code) {
+    for (orbx_pnp* h : hs)
+      if (h) {
+        if (h->d_mem) (void)hipFreeAsync(h->d_mem, h->st);
+        delete h;
+      }
+    return code;
+  };
+  size_t stage = 0;
+  for (int i = 0; i < n; i++) {
+    hs[i] = pnp_new(&problems[i], prm, device);
+    if (!hs[i]) return fail(ORBX_ERR_HIP);
+    if (hs[i]->alloc(std::max(hs[i]->max_its, 8)) != hipSuccess) return fail(ORBX_ERR_HIP);
+    stage += align256((uint8_t*)hs[i]->d_best - (uint8_t*)hs[i]->d_p3d);
+  }
+  // all correspondences in one pinned block, one upload, one gather launch into the solvers' blocks
+  const size_t off_data = align256(n * sizeof(orbx::PnpGatherJob));
+  const size_t bytes = off_data + stage;
+  if (dev.pinned_reserve(bytes) != hipSuccess || dev.dstage_reserve(bytes) != hipSuccess) return fail(ORBX_ERR_HIP);
+  uint8_t* hp = (uint8_t*)dev.pinned;
+  uint8_t* dp = (uint8_t*)dev.dstage;
+  orbx::PnpGatherJob* jobs = (orbx::PnpGatherJob*)hp;
+  size_t o = off_data;
+  for (int i = 0; i < n; i++) {
+    orbx_pnp* h = hs[i];
+    const size_t len = (uint8_t*)h->d_best - (uint8_t*)h->d_p3d;
+    if (problems[i].n > 0) pnp_stage_problem(h, &problems[i], prm, hp + o);
+    jobs[i] = orbx::PnpGatherJob{dp + o, (uint8_t*)h->d_p3d, problems[i].n > 0 ? (int)len : 0};
+    o += align256(len);
+  }
+  hipStream_t st = dev.st;
+  if (hipMemcpyAsync(dp, hp, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return fail(ORBX_ERR_HIP);
+  hipLaunchKernelGGL(orbx::k_pnp_gather, dim3(n), dim3(256), 0, st, (const orbx::PnpGatherJob*)dp);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return fail(ORBX_ERR_HIP);
+  for (int i = 0; i < n; i++) out[i] = hs[i];
   return ORBX_OK;
 }
 
@@ -1342,7 +1442,7 @@ struct PnpRun {
   int k = 0;                    // next hypothesis to walk
   int launched = 0;             // hypotheses [0, launched) have counts
   int cur = 0, used = 0;
-  bool eligible = true, done = false, pending = false;
+  bool eligible = true, done = false, pending = false, read_best = false;
   std::vector<int> counts;
   orbx_pnp_result* out = nullptr;
   uint8_t* inliers = nullptr;
@@ -1420,7 +1520,7 @@ orbx_status pnp_launch_chunks(PnpDevice& dev, hipStream_t st, std::vector<std::p
   }
   PNP_CHECK(hipMemcpyAsync(dp, hp, off_counts, hipMemcpyHostToDevice, st));
   const orbx::PnpHypJob* dj = (const orbx::PnpHypJob*)dp;
-  hipLaunchKernelGGL(orbx::k_pnp_hyp_many, dim3(maxc, nj), dim3(orbx::kHypThreads), 0, st, dj);
+  hipLaunchKernelGGL(orbx::k_pnp_hyp_many, dim3(maxc, nj), dim3(orbx::kHypManyThreads), 0, st, dj);
   hipLaunchKernelGGL(orbx::k_pnp_check_many, dim3(maxc, nj), dim3(256), 0, st, dj);
   PNP_CHECK(hipGetLastError());
   int* hc = (int*)(hp + off_counts);
@@ -1461,29 +1561,67 @@ orbx_status pnp_walk(PnpRun& r, hipStream_t st) {
 }
 
 // the end of iterate() once all H hypotheses were walked without a refined pose
-orbx_status pnp_finish(PnpRun& r, hipStream_t st, std::vector<double>& pose_scratch) {
+// (the best pose and mask are read back by pnp_read_best, batched)
+void pnp_finish(PnpRun& r) {
   orbx_pnp* h = r.h;
   r.done = true;
   if (h->iterations >= h->max_its) {
     r.out->no_more = 1;
     if (h->best_inliers >= h->min_inliers) {
-      PNP_CHECK(hipMemcpyAsync(pose_scratch.data(), h->d_res + 16, 12 * sizeof(double), hipMemcpyDeviceToHost, st));
-      if (r.inliers) PNP_CHECK(hipMemcpyAsync(r.inliers, h->d_best, h->N, hipMemcpyDeviceToHost, st));
-      PNP_CHECK(hipStreamSynchronize(st));
-      pose_to_Tcw(pose_scratch.data(), h->best_Tcw);
-      std::memcpy(r.out->Tcw, h->best_Tcw, sizeof(float) * 16);
       r.out->n_inliers = h->best_inliers;
       r.out->found = 1;
+      r.read_best = true;
     }
   }
+}
+
+// best pose (12 doubles) + best mask of every run in `rs`: one gather launch, one readback
+orbx_status pnp_read_best(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*>& rs) {
+  if (rs.empty()) return ORBX_OK;
+  const size_t nj = 2 * rs.size();
+  size_t data = 0;
+  for (PnpRun* r : rs) data += 96 + align256((size_t)r->h->N);
+  const size_t off_data = align256(nj * sizeof(orbx::PnpGatherJob));
+  const size_t bytes = off_data + data;
+  PNP_CHECK(dev.pinned_reserve(bytes));
+  PNP_CHECK(dev.dstage_reserve(bytes));
+  uint8_t* hp = (uint8_t*)dev.pinned;
+  uint8_t* dp = (uint8_t*)dev.dstage;
+  orbx::PnpGatherJob* jobs = (orbx::PnpGatherJob*)hp;
+  size_t o = off_data;
+  for (size_t j = 0; j < rs.size(); j++) {
+    orbx_pnp* h = rs[j]->h;
+    jobs[2 * j] = orbx::PnpGatherJob{(const uint8_t*)(h->d_res + 16), dp + o, 96};
+    jobs[2 * j + 1] = orbx::PnpGatherJob{h->d_best, dp + o + 96, h->N};
+    o += 96 + align256((size_t)h->N);
+  }
+  PNP_CHECK(hipMemcpyAsync(dp, hp, nj * sizeof(orbx::PnpGatherJob), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(orbx::k_pnp_gather, dim3(nj), dim3(256), 0, st, (const orbx::PnpGatherJob*)dp);
+  PNP_CHECK(hipGetLastError());
+  PNP_CHECK(hipMemcpyAsync(hp + off_data, dp + off_data, data, hipMemcpyDeviceToHost, st));
+  PNP_CHECK(hipStreamSynchronize(st));
+  o = off_data;
+  for (PnpRun* r : rs) {
+    orbx_pnp* h = r->h;
+    pose_to_Tcw((const double*)(hp + o), h->best_Tcw);
+    std::memcpy(r->out->Tcw, h->best_Tcw, sizeof(float) * 16);
+    if (r->inliers) std::memcpy(r->inliers, hp + o + 96, h->N);
+    r->read_best = false;
+    o += 96 + align256((size_t)h->N);
+  }
+  rs.clear();
   return ORBX_OK;
 }
 
 orbx_status pnp_refine_round(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*>& pend) {
   if (pend.empty()) return ORBX_OK;
   const size_t nj = pend.size();
+  // staging: job records | per job 16 doubles (R t, count) | per job its refined mask
+  size_t masks = 0;
+  for (PnpRun* r : pend) masks += align256((size_t)r->h->N);
   const size_t off_res = align256(nj * sizeof(orbx::PnpRefJob));
-  const size_t bytes = off_res + nj * 16 * sizeof(double);
+  const size_t off_mask = off_res + align256(nj * 16 * sizeof(double));
+  const size_t bytes = off_mask + masks;
   PNP_CHECK(dev.pinned_reserve(bytes));
   PNP_CHECK(dev.dstage_reserve(bytes));
   uint8_t* hp = (uint8_t*)dev.pinned;
@@ -1496,10 +1634,14 @@ orbx_status pnp_refine_round(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*
   const int n_lds = (int)order.size();
   for (PnpRun* r : pend)
     if (r->h->best_inliers > orbx::kRefineLdsPts) order.push_back(r);
+  std::vector<size_t> moff(nj);
+  size_t mo = off_mask;
   for (size_t j = 0; j < nj; j++) {
     orbx_pnp* h = order[j]->h;
-    jobs[j] = orbx::PnpRefJob{h->in(), h->d_best, h->d_idx, h->d_rwork, h->d_res, h->d_refmask,
-                              (int*)(h->d_res + 12)};
+    double* out = (double*)(dp + off_res) + 16 * j;
+    moff[j] = mo;
+    jobs[j] = orbx::PnpRefJob{h->in(), h->d_best, h->d_idx, h->d_rwork, out, dp + mo, (int*)(out + 12)};
+    mo += align256((size_t)h->N);
   }
   PNP_CHECK(hipMemcpyAsync(dp, hp, nj * sizeof(orbx::PnpRefJob), hipMemcpyHostToDevice, st));
   const orbx::PnpRefJob* dj = (const orbx::PnpRefJob*)dp;
@@ -1510,17 +1652,16 @@ orbx_status pnp_refine_round(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*
     hipLaunchKernelGGL(orbx::k_pnp_refine_many<false>, dim3((int)nj - n_lds), dim3(orbx::kRefThreads), 0, st,
                        dj + n_lds);
   PNP_CHECK(hipGetLastError());
-  double* res = (double*)(hp + off_res);
-  for (size_t j = 0; j < nj; j++)
-    PNP_CHECK(hipMemcpyAsync(res + 16 * j, order[j]->h->d_res, 13 * sizeof(double), hipMemcpyDeviceToHost, st));
+  PNP_CHECK(hipMemcpyAsync(hp + off_res, dp + off_res, bytes - off_res, hipMemcpyDeviceToHost, st));
   PNP_CHECK(hipStreamSynchronize(st));
+  const double* res = (const double*)(hp + off_res);
   for (size_t j = 0; j < nj; j++) {
     PnpRun& r = *order[j];
     orbx_pnp* h = r.h;
     r.pending = false;
     const int rc = *(const int*)(res + 16 * j + 12);
     if (rc > h->min_inliers) {  // Refine() succeeded: the call returns mRefinedTcw
-      if (r.inliers) PNP_CHECK(hipMemcpyAsync(r.inliers, h->d_refmask, h->N, hipMemcpyDeviceToHost, st));
+      if (r.inliers) std::memcpy(r.inliers, hp + moff[j], h->N);
       pose_to_Tcw(res + 16 * j, r.out->Tcw);
       r.out->n_inliers = rc;
       r.out->found = 1;
@@ -1529,7 +1670,6 @@ orbx_status pnp_refine_round(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*
       h->refine_valid = true;
     }
   }
-  PNP_CHECK(hipStreamSynchronize(st));
   return ORBX_OK;
 }
 
@@ -1541,7 +1681,7 @@ orbx_status pnp_run_many(std::vector<PnpRun>& runs, bool shared, int* stopped) {
   const int device = runs[0].h->device;
   PnpDevice& dev = g_pnp_dev[device];
   hipStream_t st = dev.st;
-  std::vector<double> pose_scratch(16);
+  std::vector<PnpRun*> best_reads;
   const int nr = (int)runs.size();
   int active = 0;  // shared mode: the run whose walk is committed
   bool first_round = true;
@@ -1563,7 +1703,10 @@ orbx_status pnp_run_many(std::vector<PnpRun>& runs, bool shared, int* stopped) {
       PnpRun& r = runs[i];
       const bool eligible = shared ? (first_round || i == active) : true;
       if (!eligible || r.done || r.pending || r.k < r.launched || r.launched >= r.H) continue;
-      const int c = std::min(r.H - r.launched, std::max(kPnpFirstChunk, r.launched));  // 16, 16, 32, 64, ...
+      // the first chunk, then everything left: a solver still without a pose after its first
+      // hypotheses most often runs all of them (no set reaches minInliers), and one launch of
+      // them beats a chain of doubling rounds
+      const int c = r.launched == 0 ? std::min(r.H, kPnpFirstChunk) : r.H - r.launched;
       chunk.push_back({&r, c});
     }
     first_round = false;
@@ -1575,15 +1718,21 @@ orbx_status pnp_run_many(std::vector<PnpRun>& runs, bool shared, int* stopped) {
       PnpRun& r = runs[i];
       if (r.done || (shared && i != active)) continue;
       if ((s = pnp_walk(r, st)) != ORBX_OK) return s;
-      if (r.pending)
+      if (r.pending) {
         pend.push_back(&r);
-      else if (r.k >= r.H && (s = pnp_finish(r, st, pose_scratch)) != ORBX_OK)
-        return s;
+      } else if (r.k >= r.H) {
+        pnp_finish(r);
+        if (r.read_best) best_reads.push_back(&r);
+      }
     }
-    // 3. the Refine() calls of this round
+    // 3. the Refine() calls of this round, then the best poses of the runs that ended
     if ((s = pnp_refine_round(dev, st, pend)) != ORBX_OK) return s;
     for (PnpRun* r : pend)
-      if (!r->done && r->k >= r->H && (s = pnp_finish(*r, st, pose_scratch)) != ORBX_OK) return s;
+      if (!r->done && r->k >= r->H) {
+        pnp_finish(*r);
+        if (r->read_best) best_reads.push_back(r);
+      }
+    if ((s = pnp_read_best(dev, st, best_reads)) != ORBX_OK) return s;
     bool all_done = true;
     for (int i = 0; i < nr; i++) all_done = all_done && runs[i].done;
     if (!shared && all_done) break;

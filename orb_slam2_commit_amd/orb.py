@@ -566,6 +566,37 @@ class PnPsolver:
         self.min_inliers, self.max_its, self.epsilon = a.value, b.value, c.value
         self._done = 0
 
+    @classmethod
+    def create_many(cls, problems, probability=0.99, minInliers=8, maxIterations=300, minSet=4, epsilon=0.4,
+                    th2=5.991, device=0):
+        """len(problems) solvers (dicts p3d, p2d, sigma2, fx, fy, cx, cy) with one parameter set, created by
+        one orbx_pnp_create_many call (one upload for all correspondences)."""
+        n = len(problems)
+        objs, structs = [], (_lib.PnpProblem * max(n, 1))()
+        for i, P in enumerate(problems):
+            o = cls.__new__(cls)
+            o.p3d = np.ascontiguousarray(P["p3d"], np.float32).reshape(-1, 3)
+            o.p2d = np.ascontiguousarray(P["p2d"], np.float32).reshape(-1, 2)
+            o.sigma2 = np.ascontiguousarray(P["sigma2"], np.float32)
+            o.n = len(o.p3d)
+            o.intr = (float(P["fx"]), float(P["fy"]), float(P["cx"]), float(P["cy"]))
+            o.device = int(device)
+            o._h = None
+            structs[i] = _lib.PnpProblem(o.n, ptr(o.p3d), ptr(o.p2d), ptr(o.sigma2), *o.intr)
+            objs.append(o)
+        prm = _lib.PnpParams(float(probability), int(minInliers), int(maxIterations), int(minSet), float(epsilon),
+                             float(th2))
+        hs = (C.c_void_p * max(n, 1))()
+        check(_lib.lib().orbx_pnp_create_many(structs, n, C.byref(prm), int(device), hs), "orbx_pnp_create_many")
+        for o, h in zip(objs, hs):
+            o._h = C.c_void_p(h)
+            o.min_set = int(minSet)
+            a, b, c = C.c_int(), C.c_int(), C.c_float()
+            check(_lib.lib().orbx_pnp_get_params(o._h, C.byref(a), C.byref(b), C.byref(c)), "orbx_pnp_get_params")
+            o.min_inliers, o.max_its, o.epsilon = a.value, b.value, c.value
+            o._done = 0
+        return objs
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().orbx_pnp_destroy(self._h)

@@ -337,3 +337,24 @@ def test_rand_state_bridge_round_trip():
     assert [_lib.lib().orbx_rand_next(C.byref(st)) for _ in range(100)] == ref.take(100)
     _rand_restore(g, st)
     assert g.take(50) == ref.take(50)
+
+
+@pytest.mark.gpu
+def test_gpu_pnp_create_many_equals_create(gpu):
+    """orbx_pnp_create_many == n orbx_pnp_create calls: same derived parameters, same iterate() results."""
+    from orb_slam2_commit_amd import PnPsolver
+    probs = [_reloc_problem(k, 90 + i) for i, k in enumerate(["good", "few", "bad", "hard", "good"])]
+    many = PnPsolver.create_many(probs, *TRACKING_PARAMS)
+    one = [_gpu_solver(P) for P in probs]
+    ga, gb = GlibcRand(1), GlibcRand(1)
+    for a, b in zip(many, one):
+        assert (a.min_inliers, a.max_its, a.epsilon) == (b.min_inliers, b.max_its, b.epsilon)
+        Ta, nma, inla, nia = a.iterate(5, ga)
+        Tb, nmb, inlb, nib = b.iterate(5, gb)
+        assert (Ta is None) == (Tb is None) and nma == nmb and nia == nib
+        if Ta is not None:
+            np.testing.assert_array_equal(Ta, Tb)
+            np.testing.assert_array_equal(inla, inlb)
+        assert ga.peek(4) == gb.peek(4)
+    for s in many + one:
+        s.close()
