@@ -155,11 +155,33 @@ __device__ __forceinline__ void jacobi_tail(double* At, double* W, double* Wout,
       } else {
         swap_d(W[i], W[j]);
       }
+      if constexpr (kSmall) {  // rows of register arrays: swap with every candidate row under a
+                               // select (static indices), never a runtime-indexed (scratch) access
 #pragma unroll
-      for (int k = 0; k < M; k++) swap_d(At[i * M + k], At[j * M + k]);
-      if (kV) {
+        for (int r = i + 1; r < N; r++) {
+          const bool sw = r == j;
 #pragma unroll
-        for (int k = 0; k < N; k++) swap_d(Vt[i * N + k], Vt[j * N + k]);
+          for (int k = 0; k < M; k++) {
+            const double a = At[i * M + k], b = At[r * M + k];
+            At[i * M + k] = sw ? b : a;
+            At[r * M + k] = sw ? a : b;
+          }
+          if (kV) {
+#pragma unroll
+            for (int k = 0; k < N; k++) {
+              const double a = Vt[i * N + k], b = Vt[r * N + k];
+              Vt[i * N + k] = sw ? b : a;
+              Vt[r * N + k] = sw ? a : b;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < M; k++) swap_d(At[i * M + k], At[j * M + k]);
+        if (kV) {
+#pragma unroll
+          for (int k = 0; k < N; k++) swap_d(Vt[i * N + k], Vt[j * N + k]);
+        }
       }
     }
   }
@@ -895,7 +917,7 @@ struct PnpHypJob {
 // four hypotheses share a CU where the 4-wave latency form (whose VGPR budget allows one
 // block per CU) runs one
 constexpr int kHypManyThreads = 64;
-__global__ __launch_bounds__(kHypManyThreads) void k_pnp_hyp_many(const PnpHypJob* __restrict__ jobs) {
+__global__ __launch_bounds__(kHypManyThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_pnp_hyp_many(const PnpHypJob* __restrict__ jobs) {
   const PnpHypJob& J = jobs[blockIdx.y];
   if ((int)blockIdx.x >= J.H) return;  // block-uniform
   const int h = J.h0 + blockIdx.x;
@@ -1443,6 +1465,9 @@ struct PnpRun {
   int launched = 0;             // hypotheses [0, launched) have counts
   int cur = 0, used = 0;
   bool eligible = true, done = false, pending = false, read_best = false;
+  int best_k = -1;  // hypothesis of this call holding the best set (-1: d_best / d_res+16 of an earlier call)
+  const uint8_t* best_mask() const { return best_k >= 0 ? h->d_masks + (size_t)best_k * h->N : h->d_best; }
+  const double* best_pose() const { return best_k >= 0 ? h->d_poses + 12 * (size_t)best_k : h->d_res + 16; }
   std::vector<int> counts;
   orbx_pnp_result* out = nullptr;
   uint8_t* inliers = nullptr;
@@ -1538,20 +1563,17 @@ orbx_status pnp_launch_chunks(PnpDevice& dev, hipStream_t st, std::vector<std::p
 
 // the walk of orbx_pnp_iterate from hypothesis r.k: stops at a Refine() request,
 // at the end of the launched hypotheses, or at the end of the call
-orbx_status pnp_walk(PnpRun& r, hipStream_t st) {
+orbx_status pnp_walk(PnpRun& r) {
   orbx_pnp* h = r.h;
-  const int N = h->N;
   while (!r.pending && r.k < r.launched) {
     const int k = r.k++;
     r.cur++;
     h->iterations++;
     r.used += h->min_set;
     if (r.counts[k] < h->min_inliers) continue;
-    if (r.counts[k] > h->best_inliers) {  // new best: mask + pose stay on the device
+    if (r.counts[k] > h->best_inliers) {  // new best: its mask and pose stay where they are
       h->best_inliers = r.counts[k];
-      PNP_CHECK(hipMemcpyAsync(h->d_best, h->d_masks + (size_t)k * N, N, hipMemcpyDeviceToDevice, st));
-      PNP_CHECK(hipMemcpyAsync(h->d_res + 16, h->d_poses + 12 * (size_t)k, 12 * sizeof(double),
-                               hipMemcpyDeviceToDevice, st));
+      r.best_k = k;
       h->refine_valid = false;
     }
     if (h->refine_valid) continue;  // same best set: Refine() fails again
@@ -1591,8 +1613,8 @@ orbx_status pnp_read_best(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*>& 
   size_t o = off_data;
   for (size_t j = 0; j < rs.size(); j++) {
     orbx_pnp* h = rs[j]->h;
-    jobs[2 * j] = orbx::PnpGatherJob{(const uint8_t*)(h->d_res + 16), dp + o, 96};
-    jobs[2 * j + 1] = orbx::PnpGatherJob{h->d_best, dp + o + 96, h->N};
+    jobs[2 * j] = orbx::PnpGatherJob{(const uint8_t*)rs[j]->best_pose(), dp + o, 96};
+    jobs[2 * j + 1] = orbx::PnpGatherJob{rs[j]->best_mask(), dp + o + 96, h->N};
     o += 96 + align256((size_t)h->N);
   }
   PNP_CHECK(hipMemcpyAsync(dp, hp, nj * sizeof(orbx::PnpGatherJob), hipMemcpyHostToDevice, st));
@@ -1640,7 +1662,7 @@ orbx_status pnp_refine_round(PnpDevice& dev, hipStream_t st, std::vector<PnpRun*
     orbx_pnp* h = order[j]->h;
     double* out = (double*)(dp + off_res) + 16 * j;
     moff[j] = mo;
-    jobs[j] = orbx::PnpRefJob{h->in(), h->d_best, h->d_idx, h->d_rwork, out, dp + mo, (int*)(out + 12)};
+    jobs[j] = orbx::PnpRefJob{h->in(), order[j]->best_mask(), h->d_idx, h->d_rwork, out, dp + mo, (int*)(out + 12)};
     mo += align256((size_t)h->N);
   }
   PNP_CHECK(hipMemcpyAsync(dp, hp, nj * sizeof(orbx::PnpRefJob), hipMemcpyHostToDevice, st));
@@ -1717,7 +1739,7 @@ orbx_status pnp_run_many(std::vector<PnpRun>& runs, bool shared, int* stopped) {
     for (int i = 0; i < nr; i++) {
       PnpRun& r = runs[i];
       if (r.done || (shared && i != active)) continue;
-      if ((s = pnp_walk(r, st)) != ORBX_OK) return s;
+      if ((s = pnp_walk(r)) != ORBX_OK) return s;
       if (r.pending) {
         pend.push_back(&r);
       } else if (r.k >= r.H) {
@@ -1739,6 +1761,26 @@ orbx_status pnp_run_many(std::vector<PnpRun>& runs, bool shared, int* stopped) {
     if (shared && all_done) {
       // fall through to the stop scan at the top
     }
+  }
+  // persist the best set of every solver whose best now comes from this call (the next call
+  // reuses the hypothesis buffers): one gather launch
+  std::vector<orbx::PnpGatherJob> keep;
+  for (PnpRun& r : runs)
+    if (r.best_k >= 0) {
+      keep.push_back(orbx::PnpGatherJob{r.best_mask(), r.h->d_best, r.h->N});
+      keep.push_back(orbx::PnpGatherJob{(const uint8_t*)r.best_pose(), (uint8_t*)(r.h->d_res + 16), 96});
+      r.best_k = -1;
+    }
+  if (!keep.empty()) {
+    const size_t bytes = keep.size() * sizeof(orbx::PnpGatherJob);
+    PNP_CHECK(dev.pinned_reserve(bytes));
+    PNP_CHECK(dev.dstage_reserve(bytes));
+    std::memcpy(dev.pinned, keep.data(), bytes);
+    PNP_CHECK(hipMemcpyAsync(dev.dstage, dev.pinned, bytes, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(orbx::k_pnp_gather, dim3((unsigned)keep.size()), dim3(256), 0, st,
+                       (const orbx::PnpGatherJob*)dev.dstage);
+    PNP_CHECK(hipGetLastError());
+    PNP_CHECK(hipStreamSynchronize(st));
   }
   return ORBX_OK;
 }
