@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
+    ap.add_argument("--ba-concurrent", type=int, default=4, help="LocalBA problems in flight per GPU for the "
+                                                                  "throughput form (<=1: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=3, help="config-5 batches per rank (0: skip)")
     ap.add_argument("--c3-steps", type=int, default=3, help="config-3 (EuRoC + PnP RANSAC) steps per rank (0: skip)")
     ap.add_argument("--c3-batch", type=int, default=128, help="config-3 frames (sequences) per step per GPU")
@@ -259,6 +261,38 @@ def localba_leg(args, rank, world, dev, odist, oracle_mod=None, flags=None, cpus
                                   "of this rank; the trial is a chain of ~12 dependent small launches "
                                   "(latency-bound; per-kernel split in profiles/*localba_kernel_stats.csv)"),
                dtype="f64", scaling="weak", cpu_baseline=None)
+    if args.ba_concurrent > 1:
+        # throughput form: K independent LocalBA problems in flight on this GPU (one solver handle, HIP
+        # stream and host thread each -- K maps / sequences per GPU); a single problem leaves most CUs
+        # idle (its trial is a chain of small dependent launches)
+        K = args.ba_concurrent
+        probs = [synth.localba_problem(seed=7 + 1000 * rank + 17 * k) for k in range(K)]
+        opts = [Optimizer(dev.index) for _ in range(K)]
+        for o, Pk in zip(opts, probs):
+            o.LocalBundleAdjustment(Pk)
+        kits = [0] * K
+
+        def run(k):
+            for _ in range(args.ba_calls):
+                kits[k] += sum(opts[k].LocalBundleAdjustment(probs[k])["iterations"])
+
+        th = [threading.Thread(target=run, args=(k,)) for k in range(K)]
+        odist.barrier()
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize(dev)
+        odist.barrier()
+        elk = odist.max_over_ranks(time.perf_counter() - t0, dev)
+        its_k = odist.sum_over_ranks(float(sum(kits)), dev)
+        for o in opts:
+            o.close()
+        out["concurrent"] = dict(problems_per_gpu=K, iters_per_s=round(its_k / elk, 2),
+                                 ms_per_call=round(elk / args.ba_calls * 1e3, 3),
+                                 note="K independent config-4-shaped problems (different seeds) in flight per GPU, "
+                                      "one host thread + HIP stream each; aggregate LM iterations/s")
     if rank == 0 and world == 1 and oracle_mod is not None:
         old = os.sched_getaffinity(0) if hasattr(os, "sched_setaffinity") else None
         try:
