@@ -46,5 +46,6 @@ def run(S, B, steps=20):
 
 
 if __name__ == "__main__":
-    for S, B in [(1, 256), (2, 256), (2, 128), (3, 128), (4, 128)]:
+    combos = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]] or [(1, 256), (2, 256), (2, 128), (3, 128), (4, 128)]
+    for S, B in combos:
         print(json.dumps(run(S, B)), flush=True)
