@@ -326,7 +326,8 @@ def localba_leg(args, rank, world, dev, odist, oracle_mod=None, flags=None, cpus
 def config3_leg(args, rank, world, dev, odist, stream, oracle_mod=None, flags=None, cpus=None):
     """EuRoC MH_01-shaped stereo (752x480, 1200 features) + PnP RANSAC per frame (BASELINE configs[2]):
     a step = extract L+R + stereo match of B3 frames (one per synthetic sequence, device batch) and, per
-    frame, a fresh PnPsolver (1,200 matches, 40 % outliers, Tracking's (0.99,10,300,4,0.5,5.991)) run by
+    frame, a fresh PnPsolver over its device-resident correspondences (1,200 matches, 40 % outliers,
+    Tracking's (0.99,10,300,4,0.5,5.991)) run by
     iterate(5) on that sequence's own rand() stream -- all B3 solvers in one orbx_pnp_iterate_many call.
     Returns whole-job frames/s (+ the split) and a single-core oracle baseline of the same unit."""
     import torch
@@ -350,11 +351,18 @@ def config3_leg(args, rank, world, dev, odist, stream, oracle_mod=None, flags=No
     probs = [synth.pnp_problem(seed=3000 * (rank + 1) + f, n=1200, outlier_frac=0.4) for f in range(B3)]
     rngs = [GlibcRand(1 + f + 1000 * rank) for f in range(B3)]  # one process rand() per sequence
     prm = (0.99, 10, 300, 4, 0.5, 5.991)
+    # the frames' 3D-2D correspondences resident in HBM back to back (as a device matcher leaves them)
+    offs = np.concatenate([[0], np.cumsum([len(P["p3d"]) for P in probs])]).astype(np.int32)
+    d_p3d = torch.from_numpy(np.concatenate([P["p3d"] for P in probs]).astype(np.float32)).to(dev)
+    d_p2d = torch.from_numpy(np.concatenate([P["p2d"] for P in probs]).astype(np.float32)).to(dev)
+    d_s2 = torch.from_numpy(np.concatenate([P["sigma2"] for P in probs]).astype(np.float32)).to(dev)
+    intr = np.array([[P["fx"], P["fy"], P["cx"], P["cy"]] for P in probs], np.float32)
 
     def step():
         ex.stereo_frames_device(images, kps, desc, counts, bf, baseline, uR, depth, nmatch, stream)
         t_e = time.perf_counter()
-        solvers = PnPsolver.create_many(probs, *prm, device=dev.index)  # a new PnPsolver per frame
+        # a new PnPsolver per frame, from the device-resident correspondences
+        solvers = PnPsolver.create_many_device(d_p3d, d_p2d, d_s2, offs, intr, *prm, device=dev.index)
         t_c = time.perf_counter()
         res = pnp_iterate_many(solvers, 5, rngs)
         t_r = time.perf_counter()

@@ -279,6 +279,12 @@ orbx_status orbx_pnp_create(const orbx_pnp_problem* problem, const orbx_pnp_para
  * solver is released with orbx_pnp_destroy. */
 orbx_status orbx_pnp_create_many(const orbx_pnp_problem* problems, int n, const orbx_pnp_params* params, int device,
                                  orbx_pnp** out);
+/* The same from device-resident correspondences (e.g. the matches a device SearchByBoW produced):
+ * problem i is rows offsets[i] .. offsets[i+1]-1 of d_p3d (x3), d_p2d (x2), d_sigma2 (device
+ * pointers); offsets[n+1] and intr[4n] (fx, fy, cx, cy per problem) are host arrays. */
+orbx_status orbx_pnp_create_many_device(const float* d_p3d, const float* d_p2d, const float* d_sigma2,
+                                        const int32_t* offsets, const float* intr, int n,
+                                        const orbx_pnp_params* params, int device, orbx_pnp** out);
 orbx_status orbx_pnp_destroy(orbx_pnp* h);
 /* Derived RANSAC parameters (mRansacMinInliers, mRansacMaxIts, mRansacEpsilon). */
 orbx_status orbx_pnp_get_params(const orbx_pnp* h, int* min_inliers, int* max_iterations, float* epsilon);

@@ -146,6 +146,7 @@ SIGNATURES = {
     "orbx_search_by_bow_device": ([C.POINTER(BowProblem), C.c_int, P], C.c_int),
     "orbx_pnp_create": ([C.POINTER(PnpProblem), C.POINTER(PnpParams), C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "orbx_pnp_create_many": ([P, C.c_int, C.POINTER(PnpParams), C.c_int, P], C.c_int),
+    "orbx_pnp_create_many_device": ([P, P, P, P, P, C.c_int, C.POINTER(PnpParams), C.c_int, P], C.c_int),
     "orbx_pnp_destroy": ([P], C.c_int),
     "orbx_pnp_get_params": ([P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)], C.c_int),
     "orbx_pnp_iterate": ([P, C.c_int, P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), P, P,

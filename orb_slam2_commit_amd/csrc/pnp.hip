@@ -1033,6 +1033,29 @@ __global__ __launch_bounds__(256) void k_pnp_gather(const PnpGatherJob* __restri
   for (int i = threadIdx.x; i < J.n; i += 256) J.dst[i] = J.src[i];
 }
 
+// correspondences of device-resident problems into their solvers' blocks (orbx_pnp_create_many_device):
+// p3d, p2d copied, maxError = sigma2 * th2 (src/PnPsolver.cc:107, the float product of the host path)
+struct PnpSetupJob {
+  const float* p3d;
+  const float* p2d;
+  const float* sigma2;
+  float* d_p3d;
+  float* d_p2d;
+  float* d_maxerr;
+  int n;
+};
+__global__ __launch_bounds__(256) void k_pnp_setup(const PnpSetupJob* __restrict__ jobs, float th2) {
+  const PnpSetupJob J = jobs[blockIdx.x];
+  for (int i = threadIdx.x; i < J.n; i += 256) {
+    J.d_p3d[3 * i] = J.p3d[3 * i];
+    J.d_p3d[3 * i + 1] = J.p3d[3 * i + 1];
+    J.d_p3d[3 * i + 2] = J.p3d[3 * i + 2];
+    J.d_p2d[2 * i] = J.p2d[2 * i];
+    J.d_p2d[2 * i + 1] = J.p2d[2 * i + 1];
+    J.d_maxerr[i] = J.sigma2[i] * th2;
+  }
+}
+
 }  // namespace orbx
 
 // ------------------------------------------------------------------ host / C ABI
@@ -1328,6 +1351,50 @@ orbx_status orbx_pnp_create_many(const orbx_pnp_problem* problems, int n, const 
   hipStream_t st = dev.st;
   if (hipMemcpyAsync(dp, hp, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return fail(ORBX_ERR_HIP);
   hipLaunchKernelGGL(orbx::k_pnp_gather, dim3(n), dim3(256), 0, st, (const orbx::PnpGatherJob*)dp);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return fail(ORBX_ERR_HIP);
+  for (int i = 0; i < n; i++) out[i] = hs[i];
+  return ORBX_OK;
+}
+
+orbx_status orbx_pnp_create_many_device(const float* d_p3d, const float* d_p2d, const float* d_sigma2,
+                                        const int32_t* offsets, const float* intr, int n,
+                                        const orbx_pnp_params* prm, int device, orbx_pnp** out) {
+  if (n < 0 || (n > 0 && (!offsets || !intr || !out || !prm))) return ORBX_ERR_ARG;
+  if (n == 0) return ORBX_OK;
+  if (!d_p3d || !d_p2d || !d_sigma2 || prm->min_set < 1 || prm->min_set > orbx::kPnpMaxSet) return ORBX_ERR_ARG;
+  for (int i = 0; i < n; i++) {
+    if (offsets[i + 1] < offsets[i]) return ORBX_ERR_ARG;
+    out[i] = nullptr;
+  }
+  orbx_status s = pnp_device_check(device);
+  if (s != ORBX_OK) return s;
+  PnpDevice& dev = g_pnp_dev[device];
+  std::lock_guard<std::mutex> lock(dev.mu);
+  std::vector<orbx_pnp*> hs(n, nullptr);
+  auto fail = [&](orbx_status code) {
+    for (orbx_pnp* h : hs)
+      if (h) {
+        if (h->d_mem) (void)hipFreeAsync(h->d_mem, h->st);
+        delete h;
+      }
+    return code;
+  };
+  const size_t bytes = n * sizeof(orbx::PnpSetupJob);
+  if (dev.pinned_reserve(bytes) != hipSuccess || dev.dstage_reserve(bytes) != hipSuccess) return fail(ORBX_ERR_HIP);
+  orbx::PnpSetupJob* jobs = (orbx::PnpSetupJob*)dev.pinned;
+  for (int i = 0; i < n; i++) {
+    const orbx_pnp_problem p{offsets[i + 1] - offsets[i], nullptr, nullptr, nullptr, intr[4 * i], intr[4 * i + 1],
+                             intr[4 * i + 2], intr[4 * i + 3]};
+    hs[i] = pnp_new(&p, prm, device);
+    if (!hs[i]) return fail(ORBX_ERR_HIP);
+    if (hs[i]->alloc(std::max(hs[i]->max_its, 8)) != hipSuccess) return fail(ORBX_ERR_HIP);
+    const size_t o = (size_t)offsets[i];
+    jobs[i] = orbx::PnpSetupJob{d_p3d + 3 * o, d_p2d + 2 * o, d_sigma2 + o, hs[i]->d_p3d, hs[i]->d_p2d,
+                                hs[i]->d_maxerr, p.n};
+  }
+  hipStream_t st = dev.st;
+  if (hipMemcpyAsync(dev.dstage, dev.pinned, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return fail(ORBX_ERR_HIP);
+  hipLaunchKernelGGL(orbx::k_pnp_setup, dim3(n), dim3(256), 0, st, (const orbx::PnpSetupJob*)dev.dstage, prm->th2);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return fail(ORBX_ERR_HIP);
   for (int i = 0; i < n; i++) out[i] = hs[i];
   return ORBX_OK;

@@ -597,6 +597,35 @@ class PnPsolver:
             o._done = 0
         return objs
 
+    @classmethod
+    def create_many_device(cls, p3d, p2d, sigma2, offsets, intr, probability=0.99, minInliers=8,
+                           maxIterations=300, minSet=4, epsilon=0.4, th2=5.991, device=0):
+        """Solvers over device-resident correspondences: p3d [M,3], p2d [M,2], sigma2 [M] float32 device
+        tensors holding the problems back to back (problem i = rows offsets[i]..offsets[i+1]-1), intr [n,4]
+        (fx, fy, cx, cy) on the host -- one orbx_pnp_create_many_device call."""
+        offs = np.ascontiguousarray(offsets, np.int32)
+        it = np.ascontiguousarray(intr, np.float32).reshape(-1, 4)
+        n = len(offs) - 1
+        prm = _lib.PnpParams(float(probability), int(minInliers), int(maxIterations), int(minSet), float(epsilon),
+                             float(th2))
+        hs = (C.c_void_p * max(n, 1))()
+        check(_lib.lib().orbx_pnp_create_many_device(C.c_void_p(p3d.data_ptr()), C.c_void_p(p2d.data_ptr()),
+                                                     C.c_void_p(sigma2.data_ptr()), ptr(offs), ptr(it), n,
+                                                     C.byref(prm), int(device), hs), "orbx_pnp_create_many_device")
+        objs = []
+        for i in range(n):
+            o = cls.__new__(cls)
+            o.n = int(offs[i + 1] - offs[i])
+            o.device = int(device)
+            o._h = C.c_void_p(hs[i])
+            o.min_set = int(minSet)
+            a, b, c = C.c_int(), C.c_int(), C.c_float()
+            check(_lib.lib().orbx_pnp_get_params(o._h, C.byref(a), C.byref(b), C.byref(c)), "orbx_pnp_get_params")
+            o.min_inliers, o.max_its, o.epsilon = a.value, b.value, c.value
+            o._done = 0
+            objs.append(o)
+        return objs
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().orbx_pnp_destroy(self._h)

@@ -358,3 +358,32 @@ def test_gpu_pnp_create_many_equals_create(gpu):
         assert ga.peek(4) == gb.peek(4)
     for s in many + one:
         s.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pnp_create_many_device_equals_host(gpu):
+    """orbx_pnp_create_many_device (correspondences already in HBM, back to back) == the host form."""
+    import torch
+    from orb_slam2_commit_amd import PnPsolver
+    from orb_slam2_commit_amd.orb import pnp_iterate_many
+    probs = [_reloc_problem(k, 110 + i) for i, k in enumerate(["good", "few", "bad", "hard", "good", "good"])]
+    offs = np.concatenate([[0], np.cumsum([len(P["p3d"]) for P in probs])]).astype(np.int32)
+    cat = lambda key, w: torch.from_numpy(np.ascontiguousarray(  # noqa: E731
+        np.concatenate([np.asarray(P[key], np.float32).reshape(-1, w) for P in probs]))).to(gpu)
+    intr = np.array([[P["fx"], P["fy"], P["cx"], P["cy"]] for P in probs], np.float32)
+    dev = PnPsolver.create_many_device(cat("p3d", 3), cat("p2d", 2), cat("sigma2", 1).reshape(-1), offs, intr,
+                                       *TRACKING_PARAMS)
+    host = PnPsolver.create_many(probs, *TRACKING_PARAMS)
+    ga = [GlibcRand(1 + i) for i in range(len(probs))]
+    gb = [GlibcRand(1 + i) for i in range(len(probs))]
+    for a, b in zip(dev, host):
+        assert (a.min_inliers, a.max_its, a.epsilon) == (b.min_inliers, b.max_its, b.epsilon)
+    ra, rb = pnp_iterate_many(dev, 5, ga), pnp_iterate_many(host, 5, gb)
+    for (Ta, nma, inla, nia), (Tb, nmb, inlb, nib) in zip(ra, rb):
+        assert (Ta is None) == (Tb is None) and nma == nmb and nia == nib
+        if Ta is not None:
+            np.testing.assert_array_equal(Ta, Tb)
+            np.testing.assert_array_equal(inla, inlb)
+    assert [g.peek(2) for g in ga] == [g.peek(2) for g in gb]
+    for s in dev + host:
+        s.close()
