@@ -1259,6 +1259,269 @@ __global__ __launch_bounds__(LBS) void k_ba_restore(BaDev D) {
   }
 }
 
+// Block-wide exclusive scan of one int per thread under `op` (identity
+// `ident`); *total gets the reduction over the block.  ws: NT/64 ints of LDS.
+template <int NT, typename Op>
+__device__ inline int ba_block_scan(int v, int ident, Op op, int* ws, int* total) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x = op(x, y);
+  }
+  if (lane == 63) ws[w] = x;
+  __syncthreads();
+  if (w == 0) {  // scan of the wave totals: NW lanes of wave 0
+    int s = lane < NW ? ws[lane] : ident;
+    for (int d = 1; d < NW; d <<= 1) {
+      const int y = __shfl_up(s, d, 64);
+      if (lane >= d) s = op(s, y);
+    }
+    if (lane < NW) ws[lane] = s;
+  }
+  __syncthreads();
+  int ex = __shfl_up(x, 1, 64);
+  if (lane == 0) ex = ident;
+  const int r = w ? op(ws[w - 1], ex) : ex;
+  *total = ws[NW - 1];
+  __syncthreads();  // ws free for the next scan
+  return r;
+}
+
+// Lanes of the wave holding the same key (keys < 2^nbits): one ballot per bit.
+__device__ inline uint64_t ba_match(int key, int nbits) {
+  uint64_t m = ~0ull;
+  for (int b = 0; b < nbits; b++) {
+    const bool s = (key >> b) & 1;
+    const uint64_t bal = __ballot(s);
+    m &= s ? bal : ~bal;
+  }
+  return m;
+}
+
+// Active-edge structure of a phase on the device: build_structure's one-pass
+// (edges grouped by point) path, same arrays, same order, in three launches
+// over tiles of kTileE edges (kTileT threads x kStructV contiguous edges, so
+// positions keep edge order):
+//  k_ba_struct_count  per tile: active edges per camera, active count,
+//                     first/last active point, point segments inside the tile;
+//  k_ba_struct_scan   one block: camera totals -> pose tables (one camera per
+//                     thread, nc <= kStructMaxNc), per (tile, camera) cam_pos
+//                     offsets, per tile position/point/segment carries, boff
+//                     and the five sizes;
+//  k_ba_struct_fill   per tile: act/pos_pt/pcam/pt_off/pt_id, and cam_pos as a
+//                     stable per-wave multisplit of the tile's positions by
+//                     camera (bitwise match, no atomics), ascending in a pose.
+constexpr int kTileT = 256, kStructV = 8, kTileE = kTileT * kStructV;  // kTileE < 2^16: packed scans
+constexpr int kStructNT = 1024, kStructMaxNc = 512, kStructMaxTiles = kStructNT;
+
+__device__ inline void ba_tile_load(const BaDev& D, const uint8_t* __restrict__ flag, int lvl, int e0, bool* a,
+                                    int* pt, int* cm) {
+#pragma unroll
+  for (int j = 0; j < kStructV; j++) {
+    const int e = e0 + j;
+    const bool in = e < D.ne;
+    pt[j] = in ? D.ept[e] : -1;
+    cm[j] = in ? D.ecam[e] : 0;
+    a[j] = in && (lvl < 0 || flag[e] == lvl);
+  }
+}
+
+struct BaAdd {
+  __device__ int operator()(int a, int b) const { return a + b; }
+};
+struct BaMax {
+  __device__ int operator()(int a, int b) const { return a > b ? a : b; }
+};
+struct BaMin {
+  __device__ int operator()(int a, int b) const { return a < b ? a : b; }
+};
+
+__global__ __launch_bounds__(kTileT) void k_ba_struct_count(BaDev D, const uint8_t* __restrict__ flag, int lvl,
+                                                            int* __restrict__ tcnt, int4* __restrict__ ttot) {
+  constexpr int V = kStructV;
+  extern __shared__ int sm_sc[];
+  const int nc = D.nc, t = threadIdx.x, tile = blockIdx.x;
+  int* hc = sm_sc;    // nc
+  int* ws = hc + nc;  // kTileT/64
+  for (int i = t; i < nc; i += kTileT) hc[i] = 0;
+  bool a[V];
+  int pt[V], cm[V];
+  ba_tile_load(D, flag, lvl, tile * kTileE + t * V, a, pt, cm);
+  __syncthreads();
+  int nact = 0, lastp = -1, firstp = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < V; j++)
+    if (a[j]) {
+      atomicAdd(&hc[cm[j]], 1);
+      nact++;
+      lastp = pt[j];
+      firstp = min(firstp, pt[j]);
+    }
+  int tlast, tot, tfirst;
+  // points ascend along the edge list: the max over earlier edges is the
+  // point of the last active edge before this thread's (-1: none in the tile)
+  const int p = ba_block_scan<kTileT>(lastp, -1, BaMax(), ws, &tlast);
+  int nseg = 0;
+#pragma unroll
+  for (int j = 0, q = p; j < V; j++)
+    if (a[j]) {
+      nseg += pt[j] != q;
+      q = pt[j];
+    }
+  (void)ba_block_scan<kTileT>(nact | nseg << 16, 0, BaAdd(), ws, &tot);
+  (void)ba_block_scan<kTileT>(firstp, 0x7fffffff, BaMin(), ws, &tfirst);
+  for (int i = t; i < nc; i += kTileT) tcnt[(size_t)tile * nc + i] = hc[i];
+  if (t == 0) ttot[tile] = make_int4(tot & 0xffff, tfirst, tlast, tot >> 16);
+}
+
+__global__ __launch_bounds__(kStructNT) void k_ba_struct_scan(BaDev D, const uint8_t* __restrict__ fixed, int ntiles,
+                                                              int* __restrict__ tcnt, const int4* __restrict__ ttot,
+                                                              int4* __restrict__ tcar, int* __restrict__ out) {
+  constexpr int NT = kStructNT;
+  extern __shared__ int sm_ss[];
+  const int nc = D.nc, t = threadIdx.x;
+  int* coff = sm_ss;        // nposes+1
+  int* ws = coff + nc + 1;  // NW
+  // camera totals; tcnt becomes each tile's offset inside its camera's run
+  int cc = 0;
+  if (t < nc)
+    for (int i0 = 0; i0 < ntiles; i0 += 8) {  // loads of 8 tiles in flight before their stores
+      int x[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) x[j] = i0 + j < ntiles ? tcnt[(size_t)(i0 + j) * nc + t] : 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        if (i0 + j < ntiles) tcnt[(size_t)(i0 + j) * nc + t] = cc;
+        cc += x[j];
+      }
+    }
+  int nposes, tot, maxc, na, npa, nslots, tmp;
+  const bool pose = t < nc && cc > 0 && !fixed[t];
+  const int pidx = ba_block_scan<NT>(pose ? 1 : 0, 0, BaAdd(), ws, &nposes);
+  const int pofs = ba_block_scan<NT>(pose ? cc : 0, 0, BaAdd(), ws, &tot);
+  (void)ba_block_scan<NT>(pose ? cc : 0, 0, BaMax(), ws, &maxc);
+  if (t < nc) D.chidx[t] = pose ? pidx : -1;
+  if (pose) {
+    D.pose_cam[pidx] = t;
+    coff[pidx] = pofs;
+    D.cam_off[pidx] = pofs;
+  }
+  // tile carries: first position, last active point before the tile, first segment
+  const int4 tt = t < ntiles ? ttot[t] : make_int4(0, 0x7fffffff, -1, 0);
+  const int kb = ba_block_scan<NT>(tt.x, 0, BaAdd(), ws, &na);
+  const int pv = ba_block_scan<NT>(tt.z, -1, BaMax(), ws, &tmp);
+  const int sg = tt.w - (tt.x > 0 && tt.y == pv ? 1 : 0);  // first point continues the previous tile's
+  const int sb = ba_block_scan<NT>(sg, 0, BaAdd(), ws, &npa);
+  if (t < ntiles) tcar[t] = make_int4(kb, pv, sb, 0);
+  if (t == 0) {
+    coff[nposes] = tot;
+    D.cam_off[nposes] = tot;
+    D.pt_off[npa] = na;
+  }
+  __syncthreads();
+  // boff: block (c1, c2 >= c1) holds one slot per position of pose c1
+  const int n1 = t < nposes ? coff[t + 1] - coff[t] : 0;
+  const int q = ba_block_scan<NT>(t < nposes ? n1 * (nposes - t) : 0, 0, BaAdd(), ws, &nslots);
+  if (t < nposes) {
+    const int b0 = t * nposes - t * (t - 1) / 2;
+    for (int j = 0; j < nposes - t; j++) D.boff[b0 + j] = q + j * n1;
+  }
+  if (t == 0) {
+    D.boff[nposes * (nposes + 1) / 2] = nslots;
+    out[0] = na;
+    out[1] = npa;
+    out[2] = nposes;
+    out[3] = maxc;
+    out[4] = nslots;
+  }
+}
+
+__global__ __launch_bounds__(kTileT) void k_ba_struct_fill(BaDev D, const uint8_t* __restrict__ flag, int lvl,
+                                                           const int* __restrict__ tcnt,
+                                                           const int4* __restrict__ tcar) {
+  constexpr int V = kStructV, NW = kTileT / 64;
+  extern __shared__ int sm_sf[];
+  const int nc = D.nc, t = threadIdx.x, lane = t & 63, w = t >> 6, tile = blockIdx.x;
+  int* chl = sm_sf;        // nc: pose index per camera
+  int* cw = chl + nc;      // NW*nc: per-wave camera counts, then fill cursors
+  int* lpc = cw + NW * nc; // kTileE: camera of each tile position (-1: fixed)
+  int* ws = lpc + kTileE;  // NW
+  for (int i = t; i < nc; i += kTileT) chl[i] = D.chidx[i];
+  for (int i = t; i < NW * nc; i += kTileT) cw[i] = 0;
+  const int4 car = tcar[tile];
+  bool a[V];
+  int pt[V], cm[V];
+  const int e0 = tile * kTileE + t * V;
+  ba_tile_load(D, flag, lvl, e0, a, pt, cm);
+  int nact = 0, lastp = -1;
+#pragma unroll
+  for (int j = 0; j < V; j++) {
+    nact += a[j];
+    if (a[j]) lastp = pt[j];
+  }
+  int tlast, tks;
+  int p = max(car.y, ba_block_scan<kTileT>(lastp, -1, BaMax(), ws, &tlast));
+  int nseg = 0;
+#pragma unroll
+  for (int j = 0, q = p; j < V; j++)
+    if (a[j]) {
+      nseg += pt[j] != q;
+      q = pt[j];
+    }
+  const int ks = ba_block_scan<kTileT>(nact | nseg << 16, 0, BaAdd(), ws, &tks);
+  int kl = ks & 0xffff;
+  int s = car.z + (ks >> 16) - 1;
+#pragma unroll
+  for (int j = 0; j < V; j++)
+    if (a[j]) {
+      if (pt[j] != p) {
+        s++;
+        D.pt_off[s] = car.x + kl;
+        D.pt_id[s] = pt[j];
+        p = pt[j];
+      }
+      const int pc = chl[cm[j]];
+      D.act[car.x + kl] = e0 + j;
+      D.pos_pt[car.x + kl] = s;
+      D.pcam[car.x + kl] = pc;
+      lpc[kl] = pc >= 0 ? cm[j] : -1;
+      kl++;
+    }
+  __syncthreads();
+  // cam_pos: stable multisplit of the tile's positions by camera
+  const int nt = tks & 0xffff, nbits = 32 - __clz(nc);
+  const int R = (((nt + NW - 1) / NW) + 63) & ~63;
+  const int k0 = min(w * R, nt), k1 = min(k0 + R, nt);
+  for (int kb = k0; kb < k1; kb += 64) {
+    const int kk = kb + lane;
+    const int c = kk < k1 ? lpc[kk] : -1;
+    const uint64_t m = ba_match(c >= 0 ? c : nc, nbits);
+    if (c >= 0 && __popcll(m & ((1ull << lane) - 1)) == 0) cw[w * nc + c] += __popcll(m);
+  }
+  __syncthreads();
+  for (int c = t; c < nc; c += kTileT)
+    if (chl[c] >= 0) {
+      int run = D.cam_off[chl[c]] + tcnt[(size_t)tile * nc + c];
+      for (int v = 0; v < NW; v++) {
+        const int x = cw[v * nc + c];
+        cw[v * nc + c] = run;
+        run += x;
+      }
+    }
+  __syncthreads();
+  for (int kb = k0; kb < k1; kb += 64) {
+    const int kk = kb + lane;
+    const int c = kk < k1 ? lpc[kk] : -1;
+    const uint64_t m = ba_match(c >= 0 ? c : nc, nbits);
+    const int r = __popcll(m & ((1ull << lane) - 1));
+    const int b = c >= 0 ? cw[w * nc + c] : 0;
+    if (c >= 0) D.cam_pos[b + r] = car.x + kk;
+    if (c >= 0 && r == 0) cw[w * nc + c] = b + __popcll(m);
+  }
+}
+
 // phase transition (:764-802) and the final erase test (:817-847): per edge
 // chi2 of its stored error against th, and depth of the current estimate
 __global__ __launch_bounds__(LBS) void k_ba_outliers(BaDev D, uint8_t* flag, int drop_kernel) {
@@ -1418,6 +1681,7 @@ struct LocalBA {
   ~LocalBA() {
     if (rb_host) (void)hipHostFree(rb_host);
     if (rb_ev) (void)hipEventDestroy(rb_ev);
+    if (sint_host) (void)hipHostFree(sint_host);
   }
   static void use_lin(BaDev& D, const LinSet& L) {
     D.Hpl = L.Hpl;
@@ -1448,8 +1712,14 @@ struct LocalBA {
   // reference adds them per MapPoint, Optimizer.cc:659-745) take the one-pass
   // path; otherwise a stable counting sort by point.  Schur pairs are found on
   // the device (k_ba_pairs), not listed here.
-  double t_struct[4] = {0, 0, 0, 0};  // host ms: index/CSR, pose groups, (unused), upload+alloc
+  double t_struct[4] = {0, 0, 0, 0};  // host ms: index/CSR, pose groups, device build, upload+alloc
+  bool dev_struct = false;  // k_ba_struct_* build the arrays (edges grouped by point, nc <= kStructMaxNc)
+  const uint8_t* dfix = nullptr;  // device copy of the fixed flags
+  DBuf<int> sbuf;                 // k_ba_struct_* tiles and outputs, sized for the whole edge list
+  int* sint_host = nullptr;       // pinned: k_ba_struct_scan's five sizes
+  int sizes1[5] = {0, 0, 0, 0, 0};  // phase-1 sizes (all edges active), counted on the host
   orbx_status build_structure(int lvl, hipStream_t st) {
+    if (dev_struct) return build_structure_dev(lvl, st, lvl < 0 ? sizes1 : nullptr);
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
@@ -1479,7 +1749,6 @@ struct LocalBA {
     const int nposes = (int)pose_cam.size();
     int maxc = 0;
     for (int ci = 0; ci < nposes; ci++) maxc = std::max(maxc, cam_off[ci + 1] - cam_off[ci]);
-    const int gsplit = std::min(std::max((maxc + 2 * kGB - 1) / (2 * kGB), 1), 64);  // ~2 positions per thread
     act.resize(na);
     pos_pt.resize(na);
     pcam.resize(na);
@@ -1551,6 +1820,68 @@ struct LocalBA {
     D.pcam = A.put(pcam);
     D.boff = A.put(boff);
     BA_CHECK(A.upload(st));
+    const orbx_status fs = finish_structure(na, npa, nposes, maxc, boff.back(), st);
+    const auto T4 = now();
+    t_struct[0] += ms(T0, T1);
+    t_struct[1] += ms(T1, T2);
+    t_struct[2] += ms(T2, T3);
+    t_struct[3] += ms(T3, T4);
+    return fs;
+  }
+
+  // The same arrays built by k_ba_struct_* from the device-resident edge list
+  // and phase flags (no host copy of the flags, no upload); one readback of
+  // the five sizes the launch grids and allocations need (none when the
+  // sizes are known: phase 1, every edge active).
+  orbx_status build_structure_dev(int lvl, hipStream_t st, const int* known) {
+    const auto T0 = std::chrono::steady_clock::now();
+    const int nc = D.nc, ne = D.ne;
+    const int ntiles = (ne + kTileE - 1) / kTileE;
+    const size_t nb = (size_t)nc * (nc + 1) / 2 + 1;
+    BA_CHECK(sbuf.alloc(8 * (size_t)ntiles + (size_t)ntiles * nc + 6 * (size_t)ne + 1 + 3 * (size_t)nc + 1 + nb + 8));
+    if (!sint_host) BA_CHECK(hipHostMalloc((void**)&sint_host, 8 * sizeof(int), hipHostMallocDefault));
+    int* p = sbuf.p;
+    int4* ttot = reinterpret_cast<int4*>(p);  // first: 16-byte aligned
+    p += 4 * (size_t)ntiles;
+    int4* tcar = reinterpret_cast<int4*>(p);
+    p += 4 * (size_t)ntiles;
+    int* tcnt = p;
+    p += (size_t)ntiles * nc;
+    D.act = p, p += ne;
+    D.pos_pt = p, p += ne;
+    D.pcam = p, p += ne;
+    D.cam_pos = p, p += ne;
+    D.pt_id = p, p += ne;
+    D.pt_off = p, p += ne + 1;
+    D.chidx = p, p += nc;
+    D.pose_cam = p, p += nc;
+    D.cam_off = p, p += nc + 1;
+    D.boff = p, p += nb;
+    const uint8_t* fl = lvl < 0 ? nullptr : (const uint8_t*)c.flag.p;
+    if (ntiles > 0)
+      hipLaunchKernelGGL(k_ba_struct_count, dim3(ntiles), dim3(kTileT), sizeof(int) * (nc + kTileT / 64), st, D, fl,
+                         lvl, tcnt, ttot);
+    hipLaunchKernelGGL(k_ba_struct_scan, dim3(1), dim3(kStructNT), sizeof(int) * (nc + 1 + kStructNT / 64), st, D,
+                       dfix, ntiles, tcnt, ttot, tcar, p);
+    if (ntiles > 0)
+      hipLaunchKernelGGL(k_ba_struct_fill, dim3(ntiles), dim3(kTileT),
+                         sizeof(int) * ((1 + kTileT / 64) * (size_t)nc + kTileE + kTileT / 64), st, D, fl, lvl, tcnt,
+                         tcar);
+    BA_CHECK(hipGetLastError());
+    const int* sz = known;
+    if (!sz) {
+      BA_CHECK(hipMemcpyAsync(sint_host, p, 5 * sizeof(int), hipMemcpyDeviceToHost, st));
+      BA_CHECK(hipStreamSynchronize(st));
+      sz = sint_host;
+    }
+    const orbx_status fs = finish_structure(sz[0], sz[1], sz[2], sz[3], sz[4], st);
+    t_struct[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
+    return fs;
+  }
+
+  // Sizes known: scratch allocations, readback block, Schur pair table.
+  orbx_status finish_structure(int na, int npa, int nposes, int maxc, int nslots, hipStream_t st) {
+    const int gsplit = std::min(std::max((maxc + 2 * kGB - 1) / (2 * kGB), 1), 64);  // ~2 positions per thread
     const size_t N = 6 * (size_t)nposes;
     BA_CHECK(c.Hpl.alloc(18 * (size_t)na));
     BA_CHECK(c.ptc.alloc(12 * (size_t)na));
@@ -1593,7 +1924,7 @@ struct LocalBA {
       BA_CHECK(hipHostMalloc((void**)&rb_host, n_rb * sizeof(double), hipHostMallocDefault));
       rb_cap = n_rb;
     }
-    BA_CHECK(c.ptab.alloc(boff.back()));
+    BA_CHECK(c.ptab.alloc(nslots));
     D.ptab = c.ptab.p;
     if (D.nblk > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk, gsplit), dim3(kPB), 0, st, D);
     BA_CHECK(hipGetLastError());
@@ -1609,11 +1940,6 @@ struct LocalBA {
     lin[1] = LinSet{Hpl2.p, Hll2.p, bl2.p, dmax2.p, Hpp2.p, bp2.p};
     lin_cur = 0;
     use_lin(D, lin[0]);
-    const auto T4 = now();
-    t_struct[0] += ms(T0, T1);
-    t_struct[1] += ms(T1, T2);
-    t_struct[2] += ms(T2, T3);
-    t_struct[3] += ms(T3, T4);
     return ORBX_OK;
   }
 
@@ -1765,9 +2091,31 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   D.nc = nc;
   D.np = np;
   D.ne = ne;
-  for (int e = 0; e < ne; e++)
+  bool grouped = true;  // edges ordered by point (the reference adds them per MapPoint)
+  L.ccnt.assign(nc, 0);
+  int npts = 0;
+  for (int e = 0; e < ne; e++) {
     if (pb->edge_point[e] < 0 || pb->edge_point[e] >= np || pb->edge_cam[e] < 0 || pb->edge_cam[e] >= nc)
       return ORBX_ERR_ARG;
+    grouped &= e == 0 || pb->edge_point[e] >= pb->edge_point[e - 1];
+    npts += e == 0 || pb->edge_point[e] != pb->edge_point[e - 1];
+    L.ccnt[pb->edge_cam[e]]++;
+  }
+  L.dev_struct = grouped && nc <= kStructMaxNc && (ne + kTileE - 1) / kTileE <= kStructMaxTiles &&
+                 std::getenv("ORBX_BA_HOST_STRUCT") == nullptr;
+  if (L.dev_struct) {  // phase-1 sizes: the launches need no readback
+    int nposes = 0, maxc = 0;
+    for (int i = 0; i < nc; i++)
+      if (L.ccnt[i] && !(pb->fixed && pb->fixed[i])) {
+        nposes++;
+        maxc = std::max(maxc, L.ccnt[i]);
+      }
+    int nslots = 0;
+    for (int i = 0, j = 0; i < nc; i++)
+      if (L.ccnt[i] && !(pb->fixed && pb->fixed[i])) nslots += L.ccnt[i] * (nposes - j++);
+    const int s1[5] = {ne, npts, nposes, maxc, nslots};
+    std::memcpy(L.sizes1, s1, sizeof s1);
+  }
   L.e_pt.assign(pb->edge_point, pb->edge_point + ne);
   L.e_cam.assign(pb->edge_cam, pb->edge_cam + ne);
   L.fixed.assign(nc, 0);
@@ -1775,7 +2123,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   Arena& A = L.prob_arena;
   if (A.reserve(arena_bytes({32 * (size_t)nc, 24 * (size_t)nc, 40 * (size_t)nc, 24 * (size_t)np, 4 * (size_t)ne,
                              4 * (size_t)ne, (size_t)ne, 24 * (size_t)ne, 8 * (size_t)ne, 8 * (size_t)ne,
-                             4 * (size_t)ne, (size_t)ne})) != hipSuccess)
+                             4 * (size_t)ne, (size_t)ne, (size_t)nc})) != hipSuccess)
     return ORBX_ERR_HIP;
   double* cq = A.take<double>(4 * (size_t)nc);
   double* ct = A.take<double>(3 * (size_t)nc);
@@ -1789,6 +2137,8 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   double* edelta = A.take<double>(ne);
   float* edsqr = A.take<float>(ne);
   uint8_t* erob = A.take<uint8_t>(ne);
+  uint8_t* dfix = A.take<uint8_t>(nc);
+  L.dfix = dfix;
   // vertices: Converter::toSE3Quat (float -> double, Quaterniond(R), normalize)
   {
     double* hq = A.host(cq);
@@ -1808,6 +2158,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       ht[3 * i + 2] = T[11];
       for (int k = 0; k < 5; k++) hi[5 * i + k] = pb->intr[5 * i + k];
       L.fixed[i] = pb->fixed ? pb->fixed[i] : 0;
+      A.host(dfix)[i] = L.fixed[i];
     }
     double* hx = A.host(X);
     for (int i = 0; i < 3 * np; i++) hx[i] = pb->Xw[i];
@@ -1861,7 +2212,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   bool ran = false;
   if (!(stop())) {  // src/Optimizer.cc:749-751
     ran = true;
-    L.level.assign(ne, 0);
+    if (!L.dev_struct) L.level.assign(ne, 0);
     const auto tb0 = std::chrono::steady_clock::now();
     orbx_status s = L.build_structure(-1, st);
     const auto tb1 = std::chrono::steady_clock::now();
@@ -1873,8 +2224,10 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       // :764-802 level-1 outliers, drop robust kernels
       if (ne > 0) hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 1);
       BA_CHECK(hipGetLastError());
-      BA_CHECK(hipMemcpyAsync(L.level.data(), c.flag.p, ne, hipMemcpyDeviceToHost, st));
-      BA_CHECK(hipStreamSynchronize(st));
+      if (!L.dev_struct) {
+        BA_CHECK(hipMemcpyAsync(L.level.data(), c.flag.p, ne, hipMemcpyDeviceToHost, st));
+        BA_CHECK(hipStreamSynchronize(st));
+      }
       const auto tb2 = std::chrono::steady_clock::now();
       s = L.build_structure(0, st);
       host_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb2).count();
@@ -1915,7 +2268,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   BA_CHECK(hipStreamSynchronize(st));
   if (std::getenv("ORBX_BA_TRACE"))
     std::fprintf(stderr,
-                 "[orbx_ba] total %.3f ms, host structure %.3f ms (index %.3f, poses %.3f, pairs %.3f, upload %.3f), "
+                 "[orbx_ba] total %.3f ms, structure %.3f ms (host index %.3f, host poses %.3f, device %.3f, upload %.3f), "
                  "iterations %d+%d, trials %d\n",
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(),
                  host_build_ms, L.t_struct[0], L.t_struct[1], L.t_struct[2], L.t_struct[3], res->iterations[0],

@@ -268,6 +268,37 @@ def test_gpu_localba_rejections_match_oracle(ba, name, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["config4", "small", "many_kfs", "no_outliers", "all_fixed", "empty", "one_edge"])
+def test_gpu_localba_device_structure_bit_identical(ba, case, monkeypatch):
+    """The per-phase active-edge structure built on the device (k_ba_struct: point
+    segments, pose indices, pose-grouped positions, pair-table offsets) gives
+    bit-identical poses, points, outlier flags and LM counts to the host build
+    (ORBX_BA_HOST_STRUCT=1), both phases (phase 2 reads the outlier flags on the device)."""
+    if case == "config4":
+        P = synth.localba_problem(seed=7)
+    elif case == "many_kfs":
+        P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
+    elif case == "no_outliers":
+        P = small_problem(seed=6, outlier_frac=0.0)
+    else:
+        P = dict(small_problem(seed=12))
+        if case == "all_fixed":
+            P["fixed"] = np.ones(len(P["fixed"]), np.uint8)
+        elif case in ("empty", "one_edge"):
+            n = 0 if case == "empty" else 1
+            for k in ("edge_point", "edge_cam", "obs", "inv_sigma2"):
+                P[k] = np.ascontiguousarray(np.asarray(P[k])[:n])
+    a = ba.LocalBundleAdjustment(P)
+    monkeypatch.setenv("ORBX_BA_HOST_STRUCT", "1")
+    b = ba.LocalBundleAdjustment(P)
+    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
+    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+    if case in ("config4", "small"):
+        _compare(a, oracle.local_ba(P))
+
+
+@pytest.mark.gpu
 def test_gpu_localba_repeatable(ba):
     P = small_problem(seed=10)
     a = ba.LocalBundleAdjustment(P)
