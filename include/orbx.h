@@ -238,13 +238,19 @@ typedef struct orbx_ba orbx_ba;
 orbx_status orbx_ba_create(int device, orbx_ba** out);
 orbx_status orbx_ba_destroy(orbx_ba* h);
 /* *stop_flag != 0 (the reference's pbStopFlag / setForceStopFlag) is polled
- * before the run and between LM trials. */
+ * before the run and between LM trials -- by the device itself while the LM
+ * loop runs there: the flag's page is mapped into the GPU's address space
+ * (pinned memory as is, any other page registered once per handle). */
 orbx_status orbx_ba_run(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_result* result,
                         const volatile int* stop_flag);
 /* The same with the reference's own flag type: LocalBundleAdjustment(KeyFrame*, bool* pbStopFlag, Map*)
  * (include/Optimizer.h:61), set from LocalMapping::InterruptBA on another thread. */
 orbx_status orbx_ba_run_bool(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_result* result,
                              const volatile bool* stop_flag);
+/* A stop flag owned by the handle, in pinned host memory the device reads
+ * directly (no page registration): set it from another thread to interrupt
+ * orbx_ba_run(h, ..., flag) like LocalMapping::InterruptBA sets mbAbortBA. */
+orbx_status orbx_ba_stop_flag(orbx_ba* h, volatile int** flag);
 /* One-shot form: create, run, destroy. */
 orbx_status orbx_local_ba(const orbx_ba_problem* problem, orbx_ba_result* result, const volatile int* stop_flag,
                           int device);

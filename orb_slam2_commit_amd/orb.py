@@ -471,11 +471,15 @@ class Optimizer:
         check(_lib.lib().orbx_ba_create(int(device), C.byref(h)), "orbx_ba_create")
         self._h = h
         self.device = int(device)
+        f = C.POINTER(C.c_int)()
+        check(_lib.lib().orbx_ba_stop_flag(h, C.byref(f)), "orbx_ba_stop_flag")
+        self._stop = f  # the handle's pinned flag (the device polls it without registration)
 
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().orbx_ba_destroy(self._h)
             self._h = None
+            self._stop = None
 
     def __del__(self):
         try:
@@ -498,7 +502,9 @@ class Optimizer:
 
     def LocalBundleAdjustment(self, prob, stop=False):
         """prob: dict(Tcw[n,12], fixed[n], intr[n,5] fx,fy,cx,cy,bf, Xw[m,3], edge_point, edge_cam,
-        obs[e,3] (u, v, ur; ur<0 mono), inv_sigma2[e]).  ``stop`` mirrors *pbStopFlag.
+        obs[e,3] (u, v, ur; ur<0 mono), inv_sigma2[e]).  ``stop`` mirrors *pbStopFlag: a bool, or
+        a one-element int32 array another thread may set while the call runs (the LM loop polls
+        it between iterations and trials, src/Optimizer.cc:749-762).
 
         Returns dict(Tcw, Xw, edge_outlier, Tcw_d, Xw_d, iterations, trials, chi2)."""
         a = _ba_arrays(prob)
@@ -509,8 +515,14 @@ class Optimizer:
                    edge_outlier=np.zeros(ne, np.uint8), Tcw_d=np.zeros((nc, 12)), Xw_d=np.zeros((npt, 3)))
         R = _lib.BaResult(ptr(out["Tcw"]), ptr(out["Xw"]), ptr(out["edge_outlier"]), ptr(out["Tcw_d"]),
                           ptr(out["Xw_d"]))
-        flag = np.array([1 if stop else 0], np.int32)
-        check(_lib.lib().orbx_ba_run(self._h, C.byref(P), C.byref(R), ptr(flag)), "orbx_ba_run")
+        if isinstance(stop, np.ndarray):
+            if stop.dtype != np.int32 or stop.size != 1 or not stop.flags.c_contiguous:
+                raise ValueError("stop flag array must be one contiguous int32")
+            flag = C.c_void_p(stop.ctypes.data)
+        else:
+            self._stop[0] = 1 if stop else 0
+            flag = C.cast(self._stop, C.c_void_p)
+        check(_lib.lib().orbx_ba_run(self._h, C.byref(P), C.byref(R), flag), "orbx_ba_run")
         out.update(iterations=tuple(R.iterations), trials=R.trials, chi2=tuple(R.chi2))
         return out
 

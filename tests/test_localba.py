@@ -336,3 +336,42 @@ def test_gpu_reduced_system_ldlt_zero_pivot(gpu):
     ms = C.c_float(0)
     rc = _lib.lib().orbx_debug_ldlt(_lib.ptr(S), _lib.ptr(np.ones(N)), N, _lib.ptr(x), 1, C.byref(ms))
     assert rc == _lib.ORBX_ERR_STATE if hasattr(_lib, "ORBX_ERR_STATE") else rc == -6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["config4", "many_kfs"] + sorted(REJECT_CASES))
+def test_gpu_localba_device_lm_bit_identical(ba, case, monkeypatch):
+    """LM control on the device (k_ba_lm_control: accept/reject, lambda, the trial budget,
+    rho == 0 and _nBad, trials queued without a host round trip) gives the same bits,
+    iterations and trials as the host-controlled loop (ORBX_BA_HOST_LM=1)."""
+    if case == "config4":
+        P = synth.localba_problem(seed=7)
+    elif case == "many_kfs":
+        P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
+    else:
+        P = reject_problem(case)
+    a = ba.LocalBundleAdjustment(P)
+    monkeypatch.setenv("ORBX_BA_HOST_LM", "1")
+    b = ba.LocalBundleAdjustment(P)
+    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
+    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+    assert a["chi2"] == b["chi2"]
+
+
+@pytest.mark.gpu
+def test_gpu_localba_stop_flag_mid_run(ba):
+    """A stop flag raised by another thread while the device runs the LM loop ends the
+    optimisation early (the device polls the host-mapped flag), with finite outputs."""
+    import threading
+    import time
+    P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
+    full = ba.LocalBundleAdjustment(P)
+    flag = np.zeros(1, np.int32)
+    t = threading.Thread(target=lambda: (time.sleep(0.002), flag.__setitem__(0, 1)))
+    t.start()
+    r = ba.LocalBundleAdjustment(P, stop=flag)
+    t.join()
+    assert flag[0] == 1
+    assert sum(r["iterations"]) < sum(full["iterations"])
+    assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
