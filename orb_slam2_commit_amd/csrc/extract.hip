@@ -530,15 +530,14 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     }
 #pragma unroll
     for (int u = 0; u < QU; u++) {
-      // the eight comparisons are lane masks (v_cmp -> SGPR pairs), combined with scalar logic
+      // the eight comparisons as sign bits of differences, combined in VALU
+      // (x < 0 && y < 0 <=> (x & y) < 0), one v_cmp for the lane mask
       const int dlo = cv[u] - tlo, dhi = cv[u] + tlo;
-      const uint64_t k0 = __ballot(c0[u] < dlo), k4 = __ballot(c4[u] < dlo), k8 = __ballot(c8[u] < dlo),
-                     k12 = __ballot(c12[u] < dlo);
-      const uint64_t b0 = __ballot(c0[u] > dhi), b4 = __ballot(c4[u] > dhi), b8 = __ballot(c8[u] > dhi),
-                     b12 = __ballot(c12[u] > dhi);
-      const uint64_t m = (((k0 & k4) | (k4 & k8) | (k8 & k12) | (k12 & k0)) |
-                          ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0))) &
-                         col_ok & __ballot(y0r + u * RP + ly < H);
+      const int d0 = c0[u] - dlo, d4 = c4[u] - dlo, d8 = c8[u] - dlo, d12 = c12[u] - dlo;
+      const int e0 = dhi - c0[u], e4 = dhi - c4[u], e8 = dhi - c8[u], e12 = dhi - c12[u];
+      const int pk = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
+      const int pb = (e0 & e4) | (e4 & e8) | (e8 & e12) | (e12 & e0);
+      const uint64_t m = __ballot((pk | pb) < 0) & col_ok & __ballot(y0r + u * RP + ly < H);
       if (__builtin_amdgcn_inverse_ballot_w64(m)) list[n + lane_rank(m)] = (uint16_t)(eb + u * RP * S);
       n += __popcll(m);
     }
@@ -570,8 +569,9 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     const int s = m[S + 1];
     const int n0 = m[0], n1 = m[1], n2 = m[2], n3 = m[S], n4 = m[S + 2], n5 = m[2 * S], n6 = m[2 * S + 1],
               n7 = m[2 * S + 2];
-    auto beats = [&](int nv) -> int { return nv >= thr && nv >= s; };  // int: branch-free OR below
-    const bool lost = (beats(n0) | beats(n1) | beats(n2) | beats(n3) | beats(n4) | beats(n5) | beats(n6) | beats(n7)) != 0;
+    // a neighbour beats the centre iff nv >= thr and nv >= s: one max over the eight
+    const int mx = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+    const bool lost = mx >= max(thr, s);
     return s >= thr && s > 1 && !lost;
   };
   // 4. survivors at iniThFAST (verdict kept in bit 15 of the list entry)
