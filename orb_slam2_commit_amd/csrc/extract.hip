@@ -513,7 +513,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const int tlo = min(ini, mint);
   // 2. compass quick test, row-major compaction of tile offsets
   const int ly = RP == 2 ? (lane >> 5) : 0, lx = RP == 2 ? (lane & 31) : lane;
-  const uint64_t col_ok = __ballot(lx < W);
+  const int cw = lx - W;
   int n = 0;
   constexpr int QU = 8 / RP;
   for (int y0r = 0; y0r < H; y0r += QU * RP) {
@@ -537,8 +537,10 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
       const int e0 = dhi - c0[u], e4 = dhi - c4[u], e8 = dhi - c8[u], e12 = dhi - c12[u];
       const int pk = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
       const int pb = (e0 & e4) | (e4 & e8) | (e8 & e12) | (e12 & e0);
-      const uint64_t m = __ballot((pk | pb) < 0) & col_ok & __ballot(y0r + u * RP + ly < H);
-      if (__builtin_amdgcn_inverse_ballot_w64(m)) list[n + lane_rank(m)] = (uint16_t)(eb + u * RP * S);
+      // lane inside the region: (col - W) and (row - H) both negative
+      const bool hit = ((pk | pb) & cw & (y0r + u * RP + ly - H)) < 0;
+      const uint64_t m = __ballot(hit);
+      if (hit) list[n + lane_rank(m)] = (uint16_t)(eb + u * RP * S);
       n += __popcll(m);
     }
   }
