@@ -1680,6 +1680,36 @@ __global__ __launch_bounds__(kTileT) void k_ba_struct_fill(BaDev D, const uint8_
   }
 }
 
+// Problem intake on the device: the caller's float observations / points
+// become the FP64 edge and vertex arrays (Converter / g2o setMeasurement
+// casts), the per-edge stereo flag, Huber delta (the float sqrt thresholds of
+// src/Optimizer.cc:653-654, passed from the host) and its float square, robust
+// flags on, stored errors zero.  Only the raw arrays cross PCIe.
+__global__ __launch_bounds__(LBS) void k_ba_prep(int ne, int np, const float* __restrict__ obs,
+                                                 const float* __restrict__ isig, const float* __restrict__ Xf,
+                                                 double* __restrict__ X, uint8_t* __restrict__ est,
+                                                 double* __restrict__ eobs, double* __restrict__ einfo,
+                                                 double* __restrict__ edelta, float* __restrict__ edsqr,
+                                                 uint8_t* __restrict__ erob, double* __restrict__ eerr, float thMono,
+                                                 float thStereo) {
+  const int i = blockIdx.x * LBS + threadIdx.x;
+  if (i < ne) {
+    const float u = obs[3 * i], v = obs[3 * i + 1], ur = obs[3 * i + 2];
+    const bool s = ur >= 0;
+    est[i] = s ? 1 : 0;
+    eobs[3 * i] = u;
+    eobs[3 * i + 1] = v;
+    eobs[3 * i + 2] = ur;
+    einfo[i] = isig[i];
+    const double d = s ? thStereo : thMono;
+    edelta[i] = d;
+    edsqr[i] = (float)(d * d);
+    erob[i] = 1;
+    eerr[3 * i] = eerr[3 * i + 1] = eerr[3 * i + 2] = 0.0;
+  }
+  if (i < 3 * np) X[i] = Xf[i];
+}
+
 // phase transition (:764-802) and the final erase test (:817-847): per edge
 // chi2 of its stored error against th, and depth of the current estimate
 __global__ __launch_bounds__(LBS) void k_ba_outliers(BaDev D, uint8_t* flag, int drop_kernel) {
@@ -1754,6 +1784,7 @@ struct Ctx {
   DBuf<int> ptab;
   DBuf<uint8_t> flag;
   DBuf<LmState> lm;
+  DBuf<uint8_t> prob;  // k_ba_prep outputs: FP64 points and edge arrays
   DBuf<float> Tcw_out, Xw_out;
   DBuf<double> Tcw_d_out, Xw_d_out;
 };
@@ -1816,7 +1847,7 @@ struct LocalBA {
   Ctx c;  // device buffers, kept across calls (grow only)
   Arena prob_arena, struct_arena;
   std::vector<int> e_pt, e_cam;
-  std::vector<uint8_t> e_st, fixed;
+  std::vector<uint8_t> fixed;
   std::vector<uint8_t> level;  // 0/1 per edge
   int trials = 0;
   int nbu = 1, n_rb = 8;           // k_ba_update blocks; doubles in the readback block
@@ -2395,29 +2426,39 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
     const int s1[5] = {ne, npts, nposes, maxc, nslots};
     std::memcpy(L.sizes1, s1, sizeof s1);
   }
-  L.e_pt.assign(pb->edge_point, pb->edge_point + ne);
-  L.e_cam.assign(pb->edge_cam, pb->edge_cam + ne);
+  if (!L.dev_struct) {  // the host structure build reads them
+    L.e_pt.assign(pb->edge_point, pb->edge_point + ne);
+    L.e_cam.assign(pb->edge_cam, pb->edge_cam + ne);
+  }
   L.fixed.assign(nc, 0);
-  L.e_st.resize(ne);
   Arena& A = L.prob_arena;
-  if (A.reserve(arena_bytes({32 * (size_t)nc, 24 * (size_t)nc, 40 * (size_t)nc, 24 * (size_t)np, 4 * (size_t)ne,
-                             4 * (size_t)ne, (size_t)ne, 24 * (size_t)ne, 8 * (size_t)ne, 8 * (size_t)ne,
-                             4 * (size_t)ne, (size_t)ne, (size_t)nc})) != hipSuccess)
+  if (A.reserve(arena_bytes({32 * (size_t)nc, 24 * (size_t)nc, 40 * (size_t)nc, 12 * (size_t)np, 4 * (size_t)ne,
+                             4 * (size_t)ne, 12 * (size_t)ne, 4 * (size_t)ne, (size_t)nc})) != hipSuccess)
     return ORBX_ERR_HIP;
   double* cq = A.take<double>(4 * (size_t)nc);
   double* ct = A.take<double>(3 * (size_t)nc);
   double* intr = A.take<double>(5 * (size_t)nc);
-  double* X = A.take<double>(3 * (size_t)np);
+  float* Xf = A.take<float>(3 * (size_t)np);
   int* ept = A.take<int>(ne);
   int* ecam = A.take<int>(ne);
-  uint8_t* est = A.take<uint8_t>(ne);
-  double* eobs = A.take<double>(3 * (size_t)ne);
-  double* einfo = A.take<double>(ne);
-  double* edelta = A.take<double>(ne);
-  float* edsqr = A.take<float>(ne);
-  uint8_t* erob = A.take<uint8_t>(ne);
+  float* obs_f = A.take<float>(3 * (size_t)ne);
+  float* isig_f = A.take<float>(ne);
   uint8_t* dfix = A.take<uint8_t>(nc);
   L.dfix = dfix;
+  // device-only FP64 / flag arrays, filled by k_ba_prep
+  const size_t al = 256;
+  auto rnd = [&](size_t b) { return (std::max<size_t>(b, 1) + al - 1) / al * al; };
+  const size_t o_X = 0, o_eobs = o_X + rnd(24 * (size_t)np), o_einfo = o_eobs + rnd(24 * (size_t)ne),
+               o_edelta = o_einfo + rnd(8 * (size_t)ne), o_edsqr = o_edelta + rnd(8 * (size_t)ne),
+               o_est = o_edsqr + rnd(4 * (size_t)ne), o_erob = o_est + rnd(ne), o_end = o_erob + rnd(ne);
+  BA_CHECK(c.prob.alloc(o_end));
+  double* X = reinterpret_cast<double*>(c.prob.p + o_X);
+  double* eobs = reinterpret_cast<double*>(c.prob.p + o_eobs);
+  double* einfo = reinterpret_cast<double*>(c.prob.p + o_einfo);
+  double* edelta = reinterpret_cast<double*>(c.prob.p + o_edelta);
+  float* edsqr = reinterpret_cast<float*>(c.prob.p + o_edsqr);
+  uint8_t* est = c.prob.p + o_est;
+  uint8_t* erob = c.prob.p + o_erob;
   // vertices: Converter::toSE3Quat (float -> double, Quaterniond(R), normalize)
   {
     double* hq = A.host(cq);
@@ -2439,33 +2480,26 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       L.fixed[i] = pb->fixed ? pb->fixed[i] : 0;
       A.host(dfix)[i] = L.fixed[i];
     }
-    double* hx = A.host(X);
-    for (int i = 0; i < 3 * np; i++) hx[i] = pb->Xw[i];
+    if (np) std::memcpy(A.host(Xf), pb->Xw, 12 * (size_t)np);
     if (ne) {
       std::memcpy(A.host(ept), pb->edge_point, 4 * (size_t)ne);
       std::memcpy(A.host(ecam), pb->edge_cam, 4 * (size_t)ne);
-    }
-    const float thMono = std::sqrt(5.991f), thStereo = std::sqrt(7.815f);  // src/Optimizer.cc:653-654
-    uint8_t* hs = A.host(est);
-    double* ho = A.host(eobs);
-    double* hinf = A.host(einfo);
-    double* hd = A.host(edelta);
-    float* hd2 = A.host(edsqr);
-    uint8_t* hr = A.host(erob);
-    for (int e = 0; e < ne; e++) {
-      L.e_st[e] = hs[e] = pb->obs[3 * e + 2] >= 0 ? 1 : 0;
-      for (int k = 0; k < 3; k++) ho[3 * e + k] = pb->obs[3 * e + k];
-      hinf[e] = pb->inv_sigma2[e];
-      hd[e] = hs[e] ? thStereo : thMono;
-      hd2[e] = (float)(hd[e] * hd[e]);
-      hr[e] = 1;
+      std::memcpy(A.host(obs_f), pb->obs, 12 * (size_t)ne);
+      std::memcpy(A.host(isig_f), pb->inv_sigma2, 4 * (size_t)ne);
     }
   }
   BA_CHECK(A.upload(st));
   BA_CHECK(c.cbak.alloc(7 * (size_t)nc));
   BA_CHECK(c.Xbak.alloc(3 * (size_t)np));
   BA_CHECK(c.eerr.alloc(3 * (size_t)ne));
-  BA_CHECK(hipMemsetAsync(c.eerr.p, 0, 3 * sizeof(double) * std::max(ne, 1), st));
+  {
+    const float thMono = std::sqrt(5.991f), thStereo = std::sqrt(7.815f);  // src/Optimizer.cc:653-654
+    const int gpre = (std::max(ne, 3 * np) + LBS - 1) / LBS;
+    if (gpre > 0)
+      hipLaunchKernelGGL(k_ba_prep, dim3(gpre), dim3(LBS), 0, st, ne, np, obs_f, isig_f, Xf, X, est, eobs, einfo,
+                         edelta, edsqr, erob, c.eerr.p, thMono, thStereo);
+    BA_CHECK(hipGetLastError());
+  }
   BA_CHECK(c.flag.alloc(ne));
   BA_CHECK(c.scal.alloc(8));
   D.cq = cq;
