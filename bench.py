@@ -76,6 +76,28 @@ def level_sizes(w, h, inv_scales):
             for s in inv_scales]
 
 
+def hbm_copy_peak(dev, nbytes=2 << 30, reps=10):
+    """On-box HBM reference: a streaming 16-B copy kernel between two 2 GiB device buffers
+    (orbx_debug_hbm_copy; read + write bytes per copy / time), the stream-copy figure the
+    spec's 8 TB/s is compared against."""
+    import ctypes as C
+    import torch
+    from orb_slam2_commit_amd import _lib
+    try:
+        with torch.cuda.device(dev):
+            src = torch.ones(nbytes, dtype=torch.uint8, device=dev)
+            dst = torch.empty_like(src)
+            torch.cuda.synchronize(dev)
+            ms = C.c_float(0)
+            if _lib.lib().orbx_debug_hbm_copy(C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()),
+                                              nbytes, reps, C.byref(ms)) != 0:
+                return None
+            del src, dst
+        return round(2 * nbytes / (ms.value / 1e3) / 1e9, 1)
+    except Exception:
+        return None
+
+
 def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, cand_per_img):
     """Algorithmic HBM bytes of one launch of `stage` over the batch."""
     sP = sum(P)
@@ -596,6 +618,7 @@ def main():
             sq_src = os.path.relpath(args.sq, ROOT)
         except Exception:
             sq_all = {}
+    copy_gbs = hbm_copy_peak(dev) if rank == 0 else None
     roofline = None
     if dom:
         ms_tot, nl = stages[dom]
@@ -606,6 +629,8 @@ def main():
                         frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic_all.get(dom),
                         traffic_source=traffic_src,
                         algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4))
+        if copy_gbs:
+            roofline.update(measured_copy_peak=copy_gbs, frac_of_measured_peak=round(achieved / copy_gbs, 5))
         if dom in sq_all:
             roofline.update(valu_issue_frac=sq_all[dom].get("valu_issue_frac"),
                             salu_issue_frac=sq_all[dom].get("salu_issue_frac"),

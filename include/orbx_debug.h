@@ -28,6 +28,11 @@ long long orbx_debug_copy(orbx_extractor* h, int what, int image, int arg, void*
  * a zero pivot. */
 int orbx_debug_ldlt(const double* S, const double* b, int N, double* x, int reps, float* ms);
 
+/* On-box HBM reference: copy `bytes` (multiple of 16) between two device
+ * buffers with a streaming 16-B kernel, reps times on the null stream;
+ * *ms = mean time per copy (2 * bytes of HBM traffic each). */
+int orbx_debug_hbm_copy(void* dst, const void* src, size_t bytes, int reps, float* ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -186,6 +186,7 @@ SIGNATURES = {
     # include/orbx_debug.h
     "orbx_debug_copy": ([P, C.c_int, C.c_int, C.c_int, P, C.c_size_t], C.c_longlong),
     "orbx_debug_ldlt": ([P, P, C.c_int, P, C.c_int, C.POINTER(C.c_float)], C.c_int),
+    "orbx_debug_hbm_copy": ([P, P, C.c_size_t, C.c_int, C.POINTER(C.c_float)], C.c_int),
 }
 
 _lib = None
