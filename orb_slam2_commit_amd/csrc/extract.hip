@@ -456,6 +456,10 @@ __device__ __forceinline__ int ring_score1(const uint8_t* t) {
   return max(a, b);
 }
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s16x2(int v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ int as_int(s16x2 v) { return __builtin_bit_cast(int, v); }
+
 __device__ __forceinline__ int lane_rank(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -530,15 +534,16 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     }
 #pragma unroll
     for (int u = 0; u < QU; u++) {
-      // the eight comparisons as sign bits of differences, combined in VALU
-      // (x < 0 && y < 0 <=> (x & y) < 0), one v_cmp for the lane mask
-      const int dlo = cv[u] - tlo, dhi = cv[u] + tlo;
-      const int d0 = c0[u] - dlo, d4 = c4[u] - dlo, d8 = c8[u] - dlo, d12 = c12[u] - dlo;
-      const int e0 = dhi - c0[u], e4 = dhi - c4[u], e8 = dhi - c8[u], e12 = dhi - c12[u];
+      // the eight comparisons as sign bits of differences, both polarities at
+      // once in packed 16-bit halves: p = (c, -c) (one 24-bit mad), y = (dlo,
+      // -dhi), p - y = (c - dlo, dhi - c); x < 0 && z < 0 <=> (x & z) < 0 per half
+      const s16x2 y = as_s16x2(cv[u] * -65535) - (s16x2){(short)tlo, (short)tlo};
+      const int d0 = as_int(as_s16x2(c0[u] * -65535) - y), d4 = as_int(as_s16x2(c4[u] * -65535) - y),
+                d8 = as_int(as_s16x2(c8[u] * -65535) - y), d12 = as_int(as_s16x2(c12[u] * -65535) - y);
       const int pk = (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
-      const int pb = (e0 & e4) | (e4 & e8) | (e8 & e12) | (e12 & e0);
       // lane inside the region: (col - W) and (row - H) both negative
-      const bool hit = ((pk | pb) & cw & (y0r + u * RP + ly - H)) < 0;
+      // (bit 15 folded onto bit 31, which also carries the region test)
+      const bool hit = ((pk | (pk << 16)) & cw & (y0r + u * RP + ly - H)) < 0;
       const uint64_t m = __ballot(hit);
       if (hit) list[n + lane_rank(m)] = (uint16_t)(eb + u * RP * S);
       n += __popcll(m);
