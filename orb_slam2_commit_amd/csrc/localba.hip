@@ -255,6 +255,7 @@ struct BaDev {
   double* gpart;   // chunk partials of the pose-list gathers (summed by the *_fin kernels)
   int gsplit;      // chunks per pose list in the gather kernels
   int nbe;         // k_ba_errors blocks; scal[8..] holds its block partials (2 slots), then k_ba_update's
+  int nbu;         // k_ba_update blocks (its LM-scale partials)
   double* scal;    // scalars: [0] chi at iteration start, [1] chi after the trial, [2] solve ok, [3] max diag, [4] LM scale
   const LmState* lm;  // device LM state: gates the trial's kernels and carries lambda (null: host control)
 };
@@ -377,8 +378,8 @@ __device__ inline void huber(double chi, double delta, float dsqr, double rho[3]
   }
 }
 
-__global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute, int dst) {
-  if (lm_skip(D)) return;
+__device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, int dst) {
+  if (lm_skip(D) || (int)blockIdx.x >= D.nbe) return;  // (a batched grid spans the largest problem)
   const int k = blockIdx.x * LBS + threadIdx.x;
   double chi = 0;
   if (k < D.na) {
@@ -403,6 +404,10 @@ __global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute, int d
     }
   }
   block_partial(chi, D.scal + 8 + dst * D.nbe);
+}
+__global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute, int dst) { k_ba_errors_body(D, recompute, dst); }
+__global__ __launch_bounds__(LBS) void k_ba_errors_many(const BaDev* __restrict__ Ds, int recompute, int dst) {
+  k_ba_errors_body(Ds[blockIdx.z], recompute, dst);
 }
 
 // Deterministic sum / max of n doubles into *out (one block).
@@ -478,7 +483,7 @@ __device__ __forceinline__ void lin_accumulate(const BaDev& D, int k, int e, int
   }
 }
 
-__global__ __launch_bounds__(LBS) void k_ba_linearize(BaDev D) {
+__device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
   if (lm_skip_lin(D)) return;
   const int k = blockIdx.x * LBS + threadIdx.x;
   if (k >= D.na) return;
@@ -532,8 +537,12 @@ __global__ __launch_bounds__(LBS) void k_ba_linearize(BaDev D) {
   else
     lin_accumulate<2>(D, k, e, c, A, Bm);
 }
+__global__ __launch_bounds__(LBS) void k_ba_linearize(BaDev D) { k_ba_linearize_body(D); }
+__global__ __launch_bounds__(LBS) void k_ba_linearize_many(const BaDev* __restrict__ Ds) {
+  k_ba_linearize_body(Ds[blockIdx.z]);
+}
 
-__global__ __launch_bounds__(LBS) void k_ba_point_sum(BaDev D) {
+__device__ __forceinline__ void k_ba_point_sum_body(const BaDev& D) {
   if (lm_skip_lin(D)) return;
   const int i = blockIdx.x * LBS + threadIdx.x;
   if (i >= D.npa) return;
@@ -546,6 +555,10 @@ __global__ __launch_bounds__(LBS) void k_ba_point_sum(BaDev D) {
   for (int j = 0; j < 9; j++) D.Hll[9 * i + j] = h[j];
   for (int j = 0; j < 3; j++) D.bl[3 * i + j] = h[9 + j];
   D.dmax_p[i] = fmax(fmax(fabs(h[0]), fabs(h[4])), fabs(h[8]));
+}
+__global__ __launch_bounds__(LBS) void k_ba_point_sum(BaDev D) { k_ba_point_sum_body(D); }
+__global__ __launch_bounds__(LBS) void k_ba_point_sum_many(const BaDev* __restrict__ Ds) {
+  k_ba_point_sum_body(Ds[blockIdx.z]);
 }
 
 // Fixed-order block sum of NV per-thread partials over a kGB-thread block
@@ -587,15 +600,15 @@ __device__ inline void chunk_range(int lo, int hi, int s, int S, int& a, int& b)
 // Hpp, bp per pose: grid (pose, chunk); a chunk's threads take its positions
 // t, t+kGB, ... ; only the upper triangle (21) + b (6) are summed.  Chunk
 // partials -> gpart, summed in chunk order by k_ba_cam_fin.
-__global__ __launch_bounds__(kGB) void k_ba_cam_sum(BaDev D) {
-  if (lm_skip_lin(D)) return;
+__device__ __forceinline__ void k_ba_cam_sum_body(const BaDev& D) {
+  if (lm_skip_lin(D) || (int)blockIdx.x >= D.nposes || (int)blockIdx.y >= D.gsplit) return;
   __shared__ double red[(kGW + 1) * 27];
   const int ci = blockIdx.x;
   double v[27];
 #pragma unroll
   for (int j = 0; j < 27; j++) v[j] = 0;
   int lo, hi;
-  chunk_range(D.cam_off[ci], D.cam_off[ci + 1], blockIdx.y, gridDim.y, lo, hi);
+  chunk_range(D.cam_off[ci], D.cam_off[ci + 1], blockIdx.y, D.gsplit, lo, hi);
   for (int t = lo + threadIdx.x; t < hi; t += kGB) {
     const double* cm = D.cmc + 42 * (size_t)D.cam_pos[t];
     int j = 0;
@@ -607,12 +620,16 @@ __global__ __launch_bounds__(kGB) void k_ba_cam_sum(BaDev D) {
     for (int r = 0; r < 6; r++) v[21 + r] += cm[36 + r];
   }
   const double* tot = block_sum_fixed<27>(v, red);
-  if (threadIdx.x < 27) D.gpart[((size_t)ci * gridDim.y + blockIdx.y) * 27 + threadIdx.x] = tot[threadIdx.x];
+  if (threadIdx.x < 27) D.gpart[((size_t)ci * D.gsplit + blockIdx.y) * 27 + threadIdx.x] = tot[threadIdx.x];
+}
+__global__ __launch_bounds__(kGB) void k_ba_cam_sum(BaDev D) { k_ba_cam_sum_body(D); }
+__global__ __launch_bounds__(kGB) void k_ba_cam_sum_many(const BaDev* __restrict__ Ds) {
+  k_ba_cam_sum_body(Ds[blockIdx.z]);
 }
 
 // One 64-thread block per pose: Hpp (symmetric), bp, max |Hpp_jj|.
-__global__ __launch_bounds__(64) void k_ba_cam_fin(BaDev D) {
-  if (lm_skip_lin(D)) return;
+__device__ __forceinline__ void k_ba_cam_fin_body(const BaDev& D) {
+  if (lm_skip_lin(D) || (int)blockIdx.x >= D.nposes) return;
   __shared__ double tot[27];
   const int ci = blockIdx.x, j = threadIdx.x, S = D.gsplit;
   if (j < 27) {
@@ -637,10 +654,14 @@ __global__ __launch_bounds__(64) void k_ba_cam_fin(BaDev D) {
     D.dmax_c[ci] = m;
   }
 }
+__global__ __launch_bounds__(64) void k_ba_cam_fin(BaDev D) { k_ba_cam_fin_body(D); }
+__global__ __launch_bounds__(64) void k_ba_cam_fin_many(const BaDev* __restrict__ Ds) {
+  k_ba_cam_fin_body(Ds[blockIdx.z]);
+}
 
 // One thread per active edge position: D = Hll + lambda I of its point,
 // Dinv (stored once per point), BD_e = Hpl_e Dinv, cf_e = Hpl_e Dinv bl.
-__global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) {
+__device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lambda) {
   if (lm_skip(D)) return;
   lambda = lm_lambda(D, lambda);
   const int k = blockIdx.x * LBS + threadIdx.x;
@@ -666,6 +687,10 @@ __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) 
     for (int c = 0; c < 3; c++) bd[3 * r + c] = B1[3 * r] * Di[c] + B1[3 * r + 1] * Di[3 + c] + B1[3 * r + 2] * Di[6 + c];
     D.cf[6 * (size_t)k + r] = B1[3 * r] * db[0] + B1[3 * r + 1] * db[1] + B1[3 * r + 2] * db[2];
   }
+}
+__global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) { k_ba_point_schur_body(D, lambda); }
+__global__ __launch_bounds__(LBS) void k_ba_point_schur_many(const BaDev* __restrict__ Ds, double lambda) {
+  k_ba_point_schur_body(Ds[blockIdx.z], lambda);
 }
 
 // Accumulates acc += BD_k1 Hpl_k2^T (6x3 * 3x6), one Hpl row at a time.
@@ -716,10 +741,10 @@ __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
 // (k1, k2) order).  Blocks b >= nblk: sum of cf over pose b - nblk's positions
 // (the Schur rhs correction).  Chunk partials -> gpart; k_ba_schur_fin sums
 // them in chunk order (deterministic).
-__global__ __launch_bounds__(kPB) void k_ba_pairs(BaDev D) {
-  if (lm_skip(D)) return;
+__device__ __forceinline__ void k_ba_pairs_body(const BaDev& D) {
+  if (lm_skip(D) || (int)blockIdx.x >= D.nblk + D.nposes || (int)blockIdx.y >= D.gsplit) return;
   __shared__ double red[(kPB / 64 + 1) * 36];
-  const int S = gridDim.y, s = blockIdx.y;
+  const int S = D.gsplit, s = blockIdx.y;
   if ((int)blockIdx.x >= D.nblk) {
     const int ci = blockIdx.x - D.nblk;
     double v[6] = {0, 0, 0, 0, 0, 0};
@@ -762,12 +787,16 @@ __global__ __launch_bounds__(kPB) void k_ba_pairs(BaDev D) {
   const double* tot = block_sum_fixed<36, kPB / 64>(acc, red);
   if (threadIdx.x < 36) D.gpart[((size_t)blockIdx.x * S + s) * 36 + threadIdx.x] = tot[threadIdx.x];
 }
+__global__ __launch_bounds__(kPB) void k_ba_pairs(BaDev D) { k_ba_pairs_body(D); }
+__global__ __launch_bounds__(kPB) void k_ba_pairs_many(const BaDev* __restrict__ Ds) {
+  k_ba_pairs_body(Ds[blockIdx.z]);
+}
 
 // Reduced system from the chunk partials: blocks b < nblk write Hschur block
 // (c1, c2) = [c1==c2](Hpp + lambda I) - pair sum (both triangles, so every
 // entry of S is written); blocks b >= nblk write bs = bp - sum cf.
-__global__ __launch_bounds__(64) void k_ba_schur_fin(BaDev D, double lambda) {
-  if (lm_skip(D)) return;
+__device__ __forceinline__ void k_ba_schur_fin_body(const BaDev& D, double lambda) {
+  if (lm_skip(D) || (int)blockIdx.x >= D.nblk + D.nposes) return;
   lambda = lm_lambda(D, lambda);
   const int j = threadIdx.x, S = D.gsplit;
   if ((int)blockIdx.x >= D.nblk) {
@@ -794,6 +823,10 @@ __global__ __launch_bounds__(64) void k_ba_schur_fin(BaDev D, double lambda) {
     D.S[(size_t)(6 * c2 + c) * N + 6 * c1 + r] = sv;
   }
   D.S[(size_t)(6 * c1 + r) * N + 6 * c2 + c] = sv;
+}
+__global__ __launch_bounds__(64) void k_ba_schur_fin(BaDev D, double lambda) { k_ba_schur_fin_body(D, lambda); }
+__global__ __launch_bounds__(64) void k_ba_schur_fin_many(const BaDev* __restrict__ Ds, double lambda) {
+  k_ba_schur_fin_body(Ds[blockIdx.z], lambda);
 }
 
 __device__ inline double readlane_d(double v, int l) {
@@ -1095,7 +1128,7 @@ __device__ __forceinline__ void ldlt_col_step(double* Lc, double* rinv, double (
 }
 
 template <int TPT, int NT>
-__global__ __launch_bounds__(NT) void k_ba_ldlt_col(BaDev D) {
+__device__ __forceinline__ void k_ba_ldlt_col_body(const BaDev& D) {
   if (lm_skip(D)) return;
   extern __shared__ __attribute__((aligned(16))) double Lc[];
   __shared__ int fail;
@@ -1192,6 +1225,12 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_col(BaDev D) {
     if (lane + 64 * r < N) D.xp[lane + 64 * r] = y[r];
   if (lane == 0) D.scal[2] = 1.0;
 }
+template <int TPT, int NT>
+__global__ __launch_bounds__(NT) void k_ba_ldlt_col(BaDev D) { k_ba_ldlt_col_body<TPT, NT>(D); }
+template <int TPT, int NT>
+__global__ __launch_bounds__(NT) void k_ba_ldlt_col_many(const BaDev* __restrict__ Ds) {
+  k_ba_ldlt_col_body<TPT, NT>(Ds[blockIdx.z]);
+}
 
 // Launch plan for the reduced system: the column-step kernel while the
 // packed factor fits LDS, else the 16-wide blocked kernel (LDS or global).
@@ -1245,8 +1284,8 @@ struct LdltPlan {
 
 // back-substitution + update (push first) + LM scale, skipped when the
 // solve failed (scal[2] == 0).  Threads: active points, then active poses.
-__global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
-  if (lm_skip(D)) return;
+__device__ __forceinline__ void k_ba_update_body(const BaDev& D, double lambda) {
+  if (lm_skip(D) || (int)blockIdx.x >= D.nbu) return;
   lambda = lm_lambda(D, lambda);
   const int i = blockIdx.x * LBS + threadIdx.x;
   if (D.lm && D.lm->rejected) {  // device LM: the previous trial's pop, same thread mapping as k_ba_restore
@@ -1304,8 +1343,12 @@ __global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) {
   }
   block_partial(sc, D.scal + 8 + 2 * D.nbe);
 }
+__global__ __launch_bounds__(LBS) void k_ba_update(BaDev D, double lambda) { k_ba_update_body(D, lambda); }
+__global__ __launch_bounds__(LBS) void k_ba_update_many(const BaDev* __restrict__ Ds, double lambda) {
+  k_ba_update_body(Ds[blockIdx.z], lambda);
+}
 
-__global__ __launch_bounds__(LBS) void k_ba_restore(BaDev D) {
+__device__ __forceinline__ void k_ba_restore_body(const BaDev& D) {
   if (D.lm && !D.lm->rejected) return;
   const int i = blockIdx.x * LBS + threadIdx.x;
   if (i < D.npa) {
@@ -1316,6 +1359,10 @@ __global__ __launch_bounds__(LBS) void k_ba_restore(BaDev D) {
     for (int r = 0; r < 4; r++) D.cq[4 * c + r] = D.cbak[7 * c + r];
     for (int r = 0; r < 3; r++) D.ct[3 * c + r] = D.cbak[7 * c + 4 + r];
   }
+}
+__global__ __launch_bounds__(LBS) void k_ba_restore(BaDev D) { k_ba_restore_body(D); }
+__global__ __launch_bounds__(LBS) void k_ba_restore_many(const BaDev* __restrict__ Ds) {
+  k_ba_restore_body(Ds[blockIdx.z]);
 }
 
 // The caller's stop flag as the device sees it (host-mapped pinned pages):
@@ -1348,7 +1395,8 @@ __device__ inline double seq_sum_wave(const double* p, int n) {
   return s;
 }
 
-__global__ __launch_bounds__(64) void k_ba_lm_init(BaDev D, LmState* L, int iterations) {
+__device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations) {
+  LmState* L = const_cast<LmState*>(D.lm);
   const double a = seq_sum_wave(D.scal + 8, D.nbe);
   if (threadIdx.x != 0) return;
   L->lambda = 1e-5 * D.scal[3];
@@ -1361,6 +1409,10 @@ __global__ __launch_bounds__(64) void k_ba_lm_init(BaDev D, LmState* L, int iter
   L->stopped = 0;  // the host polled the flag just before this phase
   L->done = iterations <= 0 ? 1 : 0;
 }
+__global__ __launch_bounds__(64) void k_ba_lm_init(BaDev D, int iterations) { k_ba_lm_init_body(D, iterations); }
+__global__ __launch_bounds__(64) void k_ba_lm_init_many(const BaDev* __restrict__ Ds, int iterations) {
+  k_ba_lm_init_body(Ds[blockIdx.z], iterations);
+}
 
 // One LM trial's verdict (OptimizationAlgorithmLevenberg::solve, the
 // reference's arithmetic in the same order as the host loop of
@@ -1368,7 +1420,9 @@ __global__ __launch_bounds__(64) void k_ba_lm_init(BaDev D, LmState* L, int iter
 // block order, accept (lambda *= max(1/3, min(2/3, 1-(2rho-1)^3))) or reject
 // (lambda *= ni, ni *= 2, restore), then the iteration bookkeeping: the
 // <= 10 trial budget, rho == 0, the _nBad rule and the stop flag.
-__global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, LmState* L, int nbu, DevStop stop) {
+__device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop stop) {
+  LmState* L = const_cast<LmState*>(D.lm);
+  const int nbu = D.nbu;
   if (L->done) return;  // uniform; a finished phase keeps `rejected` for the final restore
   const double* p = D.scal + 8;
   const double b = seq_sum_wave(p + D.nbe, D.nbe);
@@ -1415,6 +1469,10 @@ __global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, LmState* L, int n
   L->stopped = st || st2;
   L->done = (brk || L->it >= L->iterations || st2) ? 1 : 0;
   L->relin = L->done ? 0 : 1;
+}
+__global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, DevStop stop) { k_ba_lm_control_body(D, stop); }
+__global__ __launch_bounds__(64) void k_ba_lm_control_many(const BaDev* __restrict__ Ds, DevStop stop) {
+  k_ba_lm_control_body(Ds[blockIdx.z], stop);
 }
 
 // Block-wide exclusive scan of one int per thread under `op` (identity
@@ -2108,6 +2166,7 @@ struct LocalBA {
     // readback block: scal[0..7], then errors partials (2 slots of nbe), then update partials
     D.nbe = std::max((na + LBS - 1) / LBS, 1);
     nbu = std::max((npa + nposes + LBS - 1) / LBS, 1);
+    D.nbu = nbu;
     n_rb = 8 + 2 * D.nbe + nbu;
     BA_CHECK(c.scal.alloc(n_rb));
     D.scal = c.scal.p;
@@ -2306,7 +2365,7 @@ struct LocalBA {
       hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, D0, 1, 0);
       linearize(D0, st);
       hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D0.dmax_p, D0.npa + D0.nposes, D0.scal + 3, 1);
-      hipLaunchKernelGGL(k_ba_lm_init, dim3(1), dim3(64), 0, st, D0, c.lm.p, iterations);
+      hipLaunchKernelGGL(k_ba_lm_init, dim3(1), dim3(64), 0, st, Dg, iterations);
       BA_CHECK(hipGetLastError());
       auto trial = [&](bool lin) {
         if (lin) linearize(Dg, st);  // gated: only at the start of a new iteration
@@ -2318,7 +2377,7 @@ struct LocalBA {
         }
         hipLaunchKernelGGL(k_ba_update, dim3(gp), dim3(LBS), 0, st, Dg, 0.0);
         hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, Dg, 1, 1);
-        hipLaunchKernelGGL(k_ba_lm_control, dim3(1), dim3(64), 0, st, Dg, c.lm.p, nbu, dstop);
+        hipLaunchKernelGGL(k_ba_lm_control, dim3(1), dim3(64), 0, st, Dg, dstop);
       };
       // (capturing the trial as a HIP graph and launching that instead measured slower on this
       // stack: 2.81 vs 2.76 ms per config-4 call)
