@@ -247,6 +247,13 @@ orbx_status orbx_ba_run(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_resu
  * (include/Optimizer.h:61), set from LocalMapping::InterruptBA on another thread. */
 orbx_status orbx_ba_run_bool(orbx_ba* h, const orbx_ba_problem* problem, orbx_ba_result* result,
                              const volatile bool* stop_flag);
+/* K independent LocalBundleAdjustment problems in one call (e.g. one local map
+ * per sequence): every LM trial kernel runs once for all of them, each on its
+ * own arrays and LM state, so K problems cost about one problem's launches.
+ * Results are bit-identical to K orbx_ba_run calls.  problems/results are
+ * arrays of n; one stop flag for all. */
+orbx_status orbx_ba_run_many(orbx_ba* h, int n, const orbx_ba_problem* problems, orbx_ba_result* results,
+                             const volatile int* stop_flag);
 /* A stop flag owned by the handle, in pinned host memory the device reads
  * directly (no page registration): set it from another thread to interrupt
  * orbx_ba_run(h, ..., flag) like LocalMapping::InterruptBA sets mbAbortBA. */

@@ -176,6 +176,7 @@ SIGNATURES = {
     "orbx_ba_run": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),
     "orbx_ba_run_bool": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),
     "orbx_ba_stop_flag": ([P, C.POINTER(C.POINTER(C.c_int))], C.c_int),
+    "orbx_ba_run_many": ([P, C.c_int, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),
     "orbx_local_ba": ([C.POINTER(BaProblem), C.POINTER(BaResult), P, C.c_int], C.c_int),
     "orbx_device_count": ([], C.c_int),
     "orbx_version": ([], C.c_char_p),

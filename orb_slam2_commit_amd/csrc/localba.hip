@@ -35,6 +35,7 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <vector>
 
 #include "../../include/orbx.h"
@@ -186,6 +187,7 @@ struct LmState {
   int iterations;  // the phase's iteration budget
   int stopped;     // the stop flag was seen
   int pad;
+  double final_chi;  // batched driver: activeRobustChi2 of the stored errors at the phase end
 };
 
 // rho's cube rounded once (std::pow(x, 3) in the reference; glibc's pow is
@@ -1270,6 +1272,22 @@ struct LdltPlan {
     }
     return in_lds ? (const void*)k_ba_ldlt<true> : (const void*)k_ba_ldlt<false>;
   }
+  // batched driver: the column-step kernel over K problems (blockIdx.z), sized for the largest
+  const void* many_ptr() const {
+    if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col_many<1, 1024> : (const void*)k_ba_ldlt_col_many<2, 1024>;
+    if (nt == 512)
+      return tpt == 1 ? (const void*)k_ba_ldlt_col_many<1, 512>
+                      : tpt == 2 ? (const void*)k_ba_ldlt_col_many<2, 512> : (const void*)k_ba_ldlt_col_many<4, 512>;
+    return tpt <= 2 ? (const void*)k_ba_ldlt_col_many<2, 256>
+                    : tpt == 4 ? (const void*)k_ba_ldlt_col_many<4, 256> : (const void*)k_ba_ldlt_col_many<8, 256>;
+  }
+  hipError_t prepare_many() const {
+    return hipFuncSetAttribute(many_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  }
+  void launch_many(const BaDev* Ds, int K, hipStream_t st) const {
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(const BaDev*)>(const_cast<void*>(many_ptr())), dim3(1, 1, K),
+                       dim3(nt), smem, st, Ds);
+  }
   void launch(const BaDev& D, hipStream_t st, int stage_limit = 99) const {
     if (col) {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BaDev)>(const_cast<void*>(kernel_ptr())), dim3(1), dim3(nt),
@@ -1473,6 +1491,29 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
 __global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, DevStop stop) { k_ba_lm_control_body(D, stop); }
 __global__ __launch_bounds__(64) void k_ba_lm_control_many(const BaDev* __restrict__ Ds, DevStop stop) {
   k_ba_lm_control_body(Ds[blockIdx.z], stop);
+}
+
+// Batched driver helpers (one block per problem, blockIdx.z): the lambda-init
+// maximum of |H_jj| (k_reduce's partition and order) and the phase's final
+// chi from errors slot 0 (summed in block order, like the host readback).
+__global__ __launch_bounds__(1024) void k_ba_dmax_many(const BaDev* __restrict__ Ds) {
+  const BaDev& D = Ds[blockIdx.z];
+  __shared__ double sm[1024];
+  const int n = D.npa + D.nposes;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) acc = fmax(acc, D.dmax_p[i]);
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) D.scal[3] = sm[0];
+}
+__global__ __launch_bounds__(64) void k_ba_lm_final_many(const BaDev* __restrict__ Ds) {
+  const BaDev& D = Ds[blockIdx.z];
+  const double a = seq_sum_wave(D.scal + 8, D.nbe);
+  if (threadIdx.x == 0) const_cast<LmState*>(D.lm)->final_chi = a;
 }
 
 // Block-wide exclusive scan of one int per thread under `op` (identity
@@ -2448,13 +2489,12 @@ struct LocalBA {
   }
 };
 
-orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, const StopFlag& stop,
-                         hipStream_t st) {
+// Problem intake: validation, the phase-1 sizes, one pinned-arena upload of
+// the raw arrays and k_ba_prep (src/Optimizer.cc:603-745's graph assembly).
+orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
   L.trials = 0;
   for (double& t : L.t_struct) t = 0;
   BaDev& D = L.D;
-  double host_build_ms = 0;
-  const auto t_start = std::chrono::steady_clock::now();
   Ctx& c = L.c;
   const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
   D.nc = nc;
@@ -2577,6 +2617,57 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   D.erobust = erob;
   D.eerr = c.eerr.p;
   D.scal = c.scal.p;
+  return ORBX_OK;
+}
+
+// Write-back (src/Optimizer.cc:817-885): the erase list, poses and points,
+// copied into the caller's arrays asynchronously on st (the caller syncs).
+orbx_status ba_writeback(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, bool ran, hipStream_t st) {
+  BaDev& D = L.D;
+  Ctx& c = L.c;
+  const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
+  const int ge = (ne + LBS - 1) / LBS;
+  res->trials = L.trials;
+  if (!ran) {  // src/Optimizer.cc:749-751: return before any write-back
+    std::memcpy(res->Tcw, pb->Tcw, sizeof(float) * 12 * nc);
+    std::memcpy(res->Xw, pb->Xw, sizeof(float) * 3 * np);
+    if (ne > 0) std::memset(res->edge_outlier, 0, ne);
+    if (res->Tcw_d)
+      for (int i = 0; i < 12 * nc; i++) res->Tcw_d[i] = pb->Tcw[i];
+    if (res->Xw_d)
+      for (int i = 0; i < 3 * np; i++) res->Xw_d[i] = pb->Xw[i];
+    return ORBX_OK;
+  }
+  // :817-847 vToErase
+  if (ne > 0) {
+    hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 0);
+    BA_CHECK(hipGetLastError());
+    BA_CHECK(hipMemcpyAsync(res->edge_outlier, c.flag.p, ne, hipMemcpyDeviceToHost, st));
+  }
+  BA_CHECK(c.Tcw_out.alloc(12 * (size_t)nc));
+  BA_CHECK(c.Xw_out.alloc(3 * (size_t)np));
+  if (res->Tcw_d) BA_CHECK(c.Tcw_d_out.alloc(12 * (size_t)nc));
+  if (res->Xw_d) BA_CHECK(c.Xw_d_out.alloc(3 * (size_t)np));
+  const int gx = (std::max(nc, np) + LBS - 1) / LBS;
+  hipLaunchKernelGGL(k_ba_export, dim3(std::max(gx, 1)), dim3(LBS), 0, st, D, c.Tcw_out.p, c.Xw_out.p,
+                     res->Tcw_d ? c.Tcw_d_out.p : nullptr, res->Xw_d ? c.Xw_d_out.p : nullptr);
+  BA_CHECK(hipGetLastError());
+  BA_CHECK(hipMemcpyAsync(res->Tcw, c.Tcw_out.p, 12 * sizeof(float) * nc, hipMemcpyDeviceToHost, st));
+  BA_CHECK(hipMemcpyAsync(res->Xw, c.Xw_out.p, 3 * sizeof(float) * np, hipMemcpyDeviceToHost, st));
+  if (res->Tcw_d) BA_CHECK(hipMemcpyAsync(res->Tcw_d, c.Tcw_d_out.p, 12 * sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+  if (res->Xw_d) BA_CHECK(hipMemcpyAsync(res->Xw_d, c.Xw_d_out.p, 3 * sizeof(double) * np, hipMemcpyDeviceToHost, st));
+  return ORBX_OK;
+}
+
+orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, const StopFlag& stop,
+                         hipStream_t st) {
+  double host_build_ms = 0;
+  const auto t_start = std::chrono::steady_clock::now();
+  orbx_status s0 = ba_intake(L, pb, st);
+  if (s0 != ORBX_OK) return s0;
+  BaDev& D = L.D;
+  Ctx& c = L.c;
+  const int ne = pb->n_edges;
   res->iterations[0] = res->iterations[1] = 0;
   res->trials = 0;
   res->chi2[0] = res->chi2[1] = 0;
@@ -2614,35 +2705,8 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       if (s != ORBX_OK) return s;
     }
   }
-  res->trials = L.trials;
-  if (!ran) {  // src/Optimizer.cc:749-751: return before any write-back
-    std::memcpy(res->Tcw, pb->Tcw, sizeof(float) * 12 * nc);
-    std::memcpy(res->Xw, pb->Xw, sizeof(float) * 3 * np);
-    if (ne > 0) std::memset(res->edge_outlier, 0, ne);
-    if (res->Tcw_d)
-      for (int i = 0; i < 12 * nc; i++) res->Tcw_d[i] = pb->Tcw[i];
-    if (res->Xw_d)
-      for (int i = 0; i < 3 * np; i++) res->Xw_d[i] = pb->Xw[i];
-    return ORBX_OK;
-  }
-  // :817-847 vToErase
-  if (ne > 0) {
-    hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 0);
-    BA_CHECK(hipGetLastError());
-    BA_CHECK(hipMemcpyAsync(res->edge_outlier, c.flag.p, ne, hipMemcpyDeviceToHost, st));
-  }
-  BA_CHECK(c.Tcw_out.alloc(12 * (size_t)nc));
-  BA_CHECK(c.Xw_out.alloc(3 * (size_t)np));
-  if (res->Tcw_d) BA_CHECK(c.Tcw_d_out.alloc(12 * (size_t)nc));
-  if (res->Xw_d) BA_CHECK(c.Xw_d_out.alloc(3 * (size_t)np));
-  const int gx = (std::max(nc, np) + LBS - 1) / LBS;
-  hipLaunchKernelGGL(k_ba_export, dim3(std::max(gx, 1)), dim3(LBS), 0, st, D, c.Tcw_out.p, c.Xw_out.p,
-                     res->Tcw_d ? c.Tcw_d_out.p : nullptr, res->Xw_d ? c.Xw_d_out.p : nullptr);
-  BA_CHECK(hipGetLastError());
-  BA_CHECK(hipMemcpyAsync(res->Tcw, c.Tcw_out.p, 12 * sizeof(float) * nc, hipMemcpyDeviceToHost, st));
-  BA_CHECK(hipMemcpyAsync(res->Xw, c.Xw_out.p, 3 * sizeof(float) * np, hipMemcpyDeviceToHost, st));
-  if (res->Tcw_d) BA_CHECK(hipMemcpyAsync(res->Tcw_d, c.Tcw_d_out.p, 12 * sizeof(double) * nc, hipMemcpyDeviceToHost, st));
-  if (res->Xw_d) BA_CHECK(hipMemcpyAsync(res->Xw_d, c.Xw_d_out.p, 3 * sizeof(double) * np, hipMemcpyDeviceToHost, st));
+  BA_CHECK(ba_writeback(L, pb, res, ran, st));
+  if (!ran) return ORBX_OK;
   BA_CHECK(hipStreamSynchronize(st));
   if (std::getenv("ORBX_BA_TRACE"))
     std::fprintf(stderr,
@@ -2654,12 +2718,194 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   return ORBX_OK;
 }
 
+// ---- batched driver: K independent problems through the same launches ----
+// Every trial kernel runs once for all K problems (blockIdx.z), each block on
+// its own problem's arrays and LM state; grids span the largest problem and
+// the smaller ones' extra blocks return at once.  Per problem the arithmetic,
+// partitions and reduction orders are those of the single-problem device LM
+// loop, so every problem's result is bit-identical to running it alone.
+struct BaBatch {
+  DBuf<BaDev> dev;       // [Dg_0..Dg_K-1, D0_0..D0_K-1]
+  DBuf<LmState> lm;      // K
+  LmState* lm_host = nullptr;
+  int cap = 0;
+  std::vector<BaDev> hostD;
+  ~BaBatch() {
+    if (lm_host) (void)hipHostFree(lm_host);
+  }
+};
+
+orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations, const StopFlag& stop,
+                          const DevStop& dstop, hipStream_t st, int* iters, double* chis) {
+  int Nmax = 0, gaM = 1, gpM = 1, geM = 1, gnpM = 1, nbpM = 0, gsM = 1, nposM = 0;
+  for (int i = 0; i < K; i++) {
+    const BaDev& D = Ls[i]->D;
+    Nmax = std::max(Nmax, 6 * D.nposes);
+    gaM = std::max(gaM, (D.na + LBS - 1) / LBS);
+    gpM = std::max(gpM, D.nbu);
+    geM = std::max(geM, D.nbe);
+    gnpM = std::max(gnpM, (D.npa + LBS - 1) / LBS);
+    nbpM = std::max(nbpM, D.nblk + D.nposes);
+    gsM = std::max(gsM, D.gsplit);
+    nposM = std::max(nposM, D.nposes);
+  }
+  LdltPlan ldlt;
+  BA_CHECK(ldlt.prepare(Nmax));
+  if (!ldlt.col) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
+  BA_CHECK(ldlt.prepare_many());
+  if (B.cap < K) {
+    if (B.lm_host) (void)hipHostFree(B.lm_host);
+    B.lm_host = nullptr;
+    B.cap = 0;
+    BA_CHECK(hipHostMalloc((void**)&B.lm_host, sizeof(LmState) * K, hipHostMallocDefault));
+    B.cap = K;
+  }
+  BA_CHECK(B.lm.alloc(K));
+  BA_CHECK(B.dev.alloc(2 * (size_t)K));
+  B.hostD.resize(2 * (size_t)K);
+  for (int i = 0; i < K; i++) {
+    B.hostD[i] = Ls[i]->D;
+    B.hostD[i].lm = B.lm.p + i;
+    B.hostD[K + i] = Ls[i]->D;
+    B.hostD[K + i].lm = nullptr;
+  }
+  BA_CHECK(hipMemcpyAsync(B.dev.p, B.hostD.data(), sizeof(BaDev) * 2 * K, hipMemcpyHostToDevice, st));
+  const BaDev* Dg = B.dev.p;
+  const BaDev* D0 = B.dev.p + K;
+  auto linearize = [&](const BaDev* Ds) {
+    hipLaunchKernelGGL(k_ba_linearize_many, dim3(gaM, 1, K), dim3(LBS), 0, st, Ds);
+    hipLaunchKernelGGL(k_ba_point_sum_many, dim3(gnpM, 1, K), dim3(LBS), 0, st, Ds);
+    if (nposM > 0) {
+      hipLaunchKernelGGL(k_ba_cam_sum_many, dim3(nposM, gsM, K), dim3(kGB), 0, st, Ds);
+      hipLaunchKernelGGL(k_ba_cam_fin_many, dim3(nposM, 1, K), dim3(64), 0, st, Ds);
+    }
+  };
+  for (int i = 0; i < K; i++) iters[i] = 0;
+  if (!(stop())) {
+    hipLaunchKernelGGL(k_ba_errors_many, dim3(geM, 1, K), dim3(LBS), 0, st, D0, 1, 0);
+    linearize(D0);
+    hipLaunchKernelGGL(k_ba_dmax_many, dim3(1, 1, K), dim3(1024), 0, st, D0);
+    hipLaunchKernelGGL(k_ba_lm_init_many, dim3(1, 1, K), dim3(64), 0, st, Dg, iterations);
+    BA_CHECK(hipGetLastError());
+    for (int budget = iterations, first = 1;; first = 0) {
+      for (int t = 0; t < budget; t++) {
+        if (!(first && t == 0)) linearize(Dg);  // gated per problem
+        hipLaunchKernelGGL(k_ba_point_schur_many, dim3(gaM, 1, K), dim3(LBS), 0, st, Dg, 0.0);
+        if (nposM > 0) {
+          hipLaunchKernelGGL(k_ba_pairs_many, dim3(nbpM, gsM, K), dim3(kPB), 0, st, Dg);
+          hipLaunchKernelGGL(k_ba_schur_fin_many, dim3(nbpM, 1, K), dim3(64), 0, st, Dg, 0.0);
+          ldlt.launch_many(Dg, K, st);
+        }
+        hipLaunchKernelGGL(k_ba_update_many, dim3(gpM, 1, K), dim3(LBS), 0, st, Dg, 0.0);
+        hipLaunchKernelGGL(k_ba_errors_many, dim3(geM, 1, K), dim3(LBS), 0, st, Dg, 1, 1);
+        hipLaunchKernelGGL(k_ba_lm_control_many, dim3(1, 1, K), dim3(64), 0, st, Dg, dstop);
+      }
+      hipLaunchKernelGGL(k_ba_errors_many, dim3(geM, 1, K), dim3(LBS), 0, st, D0, 0, 0);
+      hipLaunchKernelGGL(k_ba_lm_final_many, dim3(1, 1, K), dim3(64), 0, st, Dg);
+      BA_CHECK(hipGetLastError());
+      BA_CHECK(hipMemcpyAsync(B.lm_host, B.lm.p, sizeof(LmState) * K, hipMemcpyDeviceToHost, st));
+      BA_CHECK(hipStreamSynchronize(st));
+      int left = 0;
+      for (int i = 0; i < K; i++)
+        if (!B.lm_host[i].done) left = std::max(left, iterations - B.lm_host[i].it);
+      if (left == 0) break;
+      budget = std::max(1, left);
+    }
+    bool rej = false;
+    for (int i = 0; i < K; i++) {
+      iters[i] = B.lm_host[i].it;
+      Ls[i]->trials += B.lm_host[i].trials;
+      chis[i] = B.lm_host[i].final_chi;
+      rej |= B.lm_host[i].rejected != 0;
+    }
+    if (rej) {  // the pops of problems that ended on a rejected trial (gated per problem)
+      hipLaunchKernelGGL(k_ba_restore_many, dim3(gpM, 1, K), dim3(LBS), 0, st, Dg);
+      BA_CHECK(hipGetLastError());
+    }
+  } else {
+    hipLaunchKernelGGL(k_ba_errors_many, dim3(geM, 1, K), dim3(LBS), 0, st, D0, 0, 0);
+    hipLaunchKernelGGL(k_ba_lm_final_many, dim3(1, 1, K), dim3(64), 0, st, Dg);
+    BA_CHECK(hipGetLastError());
+    BA_CHECK(hipMemcpyAsync(B.lm_host, B.lm.p, sizeof(LmState) * K, hipMemcpyDeviceToHost, st));
+    BA_CHECK(hipStreamSynchronize(st));
+    for (int i = 0; i < K; i++) chis[i] = B.lm_host[i].final_chi;
+  }
+  return ORBX_OK;
+}
+
+// K LocalBundleAdjustment calls at once: per-problem intake and structure,
+// each LM phase batched, per-problem write-back.  Problems that need the host
+// structure build or a reduced system beyond the column-step kernel run one
+// by one instead (same results).
+orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_ba_problem* pbs,
+                              orbx_ba_result* ress, const StopFlag& stop, hipStream_t st) {
+  for (int i = 0; i < K; i++) {
+    orbx_status s = ba_intake(*Ls[i], &pbs[i], st);
+    if (s != ORBX_OK) return s;
+  }
+  DevStop dstop{nullptr, nullptr};
+  bool batch = std::getenv("ORBX_BA_HOST_LM") == nullptr && Ls[0]->map_stop(stop, &dstop);
+  for (int i = 0; i < K; i++) batch &= Ls[i]->dev_struct;
+  if (!batch) {  // one by one (intake again inside: the arenas are reused)
+    for (int i = 0; i < K; i++) {
+      orbx_status s = run_local_ba(*Ls[i], &pbs[i], &ress[i], stop, st);
+      if (s != ORBX_OK) return s;
+    }
+    return ORBX_OK;
+  }
+  std::vector<int> it(K);
+  std::vector<double> chi(K);
+  for (int i = 0; i < K; i++) {
+    ress[i].iterations[0] = ress[i].iterations[1] = 0;
+    ress[i].trials = 0;
+    ress[i].chi2[0] = ress[i].chi2[1] = 0;
+  }
+  bool ran = false;
+  if (!(stop())) {  // src/Optimizer.cc:749-751
+    ran = true;
+    for (int i = 0; i < K; i++) BA_CHECK(Ls[i]->build_structure(-1, st));
+    orbx_status s = optimize_many(Ls, K, B, 5, stop, dstop, st, it.data(), chi.data());
+    if (s == ORBX_ERR_SIZE) {  // reduced system beyond the column-step kernel: one by one
+      for (int i = 0; i < K; i++) {
+        s = run_local_ba(*Ls[i], &pbs[i], &ress[i], stop, st);
+        if (s != ORBX_OK) return s;
+      }
+      return ORBX_OK;
+    }
+    if (s != ORBX_OK) return s;
+    for (int i = 0; i < K; i++) {
+      ress[i].iterations[0] = it[i];
+      ress[i].chi2[0] = chi[i];
+    }
+    if (!(stop())) {
+      for (int i = 0; i < K; i++) {  // :764-802 level-1 outliers, drop robust kernels
+        const int ne = pbs[i].n_edges;
+        if (ne > 0)
+          hipLaunchKernelGGL(k_ba_outliers, dim3((ne + LBS - 1) / LBS), dim3(LBS), 0, st, Ls[i]->D, Ls[i]->c.flag.p, 1);
+        BA_CHECK(hipGetLastError());
+      }
+      for (int i = 0; i < K; i++) BA_CHECK(Ls[i]->build_structure(0, st));
+      s = optimize_many(Ls, K, B, 10, stop, dstop, st, it.data(), chi.data());
+      if (s != ORBX_OK) return s;
+      for (int i = 0; i < K; i++) {
+        ress[i].iterations[1] = it[i];
+        ress[i].chi2[1] = chi[i];
+      }
+    }
+  }
+  for (int i = 0; i < K; i++) BA_CHECK(ba_writeback(*Ls[i], &pbs[i], &ress[i], ran, st));
+  BA_CHECK(hipStreamSynchronize(st));
+  return ORBX_OK;
+}
+
 }  // namespace orbx
 
 struct orbx_ba {
   int device = 0;
   hipStream_t st = nullptr;
   orbx::LocalBA L;
+  std::vector<std::unique_ptr<orbx::LocalBA>> more;  // orbx_ba_run_many: problems 1..K-1
+  orbx::BaBatch batch;
 };
 
 extern "C" {
@@ -2680,6 +2926,35 @@ orbx_status orbx_ba_create(int device, orbx_ba** out) {
   }
   *out = h;
   return ORBX_OK;
+}
+
+orbx_status orbx_ba_run_many(orbx_ba* h, int n, const orbx_ba_problem* problems, orbx_ba_result* results,
+                             const volatile int* stop_flag) {
+  if (!h || n < 0 || (n > 0 && (!problems || !results))) return ORBX_ERR_ARG;
+  if (n == 0) return ORBX_OK;
+  for (int i = 0; i < n; i++) {
+    const orbx_ba_problem* p = &problems[i];
+    const orbx_ba_result* r = &results[i];
+    if (p->n_cams < 0 || p->n_points < 0 || p->n_edges < 0 || (p->n_cams > 0 && (!p->Tcw || !p->intr)) ||
+        (p->n_points > 0 && !p->Xw) ||
+        (p->n_edges > 0 && (!p->edge_point || !p->edge_cam || !p->obs || !p->inv_sigma2 || !r->edge_outlier)) ||
+        (p->n_cams > 0 && !r->Tcw) || (p->n_points > 0 && !r->Xw))
+      return ORBX_ERR_ARG;
+  }
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  while ((int)h->more.size() < n - 1) {
+    h->more.emplace_back(new (std::nothrow) orbx::LocalBA());
+    if (!h->more.back()) {
+      h->more.pop_back();
+      return ORBX_ERR_HIP;
+    }
+  }
+  std::vector<orbx::LocalBA*> Ls(n);
+  Ls[0] = &h->L;
+  for (int i = 1; i < n; i++) Ls[i] = h->more[i - 1].get();
+  orbx::StopFlag sf;
+  sf.i = stop_flag;
+  return orbx::run_local_ba_many(Ls.data(), n, h->batch, problems, results, sf, h->st);
 }
 
 orbx_status orbx_ba_stop_flag(orbx_ba* h, volatile int** flag) {

@@ -526,6 +526,29 @@ class Optimizer:
         out.update(iterations=tuple(R.iterations), trials=R.trials, chi2=tuple(R.chi2))
         return out
 
+    def LocalBundleAdjustmentMany(self, probs, stop=False):
+        """K independent problems through one batched LM loop (orbx_ba_run_many); returns the
+        list of result dicts, each bit-identical to LocalBundleAdjustment on that problem."""
+        K = len(probs)
+        keep, outs = [], []
+        Ps, Rs = (_lib.BaProblem * K)(), (_lib.BaResult * K)()
+        for k, prob in enumerate(probs):
+            a = _ba_arrays(prob)
+            nc, npt, ne = len(a["Tcw"]), len(a["Xw"]), len(a["edge_point"])
+            Ps[k] = _lib.BaProblem(nc, ptr(a["Tcw"]), ptr(a["fixed"]), ptr(a["intr"]), npt, ptr(a["Xw"]), ne,
+                                   ptr(a["edge_point"]), ptr(a["edge_cam"]), ptr(a["obs"]), ptr(a["inv_sigma2"]))
+            out = dict(Tcw=np.zeros((nc, 12), np.float32), Xw=np.zeros((npt, 3), np.float32),
+                       edge_outlier=np.zeros(ne, np.uint8), Tcw_d=np.zeros((nc, 12)), Xw_d=np.zeros((npt, 3)))
+            Rs[k] = _lib.BaResult(ptr(out["Tcw"]), ptr(out["Xw"]), ptr(out["edge_outlier"]), ptr(out["Tcw_d"]),
+                                  ptr(out["Xw_d"]))
+            keep.append(a)
+            outs.append(out)
+        self._stop[0] = 1 if stop else 0
+        check(_lib.lib().orbx_ba_run_many(self._h, K, Ps, Rs, C.cast(self._stop, C.c_void_p)), "orbx_ba_run_many")
+        for k in range(K):
+            outs[k].update(iterations=tuple(Rs[k].iterations), trials=Rs[k].trials, chi2=tuple(Rs[k].chi2))
+        return outs
+
 
 def pose_problem_struct(prob, outputs=None):
     """orbx_pose_problem from a dict (host numpy or device tensors); outputs allocated on the host

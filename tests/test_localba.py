@@ -375,3 +375,27 @@ def test_gpu_localba_stop_flag_mid_run(ba):
     assert flag[0] == 1
     assert sum(r["iterations"]) < sum(full["iterations"])
     assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_localba_batched_bit_identical(ba):
+    """orbx_ba_run_many: problems of different sizes, LM histories (rejections, _nBad stop)
+    and fixed cameras through one batched LM loop give each problem the bits, iterations and
+    trials of its own orbx_ba_run."""
+    probs = [synth.localba_problem(seed=7), reject_problem("rejects_b"), small_problem(seed=12),
+             synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000), reject_problem("nbad_stop"),
+             synth.localba_problem(seed=9, n_local=12, n_fixed=3, n_points=3000)]
+    many = ba.LocalBundleAdjustmentMany(probs)
+    for P, a in zip(probs, many):
+        b = ba.LocalBundleAdjustment(P)
+        for k in ("Tcw", "Xw", "Tcw_d", "Xw_d", "edge_outlier"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
+        assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+        assert a["chi2"] == b["chi2"]
+    _compare(many[0], oracle.local_ba(probs[0]))
+    one = ba.LocalBundleAdjustmentMany(probs[:1])[0]  # K = 1 through the batched path
+    np.testing.assert_array_equal(one["Tcw_d"], many[0]["Tcw_d"])
+    stopped = ba.LocalBundleAdjustmentMany(probs[:2], stop=True)
+    for P, r in zip(probs[:2], stopped):
+        assert list(r["iterations"]) == [0, 0] and r["trials"] == 0
+        np.testing.assert_array_equal(r["Tcw"], np.asarray(P["Tcw"], np.float32).reshape(-1, 12))
