@@ -666,29 +666,48 @@ __global__ __launch_bounds__(64) void k_ba_cam_fin_many(const BaDev* __restrict_
 __device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lambda) {
   if (lm_skip(D)) return;
   lambda = lm_lambda(D, lambda);
-  const int k = blockIdx.x * LBS + threadIdx.x;
+  // the block's 256 positions are contiguous: Hpl comes in and BD / cf go out
+  // through LDS with coalesced 8-B accesses (per-lane 144-B strides made every
+  // load/store instruction touch 64 separate lines)
+  __shared__ double sh[LBS * 18];
+  __shared__ double scf[LBS * 6];
+  const int k0 = blockIdx.x * LBS, t = threadIdx.x, k = k0 + t;
   if (k == 0 && D.nposes == 0) D.scal[2] = 1.0;  // no reduced system to factor
-  if (k >= D.na) return;
-  const int i = D.pos_pt[k];
-  double Dm[9];
-  for (int j = 0; j < 9; j++) Dm[j] = D.Hll[9 * i + j];
-  Dm[0] += lambda;
-  Dm[4] += lambda;
-  Dm[8] += lambda;
-  double Di[9];
-  inv3(Dm, Di);
-  if (k == D.pt_off[i])
-    for (int j = 0; j < 9; j++) D.Dinv[9 * i + j] = Di[j];
-  if (D.pcam[k] < 0) return;
-  const double b0 = D.bl[3 * i], b1 = D.bl[3 * i + 1], b2 = D.bl[3 * i + 2];
-  double db[3];
-  for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
-  const double* B1 = D.Hpl + 18 * (size_t)k;
-  double* bd = D.BD + 18 * (size_t)k;
-  for (int r = 0; r < 6; r++) {
-    for (int c = 0; c < 3; c++) bd[3 * r + c] = B1[3 * r] * Di[c] + B1[3 * r + 1] * Di[3 + c] + B1[3 * r + 2] * Di[6 + c];
-    D.cf[6 * (size_t)k + r] = B1[3 * r] * db[0] + B1[3 * r + 1] * db[1] + B1[3 * r + 2] * db[2];
+  if (k0 >= D.na) return;  // block-uniform
+  const int nk = min(LBS, D.na - k0);
+  for (int j = t; j < nk * 18; j += LBS) sh[j] = D.Hpl[18 * (size_t)k0 + j];
+  __syncthreads();
+  double bdv[18], cfv[6];
+  const bool act = k < D.na;
+  if (act) {
+    const int i = D.pos_pt[k];
+    double Dm[9];
+    for (int j = 0; j < 9; j++) Dm[j] = D.Hll[9 * i + j];
+    Dm[0] += lambda;
+    Dm[4] += lambda;
+    Dm[8] += lambda;
+    double Di[9];
+    inv3(Dm, Di);
+    if (k == D.pt_off[i])
+      for (int j = 0; j < 9; j++) D.Dinv[9 * i + j] = Di[j];
+    const double b0 = D.bl[3 * i], b1 = D.bl[3 * i + 1], b2 = D.bl[3 * i + 2];
+    double db[3];
+    for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+    const double* B1 = sh + 18 * t;
+    for (int r = 0; r < 6; r++) {
+      for (int c = 0; c < 3; c++) bdv[3 * r + c] = B1[3 * r] * Di[c] + B1[3 * r + 1] * Di[3 + c] + B1[3 * r + 2] * Di[6 + c];
+      cfv[r] = B1[3 * r] * db[0] + B1[3 * r + 1] * db[1] + B1[3 * r + 2] * db[2];
+    }
   }
+  __syncthreads();
+  if (act) {
+    for (int j = 0; j < 18; j++) sh[18 * t + j] = bdv[j];
+    for (int r = 0; r < 6; r++) scf[6 * t + r] = cfv[r];
+  }
+  __syncthreads();
+  // (positions on fixed cameras get values too; nothing reads them)
+  for (int j = t; j < nk * 18; j += LBS) D.BD[18 * (size_t)k0 + j] = sh[j];
+  for (int j = t; j < nk * 6; j += LBS) D.cf[6 * (size_t)k0 + j] = scf[j];
 }
 __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) { k_ba_point_schur_body(D, lambda); }
 __global__ __launch_bounds__(LBS) void k_ba_point_schur_many(const BaDev* __restrict__ Ds, double lambda) {
