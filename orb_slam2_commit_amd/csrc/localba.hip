@@ -427,69 +427,105 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ in, 
 }
 
 // constructQuadraticForm of one edge with DIM-dimensional error (2 mono, 3 stereo)
-template <int DIM>
-__device__ __forceinline__ void lin_accumulate(const BaDev& D, int k, int e, int c, const double* A, const double* Bm) {
-  const double info = D.einfo[e];
-  double omr[DIM], W = info;
+// One staged output array of the linearisation: each thread's NV values go to
+// LDS, then the block's contiguous NV doubles per position leave with
+// coalesced 8-B stores (position k's values land at out[NV * k + j], as
+// before); PARTS > 1 stages the block's positions in that many slices so the
+// LDS buffer stays at LBS * 21 doubles.
+template <int NV, int PARTS, class F>
+__device__ __forceinline__ void lin_stage_store(double* sh, double* out, int k0, int nk, bool act, F f) {
+  constexpr int PS = LBS / PARTS;
+  const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < DIM; i++) omr[i] = -info * D.eerr[3 * e + i];
+  for (int q = 0; q < PARTS; q++) {
+    if (act && t / PS == q) f(sh + NV * (t - q * PS));
+    __syncthreads();
+    const int n = min(PS, nk - q * PS);
+    for (int j = t; j < n * NV; j += LBS) out[NV * ((size_t)k0 + q * PS) + j] = sh[j];
+    __syncthreads();
+  }
+}
+
+// constructQuadraticForm terms of one edge (DIM = 2 mono, 3 stereo); written
+// through LDS by the block (positions on fixed cameras get pose terms too:
+// nothing reads them).
+struct LinTerms {
+  double omr[3], W;
+};
+template <int DIM>
+__device__ __forceinline__ LinTerms lin_weights(const BaDev& D, int e) {
+  LinTerms T;
+  const double info = D.einfo[e];
+  T.W = info;
+#pragma unroll
+  for (int i = 0; i < DIM; i++) T.omr[i] = -info * D.eerr[3 * e + i];
   if (D.erobust[e]) {
     double c2 = 0;
 #pragma unroll
     for (int i = 0; i < DIM; i++) c2 += D.eerr[3 * e + i] * (info * D.eerr[3 * e + i]);
     double rho[3];
     huber(c2, D.edelta[e], D.edsqr[e], rho);
-    W = rho[1] * info;
+    T.W = rho[1] * info;
 #pragma unroll
-    for (int i = 0; i < DIM; i++) omr[i] *= rho[1];
+    for (int i = 0; i < DIM; i++) T.omr[i] *= rho[1];
   }
-  double* pc = D.ptc + 12 * (size_t)k;
+  return T;
+}
+template <int DIM>
+__device__ __forceinline__ void lin_point_terms(const LinTerms& T, const double* A, double* pc) {
 #pragma unroll
   for (int r = 0; r < 3; r++) {
     double s = 0;
 #pragma unroll
-    for (int d = 0; d < DIM; d++) s += A[3 * d + r] * omr[d];
+    for (int d = 0; d < DIM; d++) s += A[3 * d + r] * T.omr[d];
     pc[9 + r] = s;
 #pragma unroll
     for (int cc = 0; cc < 3; cc++) {
       double h = 0;
 #pragma unroll
-      for (int d = 0; d < DIM; d++) h += A[3 * d + r] * W * A[3 * d + cc];
+      for (int d = 0; d < DIM; d++) h += A[3 * d + r] * T.W * A[3 * d + cc];
       pc[3 * r + cc] = h;
     }
   }
-  if (D.chidx[c] >= 0) {
-    double* cm = D.cmc + 42 * (size_t)k;
-    double* hp = D.Hpl + 18 * (size_t)k;
+}
+template <int DIM>
+__device__ __forceinline__ void lin_pose_terms(const LinTerms& T, const double* Bm, double* cm) {
 #pragma unroll
-    for (int r = 0; r < 6; r++) {
-      double s = 0;
+  for (int r = 0; r < 6; r++) {
+    double s = 0;
 #pragma unroll
-      for (int d = 0; d < DIM; d++) s += Bm[6 * d + r] * omr[d];
-      cm[36 + r] = s;
+    for (int d = 0; d < DIM; d++) s += Bm[6 * d + r] * T.omr[d];
+    cm[36 + r] = s;
 #pragma unroll
-      for (int cc = 0; cc < 6; cc++) {
-        double h = 0;
+    for (int cc = 0; cc < 6; cc++) {
+      double h = 0;
 #pragma unroll
-        for (int d = 0; d < DIM; d++) h += Bm[6 * d + r] * W * Bm[6 * d + cc];
-        cm[6 * r + cc] = h;
-      }
-#pragma unroll
-      for (int cc = 0; cc < 3; cc++) {
-        double h = 0;
-#pragma unroll
-        for (int d = 0; d < DIM; d++) h += Bm[6 * d + r] * W * A[3 * d + cc];
-        hp[3 * r + cc] = h;
-      }
+      for (int d = 0; d < DIM; d++) h += Bm[6 * d + r] * T.W * Bm[6 * d + cc];
+      cm[6 * r + cc] = h;
     }
   }
+}
+template <int DIM>
+__device__ __forceinline__ void lin_cross_terms(const LinTerms& T, const double* A, const double* Bm, double* hp) {
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int cc = 0; cc < 3; cc++) {
+      double h = 0;
+#pragma unroll
+      for (int d = 0; d < DIM; d++) h += Bm[6 * d + r] * T.W * A[3 * d + cc];
+      hp[3 * r + cc] = h;
+    }
 }
 
 __device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
   if (lm_skip_lin(D)) return;
-  const int k = blockIdx.x * LBS + threadIdx.x;
-  if (k >= D.na) return;
-  const int e = D.act[k];
+  __shared__ double sh[LBS * 21];
+  const int k0 = blockIdx.x * LBS, k = k0 + threadIdx.x;
+  if (k0 >= D.na) return;  // block-uniform
+  const int nk = min(LBS, D.na - k0);
+  const bool act = k < D.na;
+  const int e = act ? D.act[k] : D.act[k0];
   const int c = D.ecam[e], p = D.ept[e];
   Quat q = {D.cq[4 * c], D.cq[4 * c + 1], D.cq[4 * c + 2], D.cq[4 * c + 3]};
   const double Xw[3] = {D.X[3 * p], D.X[3 * p + 1], D.X[3 * p + 2]};
@@ -534,10 +570,16 @@ __device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
     Bm[16] = 0;
     Bm[17] = Bm[5] - bf / z_2;
   }
-  if (st)
-    lin_accumulate<3>(D, k, e, c, A, Bm);
-  else
-    lin_accumulate<2>(D, k, e, c, A, Bm);
+  const LinTerms T = st ? lin_weights<3>(D, e) : lin_weights<2>(D, e);
+  lin_stage_store<12, 1>(sh, D.ptc, k0, nk, act, [&](double* o) {
+    if (st) lin_point_terms<3>(T, A, o); else lin_point_terms<2>(T, A, o);
+  });
+  lin_stage_store<18, 1>(sh, D.Hpl, k0, nk, act, [&](double* o) {
+    if (st) lin_cross_terms<3>(T, A, Bm, o); else lin_cross_terms<2>(T, A, Bm, o);
+  });
+  lin_stage_store<42, 2>(sh, D.cmc, k0, nk, act, [&](double* o) {
+    if (st) lin_pose_terms<3>(T, Bm, o); else lin_pose_terms<2>(T, Bm, o);
+  });
 }
 __global__ __launch_bounds__(LBS) void k_ba_linearize(BaDev D) { k_ba_linearize_body(D); }
 __global__ __launch_bounds__(LBS) void k_ba_linearize_many(const BaDev* __restrict__ Ds) {
