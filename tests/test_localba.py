@@ -399,3 +399,34 @@ def test_gpu_localba_batched_bit_identical(ba):
     for P, r in zip(probs[:2], stopped):
         assert list(r["iterations"]) == [0, 0] and r["trials"] == 0
         np.testing.assert_array_equal(r["Tcw"], np.asarray(P["Tcw"], np.float32).reshape(-1, 12))
+
+
+@pytest.mark.gpu
+def test_gpu_localba_batched_fallback_and_stop(ba):
+    """A batch holding a problem whose edges are not grouped by point (host structure build)
+    runs one by one with the same results; a stop flag raised mid-run ends the batched loop."""
+    import threading
+    import time
+    P1 = synth.localba_problem(seed=7)
+    P2 = dict(small_problem(seed=11))
+    perm = np.random.default_rng(0).permutation(len(P2["edge_point"]))
+    for k in ("edge_point", "edge_cam", "obs", "inv_sigma2"):
+        P2[k] = np.ascontiguousarray(np.asarray(P2[k])[perm])
+    many = ba.LocalBundleAdjustmentMany([P1, P2])
+    for P, a in zip((P1, P2), many):
+        b = ba.LocalBundleAdjustment(P)
+        for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
+        assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+    probs = [synth.localba_problem(seed=8 + k, n_local=30, n_fixed=4, n_points=4000) for k in range(4)]
+    full = ba.LocalBundleAdjustmentMany(probs)
+    flag = ba._stop
+    t = threading.Thread(target=lambda: (time.sleep(0.003), flag.__setitem__(0, 1)))
+    t.start()
+    # the wrapper writes the handle flag (0) before the call; the thread raises it mid-run
+    rs = ba.LocalBundleAdjustmentMany(probs)
+    t.join()
+    flag[0] = 0
+    assert sum(sum(r["iterations"]) for r in rs) < sum(sum(r["iterations"]) for r in full)
+    for r in rs:
+        assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
