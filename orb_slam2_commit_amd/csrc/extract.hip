@@ -490,18 +490,18 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     const bool lane_ok = lr < RPI;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, TH * lw + S, 0x00020000);
+    // every load unconditional (a lane outside the window reads past num_records and gets
+    // zeros): no branch between them, so all KMAX are in flight before the first wait
     uint32_t v[KMAX][4];
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
       const int r = k * RPI + lr;
-      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0;
-      if (k * RPI < TH && lane_ok && r < TH) {
-        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, r * lw + 16 * lj, 0, 0);
-        v[k][0] = q[0];
-        v[k][1] = q[1];
-        v[k][2] = q[2];
-        v[k][3] = q[3];
-      }
+      const uint32_t off = (lane_ok && r < TH) ? (uint32_t)(r * lw + 16 * lj) : 0x80000000u;
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      v[k][0] = q[0];
+      v[k][1] = q[1];
+      v[k][2] = q[2];
+      v[k][3] = q[3];
     }
     // zero the score map (its border row/column stands for "outside the region")
     for (int i = lane * 16; i < map_bytes; i += 64 * 16) *(uint4*)(smap + i) = make_uint4(0, 0, 0, 0);
