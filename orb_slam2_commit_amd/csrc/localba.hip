@@ -1503,6 +1503,9 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
   LmState* L = const_cast<LmState*>(D.lm);
   const int nbu = D.nbu;
   if (L->done) return;  // uniform; a finished phase keeps `rejected` for the final restore
+  // the flag's host-memory read is issued first, so its latency hides behind the sums (one read
+  // serves both of the loop's polls below; a flag raised after it is seen at the next trial)
+  const bool st = stop();
   const double* p = D.scal + 8;
   const double b = seq_sum_wave(p + D.nbe, D.nbe);
   const double u = seq_sum_wave(p + 2 * D.nbe, nbu);
@@ -1529,7 +1532,6 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
     if (ok2) L->rejected = 1;
   }
   L->qmax++;
-  const bool st = stop();
   if (rho < 0 && L->qmax < 10 && !st) {  // another trial of this iteration
     L->relin = 0;
     return;
@@ -1544,7 +1546,7 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
     brk = L->nBad >= 3;
   }
   L->qmax = 0;
-  const bool st2 = !brk && L->it < L->iterations && stop();
+  const bool st2 = !brk && L->it < L->iterations && st;
   L->stopped = st || st2;
   L->done = (brk || L->it >= L->iterations || st2) ? 1 : 0;
   L->relin = L->done ? 0 : 1;
