@@ -1367,58 +1367,71 @@ __device__ __forceinline__ void k_ba_update_body(const BaDev& D, double lambda) 
   if (lm_skip(D) || (int)blockIdx.x >= D.nbu) return;
   lambda = lm_lambda(D, lambda);
   const int i = blockIdx.x * LBS + threadIdx.x;
-  if (D.lm && D.lm->rejected) {  // device LM: the previous trial's pop, same thread mapping as k_ba_restore
-    if (i < D.npa) {
-      const int p = D.pt_id[i];
-      for (int r = 0; r < 3; r++) D.X[3 * p + r] = D.Xbak[3 * p + r];
-    } else if (i < D.npa + D.nposes) {
-      const int c = D.pose_cam[i - D.npa];
-      for (int r = 0; r < 4; r++) D.cq[4 * c + r] = D.cbak[7 * c + r];
-      for (int r = 0; r < 3; r++) D.ct[3 * c + r] = D.cbak[7 * c + 4 + r];
-    }
-  }
+  // device LM: the previous trial's pop is folded in (same thread mapping as k_ba_restore).
+  // Every state value is loaded into registers before any store: the X / Xbak (cq, cbak)
+  // stores may alias the next loads as far as the compiler knows, which otherwise
+  // serialised each load behind the previous store (one memory round trip apiece).
+  const bool rej = D.lm && D.lm->rejected;
   const bool ok = D.scal[2] != 0.0;
   double sc = 0;
-  if (ok && i < D.npa) {
-    double c[3] = {D.bl[3 * i], D.bl[3 * i + 1], D.bl[3 * i + 2]};
-    for (int k = D.pt_off[i]; k < D.pt_off[i + 1]; k++) {
-      const int ci = D.pcam[k];
-      if (ci < 0) continue;
-      const double* B = D.Hpl + 18 * (size_t)k;
-      for (int j = 0; j < 3; j++)
-        for (int r = 0; r < 6; r++) c[j] -= B[3 * r + j] * D.xp[6 * ci + r];
-    }
-    const double* Di = D.Dinv + 9 * (size_t)i;
-    double x[3];
-    for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
+  if (i < D.npa) {
     const int p = D.pt_id[i];
-    for (int r = 0; r < 3; r++) {
-      D.Xbak[3 * p + r] = D.X[3 * p + r];
-      D.X[3 * p + r] += x[r];
-      sc += x[r] * (lambda * x[r] + D.bl[3 * i + r]);
+    const double* from = rej ? D.Xbak : D.X;
+    const double X0[3] = {from[3 * p], from[3 * p + 1], from[3 * p + 2]};
+    if (ok) {
+      double c[3] = {D.bl[3 * i], D.bl[3 * i + 1], D.bl[3 * i + 2]};
+      for (int k = D.pt_off[i]; k < D.pt_off[i + 1]; k++) {
+        const int ci = D.pcam[k];
+        if (ci < 0) continue;
+        const double* B = D.Hpl + 18 * (size_t)k;
+        for (int j = 0; j < 3; j++)
+          for (int r = 0; r < 6; r++) c[j] -= B[3 * r + j] * D.xp[6 * ci + r];
+      }
+      const double* Di = D.Dinv + 9 * (size_t)i;
+      double x[3];
+      for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
+      for (int r = 0; r < 3; r++) sc += x[r] * (lambda * x[r] + D.bl[3 * i + r]);
+      for (int r = 0; r < 3; r++) {
+        D.Xbak[3 * p + r] = X0[r];
+        D.X[3 * p + r] = X0[r] + x[r];
+      }
+    } else if (rej) {
+      for (int r = 0; r < 3; r++) D.X[3 * p + r] = X0[r];
     }
-  } else if (ok && i < D.npa + D.nposes) {
+  } else if (i < D.npa + D.nposes) {
     const int pi = i - D.npa;
     const int c = D.pose_cam[pi];
-    double u[6];
-    for (int r = 0; r < 6; r++) {
-      u[r] = D.xp[6 * pi + r];
-      sc += u[r] * (lambda * u[r] + D.bp[6 * pi + r]);
+    double q4[4], t3[3];
+    if (rej) {
+      for (int r = 0; r < 4; r++) q4[r] = D.cbak[7 * c + r];
+      for (int r = 0; r < 3; r++) t3[r] = D.cbak[7 * c + 4 + r];
+    } else {
+      for (int r = 0; r < 4; r++) q4[r] = D.cq[4 * c + r];
+      for (int r = 0; r < 3; r++) t3[r] = D.ct[3 * c + r];
     }
-    for (int r = 0; r < 4; r++) D.cbak[7 * c + r] = D.cq[4 * c + r];
-    for (int r = 0; r < 3; r++) D.cbak[7 * c + 4 + r] = D.ct[3 * c + r];
-    const SE3d E = se3_exp(u);
-    const Quat q = {D.cq[4 * c], D.cq[4 * c + 1], D.cq[4 * c + 2], D.cq[4 * c + 3]};
-    const double t[3] = {D.ct[3 * c], D.ct[3 * c + 1], D.ct[3 * c + 2]};
-    double rt[3];
-    qrot(E.q, t, rt);
-    Quat nq = qmul(E.q, q);
-    qnormalize(nq);
-    D.cq[4 * c] = nq.x;
-    D.cq[4 * c + 1] = nq.y;
-    D.cq[4 * c + 2] = nq.z;
-    D.cq[4 * c + 3] = nq.w;
-    for (int r = 0; r < 3; r++) D.ct[3 * c + r] = E.t[r] + rt[r];
+    if (ok) {
+      double u[6];
+      for (int r = 0; r < 6; r++) {
+        u[r] = D.xp[6 * pi + r];
+        sc += u[r] * (lambda * u[r] + D.bp[6 * pi + r]);
+      }
+      for (int r = 0; r < 4; r++) D.cbak[7 * c + r] = q4[r];
+      for (int r = 0; r < 3; r++) D.cbak[7 * c + 4 + r] = t3[r];
+      const SE3d E = se3_exp(u);
+      const Quat q = {q4[0], q4[1], q4[2], q4[3]};
+      double rt[3];
+      qrot(E.q, t3, rt);
+      Quat nq = qmul(E.q, q);
+      qnormalize(nq);
+      D.cq[4 * c] = nq.x;
+      D.cq[4 * c + 1] = nq.y;
+      D.cq[4 * c + 2] = nq.z;
+      D.cq[4 * c + 3] = nq.w;
+      for (int r = 0; r < 3; r++) D.ct[3 * c + r] = E.t[r] + rt[r];
+    } else if (rej) {
+      for (int r = 0; r < 4; r++) D.cq[4 * c + r] = q4[r];
+      for (int r = 0; r < 3; r++) D.ct[3 * c + r] = t3[r];
+    }
   }
   block_partial(sc, D.scal + 8 + 2 * D.nbe);
 }
@@ -1432,11 +1445,14 @@ __device__ __forceinline__ void k_ba_restore_body(const BaDev& D) {
   const int i = blockIdx.x * LBS + threadIdx.x;
   if (i < D.npa) {
     const int p = D.pt_id[i];
-    for (int r = 0; r < 3; r++) D.X[3 * p + r] = D.Xbak[3 * p + r];
+    const double v[3] = {D.Xbak[3 * p], D.Xbak[3 * p + 1], D.Xbak[3 * p + 2]};  // loads before stores
+    for (int r = 0; r < 3; r++) D.X[3 * p + r] = v[r];
   } else if (i < D.npa + D.nposes) {
     const int c = D.pose_cam[i - D.npa];
-    for (int r = 0; r < 4; r++) D.cq[4 * c + r] = D.cbak[7 * c + r];
-    for (int r = 0; r < 3; r++) D.ct[3 * c + r] = D.cbak[7 * c + 4 + r];
+    double v[7];
+    for (int r = 0; r < 7; r++) v[r] = D.cbak[7 * c + r];
+    for (int r = 0; r < 4; r++) D.cq[4 * c + r] = v[r];
+    for (int r = 0; r < 3; r++) D.ct[3 * c + r] = v[4 + r];
   }
 }
 __global__ __launch_bounds__(LBS) void k_ba_restore(BaDev D) { k_ba_restore_body(D); }
