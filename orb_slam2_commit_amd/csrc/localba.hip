@@ -386,6 +386,10 @@ __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, 
   double chi = 0;
   if (k < D.na) {
     const int e = D.act[k];
+    // robust-kernel inputs loaded up front (not behind the eerr stores and the flag's branch)
+    const bool rob = D.erobust[e] != 0;
+    const double dl = D.edelta[e];
+    const float ds = D.edsqr[e];
     double c2;
     if (recompute) {
       double err[3];
@@ -399,9 +403,9 @@ __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, 
       for (int i = 0; i < (D.est[e] ? 3 : 2); i++) c2 += D.eerr[3 * e + i] * (info * D.eerr[3 * e + i]);
     }
     chi = c2;
-    if (D.erobust[e]) {
+    if (rob) {
       double rho[3];
-      huber(c2, D.edelta[e], D.edsqr[e], rho);
+      huber(c2, dl, ds, rho);
       chi = rho[0];
     }
   }
@@ -456,15 +460,18 @@ template <int DIM>
 __device__ __forceinline__ LinTerms lin_weights(const BaDev& D, int e) {
   LinTerms T;
   const double info = D.einfo[e];
+  const bool rob = D.erobust[e] != 0;
+  const double dl = D.edelta[e];
+  const float ds = D.edsqr[e];
   T.W = info;
 #pragma unroll
   for (int i = 0; i < DIM; i++) T.omr[i] = -info * D.eerr[3 * e + i];
-  if (D.erobust[e]) {
+  if (rob) {
     double c2 = 0;
 #pragma unroll
     for (int i = 0; i < DIM; i++) c2 += D.eerr[3 * e + i] * (info * D.eerr[3 * e + i]);
     double rho[3];
-    huber(c2, D.edelta[e], D.edsqr[e], rho);
+    huber(c2, dl, ds, rho);
     T.W = rho[1] * info;
 #pragma unroll
     for (int i = 0; i < DIM; i++) T.omr[i] *= rho[1];
