@@ -22,7 +22,10 @@ namespace orbx {
 __constant__ float c_pattern_f[1024] = {  // bit_pattern_31_ as floats (exact small integers)
 #include "brief_pattern_31.inc"
 };
-__constant__ int c_umax[16];
+// IC_Angle's circle (umax, src/ORBextractor.cc:77-105) as per-lane byte masks over the 31x31
+// box: lane = (row r = lane >> 1, half h = lane & 1) keeps byte b (column 16h + b) iff that
+// column is inside row r - 15's span; lanes 62, 63 keep nothing
+__constant__ uint4 c_icmask[64];
 
 constexpr int BS = 256;
 
@@ -1103,38 +1106,31 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
       pv[k] = q < kPatchRows * kPatchDw ? *reinterpret_cast<const uint32_t*>(pb + (uint32_t)(r * bs + 4 * j)) : 0u;
     }
   }
-  // IC_Angle: lanes 0..61 -> column u = lane%31-15, rows v in [-15,0] or [1,15]
+  // IC_Angle (src/ORBextractor.cc:77-105) on the raw level
   const uint8_t* raw = level_ptr(*G, B, img, l);
   int m01 = 0, m10 = 0;
   {
-    // circle table in scalar registers; every load below is unconditional (the
-    // 31x31 box around a keypoint is always inside its level) and masked by
-    // multiplication, so all 16 loads are in flight together.  Row i of the
-    // top half is (y-15+i), of the bottom half (y+1+i): a uniform row base plus
-    // the lane's column offset (bottom lanes +16 rows).
-    int um[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) um[i] = c_umax[i];
-    const bool lo = lane < 31;
-    const int u = lane < 62 ? (lane % 31) - 15 : 0;
-    const int au = u < 0 ? -u : u;
-    const int vb = lo ? -15 : 1;
-    const uint8_t* top = raw + (size_t)(y - 15) * w + x;  // uniform
-    const uint32_t o = (uint32_t)(u + 15) + (lo ? 0u : 16u * (uint32_t)w);
-    const uint32_t o15 = lo ? o : o - (uint32_t)w;  // the bottom half has 15 rows: row 15 re-reads row 14 (masked)
-    int I[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int lim = lo ? um[15 - i] : (i < 15 ? um[1 + i] : -1);
-      const int ok = (lane < 62 && au <= lim) ? 1 : 0;
-      const uint8_t* rowp = top - 15 + (size_t)i * w;
-      I[i] = (int)rowp[i < 15 ? o : o15] * ok;
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      m10 += u * I[i];
-      m01 += (vb + i) * I[i];
-    }
+    // lane (r, h) takes the 16 bytes at columns 16h .. 16h + 15 of box row r (x - 15 ..,
+    // y - 15 ..) with ONE unaligned 16-B buffer load (the box is always inside the level),
+    // masks them to the circle and sums by v_dot4_u32_u8: s0 = sum I, s1 = sum b * I.  Then
+    // m01 = v * s0 and m10 = sum (16h + b - 15) I = s1 + (16h - 15) s0 (integers: exact in any order)
+    const int r = lane >> 1, h = lane & 1;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(raw + (size_t)(y - 15) * w + (x - 15)), (short)0, 31 * w, 0x00020000);
+    const uint32_t off = lane < 62 ? (uint32_t)(r * w + 16 * h) : 0x80000000u;
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    const uint4 mk = c_icmask[lane];
+    const uint32_t I0 = q[0] & mk.x, I1 = q[1] & mk.y, I2 = q[2] & mk.z, I3 = q[3] & mk.w;
+    uint32_t s0 = __builtin_amdgcn_udot4(I0, 0x01010101u, 0u, false);
+    s0 = __builtin_amdgcn_udot4(I1, 0x01010101u, s0, false);
+    s0 = __builtin_amdgcn_udot4(I2, 0x01010101u, s0, false);
+    s0 = __builtin_amdgcn_udot4(I3, 0x01010101u, s0, false);
+    uint32_t s1 = __builtin_amdgcn_udot4(I0, 0x03020100u, 0u, false);
+    s1 = __builtin_amdgcn_udot4(I1, 0x07060504u, s1, false);
+    s1 = __builtin_amdgcn_udot4(I2, 0x0B0A0908u, s1, false);
+    s1 = __builtin_amdgcn_udot4(I3, 0x0F0E0D0Cu, s1, false);
+    m01 = (r - 15) * (int)s0;
+    m10 = (int)s1 + (16 * h - 15) * (int)s0;
   }
   m01 = wave_sum_dpp(m01);
   m10 = wave_sum_dpp(m10);
@@ -1200,7 +1196,15 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
 
 // ------------------------------------------------------------------ launch
 hipError_t upload_constants(const int* umax16, const int* gauss7) {
-  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax16, 16 * sizeof(int));
+  uint32_t mask[64][4] = {};
+  for (int lane = 0; lane < 62; lane++) {
+    const int r = lane >> 1, h = lane & 1, v = r - 15, um = umax16[v < 0 ? -v : v];
+    for (int b = 0; b < 16; b++) {
+      const int u = 16 * h + b - 15;
+      if (u <= 15 && u >= -um && u <= um) mask[lane][b >> 2] |= 0xFFu << (8 * (b & 3));
+    }
+  }
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), mask, sizeof(mask));
   if (e != hipSuccess) return e;
   return hipMemcpyToSymbol(HIP_SYMBOL(c_gauss), gauss7, 7 * sizeof(int));
 }
