@@ -1048,8 +1048,8 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 // radius 18.39, so |row|, |col| <= 18 after cvRound
 constexpr int kPatchR = 18;
 constexpr int kPatchRows = 2 * kPatchR + 1;            // 37
-constexpr int kPatchDw = (3 + 2 * kPatchR + 1 + 3) / 4;  // 11 dwords: up to 3 bytes of alignment slack
-constexpr int kPatchIt = (kPatchRows * kPatchDw + 63) / 64;
+constexpr int kPatchCh = 4;  // 16-B chunks per staged row: 16-aligned start, 37 bytes + up to 15 of slack
+constexpr int kPatchIt = (kPatchRows * kPatchCh + 63) / 64;
 
 // One wave per keypoint: IC_Angle on the raw level (src/ORBextractor.cc:77-105),
 // computeOrbDescriptor on the blurred level (:110-152), then the keypoint
@@ -1061,11 +1061,11 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                  int32_t* __restrict__ counts, int kp_cap) {
   // rBRIEF pattern as floats, once per block; each wave's 37 x 37 blurred patch
-  // (rows y-18..y+18, dword-aligned columns from (x-18) & ~3) staged with
-  // coalesced dword loads, so the 512 rotated samples are LDS gathers rather
+  // (rows y-18..y+18, 16-aligned columns from (x-18) & ~15) staged with
+  // 16-B buffer loads, so the 512 rotated samples are LDS gathers rather
   // than ~30 cache lines per global gather instruction
   __shared__ float4 s_pat[256];
-  __shared__ uint32_t s_patch[BS / 64][kPatchRows * kPatchDw];
+  __shared__ uint4 s_patch[BS / 64][kPatchRows * kPatchCh];
   const int2 bi = xcd_block2();
   const int img = bi.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1096,14 +1096,22 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   const int w = L.w;
   const uint8_t* blur = B.blur + (size_t)img * G->blur_bytes + L.boff;  // uniform
   const int bs = L.bstride;
-  const int x0 = (x - kPatchR) & ~3;  // x - 18 >= 1: keypoints sit >= 19 px inside the level
-  uint32_t pv[kPatchIt];
+  const int x0 = (x - kPatchR) & ~15;  // x - 18 >= 1: keypoints sit >= 19 px inside the level
+  // 16-B chunks from a 16-aligned column: with the 16-byte row stride a chunk is wholly inside
+  // its row or wholly past the row's end (and, in the last row, past num_records: zeros)
+  uint32_t pv[kPatchIt][4];
   {
-    const uint8_t* pb = blur + (size_t)(y - kPatchR) * bs + x0;  // 4-byte aligned (16-byte row stride)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(blur + (size_t)(y - kPatchR) * bs + x0), (short)0, kPatchRows * bs, 0x00020000);
 #pragma unroll
     for (int k = 0; k < kPatchIt; k++) {
-      const int q = lane + 64 * k, r = q / kPatchDw, j = q - r * kPatchDw;
-      pv[k] = q < kPatchRows * kPatchDw ? *reinterpret_cast<const uint32_t*>(pb + (uint32_t)(r * bs + 4 * j)) : 0u;
+      const int q = lane + 64 * k, r = q >> 2, j = q & 3;
+      const uint32_t off = q < kPatchRows * kPatchCh ? (uint32_t)(r * bs + 16 * j) : 0x80000000u;
+      const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      pv[k][0] = v4[0];
+      pv[k][1] = v4[1];
+      pv[k][2] = v4[2];
+      pv[k][3] = v4[3];
     }
   }
   // IC_Angle (src/ORBextractor.cc:77-105) on the raw level
@@ -1141,12 +1149,12 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   const float a = cs, b = sn;
 #pragma unroll
   for (int k = 0; k < kPatchIt; k++)
-    if (lane + 64 * k < kPatchRows * kPatchDw) s_patch[wv][lane + 64 * k] = pv[k];
+    if (lane + 64 * k < kPatchRows * kPatchCh) s_patch[wv][lane + 64 * k] = make_uint4(pv[k][0], pv[k][1], pv[k][2], pv[k][3]);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint8_t* patch = reinterpret_cast<const uint8_t*>(s_patch[wv]);
-  constexpr int PS = 4 * kPatchDw;  // patch row stride (bytes)
+  constexpr int PS = 16 * kPatchCh;  // patch row stride (bytes)
   // Rotated pattern point (px, py) -> pixel (y + r, x + c) with
   //   r = cvRound(px*b + py*a), c = cvRound(px*a - py*b)    (src/ORBextractor.cc:119-125)
   // Both coordinates ride in packed-f32 lanes.  Each sum is rounded exactly as
