@@ -26,6 +26,20 @@ __constant__ float c_pattern_f[1024] = {  // bit_pattern_31_ as floats (exact sm
 // box: lane = (row r = lane >> 1, half h = lane & 1) keeps byte b (column 16h + b) iff that
 // column is inside row r - 15's span; lanes 62, 63 keep nothing
 __constant__ uint4 c_icmask[64];
+// sincos_det constants (orbx_device.h); external linkage keeps them loads, not folded immediates
+__constant__ double c_sincos[23] = {
+    6.36619772367581382433e-01,  // 2/pi
+    1.57079632673412561417e+00,  // pi/2 hi
+    6.07710050650619224932e-11,  // pi/2 lo
+    1.0 / 51090942171709440000.0, -1.0 / 121645100408832000.0, 1.0 / 355687428096000.0,
+    -1.0 / 1307674368000.0,       1.0 / 6227020800.0,           -1.0 / 39916800.0,
+    1.0 / 362880.0,               -1.0 / 5040.0,                1.0 / 120.0,
+    -1.0 / 6.0,  // sin: x^19 .. x^3
+    1.0 / 2432902008176640000.0,  -1.0 / 6402373705728000.0,    1.0 / 20922789888000.0,
+    -1.0 / 87178291200.0,         1.0 / 479001600.0,            -1.0 / 3628800.0,
+    1.0 / 40320.0,                -1.0 / 720.0,                 1.0 / 24.0,
+    -0.5};  // cos: x^20 .. x^2
+
 
 constexpr int BS = 256;
 
@@ -1145,7 +1159,7 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   const float angle = fast_atan2((float)m01, (float)m10);
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float sn, cs;
-  sincos_det(angle * factorPI, &sn, &cs);
+  sincos_det(angle * factorPI, c_sincos, &sn, &cs);
   const float a = cs, b = sn;
 #pragma unroll
   for (int k = 0; k < kPatchIt; k++)

@@ -65,37 +65,24 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 
 // Deterministic float sin/cos: double-precision Cody-Waite reduction + Taylor
 // polynomials, rounded once to float (same operation sequence as the CPU
-// restatement).
-__device__ __forceinline__ void sincos_det(float xf, float* s_out, float* c_out) {
+// restatement).  The 23 constants sit in a constant-memory
+// table: a few wide scalar loads instead of two s_mov_b32 per double on the
+// (scalar-issue-bound) describe path.  x - c is x + (-c) exactly, so the table
+// holds the polynomial coefficients with their signs.
+// K: the 23 constants in this order (extract.hip's c_sincos).
+__device__ __forceinline__ void sincos_det(float xf, const double* __restrict__ K, float* s_out, float* c_out) {
   const double x = (double)xf;
-  const double kInvPio2 = 6.36619772367581382433e-01;
-  const double kPio2Hi = 1.57079632673412561417e+00;
-  const double kPio2Lo = 6.07710050650619224932e-11;
-  double kd = __builtin_rint(x * kInvPio2);
+  double kd = __builtin_rint(x * K[0]);
   int q = (int)kd;
-  double r = (x - kd * kPio2Hi) - kd * kPio2Lo;
+  double r = (x - kd * K[1]) - kd * K[2];
   double r2 = r * r;
-  double ps = 1.0 / 51090942171709440000.0;
-  ps = ps * r2 - 1.0 / 121645100408832000.0;
-  ps = ps * r2 + 1.0 / 355687428096000.0;
-  ps = ps * r2 - 1.0 / 1307674368000.0;
-  ps = ps * r2 + 1.0 / 6227020800.0;
-  ps = ps * r2 - 1.0 / 39916800.0;
-  ps = ps * r2 + 1.0 / 362880.0;
-  ps = ps * r2 - 1.0 / 5040.0;
-  ps = ps * r2 + 1.0 / 120.0;
-  ps = ps * r2 - 1.0 / 6.0;
+  double ps = K[3];
+#pragma unroll
+  for (int i = 4; i < 13; i++) ps = ps * r2 + K[i];
   double sr = r + r * (r2 * ps);
-  double pc = 1.0 / 2432902008176640000.0;
-  pc = pc * r2 - 1.0 / 6402373705728000.0;
-  pc = pc * r2 + 1.0 / 20922789888000.0;
-  pc = pc * r2 - 1.0 / 87178291200.0;
-  pc = pc * r2 + 1.0 / 479001600.0;
-  pc = pc * r2 - 1.0 / 3628800.0;
-  pc = pc * r2 + 1.0 / 40320.0;
-  pc = pc * r2 - 1.0 / 720.0;
-  pc = pc * r2 + 1.0 / 24.0;
-  pc = pc * r2 - 0.5;
+  double pc = K[13];
+#pragma unroll
+  for (int i = 14; i < 23; i++) pc = pc * r2 + K[i];
   double cr = 1.0 + r2 * pc;
   double s, c;
   switch (q & 3) {
