@@ -1063,6 +1063,8 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 constexpr int kPatchR = 18;
 constexpr int kPatchRows = 2 * kPatchR + 1;            // 37
 constexpr int kPatchCh = 4;  // 16-B chunks per staged row: 16-aligned start, 37 bytes + up to 15 of slack
+constexpr int kPatchRowCh = 5;  // LDS row stride in chunks: 80 B = 20 dwords, so the rotated samples'
+                                // rows spread over the banks (a 64-B stride folds every 4th row together)
 constexpr int kPatchIt = (kPatchRows * kPatchCh + 63) / 64;
 
 // One wave per keypoint: IC_Angle on the raw level (src/ORBextractor.cc:77-105),
@@ -1079,7 +1081,7 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   // 16-B buffer loads, so the 512 rotated samples are LDS gathers rather
   // than ~30 cache lines per global gather instruction
   __shared__ float4 s_pat[256];
-  __shared__ uint4 s_patch[BS / 64][kPatchRows * kPatchCh];
+  __shared__ uint4 s_patch[BS / 64][kPatchRows * kPatchRowCh];
   const int2 bi = xcd_block2();
   const int img = bi.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1163,12 +1165,13 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   const float a = cs, b = sn;
 #pragma unroll
   for (int k = 0; k < kPatchIt; k++)
-    if (lane + 64 * k < kPatchRows * kPatchCh) s_patch[wv][lane + 64 * k] = make_uint4(pv[k][0], pv[k][1], pv[k][2], pv[k][3]);
+    if (lane + 64 * k < kPatchRows * kPatchCh)
+      s_patch[wv][((lane + 64 * k) >> 2) * kPatchRowCh + ((lane + 64 * k) & 3)] = make_uint4(pv[k][0], pv[k][1], pv[k][2], pv[k][3]);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint8_t* patch = reinterpret_cast<const uint8_t*>(s_patch[wv]);
-  constexpr int PS = 16 * kPatchCh;  // patch row stride (bytes)
+  constexpr int PS = 16 * kPatchRowCh;  // patch row stride (bytes)
   // Rotated pattern point (px, py) -> pixel (y + r, x + c) with
   //   r = cvRound(px*b + py*a), c = cvRound(px*a - py*b)    (src/ORBextractor.cc:119-125)
   // Both coordinates ride in packed-f32 lanes.  Each sum is rounded exactly as
