@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--ba-concurrent", type=int, default=8, help="LocalBA problems in flight per GPU for the "
                                                                   "throughput form (<=1: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=3, help="config-5 batches per rank (0: skip)")
+    ap.add_argument("--single-frames", type=int, default=200, help="frames of the single-frame drop-in leg (0: skip)")
     ap.add_argument("--c3-steps", type=int, default=3, help="config-3 (EuRoC + PnP RANSAC) steps per rank (0: skip)")
     ap.add_argument("--c3-batch", type=int, default=128, help="config-3 frames (sequences) per step per GPU")
     ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r02_sq_counters.json"),
@@ -361,6 +362,42 @@ def localba_leg(args, rank, world, dev, odist, oracle_mod=None, flags=None, cpus
     return out
 
 
+# ------------------------------------------------------------------ single-frame (drop-in) leg
+def single_frame_leg(args, pairs, cpu):
+    """The drop-in path as ORB-SLAM2 drives it: one stereo Frame per TrackStereo call on the Tracking
+    thread (Examples/Stereo/stereo_kitti.cc:82-99 times that call), i.e. the C++ shim's Frame stereo
+    constructor -- two extraction threads on two ORBextractor handles (src/Frame.cc:80-84),
+    UndistortKeyPoints, ComputeStereoMatches -- from host images to host vectors
+    (shim/build/frame_bench, a separate process).  Reported beside the oracle's per-frame time."""
+    exe = os.path.join(ROOT, "shim", "build", "frame_bench")
+    if not os.path.exists(exe):
+        return dict(error="shim/build/frame_bench not built")
+    W, H = KITTI["width"], KITTI["height"]
+    fd, path = tempfile.mkstemp(prefix="orbx_frames_", suffix=".u8")
+    try:
+        with os.fdopen(fd, "wb") as f:
+            for L, R in pairs:
+                f.write(np.ascontiguousarray(L).tobytes())
+                f.write(np.ascontiguousarray(R).tobytes())
+        cmd = [exe, path, str(W), str(H), str(len(pairs)), str(args.single_frames), "20", str(KITTI["nfeatures"]),
+               repr(KITTI["bf"]), repr(KITTI["fx"])]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return dict(error="frame_bench rc %d: %s" % (r.returncode, (r.stderr or r.stdout)[-300:]))
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        os.unlink(path)
+    out.update(unit="ms per stereo frame (Frame constructor, host images in, host keypoints/descriptors/"
+                    "uRight/depth out)", warmup_frames=20,
+               path="shim Frame(imLeft, imRight, ...) -> 2 x ORBextractor::operator() on two threads + "
+                    "UndistortKeyPoints + ComputeStereoMatches")
+    if cpu:
+        out["cpu_baseline"] = dict(median_ms=cpu.get("median_ms"), p90_ms=cpu.get("p90_ms"),
+                                   two_thread_median_ms=(cpu.get("two_thread") or {}).get("median_ms"),
+                                   kind=cpu.get("kind"), note="the oracle's per-frame time from cpu_baseline")
+    return out
+
+
 # ------------------------------------------------------------------ config-3 leg
 def config3_leg(args, rank, world, dev, odist, stream, oracle_mod=None, flags=None, cpus=None):
     """EuRoC MH_01-shaped stereo (752x480, 1200 features) + PnP RANSAC per frame (BASELINE configs[2]):
@@ -538,14 +575,15 @@ def main():
     from orb_slam2_commit_amd import _lib
 
     W, H, B = KITTI["width"], KITTI["height"], args.batch
-    # synthetic frames: sequence = rank (distinct seeds per rank: frame shards); every slot distinct
+    # synthetic frames: sequence = rank (distinct seeds per rank: frame shards); every frame of every
+    # in-flight batch distinct (batch k holds frames k*B .. k*B+B-1 of the rank's sequence)
     pairs = [synth.stereo_pair(s, W, H) for s in synth.sequence_seeds(rank, args.unique)]
-    host = synth.stereo_batch(rank, B, pairs=pairs)
-    images = torch.from_numpy(host).to(dev)
-    # S = --inflight extractor handles, each with its own HIP stream and output buffers: step i runs on
-    # slot i % S, so consecutive batches overlap (one batch's latency-bound stages -- octree, small
-    # pyramid levels, stereo finalize -- fill in beside the next batch's bandwidth-bound ones)
+    # S = --inflight extractor handles, each with its own HIP stream, input batch and output buffers:
+    # step i runs on slot i % S, so consecutive batches overlap (one batch's latency-bound stages --
+    # octree, small pyramid levels, stereo finalize -- fill in beside the next batch's bandwidth-bound ones)
     S = max(1, args.inflight)
+    batch_images = [torch.from_numpy(synth.stereo_batch(rank, B, pairs=pairs, first=k * B)).to(dev) for k in range(S)]
+    images = batch_images[0]
     exs = [ORBextractor(KITTI["nfeatures"], 1.2, 8, 20, 7, device=local) for _ in range(S)]
     ex = exs[0]
     cap = ex.max_keypoints(W, H)
@@ -570,8 +608,8 @@ def main():
     def step(i=0):
         k = i % S
         sl = slots[k]
-        exs[k].stereo_frames_device(images, sl["kps"], sl["desc"], sl["counts"], bf, baseline, sl["uR"], sl["depth"],
-                                    sl["nmatch"], sl["stream"])
+        exs[k].stereo_frames_device(batch_images[k], sl["kps"], sl["desc"], sl["counts"], bf, baseline, sl["uR"],
+                                    sl["depth"], sl["nmatch"], sl["stream"])
 
     for i in range(max(args.warmup, S)):
         step(i)
@@ -681,7 +719,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (%d seeded stereo scenes per rank, each batch slot a distinct horizontal roll of one)" % args.unique,
+        "data": "synthetic (%d seeded stereo scenes per rank; every frame of the %d in-flight batches a distinct "
+                "horizontal roll of one)" % (args.unique, S),
         "config": {"workload": "KITTI-00 stereo 1241x376, 2000 features, extract L+R + ComputeStereoMatches",
                    "batch_frames_per_gpu": B, "global_batch_frames": B * world, "nlevels": 8,
                    "scale_factor": 1.2, "fast_th": [20, 7], "parallelism": "frame-sharded x%d" % world,
@@ -700,6 +739,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         oracle_mod, flags = load_oracle()
         out["cpu_baseline"] = cpu_baseline(oracle_mod, flags, pairs, args.cpu_baseline_seconds, cpus)
+    if args.single_frames > 0 and rank == 0 and world == 1:
+        out["single_frame"] = single_frame_leg(args, pairs, out["cpu_baseline"])
     if args.ba_calls > 0:
         out["localba"] = localba_leg(args, rank, world, dev, odist, oracle_mod, flags, cpus)
         out["localba_iters_per_s"] = out["localba"]["iters_per_s"]

@@ -198,6 +198,17 @@ orbx_status orbx_voc_info(const orbx_voc* v, int32_t info[6]);
 orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* set_off, int n_sets, int levelsup,
                                uint32_t* bow_words, double* bow_values, int32_t* n_bow, uint32_t* fv_nodes,
                                int32_t* fv_off, int32_t* fv_feat, int32_t* n_fv);
+/* The same on a device batch, e.g. the left images of orbx_stereo_frames_device (Frame::ComputeBoW
+ * for every frame of the batch at once): set s is rows s*stride .. s*stride + count[s*count_step]-1
+ * of d_desc (at most cap <= 8192 rows; the stereo batch's left images: stride = 2*cap,
+ * count_step = 2).  Outputs as above with set_off[s] = s*cap (fv_off of set s starts at
+ * s*(cap+1)).  All pointers device pointers, queued on `stream` (NULL: the vocabulary's own),
+ * no host synchronisation. */
+orbx_status orbx_voc_transform_device(orbx_voc* v, const uint8_t* d_desc, int cap, long long stride,
+                                      const int32_t* d_count, int count_step, int n_sets, int levelsup,
+                                      uint32_t* d_bow_words, double* d_bow_values, int32_t* d_n_bow,
+                                      uint32_t* d_fv_nodes, int32_t* d_fv_off, int32_t* d_fv_feat, int32_t* d_n_fv,
+                                      void* stream);
 
 /* Optimizer::LocalBundleAdjustment on g2o semantics (BlockSolver_6_3 +
  * LinearSolverEigen + Levenberg, Huber kernels, two phases), FP64 on the GPU.

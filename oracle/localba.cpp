@@ -17,6 +17,7 @@
 // The reduced camera system is solved with a dense LDLT (no pivoting); the
 // reference uses a sparse LDLT with AMD ordering -- same solution to rounding.
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <limits>
@@ -525,6 +526,8 @@ struct Optimizer {
       if (ok2) update();
       compute_active_errors();
       double tempChi = active_robust_chi2();
+      if (nan_trial >= 0 && phase_trial == nan_trial) tempChi = std::nan("");  // test hook (ORBX_BA_NAN_TRIAL)
+      phase_trial++;
       if (!ok2) tempChi = std::numeric_limits<double>::max();
       rho = currentChi - tempChi;
       double scale = ok2 ? compute_scale(lambda) : 0.0;
@@ -554,8 +557,14 @@ struct Optimizer {
     return OK;
   }
 
+  // test hook: the given trial of each optimize() call computes a NaN chi (rho NaN), as the GPU
+  // library's ORBX_BA_NAN_TRIAL does
+  int nan_trial = std::getenv("ORBX_BA_NAN_TRIAL") ? std::atoi(std::getenv("ORBX_BA_NAN_TRIAL")) : -1;
+  int phase_trial = 0;
+
   int optimize(int iterations, double* final_chi) {
     int it = 0;
+    phase_trial = 0;
     for (int i = 0; i < iterations && !terminate(); i++) {
       Result r = lm_iteration(i);
       ++it;

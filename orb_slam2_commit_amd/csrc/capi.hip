@@ -19,6 +19,7 @@
 
 #include "../../include/orbx.h"
 #include "orbx_internal.h"
+#include "orbx_scratch.h"
 #include "orbx_stereo.h"
 #include "orbx_prof.h"
 #include "orbx_bow.h"
@@ -328,20 +329,20 @@ struct orbx_extractor {
   DevBuf<uint8_t> pyr, blur;
   DevBuf<uint32_t> cand, kpos, oct;
   DevBuf<int> cell_count, knode, oct_count;
-  // host-API staging
-  DevBuf<uint8_t> in, desc;
-  DevBuf<orbx_keypoint> kps;
-  DevBuf<int32_t> counts;
+  // host-API staging: the input image, and ONE output block [count | keypoints | descriptors]
+  // (orbx_extract reads it back with one copy; orbx_stereo_match reads it in place)
+  DevBuf<uint8_t> in, out;
+  size_t out_kps = 0, out_desc = 0, out_bytes = 0;
+  uint8_t* hstage = nullptr;  // pinned: the input image on the way in, the output block on the way out
+  size_t hstage_cap = 0;
   // stereo scratch
   DevBuf<uint64_t> rkeys;
   DevBuf<int2> rxi;
   DevBuf<uint4> rdesc;
   DevBuf<uint32_t> rtab;
   DevBuf<int> oct_start, sad;
-  DevBuf<float> uR, depth;
-  DevBuf<int32_t> nmatch, nbuf;
-  DevBuf<orbx_keypoint> skL, skR;
-  DevBuf<uint8_t> sdL, sdR;
+  DevBuf<float> sres;  // orbx_stereo_match: uRight | depth, adjacent (one copy back)
+  DevBuf<int32_t> nmatch;
   StageTimer timer;
   // last batch (mvImagePyramid)
   Plan* last_plan = nullptr;
@@ -353,6 +354,19 @@ struct orbx_extractor {
   bool last_host = false;
   int last_fp_n = 0;
   uint64_t last_fp = 0;
+  ~orbx_extractor() {
+    if (hstage) (void)hipHostFree(hstage);
+  }
+  hipError_t ensure_stage(size_t bytes) {
+    if (bytes <= hstage_cap && hstage) return hipSuccess;
+    if (hstage) (void)hipHostFree(hstage);
+    hstage = nullptr;
+    hstage_cap = 0;
+    const size_t cap = (bytes + 4095) & ~(size_t)4095;
+    hipError_t e = hipHostMalloc((void**)&hstage, cap, hipHostMallocDefault);
+    if (e == hipSuccess) hstage_cap = cap;
+    return e;
+  }
 };
 
 namespace {
@@ -442,12 +456,21 @@ orbx_status run_extract(orbx_extractor* h, Plan* P, int n, const uint8_t* d_in, 
 
 hipStream_t pick_stream(orbx_extractor* h, void* s) { return s ? (hipStream_t)s : h->stream; }
 
-// 64-bit FNV-1a over the keypoint records, one 32-bit word per step (28-B records are word multiples)
-uint64_t keypoint_fingerprint(const orbx_keypoint* k, int n) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(k);
+// 64-bit fingerprint of n keypoint records and their descriptors (multiply-xorshift over 32-bit
+// words, a few microseconds for 2,000 keypoints): orbx_stereo_match uses the device copies of the
+// extraction only when the caller hands back exactly what that extraction returned
+uint64_t fingerprint_words(const void* p, size_t nw, uint64_t h) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  for (size_t i = 0; i < nw; i++) {
+    h = (h ^ w[i]) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+  }
+  return h;
+}
+uint64_t keypoint_fingerprint(const orbx_keypoint* k, const uint8_t* desc, int n) {
   uint64_t h = 1469598103934665603ull ^ (uint64_t)n;
-  const size_t nw = (size_t)n * (sizeof(orbx_keypoint) / 4);
-  for (size_t i = 0; i < nw; i++) h = (h ^ w[i]) * 1099511628211ull;
+  h = fingerprint_words(k, (size_t)n * (sizeof(orbx_keypoint) / 4), h);
+  if (desc) h = fingerprint_words(desc, (size_t)n * 8, h ^ 0xD6E8FEB86659FD93ull);
   return h;
 }
 
@@ -535,37 +558,38 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
   const int kcap = P->G.max_kps;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
-  chk(h->in.ensure((size_t)width * height));
-  chk(h->kps.ensure(kcap));
-  chk(h->desc.ensure((size_t)kcap * 32));
-  chk(h->counts.ensure(1));
+  const size_t npx = (size_t)width * height;
+  h->out_kps = 256;
+  h->out_desc = h->out_kps + (((size_t)kcap * sizeof(orbx_keypoint) + 255) & ~(size_t)255);
+  h->out_bytes = h->out_desc + (size_t)kcap * 32;
+  chk(h->in.ensure(npx));
+  chk(h->out.ensure(h->out_bytes));
+  chk(h->ensure_stage(std::max(npx, h->out_bytes)));
   if (e != hipSuccess) return ORBX_ERR_HIP;
   hipStream_t st = h->stream;
-  if (hipMemcpy2DAsync(h->in.p, width, img, stride, width, height, hipMemcpyHostToDevice, st) != hipSuccess)
-    return ORBX_ERR_HIP;
-  s = run_extract(h, P, 1, h->in.p, (size_t)width * height, h->kps.p, h->desc.p, h->counts.p, kcap, st);
+  // the image through pinned staging (a pageable copy is staged by the runtime, synchronously)
+  for (int y = 0; y < height; y++) std::memcpy(h->hstage + (size_t)y * width, img + (size_t)y * stride, width);
+  if (hipMemcpyAsync(h->in.p, h->hstage, npx, hipMemcpyHostToDevice, st) != hipSuccess) return ORBX_ERR_HIP;
+  int32_t* d_count = (int32_t*)h->out.p;
+  orbx_keypoint* d_kps = (orbx_keypoint*)(h->out.p + h->out_kps);
+  uint8_t* d_desc = h->out.p + h->out_desc;
+  s = run_extract(h, P, 1, h->in.p, npx, d_kps, d_desc, d_count, kcap, st);
   if (s != ORBX_OK) return s;
-  int32_t cnt = 0;
-  chk(hipMemcpyAsync(&cnt, h->counts.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  // count, keypoints and descriptors in ONE copy, then the stream's only synchronisation
+  chk(hipMemcpyAsync(h->hstage, h->out.p, h->out_bytes, hipMemcpyDeviceToHost, st));
   chk(hipStreamSynchronize(st));
   if (e != hipSuccess) return ORBX_ERR_HIP;
+  const int32_t cnt = *(const int32_t*)h->hstage;
   *n = cnt;
   if (cnt > cap) return ORBX_ERR_CAPACITY;
-  std::vector<orbx_keypoint> own;
-  orbx_keypoint* kdst = kps;
-  if (!kdst && cnt > 0) {
-    own.resize(cnt);
-    kdst = own.data();
-  }
+  const orbx_keypoint* hk = (const orbx_keypoint*)(h->hstage + h->out_kps);
   if (cnt > 0) {
-    chk(hipMemcpyAsync(kdst, h->kps.p, sizeof(orbx_keypoint) * cnt, hipMemcpyDeviceToHost, st));
-    if (desc) chk(hipMemcpyAsync(desc, h->desc.p, (size_t)32 * cnt, hipMemcpyDeviceToHost, st));
-    chk(hipStreamSynchronize(st));
+    if (kps) std::memcpy(kps, hk, sizeof(orbx_keypoint) * cnt);
+    if (desc) std::memcpy(desc, h->hstage + h->out_desc, (size_t)32 * cnt);
   }
-  if (e != hipSuccess) return ORBX_ERR_HIP;
   h->last_host = true;
   h->last_fp_n = cnt;
-  h->last_fp = keypoint_fingerprint(kdst, cnt);
+  h->last_fp = keypoint_fingerprint(hk, h->hstage + h->out_desc, cnt);
   return ORBX_OK;
 }
 
@@ -668,8 +692,8 @@ orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const
   // returned exactly these keypoints (src/Frame.cc:556,681 read mpORBextractorLeft/Right->mvImagePyramid
   // of the extraction that produced mvKeys/mvKeysRight)
   if (!left->last_host || !right->last_host || nL != left->last_fp_n || nR != right->last_fp_n ||
-      (nL > 0 && keypoint_fingerprint(kpsL, nL) != left->last_fp) ||
-      (nR > 0 && keypoint_fingerprint(kpsR, nR) != right->last_fp))
+      (nL > 0 && keypoint_fingerprint(kpsL, descL, nL) != left->last_fp) ||
+      (nR > 0 && keypoint_fingerprint(kpsR, descR, nR) != right->last_fp))
     return ORBX_ERR_STATE;
   if (left->last_plan->G.width != right->last_plan->G.width ||
       left->last_plan->G.height != right->last_plan->G.height || left->device != right->device)
@@ -680,34 +704,27 @@ orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const
   if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
-  chk(h->skL.ensure(nL));
-  chk(h->sdL.ensure((size_t)nL * 32));
-  chk(h->skR.ensure(std::max(nR, 1)));
-  chk(h->sdR.ensure((size_t)std::max(nR, 1) * 32));
-  chk(h->uR.ensure(nL));
-  chk(h->depth.ensure(nL));
+  chk(h->sres.ensure(2 * (size_t)nL));
   chk(h->nmatch.ensure(1));
-  chk(h->nbuf.ensure(2));
+  chk(h->ensure_stage(std::max(h->hstage_cap, (size_t)8 * nL)));
   if (e != hipSuccess) return ORBX_ERR_HIP;
   hipStream_t st = h->stream;
-  // the right handle's last extraction must be complete before we read its pyramid
-  chk(hipStreamSynchronize(right->stream));
-  int32_t ns[2] = {nL, nR};
-  chk(hipMemcpyAsync(h->nbuf.p, ns, sizeof(ns), hipMemcpyHostToDevice, st));
-  chk(hipMemcpyAsync(h->skL.p, kpsL, sizeof(orbx_keypoint) * nL, hipMemcpyHostToDevice, st));
-  chk(hipMemcpyAsync(h->sdL.p, descL, (size_t)32 * nL, hipMemcpyHostToDevice, st));
-  if (nR > 0) {
-    chk(hipMemcpyAsync(h->skR.p, kpsR, sizeof(orbx_keypoint) * nR, hipMemcpyHostToDevice, st));
-    chk(hipMemcpyAsync(h->sdR.p, descR, (size_t)32 * nR, hipMemcpyHostToDevice, st));
-  }
-  if (e != hipSuccess) return ORBX_ERR_HIP;
-  orbx_status s = run_stereo(left, right, 1, h->skL.p, h->sdL.p, h->nbuf.p, 0, 0, h->skR.p, h->sdR.p, h->nbuf.p + 1,
-                             0, 0, 0, 0, 0, 0, nL, bf, baseline, h->uR.p, h->depth.p, nL, h->nmatch.p, st);
+  // The keypoints and descriptors are the ones each handle's last orbx_extract left on the device
+  // (the fingerprints above prove it): no upload.  orbx_extract synchronised both streams before
+  // returning them, so the right handle's block and pyramid are complete.
+  const int32_t* cL = (const int32_t*)left->out.p;
+  const int32_t* cR = (const int32_t*)right->out.p;
+  orbx_status s = run_stereo(left, right, 1, (const orbx_keypoint*)(left->out.p + left->out_kps),
+                             left->out.p + left->out_desc, cL, 0, 0,
+                             (const orbx_keypoint*)(right->out.p + right->out_kps), right->out.p + right->out_desc,
+                             cR, 0, 0, 0, 0, 0, 0, nL, bf, baseline, h->sres.p, h->sres.p + nL, nL, h->nmatch.p, st);
   if (s != ORBX_OK) return s;
-  chk(hipMemcpyAsync(uRight, h->uR.p, sizeof(float) * nL, hipMemcpyDeviceToHost, st));
-  chk(hipMemcpyAsync(depth, h->depth.p, sizeof(float) * nL, hipMemcpyDeviceToHost, st));
+  chk(hipMemcpyAsync(h->hstage, h->sres.p, sizeof(float) * 2 * nL, hipMemcpyDeviceToHost, st));
   chk(hipStreamSynchronize(st));
-  return hip_status(e);
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  std::memcpy(uRight, h->hstage, sizeof(float) * nL);
+  std::memcpy(depth, h->hstage + sizeof(float) * nL, sizeof(float) * nL);
+  return ORBX_OK;
 }
 
 orbx_status orbx_stereo_frames_device(orbx_extractor* h, int n_frames, const uint8_t* d_images, int width,
@@ -741,13 +758,15 @@ static orbx_status bow_host(const orbx_bow_side* A, const orbx_bow_side* B, floa
            (size_t)(s->n_nodes + 1) * 4 + (size_t)(s->n_nodes ? s->node_off[s->n_nodes] : 0) * 4 + 64;
   };
   const size_t bytes = side_bytes(A) + side_bytes(B) + (size_t)nout * 4 + 64 + sizeof(BowProblem) + 64;
-  std::vector<uint8_t> host(bytes, 0);
-  uint8_t* dbase = nullptr;
-  if (hipMalloc((void**)&dbase, bytes) != hipSuccess) return ORBX_ERR_HIP;
+  // a pooled lease (orbx_scratch.h): no allocation, no device-wide synchronisation per call
+  ScratchGuard g(device);
+  if (!g.l || g.l->reserve(bytes, bytes) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* host = g.l->h;
+  uint8_t* dbase = g.l->d;
   size_t off = 0;
   auto put = [&](const void* src, size_t nbytes) -> void* {
     off = (off + 15) & ~(size_t)15;
-    if (src && nbytes) std::memcpy(host.data() + off, src, nbytes);
+    if (src && nbytes) std::memcpy(host + off, src, nbytes);
     void* d = dbase + off;
     off += nbytes;
     return d;
@@ -769,15 +788,21 @@ static orbx_status bow_host(const orbx_bow_side* A, const orbx_bow_side* B, floa
   P.nnratio = nnratio;
   P.check_ori = check_ori;
   P.mode = mode;
+  const size_t o_out = (off + 15) & ~(size_t)15;
   P.match = (int32_t*)put(nullptr, (size_t)nout * 4);
   P.nmatches = (int32_t*)put(nullptr, 4);
+  const size_t o_end = off;
   BowProblem* dP = (BowProblem*)put(&P, sizeof(P));
-  hipError_t e = hipMemcpy(dbase, host.data(), off, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = launch_search_by_bow(dP, 1, nullptr);
-  if (e == hipSuccess && nout) e = hipMemcpy(match, P.match, (size_t)nout * 4, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipMemcpy(nmatches, P.nmatches, 4, hipMemcpyDeviceToHost);
-  (void)hipFree(dbase);
-  return hip_status(e);
+  hipStream_t st = g.l->st;
+  // outputs [o_out, o_end) come back in one copy: matches then the count
+  hipError_t e = hipMemcpyAsync(dbase, host, off, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = launch_search_by_bow(dP, 1, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(host + o_out, dbase + o_out, o_end - o_out, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = g.l->sync();
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  if (nout) std::memcpy(match, host + o_out, (size_t)nout * 4);
+  std::memcpy(nmatches, host + ((uint8_t*)P.nmatches - dbase), 4);
+  return ORBX_OK;
 }
 
 orbx_status orbx_search_by_bow_kf_f(const orbx_bow_side* kf, const orbx_bow_side* f, float nnratio, int check_ori,

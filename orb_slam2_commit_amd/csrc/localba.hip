@@ -36,6 +36,7 @@
 #include <cstring>
 #include <limits>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "../../include/orbx.h"
@@ -186,7 +187,9 @@ struct LmState {
   int rejected;    // the last trial was rejected after a successful solve: restore
   int iterations;  // the phase's iteration budget
   int stopped;     // the stop flag was seen
-  int pad;
+  int refresh;     // an iteration ended on a rejected trial (rho NaN) and the phase goes on: the
+                   // phase pauses (done) until the host pops the trial, recomputes the errors at
+                   // the restored state and resumes (k_ba_lm_resume), as g2o's next iteration does
   double final_chi;  // batched driver: activeRobustChi2 of the stored errors at the phase end
 };
 
@@ -260,6 +263,9 @@ struct BaDev {
   int nbu;         // k_ba_update blocks (its LM-scale partials)
   double* scal;    // scalars: [0] chi at iteration start, [1] chi after the trial, [2] solve ok, [3] max diag, [4] LM scale
   const LmState* lm;  // device LM state: gates the trial's kernels and carries lambda (null: host control)
+  int nan_trial;      // debug (ORBX_BA_NAN_TRIAL): this trial's chi is NaN; -1 off
+  int host_trial;     // host-controlled loop: the trial being queued (the device loop counts its own)
+  int raise_after;    // debug (ORBX_BA_RAISE_STOP_AFTER): the device raises the stop mirror after this many trials; -1 off
 };
 
 // gates of the device LM loop (uniform per launch, checked before any barrier)
@@ -381,7 +387,9 @@ __device__ inline void huber(double chi, double delta, float dsqr, double rho[3]
 }
 
 __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, int dst) {
-  if (lm_skip(D) || (int)blockIdx.x >= D.nbe) return;  // (a batched grid spans the largest problem)
+  // recompute == 2: the refresh launch (only while the device LM state asks for it)
+  if (recompute == 2 ? !(D.lm && D.lm->refresh) : lm_skip(D)) return;
+  if ((int)blockIdx.x >= D.nbe) return;  // (a batched grid spans the largest problem)
   const int k = blockIdx.x * LBS + threadIdx.x;
   double chi = 0;
   if (k < D.na) {
@@ -408,6 +416,9 @@ __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, 
       huber(c2, dl, ds, rho);
       chi = rho[0];
     }
+    // debug hook (ORBX_BA_NAN_TRIAL): the given trial's chi is NaN, i.e. rho is NaN
+    if (dst == 1 && k == 0 && D.nan_trial >= 0 && (D.lm ? D.lm->trials : D.host_trial) == D.nan_trial)
+      chi = __builtin_nan("");
   }
   block_partial(chi, D.scal + 8 + dst * D.nbe);
 }
@@ -1448,7 +1459,7 @@ __global__ __launch_bounds__(LBS) void k_ba_update_many(const BaDev* __restrict_
 }
 
 __device__ __forceinline__ void k_ba_restore_body(const BaDev& D) {
-  if (D.lm && !D.lm->rejected) return;
+  if (D.lm && !D.lm->rejected) return;  // (a refresh always follows a rejected trial)
   const int i = blockIdx.x * LBS + threadIdx.x;
   if (i < D.npa) {
     const int p = D.pt_id[i];
@@ -1509,6 +1520,7 @@ __device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations
   L->rejected = 0;
   L->iterations = iterations;
   L->stopped = 0;  // the host polled the flag just before this phase
+  L->refresh = 0;
   L->done = iterations <= 0 ? 1 : 0;
 }
 __global__ __launch_bounds__(64) void k_ba_lm_init(BaDev D, int iterations) { k_ba_lm_init_body(D, iterations); }
@@ -1528,7 +1540,7 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
   if (L->done) return;  // uniform; a finished phase keeps `rejected` for the final restore
   // the flag's host-memory read is issued first, so its latency hides behind the sums (one read
   // serves both of the loop's polls below; a flag raised after it is seen at the next trial)
-  const bool st = stop();
+  const bool st = stop() || (D.raise_after >= 0 && L->trials >= D.raise_after);  // (+ test hook)
   const double* p = D.scal + 8;
   const double b = seq_sum_wave(p + D.nbe, D.nbe);
   const double u = seq_sum_wave(p + 2 * D.nbe, nbu);
@@ -1573,6 +1585,31 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
   L->stopped = st || st2;
   L->done = (brk || L->it >= L->iterations || st2) ? 1 : 0;
   L->relin = L->done ? 0 : 1;
+  if (!L->done && L->rejected) {
+    // rho was NaN: the iteration ended on a rejection and the phase goes on.  g2o pops the
+    // trial and its next iteration recomputes the errors at the restored state; pause the
+    // phase until the host has queued exactly that (restore, errors, k_ba_lm_resume).
+    L->refresh = 1;
+    L->done = 1;
+  }
+}
+
+// Resume a phase paused for a refresh: chi of the recomputed errors (slot 0, block order, as
+// the host loop's computeActiveErrors + activeRobustChi2) becomes the iteration's starting chi.
+__device__ __forceinline__ void k_ba_lm_resume_body(const BaDev& D) {
+  LmState* L = const_cast<LmState*>(D.lm);
+  if (!L->refresh) return;
+  const double a = seq_sum_wave(D.scal + 8, D.nbe);
+  if (threadIdx.x != 0) return;
+  L->currentChi = a;
+  L->rejected = 0;
+  L->refresh = 0;
+  L->done = 0;
+  L->relin = 1;
+}
+__global__ __launch_bounds__(64) void k_ba_lm_resume(BaDev D) { k_ba_lm_resume_body(D); }
+__global__ __launch_bounds__(64) void k_ba_lm_resume_many(const BaDev* __restrict__ Ds) {
+  k_ba_lm_resume_body(Ds[blockIdx.z]);
 }
 __global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, DevStop stop) { k_ba_lm_control_body(D, stop); }
 __global__ __launch_bounds__(64) void k_ba_lm_control_many(const BaDev* __restrict__ Ds, DevStop stop) {
@@ -2059,9 +2096,10 @@ struct LocalBA {
     if (sint_host) (void)hipHostFree(sint_host);
     if (lm_host) (void)hipHostFree(lm_host);
     if (own_stop) (void)hipHostFree(own_stop);
-    unmap_stop();
+    if (mirror) (void)hipHostFree(mirror);
   }
   int* own_stop = nullptr;  // orbx_ba_stop_flag: pinned, device-readable
+  bool hook_stopped = false;  // ORBX_BA_RAISE_STOP_AFTER fired (the host then stops as for a raised flag)
   static void use_lin(BaDev& D, const LinSet& L) {
     D.Hpl = L.Hpl;
     D.Hll = L.Hll;
@@ -2341,7 +2379,7 @@ struct LocalBA {
     return e;
   }
   hipError_t finish_read(double out[5]) {
-    hipError_t e = hipEventSynchronize(rb_ev);
+    hipError_t e = wait_event(rb_ev);
     if (e != hipSuccess) return e;
     out[2] = rb_host[2];
     out[3] = rb_host[3];
@@ -2374,6 +2412,7 @@ struct LocalBA {
     const int gp = std::max((D.npa + D.nposes + LBS - 1) / LBS, 1);
     const int ga = std::max((D.na + LBS - 1) / LBS, 1);
     double sc[5];
+    int ptrial = 0;  // trials of this phase (the ORBX_BA_NAN_TRIAL hook counts per phase, as the device loop)
     const bool spec_on = std::getenv("ORBX_BA_NO_SPEC") == nullptr;  // A/B switch
     bool spec_ready = false;  // the other LinSet holds the linearisation at the current state
     double spec_chi = 0;      // its chi (the accepted trial's)
@@ -2406,6 +2445,7 @@ struct LocalBA {
           ldlt.launch(D, st);
         }
         hipLaunchKernelGGL(k_ba_update, dim3(gp), dim3(LBS), 0, st, D, lambda);
+        D.host_trial = ptrial++;
         BA_CHECK(errors(st, 1, 1));
         BA_CHECK(start_read(st));
         bool launched = false;
@@ -2517,11 +2557,19 @@ struct LocalBA {
         BA_CHECK(hipMemcpyAsync(lm_host, c.lm.p, sizeof(LmState), hipMemcpyDeviceToHost, st));
         BA_CHECK(start_read(st));
         BA_CHECK(finish_read(sc));
-        if (lm_host->done) break;
+        if (lm_host->refresh) {  // paused on a NaN-rho rejection: pop, errors at the restored state, resume
+          hipLaunchKernelGGL(k_ba_restore, dim3(gp), dim3(LBS), 0, st, Dg);
+          hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, Dg, 2, 0);
+          hipLaunchKernelGGL(k_ba_lm_resume, dim3(1), dim3(64), 0, st, Dg);
+          BA_CHECK(hipGetLastError());
+        } else if (lm_host->done) {
+          break;
+        }
         budget = std::max(1, iterations - lm_host->it);
       }
       it = lm_host->it;
       trials += lm_host->trials;
+      hook_stopped |= lm_host->stopped && D.raise_after >= 0;
       if (lm_host->rejected) {  // ended on a rejected trial: its pop (chi above reads errors only)
         hipLaunchKernelGGL(k_ba_restore, dim3(gp), dim3(LBS), 0, st, Dg);
         BA_CHECK(hipGetLastError());
@@ -2536,42 +2584,55 @@ struct LocalBA {
     return ORBX_OK;
   }
 
-  // Host-mapped view of the caller's stop flag for k_ba_lm_control: pinned
-  // memory (e.g. orbx_ba_stop_flag's) maps as is; any other page is
-  // registered once and stays registered while the handle lives (the
-  // reference passes the same &mbAbortBA every call), so registration --
-  // which synchronises the device -- is not paid per call.
-  void* stop_reg = nullptr;
+  // The stop flag as k_ba_lm_control sees it.  The handle's own flag (orbx_ba_stop_flag:
+  // pinned, mapped) is read by the device directly.  Any other caller flag is never mapped or
+  // registered: the device polls a pinned per-handle MIRROR, and the calling thread -- blocked
+  // in the call anyway -- copies the caller's flag into it while it waits for the device
+  // (wait_event).  So the device never holds an address whose page the caller may free or
+  // remap, and no registration outlives the call (or is shared between handles).
+  int* mirror = nullptr;  // pinned, mapped
+  StopFlag mirror_src;    // the caller flag the mirror follows during a call (empty: none)
   bool map_stop(const StopFlag& s, DevStop* ds) {
     ds->i = nullptr;
     ds->b = nullptr;
-    const void* hp = s.i ? (const void*)s.i : (const void*)s.b;
-    if (!hp) return true;
+    mirror_src = StopFlag{};
+    if (!s.i && !s.b) return true;
     void* dp = nullptr;
-    void* base = (void*)((uintptr_t)hp & ~(uintptr_t)4095);
-    if (base != stop_reg && hipHostGetDevicePointer(&dp, const_cast<void*>(hp), 0) != hipSuccess) {
-      (void)hipGetLastError();
-      unmap_stop();
-      if (hipHostRegister(base, 4096, hipHostRegisterMapped) != hipSuccess) {
+    if (s.i && own_stop && (const void*)s.i == (const void*)own_stop) {
+      if (hipHostGetDevicePointer(&dp, own_stop, 0) != hipSuccess) {
         (void)hipGetLastError();
         return false;
       }
-      stop_reg = base;
+      ds->i = (const int*)dp;
+      return true;
     }
-    if (!dp && hipHostGetDevicePointer(&dp, const_cast<void*>(hp), 0) != hipSuccess) {
+    if (!mirror) {
+      if (hipHostMalloc((void**)&mirror, sizeof(int), hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        mirror = nullptr;
+        return false;
+      }
+    }
+    if (hipHostGetDevicePointer(&dp, mirror, 0) != hipSuccess) {
       (void)hipGetLastError();
-      unmap_stop();
       return false;
     }
-    if (s.i)
-      ds->i = (const int*)dp;
-    else
-      ds->b = (const bool*)dp;
+    mirror_src = s;
+    *(volatile int*)mirror = s() ? 1 : 0;
+    ds->i = (const int*)dp;
     return true;
   }
-  void unmap_stop() {
-    if (stop_reg) (void)hipHostUnregister(stop_reg);
-    stop_reg = nullptr;
+  void unmap_stop() { mirror_src = StopFlag{}; }
+  // hipEventSynchronize that keeps the device's view of the caller's stop flag current
+  hipError_t wait_event(hipEvent_t ev) {
+    if (!mirror_src.i && !mirror_src.b) return hipEventSynchronize(ev);
+    for (;;) {
+      const int v = mirror_src() ? 1 : 0;
+      if (*(volatile int*)mirror != v) *(volatile int*)mirror = v;
+      const hipError_t q = hipEventQuery(ev);
+      if (q != hipErrorNotReady) return q;
+      std::this_thread::yield();
+    }
   }
 };
 
@@ -2581,6 +2642,13 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
   L.trials = 0;
   for (double& t : L.t_struct) t = 0;
   BaDev& D = L.D;
+  {  // test hooks (off unless the environment asks): a NaN trial, a device-raised stop flag
+    const char* e1 = std::getenv("ORBX_BA_NAN_TRIAL");
+    const char* e2 = std::getenv("ORBX_BA_RAISE_STOP_AFTER");
+    D.nan_trial = e1 ? std::atoi(e1) : -1;
+    D.raise_after = e2 ? std::atoi(e2) : -1;
+    D.host_trial = 0;
+  }
   Ctx& c = L.c;
   const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
   D.nc = nc;
@@ -2761,6 +2829,8 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   bool ran = false;
   // LM control on the device unless the stop flag cannot be mapped (or ORBX_BA_HOST_LM=1)
   DevStop dstop{nullptr, nullptr};
+  L.unmap_stop();
+  L.hook_stopped = false;
   const bool dev_lm = std::getenv("ORBX_BA_HOST_LM") == nullptr && L.map_stop(stop, &dstop);
   auto optimize = [&](int iterations, int* iters, double* chi) {
     return dev_lm ? L.optimize_dev(iterations, stop, dstop, st, iters, chi) : L.optimize(iterations, stop, st, iters, chi);
@@ -2775,7 +2845,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
     if (s != ORBX_OK) return s;
     s = optimize(5, &res->iterations[0], &res->chi2[0]);
     if (s != ORBX_OK) return s;
-    if (!(stop())) {
+    if (!(stop()) && !L.hook_stopped) {
       // :764-802 level-1 outliers, drop robust kernels
       if (ne > 0) hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 1);
       BA_CHECK(hipGetLastError());
@@ -2792,6 +2862,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
     }
   }
   BA_CHECK(ba_writeback(L, pb, res, ran, st));
+  L.unmap_stop();
   if (!ran) return ORBX_OK;
   BA_CHECK(hipStreamSynchronize(st));
   if (std::getenv("ORBX_BA_TRACE"))
@@ -2890,11 +2961,21 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
       hipLaunchKernelGGL(k_ba_lm_final_many, dim3(1, 1, K), dim3(64), 0, st, Dg);
       BA_CHECK(hipGetLastError());
       BA_CHECK(hipMemcpyAsync(B.lm_host, B.lm.p, sizeof(LmState) * K, hipMemcpyDeviceToHost, st));
-      BA_CHECK(hipStreamSynchronize(st));
+      BA_CHECK(hipEventRecord(Ls[0]->rb_ev, st));
+      BA_CHECK(Ls[0]->wait_event(Ls[0]->rb_ev));  // keeps the device's stop mirror current
       int left = 0;
-      for (int i = 0; i < K; i++)
-        if (!B.lm_host[i].done) left = std::max(left, iterations - B.lm_host[i].it);
+      bool refresh = false;
+      for (int i = 0; i < K; i++) {
+        if (!B.lm_host[i].done || B.lm_host[i].refresh) left = std::max(left, iterations - B.lm_host[i].it);
+        refresh |= B.lm_host[i].refresh != 0;
+      }
       if (left == 0) break;
+      if (refresh) {  // problems paused on a NaN-rho rejection (all three launches gated per problem)
+        hipLaunchKernelGGL(k_ba_restore_many, dim3(gpM, 1, K), dim3(LBS), 0, st, Dg);
+        hipLaunchKernelGGL(k_ba_errors_many, dim3(geM, 1, K), dim3(LBS), 0, st, Dg, 2, 0);
+        hipLaunchKernelGGL(k_ba_lm_resume_many, dim3(1, 1, K), dim3(64), 0, st, Dg);
+        BA_CHECK(hipGetLastError());
+      }
       budget = std::max(1, left);
     }
     bool rej = false;
@@ -2930,6 +3011,7 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
     if (s != ORBX_OK) return s;
   }
   DevStop dstop{nullptr, nullptr};
+  for (int i = 0; i < K; i++) Ls[i]->unmap_stop();
   bool batch = std::getenv("ORBX_BA_HOST_LM") == nullptr && Ls[0]->map_stop(stop, &dstop);
   for (int i = 0; i < K; i++) batch &= Ls[i]->dev_struct;
   if (!batch) {  // one by one (intake again inside: the arenas are reused)
@@ -2959,11 +3041,13 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
       return ORBX_OK;
     }
     if (s != ORBX_OK) return s;
+    bool hook = false;
     for (int i = 0; i < K; i++) {
       ress[i].iterations[0] = it[i];
       ress[i].chi2[0] = chi[i];
+      hook |= B.lm_host[i].stopped && Ls[i]->D.raise_after >= 0;
     }
-    if (!(stop())) {
+    if (!(stop()) && !hook) {
       for (int i = 0; i < K; i++) {  // :764-802 level-1 outliers, drop robust kernels
         const int ne = pbs[i].n_edges;
         if (ne > 0)
@@ -2980,6 +3064,7 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
     }
   }
   for (int i = 0; i < K; i++) BA_CHECK(ba_writeback(*Ls[i], &pbs[i], &ress[i], ran, st));
+  Ls[0]->unmap_stop();
   BA_CHECK(hipStreamSynchronize(st));
   return ORBX_OK;
 }

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <vector>
 
+#include "orbx_scratch.h"
 #include "orbx_device.h"
 #include "orbx_internal.h"
 
@@ -157,21 +158,33 @@ extern "C" orbx_status orbx_distinctive_descriptors(const uint8_t* desc, const i
   const size_t nd = (size_t)obs_off[n_points];
   const size_t b_desc = (nd * 32 + 255) & ~(size_t)255, b_off = ((size_t)(n_points + 1) * 4 + 255) & ~(size_t)255;
   const size_t b_best = ((size_t)n_points * 4 + 255) & ~(size_t)255;
-  uint8_t* d = nullptr;
-  if (hipMalloc((void**)&d, b_desc + b_off + b_best + (size_t)n_points * 32) != hipSuccess) return ORBX_ERR_HIP;
+  // pooled lease (orbx_scratch.h): inputs staged in pinned memory, one stream, no allocation
+  const size_t total = b_desc + b_off + b_best + (size_t)n_points * 32;
+  orbx::ScratchGuard g(device);
+  if (!g.l || g.l->reserve(total, total) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* d = g.l->d;
+  uint8_t* h = g.l->h;
   uint8_t *d_desc = d, *d_off = d + b_desc, *d_best = d_off + b_off, *d_out = d_best + b_best;
-  hipError_t e = nd ? hipMemcpy(d_desc, desc, nd * 32, hipMemcpyHostToDevice) : hipSuccess;
-  if (e == hipSuccess) e = hipMemcpy(d_off, obs_off, (size_t)(n_points + 1) * 4, hipMemcpyHostToDevice);
+  if (nd) std::memcpy(h, desc, nd * 32);
+  std::memcpy(h + b_desc, obs_off, (size_t)(n_points + 1) * 4);
+  hipStream_t sm = g.l->st;
+  hipError_t e = hipMemcpyAsync(d, h, b_desc + (size_t)(n_points + 1) * 4, hipMemcpyHostToDevice, sm);
   orbx_status st = ORBX_ERR_HIP;
   if (e == hipSuccess)
     st = orbx_distinctive_descriptors_device(d_desc, (const int32_t*)d_off, n_points, (int32_t*)d_best,
-                                             out_desc ? d_out : nullptr, nullptr);
+                                             out_desc ? d_out : nullptr, sm);
   if (st == ORBX_OK) {
-    e = hipMemcpy(best, d_best, (size_t)n_points * 4, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && out_desc) e = hipMemcpy(out_desc, d_out, (size_t)n_points * 32, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) st = ORBX_ERR_HIP;
+    // best and the descriptors are adjacent: one copy back
+    e = hipMemcpyAsync(h + (d_best - d), d_best, out_desc ? b_best + (size_t)n_points * 32 : (size_t)n_points * 4,
+                       hipMemcpyDeviceToHost, sm);
+    if (e == hipSuccess) e = g.l->sync();
+    if (e != hipSuccess) {
+      st = ORBX_ERR_HIP;
+    } else {
+      std::memcpy(best, h + (d_best - d), (size_t)n_points * 4);
+      if (out_desc) std::memcpy(out_desc, h + (d_out - d), (size_t)n_points * 32);
+    }
   }
-  (void)hipFree(d);
   return st;
 }
 
@@ -196,19 +209,31 @@ extern "C" orbx_status orbx_undistort_keypoints(const orbx_keypoint* keys, int n
   const orbx_status ds = set_device(device);
   if (ds != ORBX_OK) return ds;
   const size_t bk = ((size_t)n * sizeof(orbx_keypoint) + 255) & ~(size_t)255;
-  uint8_t* d = nullptr;
-  if (hipMalloc((void**)&d, 2 * bk + 256 + sizeof(orbx_camera)) != hipSuccess) return ORBX_ERR_HIP;
+  const size_t total = 2 * bk + 256 + sizeof(orbx_camera);
+  orbx::ScratchGuard g(device);  // pooled lease (orbx_scratch.h)
+  if (!g.l || g.l->reserve(total, total) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* d = g.l->d;
+  uint8_t* h = g.l->h;
   orbx_keypoint *d_in = (orbx_keypoint*)d, *d_out = (orbx_keypoint*)(d + bk);
   int32_t* d_off = (int32_t*)(d + 2 * bk);
   orbx_camera* d_cam = (orbx_camera*)(d + 2 * bk + 256);
   const int32_t off[2] = {0, n};
-  hipError_t e = hipMemcpy(d_in, keys, (size_t)n * sizeof(orbx_keypoint), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(d_off, off, sizeof(off), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(d_cam, cam, sizeof(orbx_camera), hipMemcpyHostToDevice);
+  std::memcpy(h, keys, (size_t)n * sizeof(orbx_keypoint));
+  std::memcpy(h + 2 * bk, off, sizeof(off));
+  std::memcpy(h + 2 * bk + 256, cam, sizeof(orbx_camera));
+  hipStream_t sm = g.l->st;
+  // inputs in two copies (keypoints; offsets + camera), the output in one
+  hipError_t e = hipMemcpyAsync(d, h, (size_t)n * sizeof(orbx_keypoint), hipMemcpyHostToDevice, sm);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + 2 * bk, h + 2 * bk, 256 + sizeof(orbx_camera), hipMemcpyHostToDevice, sm);
   orbx_status st = ORBX_ERR_HIP;
-  if (e == hipSuccess) st = orbx_undistort_keypoints_device(d_in, d_off, 1, n, d_cam, d_out, nullptr);
-  if (st == ORBX_OK && hipMemcpy(keys_un, d_out, (size_t)n * sizeof(orbx_keypoint), hipMemcpyDeviceToHost) != hipSuccess)
-    st = ORBX_ERR_HIP;
-  (void)hipFree(d);
+  if (e == hipSuccess) st = orbx_undistort_keypoints_device(d_in, d_off, 1, n, d_cam, d_out, sm);
+  if (st == ORBX_OK) {
+    e = hipMemcpyAsync(h + bk, d_out, (size_t)n * sizeof(orbx_keypoint), hipMemcpyDeviceToHost, sm);
+    if (e == hipSuccess) e = g.l->sync();
+    if (e != hipSuccess)
+      st = ORBX_ERR_HIP;
+    else
+      std::memcpy(keys_un, h + bk, (size_t)n * sizeof(orbx_keypoint));
+  }
   return st;
 }

@@ -1895,6 +1895,9 @@ orbx_status orbx_pnp_iterate_candidates(orbx_pnp* const* solvers, int n, int n_i
   }
   if ((s = pnp_run_many(runs, true, stopped)) != ORBX_OK) return s;
   for (int i = 0; i < n; i++) results[i].used = runs[i].used;
+  // the reference never reaches the candidates after the one that returned a pose: their
+  // results are all zero (pnp_begin above already set bNoMore for N < minInliers on them)
+  for (int i = *stopped + 1; i < n; i++) std::memset(&results[i], 0, sizeof(results[i]));
   size_t used = 0;
   for (int i = 0; i < n && i <= *stopped; i++) used += runs[i].used;
   for (size_t k = 0; k < used; k++) (void)orbx_rand_next(rng);

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "orbx_device.h"
+#include "orbx_scratch.h"
 #include "orbx_internal.h"
 
 namespace orbx {
@@ -690,14 +691,16 @@ extern "C" orbx_status orbx_pose_optimization(const orbx_pose_problem* p, int de
                o_out = o_Tout + al(64), o_ng = o_out + al(n), o_it = o_ng + al(4),
                o_scr = o_it + al(16), o_act = o_scr + al(n * orbx::pose::kRow * 8), o_dev = o_act + al(n * 4),
                total = o_dev + al(sizeof(orbx::pose::PoseDev));
-  std::vector<uint8_t> host(o_scr, 0);
+  orbx::ScratchGuard g(device);  // pooled lease: no per-call allocation (orbx_scratch.h)
+  if (!g.l || g.l->reserve(total, o_scr + sizeof(orbx::pose::PoseDev)) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* host = g.l->h;
+  std::memset(host, 0, o_scr);  // outputs start zeroed, as before
   if (n) {
-    std::memcpy(host.data() + o_obs, p->obs, n * 12);
-    std::memcpy(host.data() + o_X, p->Xw, n * 12);
-    std::memcpy(host.data() + o_s2, p->inv_sigma2, n * 4);
+    std::memcpy(host + o_obs, p->obs, n * 12);
+    std::memcpy(host + o_X, p->Xw, n * 12);
+    std::memcpy(host + o_s2, p->inv_sigma2, n * 4);
   }
-  uint8_t* d = nullptr;
-  if (hipMalloc((void**)&d, total) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* d = g.l->d;
   orbx::pose::PoseDev pd;
   pd.p = *p;
   pd.p.obs = (const float*)(d + o_obs);
@@ -709,20 +712,22 @@ extern "C" orbx_status orbx_pose_optimization(const orbx_pose_problem* p, int de
   pd.p.iterations = (int32_t*)(d + o_it);
   pd.scratch = (double*)(d + o_scr);
   pd.act = (int*)(d + o_act);
-  hipError_t e = hipMemcpy(d, host.data(), o_scr, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(d + o_dev, &pd, sizeof(pd), hipMemcpyHostToDevice);
+  std::memcpy(host + o_scr, &pd, sizeof(pd));  // the record rides in the staging block's tail
+  hipStream_t st = g.l->st;
+  hipError_t e = hipMemcpyAsync(d, host, o_scr, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + o_dev, host + o_scr, sizeof(pd), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(orbx::pose::k_pose_optimization, dim3(1), dim3(orbx::pose::PBS), 0, nullptr,
+    hipLaunchKernelGGL(orbx::pose::k_pose_optimization, dim3(1), dim3(orbx::pose::PBS), 0, st,
                        (const orbx::pose::PoseDev*)(d + o_dev));
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipMemcpy(host.data(), d, o_scr, hipMemcpyDeviceToHost);
-  (void)hipFree(d);
+  if (e == hipSuccess) e = hipMemcpyAsync(host + o_Tout, d + o_Tout, o_scr - o_Tout, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = g.l->sync();
   if (e != hipSuccess) return ORBX_ERR_HIP;
-  std::memcpy(p->Tcw_out, host.data() + o_Tout, 64);
-  if (n) std::memcpy(p->outlier, host.data() + o_out, n);
-  std::memcpy(p->ngood, host.data() + o_ng, 4);
-  if (p->iterations) std::memcpy(p->iterations, host.data() + o_it, 16);
+  std::memcpy(p->Tcw_out, host + o_Tout, 64);
+  if (n) std::memcpy(p->outlier, host + o_out, n);
+  std::memcpy(p->ngood, host + o_ng, 4);
+  if (p->iterations) std::memcpy(p->iterations, host + o_it, 16);
   return ORBX_OK;
 }
 

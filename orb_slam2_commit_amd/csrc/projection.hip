@@ -35,6 +35,7 @@
 #include <cstring>
 #include <vector>
 
+#include "orbx_scratch.h"
 #include "orbx_device.h"
 #include "orbx_internal.h"
 #include "orbx_proj.h"
@@ -565,7 +566,6 @@ extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int
   const size_t nF = (size_t)p->f.n, nP = (size_t)p->n_points;
   const bool local = p->kind == ORBX_PROJ_LOCAL;
   // one arena: inputs, outputs, problem descriptor
-  std::vector<uint8_t> host;
   size_t off = 0;
   struct Item { const void* src; size_t bytes; size_t at; };
   std::vector<Item> items;
@@ -593,11 +593,13 @@ extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int
   const size_t a_pm = reserve(nullptr, nP * 4);
   const size_t a_nm = reserve(nullptr, 4);
   const size_t a_prob = reserve(nullptr, sizeof(orbx_proj_problem));
-  host.assign(off, 0);
+  orbx::ScratchGuard g(device);  // pooled lease: no per-call allocation (orbx_scratch.h)
+  if (!g.l || g.l->reserve(off, off) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* hst = g.l->h;
+  std::memset(hst, 0, off);
   for (const Item& it : items)
-    if (it.src && it.bytes) std::memcpy(host.data() + it.at, it.src, it.bytes);
-  uint8_t* d = nullptr;
-  if (hipMalloc((void**)&d, off) != hipSuccess) return ORBX_ERR_HIP;
+    if (it.src && it.bytes) std::memcpy(hst + it.at, it.src, it.bytes);
+  uint8_t* d = g.l->d;
   orbx_proj_problem q = *p;
   q.f.keys_un = (const orbx_keypoint*)(d + a_keys);
   q.f.desc = d + a_fdesc;
@@ -615,18 +617,20 @@ extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int
   q.frame_out = (int32_t*)(d + a_fout);
   q.point_match = (int32_t*)(d + a_pm);
   q.nmatches = (int32_t*)(d + a_nm);
-  std::memcpy(host.data() + a_prob, &q, sizeof(q));
-  hipError_t e = hipMemcpy(d, host.data(), off, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = orbx::launch_search_by_projection((const orbx::ProjProblem*)(d + a_prob), 1, nullptr);
-  if (e == hipSuccess) e = hipMemcpy(host.data(), d, off, hipMemcpyDeviceToHost);
-  (void)hipFree(d);
+  std::memcpy(hst + a_prob, &q, sizeof(q));
+  hipStream_t st = g.l->st;
+  const size_t o_out = local ? a_trk : a_fout;  // outputs are contiguous up to the descriptor
+  hipError_t e = hipMemcpyAsync(d, hst, off, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = orbx::launch_search_by_projection((const orbx::ProjProblem*)(d + a_prob), 1, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hst + o_out, d + o_out, a_prob - o_out, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = g.l->sync();
   if (e != hipSuccess) return proj_status(e);
-  if (nF) std::memcpy(p->frame_out, host.data() + a_fout, nF * 4);
-  if (nP) std::memcpy(p->point_match, host.data() + a_pm, nP * 4);
-  std::memcpy(p->nmatches, host.data() + a_nm, 4);
+  if (nF) std::memcpy(p->frame_out, hst + a_fout, nF * 4);
+  if (nP) std::memcpy(p->point_match, hst + a_pm, nP * 4);
+  std::memcpy(p->nmatches, hst + a_nm, 4);
   if (local && p->frustum && nP) {
-    std::memcpy(p->track, host.data() + a_trk, nP * 16);
-    std::memcpy(p->track_level, host.data() + a_lvl, nP * 4);
+    std::memcpy(p->track, hst + a_trk, nP * 16);
+    std::memcpy(p->track_level, hst + a_lvl, nP * 4);
   }
   return ORBX_OK;
 }

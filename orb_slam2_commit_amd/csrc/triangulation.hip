@@ -17,6 +17,7 @@
 #include <cstring>
 #include <vector>
 
+#include "orbx_scratch.h"
 #include "orbx_device.h"
 #include "orbx_internal.h"
 
@@ -238,7 +239,6 @@ extern "C" orbx_status orbx_search_for_triangulation(const orbx_tri_problem* p, 
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_NODEV;
   if (device < 0 || device >= ndev || hipSetDevice(device) != hipSuccess) return ORBX_ERR_ARG;
-  std::vector<uint8_t> host;
   size_t off = 0;
   struct Item { const void* src; size_t bytes; size_t at; };
   std::vector<Item> items;
@@ -263,11 +263,13 @@ extern "C" orbx_status orbx_search_for_triangulation(const orbx_tri_problem* p, 
   }
   const size_t a_m = put(nullptr, (size_t)p->kf1.n * 4), a_n = put(nullptr, 4);
   const size_t a_p = put(nullptr, sizeof(orbx_tri_problem));
-  host.assign(off, 0);
+  orbx::ScratchGuard g(device);  // pooled lease: no per-call allocation (orbx_scratch.h)
+  if (!g.l || g.l->reserve(off, off) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* hst = g.l->h;
+  std::memset(hst, 0, off);
   for (const Item& it : items)
-    if (it.src && it.bytes) std::memcpy(host.data() + it.at, it.src, it.bytes);
-  uint8_t* d = nullptr;
-  if (hipMalloc((void**)&d, off) != hipSuccess) return ORBX_ERR_HIP;
+    if (it.src && it.bytes) std::memcpy(hst + it.at, it.src, it.bytes);
+  uint8_t* d = g.l->d;
   orbx_tri_problem q = *p;
   for (int s = 0; s < 2; s++) {
     const orbx_tri_kf& k = s ? p->kf2 : p->kf1;
@@ -282,17 +284,21 @@ extern "C" orbx_status orbx_search_for_triangulation(const orbx_tri_problem* p, 
   }
   q.match12 = (int32_t*)(d + a_m);
   q.nmatches = (int32_t*)(d + a_n);
-  std::memcpy(host.data() + a_p, &q, sizeof(q));
-  hipError_t e = hipMemcpy(d, host.data(), off, hipMemcpyHostToDevice);
+  std::memcpy(hst + a_p, &q, sizeof(q));
+  hipStream_t st = g.l->st;
+  hipError_t e = hipMemcpyAsync(d, hst, off, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(orbx::tri::k_search_for_triangulation, dim3(1), dim3(orbx::tri::TBS), 0, nullptr,
+    hipLaunchKernelGGL(orbx::tri::k_search_for_triangulation, dim3(1), dim3(orbx::tri::TBS), 0, st,
                        (const orbx_tri_problem*)(d + a_p));
     e = hipGetLastError();
   }
-  if (e == hipSuccess && p->kf1.n) e = hipMemcpy(p->match12, d + a_m, (size_t)p->kf1.n * 4, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipMemcpy(p->nmatches, d + a_n, 4, hipMemcpyDeviceToHost);
-  (void)hipFree(d);
-  return e == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
+  // match12 and the count are adjacent: one copy back
+  if (e == hipSuccess) e = hipMemcpyAsync(hst + a_m, d + a_m, a_p - a_m, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = g.l->sync();
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  if (p->kf1.n) std::memcpy(p->match12, hst + a_m, (size_t)p->kf1.n * 4);
+  std::memcpy(p->nmatches, hst + a_n, 4);
+  return ORBX_OK;
 }
 
 extern "C" orbx_status orbx_search_for_triangulation_device(const orbx_tri_problem* problems, int n, void* stream) {

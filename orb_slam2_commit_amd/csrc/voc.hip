@@ -49,13 +49,22 @@ __device__ __forceinline__ int hamming4(const uint64_t f[4], const uint64_t* d) 
   return __popcll(f[0] ^ d[0]) + __popcll(f[1] ^ d[1]) + __popcll(f[2] ^ d[2]) + __popcll(f[3] ^ d[3]);
 }
 
+// set_cnt != nullptr: strided sets -- output row i is row r = i % cap of set s = i / cap, read
+// from input row s * stride + r, live while r < set_cnt[s * cnt_step] (the device batch layout:
+// each image's descriptors at a fixed capacity stride with its count on the device)
 __global__ __launch_bounds__(256) void k_voc_descend(VocDev V, const uint64_t* __restrict__ feats, int total,
                                                      int levelsup, int* __restrict__ word, double* __restrict__ weight,
-                                                     int* __restrict__ nid) {
+                                                     int* __restrict__ nid, const int32_t* __restrict__ set_cnt,
+                                                     int cap, long long stride, int cnt_step) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
-  const uint64_t f[4] = {feats[4 * (size_t)i], feats[4 * (size_t)i + 1], feats[4 * (size_t)i + 2],
-                         feats[4 * (size_t)i + 3]};
+  size_t row = (size_t)i;
+  if (set_cnt) {
+    const int s = i / cap, r = i - s * cap;
+    if (r >= set_cnt[(size_t)s * cnt_step]) return;
+    row = (size_t)s * stride + r;
+  }
+  const uint64_t f[4] = {feats[4 * row], feats[4 * row + 1], feats[4 * row + 2], feats[4 * row + 3]};
   const int nid_level = V.L - levelsup;
   int nv = 0, node = 0, level = 0;
   for (;;) {
@@ -167,10 +176,14 @@ struct VocSetOut {
 __global__ __launch_bounds__(kVocBuildThreads) void k_voc_build(VocDev V, const int32_t* __restrict__ set_off,
                                                                 const int* __restrict__ word,
                                                                 const double* __restrict__ weight,
-                                                                const int* __restrict__ nid, VocSetOut O) {
+                                                                const int* __restrict__ nid, VocSetOut O,
+                                                                const int32_t* __restrict__ set_cnt, int cap,
+                                                                int cnt_step) {
   extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // P keys, then P run starts (int)
   __shared__ int sh[kVocBuildThreads / 64 + 1];
-  const int s = blockIdx.x, o = set_off[s], n = set_off[s + 1] - o;
+  const int s = blockIdx.x;
+  const int o = set_cnt ? s * cap : set_off[s];
+  const int n = set_cnt ? min(set_cnt[(size_t)s * cnt_step], cap) : set_off[s + 1] - o;
   int P = 1;
   while (P < n) P <<= 1;
   int* rs = reinterpret_cast<int*>(keys + P);
@@ -481,7 +494,7 @@ orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* 
   VOC_CHECK(hipMemcpyAsync(d_desc, desc, 32 * nt, hipMemcpyHostToDevice, st));
   VOC_CHECK(hipMemcpyAsync(d_soff, set_off, 4 * (ns + 1), hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(orbx::k_voc_descend, dim3((total + 255) / 256), dim3(256), 0, st, v->dev, d_desc, total,
-                     levelsup, d_word, d_wt, d_nid);
+                     levelsup, d_word, d_wt, d_nid, nullptr, 1, 1LL, 1);
   int P = 1;
   while (P < maxn) P <<= 1;
   const size_t smem = (size_t)P * 8 + (size_t)P * 4;
@@ -489,7 +502,7 @@ orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* 
     VOC_CHECK(hipFuncSetAttribute((const void*)orbx::k_voc_build, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)smem));
   hipLaunchKernelGGL(orbx::k_voc_build, dim3(n_sets), dim3(orbx::kVocBuildThreads), smem, st, v->dev, d_soff,
-                     d_word, d_wt, d_nid, O);
+                     d_word, d_wt, d_nid, O, nullptr, 0, 1);
   VOC_CHECK(hipGetLastError());
   VOC_CHECK(hipMemcpyAsync(bow_words, O.bow_words, 4 * nt, hipMemcpyDeviceToHost, st));
   VOC_CHECK(hipMemcpyAsync(bow_values, O.bow_values, 8 * nt, hipMemcpyDeviceToHost, st));
@@ -499,6 +512,51 @@ orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* 
   VOC_CHECK(hipMemcpyAsync(fv_feat, O.fv_feat, 4 * nt, hipMemcpyDeviceToHost, st));
   VOC_CHECK(hipMemcpyAsync(n_fv, O.n_fv, 4 * ns, hipMemcpyDeviceToHost, st));
   VOC_CHECK(hipStreamSynchronize(st));
+  return ORBX_OK;
+}
+
+orbx_status orbx_voc_transform_device(orbx_voc* v, const uint8_t* d_desc, int cap, long long stride,
+                                      const int32_t* d_count, int count_step, int n_sets, int levelsup,
+                                      uint32_t* d_bow_words, double* d_bow_values, int32_t* d_n_bow,
+                                      uint32_t* d_fv_nodes, int32_t* d_fv_off, int32_t* d_fv_feat, int32_t* d_n_fv,
+                                      void* stream) {
+  if (!v || n_sets < 0 || cap <= 0 || stride < cap || count_step < 1 || (n_sets > 0 && (!d_desc || !d_count)))
+    return ORBX_ERR_ARG;
+  if (n_sets == 0) return ORBX_OK;
+  if (!d_bow_words || !d_bow_values || !d_n_bow || !d_fv_nodes || !d_fv_off || !d_fv_feat || !d_n_fv)
+    return ORBX_ERR_ARG;
+  if (cap > orbx::kVocMaxSet) return ORBX_ERR_SIZE;
+  if (v->empty) return ORBX_ERR_STATE;
+  if (hipSetDevice(v->device) != hipSuccess) return ORBX_ERR_HIP;
+  hipStream_t st = stream ? (hipStream_t)stream : v->st;
+  const size_t nt = (size_t)n_sets * cap;
+  if (nt > (size_t)0x7FFFFFFF) return ORBX_ERR_SIZE;
+  const size_t need = a256(4 * nt) + a256(8 * nt) + a256(4 * nt);  // word | weight | nid
+  if (need > v->work_cap) {
+    VOC_CHECK(hipStreamSynchronize(st));  // the scratch may still be read by a queued build
+    if (v->d_work) (void)hipFree(v->d_work);
+    v->d_work = nullptr;
+    v->work_cap = 0;
+    VOC_CHECK(hipMalloc(&v->d_work, need));
+    v->work_cap = need;
+  }
+  uint8_t* w = (uint8_t*)v->d_work;
+  int* d_word = (int*)w;
+  double* d_wt = (double*)(w + a256(4 * nt));
+  int* d_nid = (int*)(w + a256(4 * nt) + a256(8 * nt));
+  orbx::VocSetOut O{d_bow_words, d_bow_values, d_n_bow, d_fv_nodes, d_fv_off, d_fv_feat, d_n_fv};
+  hipLaunchKernelGGL(orbx::k_voc_descend, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, v->dev,
+                     (const uint64_t*)d_desc, (int)nt, levelsup, d_word, d_wt, d_nid, d_count, cap, stride,
+                     count_step);
+  int P = 1;
+  while (P < cap) P <<= 1;
+  const size_t smem = (size_t)P * 8 + (size_t)P * 4;
+  if (smem > 64 * 1024)
+    VOC_CHECK(hipFuncSetAttribute((const void*)orbx::k_voc_build, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)smem));
+  hipLaunchKernelGGL(orbx::k_voc_build, dim3(n_sets), dim3(orbx::kVocBuildThreads), smem, st, v->dev, nullptr,
+                     d_word, d_wt, d_nid, O, d_count, cap, count_step);
+  VOC_CHECK(hipGetLastError());
   return ORBX_OK;
 }
 

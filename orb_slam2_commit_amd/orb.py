@@ -712,11 +712,12 @@ def _pnp_outputs(solvers, res, inl):
     return out
 
 
-def pnp_iterate_candidates(solvers, nIterations, rng):
+def pnp_iterate_candidates(solvers, nIterations, rng, raw_results=None):
     """Tracking::Relocalization's candidate loop (src/Tracking.cc:1738-1757) in one call:
     solvers[0].iterate(n), solvers[1].iterate(n), ... on the shared stream `rng` (GlibcRand),
     stopping after the first that returns a pose.  Returns (stopped, [(Tcw|None, bNoMore,
-    vbInliers, nInliers)] for solvers[0..stopped]); rng advances by exactly what was drawn."""
+    vbInliers, nInliers)] for solvers[0..stopped]); rng advances by exactly what was drawn.
+    raw_results: optional list that receives every solver's orbx_pnp_result (tests)."""
     n = len(solvers)
     hs = (C.c_void_p * max(n, 1))(*[s._h for s in solvers])
     res = (_lib.PnpResult * max(n, 1))()
@@ -727,6 +728,8 @@ def pnp_iterate_candidates(solvers, nIterations, rng):
     check(_lib.lib().orbx_pnp_iterate_candidates(hs, n, int(nIterations), C.byref(st), res, ip, C.byref(stopped)),
           "orbx_pnp_iterate_candidates")
     _rand_restore(rng, st)
+    if raw_results is not None:
+        raw_results.extend(res[i] for i in range(n))
     k = min(stopped.value + 1, n)
     return stopped.value, _pnp_outputs(solvers[:k], res[:k], inl[:k])
 

@@ -98,13 +98,32 @@ def new_arena(layout, device):
     return torch.zeros(layout.nbytes, dtype=torch.uint8, device=device)
 
 
+def agree_max(value):
+    """The maximum of an integer over every rank of the process group (the value itself without
+    one).  all_gather_into_tensor / gloo all_gather need the same tensor size on every rank, and
+    sequences differ in image size (KITTI 00-02 1241x376, 03 1242x375, 04-10 1226x370) and in
+    local-map size, so every size that shapes an exchanged buffer is agreed on first."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return int(value)
+    dev = "cpu"
+    if dist.get_backend() != "gloo":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
+
+
 class SequenceShard:
     """One rank's share of config 5: extract + stereo-match its sequence's frames batch by batch into
-    a FrameRecords arena (orbx_stereo_frames_device writes straight into the arena's sections)."""
+    a FrameRecords arena (orbx_stereo_frames_device writes straight into the arena's sections).  The
+    layout (frames per batch, keypoint capacity) is the maximum over the ranks, so every rank's arena
+    has the same size for the all-gather whatever its sequence's image size."""
 
     def __init__(self, extractor, n_frames, width, height, bf, baseline, device):
         self.ex = extractor
-        self.layout = FrameRecords(n_frames, extractor.max_keypoints(width, height))
+        self.layout = FrameRecords(agree_max(n_frames), agree_max(extractor.max_keypoints(width, height)))
         self.arena = new_arena(self.layout, device)
         self.v = self.layout.views(self.arena)
         self.bf, self.baseline = float(bf), float(baseline)
@@ -138,21 +157,31 @@ class SequenceShard:
 
 
 # ------------------------------------------------------------------ LocalBA summary record
-def ba_summary(result, n_cams):
-    """Fixed-size FP64 record of one LocalBundleAdjustment call: [iterations phase 1, phase 2, trials,
-    chi2 phase 1, chi2 phase 2, outlier edges, n_cams, Tcw (n_cams x 12, row-major 3x4)]."""
+MAX_BA_CAMS = 64  # local window KFs + fixed KFs of one LocalBA call, far above ORB-SLAM2's usual ~30
+BA_HEAD = 7
+
+
+def ba_summary(result, n_cams, max_cams=MAX_BA_CAMS):
+    """Fixed-size FP64 record of one LocalBundleAdjustment call (the same length on every rank,
+    whatever its local map): [iterations phase 1, phase 2, trials, chi2 phase 1, chi2 phase 2, outlier
+    edges, n_cams, Tcw (max_cams x 12, row-major 3x4; rows past n_cams zero)]."""
+    if n_cams > max_cams:
+        raise ValueError("LocalBA summary: %d cameras > max_cams %d" % (n_cams, max_cams))
     its = list(result["iterations"]) + [0, 0]
     chi = list(result.get("chi2", (0.0, 0.0))) + [0.0, 0.0]
     head = [its[0], its[1], result["trials"], chi[0], chi[1], float(np.sum(result["edge_outlier"])), n_cams]
+    rec = np.zeros(BA_HEAD + 12 * max_cams, np.float64)
+    rec[:BA_HEAD] = head
     T = np.asarray(result["Tcw_d"], np.float64).reshape(-1)
-    return np.concatenate([np.asarray(head, np.float64), T[:12 * n_cams]])
+    rec[BA_HEAD:BA_HEAD + 12 * n_cams] = T[:12 * n_cams]
+    return rec
 
 
 def parse_ba_summary(rec):
     rec = np.asarray(rec, np.float64)
     n = int(rec[6])
     return dict(iterations=(int(rec[0]), int(rec[1])), trials=int(rec[2]), chi2=(rec[3], rec[4]),
-                outliers=int(rec[5]), Tcw=rec[7:7 + 12 * n].reshape(n, 12))
+                outliers=int(rec[5]), Tcw=rec[BA_HEAD:BA_HEAD + 12 * n].reshape(n, 12))
 
 
 # ------------------------------------------------------------------ collectives
@@ -176,8 +205,14 @@ def all_gather_bytes(t):
 
 
 def gather_sequence_results(shard_arena, ba_record, device=None):
-    """The config-5 exchange: every rank's frame-record arena and LocalBA summary to every rank."""
+    """The config-5 exchange: every rank's frame-record arena and LocalBA summary to every rank.
+    Both must have the same size on every rank (SequenceShard / ba_summary make them so); a mismatch
+    is an error here rather than a hang inside the collective."""
     import torch
+    for what, n in (("frame-record arena", shard_arena.numel()), ("LocalBA summary", len(ba_record))):
+        mx, mn = agree_max(n), -agree_max(-n)  # both collectives on every rank, then the verdict
+        if mx != mn:
+            raise ValueError("config-5 exchange: %s size differs between ranks (%d here)" % (what, n))
     recs = all_gather_bytes(shard_arena)
     ba = torch.as_tensor(np.asarray(ba_record, np.float64))
     if device is not None and _backend() != "gloo":

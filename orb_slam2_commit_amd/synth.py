@@ -96,15 +96,17 @@ def sequence_seeds(seq, n_unique):
     return [1000 * seq + s for s in range(n_unique)]
 
 
-def stereo_batch(seq, n_frames, n_unique=16, width=1241, height=376, pairs=None):
-    """Frames of synthetic sequence `seq` as one (2*n_frames, height, width) u8 array ordered
-    L0,R0,L1,R1,... (the orbx_stereo_frames_device layout).  Frame f is scene f % U rolled
-    horizontally by 53*(f // U) px (left and right alike, so the disparity field is kept): no two
-    frames share bytes.  This is exactly the bench.py batch."""
+def stereo_batch(seq, n_frames, n_unique=16, width=1241, height=376, pairs=None, first=0):
+    """Frames first .. first+n_frames-1 of synthetic sequence `seq` as one (2*n_frames, height, width)
+    u8 array ordered L0,R0,L1,R1,... (the orbx_stereo_frames_device layout).  Frame f is scene f % U
+    rolled horizontally by 53*(f // U) px (left and right alike, so the disparity field is kept); 53
+    is coprime with the KITTI width, so no two of the first U*width frames share bytes.  bench.py's
+    in-flight batch k is first = k*B."""
     if pairs is None:
         pairs = [stereo_pair(s, width, height) for s in sequence_seeds(seq, n_unique)]
     U = len(pairs)
-    return np.stack([np.roll(pairs[f % U][k], 53 * (f // U), axis=1) for f in range(n_frames) for k in (0, 1)])
+    return np.stack([np.roll(pairs[f % U][k], 53 * (f // U), axis=1)
+                     for f in range(first, first + n_frames) for k in (0, 1)])
 
 
 def mono_image(seed, width=640, height=480):

@@ -32,11 +32,12 @@ class ORBextractor {
   std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2; }
   std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
-  // Filled after every operator() call when mbDownloadPyramid (default): readers outside the
-  // stereo matcher (src/Frame.cc:556,681,694,700 in the reference) see the same levels.  The GPU
-  // stereo matcher reads the device copy, so a caller that needs no host pyramid turns it off.
+  // The reference's only readers of mvImagePyramid are in Frame::ComputeStereoMatches
+  // (src/Frame.cc:556,681,694,700), which here runs on the device copy; so by default the host
+  // copy is NOT downloaded (eight synchronous copies per call).  A caller that reads the levels
+  // on the host sets mbDownloadPyramid, and every operator() call then fills them.
   std::vector<cv::Mat> mvImagePyramid;
-  bool mbDownloadPyramid = true;
+  bool mbDownloadPyramid = false;
 
   // The device handle (Frame::ComputeStereoMatches binds two of them).
   orbx_extractor* gpu() const { return mpGpu; }

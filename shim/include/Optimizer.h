@@ -1,7 +1,12 @@
 // Optimizer.h -- Optimizer::LocalBundleAdjustment (include/Optimizer.h:61, src/Optimizer.cc:530-885)
-// over liborbx.so, taking the local window as an explicit problem: the caller gathers
-// lLocalKeyFrames / lFixedCameras / lLocalMapPoints and their observations exactly as
-// src/Optimizer.cc:532-650 does and applies the result under the map mutex (:817-885).
+// over liborbx.so.  Two forms:
+//   * the reference signature LocalBundleAdjustment(KeyFrame*, bool*, Map*): the shim gathers the
+//     local window from the object graph exactly as src/Optimizer.cc:532-745 does (covisible
+//     KeyFrames, their MapPoints, the fixed cameras that observe them, one edge per observation in
+//     GetObservations() order), runs it on the MI355X, and applies the result as :817-884 does
+//     (EraseMapPointMatch / EraseObservation under Map::mMutexMapUpdate, SetPose, SetWorldPos,
+//     UpdateNormalAndDepth);
+//   * the same on an explicit problem (the caller gathers and applies).
 // g2o semantics (BlockSolver_6_3, LinearSolverEigen, Levenberg, Huber kernels, optimize(5),
 // outlier levels, optimize(10)) run in FP64 on the MI355X.
 #pragma once
@@ -37,12 +42,22 @@ struct LocalBAResult {
   int trials = 0;
 };
 
+class KeyFrame;
+class Map;
+
 class Optimizer {
  public:
-  // pbStopFlag: the reference's bool* (NULL allowed), polled before the run and between LM trials.
-  // Throws std::runtime_error on a library error.
+  // include/Optimizer.h:61.  pbStopFlag: the reference's bool* (NULL allowed), polled before the
+  // run and between LM trials.  Runs on device mnDevice.  Throws std::runtime_error on a library
+  // error (the object graph is then left as it was).
+  void static LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap);
+  // The explicit-problem form.  Throws std::runtime_error on a library error.
   void static LocalBundleAdjustment(const LocalBAProblem& problem, bool* pbStopFlag, LocalBAResult& result,
                                     int device = 0);
+
+  static int mnDevice;  // device of the graph form (default 0)
+  // test hook: called with the window the graph form gathered, before it runs (NULL: none)
+  static void (*mpfnGatheredHook)(const LocalBAProblem& problem, const std::vector<KeyFrame*>& cameras);
 };
 
 }  // namespace ORB_SLAM2

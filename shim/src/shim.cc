@@ -1,12 +1,15 @@
 // shim.cc -- the reference's hot-path classes (ORBextractor, Frame's ORB/stereo part, ORBmatcher's
-// SearchByBoW / DescriptorDistance, Optimizer::LocalBundleAdjustment) as thin C++ over the C ABI of
-// liborbx.so (include/orbx.h).  Argument meaning and error behaviour follow the reference; a
-// library error (no device, bad geometry) throws std::runtime_error where the reference would
-// assert or crash.  No computation happens here beyond marshalling.
+// SearchByBoW / DescriptorDistance, PnPsolver, Optimizer::LocalBundleAdjustment) as thin C++ over
+// the C ABI of liborbx.so (include/orbx.h).  Argument meaning and error behaviour follow the
+// reference; a library error (no device, bad geometry) throws std::runtime_error where the
+// reference would assert or crash.  No computation happens here beyond marshalling: gathering the
+// inputs from the object graph and applying the results to it, as the reference's own members do.
 #include <cstddef>
 #include <cstdio>
 #include <exception>
 #include <cstring>
+#include <list>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -15,6 +18,7 @@
 #include "ORBmatcher.h"
 #include "Objects.h"
 #include "Optimizer.h"
+#include "PnPsolver.h"
 #include "orbx.h"
 
 static_assert(sizeof(cv::KeyPoint) == sizeof(orbx_keypoint), "cv::KeyPoint layout");
@@ -84,6 +88,8 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray, std::vector
 }
 
 // ------------------------------------------------------------------ Frame (stereo ORB part)
+float Frame::fx = 0.f, Frame::fy = 0.f, Frame::cx = 0.f, Frame::cy = 0.f, Frame::invfx = 0.f, Frame::invfy = 0.f;
+
 Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extractorLeft,
              ORBextractor* extractorRight, const cv::Mat& K, const cv::Mat& distCoef, float bf, float thDepth)
     : mpORBextractorLeft(extractorLeft), mpORBextractorRight(extractorRight), mbf(bf), mThDepth(thDepth) {
@@ -102,8 +108,21 @@ Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extrac
   if (errL) std::rethrow_exception(errL);
   if (errR) std::rethrow_exception(errR);
   N = (int)mvKeys.size();
+  // scale tables (src/Frame.cc:66-73) and the static intrinsics (:111-126)
+  mnScaleLevels = mpORBextractorLeft->GetLevels();
+  mfScaleFactor = mpORBextractorLeft->GetScaleFactor();
+  mvScaleFactors = mpORBextractorLeft->GetScaleFactors();
+  mvInvScaleFactors = mpORBextractorLeft->GetInverseScaleFactors();
+  mvLevelSigma2 = mpORBextractorLeft->GetScaleSigmaSquares();
+  mvInvLevelSigma2 = mpORBextractorLeft->GetInverseScaleSigmaSquares();
+  fx = mK.at<float>(0, 0);
+  fy = mK.at<float>(1, 1);
+  cx = mK.at<float>(0, 2);
+  cy = mK.at<float>(1, 2);
+  invfx = 1.0f / fx;
+  invfy = 1.0f / fy;
   if (mvKeys.empty()) return;
-  mb = mbf / mK.at<float>(0, 0);  // :133-134
+  mb = mbf / fx;  // :133-134
   UndistortKeyPoints();
   ComputeStereoMatches();
   mvpMapPoints.assign(N, nullptr);
@@ -241,7 +260,202 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint
   return n;
 }
 
+// ------------------------------------------------------------------ PnPsolver
+int PnPsolver::mnDevice = 0;
+
+namespace {
+// the process-wide stream DUtils::Random::RandomInt draws from (glibc rand(), seed 1)
+std::mutex g_rand_mu;
+orbx_rand_state g_rand = [] {
+  orbx_rand_state s;
+  orbx_rand_seed(&s, 1);
+  return s;
+}();
+}  // namespace
+
+void PnPsolver::SeedRandom(unsigned int seed) {
+  std::lock_guard<std::mutex> lock(g_rand_mu);
+  orbx_rand_seed(&g_rand, seed);
+}
+
+PnPsolver::PnPsolver(const Frame& F, const std::vector<MapPoint*>& vpMapPointMatches)
+    : mvpMapPointMatches(vpMapPointMatches) {
+  // src/PnPsolver.cc:67-125: one correspondence per matched, non-bad MapPoint, in feature order
+  for (size_t i = 0; i < vpMapPointMatches.size(); i++) {
+    MapPoint* pMP = vpMapPointMatches[i];
+    if (!pMP || pMP->isBad()) continue;
+    const cv::KeyPoint& kp = F.mvKeysUn[i];
+    mvP2D.push_back(kp.pt.x);
+    mvP2D.push_back(kp.pt.y);
+    mvSigma2.push_back(F.mvLevelSigma2[kp.octave]);
+    const cv::Mat Pos = pMP->GetWorldPos();
+    for (int k = 0; k < 3; k++) mvP3Dw.push_back(Pos.at<float>(k, 0));
+    mvKeyPointIndices.push_back(i);
+  }
+  fu = F.fx;
+  fv = F.fy;
+  uc = F.cx;
+  vc = F.cy;
+  SetRansacParameters();
+}
+
+PnPsolver::~PnPsolver() {
+  if (mpGpu) orbx_pnp_destroy(mpGpu);
+}
+
+void PnPsolver::SetRansacParameters(double probability, int minInliers, int maxIterations, int minSet, float epsilon,
+                                    float th2) {
+  if (mbStarted) throw std::logic_error("PnPsolver::SetRansacParameters after iterate()");
+  mParams = orbx_pnp_params{probability, minInliers, maxIterations, minSet, epsilon, th2};
+  if (mpGpu) {
+    orbx_pnp_destroy(mpGpu);
+    mpGpu = nullptr;
+  }
+}
+
+void PnPsolver::ensure_solver() {
+  if (mpGpu) return;
+  const int n = (int)mvSigma2.size();
+  const orbx_pnp_problem prob{n, n ? mvP3Dw.data() : nullptr, n ? mvP2D.data() : nullptr,
+                              n ? mvSigma2.data() : nullptr, fu, fv, uc, vc};
+  check(orbx_pnp_create(&prob, &mParams, mnDevice, &mpGpu), "orbx_pnp_create");
+  int mi = 0;
+  float eps = 0;
+  check(orbx_pnp_get_params(mpGpu, &mi, &mRansacMaxIts, &eps), "orbx_pnp_get_params");
+}
+
+cv::Mat PnPsolver::find(std::vector<bool>& vbInliers, int& nInliers) {
+  ensure_solver();
+  bool bFlag;
+  return iterate(mRansacMaxIts, bFlag, vbInliers, nInliers);  // src/PnPsolver.cc:181-185
+}
+
+cv::Mat PnPsolver::iterate(int nIterations, bool& bNoMore, std::vector<bool>& vbInliers, int& nInliers) {
+  ensure_solver();
+  mbStarted = true;
+  bNoMore = false;
+  vbInliers.clear();
+  nInliers = 0;
+  const int n = (int)mvSigma2.size();
+  std::vector<uint8_t> inl(n > 0 ? n : 1, 0);
+  float T[16];
+  int no_more = 0, ni = 0, found = 0;
+  {
+    std::lock_guard<std::mutex> lock(g_rand_mu);
+    check(orbx_pnp_iterate_stream(mpGpu, nIterations, &g_rand, &no_more, T, inl.data(), &ni, &found),
+          "orbx_pnp_iterate_stream");
+  }
+  bNoMore = no_more != 0;
+  if (!found) return cv::Mat();
+  nInliers = ni;
+  vbInliers.assign(mvpMapPointMatches.size(), false);  // :261-266 / :283-288
+  for (int i = 0; i < n; i++)
+    if (inl[i]) vbInliers[mvKeyPointIndices[i]] = true;
+  cv::Mat Tcw(4, 4, CV_32F);
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) Tcw.at<float>(r, c) = T[4 * r + c];
+  return Tcw;
+}
+
 // ------------------------------------------------------------------ Optimizer
+int Optimizer::mnDevice = 0;
+void (*Optimizer::mpfnGatheredHook)(const LocalBAProblem&, const std::vector<KeyFrame*>&) = nullptr;
+
+void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap) {
+  // src/Optimizer.cc:532-551: the local KeyFrames (pKF and its non-bad covisibles)
+  std::list<KeyFrame*> lLocalKeyFrames;
+  lLocalKeyFrames.push_back(pKF);
+  pKF->mnBALocalForKF = pKF->mnId;
+  const std::vector<KeyFrame*> vNeighKFs = pKF->GetVectorCovisibleKeyFrames();
+  for (KeyFrame* pKFi : vNeighKFs) {
+    pKFi->mnBALocalForKF = pKF->mnId;
+    if (!pKFi->isBad()) lLocalKeyFrames.push_back(pKFi);
+  }
+  // :553-572: the local MapPoints, first seen first
+  std::list<MapPoint*> lLocalMapPoints;
+  for (KeyFrame* pKFl : lLocalKeyFrames) {
+    const std::vector<MapPoint*> vpMPs = pKFl->GetMapPointMatches();
+    for (MapPoint* pMP : vpMPs)
+      if (pMP && !pMP->isBad() && pMP->mnBALocalForKF != pKF->mnId) {
+        lLocalMapPoints.push_back(pMP);
+        pMP->mnBALocalForKF = pKF->mnId;
+      }
+  }
+  // :574-592: KeyFrames that observe local MapPoints but are not local -> fixed
+  std::list<KeyFrame*> lFixedCameras;
+  for (MapPoint* pMP : lLocalMapPoints) {
+    const std::map<KeyFrame*, size_t> observations = pMP->GetObservations();
+    for (const auto& ob : observations) {
+      KeyFrame* pKFi = ob.first;
+      if (pKFi->mnBALocalForKF != pKF->mnId && pKFi->mnBAFixedForKF != pKF->mnId) {
+        pKFi->mnBAFixedForKF = pKF->mnId;
+        if (!pKFi->isBad()) lFixedCameras.push_back(pKFi);
+      }
+    }
+  }
+  // :608-640: vertices -- local poses (fixed iff mnId == 0), then the fixed cameras
+  LocalBAProblem P;
+  std::vector<KeyFrame*> cams;
+  std::map<KeyFrame*, int> cam_index;
+  auto add_cam = [&](KeyFrame* pKFi, bool fixed) {
+    cam_index[pKFi] = (int)cams.size();
+    cams.push_back(pKFi);
+    LocalBAProblem::Camera C;
+    C.Tcw = pKFi->GetPose();
+    C.fixed = fixed;
+    C.fx = pKFi->fx;
+    C.fy = pKFi->fy;
+    C.cx = pKFi->cx;
+    C.cy = pKFi->cy;
+    C.bf = pKFi->mbf;
+    P.cameras.push_back(C);
+  };
+  for (KeyFrame* pKFi : lLocalKeyFrames) add_cam(pKFi, pKFi->mnId == 0);
+  for (KeyFrame* pKFi : lFixedCameras) add_cam(pKFi, true);
+  // :656-745: one point vertex per local MapPoint, one edge per observation by a non-bad KeyFrame
+  // (GetObservations() order), monocular when mvuRight < 0
+  std::vector<MapPoint*> points(lLocalMapPoints.begin(), lLocalMapPoints.end());
+  std::vector<std::pair<KeyFrame*, MapPoint*>> edge_obj;
+  for (size_t p = 0; p < points.size(); p++) {
+    MapPoint* pMP = points[p];
+    P.points.push_back(pMP->GetWorldPos());
+    const std::map<KeyFrame*, size_t> observations = pMP->GetObservations();
+    for (const auto& ob : observations) {
+      KeyFrame* pKFi = ob.first;
+      if (pKFi->isBad()) continue;
+      const cv::KeyPoint& kpUn = pKFi->mvKeysUn[ob.second];
+      LocalBAProblem::Observation o;
+      o.point = (int)p;
+      o.camera = cam_index.at(pKFi);
+      o.u = kpUn.pt.x;
+      o.v = kpUn.pt.y;
+      o.ur = pKFi->mvuRight[ob.second];
+      o.invSigma2 = pKFi->mvInvLevelSigma2[kpUn.octave];
+      P.observations.push_back(o);
+      edge_obj.emplace_back(pKFi, pMP);
+    }
+  }
+  if (mpfnGatheredHook) mpfnGatheredHook(P, cams);
+  // :747-751: a stop requested before the optimisation leaves the map untouched
+  if (pbStopFlag && *pbStopFlag) return;
+  LocalBAResult R;
+  LocalBundleAdjustment(P, pbStopFlag, R, mnDevice);
+  // :803-847 vToErase (the library's per-edge verdict after the last phase), then :849-884
+  std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);
+  for (size_t e = 0; e < edge_obj.size(); e++) {
+    if (!R.erase[e]) continue;
+    KeyFrame* pKFi = edge_obj[e].first;
+    MapPoint* pMPi = edge_obj[e].second;
+    pKFi->EraseMapPointMatch(pMPi);
+    pMPi->EraseObservation(pKFi);
+  }
+  for (KeyFrame* pKFl : lLocalKeyFrames) pKFl->SetPose(R.Tcw[cam_index.at(pKFl)]);
+  for (size_t p = 0; p < points.size(); p++) {
+    points[p]->SetWorldPos(R.points[p]);
+    points[p]->UpdateNormalAndDepth();
+  }
+}
+
 void Optimizer::LocalBundleAdjustment(const LocalBAProblem& P, bool* pbStopFlag, LocalBAResult& R, int device) {
   const int nc = (int)P.cameras.size(), np = (int)P.points.size(), ne = (int)P.observations.size();
   std::vector<float> Tcw(12 * (size_t)nc), intr(5 * (size_t)nc), Xw(3 * (size_t)np), obs(3 * (size_t)ne),

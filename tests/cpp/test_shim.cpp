@@ -5,6 +5,9 @@
 //   stereo  IN OUT      Frame stereo ctor (two extraction threads + ComputeStereoMatches)
 //   bow     IN OUT      ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) / (KeyFrame*, KeyFrame*, ...)
 //   ba      IN OUT      Optimizer::LocalBundleAdjustment on an explicit problem
+//   bagraph IN OUT      Optimizer::LocalBundleAdjustment(KeyFrame*, bool*, Map*) on an object graph
+//   pnp     IN OUT      PnPsolver(Frame, matches) + SetRansacParameters + iterate(5) in
+//                       Tracking::Relocalization's candidate loop
 // IN/OUT are little-endian binary files written/read by tests/test_shim.py, which compares the
 // outputs with the CPU oracle.  Exit status 0 = ok.
 #include <cassert>
@@ -12,6 +15,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <list>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -21,6 +26,7 @@
 #include "ORBmatcher.h"
 #include "Objects.h"
 #include "Optimizer.h"
+#include "PnPsolver.h"
 #include "orbx.h"
 
 using namespace ORB_SLAM2;
@@ -108,6 +114,20 @@ static int mode_abi() {
     std::vector<MapPoint*> m;
     ORBmatcher matcher(0.75f, true);
     REQUIRE(throws_runtime([&] { matcher.SearchByBoW(&kf, F, m); }));
+    // PnPsolver: gathering needs no device, iterate() does
+    PnPsolver solver(F, m);
+    bool bNoMore = false;
+    std::vector<bool> inl;
+    int ni = 0;
+    REQUIRE(throws_runtime([&] { solver.iterate(5, bNoMore, inl, ni); }));
+    // the reference-signature LocalBA gathers from the graph, then needs the device
+    Map map;
+    KeyFrame k1;
+    cv::Mat I4(4, 4, CV_32F);
+    std::memset(I4.data, 0, 64);
+    for (int i = 0; i < 4; i++) I4.at<float>(i, i) = 1.f;
+    k1.SetPose(I4);
+    REQUIRE(throws_runtime([&] { Optimizer::LocalBundleAdjustment(&k1, nullptr, &map); }));
     std::printf("abi ok (no device: GPU members throw)\n");
   } else {
     std::printf("abi ok (device present)\n");
@@ -123,6 +143,8 @@ static int mode_stereo(const char* in, const char* out) {
   const float bf = r.get<float>(), fx = r.get<float>();
   std::vector<uint8_t> L = r.vec<uint8_t>((size_t)w * h), R = r.vec<uint8_t>((size_t)w * h);
   ORBextractor exL(nf, sf, nl, ini, mn), exR(nf, sf, nl, ini, mn);
+  REQUIRE(!exL.mbDownloadPyramid);  // off by default: the stereo matcher reads the device copy
+  exL.mbDownloadPyramid = true;     // this test also checks the host copy
   cv::Mat imL(h, w, CV_8U, L.data()), imR(h, w, CV_8U, R.data());
   cv::Mat K(3, 3, CV_32F), dist(4, 1, CV_32F);
   std::memset(K.data, 0, 36);
@@ -305,9 +327,270 @@ static int mode_ba(const char* in, const char* out) {
   return 0;
 }
 
+// ---------------------------------------------------------------- LocalBA on an object graph
+// Input: the synthetic problem (cameras, points, edges grouped by point) with per-edge octaves into
+// a level table.  The graph: one KeyFrame per camera (addresses ascending, so GetObservations()
+// walks cameras in index order), local KeyFrames = the non-fixed cameras (pKF = the first) plus
+// fixed camera 0 as a covisible KeyFrame with mnId 0 (a local vertex fixed by the mnId == 0 rule);
+// the other fixed cameras are reached only through the points' observations (lFixedCameras).
+// Distractors the gather must skip: a bad covisible KeyFrame that observes the first points, a bad
+// MapPoint and empty feature slots in every KeyFrame.
+static LocalBAProblem g_gathered;
+static std::vector<KeyFrame*> g_gathered_cams;
+static void gathered_hook(const LocalBAProblem& P, const std::vector<KeyFrame*>& cams) {
+  g_gathered = P;
+  g_gathered_cams = cams;
+}
+
+static int mode_bagraph(const char* in, const char* out) {
+  Reader r(in);
+  const int nc = r.get<int32_t>(), np = r.get<int32_t>(), ne = r.get<int32_t>(), nl = r.get<int32_t>();
+  const std::vector<float> T = r.vec<float>(12 * (size_t)nc);
+  const std::vector<uint8_t> fixed = r.vec<uint8_t>(nc);
+  const std::vector<float> intr = r.vec<float>(5 * (size_t)nc), X = r.vec<float>(3 * (size_t)np);
+  const std::vector<int32_t> ep = r.vec<int32_t>(ne), ec = r.vec<int32_t>(ne);
+  const std::vector<float> obs = r.vec<float>(3 * (size_t)ne);
+  const std::vector<float> levels = r.vec<float>(nl);
+  const std::vector<int32_t> octave = r.vec<int32_t>(ne);
+  const int stop = r.get<int32_t>();
+  Map map;
+  std::vector<KeyFrame> kfs(nc + 1);  // + the bad covisible KeyFrame
+  std::vector<MapPoint> mps(np + 1);  // + a bad MapPoint
+  std::vector<int> nfeat(nc + 1, 0);
+  for (int e = 0; e < ne; e++) nfeat[ec[e]]++;
+  int first_fixed = -1;
+  for (int c = 0; c < nc; c++)
+    if (fixed[c] && first_fixed < 0) first_fixed = c;
+  for (int c = 0; c <= nc; c++) {
+    KeyFrame& K = kfs[c];
+    const int cc = c < nc ? c : 0;
+    K.mnId = (c == first_fixed) ? 0 : (unsigned long)(c + 1);
+    K.fx = intr[5 * cc];
+    K.fy = intr[5 * cc + 1];
+    K.cx = intr[5 * cc + 2];
+    K.cy = intr[5 * cc + 3];
+    K.mbf = intr[5 * cc + 4];
+    K.mnScaleLevels = 8;
+    for (int l = 0; l < 8; l++) K.mvScaleFactors.push_back(std::pow(1.2f, (float)l));
+    K.mvInvLevelSigma2 = levels;
+    cv::Mat Tc(4, 4, CV_32F);
+    for (int i = 0; i < 12; i++) Tc.at<float>(i / 4, i % 4) = T[12 * cc + i];
+    Tc.at<float>(3, 0) = Tc.at<float>(3, 1) = Tc.at<float>(3, 2) = 0.f;
+    Tc.at<float>(3, 3) = 1.f;
+    K.SetPose(Tc);
+    const int nf = nfeat[c] + 10 + (c == 0 ? 1 : 0) + (c == nc ? 50 : 0);
+    K.N = nf;
+    K.mvKeysUn.resize(nf);
+    K.mvuRight.assign(nf, -1.f);
+    K.mvpMapPoints.assign(nf, nullptr);
+  }
+  kfs[nc].mbBad = true;
+  for (int p = 0; p < np; p++) {
+    cv::Mat Xp(3, 1, CV_32F);
+    for (int k = 0; k < 3; k++) Xp.at<float>(k, 0) = X[3 * p + k];
+    mps[p].SetWorldPos(Xp);
+    mps[p].mnId = (unsigned long)(p + 1);
+    mps[p].mpMap = &map;
+    map.mspMapPoints.insert(&mps[p]);
+  }
+  std::vector<int> slot(nc + 1, 0);
+  std::vector<int> edge_slot(ne);
+  for (int e = 0; e < ne; e++) {
+    KeyFrame& K = kfs[ec[e]];
+    const int idx = slot[ec[e]]++;
+    edge_slot[e] = idx;
+    K.mvKeysUn[idx] = cv::KeyPoint(obs[3 * e], obs[3 * e + 1], 31.f, -1.f, 0.f, octave[e]);
+    K.mvuRight[idx] = obs[3 * e + 2];
+    K.mvpMapPoints[idx] = &mps[ep[e]];
+    mps[ep[e]].AddObservation(&K, idx);
+    if (!mps[ep[e]].mpRefKF) mps[ep[e]].mpRefKF = &K;
+  }
+  // the bad KeyFrame observes the first 50 points (monocular): its edges must not enter the window
+  KeyFrame& Kb = kfs[nc];
+  for (int p = 0; p < 50 && p < np; p++) {
+    const int idx = slot[nc]++;
+    Kb.mvKeysUn[idx] = cv::KeyPoint(100.f, 100.f, 31.f, -1.f, 0.f, 0);
+    Kb.mvpMapPoints[idx] = &mps[p];
+    mps[p].AddObservation(&Kb, idx);
+  }
+  // a bad MapPoint in pKF's matches
+  mps[np].mbBad = true;
+  int local0 = -1;
+  for (int c = 0; c < nc; c++)
+    if (!fixed[c]) {
+      local0 = c;
+      break;
+    }
+  REQUIRE(local0 >= 0);
+  KeyFrame* pKF = &kfs[local0];
+  pKF->mvpMapPoints[slot[local0]] = &mps[np];
+  for (int c = 0; c < nc; c++)
+    if (c != local0 && !fixed[c]) pKF->mvpOrderedConnectedKeyFrames.push_back(&kfs[c]);
+  pKF->mvpOrderedConnectedKeyFrames.push_back(&kfs[nc]);
+  if (first_fixed >= 0) pKF->mvpOrderedConnectedKeyFrames.push_back(&kfs[first_fixed]);
+  std::vector<int> nobs0(np);
+  for (int p = 0; p < np; p++) nobs0[p] = mps[p].Observations();
+  Optimizer::mpfnGatheredHook = gathered_hook;
+  bool bStop = stop != 0;
+  Optimizer::LocalBundleAdjustment(pKF, &bStop, &map);
+  Optimizer::mpfnGatheredHook = nullptr;
+  // output: the gathered window (as orbx_ba_problem arrays), then the graph after the call
+  const LocalBAProblem& G = g_gathered;
+  const int gnc = (int)G.cameras.size(), gnp = (int)G.points.size(), gne = (int)G.observations.size();
+  Writer o(out);
+  o.put<int32_t>(gnc);
+  o.put<int32_t>(gnp);
+  o.put<int32_t>(gne);
+  for (int c = 0; c < gnc; c++)
+    for (int i = 0; i < 12; i++) o.put<float>(G.cameras[c].Tcw.at<float>(i / 4, i % 4));
+  for (int c = 0; c < gnc; c++) o.put<uint8_t>(G.cameras[c].fixed ? 1 : 0);
+  for (int c = 0; c < gnc; c++) {
+    const float in5[5] = {G.cameras[c].fx, G.cameras[c].fy, G.cameras[c].cx, G.cameras[c].cy, G.cameras[c].bf};
+    o.raw(in5, sizeof(in5));
+  }
+  for (int p = 0; p < gnp; p++)
+    for (int k = 0; k < 3; k++) o.put<float>(G.points[p].at<float>(k, 0));
+  for (int e = 0; e < gne; e++) o.put<int32_t>(G.observations[e].point);
+  for (int e = 0; e < gne; e++) o.put<int32_t>(G.observations[e].camera);
+  for (int e = 0; e < gne; e++) {
+    o.put<float>(G.observations[e].u);
+    o.put<float>(G.observations[e].v);
+    o.put<float>(G.observations[e].ur);
+  }
+  for (int e = 0; e < gne; e++) o.put<float>(G.observations[e].invSigma2);
+  // camera -> input index, point -> input index (the Python side maps the oracle's answer back)
+  for (int c = 0; c < gnc; c++) o.put<int32_t>((int32_t)(g_gathered_cams[c] - kfs.data()));
+  // poses after the call (all KeyFrames, gathered order), points (gathered order by id), edge state
+  for (int c = 0; c < gnc; c++) {
+    const cv::Mat Tc = g_gathered_cams[c]->GetPose();
+    for (int i = 0; i < 12; i++) o.put<float>(Tc.at<float>(i / 4, i % 4));
+  }
+  for (int p = 0; p < np; p++) {
+    const cv::Mat Xp = mps[p].GetWorldPos();
+    for (int k = 0; k < 3; k++) o.put<float>(Xp.at<float>(k, 0));
+  }
+  for (int p = 0; p < np; p++) o.put<uint8_t>(mps[p].isBad() ? 1 : 0);
+  for (int p = 0; p < np; p++) o.put<int32_t>(nobs0[p]);
+  for (int e = 0; e < ne; e++) {  // per INPUT edge: observation and KeyFrame match still present
+    const int pidx = mps[ep[e]].GetIndexInKeyFrame(&kfs[ec[e]]);
+    const bool kf_has = kfs[ec[e]].mvpMapPoints[edge_slot[e]] == &mps[ep[e]];
+    o.put<uint8_t>(pidx == edge_slot[e] ? 1 : 0);
+    o.put<uint8_t>(kf_has ? 1 : 0);
+  }
+  std::printf("bagraph ok: window %d cams / %d points / %d edges\n", gnc, gnp, gne);
+  return 0;
+}
+
+// ---------------------------------------------------------------- PnPsolver in Relocalization's loop
+// Input: C candidates, each with n correspondences (p3d, p2d, octave into its level table) and
+// intrinsics.  Every candidate's Frame interleaves features without a MapPoint and features whose
+// MapPoint is bad (the gather skips both), so vbInliers must come back in feature indices.
+static int mode_pnp(const char* in, const char* out) {
+  Reader r(in);
+  const int C = r.get<int32_t>();
+  const double prob = r.get<double>();
+  const int minInl = r.get<int32_t>(), maxIt = r.get<int32_t>(), minSet = r.get<int32_t>();
+  const float eps = r.get<float>(), th2 = r.get<float>();
+  const int max_rounds = r.get<int32_t>();
+  struct Cand {
+    Frame F;
+    std::unique_ptr<MapPoint[]> mps;
+    std::vector<int> feat_of;  // correspondence -> feature index
+    std::unique_ptr<PnPsolver> solver;
+  };
+  std::vector<std::unique_ptr<Cand>> cs;
+  for (int c = 0; c < C; c++) {
+    std::unique_ptr<Cand> cd(new Cand());
+    const int n = r.get<int32_t>();
+    const float fx = r.get<float>(), fy = r.get<float>(), cx = r.get<float>(), cy = r.get<float>();
+    const int nl = r.get<int32_t>();
+    const std::vector<float> levels = r.vec<float>(nl);
+    const std::vector<float> p3 = r.vec<float>(3 * (size_t)n), p2 = r.vec<float>(2 * (size_t)n);
+    const std::vector<int32_t> oc = r.vec<int32_t>(n);
+    Frame& F = cd->F;
+    F.mvLevelSigma2 = levels;
+    cd->mps.reset(new MapPoint[n + n / 5 + 1]);
+    int bad = n;
+    std::vector<MapPoint*> matches;
+    for (int i = 0; i < n; i++) {
+      if (i % 3 == 0) {  // a feature without a MapPoint
+        F.mvKeysUn.push_back(cv::KeyPoint(1.f, 1.f, 31.f));
+        matches.push_back(nullptr);
+      }
+      if (i % 5 == 0) {  // a feature whose MapPoint is bad
+        MapPoint& b = cd->mps[bad++];
+        b.mbBad = true;
+        F.mvKeysUn.push_back(cv::KeyPoint(2.f, 2.f, 31.f));
+        matches.push_back(&b);
+      }
+      MapPoint& m = cd->mps[i];
+      cv::Mat Xp(3, 1, CV_32F);
+      for (int k = 0; k < 3; k++) Xp.at<float>(k, 0) = p3[3 * i + k];
+      m.SetWorldPos(Xp);
+      cd->feat_of.push_back((int)F.mvKeysUn.size());
+      F.mvKeysUn.push_back(cv::KeyPoint(p2[2 * i], p2[2 * i + 1], 31.f, -1.f, 0.f, oc[i]));
+      matches.push_back(&m);
+    }
+    F.N = (int)F.mvKeysUn.size();
+    Frame::fx = fx;  // static, as in the reference (one camera)
+    Frame::fy = fy;
+    Frame::cx = cx;
+    Frame::cy = cy;
+    cd->solver.reset(new PnPsolver(F, matches));
+    cd->solver->SetRansacParameters(prob, minInl, maxIt, minSet, eps, th2);  // src/Tracking.cc:1720
+    cs.push_back(std::move(cd));
+  }
+  // src/Tracking.cc:1738-1757 (a returned pose counts as the match)
+  Writer o(out);
+  std::vector<bool> discarded(C, false);
+  int ncand = C;
+  bool match = false;
+  int calls = 0;
+  for (int round = 0; round < max_rounds && ncand > 0 && !match; round++) {
+    for (int i = 0; i < C; i++) {
+      if (discarded[i]) continue;
+      bool bNoMore = false;
+      std::vector<bool> vbInliers;
+      int nInliers = 0;
+      const cv::Mat Tcw = cs[i]->solver->iterate(5, bNoMore, vbInliers, nInliers);
+      calls++;
+      o.put<int32_t>(i);
+      o.put<int32_t>(Tcw.empty() ? 0 : 1);
+      o.put<int32_t>(bNoMore ? 1 : 0);
+      o.put<int32_t>(nInliers);
+      for (int k = 0; k < 16; k++) o.put<float>(Tcw.empty() ? 0.f : Tcw.at<float>(k / 4, k % 4));
+      const int n = (int)cs[i]->feat_of.size();
+      REQUIRE(Tcw.empty() || (int)vbInliers.size() == cs[i]->F.N);
+      for (int k = 0; k < n; k++) o.put<uint8_t>(!Tcw.empty() && vbInliers[cs[i]->feat_of[k]] ? 1 : 0);
+      if (!Tcw.empty()) {  // features without a correspondence are never inliers
+        int cnt = 0;
+        for (bool b : vbInliers) cnt += b;
+        REQUIRE(cnt == nInliers);
+      }
+      if (bNoMore) {
+        discarded[i] = true;
+        ncand--;
+      }
+      if (!Tcw.empty()) {
+        match = true;
+        break;
+      }
+    }
+  }
+  bool threw = false;  // parameters are fixed once RANSAC has started
+  try {
+    cs[0]->solver->SetRansacParameters();
+  } catch (const std::logic_error&) {
+    threw = true;
+  }
+  REQUIRE(threw);
+  std::printf("pnp ok: %d iterate() calls, match %d\n", calls, (int)match);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::fprintf(stderr, "usage: test_shim abi | stereo IN OUT | bow IN OUT | ba IN OUT\n");
+    std::fprintf(stderr, "usage: test_shim abi | stereo IN OUT | bow IN OUT | ba IN OUT | bagraph IN OUT | pnp IN OUT\n");
     return 2;
   }
   const std::string m = argv[1];
@@ -317,6 +600,8 @@ int main(int argc, char** argv) {
     if (m == "stereo") return mode_stereo(argv[2], argv[3]);
     if (m == "bow") return mode_bow(argv[2], argv[3]);
     if (m == "ba") return mode_ba(argv[2], argv[3]);
+    if (m == "bagraph") return mode_bagraph(argv[2], argv[3]);
+    if (m == "pnp") return mode_pnp(argv[2], argv[3]);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 3;

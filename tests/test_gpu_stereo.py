@@ -28,6 +28,34 @@ def test_stereo_bitexact(gpu, seed, w, h, nf, bf, fx):
     assert np.array_equal(dep.view(np.uint32), odep.view(np.uint32))
 
 
+def test_stereo_uses_only_the_last_extraction(gpu):
+    """orbx_stereo_match reads each extractor's device-resident keypoints, descriptors and pyramid
+    (no upload), so it accepts only exactly what that extractor's last orbx_extract returned:
+    a changed descriptor bit, a changed keypoint, or a newer extraction on the right handle is
+    ORBX_ERR_STATE; repeating the call on the true outputs is bit-identical."""
+    from orb_slam2_commit_amd._lib import ORBX_ERR_STATE, OrbxError
+    L, R = synth.stereo_pair(5, 1241, 376)
+    exL, exR = ORBextractor(2000, 1.2, 8, 20, 7), ORBextractor(2000, 1.2, 8, 20, 7)
+    kL, dL = exL(L)
+    kR, dR = exR(R)
+    bl = KITTI_BF / KITTI_FX
+    uR1, d1 = compute_stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, bl)
+    uR2, d2 = compute_stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, bl)
+    assert np.array_equal(uR1.view(np.uint32), uR2.view(np.uint32)) and np.array_equal(d1, d2)
+    dbad = dL.copy()
+    dbad[7, 3] ^= 1
+    kbad = kL.copy()
+    kbad["x"][0] += 0.5
+    for args in [(kL, dbad, kR, dR), (kbad, dL, kR, dR), (kL, dL, kR, dR[::-1].copy())]:
+        with pytest.raises(OrbxError) as ei:
+            compute_stereo_matches(exL, exR, *args, KITTI_BF, bl)
+        assert ei.value.code == ORBX_ERR_STATE
+    exR(synth.stereo_pair(6, 1241, 376)[1])  # a newer extraction on the right handle
+    with pytest.raises(OrbxError) as ei:
+        compute_stereo_matches(exL, exR, kL, dL, kR, dR, KITTI_BF, bl)
+    assert ei.value.code == ORBX_ERR_STATE
+
+
 def test_stereo_frames_device(gpu):
     import torch
     n = 3

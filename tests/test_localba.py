@@ -361,20 +361,84 @@ def test_gpu_localba_device_lm_bit_identical(ba, case, monkeypatch):
 
 @pytest.mark.gpu
 def test_gpu_localba_stop_flag_mid_run(ba):
-    """A stop flag raised by another thread while the device runs the LM loop ends the
-    optimisation early (the device polls the host-mapped flag), with finite outputs."""
+    """A stop flag (caller memory, not the handle's pinned flag) raised by another thread while
+    the device runs the LM loop ends the optimisation early: the calling thread mirrors it into
+    the handle's pinned flag while it waits, and the device polls that.  The raise comes after
+    15 % of a full call's own measured duration, so the margin scales with the machine."""
     import threading
     import time
     P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
+    ba.LocalBundleAdjustment(P)
+    t0 = time.perf_counter()
     full = ba.LocalBundleAdjustment(P)
+    delay = 0.15 * (time.perf_counter() - t0)
     flag = np.zeros(1, np.int32)
-    t = threading.Thread(target=lambda: (time.sleep(0.002), flag.__setitem__(0, 1)))
+    t = threading.Thread(target=lambda: (time.sleep(delay), flag.__setitem__(0, 1)))
     t.start()
     r = ba.LocalBundleAdjustment(P, stop=flag)
     t.join()
     assert flag[0] == 1
     assert sum(r["iterations"]) < sum(full["iterations"])
     assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("after", [0, 2, 4])  # inside the first phase (optimize(5))
+def test_gpu_localba_stop_raised_after_trials(ba, after, monkeypatch):
+    """Deterministic mid-run stop: ORBX_BA_RAISE_STOP_AFTER=n makes the device LM control see a
+    raised flag from trial n of the first phase on (as a flag raised by LocalMapping::InterruptBA
+    between two trials).  The phase ends at that iteration, the second phase is skipped, and the
+    result is the same bit for bit on every run and through the batched driver."""
+    P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
+    full = ba.LocalBundleAdjustment(P)
+    monkeypatch.setenv("ORBX_BA_RAISE_STOP_AFTER", str(after))
+    r = ba.LocalBundleAdjustment(P)
+    r2 = ba.LocalBundleAdjustment(P)
+    many = ba.LocalBundleAdjustmentMany([P, P])
+    assert r["iterations"][1] == 0 and 1 <= r["iterations"][0] <= after + 1
+    assert r["trials"] >= after + 1 and sum(r["iterations"]) < sum(full["iterations"])
+    for o in (r2, many[0], many[1]):
+        for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+            np.testing.assert_array_equal(np.asarray(r[k]), np.asarray(o[k]))
+        assert list(o["iterations"]) == list(r["iterations"]) and o["trials"] == r["trials"]
+    assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
+
+
+@pytest.mark.parametrize("trial", [0, 1, 3])
+def test_oracle_nan_trial_refresh(trial, monkeypatch):
+    """The oracle's NaN-trial hook (ORBX_BA_NAN_TRIAL): a rejected trial with rho NaN ends its
+    iteration and the next iteration starts from the popped state with recomputed errors
+    (g2o's computeActiveErrors at every iteration start); the history changes, outputs stay finite."""
+    P = synth.localba_problem(seed=7)
+    clean = oracle.local_ba(P)
+    monkeypatch.setenv("ORBX_BA_NAN_TRIAL", str(trial))
+    r = oracle.local_ba(P)
+    assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
+    changed = (r["trials"] != clean["trials"] or list(r["iterations"]) != list(clean["iterations"])
+               or not np.array_equal(r["Tcw_d"], clean["Tcw_d"]))
+    assert changed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,trial", [("config4", 0), ("config4", 1), ("config4", 3), ("rejects_b", 2)])
+def test_gpu_localba_nan_trial(ba, case, trial, monkeypatch):
+    """A trial whose chi is NaN (ORBX_BA_NAN_TRIAL) is rejected and, with rho NaN, ends its
+    iteration while the phase goes on: g2o pops it and the next iteration recomputes the errors
+    at the restored state before linearising.  The device LM loop pauses the phase for exactly
+    that (restore, errors, k_ba_lm_resume): GPU = oracle (1e-4, identical counts and outliers),
+    device loop = host loop (ORBX_BA_HOST_LM=1) bit for bit, batched = single bit for bit."""
+    P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(case)
+    monkeypatch.setenv("ORBX_BA_NAN_TRIAL", str(trial))
+    a = ba.LocalBundleAdjustment(P)
+    _compare(a, oracle.local_ba(P))
+    many = ba.LocalBundleAdjustmentMany([P, small_problem(seed=12)])
+    monkeypatch.setenv("ORBX_BA_HOST_LM", "1")
+    b = ba.LocalBundleAdjustment(P)
+    for o in (b, many[0]):
+        for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(o[k]))
+        assert list(a["iterations"]) == list(o["iterations"]) and a["trials"] == o["trials"]
+        assert a["chi2"] == o["chi2"]
 
 
 @pytest.mark.gpu
@@ -419,9 +483,11 @@ def test_gpu_localba_batched_fallback_and_stop(ba):
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
         assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
     probs = [synth.localba_problem(seed=8 + k, n_local=30, n_fixed=4, n_points=4000) for k in range(4)]
+    t0 = time.perf_counter()
     full = ba.LocalBundleAdjustmentMany(probs)
+    delay = 0.15 * (time.perf_counter() - t0)  # margin scaled by the call's own duration
     flag = ba._stop
-    t = threading.Thread(target=lambda: (time.sleep(0.003), flag.__setitem__(0, 1)))
+    t = threading.Thread(target=lambda: (time.sleep(delay), flag.__setitem__(0, 1)))
     t.start()
     # the wrapper writes the handle flag (0) before the call; the thread raises it mid-run
     rs = ba.LocalBundleAdjustmentMany(probs)

@@ -99,6 +99,64 @@ def test_gloo_world2_gathered_records_equal_single_process():
     assert s["iterations"] == tuple(oracle.local_ba(P[1])["iterations"])
 
 
+def _ragged_worker(rank, world, port, q):
+    """Ranks with different image sizes (KITTI 00 1241x376 vs 04 1226x370, scaled down) and
+    different local maps: the layout and the BA record size are agreed before the all-gather."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from orb_slam2_commit_amd import dist as odist
+    odist.init("gloo", rank, world)
+    nf = 500
+    w, h = (320, 240) if rank == 0 else (300, 230)
+    own_cap = nf + 8 * 8 + (64 if rank == 0 else 16)  # per-rank capacity (as max_keypoints(w, h) differs)
+    lay = pipeline.FrameRecords(pipeline.agree_max(B), pipeline.agree_max(own_cap))
+    arena = np.zeros(lay.nbytes, np.uint8)
+    v = lay.views(arena)
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    imgs = synth.stereo_batch(rank, B, n_unique=2, width=w, height=h)
+    o = oracle.extract(p, imgs[0])
+    n = len(o.keypoints)
+    v["counts"][0] = n
+    v["kps"][0, :n] = o.keypoints.view(np.uint8).reshape(n, 28)
+    P = synth.localba_problem(seed=7 + rank, n_local=4 + 3 * rank, n_fixed=2, n_points=200, obs_per_point=4)
+    rec = pipeline.ba_summary(oracle.local_ba(P), len(P["Tcw"]))
+    recs, bas = pipeline.gather_sequence_results(torch.from_numpy(arena), rec)
+    bad = None
+    try:  # a rank that skips the agreement fails loudly instead of hanging in the collective
+        pipeline.gather_sequence_results(torch.zeros(lay.nbytes + 256 * rank, dtype=torch.uint8), rec)
+    except ValueError as e:
+        bad = str(e)
+    q.put((rank, recs.numpy().tobytes(), bas.tobytes(), lay.nbytes, n, len(P["Tcw"]), bad))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_ragged_sequences():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ragged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nbytes = res[0][3]
+    assert res[1][3] == nbytes  # same agreed layout on both ranks
+    lay = pipeline.FrameRecords(B, 500 + 8 * 8 + 64)
+    assert lay.nbytes == nbytes
+    for rank, rb, bb, _, _, _, bad in res:
+        g = np.frombuffer(rb, np.uint8).reshape(world, nbytes)
+        ba = np.frombuffer(bb, np.float64).reshape(world, -1)
+        for r in range(world):
+            assert int(lay.views(g[r])["counts"][0]) == res[r][4]
+            assert pipeline.parse_ba_summary(ba[r])["Tcw"].shape == (res[r][5], 12)
+        assert bad is not None and "differs between ranks" in bad
+
+
 def test_record_layout():
     lay = pipeline.FrameRecords(256, 2024)
     assert all(o % 256 == 0 for o in lay.offsets.values())
@@ -116,9 +174,13 @@ def test_record_layout():
 def test_ba_summary_roundtrip():
     P = _ba_problem(3)
     r = oracle.local_ba(P)
-    s = pipeline.parse_ba_summary(pipeline.ba_summary(r, len(P["Tcw"])))
+    rec = pipeline.ba_summary(r, len(P["Tcw"]))
+    assert len(rec) == pipeline.BA_HEAD + 12 * pipeline.MAX_BA_CAMS  # fixed size whatever the map
+    s = pipeline.parse_ba_summary(rec)
     assert s["iterations"] == tuple(r["iterations"]) and s["trials"] == r["trials"]
     np.testing.assert_array_equal(s["Tcw"], np.asarray(r["Tcw_d"]).reshape(-1, 12))
+    with pytest.raises(ValueError):
+        pipeline.ba_summary(r, len(P["Tcw"]), max_cams=len(P["Tcw"]) - 1)
 
 
 # ----------------------------------------------------------------- GPU rehearsal (two ranks, one card)

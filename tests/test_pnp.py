@@ -252,6 +252,7 @@ RELOC_SETS = {
     "after_failures": [("bad", 41), ("few", 42), ("bad", 43), ("good", 44), ("good", 45)],
     "none_good": [("bad", 51), ("few", 52), ("bad", 53)],
     "heavy_outliers": [("bad", 61), ("hard", 62), ("good", 63)],
+    "good_then_few": [("good", 81), ("few", 82), ("good", 83)],
 }
 
 
@@ -295,6 +296,24 @@ def test_gpu_pnp_iterate_candidates_equals_reference_loop(gpu, name):
         assert stopped == ostop, (stopped, ostop)
         assert g_gpu.peek(8) == g_ora.peek(8)
         start += stopped + 1
+    for s in gs:
+        s.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pnp_candidates_after_stop_untouched(gpu):
+    """Candidates after the one that returns a pose are never reached by the reference loop:
+    their results are all zero -- in particular no bNoMore for one with N < minInliers, and
+    no pose -- and they draw nothing from the stream."""
+    from orb_slam2_commit_amd.orb import pnp_iterate_candidates
+    probs = [_reloc_problem(k, s) for k, s in RELOC_SETS["good_then_few"]]
+    gs = [_gpu_solver(P) for P in probs]
+    raw = []
+    stopped, res = pnp_iterate_candidates(gs, 5, GlibcRand(1), raw_results=raw)
+    assert stopped == 0 and res[0][0] is not None and len(raw) == 3
+    for r in raw[1:]:
+        assert (r.no_more, r.found, r.n_inliers, r.used) == (0, 0, 0, 0)
+        assert list(r.Tcw) == [0.0] * 16
     for s in gs:
         s.close()
 
