@@ -62,6 +62,7 @@ def parse():
                                                                   "throughput form (<=1: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=3, help="config-5 batches per rank (0: skip)")
     ap.add_argument("--single-frames", type=int, default=200, help="frames of the single-frame drop-in leg (0: skip)")
+    ap.add_argument("--track-steps", type=int, default=5, help="steps of the extract+match+track leg (0: skip)")
     ap.add_argument("--c3-steps", type=int, default=3, help="config-3 (EuRoC + PnP RANSAC) steps per rank (0: skip)")
     ap.add_argument("--c3-batch", type=int, default=128, help="config-3 frames (sequences) per step per GPU")
     ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r02_sq_counters.json"),
@@ -395,6 +396,73 @@ def single_frame_leg(args, pairs, cpu):
         out["cpu_baseline"] = dict(median_ms=cpu.get("median_ms"), p90_ms=cpu.get("p90_ms"),
                                    two_thread_median_ms=(cpu.get("two_thread") or {}).get("median_ms"),
                                    kind=cpu.get("kind"), note="the oracle's per-frame time from cpu_baseline")
+    return out
+
+
+# ------------------------------------------------------------------ tracking front-end leg
+def track_leg(args, rank, world, dev, odist, ex, images, stream, pairs_host, oracle_mod=None, cpus=None):
+    """Extract+match a batch, then Tracking::TrackReferenceKeyFrame's front end (src/Tracking.cc:910-969)
+    for its frames: ComputeBoW -> SearchByBoW(KF, F) (nnratio 0.7) -> PoseOptimization, all on the
+    device (orb_slam2_commit_amd/tracking.py).  Frame f is tracked against frame f-U (the same scene
+    53 px earlier: the batch holds U scenes, rolled), so B-U of the B frames are tracked per step.
+    Synthetic DBoW2 vocabulary k=10, L=5 (ORBvoc.txt is not in the image: k=10, L=6), FeatureVector
+    at levelsup 3 (the reference's levelsup 4 on L=6: the same node level, <= 100 nodes)."""
+    import torch
+    from orb_slam2_commit_amd import ORBVocabulary, synth
+    from orb_slam2_commit_amd.tracking import TrackBatch
+    W, H, B, U = KITTI["width"], KITTI["height"], args.batch, args.unique
+    cap = ex.max_keypoints(W, H)
+    text = synth.vocabulary(seed=5, k=10, L=5)[0]
+    voc = ORBVocabulary(dev.index)
+    voc.loadFromText(text)
+    fx, bf = KITTI["fx"], KITTI["bf"]
+    cx, cy = 607.1928, 185.2157
+    tb = TrackBatch(voc, B, cap, ex.GetInverseScaleSigmaSquares(), fx, fx, cx, cy, bf, dev, levelsup=3)
+    kps = torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev)
+    desc = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+    uR = torch.empty((B, cap), dtype=torch.float32, device=dev)
+    depth = torch.empty((B, cap), dtype=torch.float32, device=dev)
+    nmatch = torch.zeros(B, dtype=torch.int32, device=dev)
+    pairs = [(f - U, f) for f in range(U, B)]
+    bl = bf / fx
+
+    def step(tim=None):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        ex.stereo_frames_device(images, kps, desc, counts, bf, bl, uR, depth, nmatch, stream)
+        e1.record(stream)
+        r = tb.run(kps, desc, counts, uR, depth, pairs, stream, timings=tim)
+        return r, (e0, e1)
+
+    step()
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    tim, evs = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.track_steps):
+        r, ev = step(tim)
+        evs.append(ev)
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    el = odist.max_over_ranks(time.perf_counter() - t0, dev)
+    nmat, nedge, ngood = r
+    em_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    tim = np.asarray(tim) * 1e3
+    out = dict(frames_per_s=round(B * args.track_steps * world / el, 2),
+               tracked_frames_per_s=round(len(pairs) * args.track_steps * world / el, 2),
+               ms_per_step=round(el / args.track_steps * 1e3, 3), batch_frames=B, tracked_per_step=len(pairs),
+               split_ms=dict(extract_match_gpu=round(em_ms, 3),
+                             compute_bow_and_readback=round(float(tim[:, 0].mean()), 3),
+                             search_by_bow_gather_and_readback=round(float(tim[:, 1].mean()), 3),
+                             pose_optimization_and_readback=round(float(tim[:, 2].mean()), 3)),
+               matches_per_frame=round(float(np.mean(nmat)), 1), edges_per_frame=round(float(np.mean(nedge)), 1),
+               good_per_frame=round(float(np.mean(ngood)), 1),
+               vocabulary="synthetic DBoW2 text vocabulary k=10 L=5, FeatureVector at levelsup 3",
+               note="one batch in flight: extract+match (device batch) then ComputeBoW, SearchByBoW(KF=f-%d, F=f), "
+                    "PoseOptimization edge gather and PoseOptimization for every tracked frame; two small host "
+                    "readbacks size the problem descriptors" % U)
+    voc.close()
     return out
 
 
@@ -744,6 +812,8 @@ def main():
     if args.ba_calls > 0:
         out["localba"] = localba_leg(args, rank, world, dev, odist, oracle_mod, flags, cpus)
         out["localba_iters_per_s"] = out["localba"]["iters_per_s"]
+    if args.track_steps > 0:
+        out["track"] = track_leg(args, rank, world, dev, odist, ex, images, stream, pairs)
     if args.pipeline_steps > 0:
         out["config5"] = config5_leg(args, rank, world, dev, odist, ex, images, stream)
     if args.c3_steps > 0:

@@ -508,6 +508,30 @@ orbx_status orbx_pose_optimization(const orbx_pose_problem* p, int device);
  * pointers; one block per problem runs all four rounds on the GPU (no host round trips). */
 orbx_status orbx_pose_optimization_device(const orbx_pose_problem* problems, int n, void* stream);
 
+/* Tracking::TrackReferenceKeyFrame's gather (src/Tracking.cc:910-969) between SearchByBoW(KF, F)
+ * and PoseOptimization(&F), on a device batch: PoseOptimization's edge per current-frame feature
+ * with a MapPoint, in feature order (src/Optimizer.cc:318-410).  The reference KeyFrame's MapPoints
+ * are its stereo points: feature k has one iff kf_depth[k] > 0, at KeyFrame::UnprojectStereo(k)
+ * with pose Twc.  Writes obs / Xw / inv_sigma2 (and the feature of each edge) compacted, and
+ * *n_edges -- the inputs of an orbx_pose_problem.  Device pointers; problems[] is a HOST array. */
+typedef struct {
+  const orbx_keypoint* f_kps;      /* current frame mvKeysUn */
+  const float* f_uright;           /* current frame mvuRight (NULL: monocular) */
+  const int32_t* f_count;          /* current frame N (device) */
+  const int32_t* match;            /* SearchByBoW KF-F output: KF feature per frame feature, or -1 */
+  const orbx_keypoint* kf_kps;     /* reference KeyFrame mvKeysUn */
+  const float* kf_depth;           /* reference KeyFrame mvDepth */
+  float Twc[12];                   /* reference KeyFrame pose, camera to world, row-major 3x4 */
+  float fx, fy, cx, cy;            /* KeyFrame intrinsics */
+  const float* inv_level_sigma2;   /* current frame mvInvLevelSigma2 (device, per octave) */
+  float* obs;                      /* out: capacity N x 3 */
+  float* Xw;                       /* out: capacity N x 3 */
+  float* inv_sigma2;               /* out: capacity N */
+  int32_t* edge_feature;           /* out (optional): capacity N */
+  int32_t* n_edges;                /* out: 1 */
+} orbx_track_gather;
+orbx_status orbx_track_gather_device(const orbx_track_gather* problems, int n, void* stream);
+
 /* MapPoint::ComputeDistinctiveDescriptors() -- src/MapPoint.cc:249-320, include/MapPoint.h:83,
  * for a batch of MapPoints.  Point p's observed descriptors (pKF->mDescriptors.row(idx) for
  * each (pKF, idx) of mObservations in map order, bad KeyFrames skipped, :270-276) are rows

@@ -111,6 +111,14 @@ class TriProblem(C.Structure):
                 ("check_ori", C.c_int), ("match12", C.c_void_p), ("nmatches", C.c_void_p)]
 
 
+class TrackGather(C.Structure):
+    _fields_ = [("f_kps", C.c_void_p), ("f_uright", C.c_void_p), ("f_count", C.c_void_p), ("match", C.c_void_p),
+                ("kf_kps", C.c_void_p), ("kf_depth", C.c_void_p), ("Twc", C.c_float * 12), ("fx", C.c_float),
+                ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("inv_level_sigma2", C.c_void_p),
+                ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p), ("edge_feature", C.c_void_p),
+                ("n_edges", C.c_void_p)]
+
+
 class Camera(C.Structure):
     _fields_ = [("K", C.c_float * 9), ("dist", C.c_float * 5), ("n_dist", C.c_int)]
 
@@ -157,6 +165,9 @@ SIGNATURES = {
     "orbx_voc_destroy": ([P], C.c_int),
     "orbx_voc_info": ([P, P], C.c_int),
     "orbx_voc_transform": ([P, P, P, C.c_int, C.c_int, P, P, P, P, P, P, P], C.c_int),
+    "orbx_voc_transform_device": ([P, P, C.c_int, C.c_longlong, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P, P],
+                                  C.c_int),
+    "orbx_track_gather_device": ([C.POINTER(TrackGather), C.c_int, P], C.c_int),
     "orbx_search_by_projection": ([C.POINTER(ProjProblem), C.c_int], C.c_int),
     "orbx_search_by_projection_device": ([C.POINTER(ProjProblem), C.c_int, P], C.c_int),
     "orbx_pose_optimization": ([C.POINTER(PoseProblem), C.c_int], C.c_int),

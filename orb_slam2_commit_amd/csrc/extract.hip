@@ -483,6 +483,16 @@ __device__ __forceinline__ int lane_rank(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Phase probe (build with -DORBX_FAST_PROBE only; tools/fast_probe.py): per-phase cycles of
+// every cell wave, summed over the launch into fast_probe_sum (one vector atomic per phase
+// and wave, issued after the wave's last timestamp).
+#ifdef ORBX_FAST_PROBE
+__device__ unsigned long long fast_probe_sum[8];
+#define FAST_TS(k) const unsigned long long ts##k = __builtin_amdgcn_s_memtime()
+#else
+#define FAST_TS(k)
+#endif
+
 // S: LDS row stride of the window tile and the score map (multiple of 16, >= window width);
 // RP: region rows per compass instruction (2 when the widest cell fits 32 lanes)
 template <int S, int RP>
@@ -501,6 +511,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   const uint8_t* lvl = c.level == 0 ? B.in + (size_t)img * B.in_pitch : B.pyr + (size_t)img * G->pyr_bytes + c.loff;
   const uint8_t* base = lvl + (size_t)(c.y0 - 3) * lw + (c.x0 - 3);
   const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TH = H + 6;
+  FAST_TS(0);
   // 1. window -> LDS: lane = (row, 16-B chunk); window pixel (r, col) lands at tile[r*S + col]
   {
     constexpr int CPR = S / 16, RPI = 64 / CPR;
@@ -606,7 +617,9 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   };
   // FAST at iniThFAST only (src/ORBextractor.cc:892): the map then holds exactly the corners at
   // iniThFAST, which is all NMS at iniThFAST looks at (a weaker neighbour never beats a centre)
+  FAST_TS(1);
   int nc = detect(ini);
+  FAST_TS(2);
   // 4. survivors at iniThFAST (verdict kept in bit 15 of the list entry)
   int cnt = 0;
   for (int i0 = 0; i0 < nc; i0 += 64) {
@@ -621,7 +634,9 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   }
   // an empty cell runs FAST(window, minThFAST) (src/ORBextractor.cc:894-900): a wave-uniform
   // second pass, taken by ~10 % of the cells on the bench images
+  FAST_TS(3);
   if (cnt == 0 && mint != ini) nc = detect(mint);
+  FAST_TS(4);
   const int thr = (cnt > 0 ? ini : mint) + 1;
   // 5. row-major writes at the chosen threshold
   uint32_t* out = B.cand + (size_t)img * G->cand_total + c.cand_off;
@@ -645,6 +660,18 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
     pos += __popcll(m);
   }
   if (lane == 0) B.cell_count[(size_t)img * G->ncells + cell] = min(pos, c.cap);
+#ifdef ORBX_FAST_PROBE
+  FAST_TS(5);
+  if (lane == 0) {
+    atomicAdd(&fast_probe_sum[0], ts1 - ts0);  // window load
+    atomicAdd(&fast_probe_sum[1], ts2 - ts1);  // compass + score at iniThFAST
+    atomicAdd(&fast_probe_sum[2], ts3 - ts2);  // NMS count
+    atomicAdd(&fast_probe_sum[3], ts4 - ts3);  // minThFAST pass (empty cells)
+    atomicAdd(&fast_probe_sum[4], ts5 - ts4);  // NMS + writes
+    atomicAdd(&fast_probe_sum[5], 1ull);       // waves
+    atomicAdd(&fast_probe_sum[6], (unsigned long long)(cnt == 0));
+  }
+#endif
 }
 
 // ----------------------------------------------------------------- octree
@@ -1287,3 +1314,13 @@ hipError_t octree_set_smem_limit(size_t bytes) {
 }
 
 }  // namespace orbx
+
+#ifdef ORBX_FAST_PROBE
+extern "C" int orbx_debug_fast_probe(unsigned long long* out, int reset) {
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(orbx::fast_probe_sum), z, sizeof(z)) == hipSuccess ? 0 : -3;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::fast_probe_sum), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
+}
+#endif

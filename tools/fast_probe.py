@@ -1,4 +1,5 @@
-"""Per-phase cycles of the k_fast cell waves (s_memtime probe build build_ab/fprobe), on the bench batch."""
+"""Per-phase cycles of the k_fast cell waves on the bench batch (probe build:
+tools/build_variant.sh fprobe -DORBX_FAST_PROBE; run with ORBX_LIB_OVERRIDE=build_ab/fprobe/liborbx.so)."""
 import ctypes as C
 import sys
 
@@ -16,22 +17,21 @@ cap = ex.max_keypoints(W, H)
 kps = torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev)
 desc = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
 counts = torch.zeros(2 * B, dtype=torch.int32, device=dev)
-ex.extract_batch_device(images, kps, desc, counts) if hasattr(ex, "extract_batch_device") else None
-torch.cuda.synchronize()
-L = _lib.lib()
-buf = (C.c_ulonglong * 16)()
-L.orbx_debug_fast_probe(buf, 1)
 uR = torch.empty((B, cap), dtype=torch.float32, device=dev)
 dep = torch.empty((B, cap), dtype=torch.float32, device=dev)
 nm = torch.zeros(B, dtype=torch.int32, device=dev)
-ex.stereo_frames_device(images, kps, desc, counts, 386.1448, 386.1448 / 718.856, uR, dep, nm)
+L = _lib.lib()
+st = torch.cuda.current_stream()
+ex.stereo_frames_device(images, kps, desc, counts, 386.1448, 386.1448 / 718.856, uR, dep, nm, st)
 torch.cuda.synchronize()
-import numpy as np  # noqa: E402
-ph = np.zeros(5 << 20, np.uint32)
-L.orbx_debug_fast_phases(ph.ctypes.data_as(C.c_void_p))
-ph = ph.reshape(5, 1 << 20)[:, :int(ex.ncells() if hasattr(ex, "ncells") else 1220) * 2 * B].astype(np.float64)
-names = ["window load", "compass", "score", "nms count", "nms write"]
-tot = ph.sum(0)
-print("waves", ph.shape[1], "cycles/wave mean %.0f median %.0f p90 %.0f" % (tot.mean(), np.median(tot), np.percentile(tot, 90)))
-for k, nmk in enumerate(names):
-    print("%-12s mean %8.0f median %8.0f  %5.1f %%" % (nmk, ph[k].mean(), np.median(ph[k]), 100.0 * ph[k].sum() / tot.sum()))
+buf = (C.c_ulonglong * 8)()
+L.orbx_debug_fast_probe(buf, 1)
+ex.stereo_frames_device(images, kps, desc, counts, 386.1448, 386.1448 / 718.856, uR, dep, nm, st)
+torch.cuda.synchronize()
+L.orbx_debug_fast_probe(buf, 0)
+waves = buf[5]
+names = ["window load", "detect at iniThFAST", "NMS count", "minThFAST pass", "NMS + writes"]
+tot = sum(buf[i] for i in range(5))
+print("waves %d, empty cells %d (%.1f %%), cycles per wave %.0f" % (waves, buf[6], 100.0 * buf[6] / waves, tot / waves))
+for i, n in enumerate(names):
+    print("%-22s %8.0f cycles/wave  %5.1f %%" % (n, buf[i] / waves, 100.0 * buf[i] / tot))
