@@ -543,7 +543,7 @@ orbx_status orbx_distinctive_descriptors(const uint8_t* desc, const int32_t* obs
 orbx_status orbx_distinctive_descriptors_device(const uint8_t* desc, const int32_t* obs_off, int n_points,
                                                 int32_t* best, uint8_t* out_desc, void* stream);
 
-/* Frame::UndistortKeyPoints() -- src/Frame.cc:471-506, include/Frame.h:174 (cv::undistortPoints
+/* Frame::UndistortKeyPoints() -- src/Frame.cc:471-506, include/Frame.h:242 (cv::undistortPoints
  * with P = K) and the corner pass of Frame::ComputeImageBounds (:508-537, four keypoints at the
  * image corners).  K = mK row-major (float), dist = mDistCoef (k1, k2, p1, p2[, k3]). */
 typedef struct {

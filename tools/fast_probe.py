@@ -24,14 +24,19 @@ L = _lib.lib()
 st = torch.cuda.current_stream()
 ex.stereo_frames_device(images, kps, desc, counts, 386.1448, 386.1448 / 718.856, uR, dep, nm, st)
 torch.cuda.synchronize()
-buf = (C.c_ulonglong * 8)()
-L.orbx_debug_fast_probe(buf, 1)
+ncells = int(ex._plan_cells) if hasattr(ex, "_plan_cells") else 2000
+buf = torch.zeros((2 * B * 2000, 8), dtype=torch.int32, device=dev)
+L.orbx_debug_fast_probe.argtypes = [C.c_void_p]
+L.orbx_debug_fast_probe(C.c_void_p(buf.data_ptr()))
 ex.stereo_frames_device(images, kps, desc, counts, 386.1448, 386.1448 / 718.856, uR, dep, nm, st)
 torch.cuda.synchronize()
-L.orbx_debug_fast_probe(buf, 0)
-waves = buf[5]
-names = ["window load", "detect at iniThFAST", "NMS count", "minThFAST pass", "NMS + writes"]
-tot = sum(buf[i] for i in range(5))
-print("waves %d, empty cells %d (%.1f %%), cycles per wave %.0f" % (waves, buf[6], 100.0 * buf[6] / waves, tot / waves))
+L.orbx_debug_fast_probe(None)
+import numpy as np  # noqa: E402
+a = buf.cpu().numpy().astype(np.int64)
+a = a[a[:, 0] > 0]
+names = ["window load", "compass at iniThFAST", "score at iniThFAST", "NMS count", "minThFAST pass", "NMS + writes"]
+tot = a[:, :6].sum(1)
+print("waves %d, empty cells %.1f %%, compass survivors per cell %.1f, s_memtime ticks per wave mean %.0f median %.0f"
+      % (len(a), 100.0 * a[:, 6].mean(), a[:, 7].mean(), tot.mean(), np.median(tot)))
 for i, n in enumerate(names):
-    print("%-22s %8.0f cycles/wave  %5.1f %%" % (n, buf[i] / waves, 100.0 * buf[i] / tot))
+    print("%-22s mean %8.0f median %8.0f  %5.1f %%" % (n, a[:, i].mean(), np.median(a[:, i]), 100.0 * a[:, i].sum() / tot.sum()))
