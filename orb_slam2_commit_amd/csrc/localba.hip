@@ -1313,14 +1313,202 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_col_many(const BaDev* __restrict
   k_ba_ldlt_col_body<TPT, NT>(Ds[blockIdx.z]);
 }
 
+// ---- reduced camera system, N <= 128: 16-wide blocked LDL^T, FP64 MFMA trailing updates ----
+// The column-step kernel above pays one barrier + LDS round trip per pivot (~1,100 cycles, 120
+// pivots at config 4).  Here the pivots run in 16-wide panels; per panel p (j0 = 16p):
+//   F  wave 0 factors the 16x16 diagonal block in registers (lane r = row r; the pivot and the
+//      W[k][c] = L[k][c] d_c of the rows below it broadcast by readlane), 1/d by v_rcp_f64 + two
+//      Newton steps; it stores L (lower) and W (mirrored into the upper triangle) and d;
+//   T  every row below the panel, the augmented row b^T included, solves W_i L_pp^T = A_i (one
+//      thread per row, L_pp broadcast from LDS) and stores L_i = W_i D^-1 (lower) and W_i
+//      (mirrored: A[j0+c][i]);
+//   U  the trailing lower triangle A_ik -= W_i L_k^T as v_mfma_f64_16x16x4f64 tiles over the
+//      waves (4 MFMAs per 16x16 tile); one wave updates the augmented row with plain FMAs.
+// Three barriers per panel instead of sixteen.  The augmented row ends as y = D^-1 L^-1 b (the
+// forward solve is free), and wave 0 solves L^T x = y with the column entries prefetched eight
+// pivots at a time.  Same failure rule as the other kernels (an exactly zero pivot, scal[2] = 0).
+// LDS: (Np+1) rows x (Np+1) doubles (odd stride: a 16-lane column read spreads over the banks)
+// plus d: 134 KB at Np = 128.
+constexpr int kLdltBlkNT = 512;
+inline size_t ldlt_blk_smem(int N) {
+  const size_t Np = ldlt_np(N);
+  return ((Np + 1) * (Np + 1) + Np + 16) * sizeof(double);
+}
+inline bool ldlt_blk_fits(int N) { return ldlt_np(N) <= 128 && N > 0; }
+
+template <int NT>
+__device__ __forceinline__ void k_ba_ldlt_blk_body(const BaDev& D) {
+  if (lm_skip(D)) return;
+  extern __shared__ __attribute__((aligned(16))) double A[];
+  __shared__ int fail;
+  constexpr int NW = NT / 64;
+  const int N = 6 * D.nposes, Np = (N + 15) & ~15, T = Np >> 4, ld = Np + 1;
+  double* dg = A + (size_t)(Np + 1) * ld;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // S padded with an identity block (decoupled, never a zero pivot); row Np = b
+  for (int idx = tid; idx < (Np + 1) * Np; idx += NT) {
+    const int r = idx / Np, c = idx - r * Np;
+    double v;
+    if (r < Np)
+      v = (r < N && c < N) ? D.S[(size_t)r * N + c] : (r == c ? 1.0 : 0.0);
+    else
+      v = c < N ? D.bs[c] : 0.0;
+    A[(size_t)r * ld + c] = v;
+  }
+  if (tid == 0) fail = 0;
+  __syncthreads();
+  LDLT_TS(0);
+  for (int p = 0; p < T; p++) {
+    const int j0 = 16 * p;
+    // ---- F: the diagonal block
+    if (wv == 0) {
+      const int r = lane & 15;
+      double row[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) row[c] = A[(size_t)(j0 + r) * ld + j0 + c];
+      bool bad = false;
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const double d = readlane_d(row[c], c);
+        bad |= d == 0.0;
+        const double lrc = row[c] * rcp_nr(d);  // L[r][c] (rows r > c)
+#pragma unroll
+        for (int k = c + 1; k < 16; k++) {
+          const double wkc = readlane_d(row[c], k);  // W[k][c]
+          if (r >= k) row[k] -= lrc * wkc;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep each pivot's broadcasts next to their use
+      }
+      if (bad) {
+        if (lane == 0) fail = 1;
+      } else if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+          const double dc = readlane_d(row[c], c);
+          if (c < r) {
+            A[(size_t)(j0 + r) * ld + j0 + c] = row[c] * rcp_nr(dc);  // L
+            A[(size_t)(j0 + c) * ld + j0 + r] = row[c];               // W (mirror)
+          }
+        }
+        dg[j0 + r] = row[r];
+      }
+    }
+    __syncthreads();
+    LDLT_TS(1 + 3 * p);
+    if (fail) {
+      if (tid == 0) D.scal[2] = 0.0;
+      return;
+    }
+    // ---- T: the rows below the panel and the augmented row
+    const int nrows = Np - j0 - 16 + 1;
+    for (int t = tid; t < nrows; t += NT) {
+      const int i = j0 + 16 + t;
+      double w[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) w[c] = A[(size_t)i * ld + j0 + c];
+#pragma unroll
+      for (int c = 1; c < 16; c++)
+#pragma unroll
+        for (int m = 0; m < c; m++) w[c] -= w[m] * A[(size_t)(j0 + c) * ld + j0 + m];
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        A[(size_t)i * ld + j0 + c] = w[c] * rcp_nr(dg[j0 + c]);  // L_i
+        A[(size_t)(j0 + c) * ld + i] = w[c];                      // W_i (mirror; column Np for b)
+      }
+    }
+    __syncthreads();
+    LDLT_TS(2 + 3 * p);
+    // ---- U: trailing update A_ik -= W_i L_k^T (tiles of the lower triangle), augmented row
+    const int m = T - 1 - p, ntiles = m * (m + 1) / 2;
+    for (int t = wv; t < ntiles + (m > 0 ? 1 : 0); t += NW) {
+      if (t < ntiles) {
+        int ti = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
+        while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+        while (ti * (ti + 1) / 2 > t) ti--;
+        const int tk = t - ti * (ti + 1) / 2;
+        const int R0 = j0 + 16 + 16 * ti, C0 = j0 + 16 + 16 * tk;
+        double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+          const int k = j0 + 4 * kk + (lane >> 4);
+          const double av = A[(size_t)k * ld + R0 + (lane & 15)];   // W[row][k] (mirror)
+          const double bv = A[(size_t)(C0 + (lane & 15)) * ld + k];  // L[col][k]
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) A[(size_t)(R0 + (lane >> 4) + 4 * rr) * ld + C0 + (lane & 15)] -= acc[rr];
+      } else {
+        for (int cc = lane; cc < 16 * m; cc += 64) {
+          const int col = j0 + 16 + cc;
+          double sacc = A[(size_t)Np * ld + col];
+#pragma unroll
+          for (int c = 0; c < 16; c++) sacc -= A[(size_t)(j0 + c) * ld + Np] * A[(size_t)col * ld + j0 + c];
+          A[(size_t)Np * ld + col] = sacc;
+        }
+      }
+    }
+    __syncthreads();
+    LDLT_TS(3 + 3 * p);
+  }
+  if (wv != 0) return;
+  // y = D^-1 L^-1 b sits in row Np; L^T x = y by columns, x_k final at step k
+  double y[2];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int i = lane + 64 * q;
+    y[q] = i < N ? A[(size_t)Np * ld + i] : 0.0;
+  }
+  for (int kb = N - 1; kb >= 0; kb -= 8) {
+    double Lv[8][2];
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int i = lane + 64 * q, k = max(kb - u, 0);
+        const double v = A[(size_t)k * ld + min(i, Np - 1)];  // row k, column i: L[k][i] when i < k
+        Lv[u][q] = (i < kb - u) ? v : 0.0;
+      }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = kb - u;
+      if (k >= 0) {
+        const double xk = readlane_d(k < 64 ? y[0] : y[1], k & 63);
+#pragma unroll
+        for (int q = 0; q < 2; q++) y[q] -= Lv[u][q] * xk;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++)
+    if (lane + 64 * q < N) D.xp[lane + 64 * q] = y[q];
+  if (lane == 0) D.scal[2] = 1.0;
+  LDLT_TS(61);
+}
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ba_ldlt_blk(BaDev D) { k_ba_ldlt_blk_body<NT>(D); }
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ba_ldlt_blk_many(const BaDev* __restrict__ Ds) {
+  k_ba_ldlt_blk_body<NT>(Ds[blockIdx.z]);
+}
+
 // Launch plan for the reduced system: the column-step kernel while the
 // packed factor fits LDS, else the 16-wide blocked kernel (LDS or global).
 struct LdltPlan {
   int N = 0, tpt = 0, nt = 1024;
-  bool col = false, in_lds = false;
+  bool col = false, in_lds = false, blk = false;
   size_t smem = 0;
   hipError_t prepare(int n) {
     N = n;
+    // A/B switch: ORBX_LDLT_BLK=1 takes the MFMA-blocked kernel where it fits (measured slower than
+    // the column-step kernel at config 4: 117 vs 60 us; one launch shape per batch)
+    blk = ldlt_blk_fits(N) && std::getenv("ORBX_LDLT_BLK") && !std::getenv("ORBX_LDLT_BLOCKED");
+    if (blk) {
+      col = false;
+      in_lds = true;
+      nt = kLdltBlkNT;
+      smem = ldlt_blk_smem(N);
+      return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    }
     col = ldlt_col_fits(N) && !std::getenv("ORBX_LDLT_BLOCKED");
     if (col) {
       const char* e = std::getenv("ORBX_LDLT_NT");  // A/B: threads of the column-step kernel
@@ -1341,6 +1529,7 @@ struct LdltPlan {
     return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   }
   const void* kernel_ptr() const {
+    if (blk) return (const void*)k_ba_ldlt_blk<kLdltBlkNT>;
     if (col) {
       if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col<1, 1024> : (const void*)k_ba_ldlt_col<2, 1024>;
       if (nt == 512)
@@ -1353,6 +1542,7 @@ struct LdltPlan {
   }
   // batched driver: the column-step kernel over K problems (blockIdx.z), sized for the largest
   const void* many_ptr() const {
+    if (blk) return (const void*)k_ba_ldlt_blk_many<kLdltBlkNT>;
     if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col_many<1, 1024> : (const void*)k_ba_ldlt_col_many<2, 1024>;
     if (nt == 512)
       return tpt == 1 ? (const void*)k_ba_ldlt_col_many<1, 512>
@@ -1368,7 +1558,7 @@ struct LdltPlan {
                        dim3(nt), smem, st, Ds);
   }
   void launch(const BaDev& D, hipStream_t st, int stage_limit = 99) const {
-    if (col) {
+    if (blk || col) {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BaDev)>(const_cast<void*>(kernel_ptr())), dim3(1), dim3(nt),
                          smem, st, D);
     } else if (in_lds) {
@@ -2908,7 +3098,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
   }
   LdltPlan ldlt;
   BA_CHECK(ldlt.prepare(Nmax));
-  if (!ldlt.col) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
+  if (!ldlt.col && !ldlt.blk) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
   BA_CHECK(ldlt.prepare_many());
   if (B.cap < K) {
     if (B.lm_host) (void)hipHostFree(B.lm_host);
