@@ -150,7 +150,7 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
   G.min_th = p.min_th_fast;
   long long pyr = 0, blur = 0;
   int cand = 0, oct = 0, ntiles = 0, node_cap = 64, cell_cap = 1;
-  int fast_wmax = 1, fast_hmax = 1;
+  int lv_wmax[kMaxLevelsPlan] = {}, lv_hmax[kMaxLevelsPlan] = {};  // k_fast: largest cell per level
   P.cells.clear();
   P.tile_level.clear();
   P.xt.clear();
@@ -197,8 +197,8 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
           if (c.x1 < c.x0 || c.y1 < c.y0) continue;
           const int cw = c.x1 - c.x0 + 1, ch = c.y1 - c.y0 + 1;
           if (cw > 60 || ch > 60) return ORBX_ERR_SIZE;  // k_fast LDS tile bound
-          fast_wmax = std::max(fast_wmax, cw);
-          fast_hmax = std::max(fast_hmax, ch);
+          lv_wmax[l] = std::max(lv_wmax[l], cw);
+          lv_hmax[l] = std::max(lv_hmax[l], ch);
           c.cap = ((cw + 1) / 2) * ((ch + 1) / 2);
           c.lw = L.w;
           c.loff = (int)L.off;
@@ -264,14 +264,59 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
       }
     }
   }
-  // k_fast LDS layout for the largest cell: window tile of H+6 rows plus the compass
-  // slack (rows up to H+12 are read for out-of-region lanes) at stride S, score map
-  // (H+2) x S (one zero row/column each side), compass list W*H u16
-  G.fast_s = fast_wmax + 6 <= 48 ? 48 : 80;
-  G.fast_rp = fast_wmax <= 32 ? 2 : 1;
-  G.fast_tile_bytes = (fast_hmax + 13) * G.fast_s;
-  G.fast_map_bytes = (fast_hmax + 2) * G.fast_s;
-  G.fast_smem = G.fast_tile_bytes + G.fast_map_bytes + 2 * fast_wmax * fast_hmax;
+  // k_fast LDS layout of a launch group, sized by its largest cell: window tile of H+6 rows at
+  // stride S, score map (H+2) x S (one zero row/column each side), compass list W*H u16.  The
+  // compass reads up to 6 rows past the tile for lanes below the region (masked): they land in the
+  // map or list, or past the allocation (reads as 0).  One-wave blocks per CU are LDS-bound and
+  // k_fast is latency-bound (+1 / +2 KB of LDS per block measured +8 / +15 % time), so the stride
+  // is the smallest the kernel is built for (40 for 31-32 px cells), and the levels whose cells fit
+  // 5 KB (32 blocks per CU) get their own launch when taller cells of the other levels would not
+  // (KITTI: levels 0-3 at 5.0 KB, levels 4-7 with their 38-40-row cells at 6.0 KB).
+  {
+    auto layout = [&](int wmax, int hmax, Geometry::FastGroup& g) {
+      g.s = wmax + 6 <= 40 ? 40 : wmax + 6 <= 48 ? 48 : 80;
+      g.rp = wmax <= 32 ? 2 : 1;
+      g.tile_bytes = ((hmax + 6) * g.s + 15) & ~15;
+      g.map_bytes = ((hmax + 2) * g.s + 15) & ~15;
+      g.smem = g.tile_bytes + g.map_bytes + 2 * wmax * hmax;
+    };
+    constexpr int kFastLdsFit = 5 * 1024;
+    int split = 0, wa = 1, ha = 1;  // levels [0, split) fit kFastLdsFit together
+    for (int l = 0; l < p.nlevels; l++) {
+      Geometry::FastGroup g{};
+      layout(std::max(wa, lv_wmax[l]), std::max(ha, lv_hmax[l]), g);
+      if (g.smem > kFastLdsFit) break;
+      wa = std::max(wa, lv_wmax[l]);
+      ha = std::max(ha, lv_hmax[l]);
+      split = l + 1;
+    }
+    if (split == 0 || split == p.nlevels) split = p.nlevels;  // one launch
+    int wb = 1, hb = 1;
+    for (int l = split; l < p.nlevels; l++) {
+      wb = std::max(wb, lv_wmax[l]);
+      hb = std::max(hb, lv_hmax[l]);
+    }
+    G.n_fg = 0;
+    if (split == p.nlevels) {
+      int w = 1, h = 1;
+      for (int l = 0; l < p.nlevels; l++) {
+        w = std::max(w, lv_wmax[l]);
+        h = std::max(h, lv_hmax[l]);
+      }
+      layout(w, h, G.fg[0]);
+      G.fg[0].c0 = 0;
+      G.fg[0].c1 = (int)P.cells.size();
+      G.n_fg = 1;
+    } else {
+      layout(wa, ha, G.fg[0]);
+      G.fg[0].c0 = 0;
+      G.fg[0].c1 = G.lv[split].cell_begin;
+      layout(wb, hb, G.fg[1]);
+      G.fg[1].c0 = G.lv[split].cell_begin;
+      G.fg[1].c1 = (int)P.cells.size();
+      G.n_fg = 2;
+    }
+  }
   // k_resize staging bound: source footprint of every 128x16 output tile
   G.rz_rows = 1;
   G.rz_stride = 16;

@@ -499,15 +499,15 @@ __device__ unsigned int* fast_probe_buf;
 // RP: region rows per compass instruction (2 when the widest cell fits 32 lanes)
 template <int S, int RP>
 __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
-                                             BatchPtrs B) {
-  // dynamic LDS sized by the plan's largest cell (G->fast_*)
+                                             BatchPtrs B, int grp) {
+  // dynamic LDS sized by the launch group's largest cell (G->fg[grp])
   extern __shared__ __align__(16) uint8_t fast_smem[];
+  const int tile_bytes = G->fg[grp].tile_bytes, map_bytes = G->fg[grp].map_bytes;
   uint8_t* tile = fast_smem;
-  uint8_t* smap = fast_smem + G->fast_tile_bytes;
-  uint16_t* list = (uint16_t*)(fast_smem + G->fast_tile_bytes + G->fast_map_bytes);
-  const int map_bytes = G->fast_map_bytes;
+  uint8_t* smap = fast_smem + tile_bytes;
+  uint16_t* list = (uint16_t*)(fast_smem + tile_bytes + map_bytes);
   const int2 bi = xcd_block2();
-  const int cell = bi.x, img = bi.y, lane = threadIdx.x;
+  const int cell = G->fg[grp].c0 + bi.x, img = bi.y, lane = threadIdx.x;
   const CellInfo c = cells[cell];
   const int lw = c.lw;
   const uint8_t* lvl = c.level == 0 ? B.in + (size_t)img * B.in_pitch : B.pyr + (size_t)img * G->pyr_bytes + c.loff;
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   FAST_TS(0);
   // 1. window -> LDS: lane = (row, 16-B chunk); window pixel (r, col) lands at tile[r*S + col]
   {
-    constexpr int CPR = S / 16, RPI = 64 / CPR;
+    constexpr int CPR = (S + 15) / 16, RPI = 64 / CPR;
     constexpr int KMAX = (kMaxCell + 6 + RPI - 1) / RPI;
     const int lr = lane / CPR, lj = lane - lr * CPR;
     const bool lane_ok = lr < RPI;
@@ -540,8 +540,14 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
       const int r = k * RPI + lr;
-      if (k * RPI < TH && lane_ok && r < TH)
-        *(uint4*)(tile + r * S + 16 * lj) = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
+      if (k * RPI < TH && lane_ok && r < TH) {
+        if constexpr (S % 16 == 0) {
+          *(uint4*)(tile + r * S + 16 * lj) = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
+        } else {  // 8-B aligned rows: the chunk as two halves, the part past the stride dropped
+          if (16 * lj + 8 <= S) *(uint2*)(tile + r * S + 16 * lj) = make_uint2(v[k][0], v[k][1]);
+          if (16 * lj + 16 <= S) *(uint2*)(tile + r * S + 16 * lj + 8) = make_uint2(v[k][2], v[k][3]);
+        }
+      }
     }
   }
   __syncthreads();
@@ -789,6 +795,16 @@ __device__ __forceinline__ void oct_cands(int T, const OctCands& c, F f) {
   }
 }
 
+// Phase probe (build with -DORBX_OCT_PROBE only; tools/oct_probe.py): per block, s_memtime ticks
+// of the candidate load, the roots, the phase-1 and phase-2 rounds (with their counts) and the
+// best-response pass, plus the level's candidate count; 8 words per block, indexed img * nlevels + l.
+#ifdef ORBX_OCT_PROBE
+__device__ unsigned int* oct_probe_buf;
+#define OCT_TS(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define OCT_TS(v)
+#endif
+
 __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k_octree(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                                BatchPtrs B) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -822,6 +838,11 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   const size_t kbase = (size_t)img * G->cand_total + L.cand_begin;
   OctCands oc{s.kp, s.kn, G->oct_kcap, B.kpos + kbase, (uint32_t*)B.knode + kbase};
 
+  OCT_TS(ot0);
+#ifdef ORBX_OCT_PROBE
+  unsigned long long ot_p1 = 0, ot_p2 = 0;
+  int n_p1 = 0, n_p2 = 0;
+#endif
   // 1. candidates of this level in vToDistributeKeys order (cells row-major)
   const int ncl = L.cell_end - L.cell_begin;
   for (int c = tid; c < ncl; c += OBS) s.cpre[c] = B.cell_count[(size_t)img * G->ncells + L.cell_begin + c];
@@ -859,6 +880,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     oc.set(k, pos, nd);
   }
   __syncthreads();
+  OCT_TS(ot1);
   // 2. roots -> list (empty roots erased, src/ORBextractor.cc:604-615)
   for (int i = tid; i < nIni; i += OBS) s.sa[i] = s.ccnt[i] > 0 ? 1 : 0;
   __syncthreads();
@@ -881,12 +903,27 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   // round's opening barrier (here, and after each round's remap): one barrier
   // per round fewer than a separate clear
   for (int i = tid; i < S * 4; i += OBS) s.ccnt[i] = 0;
+  OCT_TS(ot2);
   int cur = 0;
   int seqBase = nIni;
   int phase = 1;
   const int N = L.nfeat;
   for (int round = 0; round < 256; round++) {
     __syncthreads();
+#ifdef ORBX_OCT_PROBE
+    const unsigned long long rt0 = __builtin_amdgcn_s_memtime();
+    const int rphase = phase;
+    struct RoundStamp {
+      unsigned long long t0;
+      int ph;
+      unsigned long long *p1, *p2;
+      int *n1, *n2;
+      __device__ ~RoundStamp() {
+        const unsigned long long d = __builtin_amdgcn_s_memtime() - t0;
+        if (ph == 1) { *p1 += d; ++*n1; } else { *p2 += d; ++*n2; }
+      }
+    } rstamp{rt0, rphase, &ot_p1, &ot_p2, &n_p1, &n_p2};
+#endif
     const int nb = cur ^ 1;
     // kp pass A: child digit of every keypoint whose node splits (count > 1)
     oct_cands(T, oc, [&](int, uint32_t v, uint32_t& nd) {
@@ -1080,6 +1117,20 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     oct_out[i] = ((uint32_t)(key >> 56) << 24) | (uint32_t)(key & 0xFFFFFF);
   }
   if (tid == 0) *oct_cnt = nout;
+#ifdef ORBX_OCT_PROBE
+  if (tid == 0 && oct_probe_buf) {
+    const unsigned long long ot3 = __builtin_amdgcn_s_memtime();
+    unsigned int* o = oct_probe_buf + ((size_t)img * G->nlevels + l) * 8;
+    o[0] = (unsigned int)(ot1 - ot0);
+    o[1] = (unsigned int)(ot2 - ot1);
+    o[2] = (unsigned int)ot_p1;
+    o[3] = (unsigned int)n_p1;
+    o[4] = (unsigned int)ot_p2;
+    o[5] = (unsigned int)n_p2;
+    o[6] = (unsigned int)(ot3 - ot0);
+    o[7] = (unsigned int)T;
+  }
+#endif
 }
 
 // --------------------------------------------------------------- describe
@@ -1288,8 +1339,14 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   }
   if (Gh.ncells > 0) {
     T->begin(st);
-    auto kf = Gh.fast_s == 48 ? (Gh.fast_rp == 2 ? k_fast<48, 2> : k_fast<48, 1>) : k_fast<80, 1>;
-    hipLaunchKernelGGL(kf, dim3(Gh.ncells, n_img), dim3(64), Gh.fast_smem, st, Gd, cells, B);
+    for (int g = 0; g < Gh.n_fg; g++) {
+      const Geometry::FastGroup& F = Gh.fg[g];
+      if (F.c1 <= F.c0) continue;
+      auto kf = F.s == 40   ? (F.rp == 2 ? k_fast<40, 2> : k_fast<40, 1>)
+                : F.s == 48 ? (F.rp == 2 ? k_fast<48, 2> : k_fast<48, 1>)
+                            : k_fast<80, 1>;
+      hipLaunchKernelGGL(kf, dim3(F.c1 - F.c0, n_img), dim3(64), F.smem, st, Gd, cells, B, g);
+    }
     T->end(ST_FAST, st);
   } else {
     (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
@@ -1318,6 +1375,12 @@ hipError_t octree_set_smem_limit(size_t bytes) {
 
 }  // namespace orbx
 
+#ifdef ORBX_OCT_PROBE
+extern "C" int orbx_debug_oct_probe(void* d_buf) {  // device buffer of 8 u32 per (image, level) block, or NULL
+  unsigned int* p = (unsigned int*)d_buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(orbx::oct_probe_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#endif
 #ifdef ORBX_FAST_PROBE
 extern "C" int orbx_debug_fast_probe(void* d_buf) {  // device buffer of 8 u32 per cell wave, or NULL
   unsigned int* p = (unsigned int*)d_buf;

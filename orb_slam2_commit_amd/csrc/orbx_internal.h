@@ -45,9 +45,13 @@ struct Geometry {
   int node_cap;   // octree LDS node capacity (max over levels, multiple of 64)
   int cell_cap;   // max cells in one level
   int oct_kcap;   // octree: candidates of a level kept in LDS (the rest in global scratch)
-  int fast_s;      // k_fast: LDS row stride of the window tile and the score map (48 or 80)
-  int fast_rp;     // k_fast: region rows per compass instruction (2 when every cell is <= 32 wide)
-  int fast_tile_bytes, fast_map_bytes, fast_smem;  // k_fast dynamic LDS layout (sized by the largest cell)
+  // k_fast launch groups (consecutive cell ranges, one launch each) with their LDS layout, sized by
+  // the group's largest cell: row stride s of the window tile and the score map (40, 48 or 80),
+  // region rows per compass instruction rp (2 when the group's cells are <= 32 wide)
+  struct FastGroup {
+    int c0, c1, s, rp, tile_bytes, map_bytes, smem;
+  } fg[2];
+  int n_fg;
   int rz_rows;    // k_resize: max source rows staged per 128x16 output tile
   int rz_stride;  // k_resize: LDS row stride of the staged footprint (16-B chunks covering the widest span)
 };
