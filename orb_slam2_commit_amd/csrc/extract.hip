@@ -737,6 +737,9 @@ __host__ __device__ inline size_t octree_smem_bytes(int NC, int cell_cap, int kc
 // (thousands at level 0); 512 threads beat 256 (0.42 -> 0.38 ms per 256 frames),
 // 1024 halves the resident blocks per CU and loses (0.71)
 constexpr int OBS = 512;
+// phase 2 sorts up to this many splittable nodes by rank (M^2 / OBS compares per thread), more by
+// the bitonic network
+constexpr int kOctRankSortMax = 1024;
 
 __device__ __forceinline__ void bitonic_sort_desc(uint64_t* k, int n) {
   for (int size = 2; size <= n; size <<= 1) {
@@ -859,25 +862,40 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   for (int i = tid; i < nIni; i += OBS) s.ccnt[i] = 0;
   __syncthreads();
   const uint32_t* cand = B.cand + (size_t)img * G->cand_total;
-  auto load_cand = [&](int k, uint32_t& pos, uint32_t& nd) {
-    int lo = 0, hi = ncl - 1;  // last c with cpre[c] <= k
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s.cpre[mid] <= k) lo = mid; else hi = mid - 1;
-    }
-    const CellInfo& ci = cells[L.cell_begin + lo];
-    const uint32_t v = cand[ci.cand_off + (k - s.cpre[lo])];
+  auto put_cand = [&](int k, uint32_t v) {
     const int xr = (int)(v & 0xFFF) - minBX, yr = (int)((v >> 12) & 0xFFF) - minBY;
-    pos = (v & 0xFF000000u) | ((uint32_t)yr << 12) | (uint32_t)xr;
+    const uint32_t pos = (v & 0xFF000000u) | ((uint32_t)yr << 12) | (uint32_t)xr;
     int root = (int)((float)xr / hX);
     root = min(max(root, 0), nIni - 1);
-    nd = (uint32_t)root;
+    oc.set(k, pos, (uint32_t)root);
     atomicAdd(&s.ccnt[root], 1);
   };
-  for (int k = tid; k < T; k += OBS) {
-    uint32_t pos, nd;
-    load_cand(k, pos, nd);
-    oc.set(k, pos, nd);
+  if (ncl >= OBS / 2) {
+    // many cells (the dense levels): one thread per cell walks its survivors (candidate
+    // k = cpre[c] + i), four loads in flight at a time
+    for (int c = tid; c < ncl; c += OBS) {
+      const int k0 = s.cpre[c], n = s.cpre[c + 1] - k0;
+      const uint32_t* src = cand + cells[L.cell_begin + c].cand_off;
+      int i = 0;
+      for (; i + 4 <= n; i += 4) {
+        const uint32_t v0 = src[i], v1 = src[i + 1], v2 = src[i + 2], v3 = src[i + 3];
+        put_cand(k0 + i, v0);
+        put_cand(k0 + i + 1, v1);
+        put_cand(k0 + i + 2, v2);
+        put_cand(k0 + i + 3, v3);
+      }
+      for (; i < n; i++) put_cand(k0 + i, src[i]);
+    }
+  } else {
+    // few cells with many survivors each: one thread per candidate, its cell by binary search
+    for (int k = tid; k < T; k += OBS) {
+      int lo = 0, hi = ncl - 1;  // last c with cpre[c] <= k
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s.cpre[mid] <= k) lo = mid; else hi = mid - 1;
+      }
+      put_cand(k, cand[cells[L.cell_begin + lo].cand_off + (k - s.cpre[lo])]);
+    }
   }
   __syncthreads();
   OCT_TS(ot1);
@@ -1015,7 +1033,23 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
         if ((s.cnt + cur * NC)[i] > 1)
           s.key[s.sa[i]] = ((uint64_t)(s.cnt + cur * NC)[i] << 43) | ((uint64_t)(s.seq + cur * NC)[i] << 13) | (uint64_t)i;
       __syncthreads();
-      bitonic_sort_desc(s.key, P2);
+      if (M <= kOctRankSortMax) {
+        // descending order by rank (keys are distinct: they carry the node index): key j goes to
+        // #{keys > key j}; one pass over the M keys per key instead of log2(P2)^2/2 barrier stages
+        uint64_t* tmp = reinterpret_cast<uint64_t*>(s.cidx);  // cidx is rewritten below
+        for (int j = tid; j < M; j += OBS) {
+          const uint64_t x = s.key[j];
+          int r = 0;
+#pragma unroll 4
+          for (int y = 0; y < M; y++) r += s.key[y] > x ? 1 : 0;
+          tmp[r] = x;
+        }
+        __syncthreads();
+        for (int j = tid; j < M; j += OBS) s.key[j] = tmp[j];
+        __syncthreads();
+      } else {
+        bitonic_sort_desc(s.key, P2);
+      }
       if (tid == 0) s.ctrl[1] = M - 1;
       for (int j = tid; j < M; j += OBS) {
         const int n = (int)(s.key[j] & 0x1FFF);

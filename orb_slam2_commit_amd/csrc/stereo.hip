@@ -119,7 +119,10 @@ constexpr int kSadIt = (11 * kSadDw + 63) / 64;
 
 // No LDS: candidate ranges come from the row table, (x, index) pairs from the
 // sorted array, so occupancy is bounded by registers only.
-__global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
+// 8 waves per SIMD: 64 VGPRs (the SAD holds one row group's 22 staged bytes at a time, not all
+// three): 0.539 -> 0.488 ms per step against 79 VGPRs / 6 waves; capping registers without the
+// row-group loop spilled and was slower (0.55-0.60)
+__global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
   __shared__ uint32_t s_sad[SBS / 64][11 * kSadDw];
   const int2 bi = xcd_block2();
   const int f = bi.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -252,22 +255,20 @@ __global__ __launch_bounds__(SBS) void k_stereo_match(StereoArgs A, const Geomet
       };
       const int cL = lpix(w, w);
       const int cR = rpix(w, inc + 2 * w);
-      int pv[3][2 * w + 1], qv[3][2 * w + 1];
-#pragma unroll
+      // one row group at a time: 22 staged bytes live instead of 66 (registers bound occupancy)
+#pragma unroll 1
       for (int k = 0; k < 3; k++) {
         const int dy = min(g + 5 * k, 2 * w);
+        int pv[2 * w + 1], qv[2 * w + 1];
 #pragma unroll
         for (int dx = 0; dx < 2 * w + 1; dx++) {
-          pv[k][dx] = lpix(dy, dx);
-          qv[k][dx] = rpix(dy, inc + w + dx);
+          pv[dx] = lpix(dy, dx);
+          qv[dx] = rpix(dy, inc + w + dx);
         }
-      }
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
         int rowsad = 0;
 #pragma unroll
         for (int dx = 0; dx < 2 * w + 1; dx++) {
-          const int a = pv[k][dx] - cL, c = qv[k][dx] - cR;
+          const int a = pv[dx] - cL, c = qv[dx] - cR;
           rowsad += a > c ? a - c : c - a;
         }
         part += (g + 5 * k < 2 * w + 1) ? rowsad : 0;
