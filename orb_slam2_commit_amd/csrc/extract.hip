@@ -172,54 +172,73 @@ __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, c
   int16_t* hb = (int16_t*)(rz_smem + G->rz_rows * stride);  // [rows][kRzTW]
   const uint8_t* src = level_ptr(*G, B, img, l - 1);
   const int swh = S.w * S.h;
-  // 1. footprint -> LDS
+  // the coefficient entries this thread needs later load first, beside the footprint: every
+  // global load of the block is then in flight before the first wait (they used to trail the
+  // barriers, one round trip each)
+  const int hc = tid & (kRzTW - 1);
+  const ResizeX xc = X[hc < nx ? hc : 0];
+  constexpr int kVIt = kRzTH * (kRzTW / 4) / BS;  // vertical items per thread
+  ResizeY yv[kVIt];
+#pragma unroll
+  for (int k = 0; k < kVIt; k++) {
+    const int i = (tid + k * BS) / (kRzTW / 4);
+    yv[k] = Y[i < ny ? i : 0];
+  }
+  // 1. footprint -> LDS (up to kRzLd chunk loads per thread issued before their LDS stores)
   {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, swh, 0x00020000);
     const int nch = (span + 15) >> 4, total = nrows * nch;
-    for (int q = tid; q < total; q += BS) {
-      const int r = q / nch, c = q - r * nch;
-      const int o = (ry0 + r) * S.w + cx0 + 16 * c;
-      uint32_t v0, v1, v2, v3;
-      if (o + 16 <= swh) {
-        const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-        v0 = t[0];
-        v1 = t[1];
-        v2 = t[2];
-        v3 = t[3];
-      } else {  // last bytes of the level: byte loads, each range-checked (outside -> 0, never used)
-        uint32_t w4[4] = {0, 0, 0, 0};
+    constexpr int kRzLd = 4;
+    for (int q0 = 0; q0 < total; q0 += kRzLd * BS) {
+      uint4 v[kRzLd];
 #pragma unroll
-        for (int b = 0; b < 16; b++)
-          w4[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + b, 0, 0) << (8 * (b & 3));
-        v0 = w4[0];
-        v1 = w4[1];
-        v2 = w4[2];
-        v3 = w4[3];
+      for (int u = 0; u < kRzLd; u++) {
+        const int q = q0 + u * BS + tid;
+        v[u] = make_uint4(0, 0, 0, 0);
+        if (q < total) {
+          const int r = q / nch, c = q - r * nch;
+          const int o = (ry0 + r) * S.w + cx0 + 16 * c;
+          if (o + 16 <= swh) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+            v[u] = make_uint4(t[0], t[1], t[2], t[3]);
+          } else {  // last bytes of the level: byte loads, each range-checked (outside -> 0, never used)
+            uint32_t w4[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int b = 0; b < 16; b++)
+              w4[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + b, 0, 0) << (8 * (b & 3));
+            v[u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          }
+        }
       }
-      *(uint4*)&tin[r * stride + 16 * c] = make_uint4(v0, v1, v2, v3);
+#pragma unroll
+      for (int u = 0; u < kRzLd; u++) {
+        const int q = q0 + u * BS + tid;
+        if (q < total) {
+          const int r = q / nch, c = q - r * nch;
+          *(uint4*)&tin[r * stride + 16 * c] = v[u];
+        }
+      }
     }
   }
   __syncthreads();
   // 2. horizontal pass: thread = one output column, rows strided by BS / kRzTW
-  {
-    const int c = tid & (kRzTW - 1);
-    if (c < nx) {
-      const ResizeX x = X[c];
-      const int s0 = x.sx0 - cx0, s1 = x.sx1 - cx0, a0 = x.a0, a1 = x.a1;
-      for (int r = tid / kRzTW; r < nrows; r += BS / kRzTW) {
-        const uint8_t* t = tin + r * stride;
-        hb[r * kRzTW + c] = (int16_t)((t[s0] * a0 + t[s1] * a1) >> 4);
-      }
+  if (hc < nx) {
+    const int s0 = xc.sx0 - cx0, s1 = xc.sx1 - cx0, a0 = xc.a0, a1 = xc.a1;
+    for (int r = tid / kRzTW; r < nrows; r += BS / kRzTW) {
+      const uint8_t* t = tin + r * stride;
+      hb[r * kRzTW + hc] = (int16_t)((t[s0] * a0 + t[s1] * a1) >> 4);
     }
   }
   __syncthreads();
   // 3. vertical pass: item = (output row, group of 4 columns)
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(B.pyr + (size_t)img * G->pyr_bytes + L.off), (short)0, L.w * L.h, 0x00020000);
-  for (int it = tid; it < ny * (kRzTW / 4); it += BS) {
+#pragma unroll
+  for (int k = 0; k < kVIt; k++) {
+    const int it = tid + k * BS;
     const int i = it / (kRzTW / 4), g = it - i * (kRzTW / 4);
-    if (4 * g >= nx) continue;
-    const ResizeY y = Y[i];
+    if (i >= ny || 4 * g >= nx) continue;
+    const ResizeY y = yv[k];
     const uint32_t B0 = (uint32_t)y.b0 << 16, B1 = (uint32_t)y.b1 << 16;
     const uint2 p0 = *(const uint2*)&hb[(y.sy0 - ry0) * kRzTW + 4 * g];
     const uint2 p1 = *(const uint2*)&hb[(y.sy1 - ry0) * kRzTW + 4 * g];
