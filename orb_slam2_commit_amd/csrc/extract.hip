@@ -1231,8 +1231,9 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   const int2 bi = xcd_block2();
   const int img = bi.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  s_pat[threadIdx.x] = reinterpret_cast<const float4*>(c_pattern_f)[threadIdx.x];
-  __syncthreads();
+  // the pattern's load is issued beside the level counts' and staged after them, so the block's
+  // barrier waits for both round trips at once (it used to wait for the pattern alone first)
+  const float4 patv = reinterpret_cast<const float4*>(c_pattern_f)[threadIdx.x];
   const int i = __builtin_amdgcn_readfirstlane(bi.x * (BS / 64) + wv);
   const int nl = G->nlevels;
   // level of keypoint i: per-level counts as independent scalar loads, then an
@@ -1251,6 +1252,8 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
     total += cnt[ll];
   }
   if (bi.x == 0 && threadIdx.x == 0) counts[img] = total;
+  s_pat[threadIdx.x] = patv;
+  __syncthreads();
   if (i >= total) return;  // wave-uniform: the DPP sums below see a full wave
   const LevelGeom& L = G->lv[l];
   const uint32_t v = B.oct[(size_t)img * G->oct_total + L.oct_off + (i - first)];
