@@ -370,19 +370,26 @@ __device__ inline void jacobian(const SE3& T, const orbx_pose_problem& P, const 
   J[17] = J[5] - bf * iz2;
 }
 
-// sequential sum of column j over rows 0..m-1 (row stride kRow): the g2o
-// insertion-order accumulation, one chain per lane, loads kept in flight.
-__device__ inline double chain_sum(const double* __restrict__ base, int m, double init) {
-  double s = init;
+// LDS staging of the per-edge terms for the insertion-order sums: a chunk of kCh edges' 21 H
+// (upper) + 6 b terms + the chi term at an odd row stride (kTs: lanes of the summing wave read
+// consecutive doubles; the writers' 29-double stride spreads over the banks), summed chunk by
+// chunk by one lane per entry.  The sums used to read the rows back from global scratch, 8 loads
+// in flight per lane: ~700 cycles per 8 links of the chain.
+constexpr int kCh = PBS;
+constexpr int kTerm = 28, kTs = 29;
+constexpr int kChiCh = kCh * kTs;  // chi terms per trial pass (one double each)
+
+// sequential sum of m LDS values at stride st, 8 loads in flight (insertion order kept)
+__device__ inline double lds_chain(const double* base, int m, int st, double s, bool sub) {
   int k = 0;
   for (; k + 8 <= m; k += 8) {
     double v[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) v[u] = base[(size_t)(k + u) * kRow];
+    for (int u = 0; u < 8; u++) v[u] = base[(k + u) * st];
 #pragma unroll
-    for (int u = 0; u < 8; u++) s += v[u];
+    for (int u = 0; u < 8; u++) s = sub ? s - v[u] : s + v[u];
   }
-  for (; k < m; k++) s += base[(size_t)k * kRow];
+  for (; k < m; k++) s = sub ? s - base[k * st] : s + base[k * st];
   return s;
 }
 
@@ -396,6 +403,7 @@ struct Shared {
 
 __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __restrict__ probs) {
   __shared__ Shared S;
+  __shared__ double sterm[kCh * kTs];
   const PoseDev& D = probs[blockIdx.x];
   const orbx_pose_problem& P = D.p;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -448,60 +456,60 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
     if (nact > 0) {
       for (int iter = 0; iter < 10; iter++) {
         its++;
-        // computeActiveErrors + activeRobustChi2 (currentChi)
+        // computeActiveErrors + activeRobustChi2 (currentChi) and buildSystem's terms, a chunk of
+        // kCh active edges at a time into LDS, each summed in insertion order by its own lane
         const bool robust = S.robust;
         const SE3 T = S.T;
-        for (int k = tid; k < nact; k += PBS) {
-          const int i = act[k];
-          const Edge e = load_edge(P, i);
-          double err[3];
-          edge_error(T, P, e, err);
-          double* row = scr + (size_t)k * kRow;
-          row[27] = err[0];
-          row[28] = err[1];
-          row[29] = err[2];
-          const double c = chi2_of(e, err);
-          double rho[3];
-          if (robust) huber(e.stereo, c, rho);
-          row[30] = robust ? rho[0] : c;
-          // buildSystem terms (linearizeOplus + constructQuadraticForm)
-          double J[18];
-          jacobian(T, P, e, J);
-          const int Dm = e.stereo ? 3 : 2;
-          double w = e.info, r1 = 1.0;
-          if (robust) {
-            r1 = rho[1];
-            w = rho[1] * e.info;
-          }
-          int q = 0;
-#pragma unroll
-          for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int cc = r; cc < 6; cc++) {
-              double s = (J[r] * w) * J[cc];
-              s = s + (J[6 + r] * w) * J[6 + cc];
-              if (Dm == 3) s = s + (J[12 + r] * w) * J[12 + cc];
-              row[q++] = s;
+        double acc = 0.0;  // wave 0, lanes 0..27: H upper (0..20), b (21..26, -= terms), chi (27)
+        for (int c0 = 0; c0 < nact; c0 += kCh) {
+          const int k = c0 + tid;
+          if (k < nact) {
+            const int i = act[k];
+            const Edge e = load_edge(P, i);
+            double err[3];
+            edge_error(T, P, e, err);
+            double* row = scr + (size_t)k * kRow;  // errors kept for the outlier pass
+            row[27] = err[0];
+            row[28] = err[1];
+            row[29] = err[2];
+            double* tr = sterm + tid * kTs;
+            const double c = chi2_of(e, err);
+            double rho[3];
+            if (robust) huber(e.stereo, c, rho);
+            tr[27] = robust ? rho[0] : c;
+            // buildSystem terms (linearizeOplus + constructQuadraticForm)
+            double J[18];
+            jacobian(T, P, e, J);
+            const int Dm = e.stereo ? 3 : 2;
+            double w = e.info, r1 = 1.0;
+            if (robust) {
+              r1 = rho[1];
+              w = rho[1] * e.info;
             }
+            int q = 0;
 #pragma unroll
-          for (int r = 0; r < 6; r++) {
-            double s = ((r1 * J[r]) * e.info) * err[0];
-            s = s + ((r1 * J[6 + r]) * e.info) * err[1];
-            if (Dm == 3) s = s + ((r1 * J[12 + r]) * e.info) * err[2];
-            row[21 + r] = s;
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+              for (int cc = r; cc < 6; cc++) {
+                double sv = (J[r] * w) * J[cc];
+                sv = sv + (J[6 + r] * w) * J[6 + cc];
+                if (Dm == 3) sv = sv + (J[12 + r] * w) * J[12 + cc];
+                tr[q++] = sv;
+              }
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+              double sv = ((r1 * J[r]) * e.info) * err[0];
+              sv = sv + ((r1 * J[6 + r]) * e.info) * err[1];
+              if (Dm == 3) sv = sv + ((r1 * J[12 + r]) * e.info) * err[2];
+              tr[21 + r] = sv;
+            }
           }
+          __syncthreads();
+          if (wid == 0 && lane < kTerm)
+            acc = lds_chain(sterm + lane, min(kCh, nact - c0), kTs, acc, lane >= 21 && lane < 27);
+          __syncthreads();
         }
-        __threadfence_block();
-        __syncthreads();
-        if (wid == 0 && lane < 28) {
-          // lanes 0..20: H upper triangle; 21..26: b (-= terms); 27: chi
-          const double v = lane == 27 ? chain_sum(scr + 30, nact, 0.0)
-                         : lane < 21 ? chain_sum(scr + lane, nact, 0.0) : 0.0;
-          double bb = 0.0;
-          if (lane >= 21 && lane < 27) {  // b -= t_k in order
-            const double* c = scr + lane;
-            for (int k = 0; k < nact; k++) bb -= c[(size_t)k * kRow];
-          }
+        if (wid == 0 && lane < kTerm) {
           if (lane < 21) {
             int r = 0, c = lane;
             while (c >= 6 - r) {
@@ -509,13 +517,13 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
               r++;
             }
             c += r;
-            S.H[6 * r + c] = v;
-            S.H[6 * c + r] = v;
+            S.H[6 * r + c] = acc;
+            S.H[6 * c + r] = acc;
           } else if (lane < 27) {
-            S.b[lane - 21] = bb;
+            S.b[lane - 21] = acc;
           } else {
-            S.currentChi = v;
-            S.iniChi = v;
+            S.currentChi = acc;
+            S.iniChi = acc;
           }
         }
         __syncthreads();
@@ -545,28 +553,31 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
             if (ok2) S.T = se3_mul(se3_exp(S.x), S.T);
           }
           __syncthreads();
+          double tempChi = 0.0;  // thread 0: activeRobustChi2 at the trial pose, insertion order
           {
             const SE3 Tt = S.T;
             const bool rb = S.robust;
-            for (int k = tid; k < nact; k += PBS) {
-              const int i = act[k];
-              const Edge e = load_edge(P, i);
-              double err[3];
-              edge_error(Tt, P, e, err);
-              double* row = scr + (size_t)k * kRow;
-              row[27] = err[0];
-              row[28] = err[1];
-              row[29] = err[2];
-              const double c = chi2_of(e, err);
-              double rho[3];
-              if (rb) huber(e.stereo, c, rho);
-              row[30] = rb ? rho[0] : c;
+            for (int c0 = 0; c0 < nact; c0 += kChiCh) {
+              for (int k = c0 + tid; k < min(nact, c0 + kChiCh); k += PBS) {
+                const int i = act[k];
+                const Edge e = load_edge(P, i);
+                double err[3];
+                edge_error(Tt, P, e, err);
+                double* row = scr + (size_t)k * kRow;
+                row[27] = err[0];
+                row[28] = err[1];
+                row[29] = err[2];
+                const double c = chi2_of(e, err);
+                double rho[3];
+                if (rb) huber(e.stereo, c, rho);
+                sterm[k - c0] = rb ? rho[0] : c;
+              }
+              __syncthreads();
+              if (tid == 0) tempChi = lds_chain(sterm, min(kChiCh, nact - c0), 1, tempChi, false);
+              __syncthreads();
             }
           }
-          __threadfence_block();
-          __syncthreads();
           if (tid == 0) {
-            double tempChi = chain_sum(scr + 30, nact, 0.0);
             const bool ok2 = S.ok2;
             if (!ok2) tempChi = 1.7976931348623157e308;
             double rho = S.currentChi - tempChi;
