@@ -42,7 +42,7 @@ struct SE3 {
   double t[3];
 };
 
-__device__ inline Quat qmul(const Quat& a, const Quat& b) {
+__device__ __forceinline__ Quat qmul(const Quat& a, const Quat& b) {
   Quat r;
   r.w = a.w * b.w - (a.x * b.x + a.y * b.y + a.z * b.z);
   r.x = a.w * b.x + b.w * a.x + (a.y * b.z - a.z * b.y);
@@ -50,7 +50,7 @@ __device__ inline Quat qmul(const Quat& a, const Quat& b) {
   r.z = a.w * b.z + b.w * a.z + (a.x * b.y - a.y * b.x);
   return r;
 }
-__device__ inline void qrot(const Quat& q, const double v[3], double out[3]) {
+__device__ __forceinline__ void qrot(const Quat& q, const double v[3], double out[3]) {
   double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
   uv[0] += uv[0];
   uv[1] += uv[1];
@@ -59,7 +59,7 @@ __device__ inline void qrot(const Quat& q, const double v[3], double out[3]) {
 #pragma unroll
   for (int i = 0; i < 3; i++) out[i] = v[i] + q.w * uv[i] + c[i];
 }
-__device__ inline void qmat(const Quat& q, double R[9]) {
+__device__ __forceinline__ void qmat(const Quat& q, double R[9]) {
   const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
   const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
   const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
@@ -68,7 +68,7 @@ __device__ inline void qmat(const Quat& q, double R[9]) {
   R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
   R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
-__device__ inline Quat mat2q(const double m[9]) {
+__device__ __forceinline__ Quat mat2q(const double m[9]) {
   Quat q;
   double t = m[0] + m[4] + m[8];
   if (t > 0) {
@@ -81,22 +81,30 @@ __device__ inline Quat mat2q(const double m[9]) {
   } else {
     int i = 0;
     if (m[4] > m[0]) i = 1;
-    if (m[8] > m[3 * i + i]) i = 2;
+    if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
+    // (i, j, k) a cyclic permutation; the entries are picked by value selects, so no array is
+    // indexed at run time (scratch memory otherwise); same arithmetic
+    auto at = [&](int r, int c) {  // m[3r + c] for r, c in {i, j, k}
+      const int o = 3 * r + c;
+      double v = m[0];
+#pragma unroll
+      for (int u = 1; u < 9; u++) v = o == u ? m[u] : v;
+      return v;
+    };
     const int j = (i + 1) % 3, k = (j + 1) % 3;
-    double c[3];
-    t = __builtin_sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
-    c[i] = 0.5 * t;
+    t = __builtin_sqrt(at(i, i) - at(j, j) - at(k, k) + 1.0);
+    const double ci = 0.5 * t;
     t = 0.5 / t;
-    q.w = (m[3 * k + j] - m[3 * j + k]) * t;
-    c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-    c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
-    q.x = c[0];
-    q.y = c[1];
-    q.z = c[2];
+    q.w = (at(k, j) - at(j, k)) * t;
+    const double cj = (at(j, i) + at(i, j)) * t;
+    const double ck = (at(k, i) + at(i, k)) * t;
+    q.x = i == 0 ? ci : j == 0 ? cj : ck;
+    q.y = i == 1 ? ci : j == 1 ? cj : ck;
+    q.z = i == 2 ? ci : j == 2 ? cj : ck;
   }
   return q;
 }
-__device__ inline void qnormalize(Quat& q) {
+__device__ __forceinline__ void qnormalize(Quat& q) {
   if (q.w < 0) {
     q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w;
   }
@@ -104,7 +112,7 @@ __device__ inline void qnormalize(Quat& q) {
   q.x /= n; q.y /= n; q.z /= n; q.w /= n;
 }
 
-__device__ inline void sincos_d(double x, double* s_out, double* c_out) {
+__device__ __forceinline__ void sincos_d(double x, double* s_out, double* c_out) {
   const double kInvPio2 = 6.36619772367581382433e-01;
   const double kPio2Hi = 1.57079632673412561417e+00;
   const double kPio2Lo = 6.07710050650619224932e-11;
@@ -146,7 +154,7 @@ __device__ inline void sincos_d(double x, double* s_out, double* c_out) {
 }
 
 // SE3Quat::exp(update), types/se3quat.h:223-257 (then operator* with T)
-__device__ inline SE3 se3_exp(const double u[6]) {
+__device__ __forceinline__ SE3 se3_exp(const double u[6]) {
   const double w[3] = {u[0], u[1], u[2]}, up[3] = {u[3], u[4], u[5]};
   const double theta = __builtin_sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
   const double O[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
@@ -179,7 +187,7 @@ __device__ inline SE3 se3_exp(const double u[6]) {
   qnormalize(T.q);
   return T;
 }
-__device__ inline SE3 se3_mul(const SE3& a, const SE3& b) {
+__device__ __forceinline__ SE3 se3_mul(const SE3& a, const SE3& b) {
   SE3 r = a;
   double rt[3];
   qrot(a.q, b.t, rt);
@@ -191,88 +199,127 @@ __device__ inline SE3 se3_mul(const SE3& a, const SE3& b) {
 }
 
 // Eigen::LDLT<MatrixXd> (diagonal pivoting) + solve; false when !isPositive().
-__device__ bool ldlt6(const double* Hin, const double* b, double* x) {
+// Every loop is unrolled and the pivot swaps / the permutation of the right-hand side run as
+// unrolled compare-and-swap over the candidate rows, so every index is a compile-time constant:
+// the matrix lives in registers (a runtime index put it in scratch memory, ~25k cycles per call
+// on the LM's serial path).  Same operations in the same order as before.
+// conditional exchange of two registers by value selects (a branch per candidate let the
+// compiler merge the paths into pointer phis, which sends the array to scratch memory)
+__device__ __forceinline__ void cswap(bool sw, double& a, double& b) {
+  const double x = a, y = b;
+  a = sw ? y : x;
+  b = sw ? x : y;
+}
+template <int K, int C>
+__device__ __forceinline__ void ldlt6_swap(double (&m)[36], bool sw) {  // transpositions k <-> c (c > k)
+#pragma unroll
+  for (int j = 0; j < K; j++) cswap(sw, m[6 * K + j], m[6 * C + j]);
+#pragma unroll
+  for (int i = C + 1; i < 6; i++) cswap(sw, m[6 * i + K], m[6 * i + C]);
+  cswap(sw, m[7 * K], m[7 * C]);
+#pragma unroll
+  for (int i = K + 1; i < C; i++) cswap(sw, m[6 * i + K], m[6 * C + i]);
+}
+template <int K, int C>
+__device__ __forceinline__ void ldlt6_swap_to(double (&m)[36], int big) {
+  if constexpr (C < 6) {
+    ldlt6_swap<K, C>(m, big == C);
+    ldlt6_swap_to<K, C + 1>(m, big);
+  }
+}
+template <int K>
+__device__ __forceinline__ void ldlt6_step(double (&m)[36], int (&tr)[6], int& sign, bool& zero) {
+  if constexpr (K < 6) {
+    if (!zero) {
+      int big = K;
+      double bv = __builtin_fabs(m[7 * K]);
+#pragma unroll
+      for (int i = K + 1; i < 6; i++)
+        if (__builtin_fabs(m[7 * i]) > bv) {
+          bv = __builtin_fabs(m[7 * i]);
+          big = i;
+        }
+      if (K == 0 && !(bv > 0.0)) {
+#pragma unroll
+        for (int j = 0; j < 6; j++) tr[j] = j;
+#pragma unroll
+        for (int j = 0; j < 6; j++) m[7 * j] = 0.0;
+        sign = 0;
+        zero = true;
+      } else {
+        tr[K] = big;
+        ldlt6_swap_to<K, K + 1>(m, big);
+        if constexpr (K > 0) {
+          double temp[6];
+#pragma unroll
+          for (int j = 0; j < K; j++) temp[j] = m[7 * j] * m[6 * K + j];
+          double dot = m[6 * K] * temp[0];
+#pragma unroll
+          for (int j = 1; j < K; j++) dot = dot + m[6 * K + j] * temp[j];
+          m[7 * K] -= dot;
+#pragma unroll
+          for (int i = K + 1; i < 6; i++) {
+            double sv = m[6 * i] * temp[0];
+#pragma unroll
+            for (int j = 1; j < K; j++) sv = sv + m[6 * i + j] * temp[j];
+            m[6 * i + K] -= sv;
+          }
+        }
+        const double akk = m[7 * K];
+        if (__builtin_fabs(akk) > 0.0) {
+#pragma unroll
+          for (int i = K + 1; i < 6; i++) m[6 * i + K] /= akk;
+        }
+        if (akk > 0) sign = (sign == 2 || sign == 3) ? 3 : 1;
+        else if (akk < 0) sign = (sign == 1 || sign == 3) ? 3 : 2;
+      }
+    }
+    ldlt6_step<K + 1>(m, tr, sign, zero);
+  }
+}
+// y[k] <-> y[t] for the unrolled k, t >= k (the transposition's other row)
+template <int K>
+__device__ __forceinline__ void perm_swap(double (&y)[6], int t) {
+#pragma unroll
+  for (int c = K + 1; c < 6; c++) cswap(t == c, y[K], y[c]);
+}
+__device__ __forceinline__ bool ldlt6(const double* Hin, const double* b, double* x) {
   double m[36];
 #pragma unroll
   for (int i = 0; i < 36; i++) m[i] = Hin[i];
-  int tr[6];
+  int tr[6] = {0, 1, 2, 3, 4, 5};
   int sign = 0;
-  const int n = 6;
-  for (int k = 0; k < n; k++) {
-    int big = k;
-    double bv = __builtin_fabs(m[7 * k]);
-    for (int i = k + 1; i < n; i++)
-      if (__builtin_fabs(m[7 * i]) > bv) {
-        bv = __builtin_fabs(m[7 * i]);
-        big = i;
-      }
-    if (k == 0 && !(bv > 0.0)) {
-      for (int j = 0; j < n; j++) tr[j] = j;
-      for (int j = 0; j < n; j++) m[7 * j] = 0.0;
-      sign = 0;
-      break;
-    }
-    tr[k] = big;
-    if (k != big) {
-      for (int j = 0; j < k; j++) {
-        const double t = m[6 * k + j];
-        m[6 * k + j] = m[6 * big + j];
-        m[6 * big + j] = t;
-      }
-      for (int i = big + 1; i < n; i++) {
-        const double t = m[6 * i + k];
-        m[6 * i + k] = m[6 * i + big];
-        m[6 * i + big] = t;
-      }
-      {
-        const double t = m[7 * k];
-        m[7 * k] = m[7 * big];
-        m[7 * big] = t;
-      }
-      for (int i = k + 1; i < big; i++) {
-        const double t = m[6 * i + k];
-        m[6 * i + k] = m[6 * big + i];
-        m[6 * big + i] = t;
-      }
-    }
-    double temp[6];
-    if (k > 0) {
-      for (int j = 0; j < k; j++) temp[j] = m[7 * j] * m[6 * k + j];
-      double dot = m[6 * k] * temp[0];
-      for (int j = 1; j < k; j++) dot = dot + m[6 * k + j] * temp[j];
-      m[7 * k] -= dot;
-      for (int i = k + 1; i < n; i++) {
-        double s = m[6 * i] * temp[0];
-        for (int j = 1; j < k; j++) s = s + m[6 * i + j] * temp[j];
-        m[6 * i + k] -= s;
-      }
-    }
-    const double akk = m[7 * k];
-    if (__builtin_fabs(akk) > 0.0)
-      for (int i = k + 1; i < n; i++) m[6 * i + k] /= akk;
-    if (akk > 0) sign = (sign == 2 || sign == 3) ? 3 : 1;
-    else if (akk < 0) sign = (sign == 1 || sign == 3) ? 3 : 2;
-  }
+  bool zero = false;
+  ldlt6_step<0>(m, tr, sign, zero);
   if (!(sign == 1 || sign == 0)) return false;
   double y[6];
-  for (int i = 0; i < n; i++) y[i] = b[i];
-  for (int k = 0; k < n; k++) {
-    const double t = y[k];
-    y[k] = y[tr[k]];
-    y[tr[k]] = t;
-  }
-  for (int i = 0; i < n; i++)
+#pragma unroll
+  for (int i = 0; i < 6; i++) y[i] = b[i];
+  perm_swap<0>(y, tr[0]);
+  perm_swap<1>(y, tr[1]);
+  perm_swap<2>(y, tr[2]);
+  perm_swap<3>(y, tr[3]);
+  perm_swap<4>(y, tr[4]);
+  perm_swap<5>(y, tr[5]);
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
     for (int j = 0; j < i; j++) y[i] -= m[6 * i + j] * y[j];
   const double tol = 2.2250738585072014e-308;  // numeric_limits<double>::min()
-  for (int i = 0; i < n; i++) y[i] = __builtin_fabs(m[7 * i]) > tol ? y[i] / m[7 * i] : 0.0;
-  for (int i = n - 1; i >= 0; i--)
-    for (int j = i + 1; j < n; j++) y[i] -= m[6 * j + i] * y[j];
-  for (int k = n - 1; k >= 0; k--) {
-    const double t = y[k];
-    y[k] = y[tr[k]];
-    y[tr[k]] = t;
-  }
-  for (int i = 0; i < n; i++) x[i] = y[i];
+#pragma unroll
+  for (int i = 0; i < 6; i++) y[i] = __builtin_fabs(m[7 * i]) > tol ? y[i] / m[7 * i] : 0.0;
+#pragma unroll
+  for (int i = 5; i >= 0; i--)
+#pragma unroll
+    for (int j = i + 1; j < 6; j++) y[i] -= m[6 * j + i] * y[j];
+  perm_swap<5>(y, tr[5]);
+  perm_swap<4>(y, tr[4]);
+  perm_swap<3>(y, tr[3]);
+  perm_swap<2>(y, tr[2]);
+  perm_swap<1>(y, tr[1]);
+  perm_swap<0>(y, tr[0]);
+#pragma unroll
+  for (int i = 0; i < 6; i++) x[i] = y[i];
   return true;
 }
 
@@ -287,7 +334,7 @@ struct Edge {
   double obs[3], X[3], info;
 };
 
-__device__ inline Edge load_edge(const orbx_pose_problem& P, int i) {
+__device__ __forceinline__ Edge load_edge(const orbx_pose_problem& P, int i) {
   Edge e;
   e.stereo = P.obs[3 * i + 2] >= 0;
 #pragma unroll
@@ -299,7 +346,7 @@ __device__ inline Edge load_edge(const orbx_pose_problem& P, int i) {
   return e;
 }
 
-__device__ inline void edge_error(const SE3& T, const orbx_pose_problem& P, const Edge& e, double err[3]) {
+__device__ __forceinline__ void edge_error(const SE3& T, const orbx_pose_problem& P, const Edge& e, double err[3]) {
   double Pc[3];
   qrot(T.q, e.X, Pc);
 #pragma unroll
@@ -320,14 +367,14 @@ __device__ inline void edge_error(const SE3& T, const orbx_pose_problem& P, cons
   }
 }
 
-__device__ inline double chi2_of(const Edge& e, const double err[3]) {
+__device__ __forceinline__ double chi2_of(const Edge& e, const double err[3]) {
   double s = err[0] * (e.info * err[0]);
   s += err[1] * (e.info * err[1]);
   if (e.stereo) s += err[2] * (e.info * err[2]);
   return s;
 }
 
-__device__ inline void huber(bool stereo, double chi, double rho[3]) {
+__device__ __forceinline__ void huber(bool stereo, double chi, double rho[3]) {
   const float dm = __builtin_sqrtf(5.991f), ds = __builtin_sqrtf(7.815f);
   const double delta = stereo ? ds : dm;
   const float dsqr = (float)(delta * delta);
@@ -343,7 +390,7 @@ __device__ inline void huber(bool stereo, double chi, double rho[3]) {
   }
 }
 
-__device__ inline void jacobian(const SE3& T, const orbx_pose_problem& P, const Edge& e, double J[18]) {
+__device__ __forceinline__ void jacobian(const SE3& T, const orbx_pose_problem& P, const Edge& e, double J[18]) {
   double Pc[3];
   qrot(T.q, e.X, Pc);
 #pragma unroll
@@ -379,17 +426,26 @@ constexpr int kCh = PBS;
 constexpr int kTerm = 28, kTs = 29;
 constexpr int kChiCh = kCh * kTs;  // chi terms per trial pass (one double each)
 
-// sequential sum of m LDS values at stride st, 8 loads in flight (insertion order kept)
-__device__ inline double lds_chain(const double* base, int m, int st, double s, bool sub) {
-  int k = 0;
-  for (; k + 8 <= m; k += 8) {
-    double v[8];
+// sequential sum of m LDS values at stride st (insertion order kept), software-pipelined: the next
+// 8 values load while the current 8 are added, so the chain runs at the add latency
+__device__ __forceinline__ double lds_chain(const double* base, int m, int st, double s, bool sub) {
+  const int m8 = m & ~7;
+  double v[8];
+  if (m8 > 0) {
 #pragma unroll
-    for (int u = 0; u < 8; u++) v[u] = base[(k + u) * st];
+    for (int u = 0; u < 8; u++) v[u] = base[u * st];
+  }
+  for (int k = 0; k < m8; k += 8) {
+    double w[8];
+    const int kn = k + 8 < m8 ? k + 8 : k;  // last batch: a harmless reload
+#pragma unroll
+    for (int u = 0; u < 8; u++) w[u] = base[(kn + u) * st];
 #pragma unroll
     for (int u = 0; u < 8; u++) s = sub ? s - v[u] : s + v[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = w[u];
   }
-  for (; k < m; k++) s = sub ? s - base[k * st] : s + base[k * st];
+  for (int k = m8; k < m; k++) s = sub ? s - base[k * st] : s + base[k * st];
   return s;
 }
 
@@ -401,9 +457,28 @@ struct Shared {
   int scan[PBS / 64];
 };
 
+// Phase probe (build with -DORBX_POSE_PROBE only): s_memtime ticks per phase of each block, taken
+// by thread 0 after the phase's closing barrier, into a host-provided buffer of 16 words per block.
+#ifdef ORBX_POSE_PROBE
+__device__ unsigned long long* pose_probe_buf;
+#define POSE_TS(k)                                                    \
+  do {                                                                \
+    if (tid == 0) {                                                   \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+      pacc[k] += t_ - plast;                                          \
+      plast = t_;                                                     \
+    }                                                                 \
+  } while (0)
+#else
+#define POSE_TS(k)
+#endif
+
 __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __restrict__ probs) {
   __shared__ Shared S;
   __shared__ double sterm[kCh * kTs];
+#ifdef ORBX_POSE_PROBE
+  unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, plast = __builtin_amdgcn_s_memtime();
+#endif
   const PoseDev& D = probs[blockIdx.x];
   const orbx_pose_problem& P = D.p;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -452,6 +527,7 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
     const int nact = base;
     __threadfence_block();
     __syncthreads();
+    POSE_TS(0);
     int its = 0;
     if (nact > 0) {
       for (int iter = 0; iter < 10; iter++) {
@@ -505,9 +581,11 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
             }
           }
           __syncthreads();
+          POSE_TS(1);
           if (wid == 0 && lane < kTerm)
             acc = lds_chain(sterm + lane, min(kCh, nact - c0), kTs, acc, lane >= 21 && lane < 27);
           __syncthreads();
+          POSE_TS(2);
         }
         if (wid == 0 && lane < kTerm) {
           if (lane < 21) {
@@ -527,6 +605,7 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
           }
         }
         __syncthreads();
+        POSE_TS(2);
         if (tid == 0) {
           if (iter == 0) {
             double m = 0;
@@ -541,18 +620,23 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
           S.qmax = 0;
         }
         __syncthreads();
+        POSE_TS(3);
         // ---- trials ----
         for (;;) {
           if (tid == 0) {
             S.bak = S.T;
-            double Hd[36];
+            double Hd[36];  // registers: every index static
+#pragma unroll
             for (int j = 0; j < 36; j++) Hd[j] = S.H[j];
+#pragma unroll
             for (int j = 0; j < 6; j++) Hd[7 * j] += S.lambda;
             const bool ok2 = ldlt6(Hd, S.b, S.x);
             S.ok2 = ok2;
+            POSE_TS(9);
             if (ok2) S.T = se3_mul(se3_exp(S.x), S.T);
           }
           __syncthreads();
+          POSE_TS(4);
           double tempChi = 0.0;  // thread 0: activeRobustChi2 at the trial pose, insertion order
           {
             const SE3 Tt = S.T;
@@ -573,8 +657,10 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
                 sterm[k - c0] = rb ? rho[0] : c;
               }
               __syncthreads();
+              POSE_TS(5);
               if (tid == 0) tempChi = lds_chain(sterm, min(kChiCh, nact - c0), 1, tempChi, false);
               __syncthreads();
+              POSE_TS(6);
             }
           }
           if (tid == 0) {
@@ -603,6 +689,7 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
             S.go = (rho < 0 && S.qmax < 10);
           }
           __syncthreads();
+          POSE_TS(7);
           if (!S.go) break;
         }
         if (tid == 0) {
@@ -616,6 +703,7 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
           S.term = term;
         }
         __syncthreads();
+        POSE_TS(7);
         if (S.term) break;
       }
     }
@@ -654,13 +742,19 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
     }
     __threadfence_block();
     __syncthreads();
+    POSE_TS(8);
     for (int i = tid; i < n; i += PBS) P.outlier[i] = scr[(size_t)i * kRow + 31] != 0.0 ? 1 : 0;
     nBad = S.nbad_cls;
     if (it == 2 && tid == 0) S.robust = 0;
     __threadfence_block();
     __syncthreads();
+    POSE_TS(8);
     if (n < 10) break;
   }
+#ifdef ORBX_POSE_PROBE
+  if (tid == 0 && pose_probe_buf)
+    for (int k = 0; k < 10; k++) pose_probe_buf[(size_t)blockIdx.x * 16 + k] = pacc[k];
+#endif
   if (tid == 0) {
     double R[9];
     qmat(S.T.q, R);
@@ -676,6 +770,13 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
 
 }  // namespace pose
 }  // namespace orbx
+
+#ifdef ORBX_POSE_PROBE
+extern "C" int orbx_debug_pose_probe(void* d_buf) {  // device buffer of 16 u64 per block, or NULL
+  unsigned long long* p = (unsigned long long*)d_buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(orbx::pose::pose_probe_buf), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 // ------------------------------------------------------------------ C ABI
 namespace {

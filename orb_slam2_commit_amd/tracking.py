@@ -60,11 +60,16 @@ class TrackBatch:
         sp = C.c_void_p(st.cuda_stream)
         B, cap = self.B, self.cap
         t0 = time.perf_counter()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timings is not None else None
+        if ev:
+            ev[0].record(st)
         # 1. Frame::ComputeBoW on every left image (src/Frame.cc ComputeBoW)
         check(L.orbx_voc_transform_device(self.voc._h, ptr(desc), cap, 2 * cap, ptr(counts), 2, B, self.levelsup,
                                           ptr(self.bow_words), ptr(self.bow_values), ptr(self.n_bow),
                                           ptr(self.fv_nodes), ptr(self.fv_off), ptr(self.fv_feat), ptr(self.n_fv), sp),
               "orbx_voc_transform_device")
+        if ev:
+            ev[1].record(st)
         with torch.cuda.stream(st):
             kp32 = kps.view(torch.float32).reshape(2 * B, cap, 7)
             angle = kp32[:, :, 3].contiguous()  # keypoint angles as the matcher's SoA input
@@ -89,6 +94,8 @@ class TrackBatch:
             probs[j].nnratio, probs[j].check_ori, probs[j].mode = self.nnratio, self.check_ori, 0
             probs[j].match = self.match.data_ptr() + j * cap * es
             probs[j].nmatches = self.nmatch.data_ptr() + j * es
+        if ev:
+            ev[2].record(st)
         check(L.orbx_search_by_bow_device(probs, K, sp), "orbx_search_by_bow_device")
         # 3. the PoseOptimization edges of every pair (src/Optimizer.cc:318-410)
         fx, fy, cx, cy, bf = self.cam
@@ -107,6 +114,8 @@ class TrackBatch:
             g.inv_sigma2, g.edge_feature = self.isig.data_ptr() + j * cap * 4, self.edge_feat.data_ptr() + j * cap * es
             g.n_edges = self.n_edges.data_ptr() + j * es
         check(L.orbx_track_gather_device(gs, K, sp), "orbx_track_gather_device")
+        if ev:
+            ev[3].record(st)
         with torch.cuda.stream(st):
             ne = self.n_edges[:K].cpu().numpy()  # the second readback: edge counts size the pose problems
         t2 = time.perf_counter()
@@ -125,10 +134,17 @@ class TrackBatch:
             p.outlier = self.outlier.data_ptr() + j * cap
             p.ngood = self.ngood.data_ptr() + j * es
             p.iterations = self.iters.data_ptr() + j * 16
+        if ev:
+            ev[4].record(st)
         check(L.orbx_pose_optimization_device(pp, K, sp), "orbx_pose_optimization_device")
+        if ev:
+            ev[5].record(st)
         with torch.cuda.stream(st):
             res = torch.stack([self.nmatch[:K], self.n_edges[:K], self.ngood[:K]]).cpu().numpy()
         t3 = time.perf_counter()
         if timings is not None:
-            timings.append((t1 - t0, t2 - t1, t3 - t2))
+            # host wall per phase (incl. waiting for earlier work on the stream and the readbacks), then
+            # the GPU time of each phase's launches (HIP events on the launch stream)
+            timings.append((t1 - t0, t2 - t1, t3 - t2, ev[0].elapsed_time(ev[1]) / 1e3,
+                            ev[2].elapsed_time(ev[3]) / 1e3, ev[4].elapsed_time(ev[5]) / 1e3))
         return res[0], res[1], res[2]

@@ -46,6 +46,20 @@ def main(batch=1024, n=1000, reps=5, cpu_frames=16):
     e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    if hasattr(L, "orbx_debug_pose_probe"):  # probe build (-DORBX_POSE_PROBE): per-phase ticks per block
+        buf = torch.zeros((batch, 16), dtype=torch.int64, device=dev)
+        L.orbx_debug_pose_probe.argtypes = [C.c_void_p]
+        L.orbx_debug_pose_probe(C.c_void_p(buf.data_ptr()))
+        L.orbx_pose_optimization_device(arr, batch, sp)
+        torch.cuda.synchronize()
+        L.orbx_debug_pose_probe(None)
+        a = buf.cpu().numpy()[:, :10].astype(np.float64)
+        names = ["round init scan", "edge terms", "H/b chains", "lambda init", "exp + mul (thread 0)",
+                 "trial edge errors", "trial chi chain", "LM decision", "outlier pass", "ldlt6 (thread 0)"]
+        tot = a.sum(1).mean()
+        print("ticks per block %.0f" % tot)
+        for k, nm in enumerate(names):
+            print("  %-22s %9.0f  %5.1f %%" % (nm, a[:, k].mean(), 100 * a[:, k].mean() / tot))
     its = [keep[b][1]["iterations"].cpu().numpy().sum() for b in range(16)]
     import oracle
     t0 = time.perf_counter()
