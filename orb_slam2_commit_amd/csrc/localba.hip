@@ -101,17 +101,33 @@ __host__ __device__ inline Quat mat2q(const double m[9]) {
     int i = 0;
     if (m[4] > m[0]) i = 1;
     if (m[8] > m[3 * i + i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    double c[3];
-    t = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
-    c[i] = 0.5 * t;
-    t = 0.5 / t;
-    q.w = (m[3 * k + j] - m[3 * j + k]) * t;
-    c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-    c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
-    q.x = c[0];
-    q.y = c[1];
-    q.z = c[2];
+    // the three cases spelled out on named entries: no array indexed at run time (which put the
+    // matrix in scratch memory); same arithmetic as c[i], c[j], c[k] with (i, j, k) cyclic
+    if (i == 0) {  // (0, 1, 2)
+      t = sqrt(m[0] - m[4] - m[8] + 1.0);
+      const double ci = 0.5 * t;
+      t = 0.5 / t;
+      q.w = (m[7] - m[5]) * t;
+      q.x = ci;
+      q.y = (m[3] + m[1]) * t;
+      q.z = (m[6] + m[2]) * t;
+    } else if (i == 1) {  // (1, 2, 0)
+      t = sqrt(m[4] - m[8] - m[0] + 1.0);
+      const double ci = 0.5 * t;
+      t = 0.5 / t;
+      q.w = (m[2] - m[6]) * t;
+      q.y = ci;
+      q.z = (m[7] + m[5]) * t;
+      q.x = (m[1] + m[3]) * t;
+    } else {  // (2, 0, 1)
+      t = sqrt(m[8] - m[0] - m[4] + 1.0);
+      const double ci = 0.5 * t;
+      t = 0.5 / t;
+      q.w = (m[3] - m[1]) * t;
+      q.z = ci;
+      q.x = (m[2] + m[6]) * t;
+      q.y = (m[5] + m[7]) * t;
+    }
   }
   return q;
 }

@@ -82,25 +82,33 @@ __device__ __forceinline__ Quat mat2q(const double m[9]) {
     int i = 0;
     if (m[4] > m[0]) i = 1;
     if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
-    // (i, j, k) a cyclic permutation; the entries are picked by value selects, so no array is
-    // indexed at run time (scratch memory otherwise); same arithmetic
-    auto at = [&](int r, int c) {  // m[3r + c] for r, c in {i, j, k}
-      const int o = 3 * r + c;
-      double v = m[0];
-#pragma unroll
-      for (int u = 1; u < 9; u++) v = o == u ? m[u] : v;
-      return v;
-    };
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    t = __builtin_sqrt(at(i, i) - at(j, j) - at(k, k) + 1.0);
-    const double ci = 0.5 * t;
-    t = 0.5 / t;
-    q.w = (at(k, j) - at(j, k)) * t;
-    const double cj = (at(j, i) + at(i, j)) * t;
-    const double ck = (at(k, i) + at(i, k)) * t;
-    q.x = i == 0 ? ci : j == 0 ? cj : ck;
-    q.y = i == 1 ? ci : j == 1 ? cj : ck;
-    q.z = i == 2 ? ci : j == 2 ? cj : ck;
+    // the three cases spelled out on named entries: no array indexed at run time (which put the
+    // matrix in scratch memory); same arithmetic as c[i], c[j], c[k] with (i, j, k) cyclic
+    if (i == 0) {  // (0, 1, 2)
+      t = __builtin_sqrt(m[0] - m[4] - m[8] + 1.0);
+      const double ci = 0.5 * t;
+      t = 0.5 / t;
+      q.w = (m[7] - m[5]) * t;
+      q.x = ci;
+      q.y = (m[3] + m[1]) * t;
+      q.z = (m[6] + m[2]) * t;
+    } else if (i == 1) {  // (1, 2, 0)
+      t = __builtin_sqrt(m[4] - m[8] - m[0] + 1.0);
+      const double ci = 0.5 * t;
+      t = 0.5 / t;
+      q.w = (m[2] - m[6]) * t;
+      q.y = ci;
+      q.z = (m[7] + m[5]) * t;
+      q.x = (m[1] + m[3]) * t;
+    } else {  // (2, 0, 1)
+      t = __builtin_sqrt(m[8] - m[0] - m[4] + 1.0);
+      const double ci = 0.5 * t;
+      t = 0.5 / t;
+      q.w = (m[3] - m[1]) * t;
+      q.z = ci;
+      q.x = (m[2] + m[6]) * t;
+      q.y = (m[5] + m[7]) * t;
+    }
   }
   return q;
 }
