@@ -385,6 +385,7 @@ struct orbx_extractor {
   DevBuf<int2> rxi;
   DevBuf<uint4> rdesc;
   DevBuf<uint32_t> rtab;
+  DevBuf<uint4> lrange;
   DevBuf<int> oct_start, sad;
   DevBuf<float> sres;  // orbx_stereo_match: uRight | depth, adjacent (one copy back)
   DevBuf<int32_t> nmatch;
@@ -686,6 +687,7 @@ static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_fram
   chk(h->rxi.ensure((size_t)n_frames * kMaxStereoKps));
   chk(h->rdesc.ensure((size_t)n_frames * kMaxStereoKps * 2));
   chk(h->rtab.ensure((size_t)n_frames * P->G.nlevels * std::max(P->G.height, 1)));
+  chk(h->lrange.ensure((size_t)n_frames * std::max(maxL, 1)));
   chk(h->sad.ensure((size_t)n_frames * out_stride));
   if (e != hipSuccess) return ORBX_ERR_HIP;
   StereoArgs A;
@@ -722,6 +724,7 @@ static orbx_status run_stereo(orbx_extractor* hl, orbx_extractor* hr, int n_fram
   A.rxi = h->rxi.p;
   A.rdesc = h->rdesc.p;
   A.rtab = h->rtab.p;
+  A.lrange = h->lrange.p;
   A.rows = std::max(P->G.height, 1);
   A.nmatches = nmatches;
   return hip_status(launch_stereo(A, P->dG.p, n_frames, maxL, st, &h->timer));

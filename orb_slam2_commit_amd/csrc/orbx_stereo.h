@@ -32,6 +32,7 @@ struct StereoArgs {
   int2* rxi;        // [n_frames * kMaxStereoKps]: (float bits of x, index) in (octave, y) order
   uint4* rdesc;     // [n_frames * kMaxStereoKps * 2]: right descriptors in the same sorted order
   uint32_t* rtab;   // [n_frames * nlevels * rows]: candidate range start | end << 16 per (octave, row)
+  uint4* lrange;    // [n_frames * maxL]: per left keypoint its rtab entries of octaves level-1..level+1 (0: none)
   int rows;         // rows of the row table = level-0 image height (vRowIndices size)
   int32_t* nmatches;
 };

@@ -108,6 +108,24 @@ __global__ __launch_bounds__(PBS) void k_stereo_prep(StereoArgs A, const Geometr
     }
     tab[e] = (uint32_t)a | ((uint32_t)c << 16);
   }
+  // each left keypoint's three candidate ranges (vRowIndices[vL] of octaves level-1..level+1), so
+  // the match kernel loads them beside the keypoint instead of after it (one dependent round trip
+  // fewer per keypoint)
+  __syncthreads();
+  const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
+  const orbx_keypoint* kL = A.kpL + (size_t)f * A.kL_stride;
+  uint4* lr = A.lrange + (size_t)f * A.maxL;
+  for (int i = tid; i < nL; i += PBS) {
+    const orbx_keypoint kp = kL[i];
+    const int Y = (int)kp.y;
+    uint32_t t[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const int o = kp.octave - 1 + q;
+      t[q] = (o >= 0 && o < A.nlevels && Y >= 0 && Y < A.rows) ? tab[(size_t)o * A.rows + Y] : 0u;
+    }
+    lr[i] = make_uint4(t[0], t[1], t[2], 0u);
+  }
 }
 
 // 16 left keypoints per 4-wave block (4 per wave): 128 per block left the
@@ -131,16 +149,14 @@ __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geo
   if (base >= nL) return;
   const int2* rxi = A.rxi + (size_t)f * kMaxStereoKps;
   const uint4* rdR = A.rdesc + (size_t)f * kMaxStereoKps * 2;
-  const uint32_t* tab = A.rtab + (size_t)f * A.nlevels * A.rows;
   const orbx_keypoint* kL = A.kpL + (size_t)f * A.kL_stride;
   const uint8_t* dL = A.dL + (size_t)f * A.kL_stride * 32;
   const int limg = f * A.l_step + A.l_off, rimg = f * A.r_step + A.r_off;
-  const int nl = G->nlevels;
   for (int iL = base + wid; iL < min(nL, base + kKpsPerBlock); iL += SBS / 64) {
     const orbx_keypoint kp = kL[iL];
+    const uint4 lrg = A.lrange[(size_t)f * A.maxL + iL];  // issued beside the keypoint (k_stereo_prep)
     const int levelL = kp.octave;
-    const float vL = kp.y, uL = kp.x;
-    const int Y = (int)vL;
+    const float uL = kp.x;
     const float minU = uL - A.maxD, maxU = uL - A.minD;
     float* outU = A.uR + (size_t)f * A.out_stride + iL;
     float* outD = A.depth + (size_t)f * A.out_stride + iL;
@@ -152,16 +168,12 @@ __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geo
     }
     if (maxU < 0) continue;
     // candidate ranges per octave (vRowIndices[vL], octaves levelL-1..levelL+1)
+    const uint32_t t3[3] = {lrg.x, lrg.y, lrg.z};
     int rb[3], re[3];
 #pragma unroll
     for (int q = 0; q < 3; q++) {
-      rb[q] = re[q] = 0;
-      const int o = levelL - 1 + q;
-      if (o >= 0 && o < nl && Y >= 0 && Y < A.rows) {
-        const uint32_t t = tab[(size_t)o * A.rows + Y];
-        rb[q] = (int)(t & 0xFFFF);
-        re[q] = (int)(t >> 16);
-      }
+      rb[q] = (int)(t3[q] & 0xFFFF);
+      re[q] = (int)(t3[q] >> 16);
     }
     const int n0 = re[0] - rb[0], n1 = re[1] - rb[1], n2 = re[2] - rb[2];
     const int K = n0 + n1 + n2;
