@@ -273,6 +273,8 @@ struct BaDev {
   unsigned long long* dbg;  // optional phase timestamps (debug probe only)
   double* dmax_c;  // nposes
   int* pos_pt;     // na: active point index of position k
+  int* pblk;       // nbf+1: first active point of each fused point-side block (k_ba_lin_schur), or null
+  int nbf;         // fused point-side blocks (0: the unfused kernels run)
   double* gpart;   // chunk partials of the pose-list gathers (summed by the *_fin kernels)
   int gsplit;      // chunks per pose list in the gather kernels
   int nbe;         // k_ba_errors blocks; scal[8..] holds its block partials (2 slots), then k_ba_update's
@@ -552,14 +554,14 @@ __device__ __forceinline__ void lin_cross_terms(const LinTerms& T, const double*
     }
 }
 
-__device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
-  if (lm_skip_lin(D)) return;
-  __shared__ double sh[LBS * 21];
-  const int k0 = blockIdx.x * LBS, k = k0 + threadIdx.x;
-  if (k0 >= D.na) return;  // block-uniform
-  const int nk = min(LBS, D.na - k0);
-  const bool act = k < D.na;
-  const int e = act ? D.act[k] : D.act[k0];
+// Jacobians (linearizeOplus, types_six_dof_expmap.h:80-141) and robust weights of edge e at the
+// current state: point block A (DIM x 3), pose block Bm (DIM x 6), stereo flag.
+struct LinEdge {
+  double A[9], Bm[18];
+  LinTerms T;
+  bool st;
+};
+__device__ __forceinline__ void lin_edge(const BaDev& D, int e, LinEdge& o) {
   const int c = D.ecam[e], p = D.ept[e];
   Quat q = {D.cq[4 * c], D.cq[4 * c + 1], D.cq[4 * c + 2], D.cq[4 * c + 3]};
   const double Xw[3] = {D.X[3 * p], D.X[3 * p + 1], D.X[3 * p + 2]};
@@ -571,7 +573,9 @@ __device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
   qmat(q, R);
   const double fx = D.intr[5 * c], fy = D.intr[5 * c + 1], bf = D.intr[5 * c + 4];
   const bool st = D.est[e];
-  double A[9], Bm[18] = {};
+  double* A = o.A;
+  double* Bm = o.Bm;
+  for (int i = 0; i < 18; i++) Bm[i] = 0.0;
   if (!st) {
     const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
     for (int r = 0; r < 2; r++)
@@ -604,15 +608,28 @@ __device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
     Bm[16] = 0;
     Bm[17] = Bm[5] - bf / z_2;
   }
-  const LinTerms T = st ? lin_weights<3>(D, e) : lin_weights<2>(D, e);
+  o.st = st;
+  o.T = st ? lin_weights<3>(D, e) : lin_weights<2>(D, e);
+}
+
+__device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
+  if (lm_skip_lin(D)) return;
+  __shared__ double sh[LBS * 21];
+  const int k0 = blockIdx.x * LBS, k = k0 + threadIdx.x;
+  if (k0 >= D.na) return;  // block-uniform
+  const int nk = min(LBS, D.na - k0);
+  const bool act = k < D.na;
+  const int e = act ? D.act[k] : D.act[k0];
+  LinEdge L;
+  lin_edge(D, e, L);
   lin_stage_store<12, 1>(sh, D.ptc, k0, nk, act, [&](double* o) {
-    if (st) lin_point_terms<3>(T, A, o); else lin_point_terms<2>(T, A, o);
+    if (L.st) lin_point_terms<3>(L.T, L.A, o); else lin_point_terms<2>(L.T, L.A, o);
   });
   lin_stage_store<18, 1>(sh, D.Hpl, k0, nk, act, [&](double* o) {
-    if (st) lin_cross_terms<3>(T, A, Bm, o); else lin_cross_terms<2>(T, A, Bm, o);
+    if (L.st) lin_cross_terms<3>(L.T, L.A, L.Bm, o); else lin_cross_terms<2>(L.T, L.A, L.Bm, o);
   });
   lin_stage_store<42, 2>(sh, D.cmc, k0, nk, act, [&](double* o) {
-    if (st) lin_pose_terms<3>(T, Bm, o); else lin_pose_terms<2>(T, Bm, o);
+    if (L.st) lin_pose_terms<3>(L.T, L.Bm, o); else lin_pose_terms<2>(L.T, L.Bm, o);
   });
 }
 __global__ __launch_bounds__(LBS) void k_ba_linearize(BaDev D) { k_ba_linearize_body(D); }
@@ -739,8 +756,8 @@ __global__ __launch_bounds__(64) void k_ba_cam_fin_many(const BaDev* __restrict_
 
 // One thread per active edge position: D = Hll + lambda I of its point,
 // Dinv (stored once per point), BD_e = Hpl_e Dinv, cf_e = Hpl_e Dinv bl.
-__device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lambda) {
-  if (lm_skip(D)) return;
+__device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lambda, int skip_relin = 0) {
+  if (lm_skip(D) || (skip_relin && !lm_skip_lin(D))) return;  // skip_relin: k_ba_lin_schur ran this trial
   lambda = lm_lambda(D, lambda);
   // the block's 256 positions are contiguous: Hpl comes in and BD / cf go out
   // through LDS with coalesced 8-B accesses (per-lane 144-B strides made every
@@ -785,9 +802,116 @@ __device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lam
   for (int j = t; j < nk * 18; j += LBS) D.BD[18 * (size_t)k0 + j] = sh[j];
   for (int j = t; j < nk * 6; j += LBS) D.cf[6 * (size_t)k0 + j] = scf[j];
 }
-__global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) { k_ba_point_schur_body(D, lambda); }
+__global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda, int skip_relin) {
+  k_ba_point_schur_body(D, lambda, skip_relin);
+}
+
+// ---- the point side of an iteration-start trial in one kernel (device LM, one problem) ----
+// k_ba_linearize -> k_ba_point_sum -> k_ba_point_schur fused: block b takes the whole points
+// pblk[b] .. pblk[b+1] (positions pt_off[pblk[b]] .. pt_off[pblk[b+1]], fewer than kFuseNT: a
+// block's points start inside a kFuseStride-position window and no point has more than
+// kFuseMaxDeg positions, checked at intake).  128-thread blocks with 63 KB of LDS: two per CU, so
+// a config-4 phase's ~450 blocks are all resident at once.  Per position the same linearisation; the point
+// terms stay in LDS and each point's thread sums them in position order (k_ba_point_sum's
+// order), then D = Hll + lambda I, D^-1 (once per point) and B D^-1, B D^-1 b_l per position from
+// the staged Hpl -- bit-identical to the three kernels, without their global round trips.
+constexpr int kFuseNT = 128, kFuseStride = 96, kFuseMaxDeg = 32;
+static_assert(kFuseStride - 1 + kFuseMaxDeg <= kFuseNT, "a fused block's positions fit its threads");
+__global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur(BaDev D) {
+  if (lm_skip_lin(D)) return;
+  constexpr int NT = kFuseNT;
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  double* sptc = fsm;                // NT x 12 point terms; then with sbuf: BD (18) | cf (6) staging
+  double* sbuf = sptc + NT * 12;     // NT x 21: cmc staging (two halves)
+  double* shpl = sbuf + NT * 21;     // NT x 18
+  double* sdi = shpl + NT * 18;      // NT x 12: per point D^-1 (9) and D^-1 b_l (3)
+  double* sout = sptc;               // NT x 24 over sptc + sbuf once the point sums are done
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int p0 = D.pblk[b], p1 = D.pblk[b + 1];
+  const int k0 = D.pt_off[p0], nk = D.pt_off[p1] - k0, npt = p1 - p0;
+  if (nk <= 0) return;  // block-uniform
+  const double lambda = lm_lambda(D, 0.0);
+  const bool act = t < nk;
+  const int k = k0 + (act ? t : 0);
+  LinEdge L;
+  lin_edge(D, D.act[k], L);
+  if (act) {
+    if (L.st) {
+      lin_point_terms<3>(L.T, L.A, sptc + 12 * t);
+      lin_cross_terms<3>(L.T, L.A, L.Bm, shpl + 18 * t);
+    } else {
+      lin_point_terms<2>(L.T, L.A, sptc + 12 * t);
+      lin_cross_terms<2>(L.T, L.A, L.Bm, shpl + 18 * t);
+    }
+  }
+  // pose terms out through LDS in two halves of 21 (coalesced 8-B stores, as k_ba_linearize)
+  double cm[42];
+  if (L.st) lin_pose_terms<3>(L.T, L.Bm, cm); else lin_pose_terms<2>(L.T, L.Bm, cm);
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < 21; j++) sbuf[21 * t + j] = cm[21 * h + j];
+    }
+    __syncthreads();
+    for (int j = t; j < nk * 21; j += NT) {
+      const int kk = j / 21, jj = j - 21 * kk;
+      D.cmc[42 * ((size_t)k0 + kk) + 21 * h + jj] = sbuf[j];
+    }
+    __syncthreads();
+  }
+  for (int j = t; j < nk * 18; j += NT) D.Hpl[18 * (size_t)k0 + j] = shpl[j];
+  // point sums (k_ba_point_sum's order), D^-1 and D^-1 b_l once per point
+  if (t < npt) {
+    const int i = p0 + t;
+    const int a = D.pt_off[i] - k0, e = D.pt_off[i + 1] - k0;
+    double h[12];
+    for (int j = 0; j < 12; j++) h[j] = 0;
+    for (int kk = a; kk < e; kk++)
+      for (int j = 0; j < 12; j++) h[j] += sptc[12 * kk + j];
+    for (int j = 0; j < 9; j++) D.Hll[9 * i + j] = h[j];
+    for (int j = 0; j < 3; j++) D.bl[3 * i + j] = h[9 + j];
+    D.dmax_p[i] = fmax(fmax(fabs(h[0]), fabs(h[4])), fabs(h[8]));
+    double Dm[9];
+    for (int j = 0; j < 9; j++) Dm[j] = h[j];
+    Dm[0] += lambda;
+    Dm[4] += lambda;
+    Dm[8] += lambda;
+    double Di[9];
+    inv3(Dm, Di);
+    for (int j = 0; j < 9; j++) D.Dinv[9 * i + j] = Di[j];
+    const double b0 = h[9], b1 = h[10], b2 = h[11];
+    for (int r = 0; r < 3; r++) sdi[12 * t + 9 + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+    for (int j = 0; j < 9; j++) sdi[12 * t + j] = Di[j];
+  }
+  __syncthreads();
+  if (act) {
+    const double* Di = sdi + 12 * (D.pos_pt[k] - p0);
+    const double* db = Di + 9;
+    const double* B1 = shpl + 18 * t;
+    for (int r = 0; r < 6; r++) {
+      for (int c = 0; c < 3; c++)
+        sout[18 * t + 3 * r + c] = B1[3 * r] * Di[c] + B1[3 * r + 1] * Di[3 + c] + B1[3 * r + 2] * Di[6 + c];
+      sout[18 * NT + 6 * t + r] = B1[3 * r] * db[0] + B1[3 * r + 1] * db[1] + B1[3 * r + 2] * db[2];
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < nk * 18; j += NT) D.BD[18 * (size_t)k0 + j] = sout[j];
+  for (int j = t; j < nk * 6; j += NT) D.cf[6 * (size_t)k0 + j] = sout[18 * NT + j];
+}
+constexpr size_t kFuseSmem = (size_t)kFuseNT * (12 + 21 + 18 + 12) * sizeof(double);
+
+// Per phase: pblk[b] = the first active point whose first position is >= b * kFuseStride (block b
+// then ends where block b+1's first point starts); pblk[nbf] = npa.
+__global__ __launch_bounds__(LBS) void k_ba_pblk(BaDev D) {
+  const int p = blockIdx.x * LBS + threadIdx.x;
+  if (p > D.npa) return;
+  const int cur = p < D.npa ? D.pt_off[p] / kFuseStride : D.nbf;
+  const int prev = p == 0 ? -1 : D.pt_off[p - 1] / kFuseStride;
+  for (int b = prev + 1; b <= min(cur, D.nbf); b++) D.pblk[b] = p;
+}
 __global__ __launch_bounds__(LBS) void k_ba_point_schur_many(const BaDev* __restrict__ Ds, double lambda) {
-  k_ba_point_schur_body(Ds[blockIdx.z], lambda);
+  k_ba_point_schur_body(Ds[blockIdx.z], lambda, 0);
 }
 
 // Accumulates acc += BD_k1 Hpl_k2^T (6x3 * 3x6), one Hpl row at a time.
@@ -2321,11 +2445,17 @@ struct LocalBA {
     const int ga = std::max((Dl.na + LBS - 1) / LBS, 1);
     if (Dl.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3(ga), dim3(LBS), 0, st, Dl);
     if (Dl.npa > 0) hipLaunchKernelGGL(k_ba_point_sum, dim3((Dl.npa + LBS - 1) / LBS), dim3(LBS), 0, st, Dl);
+    cam_sums(Dl, st);
+  }
+  static void cam_sums(const BaDev& Dl, hipStream_t st) {
     if (Dl.nposes > 0) {
       hipLaunchKernelGGL(k_ba_cam_sum, dim3(Dl.nposes, Dl.gsplit), dim3(kGB), 0, st, Dl);
       hipLaunchKernelGGL(k_ba_cam_fin, dim3(Dl.nposes), dim3(64), 0, st, Dl);
     }
   }
+  // fused point side (k_ba_lin_schur): edges grouped by point with at most kFuseMaxDeg per point
+  bool fuse_ok = false;
+  DBuf<int> pblk;
   // host scratch, reused across calls
   std::vector<int> act, pos_pt, chidx, pose_cam, pt_off, pt_id, cam_off, cam_pos, cnt, pcam, ccnt, boff;
 
@@ -2551,6 +2681,14 @@ struct LocalBA {
     BA_CHECK(c.ptab.alloc(nslots));
     D.ptab = c.ptab.p;
     if (D.nblk > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk, gsplit), dim3(kPB), 0, st, D);
+    D.nbf = 0;
+    D.pblk = nullptr;
+    if (fuse_ok && na > 0) {
+      D.nbf = (na - 1) / kFuseStride + 1;
+      BA_CHECK(pblk.alloc((size_t)D.nbf + 1));
+      D.pblk = pblk.p;
+      hipLaunchKernelGGL(k_ba_pblk, dim3(npa / LBS + 1), dim3(LBS), 0, st, D);
+    }
     BA_CHECK(hipGetLastError());
     D.ptc = c.ptc.p;
     D.cmc = c.cmc.p;
@@ -2644,7 +2782,7 @@ struct LocalBA {
       double rho = 0;
       int qmax = 0;
       do {
-        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, D, lambda);
+        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, D, lambda, 0);
         if (D.nposes > 0) {
           hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk + D.nposes, D.gsplit), dim3(kPB), 0, st, D);
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(D.nblk + D.nposes), dim3(64), 0, st, D, lambda);
@@ -2740,9 +2878,21 @@ struct LocalBA {
       hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D0.dmax_p, D0.npa + D0.nposes, D0.scal + 3, 1);
       hipLaunchKernelGGL(k_ba_lm_init, dim3(1), dim3(64), 0, st, Dg, iterations);
       BA_CHECK(hipGetLastError());
+      const bool fused = Dg.nbf > 0;
+      if (fused)
+        BA_CHECK(hipFuncSetAttribute((const void*)k_ba_lin_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)kFuseSmem));
       auto trial = [&](bool lin) {
-        if (lin) linearize(Dg, st);  // gated: only at the start of a new iteration
-        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0);
+        if (lin) {  // gated: only at the start of a new iteration
+          if (fused) {
+            hipLaunchKernelGGL(k_ba_lin_schur, dim3(Dg.nbf), dim3(kFuseNT), kFuseSmem, st, Dg);
+            cam_sums(Dg, st);
+          } else {
+            linearize(Dg, st);
+          }
+        }
+        // after k_ba_lin_schur the point side of an iteration-start trial is done (skip_relin)
+        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0, lin && fused ? 1 : 0);
         if (Dg.nposes > 0) {
           hipLaunchKernelGGL(k_ba_pairs, dim3(Dg.nblk + Dg.nposes, Dg.gsplit), dim3(kPB), 0, st, Dg);
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(Dg.nblk + Dg.nposes), dim3(64), 0, st, Dg, 0.0);
@@ -2862,14 +3012,19 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
   D.ne = ne;
   bool grouped = true;  // edges ordered by point (the reference adds them per MapPoint)
   L.ccnt.assign(nc, 0);
-  int npts = 0;
+  int npts = 0, run = 0, max_run = 0;
   for (int e = 0; e < ne; e++) {
     if (pb->edge_point[e] < 0 || pb->edge_point[e] >= np || pb->edge_cam[e] < 0 || pb->edge_cam[e] >= nc)
       return ORBX_ERR_ARG;
     grouped &= e == 0 || pb->edge_point[e] >= pb->edge_point[e - 1];
-    npts += e == 0 || pb->edge_point[e] != pb->edge_point[e - 1];
+    const bool new_pt = e == 0 || pb->edge_point[e] != pb->edge_point[e - 1];
+    npts += new_pt;
+    run = new_pt ? 1 : run + 1;
+    max_run = std::max(max_run, run);
     L.ccnt[pb->edge_cam[e]]++;
   }
+  // the fused point side needs every point's positions inside one block (A/B: ORBX_BA_NO_FUSE=1)
+  L.fuse_ok = grouped && max_run <= kFuseMaxDeg && std::getenv("ORBX_BA_NO_FUSE") == nullptr;
   L.dev_struct = grouped && nc <= kStructMaxNc && (ne + kTileE - 1) / kTileE <= kStructMaxTiles &&
                  std::getenv("ORBX_BA_HOST_STRUCT") == nullptr;
   if (L.dev_struct) {  // phase-1 sizes: the launches need no readback
