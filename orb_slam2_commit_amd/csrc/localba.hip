@@ -275,6 +275,8 @@ struct BaDev {
   int* pos_pt;     // na: active point index of position k
   int* pblk;       // nbf+1: first active point of each fused point-side block (k_ba_lin_schur), or null
   int nbf;         // fused point-side blocks (0: the unfused kernels run)
+  int fused;       // device-LM launches of a problem with nbf > 0: k_ba_lin_schur does the point side
+                   // of iteration-start trials (k_ba_linearize / point_sum / point_schur skip them)
   double* gpart;   // chunk partials of the pose-list gathers (summed by the *_fin kernels)
   int gsplit;      // chunks per pose list in the gather kernels
   int nbe;         // k_ba_errors blocks; scal[8..] holds its block partials (2 slots), then k_ba_update's
@@ -613,7 +615,7 @@ __device__ __forceinline__ void lin_edge(const BaDev& D, int e, LinEdge& o) {
 }
 
 __device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
-  if (lm_skip_lin(D)) return;
+  if (lm_skip_lin(D) || D.fused) return;
   __shared__ double sh[LBS * 21];
   const int k0 = blockIdx.x * LBS, k = k0 + threadIdx.x;
   if (k0 >= D.na) return;  // block-uniform
@@ -638,7 +640,7 @@ __global__ __launch_bounds__(LBS) void k_ba_linearize_many(const BaDev* __restri
 }
 
 __device__ __forceinline__ void k_ba_point_sum_body(const BaDev& D) {
-  if (lm_skip_lin(D)) return;
+  if (lm_skip_lin(D) || D.fused) return;
   const int i = blockIdx.x * LBS + threadIdx.x;
   if (i >= D.npa) return;
   double h[12];
@@ -756,8 +758,8 @@ __global__ __launch_bounds__(64) void k_ba_cam_fin_many(const BaDev* __restrict_
 
 // One thread per active edge position: D = Hll + lambda I of its point,
 // Dinv (stored once per point), BD_e = Hpl_e Dinv, cf_e = Hpl_e Dinv bl.
-__device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lambda, int skip_relin = 0) {
-  if (lm_skip(D) || (skip_relin && !lm_skip_lin(D))) return;  // skip_relin: k_ba_lin_schur ran this trial
+__device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lambda) {
+  if (lm_skip(D) || (D.fused && !lm_skip_lin(D))) return;  // k_ba_lin_schur ran this trial
   lambda = lm_lambda(D, lambda);
   // the block's 256 positions are contiguous: Hpl comes in and BD / cf go out
   // through LDS with coalesced 8-B accesses (per-lane 144-B strides made every
@@ -802,9 +804,7 @@ __device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lam
   for (int j = t; j < nk * 18; j += LBS) D.BD[18 * (size_t)k0 + j] = sh[j];
   for (int j = t; j < nk * 6; j += LBS) D.cf[6 * (size_t)k0 + j] = scf[j];
 }
-__global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda, int skip_relin) {
-  k_ba_point_schur_body(D, lambda, skip_relin);
-}
+__global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) { k_ba_point_schur_body(D, lambda); }
 
 // ---- the point side of an iteration-start trial in one kernel (device LM, one problem) ----
 // k_ba_linearize -> k_ba_point_sum -> k_ba_point_schur fused: block b takes the whole points
@@ -817,8 +817,8 @@ __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda, 
 // the staged Hpl -- bit-identical to the three kernels, without their global round trips.
 constexpr int kFuseNT = 128, kFuseStride = 96, kFuseMaxDeg = 32;
 static_assert(kFuseStride - 1 + kFuseMaxDeg <= kFuseNT, "a fused block's positions fit its threads");
-__global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur(BaDev D) {
-  if (lm_skip_lin(D)) return;
+__device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
+  if (!D.fused || lm_skip_lin(D) || (int)blockIdx.x >= D.nbf) return;
   constexpr int NT = kFuseNT;
   extern __shared__ __attribute__((aligned(16))) double fsm[];
   double* sptc = fsm;                // NT x 12 point terms; then with sbuf: BD (18) | cf (6) staging
@@ -899,6 +899,10 @@ __global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur(BaDev D) {
   for (int j = t; j < nk * 18; j += NT) D.BD[18 * (size_t)k0 + j] = sout[j];
   for (int j = t; j < nk * 6; j += NT) D.cf[6 * (size_t)k0 + j] = sout[18 * NT + j];
 }
+__global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur(BaDev D) { k_ba_lin_schur_body(D); }
+__global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur_many(const BaDev* __restrict__ Ds) {
+  k_ba_lin_schur_body(Ds[blockIdx.z]);
+}
 constexpr size_t kFuseSmem = (size_t)kFuseNT * (12 + 21 + 18 + 12) * sizeof(double);
 
 // Per phase: pblk[b] = the first active point whose first position is >= b * kFuseStride (block b
@@ -911,7 +915,7 @@ __global__ __launch_bounds__(LBS) void k_ba_pblk(BaDev D) {
   for (int b = prev + 1; b <= min(cur, D.nbf); b++) D.pblk[b] = p;
 }
 __global__ __launch_bounds__(LBS) void k_ba_point_schur_many(const BaDev* __restrict__ Ds, double lambda) {
-  k_ba_point_schur_body(Ds[blockIdx.z], lambda, 0);
+  k_ba_point_schur_body(Ds[blockIdx.z], lambda);
 }
 
 // Accumulates acc += BD_k1 Hpl_k2^T (6x3 * 3x6), one Hpl row at a time.
@@ -2683,6 +2687,7 @@ struct LocalBA {
     if (D.nblk > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk, gsplit), dim3(kPB), 0, st, D);
     D.nbf = 0;
     D.pblk = nullptr;
+    D.fused = 0;  // set on the device-LM copies only
     if (fuse_ok && na > 0) {
       D.nbf = (na - 1) / kFuseStride + 1;
       BA_CHECK(pblk.alloc((size_t)D.nbf + 1));
@@ -2782,7 +2787,7 @@ struct LocalBA {
       double rho = 0;
       int qmax = 0;
       do {
-        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, D, lambda, 0);
+        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, D, lambda);
         if (D.nposes > 0) {
           hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk + D.nposes, D.gsplit), dim3(kPB), 0, st, D);
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(D.nblk + D.nposes), dim3(64), 0, st, D, lambda);
@@ -2871,6 +2876,7 @@ struct LocalBA {
     D0.lm = nullptr;
     BaDev Dg = D;
     Dg.lm = c.lm.p;
+    Dg.fused = D.nbf > 0 ? 1 : 0;
     int it = 0;
     if (!(stop())) {  // the loop head's first poll (i = 0)
       hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, D0, 1, 0);
@@ -2891,8 +2897,8 @@ struct LocalBA {
             linearize(Dg, st);
           }
         }
-        // after k_ba_lin_schur the point side of an iteration-start trial is done (skip_relin)
-        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0, lin && fused ? 1 : 0);
+        // (returns at once after k_ba_lin_schur: the point side of an iteration-start trial is done)
+        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0);
         if (Dg.nposes > 0) {
           hipLaunchKernelGGL(k_ba_pairs, dim3(Dg.nblk + Dg.nposes, Dg.gsplit), dim3(kPB), 0, st, Dg);
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(Dg.nblk + Dg.nposes), dim3(64), 0, st, Dg, 0.0);
@@ -3255,9 +3261,11 @@ struct BaBatch {
 
 orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations, const StopFlag& stop,
                           const DevStop& dstop, hipStream_t st, int* iters, double* chis) {
-  int Nmax = 0, gaM = 1, gpM = 1, geM = 1, gnpM = 1, nbpM = 0, gsM = 1, nposM = 0;
+  int Nmax = 0, gaM = 1, gpM = 1, geM = 1, gnpM = 1, nbpM = 0, gsM = 1, nposM = 0, nbfM = 0, n_unfused = 0;
   for (int i = 0; i < K; i++) {
     const BaDev& D = Ls[i]->D;
+    nbfM = std::max(nbfM, D.nbf);
+    n_unfused += D.nbf > 0 ? 0 : 1;
     Nmax = std::max(Nmax, 6 * D.nposes);
     gaM = std::max(gaM, (D.na + LBS - 1) / LBS);
     gpM = std::max(gpM, D.nbu);
@@ -3284,15 +3292,25 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
   for (int i = 0; i < K; i++) {
     B.hostD[i] = Ls[i]->D;
     B.hostD[i].lm = B.lm.p + i;
+    B.hostD[i].fused = B.hostD[i].nbf > 0 ? 1 : 0;
     B.hostD[K + i] = Ls[i]->D;
     B.hostD[K + i].lm = nullptr;
   }
   BA_CHECK(hipMemcpyAsync(B.dev.p, B.hostD.data(), sizeof(BaDev) * 2 * K, hipMemcpyHostToDevice, st));
   const BaDev* Dg = B.dev.p;
   const BaDev* D0 = B.dev.p + K;
+  if (nbfM > 0)
+    BA_CHECK(hipFuncSetAttribute((const void*)k_ba_lin_schur_many, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)kFuseSmem));
+  // the entry launches (D0: no LM state, nothing fused) and the gated trials: per problem either
+  // k_ba_lin_schur or the three separate kernels do the point side (each returns for the other)
   auto linearize = [&](const BaDev* Ds) {
-    hipLaunchKernelGGL(k_ba_linearize_many, dim3(gaM, 1, K), dim3(LBS), 0, st, Ds);
-    hipLaunchKernelGGL(k_ba_point_sum_many, dim3(gnpM, 1, K), dim3(LBS), 0, st, Ds);
+    const bool gated = Ds == Dg;
+    if (gated && nbfM > 0) hipLaunchKernelGGL(k_ba_lin_schur_many, dim3(nbfM, 1, K), dim3(kFuseNT), kFuseSmem, st, Ds);
+    if (!gated || n_unfused > 0) {
+      hipLaunchKernelGGL(k_ba_linearize_many, dim3(gaM, 1, K), dim3(LBS), 0, st, Ds);
+      hipLaunchKernelGGL(k_ba_point_sum_many, dim3(gnpM, 1, K), dim3(LBS), 0, st, Ds);
+    }
     if (nposM > 0) {
       hipLaunchKernelGGL(k_ba_cam_sum_many, dim3(nposM, gsM, K), dim3(kGB), 0, st, Ds);
       hipLaunchKernelGGL(k_ba_cam_fin_many, dim3(nposM, 1, K), dim3(64), 0, st, Ds);
