@@ -1305,7 +1305,10 @@ __device__ inline double rcp_nr(double d) {
 }
 
 // Pivot j = 4m + U of k_ba_ldlt_col: rank-1 update of the active tiles from
-// column j, then the owners of column j+1 publish it and 1/d_{j+1}.
+// column j, then the owners of column j+1 publish it and 1/d_{j+1}.  The updates (and the
+// back solve's) are explicit FMAs: one FP64 op per link of the chain instead of a multiply and
+// a subtract (60 -> 55 us at N = 120).  The solve is tested against numpy (1e-10) and through the
+// LM decisions against the oracle; no other path shares its rounding.
 template <int TPT, int U>
 __device__ __forceinline__ void ldlt_col_step(double* Lc, double* rinv, double (&a)[TPT][4][4], const int (&ti)[TPT],
                                               const int (&tk)[TPT], int m, int N, int& fail) {
@@ -1329,7 +1332,7 @@ __device__ __forceinline__ void ldlt_col_step(double* Lc, double* rinv, double (
 #pragma unroll
       for (int p = 0; p < 4; p++)
 #pragma unroll
-        for (int q = 0; q < 4; q++) a[t][p][q] -= cr[p] * ck[q];
+        for (int q = 0; q < 4; q++) a[t][p][q] = __builtin_fma(-cr[p], ck[q], a[t][p][q]);  // one op per link
     }
   }
   constexpr int Q = (U + 1) & 3;  // column j+1 within its tile
@@ -1441,7 +1444,7 @@ __device__ __forceinline__ void k_ba_ldlt_col_body(const BaDev& D) {
         const double yk = rk == 0 ? y[0] : rk == 1 ? y[1] : rk == 2 ? y[2] : y[3];
         const double xk = readlane_d(yk, k & 63);
 #pragma unroll
-        for (int r = 0; r < 4; r++) y[r] -= Lv[u][r] * xk;
+        for (int r = 0; r < 4; r++) y[r] = __builtin_fma(-Lv[u][r], xk, y[r]);
       }
     }
   }
