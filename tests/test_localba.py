@@ -469,7 +469,10 @@ def test_gpu_localba_batched_bit_identical(ba):
     trials of its own orbx_ba_run."""
     probs = [synth.localba_problem(seed=7), reject_problem("rejects_b"), small_problem(seed=12),
              synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000), reject_problem("nbad_stop"),
-             synth.localba_problem(seed=9, n_local=12, n_fixed=3, n_points=3000)]
+             synth.localba_problem(seed=9, n_local=12, n_fixed=3, n_points=3000),
+             # points seen by up to 34 keyframes: past the fused point side's 32, so this problem runs
+             # the three separate kernels inside a batch whose other problems are fused
+             synth.localba_problem(seed=10, n_local=30, n_fixed=4, n_points=1500, obs_per_point=34)]
     many = ba.LocalBundleAdjustmentMany(probs)
     for P, a in zip(probs, many):
         b = ba.LocalBundleAdjustment(P)
