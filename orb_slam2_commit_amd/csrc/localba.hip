@@ -277,6 +277,8 @@ struct BaDev {
   int nbf;         // fused point-side blocks (0: the unfused kernels run)
   int fused;       // device-LM launches of a problem with nbf > 0: k_ba_lin_schur does the point side
                    // of iteration-start trials (k_ba_linearize / point_sum / point_schur skip them)
+  int camfold;     // device-LM trials: k_ba_pairs' rhs blocks also sum the pose terms (k_ba_cam_sum's
+                   // partials) and k_ba_schur_fin does k_ba_cam_fin's Hpp / bp (not launched)
   double* gpart;   // chunk partials of the pose-list gathers (summed by the *_fin kernels)
   int gsplit;      // chunks per pose list in the gather kernels
   int nbe;         // k_ba_errors blocks; scal[8..] holds its block partials (2 slots), then k_ba_update's
@@ -966,23 +968,51 @@ __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
 // (k1, k2) order).  Blocks b >= nblk: sum of cf over pose b - nblk's positions
 // (the Schur rhs correction).  Chunk partials -> gpart; k_ba_schur_fin sums
 // them in chunk order (deterministic).
+// device-LM trials fold k_ba_cam_sum / k_ba_cam_fin into k_ba_pairs / k_ba_schur_fin (A/B:
+// ORBX_BA_NO_CAMFOLD=1 launches them as before; results are bit-identical either way)
+static bool camfold_on() { return std::getenv("ORBX_BA_NO_CAMFOLD") == nullptr; }
+
+// pose-term chunk partials of a camfold trial, after the pair and rhs partials
+__device__ inline size_t cam_part_off(const BaDev& D) { return ((size_t)D.nblk * 36 + (size_t)D.nposes * 6) * D.gsplit; }
+
 __device__ __forceinline__ void k_ba_pairs_body(const BaDev& D) {
   if (lm_skip(D) || (int)blockIdx.x >= D.nblk + D.nposes || (int)blockIdx.y >= D.gsplit) return;
   __shared__ double red[(kPB / 64 + 1) * 36];
   const int S = D.gsplit, s = blockIdx.y;
   if ((int)blockIdx.x >= D.nblk) {
     const int ci = blockIdx.x - D.nblk;
+    const bool cam = D.camfold && !lm_skip_lin(D);  // block-uniform
     double v[6] = {0, 0, 0, 0, 0, 0};
+    double w[27];
+#pragma unroll
+    for (int j = 0; j < 27; j++) w[j] = 0;
     int lo, hi;
     chunk_range(D.cam_off[ci], D.cam_off[ci + 1], s, S, lo, hi);
     for (int t = lo + threadIdx.x; t < hi; t += kPB) {
-      const double* f = D.cf + 6 * (size_t)D.cam_pos[t];
+      const int k = D.cam_pos[t];
+      const double* f = D.cf + 6 * (size_t)k;
 #pragma unroll
       for (int r = 0; r < 6; r++) v[r] += f[r];
+      if (cam) {  // k_ba_cam_sum's accumulation (same chunks, same per-thread positions)
+        const double* cm = D.cmc + 42 * (size_t)k;
+        int j = 0;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+          for (int c = r; c < 6; c++) w[j++] += cm[6 * r + c];
+#pragma unroll
+        for (int r = 0; r < 6; r++) w[21 + r] += cm[36 + r];
+      }
     }
     const double* tot = block_sum_fixed<6, kPB / 64>(v, red);
     if (threadIdx.x < 6)
       D.gpart[(size_t)D.nblk * S * 36 + ((size_t)ci * S + s) * 6 + threadIdx.x] = tot[threadIdx.x];
+    if (cam) {
+      static_assert(kPB == kGB, "k_ba_cam_sum's block shape");
+      __syncthreads();  // red is reused
+      const double* tc = block_sum_fixed<27, kPB / 64>(w, red);
+      if (threadIdx.x < 27) D.gpart[cam_part_off(D) + ((size_t)ci * S + s) * 27 + threadIdx.x] = tc[threadIdx.x];
+    }
     return;
   }
   int c1;
@@ -1024,12 +1054,22 @@ __device__ __forceinline__ void k_ba_schur_fin_body(const BaDev& D, double lambd
   if (lm_skip(D) || (int)blockIdx.x >= D.nblk + D.nposes) return;
   lambda = lm_lambda(D, lambda);
   const int j = threadIdx.x, S = D.gsplit;
+  const bool cam = D.camfold && !lm_skip_lin(D);  // k_ba_cam_fin's sums (chunk order) done here
+  const double* camp = D.gpart + cam_part_off(D);
   if ((int)blockIdx.x >= D.nblk) {
     const int ci = blockIdx.x - D.nblk;
     if (j < 6) {
       double t = 0;
       for (int c = 0; c < S; c++) t += D.gpart[(size_t)D.nblk * S * 36 + ((size_t)ci * S + c) * 6 + j];
-      D.bs[6 * ci + j] = D.bp[6 * ci + j] - t;
+      double bp;
+      if (cam) {
+        bp = 0;
+        for (int c = 0; c < S; c++) bp += camp[((size_t)ci * S + c) * 27 + 21 + j];
+        D.bp[6 * ci + j] = bp;
+      } else {
+        bp = D.bp[6 * ci + j];
+      }
+      D.bs[6 * ci + j] = bp - t;
     }
     return;
   }
@@ -1042,7 +1082,16 @@ __device__ __forceinline__ void k_ba_schur_fin_body(const BaDev& D, double lambd
   const int r = j / 6, c = j % 6;
   double sv;
   if (c1 == c2) {
-    sv = D.Hpp[36 * c1 + j] + (r == c ? lambda : 0.0) - v;
+    double h;
+    if (cam) {
+      const int lo = min(r, c), hi = max(r, c);
+      h = 0;
+      for (int q = 0; q < S; q++) h += camp[((size_t)c1 * S + q) * 27 + lo * 6 - (lo * (lo - 1)) / 2 + (hi - lo)];
+      D.Hpp[36 * c1 + j] = h;
+    } else {
+      h = D.Hpp[36 * c1 + j];
+    }
+    sv = h + (r == c ? lambda : 0.0) - v;
   } else {
     sv = -v;
     D.S[(size_t)(6 * c2 + c) * N + 6 * c1 + r] = sv;
@@ -2449,10 +2498,13 @@ struct LocalBA {
   // computeActiveErrors is not repeated: the errors/chi stored by the trial
   // (recompute, slot 1) are the ones at the state being linearised
   void linearize(const BaDev& Dl, hipStream_t st) {
+    lin_points(Dl, st);
+    cam_sums(Dl, st);
+  }
+  static void lin_points(const BaDev& Dl, hipStream_t st) {
     const int ga = std::max((Dl.na + LBS - 1) / LBS, 1);
     if (Dl.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3(ga), dim3(LBS), 0, st, Dl);
     if (Dl.npa > 0) hipLaunchKernelGGL(k_ba_point_sum, dim3((Dl.npa + LBS - 1) / LBS), dim3(LBS), 0, st, Dl);
-    cam_sums(Dl, st);
   }
   static void cam_sums(const BaDev& Dl, hipStream_t st) {
     if (Dl.nposes > 0) {
@@ -2669,7 +2721,7 @@ struct LocalBA {
     D.nposes = nposes;
     D.nblk = nposes * (nposes + 1) / 2;
     D.gsplit = gsplit;
-    BA_CHECK(c.gpart.alloc((size_t)std::max(D.nblk * 36 + nposes * 6, nposes * 27) * gsplit));
+    BA_CHECK(c.gpart.alloc((size_t)(D.nblk * 36 + nposes * 6 + nposes * 27) * gsplit));  // pairs | rhs | camfold pose terms
     D.gpart = c.gpart.p;
     // readback block: scal[0..7], then errors partials (2 slots of nbe), then update partials
     D.nbe = std::max((na + LBS - 1) / LBS, 1);
@@ -2691,6 +2743,7 @@ struct LocalBA {
     D.nbf = 0;
     D.pblk = nullptr;
     D.fused = 0;  // set on the device-LM copies only
+    D.camfold = 0;
     if (fuse_ok && na > 0) {
       D.nbf = (na - 1) / kFuseStride + 1;
       BA_CHECK(pblk.alloc((size_t)D.nbf + 1));
@@ -2880,6 +2933,7 @@ struct LocalBA {
     BaDev Dg = D;
     Dg.lm = c.lm.p;
     Dg.fused = D.nbf > 0 ? 1 : 0;
+    Dg.camfold = camfold_on() ? 1 : 0;
     int it = 0;
     if (!(stop())) {  // the loop head's first poll (i = 0)
       hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, D0, 1, 0);
@@ -2893,12 +2947,11 @@ struct LocalBA {
                                      (int)kFuseSmem));
       auto trial = [&](bool lin) {
         if (lin) {  // gated: only at the start of a new iteration
-          if (fused) {
+          if (fused)
             hipLaunchKernelGGL(k_ba_lin_schur, dim3(Dg.nbf), dim3(kFuseNT), kFuseSmem, st, Dg);
-            cam_sums(Dg, st);
-          } else {
-            linearize(Dg, st);
-          }
+          else
+            lin_points(Dg, st);
+          if (!Dg.camfold) cam_sums(Dg, st);
         }
         // (returns at once after k_ba_lin_schur: the point side of an iteration-start trial is done)
         hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0);
@@ -3281,6 +3334,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
   LdltPlan ldlt;
   BA_CHECK(ldlt.prepare(Nmax));
   if (!ldlt.col && !ldlt.blk) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
+  const bool camfold = camfold_on();
   BA_CHECK(ldlt.prepare_many());
   if (B.cap < K) {
     if (B.lm_host) (void)hipHostFree(B.lm_host);
@@ -3296,6 +3350,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
     B.hostD[i] = Ls[i]->D;
     B.hostD[i].lm = B.lm.p + i;
     B.hostD[i].fused = B.hostD[i].nbf > 0 ? 1 : 0;
+    B.hostD[i].camfold = camfold ? 1 : 0;
     B.hostD[K + i] = Ls[i]->D;
     B.hostD[K + i].lm = nullptr;
   }
@@ -3314,7 +3369,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
       hipLaunchKernelGGL(k_ba_linearize_many, dim3(gaM, 1, K), dim3(LBS), 0, st, Ds);
       hipLaunchKernelGGL(k_ba_point_sum_many, dim3(gnpM, 1, K), dim3(LBS), 0, st, Ds);
     }
-    if (nposM > 0) {
+    if (nposM > 0 && !(gated && camfold)) {
       hipLaunchKernelGGL(k_ba_cam_sum_many, dim3(nposM, gsM, K), dim3(kGB), 0, st, Ds);
       hipLaunchKernelGGL(k_ba_cam_fin_many, dim3(nposM, 1, K), dim3(64), 0, st, Ds);
     }
