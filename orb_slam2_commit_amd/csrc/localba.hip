@@ -761,7 +761,7 @@ __global__ __launch_bounds__(64) void k_ba_cam_fin_many(const BaDev* __restrict_
 // One thread per active edge position: D = Hll + lambda I of its point,
 // Dinv (stored once per point), BD_e = Hpl_e Dinv, cf_e = Hpl_e Dinv bl.
 __device__ __forceinline__ void k_ba_point_schur_body(const BaDev& D, double lambda) {
-  if (lm_skip(D) || (D.fused && !lm_skip_lin(D))) return;  // k_ba_lin_schur ran this trial
+  if (lm_skip(D) || D.fused == 2 || (D.fused && !lm_skip_lin(D))) return;  // k_ba_lin_schur ran this trial
   lambda = lm_lambda(D, lambda);
   // the block's 256 positions are contiguous: Hpl comes in and BD / cf go out
   // through LDS with coalesced 8-B accesses (per-lane 144-B strides made every
@@ -820,7 +820,11 @@ __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) 
 constexpr int kFuseNT = 128, kFuseStride = 96, kFuseMaxDeg = 32;
 static_assert(kFuseStride - 1 + kFuseMaxDeg <= kFuseNT, "a fused block's positions fit its threads");
 __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
-  if (!D.fused || lm_skip_lin(D) || (int)blockIdx.x >= D.nbf) return;
+  if (!D.fused || lm_skip(D) || (int)blockIdx.x >= D.nbf) return;
+  // fused == 2: the trials that do not relinearise (a rejected step's new lambda) also come here,
+  // for k_ba_point_schur's part: the staged Hpl, D = Hll + lambda I, D^-1 b_l (same bits)
+  const bool lin = !lm_skip_lin(D);
+  if (!lin && D.fused != 2) return;
   constexpr int NT = kFuseNT;
   extern __shared__ __attribute__((aligned(16))) double fsm[];
   double* sptc = fsm;                // NT x 12 point terms; then with sbuf: BD (18) | cf (6) staging
@@ -835,6 +839,23 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   const double lambda = lm_lambda(D, 0.0);
   const bool act = t < nk;
   const int k = k0 + (act ? t : 0);
+  if (!lin) {
+    for (int j = t; j < nk * 18; j += NT) shpl[j] = D.Hpl[18 * (size_t)k0 + j];
+    if (t < npt) {
+      const int i = p0 + t;
+      double Dm[9];
+      for (int j = 0; j < 9; j++) Dm[j] = D.Hll[9 * i + j];
+      Dm[0] += lambda;
+      Dm[4] += lambda;
+      Dm[8] += lambda;
+      double Di[9];
+      inv3(Dm, Di);
+      for (int j = 0; j < 9; j++) D.Dinv[9 * i + j] = Di[j];
+      const double b0 = D.bl[3 * i], b1 = D.bl[3 * i + 1], b2 = D.bl[3 * i + 2];
+      for (int r = 0; r < 3; r++) sdi[12 * t + 9 + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
+      for (int j = 0; j < 9; j++) sdi[12 * t + j] = Di[j];
+    }
+  } else {
   LinEdge L;
   lin_edge(D, D.act[k], L);
   if (act) {
@@ -886,6 +907,7 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
     for (int r = 0; r < 3; r++) sdi[12 * t + 9 + r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
     for (int j = 0; j < 9; j++) sdi[12 * t + j] = Di[j];
   }
+  }  // lin
   __syncthreads();
   if (act) {
     const double* Di = sdi + 12 * (D.pos_pt[k] - p0);
@@ -971,6 +993,13 @@ __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
 // device-LM trials fold k_ba_cam_sum / k_ba_cam_fin into k_ba_pairs / k_ba_schur_fin (A/B:
 // ORBX_BA_NO_CAMFOLD=1 launches them as before; results are bit-identical either way)
 static bool camfold_on() { return std::getenv("ORBX_BA_NO_CAMFOLD") == nullptr; }
+// device-LM value of BaDev::fused: 2 = k_ba_lin_schur also takes the non-relinearising trials'
+// point side and k_ba_point_schur is not launched (A/B: ORBX_BA_NO_PSFOLD=1).  A problem without
+// free poses keeps 1 (k_ba_point_schur flags its empty reduced system).
+static int fused_mode(int nbf, int nposes) {
+  if (nbf <= 0) return 0;
+  return nposes > 0 && std::getenv("ORBX_BA_NO_PSFOLD") == nullptr ? 2 : 1;
+}
 
 // pose-term chunk partials of a camfold trial, after the pair and rhs partials
 __device__ inline size_t cam_part_off(const BaDev& D) { return ((size_t)D.nblk * 36 + (size_t)D.nposes * 6) * D.gsplit; }
@@ -2932,7 +2961,7 @@ struct LocalBA {
     D0.lm = nullptr;
     BaDev Dg = D;
     Dg.lm = c.lm.p;
-    Dg.fused = D.nbf > 0 ? 1 : 0;
+    Dg.fused = fused_mode(D.nbf, D.nposes);
     Dg.camfold = camfold_on() ? 1 : 0;
     int it = 0;
     if (!(stop())) {  // the loop head's first poll (i = 0)
@@ -2945,16 +2974,14 @@ struct LocalBA {
       if (fused)
         BA_CHECK(hipFuncSetAttribute((const void*)k_ba_lin_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)kFuseSmem));
+      const bool psfold = Dg.fused == 2;
       auto trial = [&](bool lin) {
-        if (lin) {  // gated: only at the start of a new iteration
-          if (fused)
-            hipLaunchKernelGGL(k_ba_lin_schur, dim3(Dg.nbf), dim3(kFuseNT), kFuseSmem, st, Dg);
-          else
-            lin_points(Dg, st);
-          if (!Dg.camfold) cam_sums(Dg, st);
-        }
+        // linearisation gated on the device: only at the start of a new iteration
+        if (fused && (lin || psfold)) hipLaunchKernelGGL(k_ba_lin_schur, dim3(Dg.nbf), dim3(kFuseNT), kFuseSmem, st, Dg);
+        if (lin && !fused) lin_points(Dg, st);
+        if (lin && !Dg.camfold) cam_sums(Dg, st);
         // (returns at once after k_ba_lin_schur: the point side of an iteration-start trial is done)
-        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0);
+        if (!psfold) hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0);
         if (Dg.nposes > 0) {
           hipLaunchKernelGGL(k_ba_pairs, dim3(Dg.nblk + Dg.nposes, Dg.gsplit), dim3(kPB), 0, st, Dg);
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(Dg.nblk + Dg.nposes), dim3(64), 0, st, Dg, 0.0);
@@ -3335,6 +3362,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
   BA_CHECK(ldlt.prepare(Nmax));
   if (!ldlt.col && !ldlt.blk) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
   const bool camfold = camfold_on();
+  int n_ps = 0, n_psfold = 0;  // problems that launch k_ba_point_schur / whose k_ba_lin_schur takes it
   BA_CHECK(ldlt.prepare_many());
   if (B.cap < K) {
     if (B.lm_host) (void)hipHostFree(B.lm_host);
@@ -3349,7 +3377,9 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
   for (int i = 0; i < K; i++) {
     B.hostD[i] = Ls[i]->D;
     B.hostD[i].lm = B.lm.p + i;
-    B.hostD[i].fused = B.hostD[i].nbf > 0 ? 1 : 0;
+    B.hostD[i].fused = fused_mode(B.hostD[i].nbf, B.hostD[i].nposes);
+    n_ps += B.hostD[i].fused == 2 ? 0 : 1;
+    n_psfold += B.hostD[i].fused == 2 ? 1 : 0;
     B.hostD[i].camfold = camfold ? 1 : 0;
     B.hostD[K + i] = Ls[i]->D;
     B.hostD[K + i].lm = nullptr;
@@ -3383,8 +3413,11 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
     BA_CHECK(hipGetLastError());
     for (int budget = iterations, first = 1;; first = 0) {
       for (int t = 0; t < budget; t++) {
-        if (!(first && t == 0)) linearize(Dg);  // gated per problem
-        hipLaunchKernelGGL(k_ba_point_schur_many, dim3(gaM, 1, K), dim3(LBS), 0, st, Dg, 0.0);
+        if (!(first && t == 0))
+          linearize(Dg);  // gated per problem
+        else if (n_psfold > 0)
+          hipLaunchKernelGGL(k_ba_lin_schur_many, dim3(nbfM, 1, K), dim3(kFuseNT), kFuseSmem, st, Dg);
+        if (n_ps > 0) hipLaunchKernelGGL(k_ba_point_schur_many, dim3(gaM, 1, K), dim3(LBS), 0, st, Dg, 0.0);
         if (nposM > 0) {
           hipLaunchKernelGGL(k_ba_pairs_many, dim3(nbpM, gsM, K), dim3(kPB), 0, st, Dg);
           hipLaunchKernelGGL(k_ba_schur_fin_many, dim3(nbpM, 1, K), dim3(64), 0, st, Dg, 0.0);

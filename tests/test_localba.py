@@ -361,13 +361,15 @@ def test_gpu_localba_fused_point_side_bit_identical(ba, case, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["config4", "rejects"])
-def test_gpu_localba_camfold_bit_identical(ba, case, monkeypatch):
+@pytest.mark.parametrize("switch", ["ORBX_BA_NO_CAMFOLD", "ORBX_BA_NO_PSFOLD"])
+def test_gpu_localba_trial_folds_bit_identical(ba, case, switch, monkeypatch):
     """Device-LM trials sum the pose terms inside k_ba_pairs and finish Hpp / b_p inside
-    k_ba_schur_fin (no k_ba_cam_sum / k_ba_cam_fin launches): same bits, iterations and trials as
-    with the two kernels (ORBX_BA_NO_CAMFOLD=1)."""
+    k_ba_schur_fin (no k_ba_cam_sum / k_ba_cam_fin launches), and k_ba_lin_schur also does the
+    point side of trials that do not relinearise (no k_ba_point_schur launch): same bits,
+    iterations and trials as with the separate kernels (ORBX_BA_NO_CAMFOLD=1 / ORBX_BA_NO_PSFOLD=1)."""
     P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(sorted(REJECT_CASES)[0])
     a = ba.LocalBundleAdjustment(P)
-    monkeypatch.setenv("ORBX_BA_NO_CAMFOLD", "1")
+    monkeypatch.setenv(switch, "1")
     b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw_d", "Xw_d", "edge_outlier"):
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
