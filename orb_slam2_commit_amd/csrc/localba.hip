@@ -1794,76 +1794,129 @@ struct LdltPlan {
   }
 };
 
-// back-substitution + update (push first) + LM scale, skipped when the
-// solve failed (scal[2] == 0).  Threads: active points, then active poses.
+constexpr int kUpCh = 2048;  // k_ba_update: positions per LDS chunk (48 KB)
+// back-substitution + update (push first) + LM scale, skipped when the solve failed
+// (scal[2] == 0).  Blocks: the active poses first (their se3 exp chains then overlap the point
+// blocks), then LBS active points per block; one LM-scale partial per block.
 __device__ __forceinline__ void k_ba_update_body(const BaDev& D, double lambda) {
   if (lm_skip(D) || (int)blockIdx.x >= D.nbu) return;
   lambda = lm_lambda(D, lambda);
-  const int i = blockIdx.x * LBS + threadIdx.x;
-  // device LM: the previous trial's pop is folded in (same thread mapping as k_ba_restore).
+  // device LM: the previous trial's pop is folded in (same values as k_ba_restore).
   // Every state value is loaded into registers before any store: the X / Xbak (cq, cbak)
   // stores may alias the next loads as far as the compiler knows, which otherwise
   // serialised each load behind the previous store (one memory round trip apiece).
   const bool rej = D.lm && D.lm->rejected;
   const bool ok = D.scal[2] != 0.0;
+  const int npb = (D.nposes + LBS - 1) / LBS;
   double sc = 0;
-  if (i < D.npa) {
-    const int p = D.pt_id[i];
-    const double* from = rej ? D.Xbak : D.X;
-    const double X0[3] = {from[3 * p], from[3 * p + 1], from[3 * p + 2]};
-    if (ok) {
-      double c[3] = {D.bl[3 * i], D.bl[3 * i + 1], D.bl[3 * i + 2]};
-      for (int k = D.pt_off[i]; k < D.pt_off[i + 1]; k++) {
-        const int ci = D.pcam[k];
-        if (ci < 0) continue;
-        const double* B = D.Hpl + 18 * (size_t)k;
-        for (int j = 0; j < 3; j++)
-          for (int r = 0; r < 6; r++) c[j] -= B[3 * r + j] * D.xp[6 * ci + r];
-      }
-      const double* Di = D.Dinv + 9 * (size_t)i;
-      double x[3];
-      for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
-      for (int r = 0; r < 3; r++) sc += x[r] * (lambda * x[r] + D.bl[3 * i + r]);
-      for (int r = 0; r < 3; r++) {
-        D.Xbak[3 * p + r] = X0[r];
-        D.X[3 * p + r] = X0[r] + x[r];
-      }
-    } else if (rej) {
-      for (int r = 0; r < 3; r++) D.X[3 * p + r] = X0[r];
-    }
-  } else if (i < D.npa + D.nposes) {
-    const int pi = i - D.npa;
-    const int c = D.pose_cam[pi];
-    double q4[4], t3[3];
-    if (rej) {
-      for (int r = 0; r < 4; r++) q4[r] = D.cbak[7 * c + r];
-      for (int r = 0; r < 3; r++) t3[r] = D.cbak[7 * c + 4 + r];
-    } else {
-      for (int r = 0; r < 4; r++) q4[r] = D.cq[4 * c + r];
-      for (int r = 0; r < 3; r++) t3[r] = D.ct[3 * c + r];
-    }
-    if (ok) {
-      double u[6];
+  if ((int)blockIdx.x < npb) {
+    const int pi = blockIdx.x * LBS + threadIdx.x;
+    if (pi < D.nposes) {
+      const int c = D.pose_cam[pi];
+      double u[6], bp[6];
       for (int r = 0; r < 6; r++) {
         u[r] = D.xp[6 * pi + r];
-        sc += u[r] * (lambda * u[r] + D.bp[6 * pi + r]);
+        bp[r] = D.bp[6 * pi + r];
       }
-      for (int r = 0; r < 4; r++) D.cbak[7 * c + r] = q4[r];
-      for (int r = 0; r < 3; r++) D.cbak[7 * c + 4 + r] = t3[r];
-      const SE3d E = se3_exp(u);
-      const Quat q = {q4[0], q4[1], q4[2], q4[3]};
-      double rt[3];
-      qrot(E.q, t3, rt);
-      Quat nq = qmul(E.q, q);
-      qnormalize(nq);
-      D.cq[4 * c] = nq.x;
-      D.cq[4 * c + 1] = nq.y;
-      D.cq[4 * c + 2] = nq.z;
-      D.cq[4 * c + 3] = nq.w;
-      for (int r = 0; r < 3; r++) D.ct[3 * c + r] = E.t[r] + rt[r];
-    } else if (rej) {
-      for (int r = 0; r < 4; r++) D.cq[4 * c + r] = q4[r];
-      for (int r = 0; r < 3; r++) D.ct[3 * c + r] = t3[r];
+      double q4[4], t3[3];
+      if (rej) {
+        for (int r = 0; r < 4; r++) q4[r] = D.cbak[7 * c + r];
+        for (int r = 0; r < 3; r++) t3[r] = D.cbak[7 * c + 4 + r];
+      } else {
+        for (int r = 0; r < 4; r++) q4[r] = D.cq[4 * c + r];
+        for (int r = 0; r < 3; r++) t3[r] = D.ct[3 * c + r];
+      }
+      if (ok) {
+        for (int r = 0; r < 6; r++) sc += u[r] * (lambda * u[r] + bp[r]);
+        for (int r = 0; r < 4; r++) D.cbak[7 * c + r] = q4[r];
+        for (int r = 0; r < 3; r++) D.cbak[7 * c + 4 + r] = t3[r];
+        const SE3d E = se3_exp(u);
+        const Quat q = {q4[0], q4[1], q4[2], q4[3]};
+        double rt[3];
+        qrot(E.q, t3, rt);
+        Quat nq = qmul(E.q, q);
+        qnormalize(nq);
+        D.cq[4 * c] = nq.x;
+        D.cq[4 * c + 1] = nq.y;
+        D.cq[4 * c + 2] = nq.z;
+        D.cq[4 * c + 3] = nq.w;
+        for (int r = 0; r < 3; r++) D.ct[3 * c + r] = E.t[r] + rt[r];
+      } else if (rej) {
+        for (int r = 0; r < 4; r++) D.cq[4 * c + r] = q4[r];
+        for (int r = 0; r < 3; r++) D.ct[3 * c + r] = t3[r];
+      }
+    }
+  } else {
+    const int i0 = (blockIdx.x - npb) * LBS, i = i0 + threadIdx.x, i1 = min(i0 + LBS, D.npa);
+    const bool pt = i < D.npa;
+    const int ic = pt ? i : i0;  // (i0 < npa in a point block) loads stay in range
+    // everything that depends on neither the solve's flag nor the LM state, issued first
+    const int p = D.pt_id[ic];
+    const int ka = D.pt_off[ic], kz = pt ? D.pt_off[ic + 1] : ka;
+    const int kb = D.pt_off[i0], ke = D.pt_off[i1];
+    double c[3], bl[3], Di[9];
+    for (int r = 0; r < 3; r++) c[r] = bl[r] = D.bl[3 * ic + r];
+    for (int r = 0; r < 9; r++) Di[r] = D.Dinv[9 * (size_t)ic + r];
+    const double* from = rej ? D.Xbak : D.X;
+    const double X0[3] = {from[3 * p], from[3 * p + 1], from[3 * p + 2]};
+    // b_l - sum_k Hpl_k^T x_c(k): the per-position products H_pl^T x_c are formed by all the
+    // block's threads at once (4 positions per thread per round, every load issued before the
+    // arithmetic) and staged in LDS; each point's thread then subtracts its positions' products
+    // in position order.  (A thread per point walking its own positions paid two dependent
+    // memory round trips per position.)  Unused when the solve failed.
+    __shared__ double sq[kUpCh * 3];
+    for (int base = kb; base < ke; base += kUpCh) {  // block-uniform
+      const int n = min(kUpCh, ke - base);
+      for (int u0 = threadIdx.x; u0 < n; u0 += 4 * LBS) {
+        int ci[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+          const int u = u0 + s * LBS;
+          ci[s] = u < n ? D.pcam[base + u] : -1;
+        }
+        double B[4][18], x[4][6];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+          const int u = min(u0 + s * LBS, n - 1);
+          const double* h = D.Hpl + 18 * (size_t)(base + u);
+          const double* xc = D.xp + 6 * max(ci[s], 0);
+#pragma unroll
+          for (int j = 0; j < 18; j++) B[s][j] = h[j];
+#pragma unroll
+          for (int r = 0; r < 6; r++) x[s][r] = xc[r];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+          const int u = u0 + s * LBS;
+          if (u < n) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+              double q = 0;
+#pragma unroll
+              for (int r = 0; r < 6; r++) q += B[s][3 * r + j] * x[s][r];
+              sq[3 * u + j] = ci[s] >= 0 ? q : 0.0;  // fixed camera: no term
+            }
+          }
+        }
+      }
+      __syncthreads();
+      for (int k = max(ka, base); k < min(kz, base + n); k++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) c[j] -= sq[3 * (k - base) + j];
+      __syncthreads();
+    }
+    if (pt) {
+      if (ok) {
+        double x[3];
+        for (int r = 0; r < 3; r++) x[r] = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
+        for (int r = 0; r < 3; r++) sc += x[r] * (lambda * x[r] + bl[r]);
+        for (int r = 0; r < 3; r++) {
+          D.Xbak[3 * p + r] = X0[r];
+          D.X[3 * p + r] = X0[r] + x[r];
+        }
+      } else if (rej) {
+        for (int r = 0; r < 3; r++) D.X[3 * p + r] = X0[r];
+      }
     }
   }
   block_partial(sc, D.scal + 8 + 2 * D.nbe);
@@ -2754,7 +2807,7 @@ struct LocalBA {
     D.gpart = c.gpart.p;
     // readback block: scal[0..7], then errors partials (2 slots of nbe), then update partials
     D.nbe = std::max((na + LBS - 1) / LBS, 1);
-    nbu = std::max((npa + nposes + LBS - 1) / LBS, 1);
+    nbu = std::max((nposes + LBS - 1) / LBS + (npa + LBS - 1) / LBS, 1);  // k_ba_update: pose blocks, then point blocks
     D.nbu = nbu;
     n_rb = 8 + 2 * D.nbe + nbu;
     BA_CHECK(c.scal.alloc(n_rb));
@@ -2878,7 +2931,7 @@ struct LocalBA {
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(D.nblk + D.nposes), dim3(64), 0, st, D, lambda);
           ldlt.launch(D, st);
         }
-        hipLaunchKernelGGL(k_ba_update, dim3(gp), dim3(LBS), 0, st, D, lambda);
+        hipLaunchKernelGGL(k_ba_update, dim3(D.nbu), dim3(LBS), 0, st, D, lambda);
         D.host_trial = ptrial++;
         BA_CHECK(errors(st, 1, 1));
         BA_CHECK(start_read(st));
@@ -2987,7 +3040,7 @@ struct LocalBA {
           hipLaunchKernelGGL(k_ba_schur_fin, dim3(Dg.nblk + Dg.nposes), dim3(64), 0, st, Dg, 0.0);
           ldlt.launch(Dg, st);
         }
-        hipLaunchKernelGGL(k_ba_update, dim3(gp), dim3(LBS), 0, st, Dg, 0.0);
+        hipLaunchKernelGGL(k_ba_update, dim3(Dg.nbu), dim3(LBS), 0, st, Dg, 0.0);
         hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, Dg, 1, 1);
         hipLaunchKernelGGL(k_ba_lm_control, dim3(1), dim3(64), 0, st, Dg, dstop);
       };
