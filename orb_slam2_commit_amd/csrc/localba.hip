@@ -277,6 +277,8 @@ struct BaDev {
   int nbf;         // fused point-side blocks (0: the unfused kernels run)
   int fused;       // device-LM launches of a problem with nbf > 0: k_ba_lin_schur does the point side
                    // of iteration-start trials (k_ba_linearize / point_sum / point_schur skip them)
+  int ldlt_pan;    // the reduced system goes through k_ba_ldlt_pan (else the column-step kernel): per
+                   // problem, so a batch with both kinds launches both and each skips the other's
   int camfold;     // device-LM trials: k_ba_pairs' rhs blocks also sum the pose terms (k_ba_cam_sum's
                    // partials) and k_ba_schur_fin does k_ba_cam_fin's Hpp / bp (not launched)
   double* gpart;   // chunk partials of the pose-list gathers (summed by the *_fin kernels)
@@ -1435,7 +1437,7 @@ __device__ __forceinline__ void ldlt_col_step(double* Lc, double* rinv, double (
 
 template <int TPT, int NT>
 __device__ __forceinline__ void k_ba_ldlt_col_body(const BaDev& D) {
-  if (lm_skip(D)) return;
+  if (lm_skip(D) || D.ldlt_pan) return;
   extern __shared__ __attribute__((aligned(16))) double Lc[];
   __shared__ int fail;
   const int N = 6 * D.nposes, tid = threadIdx.x;
@@ -1536,6 +1538,279 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_col(BaDev D) { k_ba_ldlt_col_bod
 template <int TPT, int NT>
 __global__ __launch_bounds__(NT) void k_ba_ldlt_col_many(const BaDev* __restrict__ Ds) {
   k_ba_ldlt_col_body<TPT, NT>(Ds[blockIdx.z]);
+}
+
+// ---- reduced camera system: 8-wide panels over the column-step kernel's register tiles ----
+// The column-step kernel pays one barrier and one LDS round trip per pivot; its per-pivot chain
+// (publish column j+1 and 1/d, barrier, read, scale, update) is what bounds it.  Here the pivots
+// go eight at a time.  Per panel M (columns c0 = 8M .. c0+7, tile columns 2M, 2M+1):
+//   B  one thread per row i = c0 .. N (the augmented row b^T included) reads the panel's 8x8
+//      diagonal block and its own row from LDS, factors the diagonal block in registers (every
+//      such thread the same way: no cross-lane broadcast on the pivot chain) and solves its row:
+//      L_i (scaled) and V_i = L_i D (unscaled) to LDS, L_i also into the packed factor;
+//   C  every register tile right of the panel takes A -= L_rows V_cols^T (8 FMAs per entry, the
+//      tile stays in registers: only the panel rows move through LDS), and the tiles of the next
+//      panel publish themselves.
+// Two barriers per eight pivots.  The augmented row ends as y = D^-1 L^-1 b, and wave 0 solves
+// L^T x = y.  Failure rule as the other kernels: an exactly zero pivot fails the solve.
+// LDS: packed strictly-lower L (N(N-1)/2), the panel values / L / V ((Np+8) x 8 each), y (N).
+__host__ __device__ inline int ldlt_pan_rows(int N) { return ldlt_np4(N) + 8; }
+// panel arrays: rows of 8 doubles in groups of four, each group padded to 34 doubles, so that
+// the lanes of a wave reading different row groups spread over the LDS banks
+__host__ __device__ inline int ldlt_prow(int i) { return (i >> 2) * 34 + (i & 3) * 8; }
+__host__ __device__ inline int ldlt_pan_arr(int N) { return ldlt_pan_rows(N) / 4 * 34; }
+inline size_t ldlt_pan_smem(int N) {
+  return ((size_t)N * (N - 1) / 2 + 3 * (size_t)ldlt_pan_arr(N) + N) * sizeof(double);
+}
+// (one tile per thread: with two the trailing update doubles and the panel kernel loses to the
+// column-step one, e.g. 91 us at N = 126)
+inline bool ldlt_pan_fits(int N) { return ldlt_pan_smem(N) <= kLdltColMaxSmem && ldlt_col_tiles(N) <= 512 && N < 128; }
+// default where it fits (A/B: ORBX_LDLT_COL=1 keeps the column-step kernel)
+inline bool ldlt_use_pan(int N) {
+  return ldlt_pan_fits(N) && !std::getenv("ORBX_LDLT_COL") && !std::getenv("ORBX_LDLT_BLK") &&
+         !std::getenv("ORBX_LDLT_BLOCKED");
+}
+constexpr int ldlt_tri(int a, int b) { return a * (a + 1) / 2 + b; }
+
+template <int TPT, int NT, int R>  // R: 64-row groups of the back solve (N < 64 R)
+__device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
+  if (lm_skip(D) || !D.ldlt_pan) return;
+  extern __shared__ __attribute__((aligned(16))) double Lpk[];  // row k: Lpk[k(k-1)/2 + c], c < k
+  __shared__ int fail;
+  const int N = 6 * D.nposes, tid = threadIdx.x;
+  const int Np4 = ldlt_np4(N), Tr = Np4 / 4, Tc = (N + 3) / 4;
+  const int ntiles = Tc * Tr - Tc * (Tc - 1) / 2;
+  const int PA = ldlt_pan_arr(N);
+  double* Pn = Lpk + (size_t)N * (N - 1) / 2;  // row i at ldlt_prow(i): current panel values
+  double* Lp = Pn + PA;                         // panel L (scaled)
+  double* Vp = Lp + PA;                         // panel V = L D (unscaled)
+  double* ys = Vp + PA;                         // [N] y = D^-1 L^-1 b
+  double a[TPT][4][4];
+  int ti[TPT], tk[TPT];
+  LDLT_TS(0);
+  if (tid == 0) fail = 0;
+  for (int j = tid; j < 3 * PA; j += NT) Pn[j] = 0.0;  // padding rows / columns stay finite
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < TPT; t++) {
+    int x = tid + NT * t, k = 0;
+    ti[t] = 0;
+    tk[t] = -1;  // inactive
+    if (x < ntiles) {
+      while (x >= Tr - k) {  // column-major tile order
+        x -= Tr - k;
+        k++;
+      }
+      tk[t] = k;
+      ti[t] = k + x;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int i = 4 * ti[t] + p, kk = 4 * tk[t] + q;
+        double v = 0.0;
+        if (tk[t] >= 0 && kk < N) v = i < N ? D.S[(size_t)i * N + kk] : (i == N ? D.bs[kk] : 0.0);
+        a[t][p][q] = v;
+      }
+    if (tk[t] >= 0 && tk[t] < 2) {
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        double2_t* dst = reinterpret_cast<double2_t*>(Pn + ldlt_prow(4 * ti[t] + p) + 4 * tk[t]);
+        dst[0] = double2_t{a[t][p][0], a[t][p][1]};
+        dst[1] = double2_t{a[t][p][2], a[t][p][3]};
+      }
+    }
+  }
+  __syncthreads();
+  LDLT_TS(1);
+  for (int M = 0; 2 * M < Tc; M++) {
+    const int c0 = 8 * M, w = min(8, N - c0);
+    // B: panel rows
+    const int i = c0 + tid;
+    if (i <= N) {
+      double Dm[36], u[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        const double2_t* src = reinterpret_cast<const double2_t*>(Pn + ldlt_prow(c0 + r));
+        const double2_t v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
+        const double row[8] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
+#pragma unroll
+        for (int c = 0; c <= r; c++) Dm[ldlt_tri(r, c)] = row[c];
+      }
+      {
+        const double2_t* src = reinterpret_cast<const double2_t*>(Pn + ldlt_prow(i));
+        const double2_t v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
+        u[0] = v0.x, u[1] = v0.y, u[2] = v1.x, u[3] = v1.y, u[4] = v2.x, u[5] = v2.y, u[6] = v3.x, u[7] = v3.y;
+      }
+      double L[8], V[8];
+      bool zero = false;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        L[q] = 0.0;
+        V[q] = 0.0;
+        if (q < w) {  // uniform
+          const double d = Dm[ldlt_tri(q, q)];
+          zero |= d == 0.0;
+          const double rq = rcp_nr(d);
+          double lq[8];
+#pragma unroll
+          for (int r = q + 1; r < 8; r++) lq[r] = Dm[ldlt_tri(r, q)] * rq;
+#pragma unroll
+          for (int r = q + 1; r < 8; r++)
+#pragma unroll
+            for (int c = q + 1; c <= r; c++) Dm[ldlt_tri(r, c)] = __builtin_fma(-lq[r], Dm[ldlt_tri(c, q)], Dm[ldlt_tri(r, c)]);
+          V[q] = u[q];
+          L[q] = u[q] * rq;
+#pragma unroll
+          for (int c = q + 1; c < 8; c++) u[c] = __builtin_fma(-L[q], Dm[ldlt_tri(c, q)], u[c]);
+        }
+      }
+      if (tid == 0 && zero) fail = 1;
+      double2_t* lo = reinterpret_cast<double2_t*>(Lp + ldlt_prow(i));
+      double2_t* vo = reinterpret_cast<double2_t*>(Vp + ldlt_prow(i));
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        lo[h] = double2_t{L[2 * h], L[2 * h + 1]};
+        vo[h] = double2_t{V[2 * h], V[2 * h + 1]};
+      }
+      if (i < N) {
+        double* lrow = Lpk + (size_t)i * (i - 1) / 2 + c0;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          if (c0 + q < i && q < w) lrow[q] = L[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          if (q < w) ys[c0 + q] = L[q];
+      }
+    }
+    __syncthreads();
+    LDLT_TS(2 + 2 * M);
+    // C: trailing tiles
+#pragma unroll
+    for (int t = 0; t < TPT; t++) {
+      if (tk[t] >= 2 * M + 2) {
+        const double* lr = Lp + 34 * ti[t];
+        const double* vr = Vp + 34 * tk[t];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          double Lv[4][4], Vv[4][4];
+#pragma unroll
+          for (int p = 0; p < 4; p++) {
+            const double2_t* ls = reinterpret_cast<const double2_t*>(lr + 8 * p + 4 * h);
+            const double2_t* vs = reinterpret_cast<const double2_t*>(vr + 8 * p + 4 * h);
+            const double2_t l0 = ls[0], l1 = ls[1], v0 = vs[0], v1 = vs[1];
+            Lv[p][0] = l0.x, Lv[p][1] = l0.y, Lv[p][2] = l1.x, Lv[p][3] = l1.y;
+            Vv[p][0] = v0.x, Vv[p][1] = v0.y, Vv[p][2] = v1.x, Vv[p][3] = v1.y;
+          }
+#pragma unroll
+          for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+#pragma unroll
+              for (int q = 0; q < 4; q++) a[t][p][q] = __builtin_fma(-Lv[p][s], Vv[q][s], a[t][p][q]);
+        }
+        if (tk[t] < 2 * M + 4) {  // the next panel publishes itself
+#pragma unroll
+          for (int p = 0; p < 4; p++) {
+            double2_t* dst = reinterpret_cast<double2_t*>(Pn + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] - 2 * M - 2));
+            dst[0] = double2_t{a[t][p][0], a[t][p][1]};
+            dst[1] = double2_t{a[t][p][2], a[t][p][3]};
+          }
+        }
+      }
+    }
+    __syncthreads();
+    LDLT_TS(3 + 2 * M);
+  }
+  if (fail) {
+    if (tid == 0) D.scal[2] = 0.0;
+    return;
+  }
+  if (tid >= 64) return;
+  // L^T x = y in 8-row blocks from the bottom: the block's eight y values (final once the rows
+  // below are done) are read out of their lanes, every lane solves the 8x8 unit upper system
+  // L_KK^T x_K = y_K the same way, then rows above take y_i -= sum_u L[k0+u][i] x_u.  A block's
+  // entries are loaded while the previous block runs (two register sets, the loop unrolled by
+  // two); loads are clamped to written entries and need no masks: rows past N have x = 0, and
+  // lanes at or below the block keep their value by a select.
+  const int lane = tid;
+  double y[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int i = lane + 64 * r;
+    y[r] = i < N ? ys[i] : 0.0;
+  }
+  const int nb = (N + 7) / 8;
+  // (row k's reads run past its k entries into the next rows or the panel arrays after the
+  // factor -- LDS that is written and finite; those terms are discarded by the selects below)
+  auto load_blk = [&](int K, double (&Lkk)[28], double (&Lr)[8][R]) {
+    const int k0 = 8 * K;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = k0 + u;
+      const double* Lk = Lpk + k * (k - 1) / 2;
+#pragma unroll
+      for (int v = 0; v < u; v++) Lkk[ldlt_tri(u - 1, v)] = Lk[k0 + v];  // L[k0+u][k0+v]
+#pragma unroll
+      for (int r = 0; r < R; r++) Lr[u][r] = Lk[lane + 64 * r];  // L[k0+u][i]
+    }
+  };
+  auto solve_blk = [&](int K, const double (&Lkk)[28], const double (&Lr)[8][R]) {
+    const int k0 = 8 * K, rb = k0 >> 6;  // the block's rows sit in y[rb] (8 | 64)
+    double x[8];
+    const double yb = rb == 0 ? y[0] : R == 2 || rb == 1 ? y[1] : y[R - 1];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const double xv = readlane_d(yb, (k0 + u) & 63);
+      x[u] = k0 + u < N ? xv : 0.0;  // rows past N (their x stays out of every sum)
+    }
+#pragma unroll
+    for (int u = 6; u >= 0; u--)
+#pragma unroll
+      for (int v = 7; v > u; v--) x[u] = __builtin_fma(-Lkk[ldlt_tri(v - 1, u)], x[v], x[u]);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int i = lane + 64 * r;
+      double s0 = Lr[0][r] * x[0], s1 = Lr[1][r] * x[1];
+      s0 = __builtin_fma(Lr[2][r], x[2], s0);
+      s1 = __builtin_fma(Lr[3][r], x[3], s1);
+      s0 = __builtin_fma(Lr[4][r], x[4], s0);
+      s1 = __builtin_fma(Lr[5][r], x[5], s1);
+      s0 = __builtin_fma(Lr[6][r], x[6], s0);
+      s1 = __builtin_fma(Lr[7][r], x[7], s1);
+      const double yn = y[r] - (s0 + s1);
+      y[r] = i < k0 ? yn : y[r];
+      if (r == rb) {  // uniform: the block's own rows take x
+        const int u = lane & 7;
+        double xv = x[0];
+#pragma unroll
+        for (int w = 1; w < 8; w++) xv = u == w ? x[w] : xv;
+        y[r] = ((lane ^ k0) & ~7 & 63) == 0 ? xv : y[r];
+      }
+    }
+  };
+  double LkA[28], LrA[8][R], LkB[28], LrB[8][R];
+  load_blk(nb - 1, LkA, LrA);
+  for (int K = nb - 1; K >= 0; K -= 2) {
+    if (K >= 1) load_blk(K - 1, LkB, LrB);
+    solve_blk(K, LkA, LrA);
+    if (K < 1) break;
+    if (K >= 2) load_blk(K - 2, LkA, LrA);
+    solve_blk(K - 1, LkB, LrB);
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (lane + 64 * r < N) D.xp[lane + 64 * r] = y[r];
+  if (lane == 0) D.scal[2] = 1.0;
+  LDLT_TS(63);
+}
+template <int TPT, int NT, int R>
+__global__ __launch_bounds__(NT) void k_ba_ldlt_pan(BaDev D) { k_ba_ldlt_pan_body<TPT, NT, R>(D); }
+template <int TPT, int NT, int R>
+__global__ __launch_bounds__(NT) void k_ba_ldlt_pan_many(const BaDev* __restrict__ Ds) {
+  k_ba_ldlt_pan_body<TPT, NT, R>(Ds[blockIdx.z]);
 }
 
 // ---- reduced camera system, N <= 128: 16-wide blocked LDL^T, FP64 MFMA trailing updates ----
@@ -1720,10 +1995,20 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_blk_many(const BaDev* __restrict
 // packed factor fits LDS, else the 16-wide blocked kernel (LDS or global).
 struct LdltPlan {
   int N = 0, tpt = 0, nt = 1024;
-  bool col = false, in_lds = false, blk = false;
+  bool col = false, in_lds = false, blk = false, pan = false;
   size_t smem = 0;
-  hipError_t prepare(int n) {
+  hipError_t prepare(int n, bool allow_pan = true) {
     N = n;
+    pan = allow_pan && ldlt_use_pan(N);
+    if (pan) {
+      col = false;
+      blk = false;
+      in_lds = true;
+      nt = 512;
+      tpt = 1;
+      smem = ldlt_pan_smem(N);
+      return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    }
     // A/B switch: ORBX_LDLT_BLK=1 takes the MFMA-blocked kernel where it fits (measured slower than
     // the column-step kernel at config 4: 117 vs 60 us; one launch shape per batch)
     blk = ldlt_blk_fits(N) && std::getenv("ORBX_LDLT_BLK") && !std::getenv("ORBX_LDLT_BLOCKED");
@@ -1754,6 +2039,7 @@ struct LdltPlan {
     return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   }
   const void* kernel_ptr() const {
+    if (pan) return (const void*)k_ba_ldlt_pan<1, 512, 2>;
     if (blk) return (const void*)k_ba_ldlt_blk<kLdltBlkNT>;
     if (col) {
       if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col<1, 1024> : (const void*)k_ba_ldlt_col<2, 1024>;
@@ -1767,6 +2053,7 @@ struct LdltPlan {
   }
   // batched driver: the column-step kernel over K problems (blockIdx.z), sized for the largest
   const void* many_ptr() const {
+    if (pan) return (const void*)k_ba_ldlt_pan_many<1, 512, 2>;
     if (blk) return (const void*)k_ba_ldlt_blk_many<kLdltBlkNT>;
     if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col_many<1, 1024> : (const void*)k_ba_ldlt_col_many<2, 1024>;
     if (nt == 512)
@@ -1783,7 +2070,7 @@ struct LdltPlan {
                        dim3(nt), smem, st, Ds);
   }
   void launch(const BaDev& D, hipStream_t st, int stage_limit = 99) const {
-    if (blk || col) {
+    if (blk || col || pan) {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BaDev)>(const_cast<void*>(kernel_ptr())), dim3(1), dim3(nt),
                          smem, st, D);
     } else if (in_lds) {
@@ -2892,6 +3179,7 @@ struct LocalBA {
     if (ldlt_np((int)N) > kLdltMaxNp) return ORBX_ERR_SIZE;
     LdltPlan ldlt;
     BA_CHECK(ldlt.prepare((int)N));
+    D.ldlt_pan = ldlt.pan ? 1 : 0;
     if (!ldlt.col && !ldlt.in_lds) {
       BA_CHECK(c.Sw.alloc((size_t)ldlt_np((int)N) * ldlt_np((int)N)));
       D.Sw = c.Sw.p;
@@ -3000,6 +3288,7 @@ struct LocalBA {
     if (ldlt_np((int)N) > kLdltMaxNp) return ORBX_ERR_SIZE;
     LdltPlan ldlt;
     BA_CHECK(ldlt.prepare((int)N));
+    D.ldlt_pan = ldlt.pan ? 1 : 0;
     if (!ldlt.col && !ldlt.in_lds) {
       BA_CHECK(c.Sw.alloc((size_t)ldlt_np((int)N) * ldlt_np((int)N)));
       D.Sw = c.Sw.p;
@@ -3411,12 +3700,26 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
     gsM = std::max(gsM, D.gsplit);
     nposM = std::max(nposM, D.nposes);
   }
-  LdltPlan ldlt;
-  BA_CHECK(ldlt.prepare(Nmax));
-  if (!ldlt.col && !ldlt.blk) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
+  // each problem takes the LDLT kernel a single call would (bit-identical results): the panel
+  // kernel for the small systems, the column-step one (or the MFMA-blocked opt-in) for the rest
+  int Npan = 0, Ncol = 0;
+  for (int i = 0; i < K; i++) {
+    const int Ni = 6 * Ls[i]->D.nposes;
+    if (ldlt_use_pan(Ni)) Npan = std::max(Npan, Ni); else Ncol = std::max(Ncol, Ni);
+  }
+  LdltPlan ldlt, lpan;
+  if (Ncol > 0 || Npan == 0) {
+    BA_CHECK(ldlt.prepare(std::max(Ncol, 6), false));
+    if (!ldlt.col && !ldlt.blk) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
+    BA_CHECK(ldlt.prepare_many());
+  }
+  if (Npan > 0) {
+    BA_CHECK(lpan.prepare(Npan));
+    if (!lpan.pan) return ORBX_ERR_SIZE;
+    BA_CHECK(lpan.prepare_many());
+  }
   const bool camfold = camfold_on();
   int n_ps = 0, n_psfold = 0;  // problems that launch k_ba_point_schur / whose k_ba_lin_schur takes it
-  BA_CHECK(ldlt.prepare_many());
   if (B.cap < K) {
     if (B.lm_host) (void)hipHostFree(B.lm_host);
     B.lm_host = nullptr;
@@ -3434,6 +3737,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
     n_ps += B.hostD[i].fused == 2 ? 0 : 1;
     n_psfold += B.hostD[i].fused == 2 ? 1 : 0;
     B.hostD[i].camfold = camfold ? 1 : 0;
+    B.hostD[i].ldlt_pan = ldlt_use_pan(6 * B.hostD[i].nposes) ? 1 : 0;
     B.hostD[K + i] = Ls[i]->D;
     B.hostD[K + i].lm = nullptr;
   }
@@ -3474,7 +3778,8 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
         if (nposM > 0) {
           hipLaunchKernelGGL(k_ba_pairs_many, dim3(nbpM, gsM, K), dim3(kPB), 0, st, Dg);
           hipLaunchKernelGGL(k_ba_schur_fin_many, dim3(nbpM, 1, K), dim3(64), 0, st, Dg, 0.0);
-          ldlt.launch_many(Dg, K, st);
+          if (Npan > 0) lpan.launch_many(Dg, K, st);
+          if (Ncol > 0) ldlt.launch_many(Dg, K, st);
         }
         hipLaunchKernelGGL(k_ba_update_many, dim3(gpM, 1, K), dim3(LBS), 0, st, Dg, 0.0);
         hipLaunchKernelGGL(k_ba_errors_many, dim3(geM, 1, K), dim3(LBS), 0, st, Dg, 1, 1);
@@ -3741,6 +4046,7 @@ extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* 
   if (orbx::ldlt_np(N) > orbx::kLdltMaxNp) e = hipErrorInvalidValue;
   orbx::LdltPlan plan;
   if (e == hipSuccess) e = plan.prepare(N);
+  D.ldlt_pan = plan.pan ? 1 : 0;
   double* dSw = nullptr;
   if (e == hipSuccess && !plan.col && !plan.in_lds)
     e = hipMalloc((void**)&dSw, (size_t)orbx::ldlt_np(N) * orbx::ldlt_np(N) * sizeof(double));

@@ -308,13 +308,16 @@ def test_gpu_localba_repeatable(ba):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["default", "mfma_blk"])
-@pytest.mark.parametrize("N", [6, 18, 60, 120, 126, 132, 180, 252])
+@pytest.mark.parametrize("kernel", ["default", "col", "mfma_blk"])
+@pytest.mark.parametrize("N", [6, 18, 60, 120, 126, 132, 168, 174, 180, 252])
 def test_gpu_reduced_system_ldlt(gpu, N, kernel, monkeypatch):
-    """The reduced-system LDLT kernels (column-step in LDS, 16-blocked above; the opt-in
-    MFMA-blocked one up to 128 padded rows) solve SPD Schur systems to FP64 accuracy."""
+    """The reduced-system LDLT kernels (8-wide panels while the packed factor fits LDS, N <= 174;
+    column-step in LDS, 16-blocked above; the opt-in MFMA-blocked one up to 128 padded rows)
+    solve SPD Schur systems to FP64 accuracy."""
     if kernel == "mfma_blk":
         monkeypatch.setenv("ORBX_LDLT_BLK", "1")
+    if kernel == "col":
+        monkeypatch.setenv("ORBX_LDLT_COL", "1")
     import ctypes as C
     from orb_slam2_commit_amd import _lib
     rng = np.random.default_rng(N)
@@ -329,10 +332,12 @@ def test_gpu_reduced_system_ldlt(gpu, N, kernel, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["default", "mfma_blk"])
+@pytest.mark.parametrize("kernel", ["default", "col", "mfma_blk"])
 def test_gpu_reduced_system_ldlt_zero_pivot(gpu, kernel, monkeypatch):
     if kernel == "mfma_blk":
         monkeypatch.setenv("ORBX_LDLT_BLK", "1")
+    if kernel == "col":
+        monkeypatch.setenv("ORBX_LDLT_COL", "1")
     import ctypes as C
     from orb_slam2_commit_amd import _lib
     N = 12
