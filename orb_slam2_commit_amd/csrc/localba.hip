@@ -1589,8 +1589,6 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   int ti[TPT], tk[TPT];
   LDLT_TS(0);
   if (tid == 0) fail = 0;
-  for (int j = tid; j < 3 * PA; j += NT) Pn[j] = 0.0;  // padding rows / columns stay finite
-  __syncthreads();
 #pragma unroll
   for (int t = 0; t < TPT; t++) {
     int x = tid + NT * t, k = 0;
@@ -1613,6 +1611,12 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
         if (tk[t] >= 0 && kk < N) v = i < N ? D.S[(size_t)i * N + kk] : (i == N ? D.bs[kk] : 0.0);
         a[t][p][q] = v;
       }
+  }
+  // (the tile loads above are in flight while the panel arrays are cleared)
+  for (int j = tid; j < 3 * PA; j += NT) Pn[j] = 0.0;  // padding rows / columns stay finite
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < TPT; t++) {
     if (tk[t] >= 0 && tk[t] < 2) {
 #pragma unroll
       for (int p = 0; p < 4; p++) {
