@@ -100,9 +100,10 @@ def hbm_copy_peak(dev, nbytes=2 << 30, reps=10):
         return None
 
 
-def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, cand_per_img):
+def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, cand_per_img, rows=KITTI["height"]):
     """Algorithmic HBM bytes of one launch of `stage` over the batch."""
     sP = sum(P)
+    n_levels = len(P)
     if stage == "k_resize":  # per launch average over the 7 level launches: read P_{l-1} + write P_l
         return n_img * sum(P[l - 1] + P[l] for l in range(1, len(P))) / (len(P) - 1)
     if stage == "k_fast":  # every level pixel read once + 4-B candidates written
@@ -113,10 +114,14 @@ def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, can
         return n_img * (4 * cand_per_img + 4 * kps_per_img)
     if stage == "k_describe":  # raw + blurred levels read, 4-B selection read, 28-B kp + 32-B desc written
         return n_img * (2 * sP + 64 * kps_per_img)
-    if stage == "k_stereo_match":  # per frame: NL*(32+28+8) + NR*(32+28) + Nacc*352
-        return n_frames * (kps_per_img * 68 + kps_per_img * 60 + acc_per_frame * 352)
+    if stage == "k_stereo_match":
+        # per frame: left kp 28 + its ranges 16 + descriptor 32 + uR/depth/SAD out 12; right
+        # (x, index) 8 + sorted descriptor 32; 11 left + 11 right patch rows per refined kp
+        return n_frames * (kps_per_img * 88 + kps_per_img * 40 + acc_per_frame * 352)
     if stage == "k_stereo_prep":
-        return n_frames * kps_per_img * (28 + 8)
+        # per frame: right kp 28 in, sort key 8 + (x, index) 8 out, descriptor 32 in + 32 out
+        # (sorted copy); left kp 28 in + ranges 16 out; row table nlevels x rows x 4 out
+        return n_frames * (kps_per_img * (28 + 8 + 8 + 32 + 32) + kps_per_img * (28 + 16) + n_levels * rows * 4)
     if stage == "k_stereo_finalize":
         return n_frames * kps_per_img * 12
     return None
