@@ -255,7 +255,7 @@ struct BaDev {
   // per position
   double* Hpl;     // na*18 (6x3)
   double* ptc;     // na*12: Hll 9 + bl 3
-  double* cmc;     // na*42: Hpp 36 + bp 6
+  double* cmc;     // na*kCmc: Hpp upper triangle 21 (row-major, c >= r) + bp 6
   double* BD;      // na*18
   double* cf;      // na*6
   // per active point
@@ -485,6 +485,8 @@ __device__ __forceinline__ void lin_stage_store(double* sh, double* out, int k0,
   }
 }
 
+constexpr int kCmc = 27;  // pose terms per position (see lin_pose_terms)
+
 // constructQuadraticForm terms of one edge (DIM = 2 mono, 3 stereo); written
 // through LDS by the block (positions on fixed cameras get pose terms too:
 // nothing reads them).
@@ -532,18 +534,21 @@ __device__ __forceinline__ void lin_point_terms(const LinTerms& T, const double*
 }
 template <int DIM>
 __device__ __forceinline__ void lin_pose_terms(const LinTerms& T, const double* Bm, double* cm) {
+  // only the upper triangle is ever summed (k_ba_cam_sum, k_ba_pairs; k_ba_schur_fin mirrors it),
+  // so only it is formed and stored: kCmc doubles per position instead of 42
+  int j = 0;
 #pragma unroll
   for (int r = 0; r < 6; r++) {
     double s = 0;
 #pragma unroll
     for (int d = 0; d < DIM; d++) s += Bm[6 * d + r] * T.omr[d];
-    cm[36 + r] = s;
+    cm[21 + r] = s;
 #pragma unroll
-    for (int cc = 0; cc < 6; cc++) {
+    for (int cc = r; cc < 6; cc++) {
       double h = 0;
 #pragma unroll
       for (int d = 0; d < DIM; d++) h += Bm[6 * d + r] * T.W * Bm[6 * d + cc];
-      cm[6 * r + cc] = h;
+      cm[j++] = h;
     }
   }
 }
@@ -634,7 +639,7 @@ __device__ __forceinline__ void k_ba_linearize_body(const BaDev& D) {
   lin_stage_store<18, 1>(sh, D.Hpl, k0, nk, act, [&](double* o) {
     if (L.st) lin_cross_terms<3>(L.T, L.A, L.Bm, o); else lin_cross_terms<2>(L.T, L.A, L.Bm, o);
   });
-  lin_stage_store<42, 2>(sh, D.cmc, k0, nk, act, [&](double* o) {
+  lin_stage_store<kCmc, 2>(sh, D.cmc, k0, nk, act, [&](double* o) {
     if (L.st) lin_pose_terms<3>(L.T, L.Bm, o); else lin_pose_terms<2>(L.T, L.Bm, o);
   });
 }
@@ -711,14 +716,9 @@ __device__ __forceinline__ void k_ba_cam_sum_body(const BaDev& D) {
   int lo, hi;
   chunk_range(D.cam_off[ci], D.cam_off[ci + 1], blockIdx.y, D.gsplit, lo, hi);
   for (int t = lo + threadIdx.x; t < hi; t += kGB) {
-    const double* cm = D.cmc + 42 * (size_t)D.cam_pos[t];
-    int j = 0;
+    const double* cm = D.cmc + kCmc * (size_t)D.cam_pos[t];
 #pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-      for (int c = r; c < 6; c++) v[j++] += cm[6 * r + c];
-#pragma unroll
-    for (int r = 0; r < 6; r++) v[21 + r] += cm[36 + r];
+    for (int j = 0; j < kCmc; j++) v[j] += cm[j];
   }
   const double* tot = block_sum_fixed<27>(v, red);
   if (threadIdx.x < 27) D.gpart[((size_t)ci * D.gsplit + blockIdx.y) * 27 + threadIdx.x] = tot[threadIdx.x];
@@ -869,19 +869,22 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
       lin_cross_terms<2>(L.T, L.A, L.Bm, shpl + 18 * t);
     }
   }
-  // pose terms out through LDS in two halves of 21 (coalesced 8-B stores, as k_ba_linearize)
-  double cm[42];
+  // pose terms out through LDS in two parts of 14 and 13 (coalesced 8-B stores, as k_ba_linearize)
+  double cm[kCmc];
   if (L.st) lin_pose_terms<3>(L.T, L.Bm, cm); else lin_pose_terms<2>(L.T, L.Bm, cm);
 #pragma unroll
   for (int h = 0; h < 2; h++) {
+    constexpr int H0 = (kCmc + 1) / 2;
+    const int off = h ? H0 : 0, wd = h ? kCmc - H0 : H0;
     if (act) {
 #pragma unroll
-      for (int j = 0; j < 21; j++) sbuf[21 * t + j] = cm[21 * h + j];
+      for (int j = 0; j < H0; j++)
+        if (j < wd) sbuf[wd * t + j] = cm[off + j];
     }
     __syncthreads();
-    for (int j = t; j < nk * 21; j += NT) {
-      const int kk = j / 21, jj = j - 21 * kk;
-      D.cmc[42 * ((size_t)k0 + kk) + 21 * h + jj] = sbuf[j];
+    for (int j = t; j < nk * wd; j += NT) {
+      const int kk = j / wd, jj = j - wd * kk;
+      D.cmc[kCmc * ((size_t)k0 + kk) + off + jj] = sbuf[j];
     }
     __syncthreads();
   }
@@ -925,7 +928,8 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   for (int j = t; j < nk * 18; j += NT) D.BD[18 * (size_t)k0 + j] = sout[j];
   for (int j = t; j < nk * 6; j += NT) D.cf[6 * (size_t)k0 + j] = sout[18 * NT + j];
 }
-__global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur(BaDev D) { k_ba_lin_schur_body(D); }
+// (LDS holds it to two blocks, i.e. one wave per SIMD: the compiler may spend every register on ILP)
+__global__ __launch_bounds__(kFuseNT) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_ba_lin_schur(BaDev D) { k_ba_lin_schur_body(D); }
 __global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur_many(const BaDev* __restrict__ Ds) {
   k_ba_lin_schur_body(Ds[blockIdx.z]);
 }
@@ -1025,14 +1029,9 @@ __device__ __forceinline__ void k_ba_pairs_body(const BaDev& D) {
 #pragma unroll
       for (int r = 0; r < 6; r++) v[r] += f[r];
       if (cam) {  // k_ba_cam_sum's accumulation (same chunks, same per-thread positions)
-        const double* cm = D.cmc + 42 * (size_t)k;
-        int j = 0;
+        const double* cm = D.cmc + kCmc * (size_t)k;
 #pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-          for (int c = r; c < 6; c++) w[j++] += cm[6 * r + c];
-#pragma unroll
-        for (int r = 0; r < 6; r++) w[21 + r] += cm[36 + r];
+        for (int j = 0; j < kCmc; j++) w[j] += cm[j];
       }
     }
     const double* tot = block_sum_fixed<6, kPB / 64>(v, red);
@@ -3070,7 +3069,7 @@ struct LocalBA {
     const size_t N = 6 * (size_t)nposes;
     BA_CHECK(c.Hpl.alloc(18 * (size_t)na));
     BA_CHECK(c.ptc.alloc(12 * (size_t)na));
-    BA_CHECK(c.cmc.alloc(42 * (size_t)na));
+    BA_CHECK(c.cmc.alloc(kCmc * (size_t)na));
     BA_CHECK(c.BD.alloc(18 * (size_t)na));
     BA_CHECK(c.cf.alloc(6 * (size_t)na));
     BA_CHECK(c.Hll.alloc(9 * (size_t)npa));
