@@ -928,8 +928,7 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   for (int j = t; j < nk * 18; j += NT) D.BD[18 * (size_t)k0 + j] = sout[j];
   for (int j = t; j < nk * 6; j += NT) D.cf[6 * (size_t)k0 + j] = sout[18 * NT + j];
 }
-// (LDS holds it to two blocks, i.e. one wave per SIMD: the compiler may spend every register on ILP)
-__global__ __launch_bounds__(kFuseNT) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_ba_lin_schur(BaDev D) { k_ba_lin_schur_body(D); }
+__global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur(BaDev D) { k_ba_lin_schur_body(D); }
 __global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur_many(const BaDev* __restrict__ Ds) {
   k_ba_lin_schur_body(Ds[blockIdx.z]);
 }
