@@ -830,7 +830,10 @@ __device__ unsigned int* oct_probe_buf;
 __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k_octree(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                                BatchPtrs B) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  const int l = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  // level-major grid (images fastest): every image's level-0 block (the longest) is dispatched
+  // first and the short top levels last, so the kernel's tail is short blocks (longest first;
+  // image-major order left one level-0 block per image until the end: 0.302 -> 0.232 ms per step)
+  const int img = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
   const LevelGeom& L = G->lv[l];
   const int NC = G->node_cap;
   const int NP2 = next_pow2(NC);
@@ -1413,7 +1416,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   if (Gh.ncells > 0) {
     const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap, Gh.oct_kcap);
     T->begin(st);
-    hipLaunchKernelGGL(k_octree, dim3(Gh.nlevels, n_img), dim3(OBS), smem, st, Gd, cells, B);
+    hipLaunchKernelGGL(k_octree, dim3(n_img, Gh.nlevels), dim3(OBS), smem, st, Gd, cells, B);
     T->end(ST_OCTREE, st);
   }
   const int nb = (Gh.max_kps + BS / 64 - 1) / (BS / 64);
