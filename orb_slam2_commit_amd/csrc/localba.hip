@@ -2764,8 +2764,6 @@ struct Ctx {
   DBuf<uint8_t> flag;
   DBuf<LmState> lm;
   DBuf<uint8_t> prob;  // k_ba_prep outputs: FP64 points and edge arrays
-  DBuf<float> Tcw_out, Xw_out;
-  DBuf<double> Tcw_d_out, Xw_d_out;
 };
 
 #define BA_CHECK(x)                          \
@@ -2825,6 +2823,14 @@ struct LocalBA {
   BaDev D{};
   Ctx c;  // device buffers, kept across calls (grow only)
   Arena prob_arena, struct_arena;
+  // result write-back: one device arena (flags, poses, points) read back by ONE copy into pinned
+  // memory, then host copies into the caller's arrays (pageable copies each block the host)
+  Arena wb_arena;
+  struct Wb {
+    double *Tcw_d, *Xw_d;
+    float *Tcw, *Xw;
+    uint8_t* flag;
+  } wb{};
   std::vector<int> e_pt, e_cam;
   std::vector<uint8_t> fixed;
   std::vector<uint8_t> level;  // 0/1 per edge
@@ -3568,11 +3574,10 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
   return ORBX_OK;
 }
 
-// Write-back (src/Optimizer.cc:817-885): the erase list, poses and points,
-// copied into the caller's arrays asynchronously on st (the caller syncs).
+// Write-back (src/Optimizer.cc:817-885): the erase list, poses and points, issued on st into the
+// write-back arena; the caller syncs st, then ba_writeback_finish fills its arrays.
 orbx_status ba_writeback(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, bool ran, hipStream_t st) {
   BaDev& D = L.D;
-  Ctx& c = L.c;
   const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
   const int ge = (ne + LBS - 1) / LBS;
   res->trials = L.trials;
@@ -3586,25 +3591,36 @@ orbx_status ba_writeback(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       for (int i = 0; i < 3 * np; i++) res->Xw_d[i] = pb->Xw[i];
     return ORBX_OK;
   }
-  // :817-847 vToErase
-  if (ne > 0) {
-    hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 0);
-    BA_CHECK(hipGetLastError());
-    BA_CHECK(hipMemcpyAsync(res->edge_outlier, c.flag.p, ne, hipMemcpyDeviceToHost, st));
-  }
-  BA_CHECK(c.Tcw_out.alloc(12 * (size_t)nc));
-  BA_CHECK(c.Xw_out.alloc(3 * (size_t)np));
-  if (res->Tcw_d) BA_CHECK(c.Tcw_d_out.alloc(12 * (size_t)nc));
-  if (res->Xw_d) BA_CHECK(c.Xw_d_out.alloc(3 * (size_t)np));
+  // :817-847 vToErase, then the poses and points; everything lands in the write-back arena and
+  // leaves in one copy (ba_writeback_finish moves it into the caller's arrays after the sync)
+  Arena& A = L.wb_arena;
+  BA_CHECK(A.reserve(arena_bytes({res->Tcw_d ? 12 * sizeof(double) * nc : 0, res->Xw_d ? 3 * sizeof(double) * np : 0,
+                                  12 * sizeof(float) * nc, 3 * sizeof(float) * np, (size_t)ne})));
+  LocalBA::Wb& w = L.wb;
+  w.Tcw_d = res->Tcw_d ? A.take<double>(12 * (size_t)nc) : nullptr;
+  w.Xw_d = res->Xw_d ? A.take<double>(3 * (size_t)np) : nullptr;
+  w.Tcw = A.take<float>(12 * (size_t)nc);
+  w.Xw = A.take<float>(3 * (size_t)np);
+  w.flag = A.take<uint8_t>((size_t)ne);
+  if (ne > 0) hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, w.flag, 0);
   const int gx = (std::max(nc, np) + LBS - 1) / LBS;
-  hipLaunchKernelGGL(k_ba_export, dim3(std::max(gx, 1)), dim3(LBS), 0, st, D, c.Tcw_out.p, c.Xw_out.p,
-                     res->Tcw_d ? c.Tcw_d_out.p : nullptr, res->Xw_d ? c.Xw_d_out.p : nullptr);
+  hipLaunchKernelGGL(k_ba_export, dim3(std::max(gx, 1)), dim3(LBS), 0, st, D, w.Tcw, w.Xw, w.Tcw_d, w.Xw_d);
   BA_CHECK(hipGetLastError());
-  BA_CHECK(hipMemcpyAsync(res->Tcw, c.Tcw_out.p, 12 * sizeof(float) * nc, hipMemcpyDeviceToHost, st));
-  BA_CHECK(hipMemcpyAsync(res->Xw, c.Xw_out.p, 3 * sizeof(float) * np, hipMemcpyDeviceToHost, st));
-  if (res->Tcw_d) BA_CHECK(hipMemcpyAsync(res->Tcw_d, c.Tcw_d_out.p, 12 * sizeof(double) * nc, hipMemcpyDeviceToHost, st));
-  if (res->Xw_d) BA_CHECK(hipMemcpyAsync(res->Xw_d, c.Xw_d_out.p, 3 * sizeof(double) * np, hipMemcpyDeviceToHost, st));
+  BA_CHECK(hipMemcpyAsync(A.hbuf, A.dbuf, A.off, hipMemcpyDeviceToHost, st));
   return ORBX_OK;
+}
+
+// After the stream has synchronised: the write-back arena's pinned copy into the caller's arrays.
+void ba_writeback_finish(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, bool ran) {
+  if (!ran) return;
+  const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
+  Arena& A = L.wb_arena;
+  const LocalBA::Wb& w = L.wb;
+  if (ne > 0) std::memcpy(res->edge_outlier, A.host(w.flag), ne);
+  std::memcpy(res->Tcw, A.host(w.Tcw), 12 * sizeof(float) * nc);
+  std::memcpy(res->Xw, A.host(w.Xw), 3 * sizeof(float) * np);
+  if (res->Tcw_d) std::memcpy(res->Tcw_d, A.host(w.Tcw_d), 12 * sizeof(double) * nc);
+  if (res->Xw_d) std::memcpy(res->Xw_d, A.host(w.Xw_d), 3 * sizeof(double) * np);
 }
 
 orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* res, const StopFlag& stop,
@@ -3659,6 +3675,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   L.unmap_stop();
   if (!ran) return ORBX_OK;
   BA_CHECK(hipStreamSynchronize(st));
+  ba_writeback_finish(L, pb, res, ran);
   if (std::getenv("ORBX_BA_TRACE"))
     std::fprintf(stderr,
                  "[orbx_ba] total %.3f ms, structure %.3f ms (host index %.3f, host poses %.3f, device %.3f, upload %.3f), "
@@ -3896,6 +3913,7 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
   for (int i = 0; i < K; i++) BA_CHECK(ba_writeback(*Ls[i], &pbs[i], &ress[i], ran, st));
   Ls[0]->unmap_stop();
   BA_CHECK(hipStreamSynchronize(st));
+  for (int i = 0; i < K; i++) ba_writeback_finish(*Ls[i], &pbs[i], &ress[i], ran);
   return ORBX_OK;
 }
 
