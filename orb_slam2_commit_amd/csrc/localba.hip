@@ -1013,8 +1013,11 @@ __device__ __forceinline__ void k_ba_pairs_body(const BaDev& D) {
   if (lm_skip(D) || (int)blockIdx.x >= D.nblk + D.nposes || (int)blockIdx.y >= D.gsplit) return;
   __shared__ double red[(kPB / 64 + 1) * 36];
   const int S = D.gsplit, s = blockIdx.y;
-  if ((int)blockIdx.x >= D.nblk) {
-    const int ci = blockIdx.x - D.nblk;
+  // dispatch order: the rhs blocks (every position of a pose, the pose terms too) first, then the
+  // Schur blocks -- the heaviest blocks leave first and the grid's second round is light ones
+  const int bx = (int)blockIdx.x < D.nposes ? D.nblk + (int)blockIdx.x : (int)blockIdx.x - D.nposes;
+  if (bx >= D.nblk) {
+    const int ci = bx - D.nblk;
     const bool cam = D.camfold && !lm_skip_lin(D);  // block-uniform
     double v[6] = {0, 0, 0, 0, 0, 0};
     double w[27];
@@ -1045,13 +1048,13 @@ __device__ __forceinline__ void k_ba_pairs_body(const BaDev& D) {
     return;
   }
   int c1;
-  const int c2 = tri_decode(blockIdx.x, D.nposes, c1);
+  const int c2 = tri_decode(bx, D.nposes, c1);
   double acc[36];
 #pragma unroll
   for (int j = 0; j < 36; j++) acc[j] = 0;
   int lo, hi;
   chunk_range(D.cam_off[c1], D.cam_off[c1 + 1], s, S, lo, hi);
-  const int* tab = D.ptab + D.boff[blockIdx.x] - D.cam_off[c1];
+  const int* tab = D.ptab + D.boff[bx] - D.cam_off[c1];
   for (int t = lo + threadIdx.x; t < hi; t += kPB) {
     const int v = tab[t];
     const int k1 = D.cam_pos[t];
@@ -1069,7 +1072,7 @@ __device__ __forceinline__ void k_ba_pairs_body(const BaDev& D) {
     }
   }
   const double* tot = block_sum_fixed<36, kPB / 64>(acc, red);
-  if (threadIdx.x < 36) D.gpart[((size_t)blockIdx.x * S + s) * 36 + threadIdx.x] = tot[threadIdx.x];
+  if (threadIdx.x < 36) D.gpart[((size_t)bx * S + s) * 36 + threadIdx.x] = tot[threadIdx.x];
 }
 __global__ __launch_bounds__(kPB) void k_ba_pairs(BaDev D) { k_ba_pairs_body(D); }
 __global__ __launch_bounds__(kPB) void k_ba_pairs_many(const BaDev* __restrict__ Ds) {
