@@ -22,10 +22,17 @@ Legs after the headline loop:
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 
-For N>1 the driver launches one rank per GPU with torch.distributed.run;
-frames shard across ranks with no data-path collective in the headline loop
-("weak" scaling), the timed region is bracketed by barrier + synchronize and
-the max over ranks is reported.  Rank 0 prints ONE JSON line.
+Ranks: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) every rank checks
+WORLD_SIZE == --gpus and fails otherwise.  Started plainly with --gpus N > 1 (no WORLD_SIZE), the
+process is only a launcher: before any torch.cuda / HIP call it starts
+`python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py
+<same args>` as a CHILD process (never exec), lets the ranks' output through and exits with the
+child's exit code.  Under RCCL (the default backend) N must not exceed the visible GPUs;
+ORBX_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks wrap onto the devices).
+Frames shard across ranks with no data-path collective in the headline loop ("weak" scaling),
+the timed region is bracketed by barrier + synchronize and the max over ranks is reported.
+Rank 0 prints ONE JSON line; `n_gpus` is the number of ranks that ran, `config.devices_used` the
+distinct GPUs they used (gathered from the ranks), `config.dist_backend` the process-group backend.
 """
 import argparse
 import json
@@ -70,6 +77,59 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/profile.sh + tools/parse_prof.py); null if absent")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(gpus, argv, port):
+    """The torch.distributed.run command line that runs this script as `gpus` ranks on one node
+    (the driver contract's own form: --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def rank_plan(args, env=None):
+    """What this process is: ("rank", world) when it runs the benchmark itself, ("launch", N) when it
+    must start N ranks.  Raises SystemExit when WORLD_SIZE and --gpus disagree (a driver that asked
+    for N GPUs must never get a silent run of a different size).  Pure: reads no GPU state."""
+    env = os.environ if env is None else env
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1 (got %d)" % args.gpus)
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != args.gpus:
+            raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d: the launcher and the flag disagree"
+                             % (world, args.gpus))
+        return "rank", world
+    if args.gpus == 1:
+        return "rank", 1
+    return "launch", args.gpus
+
+
+def launch_ranks(args, argv):
+    """Start the N-rank run as a child process (no exec: nothing here has touched the GPU, and the
+    pool forbids replacing a process anyway) and return its exit code.  The ranks inherit stdout,
+    so rank 0's JSON line is the launcher's output."""
+    backend = os.environ.get("ORBX_DIST_BACKEND", "nccl")
+    if backend != "gloo":
+        import torch  # device_count() does not initialise the GPU on this image
+        ndev = torch.cuda.device_count()
+        if args.gpus > ndev:
+            raise SystemExit("bench.py --gpus %d: only %d GPU(s) visible (RCCL needs one GPU per rank; "
+                             "ORBX_DIST_BACKEND=gloo rehearses more ranks on fewer GPUs)" % (args.gpus, ndev))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    cmd = launcher_cmd(args.gpus, argv, _free_port())
+    print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
 
 
 def level_sizes(w, h, inv_scales):
@@ -630,21 +690,25 @@ def config5_leg(args, rank, world, dev, odist, ex, images, stream):
 
 def main():
     args = parse()
+    kind, n = rank_plan(args)
+    if kind == "launch":
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     import torch
 
     from orb_slam2_commit_amd import dist as odist
     rank, local, world = odist.env_rank()
+    assert world == n
     backend = os.environ.get("ORBX_DIST_BACKEND", "nccl")
-    odist.init(backend, rank, world)
     ndev = torch.cuda.device_count()
     if backend == "gloo":
         # one-GPU rehearsal of the multi-rank flow: ranks wrap onto the available devices
         local = local % max(ndev, 1)
     elif local >= ndev:
         raise SystemExit("LOCAL_RANK %d but only %d GPU(s): one rank per GPU under RCCL" % (local, ndev))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local)  # before the process group, so RCCL binds this rank's GPU
+    odist.init(backend, rank, world)
     dev = torch.device("cuda", local)
-    devices_used = world if backend != "gloo" else min(world, max(ndev, 1))  # distinct GPUs in use
+    devices_used = odist.distinct_devices(local, dev)  # distinct GPUs the ranks actually use
 
     from orb_slam2_commit_amd import ORBextractor, synth
     from orb_slam2_commit_amd import _lib
@@ -799,7 +863,7 @@ def main():
         "config": {"workload": "KITTI-00 stereo 1241x376, 2000 features, extract L+R + ComputeStereoMatches",
                    "batch_frames_per_gpu": B, "global_batch_frames": B * world, "nlevels": 8,
                    "scale_factor": 1.2, "fast_th": [20, 7], "parallelism": "frame-sharded x%d" % world,
-                   "devices_used": devices_used, "dist_backend": backend if world > 1 else None,
+                   "devices_used": devices_used, "dist_backend": odist.backend(),
                    "batches_in_flight": S},
         "roofline": roofline,
         "stage_ms_per_step": {k: round(v[0] / args.profile_steps, 4) for k, v in stages.items()},

@@ -242,6 +242,9 @@ typedef struct {
   int iterations[2];      /* LM iterations run by optimize(5) and optimize(10) */
   int trials;             /* LM inner trials in total */
   double chi2[2];         /* active robust chi2 at the end of each phase */
+  int ran;                /* 1: the optimisation ran and the outputs are the optimised state; 0: the stop
+                           * flag was up before optimize(5) (src/Optimizer.cc:749-751) -- the reference
+                           * then returns with the map untouched, so a caller must skip its write-back */
 } orbx_ba_result;
 
 typedef struct orbx_ba orbx_ba;
@@ -310,6 +313,10 @@ orbx_status orbx_pnp_create_many_device(const float* d_p3d, const float* d_p2d, 
                                         const int32_t* offsets, const float* intr, int n,
                                         const orbx_pnp_params* params, int device, orbx_pnp** out);
 orbx_status orbx_pnp_destroy(orbx_pnp* h);
+/* PnPsolver::SetRansacParameters (src/PnPsolver.cc:136-179, include/PnPsolver.h:71) on an existing
+ * solver, at any time: the derived parameters and maxError = sigma2 * th2 (sigma2: the n values given
+ * at creation, host) are recomputed in place; mnIterations, the best inlier set and pose are kept. */
+orbx_status orbx_pnp_set_ransac_parameters(orbx_pnp* h, const float* sigma2, const orbx_pnp_params* params);
 /* Derived RANSAC parameters (mRansacMinInliers, mRansacMaxIts, mRansacEpsilon). */
 orbx_status orbx_pnp_get_params(const orbx_pnp* h, int* min_inliers, int* max_iterations, float* epsilon);
 /* iterate(nIterations, bNoMore, vbInliers, nInliers).  rand_vals: the next
@@ -511,8 +518,12 @@ orbx_status orbx_pose_optimization_device(const orbx_pose_problem* problems, int
 /* Tracking::TrackReferenceKeyFrame's gather (src/Tracking.cc:910-969) between SearchByBoW(KF, F)
  * and PoseOptimization(&F), on a device batch: PoseOptimization's edge per current-frame feature
  * with a MapPoint, in feature order (src/Optimizer.cc:318-410).  The reference KeyFrame's MapPoints
- * are its stereo points: feature k has one iff kf_depth[k] > 0, at KeyFrame::UnprojectStereo(k)
- * with pose Twc.  Writes obs / Xw / inv_sigma2 (and the feature of each edge) compacted, and
+ * are its stereo points as StereoInitialization / CreateNewKeyFrame create them
+ * (src/Tracking.cc:640-668, 1515-1555): feature k has one iff kf_depth[k] > 0, at
+ * Frame::UnprojectStereo(k) (src/Frame.cc:823-839: mvKeysUn[k], mRwc*x3Dc+mOw -- one OpenCV gemm
+ * with the addend, accumulated in double and rounded once, i.e. Twc*[x3Dc;1]) with pose Twc.
+ * (KeyFrame::UnprojectStereo, src/KeyFrame.cc:758-780, reads mvKeys instead; the two agree whenever
+ * mvKeysUn == mvKeys, i.e. for rectified input without distortion -- KITTI, rectified EuRoC.)  Writes obs / Xw / inv_sigma2 (and the feature of each edge) compacted, and
  * *n_edges -- the inputs of an orbx_pose_problem.  Device pointers; problems[] is a HOST array. */
 typedef struct {
   const orbx_keypoint* f_kps;      /* current frame mvKeysUn */

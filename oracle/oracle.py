@@ -123,6 +123,8 @@ def lib():
         L.oracle_pnp_destroy.restype = None
         L.oracle_pnp_params.argtypes = [P, P, P, P]
         L.oracle_pnp_params.restype = None
+        L.oracle_pnp_set_params.argtypes = [P, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+        L.oracle_pnp_set_params.restype = None
         L.oracle_pnp_iterate.argtypes = [P, C.c_int, P, C.c_int, P, P, P, P, P]
         L.oracle_epnp.argtypes = [P, P, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, P, P]
         L.oracle_epnp.restype = C.c_double
@@ -364,6 +366,15 @@ class PnPsolver:
         self._h = lib().oracle_pnp_create(self.n, _p(self.p3d), _p(self.p2d), _p(self.sigma2), float(fx), float(fy),
                                           float(cx), float(cy), float(probability), int(min_inliers),
                                           int(max_iterations), int(min_set), float(epsilon), float(th2))
+        a, b, c = C.c_int(), C.c_int(), C.c_float()
+        lib().oracle_pnp_params(self._h, C.byref(a), C.byref(b), C.byref(c))
+        self.min_inliers, self.max_its, self.epsilon = a.value, b.value, c.value
+
+    def SetRansacParameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=4, epsilon=0.4,
+                            th2=5.991):
+        """In place, at any time (src/PnPsolver.cc:136-179): iteration count and best set are kept."""
+        lib().oracle_pnp_set_params(self._h, float(probability), int(min_inliers), int(max_iterations), int(min_set),
+                                    float(epsilon), float(th2))
         a, b, c = C.c_int(), C.c_int(), C.c_float()
         lib().oracle_pnp_params(self._h, C.byref(a), C.byref(b), C.byref(c))
         self.min_inliers, self.max_its, self.epsilon = a.value, b.value, c.value

@@ -670,19 +670,11 @@ struct oracle_pnp {
 
 extern "C" {
 
-oracle_pnp* oracle_pnp_create(int n, const float* p3d, const float* p2d, const float* sigma2, float fx, float fy,
-                              float cx, float cy, double probability, int min_inliers, int max_iterations,
-                              int min_set, float epsilon, float th2) {
-  oracle_pnp* h = new oracle_pnp();
-  h->N = n;
-  h->p3d.assign(p3d, p3d + 3 * (size_t)n);
-  h->p2d.assign(p2d, p2d + 2 * (size_t)n);
-  h->sigma2.assign(sigma2, sigma2 + n);
-  h->fu = fx;
-  h->fv = fy;
-  h->uc = cx;
-  h->vc = cy;
-  // SetRansacParameters (:136-179)
+// SetRansacParameters (src/PnPsolver.cc:136-179): the derived parameters and mvMaxError, in place
+// (mnIterations, mnBestInliers and mvbBestInliers are kept, as in the reference)
+void oracle_pnp_set_params(oracle_pnp* h, double probability, int min_inliers, int max_iterations, int min_set,
+                           float epsilon, float th2) {
+  const int n = h->N;
   h->prob = probability;
   h->min_inliers = min_inliers;
   h->max_its = max_iterations;
@@ -701,6 +693,21 @@ oracle_pnp* oracle_pnp_create(int n, const float* p3d, const float* p2d, const f
   h->max_its = std::max(1, std::min(nIterations, h->max_its));
   h->max_error.resize(n);
   for (int i = 0; i < n; i++) h->max_error[i] = h->sigma2[i] * th2;
+}
+
+oracle_pnp* oracle_pnp_create(int n, const float* p3d, const float* p2d, const float* sigma2, float fx, float fy,
+                              float cx, float cy, double probability, int min_inliers, int max_iterations,
+                              int min_set, float epsilon, float th2) {
+  oracle_pnp* h = new oracle_pnp();
+  h->N = n;
+  h->p3d.assign(p3d, p3d + 3 * (size_t)n);
+  h->p2d.assign(p2d, p2d + 2 * (size_t)n);
+  h->sigma2.assign(sigma2, sigma2 + n);
+  h->fu = fx;
+  h->fv = fy;
+  h->uc = cx;
+  h->vc = cy;
+  oracle_pnp_set_params(h, probability, min_inliers, max_iterations, min_set, epsilon, th2);
   h->inl.assign(n, 0);
   h->best.assign(n, 0);
   h->refined.assign(n, 0);

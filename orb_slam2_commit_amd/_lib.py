@@ -58,7 +58,8 @@ class BaProblem(C.Structure):
 
 class BaResult(C.Structure):
     _fields_ = [("Tcw", C.c_void_p), ("Xw", C.c_void_p), ("edge_outlier", C.c_void_p), ("Tcw_d", C.c_void_p),
-                ("Xw_d", C.c_void_p), ("iterations", C.c_int * 2), ("trials", C.c_int), ("chi2", C.c_double * 2)]
+                ("Xw_d", C.c_void_p), ("iterations", C.c_int * 2), ("trials", C.c_int), ("chi2", C.c_double * 2),
+                ("ran", C.c_int)]
 
 
 class PnpProblem(C.Structure):
@@ -157,6 +158,7 @@ SIGNATURES = {
     "orbx_pnp_create_many_device": ([P, P, P, P, P, C.c_int, C.POINTER(PnpParams), C.c_int, P], C.c_int),
     "orbx_pnp_destroy": ([P], C.c_int),
     "orbx_pnp_get_params": ([P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_float)], C.c_int),
+    "orbx_pnp_set_ransac_parameters": ([P, P, C.POINTER(PnpParams)], C.c_int),
     "orbx_pnp_iterate": ([P, C.c_int, P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), P, P,
                           C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
     "orbx_pnp_iterate_stream": ([P, C.c_int, C.POINTER(RandState), C.POINTER(C.c_int), P, P, C.POINTER(C.c_int),

@@ -3584,6 +3584,7 @@ orbx_status ba_writeback(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
   const int ge = (ne + LBS - 1) / LBS;
   res->trials = L.trials;
+  res->ran = ran ? 1 : 0;
   if (!ran) {  // src/Optimizer.cc:749-751: return before any write-back
     std::memcpy(res->Tcw, pb->Tcw, sizeof(float) * 12 * nc);
     std::memcpy(res->Xw, pb->Xw, sizeof(float) * 3 * np);

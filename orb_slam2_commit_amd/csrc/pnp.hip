@@ -1234,18 +1234,9 @@ orbx_status pnp_device_check(int device) {
   return ORBX_OK;
 }
 
-// PnPsolver ctor + SetRansacParameters (src/PnPsolver.cc:67-179) without the upload
-orbx_pnp* pnp_new(const orbx_pnp_problem* p, const orbx_pnp_params* prm, int device) {
-  orbx_pnp* h = new (std::nothrow) orbx_pnp();
-  if (!h) return nullptr;
-  h->device = device;
-  h->st = g_pnp_dev[device].st;
-  const int n = p->n;
-  h->N = n;
-  h->fu = p->fx;
-  h->fv = p->fy;
-  h->uc = p->cx;
-  h->vc = p->cy;
+// SetRansacParameters' derived values (src/PnPsolver.cc:136-179) from the handle's N
+void pnp_derive(orbx_pnp* h, const orbx_pnp_params* prm) {
+  const int n = h->N;
   h->prob = prm->probability;
   h->min_inliers = prm->min_inliers;
   h->max_its = prm->max_iterations;
@@ -1262,6 +1253,21 @@ orbx_pnp* pnp_new(const orbx_pnp_problem* p, const orbx_pnp_params* prm, int dev
   else
     nIterations = (int)std::ceil(std::log(1 - h->prob) / std::log(1 - std::pow(h->epsilon, 3)));
   h->max_its = std::max(1, std::min(nIterations, h->max_its));
+}
+
+// PnPsolver ctor + SetRansacParameters (src/PnPsolver.cc:67-179) without the upload
+orbx_pnp* pnp_new(const orbx_pnp_problem* p, const orbx_pnp_params* prm, int device) {
+  orbx_pnp* h = new (std::nothrow) orbx_pnp();
+  if (!h) return nullptr;
+  h->device = device;
+  h->st = g_pnp_dev[device].st;
+  const int n = p->n;
+  h->N = n;
+  h->fu = p->fx;
+  h->fv = p->fy;
+  h->uc = p->cx;
+  h->vc = p->cy;
+  pnp_derive(h, prm);
   for (int i = 0; i < 16; i++) h->best_Tcw[i] = 0;
   return h;
 }
@@ -1405,6 +1411,26 @@ orbx_status orbx_pnp_destroy(orbx_pnp* h) {
   (void)hipSetDevice(h->device);
   if (h->d_mem) (void)hipFreeAsync(h->d_mem, h->st);
   delete h;
+  return ORBX_OK;
+}
+
+orbx_status orbx_pnp_set_ransac_parameters(orbx_pnp* h, const float* sigma2, const orbx_pnp_params* prm) {
+  if (!h || !prm || (h->N > 0 && !sigma2)) return ORBX_ERR_ARG;
+  if (prm->min_set < 1 || prm->min_set > orbx::kPnpMaxSet) return ORBX_ERR_ARG;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  PnpDevice& dev = g_pnp_dev[h->device];
+  std::lock_guard<std::mutex> lock(dev.mu);
+  // src/PnPsolver.cc:136-179 recomputes the parameters in place: mnIterations, mnBestInliers and
+  // mvbBestInliers (and the best pose) are kept; mvMaxError = sigma2 * th2 is rebuilt
+  pnp_derive(h, prm);
+  h->refine_valid = false;  // Refine() succeeds on "> mRansacMinInliers", which may have changed
+  if (h->N > 0) {
+    PNP_CHECK(dev.pinned_reserve(4 * (size_t)h->N));
+    float* me = (float*)dev.pinned;
+    for (int i = 0; i < h->N; i++) me[i] = sigma2[i] * prm->th2;
+    PNP_CHECK(hipMemcpyAsync(h->d_maxerr, me, 4 * (size_t)h->N, hipMemcpyHostToDevice, h->st));
+    PNP_CHECK(hipStreamSynchronize(h->st));  // the pinned block is reused by the next call
+  }
   return ORBX_OK;
 }
 

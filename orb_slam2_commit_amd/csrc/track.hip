@@ -10,8 +10,9 @@
 // MapPoint's world position and mvInvLevelSigma2[octave].  Here the reference KeyFrame's MapPoints
 // are its stereo points -- the map StereoInitialization / CreateNewKeyFrame build
 // (src/Tracking.cc:640-668, 1515-1555): feature k has a MapPoint iff mvDepth[k] > 0, at
-// KeyFrame::UnprojectStereo(k) (src/KeyFrame.cc:UnprojectStereo: x3Dc = ((u-cx)*z*invfx,
-// (v-cy)*z*invfy, z), then Twc * x3Dc with OpenCV 3.2's float gemm, which accumulates in double).
+// Frame::UnprojectStereo(k) (src/Frame.cc:823-839: x3Dc = ((u-cx)*z*invfx, (v-cy)*z*invfy, z) from
+// mvKeysUn, then mRwc*x3Dc+mOw -- one OpenCV 3.2 float gemm with the addend, accumulated in double and
+// rounded once, which is Twc * [x3Dc; 1] term for term).
 // One block per frame; the compaction is an ordered block scan, so edges keep feature order.
 #include <hip/hip_runtime.h>
 

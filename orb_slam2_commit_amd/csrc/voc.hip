@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/orbx.h"
+#include "orbx_scratch.h"
 
 namespace orbx {
 
@@ -274,9 +275,9 @@ struct orbx_voc {
   bool empty = true;
   void* d_mem = nullptr;
   orbx::VocDev dev{};
-  // per-call scratch (grow only)
-  void* d_work = nullptr;
-  size_t work_cap = 0;
+  // No per-handle scratch: ORB-SLAM2 shares one vocabulary between the Tracking and LocalMapping
+  // threads (Frame::ComputeBoW / KeyFrame::ComputeBoW), so every call brings its own -- a scratch
+  // lease (host API) or stream-ordered allocations on the caller's stream (device API).
 };
 
 namespace {
@@ -411,7 +412,6 @@ orbx_status orbx_voc_destroy(orbx_voc* v) {
   if (!v) return ORBX_ERR_ARG;
   (void)hipSetDevice(v->device);
   if (v->d_mem) (void)hipFree(v->d_mem);
-  if (v->d_work) (void)hipFree(v->d_work);
   if (v->st) (void)hipStreamDestroy(v->st);
   delete v;
   return ORBX_OK;
@@ -458,14 +458,11 @@ orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* 
                b_nid = a256(4 * nt), b_bw = a256(4 * nt), b_bv = a256(8 * nt), b_nb = a256(4 * ns),
                b_fn = a256(4 * nt), b_fo = a256(4 * (nt + ns)), b_ff = a256(4 * nt), b_nf = a256(4 * ns);
   const size_t need = b_desc + b_soff + b_word + b_w + b_nid + b_bw + b_bv + b_nb + b_fn + b_fo + b_ff + b_nf;
-  if (need > v->work_cap) {
-    if (v->d_work) (void)hipFree(v->d_work);
-    v->d_work = nullptr;
-    v->work_cap = 0;
-    VOC_CHECK(hipMalloc(&v->d_work, need));
-    v->work_cap = need;
-  }
-  uint8_t* w = (uint8_t*)v->d_work;
+  // a per-call lease (own stream + arena): concurrent callers never share scratch
+  orbx::ScratchGuard g(v->device);
+  if (!g.l) return ORBX_ERR_HIP;
+  VOC_CHECK(g.l->reserve(need, 0));
+  uint8_t* w = g.l->d;
   uint64_t* d_desc = (uint64_t*)w;
   w += b_desc;
   int32_t* d_soff = (int32_t*)w;
@@ -490,7 +487,7 @@ orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* 
   O.fv_feat = (int32_t*)w;
   w += b_ff;
   O.n_fv = (int32_t*)w;
-  hipStream_t st = v->st;
+  hipStream_t st = g.l->st;
   VOC_CHECK(hipMemcpyAsync(d_desc, desc, 32 * nt, hipMemcpyHostToDevice, st));
   VOC_CHECK(hipMemcpyAsync(d_soff, set_off, 4 * (ns + 1), hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(orbx::k_voc_descend, dim3((total + 255) / 256), dim3(256), 0, st, v->dev, d_desc, total,
@@ -532,15 +529,16 @@ orbx_status orbx_voc_transform_device(orbx_voc* v, const uint8_t* d_desc, int ca
   const size_t nt = (size_t)n_sets * cap;
   if (nt > (size_t)0x7FFFFFFF) return ORBX_ERR_SIZE;
   const size_t need = a256(4 * nt) + a256(8 * nt) + a256(4 * nt);  // word | weight | nid
-  if (need > v->work_cap) {
-    VOC_CHECK(hipStreamSynchronize(st));  // the scratch may still be read by a queued build
-    if (v->d_work) (void)hipFree(v->d_work);
-    v->d_work = nullptr;
-    v->work_cap = 0;
-    VOC_CHECK(hipMalloc(&v->d_work, need));
-    v->work_cap = need;
-  }
-  uint8_t* w = (uint8_t*)v->d_work;
+  // stream-ordered scratch on the caller's stream: freed after k_voc_build in stream order, so a
+  // later call (any thread, any stream) can never overwrite what a queued build still reads
+  int P = 1;
+  while (P < cap) P <<= 1;
+  const size_t smem = (size_t)P * 8 + (size_t)P * 4;
+  if (smem > 64 * 1024)
+    VOC_CHECK(hipFuncSetAttribute((const void*)orbx::k_voc_build, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)smem));
+  uint8_t* w = nullptr;
+  VOC_CHECK(hipMallocAsync((void**)&w, need, st));
   int* d_word = (int*)w;
   double* d_wt = (double*)(w + a256(4 * nt));
   int* d_nid = (int*)(w + a256(4 * nt) + a256(8 * nt));
@@ -548,16 +546,11 @@ orbx_status orbx_voc_transform_device(orbx_voc* v, const uint8_t* d_desc, int ca
   hipLaunchKernelGGL(orbx::k_voc_descend, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, v->dev,
                      (const uint64_t*)d_desc, (int)nt, levelsup, d_word, d_wt, d_nid, d_count, cap, stride,
                      count_step);
-  int P = 1;
-  while (P < cap) P <<= 1;
-  const size_t smem = (size_t)P * 8 + (size_t)P * 4;
-  if (smem > 64 * 1024)
-    VOC_CHECK(hipFuncSetAttribute((const void*)orbx::k_voc_build, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)smem));
   hipLaunchKernelGGL(orbx::k_voc_build, dim3(n_sets), dim3(orbx::kVocBuildThreads), smem, st, v->dev, nullptr,
                      d_word, d_wt, d_nid, O, d_count, cap, count_step);
-  VOC_CHECK(hipGetLastError());
-  return ORBX_OK;
+  const hipError_t e1 = hipGetLastError();
+  const hipError_t e2 = hipFreeAsync(w, st);
+  return (e1 == hipSuccess && e2 == hipSuccess) ? ORBX_OK : ORBX_ERR_HIP;
 }
 
 }  // extern "C"

@@ -57,6 +57,28 @@ def sum_over_ranks(value, device=None):
     return float(t.item())
 
 
+def distinct_devices(local_index, device=None):
+    """Number of distinct GPUs the ranks of this (one-node) job run on: every rank contributes its
+    device index, rank 0 counts the distinct values.  One rank: 1."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return 1
+    device = _coll_device(device)
+    t = torch.tensor([int(local_index)], dtype=torch.int64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return len({int(x.item()) for x in out})
+
+
+def backend():
+    """The initialised process group's backend ("nccl" = RCCL, "gloo"), None for one rank."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_backend()
+    return None
+
+
 def barrier():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():

@@ -588,6 +588,19 @@ class PnPsolver:
 
     def SetRansacParameters(self, probability=0.99, minInliers=8, maxIterations=300, minSet=4, epsilon=0.4,
                             th2=5.991):
+        """src/PnPsolver.cc:136-179.  May be called at any time: after iterate() the derived parameters
+        and maxError are recomputed in place and the iteration count / best set are kept, as in the
+        reference."""
+        prm = _lib.PnpParams(float(probability), int(minInliers), int(maxIterations), int(minSet), float(epsilon),
+                             float(th2))
+        if self._h:
+            check(_lib.lib().orbx_pnp_set_ransac_parameters(self._h, ptr(self.sigma2), C.byref(prm)),
+                  "orbx_pnp_set_ransac_parameters")
+            self.min_set = int(minSet)
+            a, b, c = C.c_int(), C.c_int(), C.c_float()
+            check(_lib.lib().orbx_pnp_get_params(self._h, C.byref(a), C.byref(b), C.byref(c)), "orbx_pnp_get_params")
+            self.min_inliers, self.max_its, self.epsilon = a.value, b.value, c.value
+            return
         self.close()
         prob = _lib.PnpProblem(self.n, ptr(self.p3d), ptr(self.p2d), ptr(self.sigma2), *self.intr)
         prm = _lib.PnpParams(float(probability), int(minInliers), int(maxIterations), int(minSet), float(epsilon),

@@ -10,7 +10,11 @@
 
 for every (reference KeyFrame, current frame) pair of the batch at once.  The reference KeyFrame is
 an earlier frame of the same batch whose MapPoints are its stereo points (mvDepth > 0, the map that
-StereoInitialization / CreateNewKeyFrame build), at KeyFrame::UnprojectStereo with pose Twc.  All
+StereoInitialization / CreateNewKeyFrame build), at Frame::UnprojectStereo (src/Frame.cc:823-839) with
+pose Twc.  Frame::UnprojectStereo and PoseOptimization read mvKeysUn; the batch passes the extractor's
+keypoints (mvKeys), which ARE mvKeysUn for rectified input without distortion (UndistortKeyPoints copies
+them when mDistCoef(0) == 0, src/Frame.cc:471-476) -- KITTI and rectified EuRoC.  Distorted input must
+be undistorted first (orbx_undistort_keypoints) and the undistorted keypoints passed instead.  All
 data stays in HBM; the host reads back only the per-frame counts that size the next call's
 problem descriptors (FeatureVector node counts, edge counts): two small copies per batch.
 """
@@ -55,6 +59,8 @@ class TrackBatch:
         import time
 
         import torch
+        if len(pairs) > self.B:
+            raise ValueError("TrackBatch.run: %d pairs but the per-pair buffers hold B = %d" % (len(pairs), self.B))
         L = _lib.lib()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         sp = C.c_void_p(st.cuda_stream)

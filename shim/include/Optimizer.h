@@ -40,6 +40,7 @@ struct LocalBAResult {
   std::vector<bool> erase;          // per observation: vToErase (:817-847)
   int iterations[2] = {0, 0};       // LM iterations of optimize(5) and optimize(10)
   int trials = 0;
+  bool ran = false;                 // false: stopped before optimize(5), outputs are the inputs (:749-751)
 };
 
 class KeyFrame;

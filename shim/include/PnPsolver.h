@@ -26,8 +26,8 @@ class PnPsolver {
   PnPsolver(const PnPsolver&) = delete;
   PnPsolver& operator=(const PnPsolver&) = delete;
 
-  // Must be called before the first iterate()/find() to change the defaults (as Tracking does);
-  // afterwards it throws std::logic_error (the GPU solver is built with the parameters).
+  // As the reference: may be called at any time; after iterate() the derived parameters are
+  // recomputed in place and the iteration count / best set are kept (src/PnPsolver.cc:136-179).
   void SetRansacParameters(double probability = 0.99, int minInliers = 8, int maxIterations = 300, int minSet = 4,
                            float epsilon = 0.4, float th2 = 5.991);
 
@@ -47,7 +47,6 @@ class PnPsolver {
   orbx_pnp_params mParams{0.99, 8, 300, 4, 0.4f, 5.991f};
   int mRansacMaxIts = 0;
   orbx_pnp* mpGpu = nullptr;
-  bool mbStarted = false;
 };
 
 }  // namespace ORB_SLAM2

@@ -9,6 +9,7 @@
 #include <exception>
 #include <cstring>
 #include <list>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -305,11 +306,12 @@ PnPsolver::~PnPsolver() {
 
 void PnPsolver::SetRansacParameters(double probability, int minInliers, int maxIterations, int minSet, float epsilon,
                                     float th2) {
-  if (mbStarted) throw std::logic_error("PnPsolver::SetRansacParameters after iterate()");
   mParams = orbx_pnp_params{probability, minInliers, maxIterations, minSet, epsilon, th2};
-  if (mpGpu) {
-    orbx_pnp_destroy(mpGpu);
-    mpGpu = nullptr;
+  if (mpGpu) {  // a live solver keeps mnIterations and its best set
+    check(orbx_pnp_set_ransac_parameters(mpGpu, mvSigma2.data(), &mParams), "orbx_pnp_set_ransac_parameters");
+    int mi = 0;
+    float eps = 0;
+    check(orbx_pnp_get_params(mpGpu, &mi, &mRansacMaxIts, &eps), "orbx_pnp_get_params");
   }
 }
 
@@ -332,7 +334,6 @@ cv::Mat PnPsolver::find(std::vector<bool>& vbInliers, int& nInliers) {
 
 cv::Mat PnPsolver::iterate(int nIterations, bool& bNoMore, std::vector<bool>& vbInliers, int& nInliers) {
   ensure_solver();
-  mbStarted = true;
   bNoMore = false;
   vbInliers.clear();
   nInliers = 0;
@@ -440,6 +441,9 @@ void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap
   if (pbStopFlag && *pbStopFlag) return;
   LocalBAResult R;
   LocalBundleAdjustment(P, pbStopFlag, R, mnDevice);
+  // the flag may have gone up between the check above and the library's own poll: the library then
+  // skipped optimize(5), and the reference would have returned here with the map untouched (:749-751)
+  if (!R.ran) return;
   // :803-847 vToErase (the library's per-edge verdict after the last phase), then :849-884
   std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);
   for (size_t e = 0; e < edge_obj.size(); e++) {
@@ -490,18 +494,21 @@ void Optimizer::LocalBundleAdjustment(const LocalBAProblem& P, bool* pbStopFlag,
   res.Tcw = Tout.data();
   res.Xw = Xout.data();
   res.edge_outlier = erase.data();
-  // the LocalMapping thread keeps one solver (device buffers and stream reused across calls)
-  static thread_local orbx_ba* ba = nullptr;
+  // the LocalMapping thread keeps one solver (device buffers and stream reused across calls),
+  // released when that thread exits
+  struct BaDeleter {
+    void operator()(orbx_ba* h) const { orbx_ba_destroy(h); }
+  };
+  static thread_local std::unique_ptr<orbx_ba, BaDeleter> ba;
   static thread_local int ba_device = -1;
-  if (ba && ba_device != device) {
-    orbx_ba_destroy(ba);
-    ba = nullptr;
-  }
+  if (ba && ba_device != device) ba.reset();
   if (!ba) {
-    check(orbx_ba_create(device, &ba), "orbx_ba_create");
+    orbx_ba* h = nullptr;
+    check(orbx_ba_create(device, &h), "orbx_ba_create");
+    ba.reset(h);
     ba_device = device;
   }
-  check(orbx_ba_run_bool(ba, &prob, &res, pbStopFlag), "orbx_ba_run");
+  check(orbx_ba_run_bool(ba.get(), &prob, &res, pbStopFlag), "orbx_ba_run");
   R.Tcw.resize(nc);
   for (int c = 0; c < nc; c++) {
     cv::Mat T(4, 4, CV_32F);
@@ -522,6 +529,7 @@ void Optimizer::LocalBundleAdjustment(const LocalBAProblem& P, bool* pbStopFlag,
   R.iterations[0] = res.iterations[0];
   R.iterations[1] = res.iterations[1];
   R.trials = res.trials;
+  R.ran = res.ran != 0;
 }
 
 }  // namespace ORB_SLAM2

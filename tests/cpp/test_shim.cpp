@@ -337,9 +337,18 @@ static int mode_ba(const char* in, const char* out) {
 // MapPoint and empty feature slots in every KeyFrame.
 static LocalBAProblem g_gathered;
 static std::vector<KeyFrame*> g_gathered_cams;
+static bool* g_raise_after_gather = nullptr;  // stop == 2: the flag goes up after the shim's own check
 static void gathered_hook(const LocalBAProblem& P, const std::vector<KeyFrame*>& cams) {
   g_gathered = P;
   g_gathered_cams = cams;
+  if (g_raise_after_gather) {
+    // another thread (LoopClosing) moves pKF meanwhile, then LocalMapping::InterruptBA raises the flag:
+    // the library sees it before optimize(5), and the stale gathered copy must not be written back
+    cv::Mat T = cams[0]->GetPose();
+    T.at<float>(0, 3) += 1.0f;
+    cams[0]->SetPose(T);
+    *g_raise_after_gather = true;
+  }
 }
 
 static int mode_bagraph(const char* in, const char* out) {
@@ -431,9 +440,11 @@ static int mode_bagraph(const char* in, const char* out) {
   std::vector<int> nobs0(np);
   for (int p = 0; p < np; p++) nobs0[p] = mps[p].Observations();
   Optimizer::mpfnGatheredHook = gathered_hook;
-  bool bStop = stop != 0;
+  bool bStop = stop == 1;
+  g_raise_after_gather = stop == 2 ? &bStop : nullptr;
   Optimizer::LocalBundleAdjustment(pKF, &bStop, &map);
   Optimizer::mpfnGatheredHook = nullptr;
+  g_raise_after_gather = nullptr;
   // output: the gathered window (as orbx_ba_problem arrays), then the graph after the call
   const LocalBAProblem& G = g_gathered;
   const int gnc = (int)G.cameras.size(), gnp = (int)G.points.size(), gne = (int)G.observations.size();

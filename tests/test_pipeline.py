@@ -253,3 +253,32 @@ def test_gpu_two_rank_rehearsal_gathered_records(gpu):
             assert fr[f]["descR"].tobytes() == oR.descriptors.tobytes()
             ouR, _ = oracle.stereo_match(p, oL, oR, KITTI_BF, KITTI_BF / KITTI_FX)
             assert fr[f]["uR"].tobytes() == ouR.tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_bench_launcher_gloo_two_ranks(gpu):
+    """`ORBX_DIST_BACKEND=gloo python bench.py --gpus 2` (no WORLD_SIZE): the launcher starts two ranks
+    under torch.distributed.run as a child process; rank 0's line says n_gpus 2, backend gloo, and the
+    config-5 all-gather ran over 2 ranks with every gathered slot equal to its rank's arena."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["ORBX_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "8", "--inflight", "1", "--unique", "2", "--profile-steps", "1", "--no-cpu-baseline",
+           "--ba-calls", "0", "--single-frames", "0", "--track-steps", "0", "--c3-steps", "0",
+           "--pipeline-steps", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["config"]["dist_backend"] == "gloo"
+    assert out["config"]["devices_used"] == 1  # both ranks wrapped onto the one card
+    assert out["config5"]["sequences"] == 2
+    assert out["config5"]["allgather_backend"] == "gloo"
+    assert out["config5"]["gathered_slots_match"] is True
+    assert out["value"] > 0

@@ -248,3 +248,50 @@ def test_gpu_transform_feeds_search_by_bow(gpu, orb_voc):
     np.testing.assert_array_equal(np.asarray(got[0]), np.asarray(ref[0]))
     assert got[1] == ref[1] and got[1] > 100
     g.close()
+
+
+@pytest.mark.gpu
+def test_gpu_transform_device_queued_while_host_transforms(gpu, orb_voc):
+    """One vocabulary shared by two threads (Tracking's Frame::ComputeBoW and LocalMapping's
+    KeyFrame::ComputeBoW): a device transform still queued behind other work on its stream must not
+    see its scratch overwritten by host transforms issued meanwhile (each call owns its scratch)."""
+    import ctypes as C
+
+    import torch
+    from orb_slam2_commit_amd import ORBVocabulary, _lib
+    from orb_slam2_commit_amd._lib import check, ptr
+    text, vd, leaf = orb_voc
+    o = oracle.Vocabulary(text)
+    g = ORBVocabulary()
+    g.loadFromText(text)
+    S, cap = 12, 2000
+    sets = [synth.voc_descriptors(300 + i, vd, leaf, cap - 37 * i) for i in range(S)]
+    host = np.zeros((S, cap, 32), np.uint8)
+    for i, d in enumerate(sets):
+        host[i, :len(d)] = d
+    d_desc = torch.from_numpy(host).to(gpu)
+    d_cnt = torch.tensor([len(d) for d in sets], dtype=torch.int32, device=gpu)
+    t = lambda n, dt=torch.int32: torch.zeros(n, dtype=dt, device=gpu)  # noqa: E731
+    bw, bv, nb = t(S * cap), t(S * cap, torch.float64), t(S)
+    fn, fo, ff, nf = t(S * cap), t(S * (cap + 1)), t(S * cap), t(S)
+    st = torch.cuda.Stream(gpu)
+    with torch.cuda.stream(st):  # keep the stream busy: the transform's kernels stay queued
+        a = torch.randn(4096, 4096, device=gpu)
+        for _ in range(24):
+            a = torch.tanh(a @ a)
+    check(_lib.lib().orbx_voc_transform_device(g._h, ptr(d_desc), cap, cap, ptr(d_cnt), 1, S, 4, ptr(bw), ptr(bv),
+                                               ptr(nb), ptr(fn), ptr(fo), ptr(ff), ptr(nf),
+                                               C.c_void_p(st.cuda_stream)), "orbx_voc_transform_device")
+    other = synth.voc_descriptors(999, vd, leaf, 8192)  # larger than the device call: forces scratch growth
+    want = o.transform(other, 4)
+    for _ in range(3):
+        _same(g.transform(other, 4), want)
+    st.synchronize()
+    bw, bv, nb, fn, fo, ff, nf = (x.cpu().numpy() for x in (bw, bv, nb, fn, fo, ff, nf))
+    for s, d in enumerate(sets):
+        b, q = int(nb[s]), int(nf[s])
+        foff = fo[s * (cap + 1):s * (cap + 1) + q + 1]
+        got = (bw[s * cap:s * cap + b], bv[s * cap:s * cap + b], fn[s * cap:s * cap + q], foff,
+               ff[s * cap:s * cap + int(foff[-1] if q else 0)])
+        _same(got, o.transform(d, 4))
+    g.close()
