@@ -76,6 +76,10 @@ def parse():
                     help="SQ counter summary (tools/pmc_kernel.sh + tools/sq_summary.py) for issue fractions")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/profile.sh + tools/parse_prof.py); null if absent")
+    ap.add_argument("--rocprof", default=os.path.join(ROOT, "profiles", "r04_rocprof_stages.json"),
+                    help="per-stage kernel time per step from rocprofv3 --stats (tools/rocprof_stages.py)")
+    ap.add_argument("--ba-traffic", default=os.path.join(ROOT, "profiles", "r04_localba_traffic.json"),
+                    help="LocalBA PMC bytes per LM iteration (tools/ba_traffic.py); null if absent")
     return ap.parse_args()
 
 
@@ -160,31 +164,59 @@ def hbm_copy_peak(dev, nbytes=2 << 30, reps=10):
         return None
 
 
-def algorithmic_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame, cand_per_img, rows=KITTI["height"]):
-    """Algorithmic HBM bytes of one launch of `stage` over the batch."""
+# SURVEY.md §8(d) algorithmic bytes.  Extraction, per image:
+#   B_ext = 2*P0 + sum_{l=1..7}(P_{l-1} + P_l) + 4*sum(P) + 60*N
+# (input read + L0 write; resize read + write; FAST read + orientation read + blur read/write +
+# descriptor read; 28-B keypoint + 32-B descriptor written).  Stereo, per frame:
+#   B_st = N_L*68 + N_R*60 + N_acc*352
+# Each kernel is charged the §8(d) terms it performs and nothing else (its own intermediates --
+# FAST candidates, octree selections, the stereo kernels' sorted copies and range tables -- are not
+# algorithmic bytes).  The input copy 2*P0 is never performed (level 0 IS the caller's image), so no
+# kernel carries it, but the whole-step figure keeps it, as §8(d) defines B_ext.
+STAGE_EVENTS_PER_STEP = {"k_resize": 7}  # per-stage timer events per step (k_resize: one per level)
+
+
+def s8d_stage_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame):
+    """§8(d) bytes of ONE timer event of `stage` over the batch (None: no §8(d) term, e.g. k_octree)."""
     sP = sum(P)
-    n_levels = len(P)
-    if stage == "k_resize":  # per launch average over the 7 level launches: read P_{l-1} + write P_l
+    if stage == "k_resize":  # average over the 7 level launches: read P_{l-1} + write P_l
         return n_img * sum(P[l - 1] + P[l] for l in range(1, len(P))) / (len(P) - 1)
-    if stage == "k_fast":  # every level pixel read once + 4-B candidates written
-        return n_img * (sP + 4 * cand_per_img)
-    if stage == "k_blur":  # every level pixel read + written once
+    if stage == "k_fast":  # the FAST read of every level
+        return n_img * sP
+    if stage == "k_blur":  # blur read + write of every level
         return n_img * 2 * sP
-    if stage == "k_octree":  # 4-B candidates read + 4-B selections written
-        return n_img * (4 * cand_per_img + 4 * kps_per_img)
-    if stage == "k_describe":  # raw + blurred levels read, 4-B selection read, 28-B kp + 32-B desc written
-        return n_img * (2 * sP + 64 * kps_per_img)
-    if stage == "k_stereo_match":
-        # per frame: left kp 28 + its ranges 16 + descriptor 32 + uR/depth/SAD out 12; right
-        # (x, index) 8 + sorted descriptor 32; 11 left + 11 right patch rows per refined kp
-        return n_frames * (kps_per_img * 88 + kps_per_img * 40 + acc_per_frame * 352)
-    if stage == "k_stereo_prep":
-        # per frame: right kp 28 in, sort key 8 + (x, index) 8 out, descriptor 32 in + 32 out
-        # (sorted copy); left kp 28 in + ranges 16 out; row table nlevels x rows x 4 out
-        return n_frames * (kps_per_img * (28 + 8 + 8 + 32 + 32) + kps_per_img * (28 + 16) + n_levels * rows * 4)
-    if stage == "k_stereo_finalize":
-        return n_frames * kps_per_img * 12
+    if stage == "k_describe":  # orientation read (raw) + descriptor read (blurred) + 28 + 32 B out
+        return n_img * (2 * sP + 60 * kps_per_img)
+    if stage == "stereo":  # k_stereo_prep + k_stereo_match + k_stereo_finalize together: B_st
+        return n_frames * s8d_stereo_frame(kps_per_img, kps_per_img, acc_per_frame)
     return None
+
+
+def s8d_stereo_frame(n_l, n_r, n_acc):
+    return n_l * 68 + n_r * 60 + n_acc * 352
+
+
+def s8d_frame_bytes(P, kps_per_img, acc_per_frame):
+    """§8(d) bytes of one stereo frame: 2 * B_ext + B_st."""
+    sP = sum(P)
+    b_ext = 2 * P[0] + sum(P[l - 1] + P[l] for l in range(1, len(P))) + 4 * sP + 60 * kps_per_img
+    return 2 * b_ext + s8d_stereo_frame(kps_per_img, kps_per_img, acc_per_frame)
+
+
+STEREO_KERNELS = ("k_stereo_prep", "k_stereo_match", "k_stereo_finalize")
+
+
+def rocprof_stage_ms(path):
+    """Per-step kernel time of each bench stage from a committed rocprofv3 --stats summary
+    (tools/rocprof_stages.py: TotalDurationNs of every dispatch of the stage / the profiled steps)."""
+    if not path or not os.path.exists(path):
+        return {}, None
+    try:
+        j = json.load(open(path))
+        return {k: v["ms_per_step"] for k, v in j["stages"].items()}, dict(
+            file=os.path.relpath(path, ROOT), head=j.get("head"), steps=j.get("steps"), command=j.get("command"))
+    except Exception:  # noqa: BLE001 -- evidence is reported, never fatal
+        return {}, None
 
 
 def pct(xs, q):
@@ -313,6 +345,16 @@ def localba_bytes_per_iteration(P):
     return E * 512 + M * 360 + (6 * K) ** 2 * 16
 
 
+def ba_traffic(args):
+    """PMC HBM bytes per LM iteration of the config-4 call (tools/ba_traffic.py), with its source."""
+    try:
+        j = json.load(open(args.ba_traffic))
+        return dict(bytes_per_iteration=j["bytes_per_iteration"], source=os.path.relpath(args.ba_traffic, ROOT),
+                    head=j.get("head"))
+    except Exception:  # noqa: BLE001 -- absent evidence is reported as null
+        return None
+
+
 def localba_leg(args, rank, world, dev, odist, oracle_mod=None, flags=None, cpus=None):
     """Optimizer::LocalBundleAdjustment on the config-4 problem: whole-job LM iterations/s."""
     import torch
@@ -346,7 +388,7 @@ def localba_leg(args, rank, world, dev, odist, oracle_mod=None, flags=None, cpus
                             points=int(len(P["Xw"])), edges=int(len(P["edge_point"])),
                             stereo_edges=int(np.sum(P["obs"][:, 2] >= 0))),
                roofline=dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
-                             frac=round(achieved / HBM_PEAK_GBS, 5), traffic=None,
+                             frac=round(achieved / HBM_PEAK_GBS, 5), traffic=ba_traffic(args),
                              algorithmic_bytes_per_iteration=int(bpi),
                              note="SURVEY 8d bytes per LM iteration (E*512 + M*360 + (6K)^2*16) x iterations/s "
                                   "of this rank; the trial is a chain of ~12 dependent small launches "
@@ -792,7 +834,7 @@ def main():
     ncand = L.orbx_debug_copy(ex._h, 2, 0, 0, None, 0) // 4  # FAST survivors per cell of the last batch
     cc = np.zeros(ncand, np.int32)
     L.orbx_debug_copy(ex._h, 2, 0, 0, _lib.ptr(cc), cc.nbytes)
-    cand_per_img = float(cc.sum())
+    cand_per_img = float(cc.sum())  # noqa: F841 -- FAST survivors (reported)
     P = [w * h for (w, h) in level_sizes(W, H, ex.GetInverseScaleFactors())]
     dom = max(stages, key=lambda k: stages[k][0]) if stages else None
     traffic_all, traffic_src = {}, None
@@ -812,34 +854,64 @@ def main():
             sq_src = os.path.relpath(args.sq, ROOT)
         except Exception:
             sq_all = {}
+    rp_ms, rp_src = rocprof_stage_ms(args.rocprof)
     copy_gbs = hbm_copy_peak(dev) if rank == 0 else None
+
+    # every stage against the HBM roofline with its §8(d) bytes: live = HIP events on the launch stream
+    # (profiled pass), rocprof = the committed rocprofv3 --stats summary of the same stage
+    def stage_entry(name, ev_s_live, events_per_step, rp_step_ms, traffic):
+        nb = s8d_stage_bytes(name, 2 * B, B, P, kps_per_img, acc_per_frame)
+        e = {"ms_per_step": round(ev_s_live * events_per_step * 1e3, 4), "events_per_step": events_per_step,
+             "rocprof_ms_per_step": round(rp_step_ms, 4) if rp_step_ms else None,
+             "s8d_bytes_per_event": int(nb) if nb else None, "traffic_per_event": traffic}
+        if nb:
+            gbs = nb / ev_s_live / 1e9
+            e.update({"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)})
+            if rp_step_ms:
+                e["frac_rocprof"] = round(nb * events_per_step / (rp_step_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+        return e
+
+    stage_hbm = {}
+    for k, (ms_tot, nl) in stages.items():
+        if k in STEREO_KERNELS:
+            continue
+        ev_s = ms_tot / nl / 1e3
+        stage_hbm[k] = stage_entry(k, ev_s, STAGE_EVENTS_PER_STEP.get(k, 1), rp_ms.get(k), traffic_all.get(k))
+        stage_hbm[k]["valu_issue_frac"] = sq_all.get(k, {}).get("valu_issue_frac")
+    st_k = [k for k in STEREO_KERNELS if k in stages]
+    if st_k:  # ComputeStereoMatches is three launches: charged B_st together (§8(d))
+        ev_s = sum(stages[k][0] / stages[k][1] for k in st_k) / 1e3
+        rp = sum(rp_ms.get(k, 0.0) for k in st_k) or None
+        tr = sum(traffic_all.get(k, 0) for k in st_k) or None
+        stage_hbm["stereo"] = stage_entry("stereo", ev_s, 1, rp, tr)
+        stage_hbm["stereo"]["kernels"] = {k: round(stages[k][0] / stages[k][1], 4) for k in st_k}
     roofline = None
     if dom:
         ms_tot, nl = stages[dom]
         avg_s = ms_tot / nl / 1e3
-        nbytes = algorithmic_bytes(dom, 2 * B, B, P, kps_per_img, acc_per_frame, cand_per_img)
+        ent = stage_hbm.get(dom) or stage_hbm.get("stereo")
+        nbytes = ent["s8d_bytes_per_event"]
         achieved = nbytes / avg_s / 1e9
         roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 5), traffic=traffic_all.get(dom),
-                        traffic_source=traffic_src,
-                        algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4))
+                        frac=round(achieved / HBM_PEAK_GBS, 5), frac_rocprof=ent.get("frac_rocprof"),
+                        traffic=traffic_all.get(dom), traffic_source=traffic_src, rocprof_source=rp_src,
+                        algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4),
+                        bytes_definition="SURVEY 8(d) terms of this kernel only, per timer event over the batch "
+                                         "(k_fast: sum(P) per image; no intermediates)")
         if copy_gbs:
             roofline.update(measured_copy_peak=copy_gbs, frac_of_measured_peak=round(achieved / copy_gbs, 5))
         if dom in sq_all:
             roofline.update(valu_issue_frac=sq_all[dom].get("valu_issue_frac"),
                             salu_issue_frac=sq_all[dom].get("salu_issue_frac"),
                             wait_over_active=sq_all[dom].get("wait_over_active"), sq_source=sq_src)
-
-    # every stage against the same HBM roofline (algorithmic bytes / average launch time)
-    stage_hbm = {}
-    for k, (ms_tot, nl) in stages.items():
-        nb = algorithmic_bytes(k, 2 * B, B, P, kps_per_img, acc_per_frame, cand_per_img)
-        if nb:
-            gbs = nb / (ms_tot / nl / 1e3) / 1e9
-            stage_hbm[k] = {"GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                            "traffic_per_launch": traffic_all.get(k), "algorithmic_per_launch": int(nb),
-                            "valu_issue_frac": sq_all.get(k, {}).get("valu_issue_frac")}
-
+    # the whole step against §8(d): (2 B_ext + B_st) per frame x frames/s
+    frame_b = s8d_frame_bytes(P, kps_per_img, acc_per_frame)
+    step_gbs = frame_b * B / (elapsed / args.steps) / 1e9
+    whole_step = dict(s8d_bytes_per_frame=int(frame_b), GBps=round(step_gbs, 1),
+                      frac=round(step_gbs / HBM_PEAK_GBS, 4),
+                      note="SURVEY 8(d): 2*B_ext + B_st per stereo frame x frames/s of this rank (timed loop); "
+                           "N_acc = surviving stereo matches per frame (a lower bound of the keypoints that reach "
+                           "the SAD, so the figure is conservative)")
     value = odist.job_throughput(B, args.steps, world, elapsed)
     info, cpus = host_info()
     out = {
@@ -866,10 +938,13 @@ def main():
                    "devices_used": devices_used, "dist_backend": odist.backend(),
                    "batches_in_flight": S},
         "roofline": roofline,
+        "whole_step_roofline": whole_step,
         "stage_ms_per_step": {k: round(v[0] / args.profile_steps, 4) for k, v in stages.items()},
         "stage_hbm": stage_hbm,
         "keypoints_per_image": round(kps_per_img, 1),
         "stereo_matches_per_frame": round(acc_per_frame, 1),
+        "fast_candidates_per_image": round(cand_per_img, 1),
+        "level_pixels": P,
         "localba_iters_per_s": None,
         "host": info,
         "cpu_baseline": None,
