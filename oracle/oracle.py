@@ -363,6 +363,7 @@ class PnPsolver:
         self.p2d = np.ascontiguousarray(p2d, np.float32).reshape(-1, 2)
         self.sigma2 = np.ascontiguousarray(sigma2, np.float32)
         self.n = len(self.p3d)
+        self.min_set = int(min_set)
         self._h = lib().oracle_pnp_create(self.n, _p(self.p3d), _p(self.p2d), _p(self.sigma2), float(fx), float(fy),
                                           float(cx), float(cy), float(probability), int(min_inliers),
                                           int(max_iterations), int(min_set), float(epsilon), float(th2))
@@ -375,6 +376,7 @@ class PnPsolver:
         """In place, at any time (src/PnPsolver.cc:136-179): iteration count and best set are kept."""
         lib().oracle_pnp_set_params(self._h, float(probability), int(min_inliers), int(max_iterations), int(min_set),
                                     float(epsilon), float(th2))
+        self.min_set = int(min_set)
         a, b, c = C.c_int(), C.c_int(), C.c_float()
         lib().oracle_pnp_params(self._h, C.byref(a), C.byref(b), C.byref(c))
         self.min_inliers, self.max_its, self.epsilon = a.value, b.value, c.value
@@ -387,7 +389,7 @@ class PnPsolver:
     def iterate(self, n_iterations, rng):
         """rng: object with take(k) -> rand() values; consumes exactly what the reference would.
         Returns (Tcw[4,4] f32 or None, no_more, inliers[n] bool, n_inliers)."""
-        need = 4 * max(n_iterations, self.max_its) + 16
+        need = self.min_set * max(n_iterations, self.max_its) + 16
         vals = np.asarray(rng.peek(need) if hasattr(rng, "peek") else rng.take(need), np.int32)
         used, nm, ni = C.c_int(), C.c_int(), C.c_int()
         T = np.zeros(16, np.float32)
