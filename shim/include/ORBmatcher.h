@@ -3,9 +3,23 @@
 //   static DescriptorDistance(a, b)               include/ORBmatcher.h:50 (src/ORBmatcher.cc:1844-1860)
 //   SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches)  include/ORBmatcher.h:114 (src/ORBmatcher.cc:175-325)
 //   SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12)     include/ORBmatcher.h:116 (src/ORBmatcher.cc:589-736)
+//   SearchByProjection(Frame&, const vector<MapPoint*>&, th)            include/ORBmatcher.h:64
+//                                                       (src/ORBmatcher.cc:46-142)
+//   SearchByProjection(Frame&, const Frame&, th, bMono)                 include/ORBmatcher.h:76
+//                                                       (src/ORBmatcher.cc:1489-1646)
+//   SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)   include/ORBmatcher.h:95
+//                                                       (src/ORBmatcher.cc:1648-1795)
+//   SearchForTriangulation(KeyFrame*, KeyFrame*, F12, vMatchedPairs, bOnlyStereo) include/ORBmatcher.h:134
+//                                                       (src/ORBmatcher.cc:738-925)
+//   Fuse(KeyFrame*, const vector<MapPoint*>&, th)                       include/ORBmatcher.h:148
+//                                                       (src/ORBmatcher.cc:918-1092)
 // DescriptorDistance of one pair stays on the host (a GPU launch per pair would cost more than the
-// popcounts); SearchByBoW runs on the MI355X (orbx_search_by_bow_kf_f / _kf_kf).
+// popcounts); every other member runs its matching on the MI355X (orbx_search_by_bow_*,
+// orbx_search_by_projection, orbx_search_for_triangulation) and applies the result to the object
+// graph here, as the reference's own loops do.
 #pragma once
+#include <set>
+#include <utility>
 #include <vector>
 
 #include "Objects.h"
@@ -21,6 +35,19 @@ class ORBmatcher {
 
   int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches);
   int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12);
+
+  // Tracking::SearchLocalPoints' local map (mbTrackInView / mTrackProj* set by Frame::isInFrustum)
+  int SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th = 3);
+  // Tracking::TrackWithMotionModel: the last frame's MapPoints into the current frame
+  int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono);
+  // Tracking::Relocalization: a candidate KeyFrame's MapPoints not found yet
+  int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
+                         const float th, const int ORBdist);
+  // LocalMapping::CreateNewMapPoints
+  int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
+                             std::vector<std::pair<size_t, size_t>>& vMatchedPairs, const bool bOnlyStereo);
+  // LocalMapping::SearchInNeighbors
+  int Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, const float th = 3.0);
 
   static const int TH_LOW;
   static const int TH_HIGH;

@@ -45,9 +45,14 @@ struct LocalBAResult {
 
 class KeyFrame;
 class Map;
+class Frame;
 
 class Optimizer {
  public:
+  // include/Optimizer.h:71, src/Optimizer.cc:287-528: the pose of pFrame from its MapPoint matches
+  // (four rounds of optimize(10) with outlier levels, on the MI355X).  Sets pFrame->mvbOutlier and,
+  // with >= 3 correspondences, pFrame->SetPose; returns the inlier count (0 below 3 matches).
+  int static PoseOptimization(Frame* pFrame);
   // include/Optimizer.h:61.  pbStopFlag: the reference's bool* (NULL allowed), polled before the
   // run and between LM trials.  Runs on device mnDevice.  Throws std::runtime_error on a library
   // error (the object graph is then left as it was).

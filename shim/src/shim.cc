@@ -1,6 +1,8 @@
-// shim.cc -- the reference's hot-path classes (ORBextractor, Frame's ORB/stereo part, ORBmatcher's
-// SearchByBoW / DescriptorDistance, PnPsolver, Optimizer::LocalBundleAdjustment) as thin C++ over
-// the C ABI of liborbx.so (include/orbx.h).  Argument meaning and error behaviour follow the
+// shim.cc -- the reference's hot-path classes (ORBextractor, Frame's ORB/stereo part and ComputeBoW,
+// ORBmatcher's SearchByBoW x2 / SearchByProjection x3 / SearchForTriangulation / Fuse /
+// DescriptorDistance, PnPsolver, Optimizer::PoseOptimization / LocalBundleAdjustment,
+// MapPoint::ComputeDistinctiveDescriptors, ORBVocabulary) as thin C++ over the C ABI of liborbx.so
+// (include/orbx.h).  Argument meaning and error behaviour follow the
 // reference; a library error (no device, bad geometry) throws std::runtime_error where the
 // reference would assert or crash.  No computation happens here beyond marshalling: gathering the
 // inputs from the object graph and applying the results to it, as the reference's own members do.
@@ -15,12 +17,21 @@
 #include <string>
 #include <thread>
 
+#include <algorithm>
+#include <cmath>
+#include <fstream>
+#include <iterator>
+#include <set>
+#include <sstream>
+
+#include "ORBVocabulary.h"
 #include "ORBextractor.h"
 #include "ORBmatcher.h"
 #include "Objects.h"
 #include "Optimizer.h"
 #include "PnPsolver.h"
 #include "orbx.h"
+#include "orbx_shim.h"
 
 static_assert(sizeof(cv::KeyPoint) == sizeof(orbx_keypoint), "cv::KeyPoint layout");
 static_assert(offsetof(cv::KeyPoint, octave) == offsetof(orbx_keypoint, octave), "cv::KeyPoint layout");
@@ -112,6 +123,7 @@ Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extrac
   // scale tables (src/Frame.cc:66-73) and the static intrinsics (:111-126)
   mnScaleLevels = mpORBextractorLeft->GetLevels();
   mfScaleFactor = mpORBextractorLeft->GetScaleFactor();
+  mfLogScaleFactor = std::log(mfScaleFactor);
   mvScaleFactors = mpORBextractorLeft->GetScaleFactors();
   mvInvScaleFactors = mpORBextractorLeft->GetInverseScaleFactors();
   mvLevelSigma2 = mpORBextractorLeft->GetScaleSigmaSquares();
@@ -128,6 +140,97 @@ Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extrac
   ComputeStereoMatches();
   mvpMapPoints.assign(N, nullptr);
   mvbOutlier.assign(N, false);
+}
+
+long unsigned int Frame::nNextId = 0;
+float Frame::mnMinX = 0.f, Frame::mnMaxX = 0.f, Frame::mnMinY = 0.f, Frame::mnMaxY = 0.f;
+float Frame::mfGridElementWidthInv = 0.f, Frame::mfGridElementHeightInv = 0.f;
+bool Frame::mbInitialComputations = true;
+int gOrbxDevice = 0;
+
+Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, const double& timeStamp, ORBextractor* extractorLeft,
+             ORBextractor* extractorRight, ORBVocabulary* voc, cv::Mat& K, cv::Mat& distCoef, const float& bf,
+             const float& thDepth)
+    : Frame(imLeft, imRight, extractorLeft, extractorRight, K, distCoef, bf, thDepth) {
+  mnId = nNextId++;
+  mTimeStamp = timeStamp;
+  mpORBvocabulary = voc;
+  if (mvKeys.empty()) return;  // src/Frame.cc:87-88
+  // :100-120 on the first frame: image bounds and the grid's cell inverses (FRAME_GRID_COLS/ROWS)
+  if (mbInitialComputations) {
+    ComputeImageBounds(imLeft);
+    mfGridElementWidthInv = static_cast<float>(ORBX_GRID_COLS) / (mnMaxX - mnMinX);
+    mfGridElementHeightInv = static_cast<float>(ORBX_GRID_ROWS) / (mnMaxY - mnMinY);
+    mbInitialComputations = false;
+  }
+  // AssignFeaturesToGrid (:131): the matchers build the 64x48 grid on the device per call
+}
+
+void Frame::ComputeImageBounds(const cv::Mat& imLeft) {
+  // src/Frame.cc:508-537: the undistorted image corners (cv::undistortPoints with P = K on the GPU)
+  if (!mDistCoef.empty() && mDistCoef.at<float>(0, 0) != 0.0f) {
+    const float cols = (float)imLeft.cols, rows = (float)imLeft.rows;
+    std::vector<cv::KeyPoint> corners = {cv::KeyPoint(0.f, 0.f, 1.f), cv::KeyPoint(cols, 0.f, 1.f),
+                                         cv::KeyPoint(0.f, rows, 1.f), cv::KeyPoint(cols, rows, 1.f)};
+    std::vector<cv::KeyPoint> un(4);
+    orbx_camera cam;
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) cam.K[3 * r + c] = mK.at<float>(r, c);
+    const int nd = mDistCoef.rows * mDistCoef.cols;
+    cam.n_dist = nd;
+    for (int i = 0; i < 5; i++) cam.dist[i] = i < nd ? mDistCoef.ptr<float>(0)[i] : 0.f;
+    check(orbx_undistort_keypoints(reinterpret_cast<const orbx_keypoint*>(corners.data()), 4, &cam,
+                                   reinterpret_cast<orbx_keypoint*>(un.data()), gOrbxDevice),
+          "orbx_undistort_keypoints");
+    mnMinX = std::min(un[0].pt.x, un[2].pt.x);
+    mnMaxX = std::max(un[1].pt.x, un[3].pt.x);
+    mnMinY = std::min(un[0].pt.y, un[1].pt.y);
+    mnMaxY = std::max(un[2].pt.y, un[3].pt.y);
+  } else {
+    mnMinX = 0.0f;
+    mnMaxX = (float)imLeft.cols;
+    mnMinY = 0.0f;
+    mnMaxY = (float)imLeft.rows;
+  }
+}
+
+void Frame::SetPose(const cv::Mat& Tcw) {  // src/Frame.cc:287-291
+  mTcw = Tcw.clone();
+  UpdatePoseMatrices();
+}
+
+void Frame::UpdatePoseMatrices() {  // src/Frame.cc:294-304
+  mRcw.create(3, 3, CV_32F);
+  mRwc.create(3, 3, CV_32F);
+  mtcw.create(3, 1, CV_32F);
+  mOw.create(3, 1, CV_32F);
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) {
+      mRcw.at<float>(r, c) = mTcw.at<float>(r, c);
+      mRwc.at<float>(c, r) = mTcw.at<float>(r, c);
+    }
+    mtcw.at<float>(r, 0) = mTcw.at<float>(r, 3);
+  }
+  // mOw = -mRcw.t()*mtcw: one float gemm with alpha = -1, accumulated in double, rounded once
+  for (int r = 0; r < 3; r++) {
+    double acc = 0.0;
+    for (int k = 0; k < 3; k++) acc += (double)mRcw.at<float>(k, r) * (double)mtcw.at<float>(k, 0);
+    mOw.at<float>(r, 0) = (float)(-acc);
+  }
+}
+
+void Frame::ComputeBoW() {  // src/Frame.cc:462-469
+  if (mBowVec.empty()) {
+    if (!mpORBvocabulary) throw std::runtime_error("Frame::ComputeBoW: no vocabulary");
+    mpORBvocabulary->transform(mDescriptors, mBowVec, mFeatVec, 4);
+  }
+}
+
+void KeyFrame::ComputeBoW() {  // src/KeyFrame.cc:65-80
+  if (mBowVec.empty() || mFeatVec.empty()) {
+    if (!mpORBvocabulary) throw std::runtime_error("KeyFrame::ComputeBoW: no vocabulary");
+    mpORBvocabulary->transform(mDescriptors, mBowVec, mFeatVec, 4);
+  }
 }
 
 void Frame::ExtractORB(int flag, const cv::Mat& im) {
@@ -261,6 +364,471 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint
   return n;
 }
 
+// ------------------------------------------------------------------ SearchByProjection / Fuse
+namespace {
+// mvpMapPoints on entry, as the kernel reads it: 0 NULL, 1 a MapPoint with Observations() == 0,
+// 2 a MapPoint with Observations() > 0 (the reference's "F.mvpMapPoints[idx]->Observations() > 0")
+int8_t occupancy(MapPoint* p) { return !p ? 0 : (p->Observations() > 0 ? 2 : 1); }
+
+void copy_desc(MapPoint* p, uint8_t* dst) {
+  const cv::Mat d = p->GetDescriptor();
+  if (d.empty())
+    std::memset(dst, 0, 32);
+  else
+    std::memcpy(dst, d.ptr<uint8_t>(0), 32);
+}
+
+void copy_pos(MapPoint* p, float* dst) {
+  const cv::Mat X = p->GetWorldPos();
+  for (int k = 0; k < 3; k++) dst[k] = X.at<float>(k, 0);
+}
+
+void copy_dist(MapPoint* p, float* dst) {  // mfMinDistance, mfMaxDistance (the kernel applies 0.8 / 1.2)
+  std::unique_lock<std::mutex> lock(p->mMutexPos);
+  dst[0] = p->mfMinDistance;
+  dst[1] = p->mfMaxDistance;
+}
+
+void copy_mat44(const cv::Mat& T, float* dst) {
+  for (int i = 0; i < 16; i++) dst[i] = (i < 12 || T.rows == 4) ? T.at<float>(i / 4, i % 4) : (i == 15 ? 1.f : 0.f);
+}
+
+void set_levels(orbx_proj_frame& f, int nlevels, const std::vector<float>& sf, const std::vector<float>& isig) {
+  if (nlevels < 1 || nlevels > 16 || (int)sf.size() < nlevels) throw std::invalid_argument("orbx shim: nlevels");
+  f.nlevels = nlevels;
+  for (int l = 0; l < 16; l++) {
+    f.scale_factors[l] = l < nlevels ? sf[l] : 0.f;
+    f.inv_level_sigma2[l] = l < nlevels && l < (int)isig.size() ? isig[l] : 0.f;
+  }
+}
+
+// The current Frame as orbx_proj_frame (pointers into F and into the caller's occ / desc buffers)
+orbx_proj_frame proj_frame(Frame& F, std::vector<int8_t>& occ, cv::Mat& desc) {
+  orbx_proj_frame f;
+  std::memset(&f, 0, sizeof(f));
+  f.n = F.N;
+  occ.resize(F.N > 0 ? F.N : 1);
+  for (int i = 0; i < F.N; i++) occ[i] = occupancy(F.mvpMapPoints[i]);
+  desc = continuous(F.mDescriptors);
+  f.keys_un = reinterpret_cast<const orbx_keypoint*>(F.mvKeysUn.data());
+  f.desc = F.N > 0 ? desc.data : nullptr;
+  f.u_right = F.mvuRight.empty() ? nullptr : F.mvuRight.data();
+  f.occ = occ.data();
+  f.min_x = Frame::mnMinX;
+  f.max_x = Frame::mnMaxX;
+  f.min_y = Frame::mnMinY;
+  f.max_y = Frame::mnMaxY;
+  f.grid_inv_w = Frame::mfGridElementWidthInv;
+  f.grid_inv_h = Frame::mfGridElementHeightInv;
+  set_levels(f, F.mnScaleLevels, F.mvScaleFactors, F.mvInvLevelSigma2);
+  f.log_scale_factor = F.mfLogScaleFactor;
+  f.fx = Frame::fx;
+  f.fy = Frame::fy;
+  f.cx = Frame::cx;
+  f.cy = Frame::cy;
+  f.bf = F.mbf;
+  f.b = F.mb;
+  copy_mat44(F.mTcw, f.Tcw);
+  return f;
+}
+
+// The projected MapPoints of one call, SoA
+struct ProjPoints {
+  std::vector<uint8_t> desc, flags;
+  std::vector<float> pos, normal, dist, angle, track;
+  std::vector<int32_t> octave, level, point_match;
+  explicit ProjPoints(size_t n)
+      : desc(32 * std::max<size_t>(n, 1), 0), flags(std::max<size_t>(n, 1), 0), pos(3 * std::max<size_t>(n, 1), 0.f),
+        normal(3 * std::max<size_t>(n, 1), 0.f), dist(2 * std::max<size_t>(n, 1), 0.f),
+        angle(std::max<size_t>(n, 1), 0.f), track(4 * std::max<size_t>(n, 1), 0.f),
+        octave(std::max<size_t>(n, 1), 0), level(std::max<size_t>(n, 1), 0), point_match(std::max<size_t>(n, 1), -1) {}
+  void fill(orbx_proj_problem& p, int n) {
+    p.n_points = n;
+    p.desc = desc.data();
+    p.flags = flags.data();
+    p.pos = pos.data();
+    p.normal = normal.data();
+    p.dist_minmax = dist.data();
+    p.angle = angle.data();
+    p.octave = octave.data();
+    p.track = track.data();
+    p.track_level = level.data();
+    p.point_match = point_match.data();
+  }
+};
+
+orbx_proj_problem proj_problem(int kind, float th, const ORBmatcher& m) {
+  orbx_proj_problem p;
+  std::memset(&p, 0, sizeof(p));
+  p.kind = kind;
+  p.th = th;
+  p.view_cos_limit = 0.5f;
+  (void)m;
+  return p;
+}
+
+// frame_out -> the Frame's mvpMapPoints, as the reference's assignments leave them
+void apply_frame_out(Frame& F, const std::vector<int32_t>& frame_out, const std::vector<MapPoint*>& pts) {
+  for (int i = 0; i < F.N; i++) {
+    const int k = frame_out[i];
+    if (k >= 0)
+      F.mvpMapPoints[i] = pts[k];
+    else if (k == -2)
+      F.mvpMapPoints[i] = nullptr;
+  }
+}
+}  // namespace
+
+int ORBmatcher::SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th) {
+  // src/ORBmatcher.cc:46-142.  The MapPoints carry Tracking::SearchLocalPoints' frustum results
+  // (mbTrackInView, mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos).
+  const int n = (int)vpMapPoints.size();
+  std::vector<int8_t> occ;
+  cv::Mat desc;
+  orbx_proj_problem p = proj_problem(ORBX_PROJ_LOCAL, th, *this);
+  p.f = proj_frame(F, occ, desc);
+  ProjPoints P(n);
+  for (int k = 0; k < n; k++) {
+    MapPoint* pMP = vpMapPoints[k];
+    if (!pMP) continue;
+    const bool take = pMP->mbTrackInView && !pMP->isBad();
+    P.flags[k] = (uint8_t)((take ? 1 : 0) | (pMP->Observations() > 0 ? 2 : 0));
+    if (!take) continue;
+    copy_desc(pMP, &P.desc[32 * (size_t)k]);
+    P.track[4 * k] = pMP->mTrackProjX;
+    P.track[4 * k + 1] = pMP->mTrackProjY;
+    P.track[4 * k + 2] = pMP->mTrackProjXR;
+    P.track[4 * k + 3] = pMP->mTrackViewCos;
+    P.level[k] = pMP->mnTrackScaleLevel;
+  }
+  P.fill(p, n);
+  p.frustum = 0;
+  p.nnratio = mfNNratio;
+  p.check_ori = mbCheckOrientation;
+  std::vector<int32_t> frame_out(F.N > 0 ? F.N : 1, -1);
+  int32_t nm = 0;
+  p.frame_out = frame_out.data();
+  p.nmatches = &nm;
+  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection");
+  apply_frame_out(F, frame_out, vpMapPoints);
+  return nm;
+}
+
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
+  // src/ORBmatcher.cc:1489-1646: the last frame's non-outlier MapPoints
+  const int n = LastFrame.N;
+  std::vector<int8_t> occ;
+  cv::Mat desc;
+  orbx_proj_problem p = proj_problem(ORBX_PROJ_LAST_FRAME, th, *this);
+  p.f = proj_frame(CurrentFrame, occ, desc);
+  ProjPoints P(n);
+  for (int i = 0; i < n; i++) {
+    MapPoint* pMP = LastFrame.mvpMapPoints[i];
+    if (!pMP) continue;
+    const bool take = !LastFrame.mvbOutlier[i];
+    P.flags[i] = (uint8_t)((take ? 1 : 0) | (pMP->Observations() > 0 ? 2 : 0));
+    if (!take) continue;
+    copy_desc(pMP, &P.desc[32 * (size_t)i]);
+    copy_pos(pMP, &P.pos[3 * (size_t)i]);
+    P.angle[i] = LastFrame.mvKeysUn[i].angle;
+    P.octave[i] = LastFrame.mvKeys[i].octave;
+  }
+  P.fill(p, n);
+  p.check_ori = mbCheckOrientation;
+  p.mono = bMono;
+  copy_mat44(LastFrame.mTcw, p.last_Tcw);
+  std::vector<int32_t> frame_out(CurrentFrame.N > 0 ? CurrentFrame.N : 1, -1);
+  int32_t nm = 0;
+  p.frame_out = frame_out.data();
+  p.nmatches = &nm;
+  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection");
+  apply_frame_out(CurrentFrame, frame_out, LastFrame.mvpMapPoints);
+  return nm;
+}
+
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
+                                   const float th, const int ORBdist) {
+  // src/ORBmatcher.cc:1648-1795: the KeyFrame's MapPoints not found yet
+  const std::vector<MapPoint*> vpMPs = pKF->GetMapPointMatches();
+  const int n = (int)vpMPs.size();
+  std::vector<int8_t> occ;
+  cv::Mat desc;
+  orbx_proj_problem p = proj_problem(ORBX_PROJ_KEYFRAME, th, *this);
+  p.f = proj_frame(CurrentFrame, occ, desc);
+  ProjPoints P(n);
+  for (int i = 0; i < n; i++) {
+    MapPoint* pMP = vpMPs[i];
+    if (!pMP) continue;
+    const bool take = !pMP->isBad() && !sAlreadyFound.count(pMP);
+    P.flags[i] = (uint8_t)((take ? 1 : 0) | (pMP->Observations() > 0 ? 2 : 0));
+    if (!take) continue;
+    copy_desc(pMP, &P.desc[32 * (size_t)i]);
+    copy_pos(pMP, &P.pos[3 * (size_t)i]);
+    copy_dist(pMP, &P.dist[2 * (size_t)i]);
+    P.angle[i] = pKF->mvKeysUn[i].angle;
+  }
+  P.fill(p, n);
+  p.check_ori = mbCheckOrientation;
+  p.orb_dist = ORBdist;
+  std::vector<int32_t> frame_out(CurrentFrame.N > 0 ? CurrentFrame.N : 1, -1);
+  int32_t nm = 0;
+  p.frame_out = frame_out.data();
+  p.nmatches = &nm;
+  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection");
+  apply_frame_out(CurrentFrame, frame_out, vpMPs);
+  return nm;
+}
+
+namespace {
+// pKF as the frame of a Fuse problem: its keypoints, descriptors, mvuRight, its own (integer) image
+// bounds and grid, scale tables and pose (src/ORBmatcher.cc:918-1054 reads exactly these)
+orbx_proj_frame fuse_frame(KeyFrame* pKF, cv::Mat& desc) {
+  orbx_proj_frame f;
+  std::memset(&f, 0, sizeof(f));
+  f.n = pKF->N;
+  desc = continuous(pKF->mDescriptors);
+  f.keys_un = reinterpret_cast<const orbx_keypoint*>(pKF->mvKeysUn.data());
+  f.desc = pKF->N > 0 ? desc.data : nullptr;
+  f.u_right = pKF->mvuRight.empty() ? nullptr : pKF->mvuRight.data();
+  f.occ = nullptr;
+  f.min_x = (float)pKF->mnMinX;
+  f.max_x = (float)pKF->mnMaxX;
+  f.min_y = (float)pKF->mnMinY;
+  f.max_y = (float)pKF->mnMaxY;
+  f.grid_inv_w = pKF->mfGridElementWidthInv;
+  f.grid_inv_h = pKF->mfGridElementHeightInv;
+  set_levels(f, pKF->mnScaleLevels, pKF->mvScaleFactors, pKF->mvInvLevelSigma2);
+  f.log_scale_factor = pKF->mfLogScaleFactor;
+  f.fx = pKF->fx;
+  f.fy = pKF->fy;
+  f.cx = pKF->cx;
+  f.cy = pKF->cy;
+  f.bf = pKF->mbf;
+  f.b = pKF->mb;
+  copy_mat44(pKF->GetPose(), f.Tcw);
+  return f;
+}
+
+// The matching half of Fuse for the points `which` (indices into vpMapPoints) in their current state:
+// best[k] = pKF feature for which[k], or -1
+void fuse_match(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, const std::vector<int>& which, float th,
+                int device, std::vector<int32_t>& best) {
+  const int n = (int)which.size();
+  cv::Mat desc;
+  orbx_proj_problem p;
+  std::memset(&p, 0, sizeof(p));
+  p.kind = ORBX_PROJ_FUSE;
+  p.th = th;
+  p.f = fuse_frame(pKF, desc);
+  ProjPoints P(n);
+  for (int k = 0; k < n; k++) {
+    MapPoint* pMP = vpMapPoints[which[k]];
+    if (!pMP) continue;
+    const bool take = !pMP->isBad() && !pMP->IsInKeyFrame(pKF);
+    P.flags[k] = (uint8_t)((take ? 1 : 0) | (pMP->Observations() > 0 ? 2 : 0));
+    if (!take) continue;
+    copy_desc(pMP, &P.desc[32 * (size_t)k]);
+    copy_pos(pMP, &P.pos[3 * (size_t)k]);
+    const cv::Mat nrm = pMP->GetNormal();
+    for (int c = 0; c < 3; c++) P.normal[3 * (size_t)k + c] = nrm.empty() ? 0.f : nrm.at<float>(c, 0);
+    copy_dist(pMP, &P.dist[2 * (size_t)k]);
+  }
+  P.fill(p, n);
+  std::vector<int32_t> frame_out(pKF->N > 0 ? pKF->N : 1, -1);
+  int32_t nm = 0;
+  p.frame_out = frame_out.data();
+  p.nmatches = &nm;
+  check(orbx_search_by_projection(&p, device), "orbx_search_by_projection (Fuse)");
+  best.assign(P.point_match.begin(), P.point_match.begin() + n);
+}
+}  // namespace
+
+int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, const float th) {
+  // src/ORBmatcher.cc:918-1092.  Point i's match depends only on point i and pKF's keypoints, so all
+  // points are matched in one launch on their entry state; the Replace / AddObservation block then
+  // runs here in point order, as the reference's loop does.  A later point whose own state an
+  // earlier Replace changed (it received observations and a new descriptor, or became bad) is
+  // matched again in its current state before it is applied.
+  const int n = (int)vpMapPoints.size();
+  std::vector<int> all(n);
+  for (int i = 0; i < n; i++) all[i] = i;
+  std::vector<int32_t> best;
+  fuse_match(pKF, vpMapPoints, all, th, mDevice, best);
+  std::set<MapPoint*> touched;  // MapPoints an earlier Replace modified
+  int nFused = 0;
+  for (int i = 0; i < n; i++) {
+    MapPoint* pMP = vpMapPoints[i];
+    if (!pMP) continue;
+    int bestIdx = best[i];
+    if (touched.count(pMP)) {
+      std::vector<int32_t> b1;
+      fuse_match(pKF, vpMapPoints, std::vector<int>{i}, th, mDevice, b1);
+      bestIdx = b1[0];
+    }
+    if (bestIdx < 0) continue;
+    if (pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;  // the reference's check, at this point's turn
+    MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
+    if (pMPinKF) {
+      if (!pMPinKF->isBad()) {
+        if (pMPinKF->Observations() > pMP->Observations()) {
+          pMP->Replace(pMPinKF);
+          touched.insert(pMPinKF);
+        } else {
+          pMPinKF->Replace(pMP);
+          touched.insert(pMP);
+        }
+        touched.insert(pMP);
+        touched.insert(pMPinKF);
+      }
+    } else {
+      pMP->AddObservation(pKF, bestIdx);
+      pKF->AddMapPoint(pMP, bestIdx);
+      touched.insert(pMP);
+    }
+    nFused++;
+  }
+  return nFused;
+}
+
+int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
+                                       std::vector<std::pair<size_t, size_t>>& vMatchedPairs, const bool bOnlyStereo) {
+  // src/ORBmatcher.cc:738-925 (caller LocalMapping::CreateNewMapPoints, src/LocalMapping.cc:363)
+  struct Side {
+    std::vector<uint8_t> has_mp;
+    std::vector<uint32_t> ids;
+    std::vector<int32_t> off, feat;
+    cv::Mat desc;
+    orbx_tri_kf kf(KeyFrame* K) {
+      const int n = K->N;
+      has_mp.assign(n > 0 ? n : 1, 0);
+      for (int i = 0; i < n; i++) has_mp[i] = K->GetMapPoint(i) != nullptr;
+      off.push_back(0);
+      for (const auto& node : K->mFeatVec) {
+        ids.push_back(node.first);
+        for (unsigned int f : node.second) feat.push_back((int32_t)f);
+        off.push_back((int32_t)feat.size());
+      }
+      desc = continuous(K->mDescriptors);
+      return orbx_tri_kf{n, reinterpret_cast<const orbx_keypoint*>(K->mvKeysUn.data()), n > 0 ? desc.data : nullptr,
+                         K->mvuRight.empty() ? nullptr : K->mvuRight.data(), has_mp.data(), (int)ids.size(),
+                         ids.data(), off.data(), feat.data()};
+    }
+  } s1, s2;
+  orbx_tri_problem p;
+  std::memset(&p, 0, sizeof(p));
+  p.kf1 = s1.kf(pKF1);
+  p.kf2 = s2.kf(pKF2);
+  for (int i = 0; i < 9; i++) p.F12[i] = F12.at<float>(i / 3, i % 3);
+  const cv::Mat C1 = pKF1->GetCameraCenter();
+  for (int k = 0; k < 3; k++) p.C1w[k] = C1.at<float>(k, 0);
+  copy_mat44(pKF2->GetPose(), p.T2w);
+  p.fx = pKF2->fx;
+  p.fy = pKF2->fy;
+  p.cx = pKF2->cx;
+  p.cy = pKF2->cy;
+  const int nl = pKF2->mnScaleLevels;
+  if (nl < 1 || nl > 16) throw std::invalid_argument("SearchForTriangulation: nlevels");
+  for (int l = 0; l < 16; l++) {
+    p.scale_factors2[l] = l < nl ? pKF2->mvScaleFactors[l] : 0.f;
+    p.level_sigma2_2[l] = l < nl ? pKF2->mvLevelSigma2[l] : 0.f;
+  }
+  p.only_stereo = bOnlyStereo;
+  p.check_ori = mbCheckOrientation;
+  std::vector<int32_t> m12(pKF1->N > 0 ? pKF1->N : 1, -1);
+  int32_t nm = 0;
+  p.match12 = m12.data();
+  p.nmatches = &nm;
+  check(orbx_search_for_triangulation(&p, mDevice), "orbx_search_for_triangulation");
+  vMatchedPairs.clear();
+  vMatchedPairs.reserve(nm);
+  for (int i = 0; i < pKF1->N; i++)
+    if (m12[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)m12[i]));
+  return nm;
+}
+
+// ------------------------------------------------------------------ MapPoint / ORBVocabulary
+void MapPoint::ComputeDistinctiveDescriptors() {
+  // src/MapPoint.cc:249-320: the observed descriptors of non-bad KeyFrames in observation (map)
+  // order; the one with the least median distance to the others becomes mDescriptor
+  std::map<KeyFrame*, size_t> observations;
+  {
+    std::unique_lock<std::mutex> lock1(mMutexFeatures);
+    if (mbBad) return;
+    observations = mObservations;
+  }
+  if (observations.empty()) return;
+  std::vector<uint8_t> desc;
+  desc.reserve(32 * observations.size());
+  for (const auto& o : observations) {
+    KeyFrame* pKF = o.first;
+    if (pKF->isBad()) continue;
+    const uint8_t* row = pKF->mDescriptors.ptr<uint8_t>((int)o.second);
+    desc.insert(desc.end(), row, row + 32);
+  }
+  if (desc.empty()) return;
+  const int32_t off[2] = {0, (int32_t)(desc.size() / 32)};
+  int32_t best = -1;
+  check(orbx_distinctive_descriptors(desc.data(), off, 1, &best, nullptr, gOrbxDevice), "orbx_distinctive_descriptors");
+  if (best < 0) return;
+  cv::Mat d(1, 32, CV_8U);
+  std::memcpy(d.data, &desc[32 * (size_t)best], 32);
+  std::unique_lock<std::mutex> lock(mMutexFeatures);
+  mDescriptor = d;
+}
+
+ORBVocabulary::~ORBVocabulary() {
+  if (mpGpu) orbx_voc_destroy(mpGpu);
+}
+
+bool ORBVocabulary::loadFromText(const std::string& text) {
+  if (mpGpu) {
+    orbx_voc_destroy(mpGpu);
+    mpGpu = nullptr;
+  }
+  check(orbx_voc_load_text(text.data(), text.size(), mDevice, &mpGpu), "orbx_voc_load_text");
+  check(orbx_voc_info(mpGpu, mInfo), "orbx_voc_info");
+  return true;
+}
+
+bool ORBVocabulary::loadFromTextFile(const std::string& filename) {
+  std::ifstream f(filename.c_str(), std::ios::binary);
+  if (!f.is_open()) return false;  // TemplatedVocabulary.h:1343-1347
+  std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  return loadFromText(text);
+}
+
+void ORBVocabulary::transform(const cv::Mat& descriptors, DBoW2::BowVector& v, DBoW2::FeatureVector& fv,
+                              int levelsup) const {
+  // TemplatedVocabulary.h:1125-1196 on the device: every row descends the tree there
+  v.clear();
+  fv.clear();
+  if (!mpGpu) throw std::runtime_error("ORBVocabulary::transform: no vocabulary loaded");
+  const int n = descriptors.empty() ? 0 : descriptors.rows;
+  if (n == 0) return;
+  const cv::Mat d = continuous(descriptors);
+  const int32_t set_off[2] = {0, n};
+  std::vector<uint32_t> words(n), nodes(n);
+  std::vector<double> values(n);
+  std::vector<int32_t> fv_off(n + 1), fv_feat(n);
+  int32_t nb = 0, nf = 0;
+  check(orbx_voc_transform(mpGpu, d.data, set_off, 1, levelsup, words.data(), values.data(), &nb, nodes.data(),
+                           fv_off.data(), fv_feat.data(), &nf),
+        "orbx_voc_transform");
+  for (int k = 0; k < nb; k++) v.emplace_hint(v.end(), words[k], values[k]);
+  for (int j = 0; j < nf; j++) {
+    std::vector<unsigned int>& feats = fv[nodes[j]];
+    for (int q = fv_off[j]; q < fv_off[j + 1]; q++) feats.push_back((unsigned int)fv_feat[q]);
+  }
+}
+
+void ORBVocabulary::transform(const std::vector<cv::Mat>& features, DBoW2::BowVector& v, DBoW2::FeatureVector& fv,
+                              int levelsup) const {
+  cv::Mat d((int)features.size(), 32, CV_8U);
+  for (size_t i = 0; i < features.size(); i++) std::memcpy(d.ptr<uint8_t>((int)i), features[i].ptr<uint8_t>(0), 32);
+  if (features.empty()) d.release();
+  transform(d, v, fv, levelsup);
+}
+
 // ------------------------------------------------------------------ PnPsolver
 int PnPsolver::mnDevice = 0;
 
@@ -361,6 +929,53 @@ cv::Mat PnPsolver::iterate(int nIterations, bool& bNoMore, std::vector<bool>& vb
 // ------------------------------------------------------------------ Optimizer
 int Optimizer::mnDevice = 0;
 void (*Optimizer::mpfnGatheredHook)(const LocalBAProblem&, const std::vector<KeyFrame*>&) = nullptr;
+
+int Optimizer::PoseOptimization(Frame* pFrame) {
+  // src/Optimizer.cc:287-528: one edge per feature with a MapPoint, in feature order (:318-410);
+  // mvbOutlier of those features reset to false; below 3 correspondences the pose is left as is
+  const int N = pFrame->N;
+  std::vector<float> obs, Xw, isig;
+  std::vector<int> idx;
+  for (int i = 0; i < N; i++) {
+    MapPoint* pMP = pFrame->mvpMapPoints[i];
+    if (!pMP) continue;
+    pFrame->mvbOutlier[i] = false;
+    const cv::KeyPoint& kpUn = pFrame->mvKeysUn[i];
+    obs.push_back(kpUn.pt.x);
+    obs.push_back(kpUn.pt.y);
+    obs.push_back(pFrame->mvuRight[i]);  // < 0: EdgeSE3ProjectXYZOnlyPose, else the stereo edge
+    const cv::Mat X = pMP->GetWorldPos();
+    for (int k = 0; k < 3; k++) Xw.push_back(X.at<float>(k, 0));
+    isig.push_back(pFrame->mvInvLevelSigma2[kpUn.octave]);
+    idx.push_back(i);
+  }
+  const int n = (int)idx.size();
+  if (n < 3) return 0;  // :424-425
+  orbx_pose_problem p;
+  std::memset(&p, 0, sizeof(p));
+  p.n = n;
+  p.obs = obs.data();
+  p.Xw = Xw.data();
+  p.inv_sigma2 = isig.data();
+  p.fx = Frame::fx;
+  p.fy = Frame::fy;
+  p.cx = Frame::cx;
+  p.cy = Frame::cy;
+  p.bf = pFrame->mbf;
+  copy_mat44(pFrame->mTcw, p.Tcw);
+  float T[16];
+  std::vector<uint8_t> outlier(n);
+  int32_t ngood = 0;
+  p.Tcw_out = T;
+  p.outlier = outlier.data();
+  p.ngood = &ngood;
+  check(orbx_pose_optimization(&p, mnDevice), "orbx_pose_optimization");
+  for (int k = 0; k < n; k++) pFrame->mvbOutlier[idx[k]] = outlier[k] != 0;
+  cv::Mat pose(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) pose.at<float>(i / 4, i % 4) = T[i];
+  pFrame->SetPose(pose);
+  return ngood;
+}
 
 void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap) {
   // src/Optimizer.cc:532-551: the local KeyFrames (pKF and its non-bad covisibles)

@@ -8,6 +8,12 @@
 //   bagraph IN OUT      Optimizer::LocalBundleAdjustment(KeyFrame*, bool*, Map*) on an object graph
 //   pnp     IN OUT      PnPsolver(Frame, matches) + SetRansacParameters + iterate(5) in
 //                       Tracking::Relocalization's candidate loop
+//   proj    IN OUT      ORBmatcher::SearchByProjection x3 (local map / last frame / KeyFrame)
+//   fuse    IN OUT      ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th) incl. Replace / AddObservation
+//   tri     IN OUT      ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, F12, pairs, bOnlyStereo)
+//   pose    IN OUT      Optimizer::PoseOptimization(Frame*)
+//   distinct IN OUT     MapPoint::ComputeDistinctiveDescriptors
+//   voc     IN OUT      ORBVocabulary::loadFromTextFile + Frame::ComputeBoW / KeyFrame::ComputeBoW
 // IN/OUT are little-endian binary files written/read by tests/test_shim.py, which compares the
 // outputs with the CPU oracle.  Exit status 0 = ok.
 #include <cassert>
@@ -22,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "ORBVocabulary.h"
 #include "ORBextractor.h"
 #include "ORBmatcher.h"
 #include "Objects.h"
@@ -588,14 +595,528 @@ static int mode_pnp(const char* in, const char* out) {
       }
     }
   }
-  bool threw = false;  // parameters are fixed once RANSAC has started
-  try {
-    cs[0]->solver->SetRansacParameters();
-  } catch (const std::logic_error&) {
-    threw = true;
-  }
-  REQUIRE(threw);
+  // as in the reference, SetRansacParameters may be called after iterate() (in place)
+  cs[0]->solver->SetRansacParameters(prob, minInl, maxIt, minSet, eps, th2);
   std::printf("pnp ok: %d iterate() calls, match %d\n", calls, (int)match);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------- §8(f) members
+// A current Frame from the payload: N, keypoints (cv::KeyPoint bytes), descriptors, mvuRight (or
+// none), the entry occupancy (0 NULL, 1 a MapPoint with no observation, 2 one with observations),
+// the static bounds / grid, scale tables, intrinsics and pose.
+struct FramePayload {
+  Frame F;
+  std::vector<std::unique_ptr<MapPoint>> occupants;  // the entry MapPoints of F.mvpMapPoints
+  std::vector<int8_t> occ;
+};
+
+static void read_frame(Reader& r, FramePayload& fp) {
+  Frame& F = fp.F;
+  const int n = r.get<int32_t>();
+  F.N = n;
+  F.mvKeysUn.resize(n);
+  if (n) REQUIRE(std::fread(F.mvKeysUn.data(), 28, n, r.f) == (size_t)n);
+  F.mvKeys = F.mvKeysUn;
+  F.mDescriptors.create(n > 0 ? n : 1, 32, CV_8U);
+  if (n) REQUIRE(std::fread(F.mDescriptors.data, 32, n, r.f) == (size_t)n);
+  if (n == 0) F.mDescriptors.release();
+  const int has_ur = r.get<int32_t>();
+  F.mvuRight = has_ur ? r.vec<float>(n) : std::vector<float>(n, -1.f);
+  fp.occ = r.vec<int8_t>(n);
+  F.mvpMapPoints.assign(n, nullptr);
+  F.mvbOutlier.assign(n, false);
+  for (int i = 0; i < n; i++) {
+    if (!fp.occ[i]) continue;
+    fp.occupants.emplace_back(new MapPoint());
+    fp.occupants.back()->nObs = fp.occ[i] == 2 ? 2 : 0;
+    F.mvpMapPoints[i] = fp.occupants.back().get();
+  }
+  const float b[6] = {r.get<float>(), r.get<float>(), r.get<float>(), r.get<float>(), r.get<float>(), r.get<float>()};
+  Frame::mnMinX = b[0];
+  Frame::mnMaxX = b[1];
+  Frame::mnMinY = b[2];
+  Frame::mnMaxY = b[3];
+  Frame::mfGridElementWidthInv = b[4];
+  Frame::mfGridElementHeightInv = b[5];
+  F.mnScaleLevels = r.get<int32_t>();
+  F.mvScaleFactors = r.vec<float>(F.mnScaleLevels);
+  F.mvInvLevelSigma2 = r.vec<float>(F.mnScaleLevels);
+  F.mvLevelSigma2.resize(F.mnScaleLevels);
+  for (int l = 0; l < F.mnScaleLevels; l++) F.mvLevelSigma2[l] = F.mvScaleFactors[l] * F.mvScaleFactors[l];
+  F.mfLogScaleFactor = r.get<float>();
+  Frame::fx = r.get<float>();
+  Frame::fy = r.get<float>();
+  Frame::cx = r.get<float>();
+  Frame::cy = r.get<float>();
+  F.mbf = r.get<float>();
+  F.mb = r.get<float>();
+  cv::Mat T(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) T.at<float>(i / 4, i % 4) = r.get<float>();
+  F.SetPose(T);
+}
+
+struct PointPayload {
+  int n = 0;
+  std::vector<uint8_t> desc, flags;
+  std::vector<float> pos, normal, dist, angle, track;
+  std::vector<int32_t> octave, level;
+};
+
+static void read_points(Reader& r, PointPayload& P) {
+  P.n = r.get<int32_t>();
+  const size_t n = P.n;
+  P.desc = r.vec<uint8_t>(32 * n);
+  P.flags = r.vec<uint8_t>(n);
+  P.pos = r.vec<float>(3 * n);
+  P.normal = r.vec<float>(3 * n);
+  P.dist = r.vec<float>(2 * n);
+  P.angle = r.vec<float>(n);
+  P.octave = r.vec<int32_t>(n);
+  P.track = r.vec<float>(4 * n);
+  P.level = r.vec<int32_t>(n);
+}
+
+static void make_point(MapPoint& m, const PointPayload& P, int k) {
+  cv::Mat X(3, 1, CV_32F), N(3, 1, CV_32F), D(1, 32, CV_8U);
+  for (int c = 0; c < 3; c++) {
+    X.at<float>(c, 0) = P.pos[3 * k + c];
+    N.at<float>(c, 0) = P.normal[3 * k + c];
+  }
+  std::memcpy(D.data, &P.desc[32 * (size_t)k], 32);
+  m.SetWorldPos(X);
+  m.mNormalVector = N;
+  m.mDescriptor = D;
+  m.mfMinDistance = P.dist[2 * k];
+  m.mfMaxDistance = P.dist[2 * k + 1];
+  m.nObs = (P.flags[k] & 2) ? 2 : 0;
+  m.mnId = (unsigned long)(k + 1);
+}
+
+// the Frame's mvpMapPoints after the call: point index k, -1 NULL, -10 - occ for an entry occupant
+static void write_frame_state(Writer& o, const FramePayload& fp, const std::vector<MapPoint*>& pts) {
+  std::map<const MapPoint*, int> index;
+  for (size_t k = 0; k < pts.size(); k++)
+    if (pts[k]) index[pts[k]] = (int)k;
+  for (int i = 0; i < fp.F.N; i++) {
+    MapPoint* m = fp.F.mvpMapPoints[i];
+    int v = -1;
+    if (m) {
+      auto it = index.find(m);
+      if (it != index.end())
+        v = it->second;
+      else
+        v = -10 - (m->nObs > 0 ? 2 : 1);
+    }
+    o.put<int32_t>(v);
+  }
+}
+
+// SearchByProjection x3 through the reference signatures
+static int mode_proj(const char* in, const char* out) {
+  Reader r(in);
+  const int kind = r.get<int32_t>();
+  const float th = r.get<float>(), nnratio = r.get<float>();
+  const int check_ori = r.get<int32_t>(), mono = r.get<int32_t>(), orb_dist = r.get<int32_t>();
+  cv::Mat lastT(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) lastT.at<float>(i / 4, i % 4) = r.get<float>();
+  FramePayload fp;
+  read_frame(r, fp);
+  PointPayload P;
+  read_points(r, P);
+  const int n = P.n;
+  std::vector<std::unique_ptr<MapPoint>> store;
+  std::vector<MapPoint*> pts(n, nullptr);
+  ORBmatcher matcher(nnratio, check_ori != 0);
+  int nm = 0;
+  if (kind == 0) {  // Tracking::SearchLocalPoints' list: every point non-NULL, in view by bit0
+    for (int k = 0; k < n; k++) {
+      store.emplace_back(new MapPoint());
+      MapPoint& m = *store.back();
+      make_point(m, P, k);
+      m.mbTrackInView = (P.flags[k] & 1) != 0;
+      m.mTrackProjX = P.track[4 * k];
+      m.mTrackProjY = P.track[4 * k + 1];
+      m.mTrackProjXR = P.track[4 * k + 2];
+      m.mTrackViewCos = P.track[4 * k + 3];
+      m.mnTrackScaleLevel = P.level[k];
+      pts[k] = &m;
+    }
+    nm = matcher.SearchByProjection(fp.F, pts, th);
+  } else if (kind == 1) {  // LastFrame: bit0 = pMP && !mvbOutlier -- NULL or outlier otherwise
+    Frame Last;
+    Last.N = n;
+    Last.mvpMapPoints.assign(n, nullptr);
+    Last.mvbOutlier.assign(n, false);
+    Last.mvKeys.resize(n);
+    Last.mvKeysUn.resize(n);
+    for (int k = 0; k < n; k++) {
+      Last.mvKeys[k].octave = P.octave[k];
+      Last.mvKeysUn[k].octave = P.octave[k];
+      Last.mvKeysUn[k].angle = P.angle[k];
+      if (!(P.flags[k] & 1) && k % 2 == 0) continue;  // no MapPoint
+      store.emplace_back(new MapPoint());
+      make_point(*store.back(), P, k);
+      Last.mvpMapPoints[k] = pts[k] = store.back().get();
+      Last.mvbOutlier[k] = !(P.flags[k] & 1);
+    }
+    Last.SetPose(lastT);
+    nm = matcher.SearchByProjection(fp.F, Last, th, mono != 0);
+  } else {  // KeyFrame: bit0 = pMP && !isBad() && !sAlreadyFound.count(pMP)
+    KeyFrame K;
+    K.N = n;
+    K.mvKeysUn.resize(n);
+    K.mvpMapPoints.assign(n, nullptr);
+    std::set<MapPoint*> found;
+    for (int k = 0; k < n; k++) {
+      K.mvKeysUn[k].angle = P.angle[k];
+      K.mvKeysUn[k].octave = P.octave[k];
+      if (!(P.flags[k] & 1) && k % 3 == 0) continue;  // no MapPoint
+      store.emplace_back(new MapPoint());
+      MapPoint& m = *store.back();
+      make_point(m, P, k);
+      if (!(P.flags[k] & 1)) {
+        if (k % 3 == 1)
+          m.mbBad = true;
+        else
+          found.insert(&m);
+      }
+      K.mvpMapPoints[k] = pts[k] = &m;
+    }
+    nm = matcher.SearchByProjection(fp.F, &K, found, th, orb_dist);
+  }
+  Writer o(out);
+  o.put<int32_t>(nm);
+  write_frame_state(o, fp, pts);
+  std::printf("proj ok: kind %d, %d matches\n", kind, nm);
+  return 0;
+}
+
+// Fuse(KeyFrame*, const vector<MapPoint*>&, th) with its Replace / AddObservation block.  pKF is the
+// payload frame (its features' MapPoints: the entry occupants, each observed by pKF and by some of
+// `nother` extra KeyFrames); every fuse candidate is observed by some extra KeyFrames.
+static int mode_fuse(const char* in, const char* out) {
+  Reader r(in);
+  const float th = r.get<float>();
+  FramePayload fp;
+  read_frame(r, fp);
+  PointPayload P;
+  read_points(r, P);
+  const int nother = r.get<int32_t>();
+  const int nocc = (int)fp.occupants.size();
+  // observation sets: per candidate / per occupant, a bitmask over the extra KeyFrames
+  const std::vector<uint32_t> cand_obs = r.vec<uint32_t>(P.n), occ_obs = r.vec<uint32_t>(nocc);
+  const int ikf = r.get<int32_t>();  // bounds of pKF as its integer copies
+  (void)ikf;
+  Map map;
+  const Frame& F = fp.F;
+  KeyFrame K;
+  K.mnId = 1000;
+  K.N = F.N;
+  K.mvKeysUn = F.mvKeysUn;
+  K.mDescriptors = F.mDescriptors;
+  K.mvuRight = F.mvuRight;
+  K.mvpMapPoints.assign(F.N, nullptr);
+  K.mnMinX = (int)Frame::mnMinX;
+  K.mnMaxX = (int)Frame::mnMaxX;
+  K.mnMinY = (int)Frame::mnMinY;
+  K.mnMaxY = (int)Frame::mnMaxY;
+  K.mfGridElementWidthInv = Frame::mfGridElementWidthInv;
+  K.mfGridElementHeightInv = Frame::mfGridElementHeightInv;
+  K.mnScaleLevels = F.mnScaleLevels;
+  K.mvScaleFactors = F.mvScaleFactors;
+  K.mvLevelSigma2 = F.mvLevelSigma2;
+  K.mvInvLevelSigma2 = F.mvInvLevelSigma2;
+  K.mfLogScaleFactor = F.mfLogScaleFactor;
+  K.fx = Frame::fx;
+  K.fy = Frame::fy;
+  K.cx = Frame::cx;
+  K.cy = Frame::cy;
+  K.mbf = F.mbf;
+  K.mb = F.mb;
+  K.SetPose(F.mTcw);
+  // extra KeyFrames: one monocular feature slot per MapPoint that observes them, random descriptors
+  const int nmp = P.n + nocc;
+  std::vector<std::unique_ptr<KeyFrame>> others;
+  for (int j = 0; j < nother; j++) {
+    others.emplace_back(new KeyFrame());
+    KeyFrame& O = *others.back();
+    O.mnId = (unsigned long)(2000 + j);
+    O.N = nmp;
+    O.mvKeysUn.resize(nmp);
+    O.mvuRight.assign(nmp, -1.f);
+    O.mvpMapPoints.assign(nmp, nullptr);
+    O.mDescriptors.create(nmp, 32, CV_8U);
+    for (int q = 0; q < nmp; q++)
+      for (int b = 0; b < 32; b++) O.mDescriptors.at<uint8_t>(q, b) = (uint8_t)((q * 131 + j * 71 + b * 29) & 0xFF);
+  }
+  std::vector<std::unique_ptr<MapPoint>> cands;
+  std::vector<MapPoint*> pts(P.n, nullptr);
+  auto observe_others = [&](MapPoint* m, uint32_t mask, int slot) {
+    for (int j = 0; j < nother; j++)
+      if (mask >> j & 1) {
+        others[j]->mvpMapPoints[slot] = m;
+        m->AddObservation(others[j].get(), slot);
+      }
+  };
+  for (int k = 0; k < P.n; k++) {
+    cands.emplace_back(new MapPoint());
+    MapPoint& m = *cands.back();
+    make_point(m, P, k);
+    m.nObs = 0;
+    m.mpMap = &map;
+    map.mspMapPoints.insert(&m);
+    observe_others(&m, cand_obs[k], k);
+    if (!(P.flags[k] & 1)) m.mbBad = (k % 2 == 0);  // bit0 off: bad, or already in pKF (below)
+    pts[k] = &m;
+  }
+  // the entry occupants become pKF's own MapPoints (observed by pKF at their feature)
+  std::vector<MapPoint*> occs;
+  int oi = 0;
+  for (int i = 0; i < F.N; i++) {
+    MapPoint* m = F.mvpMapPoints[i];
+    if (!m) continue;
+    m->nObs = 0;
+    m->mnId = (unsigned long)(100000 + oi);
+    m->mpMap = &map;
+    map.mspMapPoints.insert(m);
+    cv::Mat D(1, 32, CV_8U);
+    std::memcpy(D.data, F.mDescriptors.ptr<uint8_t>(i), 32);
+    m->mDescriptor = D;
+    K.mvpMapPoints[i] = m;
+    m->AddObservation(&K, i);
+    observe_others(m, occ_obs[oi], P.n + oi);
+    occs.push_back(m);
+    oi++;
+  }
+  // candidates with bit0 off and odd index: already observed by pKF at a free feature of theirs
+  for (int k = 0; k < P.n; k++)
+    if (!(P.flags[k] & 1) && k % 2 == 1) {
+      for (int i = 0; i < F.N; i++)
+        if (!K.mvpMapPoints[i]) {
+          K.mvpMapPoints[i] = pts[k];
+          pts[k]->AddObservation(&K, i);
+          break;
+        }
+    }
+  ORBmatcher matcher;
+  const int nf = matcher.Fuse(&K, pts, th);
+  Writer o(out);
+  o.put<int32_t>(nf);
+  // pKF's features: candidate k, or -100 - occupant index, -1 NULL
+  for (int i = 0; i < K.N; i++) {
+    MapPoint* m = K.mvpMapPoints[i];
+    int v = -1;
+    for (int k = 0; k < P.n && v == -1; k++)
+      if (pts[k] == m) v = k;
+    for (int q = 0; q < nocc && v == -1; q++)
+      if (occs[q] == m) v = -100 - q;
+    o.put<int32_t>(m ? v : -1);
+  }
+  // every MapPoint (candidates, then occupants): bad, nObs, mDescriptor
+  auto put_mp = [&](MapPoint* m) {
+    o.put<uint8_t>(m->isBad() ? 1 : 0);
+    o.put<int32_t>(m->Observations());
+    const cv::Mat d = m->GetDescriptor();
+    o.raw(d.data, 32);
+  };
+  for (MapPoint* m : pts) put_mp(m);
+  for (MapPoint* m : occs) put_mp(m);
+  std::printf("fuse ok: %d fused\n", nf);
+  return 0;
+}
+
+// SearchForTriangulation(KeyFrame*, KeyFrame*, F12, vMatchedPairs, bOnlyStereo)
+static void read_tri_kf(Reader& r, KeyFrame& K) {
+  K.N = r.get<int32_t>();
+  const int n = K.N;
+  K.mvKeysUn.resize(n);
+  if (n) REQUIRE(std::fread(K.mvKeysUn.data(), 28, n, r.f) == (size_t)n);
+  K.mDescriptors.create(n > 0 ? n : 1, 32, CV_8U);
+  if (n) REQUIRE(std::fread(K.mDescriptors.data, 32, n, r.f) == (size_t)n);
+  const int has_ur = r.get<int32_t>();
+  K.mvuRight = has_ur ? r.vec<float>(n) : std::vector<float>(n, -1.f);
+  const std::vector<uint8_t> has_mp = r.vec<uint8_t>(n);
+  K.mvpMapPoints.assign(n, nullptr);
+  static MapPoint dummy;
+  for (int i = 0; i < n; i++)
+    if (has_mp[i]) K.mvpMapPoints[i] = &dummy;
+  const int nn = r.get<int32_t>();
+  const std::vector<uint32_t> ids = r.vec<uint32_t>(nn);
+  const std::vector<int32_t> off = r.vec<int32_t>(nn + 1);
+  const std::vector<int32_t> feat = r.vec<int32_t>(nn ? off[nn] : 0);
+  for (int j = 0; j < nn; j++)
+    for (int q = off[j]; q < off[j + 1]; q++) K.mFeatVec[ids[j]].push_back((unsigned)feat[q]);
+}
+
+static int mode_tri(const char* in, const char* out) {
+  Reader r(in);
+  const int only_stereo = r.get<int32_t>(), check_ori = r.get<int32_t>();
+  KeyFrame K1, K2;
+  read_tri_kf(r, K1);
+  read_tri_kf(r, K2);
+  cv::Mat F12(3, 3, CV_32F);
+  for (int i = 0; i < 9; i++) F12.at<float>(i / 3, i % 3) = r.get<float>();
+  // pKF1's camera centre through a pose whose Ow is exactly C1w: Tcw = [I | -C1w]
+  cv::Mat T1(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) T1.at<float>(i / 4, i % 4) = (i % 5 == 0) ? 1.f : 0.f;
+  for (int k = 0; k < 3; k++) T1.at<float>(k, 3) = -r.get<float>();
+  K1.SetPose(T1);
+  cv::Mat T2(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) T2.at<float>(i / 4, i % 4) = r.get<float>();
+  K2.SetPose(T2);
+  K2.fx = r.get<float>();
+  K2.fy = r.get<float>();
+  K2.cx = r.get<float>();
+  K2.cy = r.get<float>();
+  K2.mnScaleLevels = r.get<int32_t>();
+  K2.mvScaleFactors = r.vec<float>(K2.mnScaleLevels);
+  K2.mvLevelSigma2 = r.vec<float>(K2.mnScaleLevels);
+  ORBmatcher matcher(0.6f, check_ori != 0);
+  std::vector<std::pair<size_t, size_t>> pairs;
+  const int nm = matcher.SearchForTriangulation(&K1, &K2, F12, pairs, only_stereo != 0);
+  REQUIRE(nm == (int)pairs.size());
+  Writer o(out);
+  o.put<int32_t>(nm);
+  for (const auto& pr : pairs) {
+    o.put<int32_t>((int32_t)pr.first);
+    o.put<int32_t>((int32_t)pr.second);
+  }
+  std::printf("tri ok: %d pairs\n", nm);
+  return 0;
+}
+
+// Optimizer::PoseOptimization(Frame*): edges from the Frame's MapPoints (every third feature
+// without one), mvbOutlier and the pose written back
+static int mode_pose(const char* in, const char* out) {
+  Reader r(in);
+  const int n = r.get<int32_t>();
+  const std::vector<float> obs = r.vec<float>(3 * (size_t)n), X = r.vec<float>(3 * (size_t)n),
+                           isig = r.vec<float>(n);
+  Frame::fx = r.get<float>();
+  Frame::fy = r.get<float>();
+  Frame::cx = r.get<float>();
+  Frame::cy = r.get<float>();
+  const float bf = r.get<float>();
+  cv::Mat T(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) T.at<float>(i / 4, i % 4) = r.get<float>();
+  Frame F;
+  F.mbf = bf;
+  std::vector<std::unique_ptr<MapPoint>> mps;
+  std::vector<int> feat_of;
+  // the information of each edge comes from mvInvLevelSigma2[octave]: one level per distinct value
+  std::vector<float> levels;
+  for (int k = 0; k < n; k++) {
+    if (k % 3 == 0) {  // a feature without a MapPoint (no edge), flagged outlier before the call
+      F.mvKeysUn.push_back(cv::KeyPoint(5.f, 5.f, 31.f, -1.f, 0.f, 0));
+      F.mvuRight.push_back(-1.f);
+      F.mvpMapPoints.push_back(nullptr);
+    }
+    int lv = -1;
+    for (size_t l = 0; l < levels.size(); l++)
+      if (levels[l] == isig[k]) lv = (int)l;
+    if (lv < 0) {
+      lv = (int)levels.size();
+      levels.push_back(isig[k]);
+    }
+    mps.emplace_back(new MapPoint());
+    cv::Mat Xp(3, 1, CV_32F);
+    for (int c = 0; c < 3; c++) Xp.at<float>(c, 0) = X[3 * k + c];
+    mps.back()->SetWorldPos(Xp);
+    feat_of.push_back((int)F.mvKeysUn.size());
+    F.mvKeysUn.push_back(cv::KeyPoint(obs[3 * k], obs[3 * k + 1], 31.f, -1.f, 0.f, lv));
+    F.mvuRight.push_back(obs[3 * k + 2]);
+    F.mvpMapPoints.push_back(mps.back().get());
+  }
+  F.N = (int)F.mvKeysUn.size();
+  F.mvInvLevelSigma2 = levels;
+  F.mvbOutlier.assign(F.N, true);
+  F.SetPose(T);
+  const int ngood = Optimizer::PoseOptimization(&F);
+  Writer o(out);
+  o.put<int32_t>(ngood);
+  for (int i = 0; i < 16; i++) o.put<float>(F.mTcw.at<float>(i / 4, i % 4));
+  for (int k = 0; k < n; k++) o.put<uint8_t>(F.mvbOutlier[feat_of[k]] ? 1 : 0);
+  // features without a MapPoint keep their flag
+  for (int i = 0; i < F.N; i++)
+    if (!F.mvpMapPoints[i]) REQUIRE(F.mvbOutlier[i]);
+  std::printf("pose ok: %d good\n", ngood);
+  return 0;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors on points observed by several KeyFrames (some bad)
+static int mode_distinct(const char* in, const char* out) {
+  Reader r(in);
+  const int np = r.get<int32_t>(), nkf = r.get<int32_t>();
+  // one array: ascending addresses, so mObservations (a map keyed by KeyFrame*) iterates in j order
+  std::unique_ptr<KeyFrame[]> kfs(new KeyFrame[nkf > 0 ? nkf : 1]);
+  for (int j = 0; j < nkf; j++) {
+    KeyFrame& K = kfs[j];
+    K.mnId = (unsigned long)j;
+    K.N = np;
+    K.mvuRight.assign(np, -1.f);
+    K.mvKeysUn.resize(np);
+    K.mvpMapPoints.assign(np, nullptr);
+    K.mDescriptors.create(np > 0 ? np : 1, 32, CV_8U);
+    if (np) REQUIRE(std::fread(K.mDescriptors.data, 32, np, r.f) == (size_t)np);
+    K.mbBad = r.get<uint8_t>() != 0;
+  }
+  Writer o(out);
+  for (int p = 0; p < np; p++) {
+    MapPoint m;
+    const uint32_t mask = r.get<uint32_t>();
+    for (int j = 0; j < nkf; j++)
+      if (mask >> j & 1) m.AddObservation(&kfs[j], p);
+    m.mDescriptor = cv::Mat(1, 32, CV_8U);
+    std::memset(m.mDescriptor.data, 0xAB, 32);  // kept when nothing is observed
+    m.ComputeDistinctiveDescriptors();
+    o.raw(m.GetDescriptor().data, 32);
+  }
+  std::printf("distinct ok\n");
+  return 0;
+}
+
+// ORBVocabulary::loadFromTextFile + Frame::ComputeBoW / KeyFrame::ComputeBoW
+static int mode_voc(const char* in, const char* out) {
+  Reader r(in);
+  const int len = r.get<int32_t>();
+  const std::vector<char> text = r.vec<char>(len);
+  const std::string path = std::string(out) + ".voc.txt";
+  {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    REQUIRE(f);
+    REQUIRE(std::fwrite(text.data(), 1, text.size(), f) == text.size());
+    std::fclose(f);
+  }
+  ORBVocabulary voc;
+  REQUIRE(!voc.loadFromTextFile(path + ".missing"));
+  REQUIRE(voc.loadFromTextFile(path));
+  const int n = r.get<int32_t>();
+  Frame F;
+  F.mpORBvocabulary = &voc;
+  F.N = n;
+  F.mDescriptors.create(n > 0 ? n : 1, 32, CV_8U);
+  if (n) REQUIRE(std::fread(F.mDescriptors.data, 32, n, r.f) == (size_t)n);
+  F.ComputeBoW();
+  KeyFrame K;
+  K.mpORBvocabulary = &voc;
+  K.mDescriptors = F.mDescriptors;
+  K.ComputeBoW();
+  REQUIRE(K.mBowVec.size() == F.mBowVec.size() && K.mFeatVec.size() == F.mFeatVec.size());
+  Writer o(out);
+  o.put<int32_t>((int32_t)F.mBowVec.size());
+  for (const auto& w : F.mBowVec) {
+    o.put<uint32_t>(w.first);
+    o.put<double>(w.second);
+  }
+  o.put<int32_t>((int32_t)F.mFeatVec.size());
+  for (const auto& node : F.mFeatVec) {
+    o.put<uint32_t>(node.first);
+    o.put<int32_t>((int32_t)node.second.size());
+    for (unsigned int f : node.second) o.put<int32_t>((int32_t)f);
+  }
+  std::remove(path.c_str());
+  std::printf("voc ok: %zu words\n", F.mBowVec.size());
   return 0;
 }
 
@@ -613,6 +1134,12 @@ int main(int argc, char** argv) {
     if (m == "ba") return mode_ba(argv[2], argv[3]);
     if (m == "bagraph") return mode_bagraph(argv[2], argv[3]);
     if (m == "pnp") return mode_pnp(argv[2], argv[3]);
+    if (m == "proj") return mode_proj(argv[2], argv[3]);
+    if (m == "fuse") return mode_fuse(argv[2], argv[3]);
+    if (m == "tri") return mode_tri(argv[2], argv[3]);
+    if (m == "pose") return mode_pose(argv[2], argv[3]);
+    if (m == "distinct") return mode_distinct(argv[2], argv[3]);
+    if (m == "voc") return mode_voc(argv[2], argv[3]);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 3;

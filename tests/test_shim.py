@@ -61,7 +61,28 @@ def test_shim_exports_reference_classes(exe):
                 "std::allocator<ORB_SLAM2::MapPoint*> > const&)",
                 "ORB_SLAM2::PnPsolver::SetRansacParameters(double, int, int, int, float, float)",
                 "ORB_SLAM2::PnPsolver::iterate(int, bool&, std::vector<bool, std::allocator<bool> >&, int&)",
-                "ORB_SLAM2::PnPsolver::find(std::vector<bool, std::allocator<bool> >&, int&)"]:
+                "ORB_SLAM2::PnPsolver::find(std::vector<bool, std::allocator<bool> >&, int&)",
+                "ORB_SLAM2::ORBmatcher::SearchByProjection(ORB_SLAM2::Frame&, std::vector<ORB_SLAM2::MapPoint*, "
+                "std::allocator<ORB_SLAM2::MapPoint*> > const&, float)",
+                "ORB_SLAM2::ORBmatcher::SearchByProjection(ORB_SLAM2::Frame&, ORB_SLAM2::Frame const&, float, bool)",
+                "ORB_SLAM2::ORBmatcher::SearchByProjection(ORB_SLAM2::Frame&, ORB_SLAM2::KeyFrame*, "
+                "std::set<ORB_SLAM2::MapPoint*, std::less<ORB_SLAM2::MapPoint*>, "
+                "std::allocator<ORB_SLAM2::MapPoint*> > const&, float, int)",
+                "ORB_SLAM2::ORBmatcher::SearchForTriangulation(ORB_SLAM2::KeyFrame*, ORB_SLAM2::KeyFrame*, cv::Mat, "
+                "std::vector<std::pair<unsigned long, unsigned long>, std::allocator<std::pair<unsigned long, "
+                "unsigned long> > >&, bool)",
+                "ORB_SLAM2::ORBmatcher::Fuse(ORB_SLAM2::KeyFrame*, std::vector<ORB_SLAM2::MapPoint*, "
+                "std::allocator<ORB_SLAM2::MapPoint*> > const&, float)",
+                "ORB_SLAM2::Optimizer::PoseOptimization(ORB_SLAM2::Frame*)",
+                "ORB_SLAM2::MapPoint::ComputeDistinctiveDescriptors()",
+                "ORB_SLAM2::Frame::ComputeBoW()",
+                "ORB_SLAM2::KeyFrame::ComputeBoW()",
+                "ORB_SLAM2::Frame::Frame(cv::Mat const&, cv::Mat const&, double const&, ORB_SLAM2::ORBextractor*, "
+                "ORB_SLAM2::ORBextractor*, ORB_SLAM2::ORBVocabulary*, cv::Mat&, cv::Mat&, float const&, float const&)",
+                "ORB_SLAM2::ORBVocabulary::loadFromTextFile(std::__cxx11::basic_string<char, std::char_traits<char>, "
+                "std::allocator<char> > const&)",
+                "ORB_SLAM2::ORBVocabulary::transform(std::vector<cv::Mat, std::allocator<cv::Mat> > const&, "
+                "DBoW2::BowVector&, DBoW2::FeatureVector&, int) const"]:
         assert sym in out, sym
 
 
@@ -328,3 +349,314 @@ def test_shim_pnpsolver_relocalization_loop(gpu, exe, tmp_path, name):
     assert o == len(out) and calls > 0
     for s in sol:
         del s
+
+
+# ------------------------------------------------------------------ §8(f) members through the shim
+def _frame_bytes(fr):
+    """A projection_frame dict in the layout test_shim.cpp's read_frame expects."""
+    from orb_slam2_commit_amd._lib import KEYPOINT_DTYPE
+    keys = np.ascontiguousarray(fr["keys_un"], KEYPOINT_DTYPE)
+    n = len(keys)
+    ur = fr.get("u_right")
+    occ = fr.get("occ")
+    occ = np.zeros(n, np.int8) if occ is None else np.asarray(occ, np.int8)
+    nl = int(fr["nlevels"])
+    sf = np.asarray(fr["scale_factors"], np.float32)[:nl]
+    isg = (np.asarray(fr["inv_level_sigma2"], np.float32)[:nl] if fr.get("inv_level_sigma2") is not None
+           else np.float32(1.0) / (sf * sf))
+    out = struct.pack("<i", n) + keys.tobytes() + np.ascontiguousarray(fr["desc"], np.uint8).tobytes()
+    out += struct.pack("<i", int(ur is not None))
+    if ur is not None:
+        out += np.asarray(ur, np.float32).tobytes()
+    out += occ.tobytes()
+    out += np.array([fr[k] for k in ("min_x", "max_x", "min_y", "max_y", "grid_inv_w", "grid_inv_h")],
+                    np.float32).tobytes()
+    out += struct.pack("<i", nl) + sf.tobytes() + isg.astype(np.float32).tobytes()
+    out += np.array([fr[k] for k in ("log_scale_factor", "fx", "fy", "cx", "cy", "bf", "b")], np.float32).tobytes()
+    out += np.asarray(fr["Tcw"], np.float32).reshape(16).tobytes()
+    return out
+
+
+def _points_bytes(pts):
+    n = len(pts["desc"])
+
+    def a(k, dt, shape):
+        v = pts.get(k)
+        return (np.zeros(shape, dt) if v is None else np.ascontiguousarray(v, dt).reshape(shape)).tobytes()
+    return (struct.pack("<i", n) + a("desc", np.uint8, (n, 32)) + a("flags", np.uint8, (n,)) + a("pos", np.float32, (n, 3))
+            + a("normal", np.float32, (n, 3)) + a("dist_minmax", np.float32, (n, 2)) + a("angle", np.float32, (n,))
+            + a("octave", np.int32, (n,)) + a("track", np.float32, (n, 4)) + a("track_level", np.int32, (n,)))
+
+
+def _proj_case(kind, variant):
+    seed = 900 + 10 * kind + variant
+    fr = synth.projection_frame(seed, n=1500 if variant % 2 else 2000, cell_crowd=0.3 if variant == 3 else 0.0)
+    pts = synth.projection_points(seed + 1, fr, kind, n_points=2500)
+    kw = dict(th=[3.0, 1.0, 5.0, 3.0][variant]) if kind == 0 else {}
+    if kind == 0:
+        kw["nnratio"] = 0.8
+    elif kind == 1:
+        fwd = np.array(fr["Tcw"], np.float32).copy()
+        fwd[2, 3] -= 2.0
+        bwd = np.array(fr["Tcw"], np.float32).copy()
+        bwd[2, 3] += 2.0
+        kw = [dict(th=7.0, last_Tcw=fr["Tcw"], mono=False), dict(th=14.0, last_Tcw=fwd, mono=False),
+              dict(th=7.0, last_Tcw=bwd, mono=False), dict(th=15.0, last_Tcw=fwd, mono=True, check_ori=False)][variant]
+    else:
+        kw = [dict(th=10.0, orb_dist=100), dict(th=3.0, orb_dist=64), dict(th=10.0, orb_dist=100, check_ori=False),
+              dict(th=3.0, orb_dist=50)][variant]
+    return fr, pts, kw
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_shim_search_by_projection(gpu, exe, tmp_path, kind, variant):
+    """ORBmatcher::SearchByProjection x3 with the reference signatures (include/ORBmatcher.h:64,76,95):
+    the shim gathers the MapPoints from the object graph (local map: mbTrackInView / mTrackProj*;
+    last frame: mvpMapPoints + mvbOutlier; KeyFrame: GetMapPointMatches minus bad and sAlreadyFound),
+    and the Frame's mvpMapPoints afterwards are the oracle's, feature for feature (entry occupants
+    with and without observations, rotation-check resets to NULL)."""
+    fr, pts, kw = _proj_case(kind, variant)
+    ref = oracle.search_by_projection(fr, pts, kind, **kw)
+    last = np.asarray(kw.get("last_Tcw", np.eye(4)), np.float32).reshape(16)
+    payload = (struct.pack("<iffiii", kind, kw["th"], kw.get("nnratio", 0.6), int(kw.get("check_ori", True)),
+                           int(kw.get("mono", False)), int(kw.get("orb_dist", 100)))
+               + last.tobytes() + _frame_bytes(fr) + _points_bytes(pts))
+    out = _run(exe, "proj", payload, tmp_path)
+    nm = struct.unpack_from("<i", out, 0)[0]
+    state = np.frombuffer(out, np.int32, offset=4)
+    occ = np.asarray(fr["occ"], np.int8)
+    want = np.where(occ == 0, -1, -10 - occ.astype(np.int32))
+    fo = ref["frame_out"]
+    want = np.where(fo >= 0, fo, np.where(fo == -2, -1, want))
+    assert nm == ref["nmatches"] and nm > 0
+    np.testing.assert_array_equal(state, want)
+
+
+def _fuse_expected(fr, pts, best, cand_obs, occ_obs, nother):
+    """The reference's Fuse loop (src/ORBmatcher.cc:1057-1087) with MapPoint::Replace
+    (src/MapPoint.cc:179-221) on the test graph of test_shim.cpp's mode_fuse, in Python."""
+    n_f, n_p = len(fr["desc"]), len(pts["desc"])
+    ur = np.asarray(fr["u_right"], np.float32)
+    occ_feats = np.nonzero(np.asarray(fr["occ"]) != 0)[0]
+    kf_mp = [None] * n_f
+    obs, bad = {}, {}
+
+    def cnt(e):
+        return sum((2 if ur[idx] >= 0 else 1) if kf == "K" else 1 for kf, idx in obs[e].items())
+    for k in range(n_p):
+        e = ("P", k)
+        obs[e] = {("O", j): k for j in range(nother) if cand_obs[k] >> j & 1}
+        bad[e] = not (pts["flags"][k] & 1) and k % 2 == 0
+    for q, i in enumerate(occ_feats):
+        e = ("Q", q)
+        kf_mp[i] = e
+        obs[e] = {"K": int(i)}
+        obs[e].update({("O", j): n_p + q for j in range(nother) if occ_obs[q] >> j & 1})
+        bad[e] = False
+    for k in range(n_p):
+        if not (pts["flags"][k] & 1) and k % 2 == 1:
+            i = kf_mp.index(None)
+            kf_mp[i] = ("P", k)
+            obs[("P", k)]["K"] = i
+
+    def replace(x, y):
+        o = obs[x]
+        obs[x] = {}
+        bad[x] = True
+        for kf, idx in o.items():
+            if kf in obs[y]:
+                if kf == "K":
+                    kf_mp[idx] = None
+            else:
+                if kf == "K":
+                    kf_mp[idx] = y
+                obs[y][kf] = idx
+    nf = 0
+    for k in range(n_p):
+        b = int(best[k])
+        a = ("P", k)
+        if b < 0 or bad[a] or "K" in obs[a]:
+            continue
+        m = kf_mp[b]
+        if m is not None:
+            if not bad[m]:
+                if cnt(m) > cnt(a):
+                    replace(a, m)
+                else:
+                    replace(m, a)
+        else:
+            obs[a]["K"] = b
+            kf_mp[b] = a
+        nf += 1
+    code = [-1 if e is None else (e[1] if e[0] == "P" else -100 - e[1]) for e in kf_mp]
+    ents = [("P", k) for k in range(n_p)] + [("Q", q) for q in range(len(occ_feats))]
+    return nf, np.array(code, np.int32), np.array([bad[e] for e in ents], np.uint8), np.array([cnt(e) for e in ents])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,th", [(0, 3.0), (1, 1.0), (2, 5.0)])
+def test_shim_fuse(gpu, exe, tmp_path, seed, th):
+    """ORBmatcher::Fuse(KeyFrame*, const vector<MapPoint*>&, th) (include/ORBmatcher.h:148): the
+    matching on the MI355X, then Replace / AddObservation / AddMapPoint in point order through the
+    object graph -- pKF's MapPoints, every MapPoint's bad flag and observation count afterwards equal
+    the reference loop's (restated here on the oracle's matches), and the return value nFused."""
+    fr = synth.projection_frame(700 + seed, n=1800, p_occ=(0.1, 0.15))
+    pts = synth.projection_points(701 + seed, fr, 3, n_points=1500, pool=0.3)
+    rng = np.random.default_rng(702 + seed)
+    nother = 6
+    nocc = int((np.asarray(fr["occ"]) != 0).sum())
+    cand_obs = rng.integers(0, 1 << nother, len(pts["desc"])).astype(np.uint32)
+    occ_obs = rng.integers(0, 1 << nother, nocc).astype(np.uint32)
+    # mode_fuse gives pKF its own integer bounds: the frame's are integral already (0 .. width)
+    ref = oracle.search_by_projection(fr, pts, 3, th=th)
+    payload = (struct.pack("<f", th) + _frame_bytes(fr) + _points_bytes(pts) + struct.pack("<i", nother)
+               + cand_obs.tobytes() + occ_obs.tobytes() + struct.pack("<i", 1))
+    out = _run(exe, "fuse", payload, tmp_path)
+    nf = struct.unpack_from("<i", out, 0)[0]
+    n_f = len(fr["desc"])
+    code = np.frombuffer(out, np.int32, n_f, 4)
+    o = 4 + 4 * n_f
+    nmp = len(pts["desc"]) + nocc
+    rec = np.frombuffer(out, np.dtype([("bad", "u1"), ("nobs", "<i4"), ("desc", "u1", 32)]), nmp, o)
+    assert o + rec.nbytes == len(out)
+    enf, ecode, ebad, ecnt = _fuse_expected(fr, pts, ref["point_match"], cand_obs, occ_obs, nother)
+    assert (ref["point_match"] >= 0).sum() > 50
+    assert nf == enf > 0
+    np.testing.assert_array_equal(code, ecode)
+    np.testing.assert_array_equal(rec["bad"], ebad)
+    np.testing.assert_array_equal(rec["nobs"], ecnt)
+
+
+def _tri_kf_bytes(d):
+    from orb_slam2_commit_amd._lib import KEYPOINT_DTYPE
+    n = len(d["desc"])
+    ur = d.get("u_right")
+    mp = d.get("has_mp")
+    out = struct.pack("<i", n) + np.ascontiguousarray(d["keys_un"], KEYPOINT_DTYPE).tobytes()
+    out += np.ascontiguousarray(d["desc"], np.uint8).tobytes() + struct.pack("<i", int(ur is not None))
+    if ur is not None:
+        out += np.asarray(ur, np.float32).tobytes()
+    out += (np.zeros(n, np.uint8) if mp is None else np.asarray(mp, np.uint8)).tobytes()
+    out += struct.pack("<i", len(d["node_id"])) + np.asarray(d["node_id"], np.uint32).tobytes()
+    out += np.asarray(d["node_off"], np.int32).tobytes() + np.asarray(d["feat"], np.int32).tobytes()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,only_stereo,check", [(0, False, True), (1, True, True), (2, False, False)])
+def test_shim_search_for_triangulation(gpu, exe, tmp_path, seed, only_stereo, check):
+    """ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, F12, vMatchedPairs, bOnlyStereo)
+    (include/ORBmatcher.h:134) on two KeyFrames (mvKeysUn, mDescriptors, mvuRight, GetMapPoint,
+    mFeatVec, poses): vMatchedPairs equals the oracle's, in ascending KF1 index."""
+    pr = synth.triangulation_problem(800 + seed)
+    nm_ref, m12 = oracle.search_for_triangulation(pr, only_stereo, check)
+    nl = len(pr["scale_factors2"])
+    payload = (struct.pack("<ii", int(only_stereo), int(check)) + _tri_kf_bytes(pr["kf1"]) + _tri_kf_bytes(pr["kf2"])
+               + np.asarray(pr["F12"], np.float32).reshape(9).tobytes()
+               + np.asarray(pr["C1w"], np.float32).reshape(3).tobytes()
+               + np.asarray(pr["T2w"], np.float32).reshape(16).tobytes()
+               + np.array([pr[k] for k in ("fx", "fy", "cx", "cy")], np.float32).tobytes()
+               + struct.pack("<i", nl) + np.asarray(pr["scale_factors2"], np.float32).tobytes()
+               + np.asarray(pr["level_sigma2_2"], np.float32).tobytes())
+    out = _run(exe, "tri", payload, tmp_path)
+    nm = struct.unpack_from("<i", out, 0)[0]
+    pairs = np.frombuffer(out, np.int32, offset=4).reshape(-1, 2)
+    i = np.nonzero(m12 >= 0)[0]
+    assert nm == nm_ref > 0
+    np.testing.assert_array_equal(pairs, np.stack([i, m12[i]], 1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n,of", [(0, 800, 0.1), (1, 300, 0.3), (2, 40, 0.0), (3, 2, 0.0)])
+def test_shim_pose_optimization(gpu, exe, tmp_path, seed, n, of):
+    """Optimizer::PoseOptimization(Frame*) (include/Optimizer.h:71): edges gathered from the Frame's
+    mvpMapPoints in feature order (features without a MapPoint skipped and their mvbOutlier kept),
+    the pose (SetPose) bit-exact and mvbOutlier / the return value equal to the oracle's; below 3
+    correspondences the pose is untouched and 0 returned."""
+    pr = synth.pose_problem(seed=600 + seed, n=n, outlier_frac=of)
+    payload = (struct.pack("<i", n) + np.asarray(pr["obs"], np.float32).tobytes()
+               + np.asarray(pr["Xw"], np.float32).tobytes() + np.asarray(pr["inv_sigma2"], np.float32).tobytes()
+               + np.array([pr[k] for k in ("fx", "fy", "cx", "cy", "bf")], np.float32).tobytes()
+               + np.asarray(pr["Tcw"], np.float32).reshape(16).tobytes())
+    out = _run(exe, "pose", payload, tmp_path)
+    ngood = struct.unpack_from("<i", out, 0)[0]
+    T = np.frombuffer(out, np.float32, 16, 4).reshape(4, 4)
+    outl = np.frombuffer(out, np.uint8, n, 68)
+    if n < 3:
+        assert ngood == 0
+        np.testing.assert_array_equal(T, np.asarray(pr["Tcw"], np.float32))
+        assert not outl.any()
+        return
+    ref = oracle.pose_optimization(pr)
+    assert ngood == ref["ngood"]
+    np.testing.assert_array_equal(T.view(np.uint32), ref["Tcw"].view(np.uint32))
+    np.testing.assert_array_equal(outl, ref["outlier"])
+
+
+@pytest.mark.gpu
+def test_shim_compute_distinctive_descriptors(gpu, exe, tmp_path):
+    """MapPoint::ComputeDistinctiveDescriptors (include/MapPoint.h:85): the observed descriptors of the
+    non-bad KeyFrames in observation order, the oracle's choice; a point with no usable observation
+    keeps its descriptor."""
+    rng = np.random.default_rng(11)
+    np_, nkf = 120, 20
+    base = rng.integers(0, 256, (np_, 32), dtype=np.uint8)
+    desc = np.stack([base ^ (rng.random((np_, 32)) < 0.1).astype(np.uint8) * rng.integers(0, 256, (np_, 32),
+                                                                                       dtype=np.uint8)
+                     for _ in range(nkf)])  # nkf x np x 32
+    bad = (rng.random(nkf) < 0.2).astype(np.uint8)
+    masks = rng.integers(0, 1 << nkf, np_).astype(np.uint32)
+    masks[0] = 0  # no observation
+    bad[3] = 1
+    masks[1] = 1 << 3  # observed by a bad KeyFrame only
+    payload = struct.pack("<ii", np_, nkf)
+    for j in range(nkf):
+        payload += desc[j].tobytes() + struct.pack("<B", int(bad[j]))
+    payload += masks.tobytes()
+    out = np.frombuffer(_run(exe, "distinct", payload, tmp_path), np.uint8).reshape(np_, 32)
+    rows, off = [], [0]
+    for p in range(np_):
+        for j in range(nkf):
+            if masks[p] >> j & 1 and not bad[j]:
+                rows.append(desc[j, p])
+        off.append(len(rows))
+    best, chosen = oracle.distinctive_descriptors(np.asarray(rows, np.uint8).reshape(-1, 32), np.asarray(off, np.int32))
+    for p in range(np_):
+        if best[p] < 0:
+            assert (out[p] == 0xAB).all()
+        else:
+            np.testing.assert_array_equal(out[p], chosen[p])
+    assert (best >= 0).sum() > 100
+
+
+@pytest.mark.gpu
+def test_shim_vocabulary_compute_bow(gpu, exe, tmp_path):
+    """ORBVocabulary::loadFromTextFile (false for a missing file) + Frame::ComputeBoW / KeyFrame::ComputeBoW
+    (src/Frame.cc:462-469: transform(..., 4)): BowVector words and f64 weights, FeatureVector nodes
+    and features equal to the oracle's transform."""
+    text, vd, leaf = synth.vocabulary(seed=17, k=10, L=5, p_short=0.02)
+    d = synth.voc_descriptors(33, vd, leaf, 2000)
+    raw = text.encode()
+    out = _run(exe, "voc", struct.pack("<i", len(raw)) + raw + struct.pack("<i", len(d)) + d.tobytes(), tmp_path)
+    w, v, fn, fo, ff = oracle.Vocabulary(text).transform(d, 4)
+    o = 0
+    nb = struct.unpack_from("<i", out, o)[0]
+    o += 4
+    bow = np.frombuffer(out, np.dtype([("w", "<u4"), ("v", "<f8")]), nb, o)
+    o += bow.nbytes
+    assert nb == len(w) > 0
+    np.testing.assert_array_equal(bow["w"], w)
+    np.testing.assert_array_equal(bow["v"], v)
+    nn = struct.unpack_from("<i", out, o)[0]
+    o += 4
+    assert nn == len(fn)
+    for j in range(nn):
+        node, cnt = struct.unpack_from("<Ii", out, o)
+        o += 8
+        feats = np.frombuffer(out, np.int32, cnt, o)
+        o += 4 * cnt
+        assert node == fn[j]
+        np.testing.assert_array_equal(feats, ff[fo[j]:fo[j + 1]])
+    assert o == len(out)
