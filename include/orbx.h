@@ -520,8 +520,8 @@ orbx_status orbx_pose_optimization_device(const orbx_pose_problem* problems, int
  * with a MapPoint, in feature order (src/Optimizer.cc:318-410).  The reference KeyFrame's MapPoints
  * are its stereo points as StereoInitialization / CreateNewKeyFrame create them
  * (src/Tracking.cc:640-668, 1515-1555): feature k has one iff kf_depth[k] > 0, at
- * Frame::UnprojectStereo(k) (src/Frame.cc:823-839: mvKeysUn[k], mRwc*x3Dc+mOw -- one OpenCV gemm
- * with the addend, accumulated in double and rounded once, i.e. Twc*[x3Dc;1]) with pose Twc.
+ * Frame::UnprojectStereo(k) (src/Frame.cc:823-839: mvKeysUn[k], mRwc*x3Dc+mOw -- cv::gemm with the
+ * addend on OpenCV 3.2's small-matrix path: the dot product in float, then a float add) with pose Twc.
  * (KeyFrame::UnprojectStereo, src/KeyFrame.cc:758-780, reads mvKeys instead; the two agree whenever
  * mvKeysUn == mvKeys, i.e. for rectified input without distortion -- KITTI, rectified EuRoC.)  Writes obs / Xw / inv_sigma2 (and the feature of each edge) compacted, and
  * *n_edges -- the inputs of an orbx_pose_problem.  Device pointers; problems[] is a HOST array. */

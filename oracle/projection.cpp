@@ -16,10 +16,12 @@
 //
 // OpenCV arithmetic restated (parity vs the genuine library is unpinned; the
 // reference ships no fixture for any of this):
-//   * `R*X + t` on 3x1 CV_32F Mats is cv::gemm, whose 32F path accumulates in
-//     double (GEMMSingleMul<float,double>) and rounds once: x = (float)(R0*X0 +
-//     R1*X1 + R2*X2 + t) in double, left to right.
-//   * `-R.t()*t` likewise with alpha = -1: (float)(-(sum)).
+//   * `R*X + t` on 3x1 CV_32F Mats is cv::gemm(R, X, 1, t, 1) on OpenCV 3.2's small-matrix
+//     path (modules/core/src/matmul.cpp: flags == 0 and 2 <= len <= 4, len == d_size.height):
+//     `float t0 = a[0]*b[0] + a[1]*b[b_step] + a[2]*b[b_step*2]` in float, left to right,
+//     then d = (float)(t0*alpha + c*beta) in double, i.e. one correctly rounded float add.
+//   * `-R.t()*t` (GEMM_1_T: not the small path) is GEMMSingleMul<float,double>: the sum in
+//     double, then (float)(sum * -1).
 //   * cv::norm(L2) of a 3-vector: sqrt of a double sum of squares, rounded to float
 //     by the float assignment; Mat::dot likewise sums double products.
 //   * std::log(float) in PredictScale: log_det() below, a double evaluation
@@ -76,12 +78,10 @@ int predict_scale(float max_distance, float dist, float log_sf, int nlevels) {
   return n;
 }
 
-void mat3x1(const float* T, const float* X, float* out) {  // R*X + t, T row-major 4x4
+void mat3x1(const float* T, const float* X, float* out) {  // R*X + t, T row-major 4x4 (small gemm path)
   for (int r = 0; r < 3; r++) {
-    double s = (double)T[4 * r + 0] * X[0];
-    s = s + (double)T[4 * r + 1] * X[1];
-    s = s + (double)T[4 * r + 2] * X[2];
-    out[r] = (float)(s + (double)T[4 * r + 3]);
+    const float t0 = T[4 * r + 0] * X[0] + T[4 * r + 1] * X[1] + T[4 * r + 2] * X[2];
+    out[r] = (float)((double)t0 + (double)T[4 * r + 3]);
   }
 }
 

@@ -45,11 +45,9 @@ int rot_bin(float a, float b) {
 extern "C" int oracle_search_for_triangulation(const oracle_tri_problem* P) {
   const oracle_tri_kf &K1 = P->kf1, &K2 = P->kf2;
   float C2[3];
-  for (int r = 0; r < 3; r++) {
-    double s = (double)P->T2w[4 * r] * P->C1w[0];
-    s = s + (double)P->T2w[4 * r + 1] * P->C1w[1];
-    s = s + (double)P->T2w[4 * r + 2] * P->C1w[2];
-    C2[r] = (float)(s + (double)P->T2w[4 * r + 3]);
+  for (int r = 0; r < 3; r++) {  // R2w*Cw+t2w (src/ORBmatcher.cc:746-749): cv::gemm's small-matrix path
+    const float t0 = P->T2w[4 * r] * P->C1w[0] + P->T2w[4 * r + 1] * P->C1w[1] + P->T2w[4 * r + 2] * P->C1w[2];
+    C2[r] = (float)((double)t0 + (double)P->T2w[4 * r + 3]);
   }
   const float invz = 1.0f / C2[2];
   const float ex = P->fx * C2[0] * invz + P->cx;

@@ -83,14 +83,15 @@ __device__ int predict_scale(float max_distance, float dist, float log_sf, int n
   return n;
 }
 
-// cv::gemm 32F (double accumulation, one rounding): R*X + t and -R^T t
+// `R*X + t` on 3x1 CV_32F Mats: cv::gemm(R, X, 1, t, 1) takes OpenCV 3.2's small-matrix path
+// (matmul.cpp: flags == 0, 2 <= len <= 4): the dot product in float, left to right, then
+// (float)(t0*alpha + c*beta) in double -- a correctly rounded float add of t.  (-R^T t, with
+// GEMM_1_T set, is the general GEMMSingleMul<float,double> path: double accumulation, below.)
 __device__ __forceinline__ void mat3x1(const float* T, const float* X, float* out) {
 #pragma unroll
   for (int r = 0; r < 3; r++) {
-    double s = (double)T[4 * r + 0] * X[0];
-    s = s + (double)T[4 * r + 1] * X[1];
-    s = s + (double)T[4 * r + 2] * X[2];
-    out[r] = (float)(s + (double)T[4 * r + 3]);
+    const float t0 = T[4 * r + 0] * X[0] + T[4 * r + 1] * X[1] + T[4 * r + 2] * X[2];
+    out[r] = (float)((double)t0 + (double)T[4 * r + 3]);
   }
 }
 __device__ __forceinline__ void camera_centre(const float* T, float* Ow) {

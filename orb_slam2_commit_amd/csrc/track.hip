@@ -11,8 +11,8 @@
 // are its stereo points -- the map StereoInitialization / CreateNewKeyFrame build
 // (src/Tracking.cc:640-668, 1515-1555): feature k has a MapPoint iff mvDepth[k] > 0, at
 // Frame::UnprojectStereo(k) (src/Frame.cc:823-839: x3Dc = ((u-cx)*z*invfx, (v-cy)*z*invfy, z) from
-// mvKeysUn, then mRwc*x3Dc+mOw -- one OpenCV 3.2 float gemm with the addend, accumulated in double and
-// rounded once, which is Twc * [x3Dc; 1] term for term).
+// mvKeysUn, then mRwc*x3Dc+mOw -- cv::gemm with the addend on OpenCV 3.2's small-matrix path:
+// the 3-term dot product in float, then one correctly rounded float add of mOw).
 // One block per frame; the compaction is an ordered block scan, so edges keep feature order.
 #include <hip/hip_runtime.h>
 
@@ -54,12 +54,9 @@ __global__ __launch_bounds__(TBS) void k_track_gather(const orbx_track_gather* _
       const float y = (kf.y - P.cy) * z * invfy;
       float X[3];
 #pragma unroll
-      for (int r = 0; r < 3; r++) {  // cv::gemm (CV_32F, double accumulation) then + Ow
-        double s = 0.0;
-        s += (double)P.Twc[4 * r] * (double)x;
-        s += (double)P.Twc[4 * r + 1] * (double)y;
-        s += (double)P.Twc[4 * r + 2] * (double)z;
-        X[r] = (float)s + P.Twc[4 * r + 3];
+      for (int r = 0; r < 3; r++) {  // mRwc*x3Dc+mOw: cv::gemm's small-matrix path (float dot, then + Ow)
+        const float t0 = P.Twc[4 * r] * x + P.Twc[4 * r + 1] * y + P.Twc[4 * r + 2] * z;
+        X[r] = (float)((double)t0 + (double)P.Twc[4 * r + 3]);
       }
       const orbx_keypoint f = P.f_kps[i];
       P.obs[3 * o] = f.x;

@@ -51,11 +51,9 @@ __global__ __launch_bounds__(TBS) void k_search_for_triangulation(const orbx_tri
   // epipole of KF1 in KF2 (src/ORBmatcher.cc:748-756)
   float C2[3];
 #pragma unroll
-  for (int r = 0; r < 3; r++) {
-    double s = (double)P.T2w[4 * r] * P.C1w[0];
-    s = s + (double)P.T2w[4 * r + 1] * P.C1w[1];
-    s = s + (double)P.T2w[4 * r + 2] * P.C1w[2];
-    C2[r] = (float)(s + (double)P.T2w[4 * r + 3]);
+  for (int r = 0; r < 3; r++) {  // R2w*Cw+t2w: cv::gemm's small-matrix path (float dot, then + t)
+    const float t0 = P.T2w[4 * r] * P.C1w[0] + P.T2w[4 * r + 1] * P.C1w[1] + P.T2w[4 * r + 2] * P.C1w[2];
+    C2[r] = (float)((double)t0 + (double)P.T2w[4 * r + 3]);
   }
   const float invz = 1.0f / C2[2];
   const float ex = P.fx * C2[0] * invz + P.cx;

@@ -27,12 +27,13 @@ f32 = np.float32
 
 # ------------------------------------------------------------------ literal Python restatement
 def _mat3x1(T, X):
+    """R*X + t: OpenCV 3.2 cv::gemm small-matrix path -- float dot product left to right, then a
+    correctly rounded float add of t."""
     out = []
     for r in range(3):
-        s = float(T[r, 0]) * float(X[0])
-        s = s + float(T[r, 1]) * float(X[1])
-        s = s + float(T[r, 2]) * float(X[2])
-        out.append(f32(s + float(T[r, 3])))
+        t0 = f32(f32(f32(T[r, 0]) * f32(X[0])) + f32(f32(T[r, 1]) * f32(X[1])))
+        t0 = f32(t0 + f32(f32(T[r, 2]) * f32(X[2])))
+        out.append(f32(float(t0) + float(T[r, 3])))
     return out
 
 

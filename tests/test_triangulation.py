@@ -30,8 +30,8 @@ def _ham(a, b):
 def py_triangulation(pr, only_stereo=False, check_ori=True):
     k1, k2 = pr["kf1"], pr["kf2"]
     T, C = pr["T2w"], pr["C1w"]
-    C2 = [f32(((float(T[r, 0]) * float(C[0]) + float(T[r, 1]) * float(C[1])) + float(T[r, 2]) * float(C[2]))
-              + float(T[r, 3])) for r in range(3)]
+    C2 = [f32(float(f32(f32(f32(T[r, 0]) * f32(C[0])) + f32(f32(T[r, 1]) * f32(C[1])))
+                    + f32(f32(T[r, 2]) * f32(C[2]))) + float(T[r, 3])) for r in range(3)]
     invz = f32(f32(1.0) / C2[2])
     ex = f32(f32(f32(pr["fx"] * C2[0]) * invz) + pr["cx"])
     ey = f32(f32(f32(pr["fy"] * C2[1]) * invz) + pr["cy"])
