@@ -85,6 +85,16 @@ void mat3x1(const float* T, const float* X, float* out) {  // R*X + t, T row-maj
   }
 }
 
+// KeyFrame::GetCameraCenter (src/KeyFrame.cc:84-87): Ow = -Rwc*tcw with Rwc a materialised Mat, so
+// cv::gemm(Rwc, tcw, -1) takes the small-matrix path: the dot product in float, then negated
+void camera_centre_kf(const float* T, float* Ow) {
+  for (int c = 0; c < 3; c++) {
+    const float t0 = T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11];
+    Ow[c] = (float)((double)t0 * -1.0);
+  }
+}
+
+// Frame's mOw = -mRcw.t()*mtcw (src/Frame.cc:294-304): GEMM_1_T, the general path (double sum)
 void camera_centre(const float* T, float* Ow) {  // -R^T t
   for (int c = 0; c < 3; c++) {
     double s = (double)T[c] * T[3];
@@ -426,7 +436,7 @@ int fuse(const oracle_proj_problem& P) {
   Frame fr(F);
   Occupancy occ(F);
   float Ow[3];
-  camera_centre(F.Tcw, Ow);
+  camera_centre_kf(F.Tcw, Ow);  // pKF->GetCameraCenter() (:928)
   int nFused = 0;
   for (int i = 0; i < P.n_points; i++) {
     P.point_match[i] = -1;

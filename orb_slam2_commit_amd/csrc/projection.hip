@@ -94,6 +94,15 @@ __device__ __forceinline__ void mat3x1(const float* T, const float* X, float* ou
     out[r] = (float)((double)t0 + (double)T[4 * r + 3]);
   }
 }
+// KeyFrame::GetCameraCenter (Fuse): Ow = -Rwc*tcw with Rwc a Mat -- cv::gemm's small-matrix path
+__device__ __forceinline__ void camera_centre_kf(const float* T, float* Ow) {
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const float t0 = T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11];
+    Ow[c] = (float)((double)t0 * -1.0);
+  }
+}
+// Frame's mOw = -mRcw.t()*mtcw: GEMM_1_T, the general GEMMSingleMul<float,double> path
 __device__ __forceinline__ void camera_centre(const float* T, float* Ow) {
 #pragma unroll
   for (int c = 0; c < 3; c++) {
@@ -290,7 +299,10 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   __syncthreads();
 
   float Ow[3];
-  camera_centre(F.Tcw, Ow);
+  if (P.kind == ORBX_PROJ_FUSE)
+    camera_centre_kf(F.Tcw, Ow);  // pKF->GetCameraCenter() (src/ORBmatcher.cc:928)
+  else
+    camera_centre(F.Tcw, Ow);
   bool fwd = false, bwd = false;
   if (P.kind == ORBX_PROJ_LAST_FRAME) {
     float tlc[3];

@@ -42,6 +42,16 @@ def _centre(T):
             for c in range(3)]
 
 
+def _centre_kf(T):
+    """KeyFrame::GetCameraCenter: Ow = -Rwc*tcw with Rwc a Mat (src/KeyFrame.cc:84-87): cv::gemm's
+    small-matrix path, the dot product in float, alpha = -1."""
+    out = []
+    for c in range(3):
+        t0 = f32(f32(f32(T[0, c]) * f32(T[0, 3])) + f32(f32(T[1, c]) * f32(T[1, 3])))
+        out.append(-f32(t0 + f32(f32(T[2, c]) * f32(T[2, 3]))))
+    return out
+
+
 def _norm3(v):
     s = float(v[0]) * float(v[0])
     s = s + float(v[1]) * float(v[1])
@@ -138,7 +148,7 @@ def py_search(fr, pts, kind, th, nnratio=0.6, check_ori=True, mono=False, orb_di
     obs = [bool(occ is not None and occ[i] == 2) for i in range(n)]
     ur = fr.get("u_right")
     T = np.asarray(fr["Tcw"], np.float32)
-    Ow = _centre(T)
+    Ow = _centre_kf(T) if kind == 3 else _centre(T)  # Fuse: pKF->GetCameraCenter(); else Frame's -Rcw.t()*tcw
     npnt = len(pts["desc"])
     pm = [-1] * npnt
     hist = [[] for _ in range(30)]
