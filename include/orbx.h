@@ -173,6 +173,13 @@ typedef struct {
   int mode;
   int32_t* match;
   int32_t* nmatches;
+  /* optional (NULL: use the side's fields): feature and FeatureVector node counts as an earlier
+   * kernel of the stream left them (e.g. orbx_voc_transform_device's n_fv and the extraction's
+   * counts); the side's n / n_nodes are then the capacities and the counts are min'd with them */
+  const int32_t* a_n_dev;
+  const int32_t* a_nodes_dev;
+  const int32_t* b_n_dev;
+  const int32_t* b_nodes_dev;
 } orbx_bow_problem;
 orbx_status orbx_search_by_bow_device(const orbx_bow_problem* problems, int n, void* stream);
 
@@ -444,6 +451,13 @@ typedef struct {
   int32_t* point_match;     /* n_points: feature index point k was assigned to (before the
                                rotation check), -1 none */
   int32_t* nmatches;        /* the reference's return value */
+  /* Device batches only (orbx_search_by_projection_device; NULL/0 otherwise): sizes and pose that
+   * an earlier kernel of the same stream produced, so no host round trip sizes the problem. */
+  const int32_t* f_n_dev;   /* N = min(*f_n_dev, f.n): f.n is then the capacity */
+  const int32_t* n_points_dev; /* n_points = min(*n_points_dev, n_points) */
+  const float* Tcw_dev;     /* 16 floats replacing f.Tcw */
+  const int32_t* gate;      /* run only if *gate < gate_below (else every output is left as is): */
+  int gate_below;           /* Tracking's "if(nmatches<20) search again with 2*th" (src/Tracking.cc:1071-1076) */
 } orbx_proj_problem;
 
 /* One problem; every pointer in *p is a HOST pointer (outputs are written back). */
@@ -507,6 +521,10 @@ typedef struct {
   uint8_t* outlier;         /* n: mvbOutlier of each edge's feature on return */
   int32_t* ngood;           /* the return value nInitialCorrespondences - nBad */
   int32_t* iterations;      /* optional [4]: LM iterations run by each round's optimize(10) */
+  /* Device batches only (NULL otherwise): the edge count and the starting pose as an earlier kernel
+   * of the stream left them -- n is then the capacity and n = min(*n_dev, n) */
+  const int32_t* n_dev;
+  const float* Tcw_dev;     /* 16 floats replacing Tcw */
 } orbx_pose_problem;
 
 /* One problem, HOST pointers. */
@@ -542,6 +560,79 @@ typedef struct {
   int32_t* n_edges;                /* out: 1 */
 } orbx_track_gather;
 orbx_status orbx_track_gather_device(const orbx_track_gather* problems, int n, void* stream);
+
+/* The MapPoints a stereo frame creates (StereoInitialization / CreateNewKeyFrame, src/Tracking.cc:640-668,
+ * 1515-1555: one per feature with mvDepth > 0) as the SoA a SearchByProjection problem takes, for the
+ * frame's features 0..N-1 (point i = feature i, the frame's descriptors are the points' descriptors):
+ *   pos      Frame::UnprojectStereo(i) (src/Frame.cc:823-839) with pose Twc
+ *   normal, dist_minmax  MapPoint::UpdateNormalAndDepth with the one observation (src/MapPoint.cc
+ *            UpdateNormalAndDepth): PC = pos - Ow, normal = PC / cv::norm(PC), mfMaxDistance =
+ *            |PC| * mvScaleFactors[octave], mfMinDistance = mfMaxDistance / mvScaleFactors[nlevels-1]
+ *   angle, octave  mvKeysUn[i].angle / .octave (LastFrame.mvKeysUn / mvKeys in SearchByProjection)
+ *   flags    bit0 = mvDepth[i] > 0 (a MapPoint, not an outlier), bit1 = 1 (observed by its KeyFrame)
+ * Device pointers, capacity cap per frame; problems[] is a HOST array. */
+typedef struct {
+  const orbx_keypoint* kps;   /* mvKeysUn */
+  const float* depth;         /* mvDepth */
+  const int32_t* count;       /* N (device) */
+  int cap;
+  float Twc[12];              /* row-major 3x4: Rwc | Ow */
+  float fx, fy, cx, cy;
+  int nlevels;
+  float scale_factors[16];
+  float* pos;                 /* cap x 3 */
+  float* normal;              /* cap x 3 */
+  float* dist_minmax;         /* cap x 2 */
+  float* angle;               /* cap */
+  int32_t* octave;            /* cap */
+  uint8_t* flags;             /* cap */
+} orbx_frame_points;
+orbx_status orbx_frame_points_device(const orbx_frame_points* problems, int n, void* stream);
+
+/* Tracking::TrackWithMotionModel + TrackLocalMap bookkeeping between the device launches
+ * (src/Tracking.cc:1049-1170, 1403-1468), one block per tracked frame, on the frame's MapPoint
+ * table fmap[i] (point index held by feature i, -1 = NULL):
+ *   ORBX_TRACK_AFTER_MOTION  fmap = SearchByProjection(F, LastFrame)'s frame_out; lost = nmatches <
+ *                            min_matches (:1078-1079); every point now held is marked seen
+ *                            (mnLastFrameSeen = current); PoseOptimization edges from fmap
+ *   ORBX_TRACK_AFTER_POSE    the edges PoseOptimization flagged outliers leave fmap (:1093-1107);
+ *                            lost |= ngood < min_good (nmatchesMap >= 10, :1135); then the inputs of
+ *                            SearchLocalPoints: occ (mvpMapPoints, Observations() > 0) and the local
+ *                            points' flags (bit0 = a MapPoint not seen in this frame, :1408-1430)
+ *   ORBX_TRACK_AFTER_LOCAL   fmap += SearchByProjection(F, local points)'s frame_out; edges again
+ * Edges (obs / Xw / inv_sigma2 / edge_feature / n_edges: orbx_pose_problem inputs) are in feature
+ * order; a lost frame gets n_edges = 0.  Device pointers; problems[] is a HOST array. */
+#define ORBX_TRACK_AFTER_MOTION 0
+#define ORBX_TRACK_AFTER_POSE 1
+#define ORBX_TRACK_AFTER_LOCAL 2
+typedef struct {
+  int op;
+  int cap;                        /* feature capacity of the frame and of the point table */
+  const int32_t* count;           /* current frame N */
+  const orbx_keypoint* kps;       /* current frame mvKeysUn */
+  const float* u_right;           /* current frame mvuRight (NULL: monocular) */
+  const float* inv_level_sigma2;  /* mvInvLevelSigma2 (device, per octave) */
+  const int32_t* n_points;        /* points in the table (device) */
+  const float* pos;               /* the points' world positions (cap x 3) */
+  const uint8_t* flags;           /* the points' flags as orbx_frame_points wrote them */
+  const int32_t* frame_out;       /* AFTER_MOTION / AFTER_LOCAL: the search's frame_out */
+  const int32_t* nmatches;        /* AFTER_MOTION: the search's return value */
+  int min_matches;                /* AFTER_MOTION: 20 */
+  const uint8_t* outlier;         /* AFTER_POSE: PoseOptimization's per-edge outlier flags */
+  const int32_t* ngood;           /* AFTER_POSE: PoseOptimization's return value */
+  int min_good;                   /* AFTER_POSE: 10 */
+  int32_t* fmap;                  /* cap */
+  uint8_t* seen;                  /* cap (points) */
+  uint8_t* local_flags;           /* cap (points): AFTER_POSE output */
+  int8_t* occ;                    /* cap (features): AFTER_POSE output */
+  int32_t* lost;                  /* 1 */
+  float* obs;                     /* cap x 3 */
+  float* Xw;                      /* cap x 3 */
+  float* inv_sigma2;              /* cap */
+  int32_t* edge_feature;          /* cap */
+  int32_t* n_edges;               /* 1 */
+} orbx_track_step;
+orbx_status orbx_track_step_device(const orbx_track_step* problems, int n, void* stream);
 
 /* MapPoint::ComputeDistinctiveDescriptors() -- src/MapPoint.cc:249-320, include/MapPoint.h:83,
  * for a batch of MapPoints.  Point p's observed descriptors (pKF->mDescriptors.row(idx) for
@@ -583,6 +674,9 @@ int orbx_profile_read(orbx_extractor* h, int stage, double* total_ms, long long*
 /* Library/device info: returns the number of visible HIP devices (<=0: none). */
 int orbx_device_count(void);
 const char* orbx_version(void);
+/* sizeof of a struct of this header by name ("orbx_proj_problem", ...), -1 if unknown: bindings
+ * (ctypes, cgo, JNA) check their layouts against it. */
+long long orbx_sizeof(const char* type);
 
 #ifdef __cplusplus
 }

@@ -47,7 +47,8 @@ class BowSide(C.Structure):
 
 class BowProblem(C.Structure):
     _fields_ = [("a", BowSide), ("b", BowSide), ("nnratio", C.c_float), ("check_ori", C.c_int), ("mode", C.c_int),
-                ("match", C.c_void_p), ("nmatches", C.c_void_p)]
+                ("match", C.c_void_p), ("nmatches", C.c_void_p), ("a_n_dev", C.c_void_p), ("a_nodes_dev", C.c_void_p),
+                ("b_n_dev", C.c_void_p), ("b_nodes_dev", C.c_void_p)]
 
 
 class BaProblem(C.Structure):
@@ -89,14 +90,15 @@ class ProjProblem(C.Structure):
                 ("track_level", C.c_void_p), ("th", C.c_float), ("nnratio", C.c_float),
                 ("view_cos_limit", C.c_float), ("check_ori", C.c_int), ("mono", C.c_int), ("orb_dist", C.c_int),
                 ("last_Tcw", C.c_float * 16), ("frame_out", C.c_void_p), ("point_match", C.c_void_p),
-                ("nmatches", C.c_void_p)]
+                ("nmatches", C.c_void_p), ("f_n_dev", C.c_void_p), ("n_points_dev", C.c_void_p),
+                ("Tcw_dev", C.c_void_p), ("gate", C.c_void_p), ("gate_below", C.c_int)]
 
 
 class PoseProblem(C.Structure):
     _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p),
                 ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
                 ("Tcw", C.c_float * 16), ("Tcw_out", C.c_void_p), ("outlier", C.c_void_p), ("ngood", C.c_void_p),
-                ("iterations", C.c_void_p)]
+                ("iterations", C.c_void_p), ("n_dev", C.c_void_p), ("Tcw_dev", C.c_void_p)]
 
 
 class TriKF(C.Structure):
@@ -110,6 +112,23 @@ class TriProblem(C.Structure):
                 ("T2w", C.c_float * 16), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
                 ("scale_factors2", C.c_float * 16), ("level_sigma2_2", C.c_float * 16), ("only_stereo", C.c_int),
                 ("check_ori", C.c_int), ("match12", C.c_void_p), ("nmatches", C.c_void_p)]
+
+
+class FramePoints(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("depth", C.c_void_p), ("count", C.c_void_p), ("cap", C.c_int),
+                ("Twc", C.c_float * 12), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("nlevels", C.c_int), ("scale_factors", C.c_float * 16), ("pos", C.c_void_p), ("normal", C.c_void_p),
+                ("dist_minmax", C.c_void_p), ("angle", C.c_void_p), ("octave", C.c_void_p), ("flags", C.c_void_p)]
+
+
+class TrackStep(C.Structure):
+    _fields_ = [("op", C.c_int), ("cap", C.c_int), ("count", C.c_void_p), ("kps", C.c_void_p), ("u_right", C.c_void_p),
+                ("inv_level_sigma2", C.c_void_p), ("n_points", C.c_void_p), ("pos", C.c_void_p),
+                ("flags", C.c_void_p), ("frame_out", C.c_void_p), ("nmatches", C.c_void_p), ("min_matches", C.c_int),
+                ("outlier", C.c_void_p), ("ngood", C.c_void_p), ("min_good", C.c_int), ("fmap", C.c_void_p),
+                ("seen", C.c_void_p), ("local_flags", C.c_void_p), ("occ", C.c_void_p), ("lost", C.c_void_p),
+                ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p), ("edge_feature", C.c_void_p),
+                ("n_edges", C.c_void_p)]
 
 
 class TrackGather(C.Structure):
@@ -170,6 +189,8 @@ SIGNATURES = {
     "orbx_voc_transform_device": ([P, P, C.c_int, C.c_longlong, P, C.c_int, C.c_int, C.c_int, P, P, P, P, P, P, P, P],
                                   C.c_int),
     "orbx_track_gather_device": ([C.POINTER(TrackGather), C.c_int, P], C.c_int),
+    "orbx_frame_points_device": ([C.POINTER(FramePoints), C.c_int, P], C.c_int),
+    "orbx_track_step_device": ([C.POINTER(TrackStep), C.c_int, P], C.c_int),
     "orbx_search_by_projection": ([C.POINTER(ProjProblem), C.c_int], C.c_int),
     "orbx_search_by_projection_device": ([C.POINTER(ProjProblem), C.c_int, P], C.c_int),
     "orbx_pose_optimization": ([C.POINTER(PoseProblem), C.c_int], C.c_int),
@@ -193,6 +214,7 @@ SIGNATURES = {
     "orbx_local_ba": ([C.POINTER(BaProblem), C.POINTER(BaResult), P, C.c_int], C.c_int),
     "orbx_device_count": ([], C.c_int),
     "orbx_version": ([], C.c_char_p),
+    "orbx_sizeof": ([C.c_char_p], C.c_longlong),
     "orbx_profile_enable": ([P, C.c_int], C.c_int),
     "orbx_profile_reset": ([P], C.c_int),
     "orbx_profile_read": ([P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_longlong),

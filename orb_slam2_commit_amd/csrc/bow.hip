@@ -34,7 +34,12 @@ __global__ __launch_bounds__(BBS) void k_search_by_bow(const BowProblem* __restr
   __shared__ uint32_t bmatched[kMaxBowFeatures / 32];  // second-side features matched so far
   __shared__ int hist[32];
   __shared__ int sel[4];
-  const BowProblem P = probs[blockIdx.x];
+  BowProblem P = probs[blockIdx.x];
+  // device-sized sides: the counts an earlier kernel of the stream wrote, capped by the capacities
+  if (P.a_n_dev) P.a.n = min(max(*P.a_n_dev, 0), P.a.n);
+  if (P.a_nodes_dev) P.a.n_nodes = min(max(*P.a_nodes_dev, 0), P.a.n_nodes);
+  if (P.b_n_dev) P.b.n = min(max(*P.b_n_dev, 0), P.b.n);
+  if (P.b_nodes_dev) P.b.n_nodes = min(max(*P.b_nodes_dev, 0), P.b.n_nodes);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool kfkf = P.mode == 1;
   const int nout = kfkf ? P.a.n : P.b.n;

@@ -15,6 +15,7 @@
 #include <memory>
 #include <new>
 #include <utility>
+#include <string>
 #include <vector>
 
 #include "../../include/orbx.h"
@@ -530,6 +531,22 @@ extern "C" {
 
 const char* orbx_version(void) { return "orbx 0.1.0 (gfx950)"; }
 
+long long orbx_sizeof(const char* type) {
+  if (!type) return -1;
+  const std::string t(type);
+#define ORBX_SIZEOF(T) \
+  if (t == #T) return (long long)sizeof(T);
+  ORBX_SIZEOF(orbx_keypoint) ORBX_SIZEOF(orbx_extractor_params) ORBX_SIZEOF(orbx_bow_side)
+  ORBX_SIZEOF(orbx_bow_problem) ORBX_SIZEOF(orbx_ba_problem) ORBX_SIZEOF(orbx_ba_result)
+  ORBX_SIZEOF(orbx_pnp_problem) ORBX_SIZEOF(orbx_pnp_params) ORBX_SIZEOF(orbx_pnp_result)
+  ORBX_SIZEOF(orbx_rand_state) ORBX_SIZEOF(orbx_proj_frame) ORBX_SIZEOF(orbx_proj_problem)
+  ORBX_SIZEOF(orbx_tri_kf) ORBX_SIZEOF(orbx_tri_problem) ORBX_SIZEOF(orbx_pose_problem)
+  ORBX_SIZEOF(orbx_track_gather) ORBX_SIZEOF(orbx_frame_points) ORBX_SIZEOF(orbx_track_step)
+  ORBX_SIZEOF(orbx_camera)
+#undef ORBX_SIZEOF
+  return -1;
+}
+
 int orbx_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -831,6 +848,7 @@ static orbx_status bow_host(const orbx_bow_side* A, const orbx_bow_side* B, floa
     return d;
   };
   BowProblem P;
+  std::memset(&P, 0, sizeof(P));  // no device-count overrides on the host path
   P.a = side(A);
   P.b = side(B);
   P.nnratio = nnratio;

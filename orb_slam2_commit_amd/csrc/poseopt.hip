@@ -490,19 +490,20 @@ __global__ __launch_bounds__(PBS) void k_pose_optimization(const PoseDev* __rest
   const PoseDev& D = probs[blockIdx.x];
   const orbx_pose_problem& P = D.p;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int n = P.n;
+  const int n = P.n_dev ? min(max(*P.n_dev, 0), P.n) : P.n;  // device-sized: P.n is the capacity
   double* scr = D.scratch;
   int* act = D.act;
+  const float* Tin = P.Tcw_dev ? P.Tcw_dev : P.Tcw;
 
   for (int i = tid; i < n; i += PBS) P.outlier[i] = 0;
-  if (tid < 16) P.Tcw_out[tid] = P.Tcw[tid];
+  if (tid < 16) P.Tcw_out[tid] = Tin[tid];
   if (P.iterations && tid < 4) P.iterations[tid] = 0;
   if (n < 3) {  // nInitialCorrespondences < 3: return 0, pose untouched
     if (tid == 0) *P.ngood = 0;
     return;
   }
   if (tid == 0) {  // Converter::toSE3Quat(pFrame->mTcw)
-    const float* T = P.Tcw;
+    const float* T = Tin;
     const double R[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
     S.T0.q = mat2q(R);
     qnormalize(S.T0.q);
@@ -802,6 +803,7 @@ extern "C" orbx_status orbx_pose_optimization(const orbx_pose_problem* p, int de
   if (!p) return ORBX_ERR_ARG;
   const orbx_status chk = pose_check(*p);
   if (chk != ORBX_OK) return chk;
+  if (p->n_dev || p->Tcw_dev) return ORBX_ERR_ARG;  // device batches only
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_NODEV;
   if (device < 0 || device >= ndev || hipSetDevice(device) != hipSuccess) return ORBX_ERR_ARG;

@@ -137,7 +137,7 @@ struct Query {
   int th;             // accept bestDist <= th
 };
 
-__device__ Query setup_query(const ProjProblem& P, int i, const float* Ow, bool fwd, bool bwd) {
+__device__ Query setup_query(const ProjProblem& P, int i, const float* Tcw, const float* Ow, bool fwd, bool bwd) {
   Query q;
   q.active = false;
   const orbx_proj_frame& F = P.f;
@@ -163,7 +163,7 @@ __device__ Query setup_query(const ProjProblem& P, int i, const float* Ow, bool 
   if (!(fl & 1)) return q;
   const float* X = P.pos + 3 * i;
   float c[3];
-  mat3x1(F.Tcw, X, c);
+  mat3x1(Tcw, X, c);
   if (P.kind == ORBX_PROJ_FUSE) {  // src/ORBmatcher.cc:960-1006
     if (c[2] < 0.0f) return q;
     const float invz = 1 / c[2];
@@ -252,7 +252,11 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   const ProjProblem& P = probs[blockIdx.x];
   const orbx_proj_frame& F = P.f;
   const int tid = threadIdx.x;
-  const int nF = F.n, nP = P.n_points;
+  if (P.gate && !(*P.gate < P.gate_below)) return;  // block-uniform: the problem is skipped whole
+  const int nF = P.f_n_dev ? min(max(*P.f_n_dev, 0), F.n) : F.n;
+  const int nP = P.n_points_dev ? min(max(*P.n_points_dev, 0), P.n_points) : P.n_points;
+  __shared__ float s_Tcw[16];
+  if (tid < 16) s_Tcw[tid] = P.Tcw_dev ? P.Tcw_dev[tid] : F.Tcw[tid];
   int* s_fw = (int*)s_keys;
 
   // ---- Frame::AssignFeaturesToGrid as a sort of (cell << 13 | index) ----
@@ -300,9 +304,9 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
 
   float Ow[3];
   if (P.kind == ORBX_PROJ_FUSE)
-    camera_centre_kf(F.Tcw, Ow);  // pKF->GetCameraCenter() (src/ORBmatcher.cc:928)
+    camera_centre_kf(s_Tcw, Ow);  // pKF->GetCameraCenter() (src/ORBmatcher.cc:928)
   else
-    camera_centre(F.Tcw, Ow);
+    camera_centre(s_Tcw, Ow);
   bool fwd = false, bwd = false;
   if (P.kind == ORBX_PROJ_LAST_FRAME) {
     float tlc[3];
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
       if (P.flags[i] & 1) {
         const float* X = P.pos + 3 * i;
         float c[3];
-        mat3x1(F.Tcw, X, c);
+        mat3x1(s_Tcw, X, c);
         if (!(c[2] < 0.0f)) {
           const float invz = 1.0f / c[2];
           const float u = F.fx * c[0] * invz + F.cx;
@@ -363,7 +367,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
     __syncthreads();
     int changed = 0;
     for (int i = g; i < nP; i += kGroups) {
-      const Query q = setup_query(P, i, Ow, fwd, bwd);
+      const Query q = setup_query(P, i, s_Tcw, Ow, fwd, bwd);
       int m = -1;
       if (q.active) {
         uint64_t dq[4];
@@ -540,6 +544,7 @@ orbx_status proj_check(const orbx_proj_problem& p, bool host) {
   if (p.f.n > ORBX_PROJ_MAX_FEATURES) return ORBX_ERR_CAPACITY;
   if (p.f.nlevels < 1 || p.f.nlevels > 16) return ORBX_ERR_ARG;
   if (!p.frame_out || !p.point_match || !p.nmatches) return ORBX_ERR_ARG;
+  if (host && (p.f_n_dev || p.n_points_dev || p.Tcw_dev || p.gate)) return ORBX_ERR_ARG;  // device batches only
   if (p.f.n > 0 && (!p.f.keys_un || !p.f.desc)) return ORBX_ERR_ARG;
   if (p.n_points > 0) {
     if (!p.desc || !p.flags) return ORBX_ERR_ARG;

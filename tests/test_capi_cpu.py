@@ -62,3 +62,22 @@ def test_keypoint_layout():
     assert KEYPOINT_DTYPE.itemsize == 28  # cv::KeyPoint
     assert [KEYPOINT_DTYPE.fields[f][1] for f in KEYPOINT_DTYPE.names] == [0, 4, 8, 12, 16, 20, 24]
     assert np.dtype(KEYPOINT_DTYPE)
+
+
+def test_ctypes_layouts_match_the_c_abi():
+    """Every ctypes mirror of an include/orbx.h struct has the C size (orbx_sizeof, no GPU needed)."""
+    import ctypes as C
+    from orb_slam2_commit_amd import _lib
+    L = _lib.lib()
+    pairs = {"orbx_extractor_params": _lib.ExtractorParams, "orbx_bow_side": _lib.BowSide,
+             "orbx_bow_problem": _lib.BowProblem, "orbx_ba_problem": _lib.BaProblem, "orbx_ba_result": _lib.BaResult,
+             "orbx_pnp_problem": _lib.PnpProblem, "orbx_pnp_params": _lib.PnpParams,
+             "orbx_pnp_result": _lib.PnpResult, "orbx_rand_state": _lib.RandState,
+             "orbx_proj_frame": _lib.ProjFrame, "orbx_proj_problem": _lib.ProjProblem,
+             "orbx_tri_kf": _lib.TriKF, "orbx_tri_problem": _lib.TriProblem, "orbx_pose_problem": _lib.PoseProblem,
+             "orbx_track_gather": _lib.TrackGather, "orbx_frame_points": _lib.FramePoints,
+             "orbx_track_step": _lib.TrackStep, "orbx_camera": _lib.Camera}
+    for name, cls in pairs.items():
+        assert L.orbx_sizeof(name.encode()) == C.sizeof(cls), name
+    assert L.orbx_sizeof(b"orbx_keypoint") == _lib.KEYPOINT_DTYPE.itemsize == 28
+    assert L.orbx_sizeof(b"no_such_type") == -1
