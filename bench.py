@@ -556,23 +556,88 @@ def track_leg(args, rank, world, dev, odist, ex, images, stream, pairs_host, ora
     nmat, nedge, ngood = r
     em_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     tim = np.asarray(tim) * 1e3
+    split = dict(extract_match_gpu=round(em_ms, 3), compute_bow_gpu=round(float(tim[:, 3].mean()), 3),
+                 search_by_bow_and_gather_gpu=round(float(tim[:, 4].mean()), 3),
+                 pose_optimization_gpu=round(float(tim[:, 5].mean()), 3))
+    step_ms = el / args.track_steps * 1e3
+    gpu_sum = sum(v for v in split.values())
+    split.update(sum_gpu=round(gpu_sum, 3), frac_of_step=round(gpu_sum / step_ms, 4),
+                 note="GPU time of contiguous phases (HIP events on the launch stream); every launch is sized on "
+                      "the device, the host reads the results back once per step")
     out = dict(frames_per_s=round(B * args.track_steps * world / el, 2),
                tracked_frames_per_s=round(len(pairs) * args.track_steps * world / el, 2),
-               ms_per_step=round(el / args.track_steps * 1e3, 3), batch_frames=B, tracked_per_step=len(pairs),
-               split_ms=dict(extract_match_gpu=round(em_ms, 3),
-                             compute_bow_gpu=round(float(tim[:, 3].mean()), 3),
-                             search_by_bow_and_gather_gpu=round(float(tim[:, 4].mean()), 3),
-                             pose_optimization_gpu=round(float(tim[:, 5].mean()), 3),
-                             note="GPU time of each phase's launches (HIP events on the launch stream); the step "
-                                  "also holds two small readbacks that size the next launches"),
+               ms_per_step=round(step_ms, 3), batch_frames=B, tracked_per_step=len(pairs), split_ms=split,
                matches_per_frame=round(float(np.mean(nmat)), 1), edges_per_frame=round(float(np.mean(nedge)), 1),
                good_per_frame=round(float(np.mean(ngood)), 1),
                vocabulary="synthetic DBoW2 text vocabulary k=10 L=5, FeatureVector at levelsup 3",
-               note="one batch in flight: extract+match (device batch) then ComputeBoW, SearchByBoW(KF=f-%d, F=f), "
-                    "PoseOptimization edge gather and PoseOptimization for every tracked frame; two small host "
-                    "readbacks size the problem descriptors" % U)
+               note="Tracking::TrackReferenceKeyFrame: one batch in flight: extract+match (device batch) then "
+                    "ComputeBoW, SearchByBoW(KF=f-%d, F=f), PoseOptimization edge gather and PoseOptimization for "
+                    "every tracked frame" % U)
     voc.close()
+    out["motion_model"] = motion_leg(args, world, dev, odist, ex, images, stream, pairs, kps, desc, counts, uR, depth,
+                                     nmatch)
     return out
+
+
+def motion_leg(args, world, dev, odist, ex, images, stream, pairs, kps, desc, counts, uR, depth, nmatch):
+    """Tracking::TrackWithMotionModel + TrackLocalMap (src/Tracking.cc:1049-1170, 1403-1468) for every tracked
+    frame of the batch (tracking.MotionTrackBatch): the last frame's MapPoints, SearchByProjection(F, LastFrame)
+    (+ the 2*th retry), PoseOptimization, outlier removal, SearchLocalPoints (frustum + SearchByProjection) and
+    PoseOptimization again, every launch sized on the device.  Frame f is tracked from frame f-U, the same
+    scene 53 px earlier: the last frame's keypoints are moved by the roll (a 'virtual' last frame), and the
+    motion-model pose guess is the identity."""
+    import torch
+    from orb_slam2_commit_amd.tracking import MotionTrackBatch
+    W, H, B = KITTI["width"], KITTI["height"], args.batch
+    cap = ex.max_keypoints(W, H)
+    fx, bf = KITTI["fx"], KITTI["bf"]
+    mt = MotionTrackBatch(len(pairs), cap, W, H, ex.GetScaleFactors(), ex.GetInverseScaleSigmaSquares(), fx, fx,
+                          607.1928, 185.2157, bf, dev)
+    lf_idx = torch.tensor([2 * lf for lf, _ in pairs], device=dev)
+    bl = bf / fx
+
+    def step(tim=None):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record(stream)
+        ex.stereo_frames_device(images, kps, desc, counts, bf, bl, uR, depth, nmatch, stream)
+        with torch.cuda.stream(stream):
+            last = kps.index_select(0, lf_idx)
+            last.view(torch.float32).view(len(pairs), cap, 7)[:, :, 0] += 53.0
+        e1.record(stream)
+        r = mt.run(kps, desc, counts, uR, depth, pairs, last_kps=last, stream=stream, timings=tim)
+        e2.record(stream)
+        return r, (e0, e1, e2)
+
+    step()
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    tim, evs = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.track_steps):
+        r, ev = step(tim)
+        evs.append(ev)
+    torch.cuda.synchronize(dev)
+    odist.barrier()
+    el = odist.max_over_ranks(time.perf_counter() - t0, dev)
+    step_ms = el / args.track_steps * 1e3
+    tim = np.asarray(tim) * 1e3
+    split = dict(extract_match_and_last_frame_gpu=round(float(np.mean([a.elapsed_time(b) for a, b, _ in evs])), 3),
+                 search_last_frame_gpu=round(float(tim[:, 0].mean()), 3),
+                 edges_and_pose_1_gpu=round(float(tim[:, 1].mean()), 3),
+                 search_local_points_gpu=round(float(tim[:, 2].mean()), 3),
+                 edges_and_pose_2_gpu=round(float(tim[:, 3].mean()), 3))
+    gpu_sum = sum(split.values())
+    split.update(sum_gpu=round(gpu_sum, 3), frac_of_step=round(gpu_sum / step_ms, 4),
+                 note="GPU time of contiguous phases (HIP events on the launch stream); no host readback between "
+                      "launches, results read once per step")
+    return dict(frames_per_s=round(B * args.track_steps * world / el, 2),
+                tracked_frames_per_s=round(len(pairs) * args.track_steps * world / el, 2),
+                ms_per_step=round(step_ms, 3), tracked_per_step=len(pairs), split_ms=split,
+                motion_matches_per_frame=round(float(np.mean(r["nmatches"])), 1),
+                motion_inliers_per_frame=round(float(np.mean(r["ngood_motion"])), 1),
+                local_matches_per_frame=round(float(np.mean(r["local_matches"])), 1),
+                inliers_per_frame=round(float(np.mean(r["inliers"])), 1), lost_frames=int(np.sum(r["lost"])),
+                note="Tracking::TrackWithMotionModel + TrackLocalMap for every tracked frame, one batch in flight")
 
 
 # ------------------------------------------------------------------ config-3 leg
