@@ -139,6 +139,12 @@ class TrackGather(C.Structure):
                 ("n_edges", C.c_void_p)]
 
 
+class BaDebugOptions(C.Structure):  # include/orbx_debug.h orbx_ba_debug_options
+    _fields_ = [("host_lm", C.c_int), ("no_spec", C.c_int), ("host_struct", C.c_int), ("no_fuse", C.c_int),
+                ("no_camfold", C.c_int), ("no_psfold", C.c_int), ("ldlt", C.c_int), ("nan_trial", C.c_int),
+                ("raise_stop_after", C.c_int), ("trace", C.c_int)]
+
+
 class Camera(C.Structure):
     _fields_ = [("K", C.c_float * 9), ("dist", C.c_float * 5), ("n_dist", C.c_int)]
 
@@ -222,6 +228,8 @@ SIGNATURES = {
     # include/orbx_debug.h
     "orbx_debug_copy": ([P, C.c_int, C.c_int, C.c_int, P, C.c_size_t], C.c_longlong),
     "orbx_debug_ldlt": ([P, P, C.c_int, P, C.c_int, C.POINTER(C.c_float)], C.c_int),
+    "orbx_debug_ldlt_ex": ([P, P, C.c_int, P, C.c_int, C.POINTER(C.c_float), C.c_int, P], C.c_int),
+    "orbx_debug_ba_options": ([P, C.POINTER(BaDebugOptions)], C.c_int),
     "orbx_debug_hbm_copy": ([P, P, C.c_size_t, C.c_int, C.POINTER(C.c_float)], C.c_int),
 }
 

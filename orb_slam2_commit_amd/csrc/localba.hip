@@ -40,7 +40,14 @@
 #include <vector>
 
 #include "../../include/orbx.h"
+#include "../../include/orbx_debug.h"
 #include "orbx_device.h"
+
+namespace orbx {
+// Debug / test options of the solver handle running on this thread (orbx_debug_ba_options); the
+// production default is all-off.  Set for the duration of an orbx_ba_run* call (BaOptScope).
+inline const orbx_ba_debug_options& ba_opts();
+}  // namespace orbx
 
 namespace orbx {
 
@@ -995,15 +1002,15 @@ __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
 // (k1, k2) order).  Blocks b >= nblk: sum of cf over pose b - nblk's positions
 // (the Schur rhs correction).  Chunk partials -> gpart; k_ba_schur_fin sums
 // them in chunk order (deterministic).
-// device-LM trials fold k_ba_cam_sum / k_ba_cam_fin into k_ba_pairs / k_ba_schur_fin (A/B:
-// ORBX_BA_NO_CAMFOLD=1 launches them as before; results are bit-identical either way)
-static bool camfold_on() { return std::getenv("ORBX_BA_NO_CAMFOLD") == nullptr; }
+// device-LM trials fold k_ba_cam_sum / k_ba_cam_fin into k_ba_pairs / k_ba_schur_fin (debug option
+// no_camfold launches them as before; results are bit-identical either way)
+static bool camfold_on() { return !ba_opts().no_camfold; }
 // device-LM value of BaDev::fused: 2 = k_ba_lin_schur also takes the non-relinearising trials'
-// point side and k_ba_point_schur is not launched (A/B: ORBX_BA_NO_PSFOLD=1).  A problem without
+// point side and k_ba_point_schur is not launched (debug option no_psfold: launched).  A problem without
 // free poses keeps 1 (k_ba_point_schur flags its empty reduced system).
 static int fused_mode(int nbf, int nposes) {
   if (nbf <= 0) return 0;
-  return nposes > 0 && std::getenv("ORBX_BA_NO_PSFOLD") == nullptr ? 2 : 1;
+  return nposes > 0 && !ba_opts().no_psfold ? 2 : 1;
 }
 
 // pose-term chunk partials of a camfold trial, after the pair and rhs partials
@@ -1566,11 +1573,8 @@ inline size_t ldlt_pan_smem(int N) {
 // (one tile per thread: with two the trailing update doubles and the panel kernel loses to the
 // column-step one, e.g. 91 us at N = 126)
 inline bool ldlt_pan_fits(int N) { return ldlt_pan_smem(N) <= kLdltColMaxSmem && ldlt_col_tiles(N) <= 512 && N < 128; }
-// default where it fits (A/B: ORBX_LDLT_COL=1 keeps the column-step kernel)
-inline bool ldlt_use_pan(int N) {
-  return ldlt_pan_fits(N) && !std::getenv("ORBX_LDLT_COL") && !std::getenv("ORBX_LDLT_BLK") &&
-         !std::getenv("ORBX_LDLT_BLOCKED");
-}
+// default where it fits (debug option ldlt = ORBX_BA_LDLT_COLUMN keeps the column-step kernel)
+inline bool ldlt_use_pan(int N) { return ldlt_pan_fits(N) && ba_opts().ldlt == ORBX_BA_LDLT_AUTO; }
 constexpr int ldlt_tri(int a, int b) { return a * (a + 1) / 2 + b; }
 
 template <int TPT, int NT, int R>  // R: 64-row groups of the back solve (N < 64 R)
@@ -1818,217 +1822,27 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_pan_many(const BaDev* __restrict
   k_ba_ldlt_pan_body<TPT, NT, R>(Ds[blockIdx.z]);
 }
 
-// ---- reduced camera system, N <= 128: 16-wide blocked LDL^T, FP64 MFMA trailing updates ----
-// The column-step kernel above pays one barrier + LDS round trip per pivot (~1,100 cycles, 120
-// pivots at config 4).  Here the pivots run in 16-wide panels; per panel p (j0 = 16p):
-//   F  wave 0 factors the 16x16 diagonal block in registers (lane r = row r; the pivot and the
-//      W[k][c] = L[k][c] d_c of the rows below it broadcast by readlane), 1/d by v_rcp_f64 + two
-//      Newton steps; it stores L (lower) and W (mirrored into the upper triangle) and d;
-//   T  every row below the panel, the augmented row b^T included, solves W_i L_pp^T = A_i (one
-//      thread per row, L_pp broadcast from LDS) and stores L_i = W_i D^-1 (lower) and W_i
-//      (mirrored: A[j0+c][i]);
-//   U  the trailing lower triangle A_ik -= W_i L_k^T as v_mfma_f64_16x16x4f64 tiles over the
-//      waves (4 MFMAs per 16x16 tile); one wave updates the augmented row with plain FMAs.
-// Three barriers per panel instead of sixteen.  The augmented row ends as y = D^-1 L^-1 b (the
-// forward solve is free), and wave 0 solves L^T x = y with the column entries prefetched eight
-// pivots at a time.  Same failure rule as the other kernels (an exactly zero pivot, scal[2] = 0).
-// LDS: (Np+1) rows x (Np+1) doubles (odd stride: a 16-lane column read spreads over the banks)
-// plus d: 134 KB at Np = 128.
-constexpr int kLdltBlkNT = 512;
-inline size_t ldlt_blk_smem(int N) {
-  const size_t Np = ldlt_np(N);
-  return ((Np + 1) * (Np + 1) + Np + 16) * sizeof(double);
-}
-inline bool ldlt_blk_fits(int N) { return ldlt_np(N) <= 128 && N > 0; }
-
-template <int NT>
-__device__ __forceinline__ void k_ba_ldlt_blk_body(const BaDev& D) {
-  if (lm_skip(D)) return;
-  extern __shared__ __attribute__((aligned(16))) double A[];
-  __shared__ int fail;
-  constexpr int NW = NT / 64;
-  const int N = 6 * D.nposes, Np = (N + 15) & ~15, T = Np >> 4, ld = Np + 1;
-  double* dg = A + (size_t)(Np + 1) * ld;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // S padded with an identity block (decoupled, never a zero pivot); row Np = b
-  for (int idx = tid; idx < (Np + 1) * Np; idx += NT) {
-    const int r = idx / Np, c = idx - r * Np;
-    double v;
-    if (r < Np)
-      v = (r < N && c < N) ? D.S[(size_t)r * N + c] : (r == c ? 1.0 : 0.0);
-    else
-      v = c < N ? D.bs[c] : 0.0;
-    A[(size_t)r * ld + c] = v;
-  }
-  if (tid == 0) fail = 0;
-  __syncthreads();
-  LDLT_TS(0);
-  for (int p = 0; p < T; p++) {
-    const int j0 = 16 * p;
-    // ---- F: the diagonal block
-    if (wv == 0) {
-      const int r = lane & 15;
-      double row[16];
-#pragma unroll
-      for (int c = 0; c < 16; c++) row[c] = A[(size_t)(j0 + r) * ld + j0 + c];
-      bool bad = false;
-#pragma unroll
-      for (int c = 0; c < 16; c++) {
-        const double d = readlane_d(row[c], c);
-        bad |= d == 0.0;
-        const double lrc = row[c] * rcp_nr(d);  // L[r][c] (rows r > c)
-#pragma unroll
-        for (int k = c + 1; k < 16; k++) {
-          const double wkc = readlane_d(row[c], k);  // W[k][c]
-          if (r >= k) row[k] -= lrc * wkc;
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep each pivot's broadcasts next to their use
-      }
-      if (bad) {
-        if (lane == 0) fail = 1;
-      } else if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; c++) {
-          const double dc = readlane_d(row[c], c);
-          if (c < r) {
-            A[(size_t)(j0 + r) * ld + j0 + c] = row[c] * rcp_nr(dc);  // L
-            A[(size_t)(j0 + c) * ld + j0 + r] = row[c];               // W (mirror)
-          }
-        }
-        dg[j0 + r] = row[r];
-      }
-    }
-    __syncthreads();
-    LDLT_TS(1 + 3 * p);
-    if (fail) {
-      if (tid == 0) D.scal[2] = 0.0;
-      return;
-    }
-    // ---- T: the rows below the panel and the augmented row
-    const int nrows = Np - j0 - 16 + 1;
-    for (int t = tid; t < nrows; t += NT) {
-      const int i = j0 + 16 + t;
-      double w[16];
-#pragma unroll
-      for (int c = 0; c < 16; c++) w[c] = A[(size_t)i * ld + j0 + c];
-#pragma unroll
-      for (int c = 1; c < 16; c++)
-#pragma unroll
-        for (int m = 0; m < c; m++) w[c] -= w[m] * A[(size_t)(j0 + c) * ld + j0 + m];
-#pragma unroll
-      for (int c = 0; c < 16; c++) {
-        A[(size_t)i * ld + j0 + c] = w[c] * rcp_nr(dg[j0 + c]);  // L_i
-        A[(size_t)(j0 + c) * ld + i] = w[c];                      // W_i (mirror; column Np for b)
-      }
-    }
-    __syncthreads();
-    LDLT_TS(2 + 3 * p);
-    // ---- U: trailing update A_ik -= W_i L_k^T (tiles of the lower triangle), augmented row
-    const int m = T - 1 - p, ntiles = m * (m + 1) / 2;
-    for (int t = wv; t < ntiles + (m > 0 ? 1 : 0); t += NW) {
-      if (t < ntiles) {
-        int ti = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
-        while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
-        while (ti * (ti + 1) / 2 > t) ti--;
-        const int tk = t - ti * (ti + 1) / 2;
-        const int R0 = j0 + 16 + 16 * ti, C0 = j0 + 16 + 16 * tk;
-        double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 4; kk++) {
-          const int k = j0 + 4 * kk + (lane >> 4);
-          const double av = A[(size_t)k * ld + R0 + (lane & 15)];   // W[row][k] (mirror)
-          const double bv = A[(size_t)(C0 + (lane & 15)) * ld + k];  // L[col][k]
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; rr++) A[(size_t)(R0 + (lane >> 4) + 4 * rr) * ld + C0 + (lane & 15)] -= acc[rr];
-      } else {
-        for (int cc = lane; cc < 16 * m; cc += 64) {
-          const int col = j0 + 16 + cc;
-          double sacc = A[(size_t)Np * ld + col];
-#pragma unroll
-          for (int c = 0; c < 16; c++) sacc -= A[(size_t)(j0 + c) * ld + Np] * A[(size_t)col * ld + j0 + c];
-          A[(size_t)Np * ld + col] = sacc;
-        }
-      }
-    }
-    __syncthreads();
-    LDLT_TS(3 + 3 * p);
-  }
-  if (wv != 0) return;
-  // y = D^-1 L^-1 b sits in row Np; L^T x = y by columns, x_k final at step k
-  double y[2];
-#pragma unroll
-  for (int q = 0; q < 2; q++) {
-    const int i = lane + 64 * q;
-    y[q] = i < N ? A[(size_t)Np * ld + i] : 0.0;
-  }
-  for (int kb = N - 1; kb >= 0; kb -= 8) {
-    double Lv[8][2];
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const int i = lane + 64 * q, k = max(kb - u, 0);
-        const double v = A[(size_t)k * ld + min(i, Np - 1)];  // row k, column i: L[k][i] when i < k
-        Lv[u][q] = (i < kb - u) ? v : 0.0;
-      }
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int k = kb - u;
-      if (k >= 0) {
-        const double xk = readlane_d(k < 64 ? y[0] : y[1], k & 63);
-#pragma unroll
-        for (int q = 0; q < 2; q++) y[q] -= Lv[u][q] * xk;
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 2; q++)
-    if (lane + 64 * q < N) D.xp[lane + 64 * q] = y[q];
-  if (lane == 0) D.scal[2] = 1.0;
-  LDLT_TS(61);
-}
-template <int NT>
-__global__ __launch_bounds__(NT) void k_ba_ldlt_blk(BaDev D) { k_ba_ldlt_blk_body<NT>(D); }
-template <int NT>
-__global__ __launch_bounds__(NT) void k_ba_ldlt_blk_many(const BaDev* __restrict__ Ds) {
-  k_ba_ldlt_blk_body<NT>(Ds[blockIdx.z]);
-}
-
-// Launch plan for the reduced system: the column-step kernel while the
-// packed factor fits LDS, else the 16-wide blocked kernel (LDS or global).
+// Launch plan for the reduced system: the 8-wide panel kernel (N < 128), the column-step kernel while
+// the packed factor fits LDS, else the 16-wide blocked MFMA kernel (LDS or global).  The debug options
+// (orbx_debug_ba_options) can force the column-step or the blocked kernel where they fit, for tests.
 struct LdltPlan {
   int N = 0, tpt = 0, nt = 1024;
-  bool col = false, in_lds = false, blk = false, pan = false;
+  bool col = false, in_lds = false, pan = false;
   size_t smem = 0;
   hipError_t prepare(int n, bool allow_pan = true) {
     N = n;
     pan = allow_pan && ldlt_use_pan(N);
     if (pan) {
       col = false;
-      blk = false;
       in_lds = true;
       nt = 512;
       tpt = 1;
       smem = ldlt_pan_smem(N);
       return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     }
-    // A/B switch: ORBX_LDLT_BLK=1 takes the MFMA-blocked kernel where it fits (measured slower than
-    // the column-step kernel at config 4: 117 vs 60 us; one launch shape per batch)
-    blk = ldlt_blk_fits(N) && std::getenv("ORBX_LDLT_BLK") && !std::getenv("ORBX_LDLT_BLOCKED");
-    if (blk) {
-      col = false;
-      in_lds = true;
-      nt = kLdltBlkNT;
-      smem = ldlt_blk_smem(N);
-      return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    }
-    col = ldlt_col_fits(N) && !std::getenv("ORBX_LDLT_BLOCKED");
+    col = ldlt_col_fits(N) && ba_opts().ldlt != ORBX_BA_LDLT_BLOCKED;
     if (col) {
-      const char* e = std::getenv("ORBX_LDLT_NT");  // A/B: threads of the column-step kernel
-      nt = e ? std::atoi(e) : 1024;
-      if (nt != 256 && nt != 512) nt = 1024;
+      nt = 1024;
       const int tiles = ldlt_col_tiles(N);
       tpt = (tiles + nt - 1) / nt;
       if (tpt > 8 || (nt == 1024 && tpt > 2) || (nt == 512 && tpt > 4)) {
@@ -2045,7 +1859,6 @@ struct LdltPlan {
   }
   const void* kernel_ptr() const {
     if (pan) return (const void*)k_ba_ldlt_pan<1, 512, 2>;
-    if (blk) return (const void*)k_ba_ldlt_blk<kLdltBlkNT>;
     if (col) {
       if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col<1, 1024> : (const void*)k_ba_ldlt_col<2, 1024>;
       if (nt == 512)
@@ -2059,7 +1872,6 @@ struct LdltPlan {
   // batched driver: the column-step kernel over K problems (blockIdx.z), sized for the largest
   const void* many_ptr() const {
     if (pan) return (const void*)k_ba_ldlt_pan_many<1, 512, 2>;
-    if (blk) return (const void*)k_ba_ldlt_blk_many<kLdltBlkNT>;
     if (nt == 1024) return tpt == 1 ? (const void*)k_ba_ldlt_col_many<1, 1024> : (const void*)k_ba_ldlt_col_many<2, 1024>;
     if (nt == 512)
       return tpt == 1 ? (const void*)k_ba_ldlt_col_many<1, 512>
@@ -2075,7 +1887,7 @@ struct LdltPlan {
                        dim3(nt), smem, st, Ds);
   }
   void launch(const BaDev& D, hipStream_t st, int stage_limit = 99) const {
-    if (blk || col || pan) {
+    if (col || pan) {
       hipLaunchKernelGGL(reinterpret_cast<void (*)(BaDev)>(const_cast<void*>(kernel_ptr())), dim3(1), dim3(nt),
                          smem, st, D);
     } else if (in_lds) {
@@ -3199,7 +3011,7 @@ struct LocalBA {
     const int ga = std::max((D.na + LBS - 1) / LBS, 1);
     double sc[5];
     int ptrial = 0;  // trials of this phase (the ORBX_BA_NAN_TRIAL hook counts per phase, as the device loop)
-    const bool spec_on = std::getenv("ORBX_BA_NO_SPEC") == nullptr;  // A/B switch
+    const bool spec_on = !ba_opts().no_spec;
     bool spec_ready = false;  // the other LinSet holds the linearisation at the current state
     double spec_chi = 0;      // its chi (the accepted trial's)
     for (int i = 0; i < iterations && !(stop()); i++) {
@@ -3440,13 +3252,10 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
   L.trials = 0;
   for (double& t : L.t_struct) t = 0;
   BaDev& D = L.D;
-  {  // test hooks (off unless the environment asks): a NaN trial, a device-raised stop flag
-    const char* e1 = std::getenv("ORBX_BA_NAN_TRIAL");
-    const char* e2 = std::getenv("ORBX_BA_RAISE_STOP_AFTER");
-    D.nan_trial = e1 ? std::atoi(e1) : -1;
-    D.raise_after = e2 ? std::atoi(e2) : -1;
-    D.host_trial = 0;
-  }
+  // test hooks (off unless orbx_debug_ba_options set them): a NaN trial, a device-raised stop flag
+  D.nan_trial = ba_opts().nan_trial;
+  D.raise_after = ba_opts().raise_stop_after;
+  D.host_trial = 0;
   Ctx& c = L.c;
   const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
   D.nc = nc;
@@ -3465,10 +3274,10 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
     max_run = std::max(max_run, run);
     L.ccnt[pb->edge_cam[e]]++;
   }
-  // the fused point side needs every point's positions inside one block (A/B: ORBX_BA_NO_FUSE=1)
-  L.fuse_ok = grouped && max_run <= kFuseMaxDeg && std::getenv("ORBX_BA_NO_FUSE") == nullptr;
+  // the fused point side needs every point's positions inside one block (debug option no_fuse: split)
+  L.fuse_ok = grouped && max_run <= kFuseMaxDeg && !ba_opts().no_fuse;
   L.dev_struct = grouped && nc <= kStructMaxNc && (ne + kTileE - 1) / kTileE <= kStructMaxTiles &&
-                 std::getenv("ORBX_BA_HOST_STRUCT") == nullptr;
+                 !ba_opts().host_struct;
   if (L.dev_struct) {  // phase-1 sizes: the launches need no readback
     int nposes = 0, maxc = 0;
     for (int i = 0; i < nc; i++)
@@ -3645,7 +3454,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   DevStop dstop{nullptr, nullptr};
   L.unmap_stop();
   L.hook_stopped = false;
-  const bool dev_lm = std::getenv("ORBX_BA_HOST_LM") == nullptr && L.map_stop(stop, &dstop);
+  const bool dev_lm = !ba_opts().host_lm && L.map_stop(stop, &dstop);
   auto optimize = [&](int iterations, int* iters, double* chi) {
     return dev_lm ? L.optimize_dev(iterations, stop, dstop, st, iters, chi) : L.optimize(iterations, stop, st, iters, chi);
   };
@@ -3680,7 +3489,7 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   if (!ran) return ORBX_OK;
   BA_CHECK(hipStreamSynchronize(st));
   ba_writeback_finish(L, pb, res, ran);
-  if (std::getenv("ORBX_BA_TRACE"))
+  if (ba_opts().trace)
     std::fprintf(stderr,
                  "[orbx_ba] total %.3f ms, structure %.3f ms (host index %.3f, host poses %.3f, device %.3f, upload %.3f), "
                  "iterations %d+%d, trials %d\n",
@@ -3733,7 +3542,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
   LdltPlan ldlt, lpan;
   if (Ncol > 0 || Npan == 0) {
     BA_CHECK(ldlt.prepare(std::max(Ncol, 6), false));
-    if (!ldlt.col && !ldlt.blk) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
+    if (!ldlt.col) return ORBX_ERR_SIZE;  // the caller runs the problems one by one
     BA_CHECK(ldlt.prepare_many());
   }
   if (Npan > 0) {
@@ -3863,7 +3672,7 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
   }
   DevStop dstop{nullptr, nullptr};
   for (int i = 0; i < K; i++) Ls[i]->unmap_stop();
-  bool batch = std::getenv("ORBX_BA_HOST_LM") == nullptr && Ls[0]->map_stop(stop, &dstop);
+  bool batch = !ba_opts().host_lm && Ls[0]->map_stop(stop, &dstop);
   for (int i = 0; i < K; i++) batch &= Ls[i]->dev_struct;
   if (!batch) {  // one by one (intake again inside: the arenas are reused)
     for (int i = 0; i < K; i++) {
@@ -3923,9 +3732,21 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
 
 }  // namespace orbx
 
+namespace orbx {
+constexpr orbx_ba_debug_options kBaOptsDefault = {0, 0, 0, 0, 0, 0, ORBX_BA_LDLT_AUTO, -1, -1, 0};
+thread_local const orbx_ba_debug_options* t_ba_opts = nullptr;
+inline const orbx_ba_debug_options& ba_opts() { return t_ba_opts ? *t_ba_opts : kBaOptsDefault; }
+struct BaOptScope {  // the handle's options for this call on this thread
+  const orbx_ba_debug_options* prev;
+  explicit BaOptScope(const orbx_ba_debug_options* o) : prev(t_ba_opts) { t_ba_opts = o; }
+  ~BaOptScope() { t_ba_opts = prev; }
+};
+}  // namespace orbx
+
 struct orbx_ba {
   int device = 0;
   hipStream_t st = nullptr;
+  orbx_ba_debug_options opts = orbx::kBaOptsDefault;
   orbx::LocalBA L;
   std::vector<std::unique_ptr<orbx::LocalBA>> more;  // orbx_ba_run_many: problems 1..K-1
   orbx::BaBatch batch;
@@ -3975,9 +3796,17 @@ orbx_status orbx_ba_run_many(orbx_ba* h, int n, const orbx_ba_problem* problems,
   std::vector<orbx::LocalBA*> Ls(n);
   Ls[0] = &h->L;
   for (int i = 1; i < n; i++) Ls[i] = h->more[i - 1].get();
+  orbx::BaOptScope scope(&h->opts);
   orbx::StopFlag sf;
   sf.i = stop_flag;
   return orbx::run_local_ba_many(Ls.data(), n, h->batch, problems, results, sf, h->st);
+}
+
+int orbx_debug_ba_options(orbx_ba* h, const orbx_ba_debug_options* o) {
+  if (!h) return ORBX_ERR_ARG;
+  if (o && (o->ldlt < ORBX_BA_LDLT_AUTO || o->ldlt > ORBX_BA_LDLT_BLOCKED)) return ORBX_ERR_ARG;
+  h->opts = o ? *o : orbx::kBaOptsDefault;
+  return ORBX_OK;
 }
 
 orbx_status orbx_ba_stop_flag(orbx_ba* h, volatile int** flag) {
@@ -4010,6 +3839,7 @@ orbx_status orbx_ba_run(orbx_ba* h, const orbx_ba_problem* p, orbx_ba_result* r,
   if (p->n_edges > 0 && (!p->edge_point || !p->edge_cam || !p->obs || !p->inv_sigma2 || !r->edge_outlier))
     return ORBX_ERR_ARG;
   if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  orbx::BaOptScope scope(&h->opts);
   orbx::StopFlag f;
   f.i = stop_flag;
   return orbx::run_local_ba(h->L, p, r, f, h->st);
@@ -4023,6 +3853,7 @@ orbx_status orbx_ba_run_bool(orbx_ba* h, const orbx_ba_problem* p, orbx_ba_resul
   if (p->n_edges > 0 && (!p->edge_point || !p->edge_cam || !p->obs || !p->inv_sigma2 || !r->edge_outlier))
     return ORBX_ERR_ARG;
   if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  orbx::BaOptScope scope(&h->opts);
   orbx::StopFlag f;
   f.b = stop_flag;
   return orbx::run_local_ba(h->L, p, r, f, h->st);
@@ -4042,8 +3873,17 @@ orbx_status orbx_local_ba(const orbx_ba_problem* p, orbx_ba_result* r, const vol
 // Debug/benchmark probe (include/orbx_debug.h): solve S x = b (N = 6 * nposes)
 // with the LocalBA LDLT kernel; ms = average kernel time over reps launches.
 extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* x, int reps, float* ms) {
+  return orbx_debug_ldlt_ex(S, b, N, x, reps, ms, ORBX_BA_LDLT_AUTO, nullptr);
+}
+
+extern "C" int orbx_debug_ldlt_ex(const double* S, const double* b, int N, double* x, int reps, float* ms, int kind,
+                                  unsigned long long* stamps) {
   if (!S || !b || !x || N <= 0 || N % 6 || reps < 1) return ORBX_ERR_ARG;
-  const int stage_limit = std::getenv("ORBX_LDLT_STAGE") ? std::atoi(std::getenv("ORBX_LDLT_STAGE")) : 99;
+  if (kind < ORBX_BA_LDLT_AUTO || kind > ORBX_BA_LDLT_BLOCKED) return ORBX_ERR_ARG;
+  orbx_ba_debug_options o = orbx::kBaOptsDefault;
+  o.ldlt = kind;
+  orbx::BaOptScope scope(&o);
+  const int stage_limit = 99;
   orbx::BaDev D{};
   D.nposes = N / 6;
   double *dS = nullptr, *dS0 = nullptr, *db = nullptr, *dx = nullptr, *dscal = nullptr;
@@ -4061,7 +3901,7 @@ extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* 
   D.xp = dx;
   D.scal = dscal;
   unsigned long long* ddbg = nullptr;
-  const bool want_ts = std::getenv("ORBX_LDLT_TS") != nullptr;
+  const bool want_ts = stamps != nullptr;
   if (e == hipSuccess && want_ts) {
     e = hipMalloc((void**)&ddbg, 64 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(ddbg, 0, 64 * sizeof(unsigned long long));
@@ -4103,13 +3943,9 @@ extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* 
   (void)hipFree(dscal);
   if (dSw) (void)hipFree(dSw);
   if (ddbg) {
-    unsigned long long ts[64];
-    if (hipMemcpy(ts, ddbg, sizeof(ts), hipMemcpyDeviceToHost) == hipSuccess) {
-      std::fprintf(stderr, "[ldlt ts N=%d] ", N);
-      for (int i = 1; i < 64; i++)
-        if (ts[i]) std::fprintf(stderr, "%d:%llu ", i, ts[i] - ts[0]);
-      std::fprintf(stderr, "\n");
-    }
+    // the kernel's s_memtime stamps (LDLT_TS points; 0 = not reached) of the last launch
+    if (hipMemcpy(stamps, ddbg, 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+      e = hipErrorUnknown;
     (void)hipFree(ddbg);
   }
   if (e != hipSuccess) return ORBX_ERR_HIP;

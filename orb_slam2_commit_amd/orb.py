@@ -17,6 +17,7 @@ Names, argument meaning and error behaviour follow the reference:
 
 Every result is computed by the HIP kernels; this module only moves bytes.
 """
+import contextlib
 import ctypes as C
 
 import numpy as np
@@ -480,6 +481,25 @@ class Optimizer:
             _lib.lib().orbx_ba_destroy(self._h)
             self._h = None
             self._stop = None
+
+    def set_debug_options(self, **kw):
+        """Test / A-B options of this solver handle (include/orbx_debug.h, orbx_ba_debug_options:
+        host_lm, no_spec, host_struct, no_fuse, no_camfold, no_psfold, ldlt, nan_trial,
+        raise_stop_after, trace); no arguments restore the production defaults."""
+        o = _lib.BaDebugOptions(0, 0, 0, 0, 0, 0, 0, -1, -1, 0)
+        for k, v in kw.items():
+            if k not in dict(o._fields_):
+                raise TypeError("unknown LocalBA debug option %r" % k)
+            setattr(o, k, int(v))
+        check(_lib.lib().orbx_debug_ba_options(self._h, C.byref(o)), "orbx_debug_ba_options")
+
+    @contextlib.contextmanager
+    def debug_options(self, **kw):
+        self.set_debug_options(**kw)
+        try:
+            yield self
+        finally:
+            self.set_debug_options()
 
     def __del__(self):
         try:

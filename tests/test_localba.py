@@ -238,30 +238,33 @@ def test_gpu_localba_stop_and_degenerate(ba):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,kw", [(7, {}), (10, {}), (8, dict(n_local=30, n_fixed=4, n_points=4000))])
-def test_gpu_localba_speculative_linearization_bit_identical(ba, seed, kw, monkeypatch):
+def test_gpu_localba_speculative_linearization_bit_identical(ba, seed, kw):
     """Linearising the next iteration into the second buffer set while the host reads a
     trial back (default) gives bit-identical poses, points, outlier flags and LM counts
-    to the in-line path (ORBX_BA_NO_SPEC=1)."""
+    to the in-line path (debug options host_lm + no_spec)."""
     P = synth.localba_problem(seed=seed, **kw)
     a = ba.LocalBundleAdjustment(P)
-    monkeypatch.setenv("ORBX_BA_NO_SPEC", "1")
-    b = ba.LocalBundleAdjustment(P)
-    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
-        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
-    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+    with ba.debug_options(host_lm=1):
+        h = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(host_lm=1, no_spec=1):
+        b = ba.LocalBundleAdjustment(P)
+    for o in (h, b):
+        for k in ("Tcw_d", "Xw_d", "edge_outlier"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(o[k]))
+        assert list(a["iterations"]) == list(o["iterations"]) and a["trials"] == o["trials"]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(REJECT_CASES))
-def test_gpu_localba_rejections_match_oracle(ba, name, monkeypatch):
+def test_gpu_localba_rejections_match_oracle(ba, name):
     """Rejected trials (pop + lambda *= ni, with a speculative linearisation launched on the
     trial state that is then discarded) and the _nBad early stop: GPU = oracle, and the
-    speculative path = the in-line path (ORBX_BA_NO_SPEC=1) bit for bit."""
+    speculative path = the in-line path (debug options host_lm + no_spec) bit for bit."""
     P = reject_problem(name)
     a = ba.LocalBundleAdjustment(P)
     _compare(a, oracle.local_ba(P))
-    monkeypatch.setenv("ORBX_BA_NO_SPEC", "1")
-    b = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(host_lm=1, no_spec=1):
+        b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw_d", "Xw_d", "edge_outlier"):
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
     assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
@@ -269,11 +272,11 @@ def test_gpu_localba_rejections_match_oracle(ba, name, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["config4", "small", "many_kfs", "no_outliers", "all_fixed", "empty", "one_edge"])
-def test_gpu_localba_device_structure_bit_identical(ba, case, monkeypatch):
+def test_gpu_localba_device_structure_bit_identical(ba, case):
     """The per-phase active-edge structure built on the device (k_ba_struct: point
     segments, pose indices, pose-grouped positions, pair-table offsets) gives
     bit-identical poses, points, outlier flags and LM counts to the host build
-    (ORBX_BA_HOST_STRUCT=1), both phases (phase 2 reads the outlier flags on the device)."""
+    (debug option host_struct), both phases (phase 2 reads the outlier flags on the device)."""
     if case == "config4":
         P = synth.localba_problem(seed=7)
     elif case == "many_kfs":
@@ -289,8 +292,8 @@ def test_gpu_localba_device_structure_bit_identical(ba, case, monkeypatch):
             for k in ("edge_point", "edge_cam", "obs", "inv_sigma2"):
                 P[k] = np.ascontiguousarray(np.asarray(P[k])[:n])
     a = ba.LocalBundleAdjustment(P)
-    monkeypatch.setenv("ORBX_BA_HOST_STRUCT", "1")
-    b = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(host_struct=1):
+        b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw_d", "Xw_d", "edge_outlier"):
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
     assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
@@ -307,17 +310,16 @@ def test_gpu_localba_repeatable(ba):
         np.testing.assert_array_equal(a[k], b[k])  # fixed-order reductions: run-to-run identical
 
 
+LDLT_KIND = {"default": 0, "col": 1, "blocked": 2}  # orbx_ba_debug_options.ldlt
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["default", "col", "mfma_blk"])
+@pytest.mark.parametrize("kernel", ["default", "col", "blocked"])
 @pytest.mark.parametrize("N", [6, 18, 60, 120, 126, 132, 168, 174, 180, 252])
-def test_gpu_reduced_system_ldlt(gpu, N, kernel, monkeypatch):
-    """The reduced-system LDLT kernels (8-wide panels while the packed factor fits LDS, N <= 174;
-    column-step in LDS, 16-blocked above; the opt-in MFMA-blocked one up to 128 padded rows)
-    solve SPD Schur systems to FP64 accuracy."""
-    if kernel == "mfma_blk":
-        monkeypatch.setenv("ORBX_LDLT_BLK", "1")
-    if kernel == "col":
-        monkeypatch.setenv("ORBX_LDLT_COL", "1")
+def test_gpu_reduced_system_ldlt(gpu, N, kernel):
+    """The reduced-system LDLT kernels (8-wide panels for N < 128, the column-step kernel while the
+    packed factor fits LDS, the blocked FP64-MFMA one above; 'col' and 'blocked' force those two
+    wherever they fit) solve SPD Schur systems to FP64 accuracy."""
     import ctypes as C
     from orb_slam2_commit_amd import _lib
     rng = np.random.default_rng(N)
@@ -326,18 +328,15 @@ def test_gpu_reduced_system_ldlt(gpu, N, kernel, monkeypatch):
     b = rng.normal(size=N)
     x = np.zeros(N)
     ms = C.c_float(0)
-    assert _lib.lib().orbx_debug_ldlt(_lib.ptr(S), _lib.ptr(b), N, _lib.ptr(x), 1, C.byref(ms)) == 0
+    assert _lib.lib().orbx_debug_ldlt_ex(_lib.ptr(S), _lib.ptr(b), N, _lib.ptr(x), 1, C.byref(ms),
+                                         LDLT_KIND[kernel], None) == 0
     ref = np.linalg.solve(S, b)
     assert np.abs(x - ref).max() <= 1e-10 * max(1.0, np.abs(ref).max())
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["default", "col", "mfma_blk"])
-def test_gpu_reduced_system_ldlt_zero_pivot(gpu, kernel, monkeypatch):
-    if kernel == "mfma_blk":
-        monkeypatch.setenv("ORBX_LDLT_BLK", "1")
-    if kernel == "col":
-        monkeypatch.setenv("ORBX_LDLT_COL", "1")
+@pytest.mark.parametrize("kernel", ["default", "col", "blocked"])
+def test_gpu_reduced_system_ldlt_zero_pivot(gpu, kernel):
     import ctypes as C
     from orb_slam2_commit_amd import _lib
     N = 12
@@ -345,20 +344,21 @@ def test_gpu_reduced_system_ldlt_zero_pivot(gpu, kernel, monkeypatch):
     S[5, 5] = 0.0  # exact zero pivot: the solve reports failure (LM then raises lambda)
     x = np.zeros(N)
     ms = C.c_float(0)
-    rc = _lib.lib().orbx_debug_ldlt(_lib.ptr(S), _lib.ptr(np.ones(N)), N, _lib.ptr(x), 1, C.byref(ms))
+    rc = _lib.lib().orbx_debug_ldlt_ex(_lib.ptr(S), _lib.ptr(np.ones(N)), N, _lib.ptr(x), 1, C.byref(ms),
+                                       LDLT_KIND[kernel], None)
     assert rc == _lib.ORBX_ERR_STATE if hasattr(_lib, "ORBX_ERR_STATE") else rc == -6
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["config4", "rejects"])
-def test_gpu_localba_fused_point_side_bit_identical(ba, case, monkeypatch):
+def test_gpu_localba_fused_point_side_bit_identical(ba, case):
     """The fused point side of iteration-start trials (k_ba_lin_schur: linearisation, point sums,
     D^-1 and B D^-1 in one kernel) gives the same bits, iterations and trials as the three
-    separate kernels (ORBX_BA_NO_FUSE=1)."""
+    separate kernels (debug option no_fuse)."""
     P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(sorted(REJECT_CASES)[0])
     a = ba.LocalBundleAdjustment(P)
-    monkeypatch.setenv("ORBX_BA_NO_FUSE", "1")
-    b = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(no_fuse=1):
+        b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw_d", "Xw_d", "edge_outlier"):
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
     assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
@@ -366,16 +366,16 @@ def test_gpu_localba_fused_point_side_bit_identical(ba, case, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["config4", "rejects"])
-@pytest.mark.parametrize("switch", ["ORBX_BA_NO_CAMFOLD", "ORBX_BA_NO_PSFOLD"])
-def test_gpu_localba_trial_folds_bit_identical(ba, case, switch, monkeypatch):
+@pytest.mark.parametrize("switch", ["no_camfold", "no_psfold"])
+def test_gpu_localba_trial_folds_bit_identical(ba, case, switch):
     """Device-LM trials sum the pose terms inside k_ba_pairs and finish Hpp / b_p inside
     k_ba_schur_fin (no k_ba_cam_sum / k_ba_cam_fin launches), and k_ba_lin_schur also does the
     point side of trials that do not relinearise (no k_ba_point_schur launch): same bits,
-    iterations and trials as with the separate kernels (ORBX_BA_NO_CAMFOLD=1 / ORBX_BA_NO_PSFOLD=1)."""
+    iterations and trials as with the separate kernels (debug options no_camfold / no_psfold)."""
     P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(sorted(REJECT_CASES)[0])
     a = ba.LocalBundleAdjustment(P)
-    monkeypatch.setenv(switch, "1")
-    b = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(**{switch: 1}):
+        b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw_d", "Xw_d", "edge_outlier"):
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
     assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
@@ -383,10 +383,10 @@ def test_gpu_localba_trial_folds_bit_identical(ba, case, switch, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["config4", "many_kfs"] + sorted(REJECT_CASES))
-def test_gpu_localba_device_lm_bit_identical(ba, case, monkeypatch):
+def test_gpu_localba_device_lm_bit_identical(ba, case):
     """LM control on the device (k_ba_lm_control: accept/reject, lambda, the trial budget,
     rho == 0 and _nBad, trials queued without a host round trip) gives the same bits,
-    iterations and trials as the host-controlled loop (ORBX_BA_HOST_LM=1)."""
+    iterations and trials as the host-controlled loop (debug option host_lm)."""
     if case == "config4":
         P = synth.localba_problem(seed=7)
     elif case == "many_kfs":
@@ -394,8 +394,8 @@ def test_gpu_localba_device_lm_bit_identical(ba, case, monkeypatch):
     else:
         P = reject_problem(case)
     a = ba.LocalBundleAdjustment(P)
-    monkeypatch.setenv("ORBX_BA_HOST_LM", "1")
-    b = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(host_lm=1):
+        b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw_d", "Xw_d", "edge_outlier"):
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
     assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
@@ -403,41 +403,32 @@ def test_gpu_localba_device_lm_bit_identical(ba, case, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_localba_stop_flag_mid_run(ba):
-    """A stop flag (caller memory, not the handle's pinned flag) raised by another thread while
-    the device runs the LM loop ends the optimisation early: the calling thread mirrors it into
-    the handle's pinned flag while it waits, and the device polls that.  The raise comes after
-    15 % of a full call's own measured duration, so the margin scales with the machine."""
-    import threading
-    import time
-    P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
-    ba.LocalBundleAdjustment(P)
-    t0 = time.perf_counter()
-    full = ba.LocalBundleAdjustment(P)
-    delay = 0.15 * (time.perf_counter() - t0)
-    flag = np.zeros(1, np.int32)
-    t = threading.Thread(target=lambda: (time.sleep(delay), flag.__setitem__(0, 1)))
-    t.start()
+def test_gpu_localba_stop_flag_caller_memory(ba):
+    """A stop flag in caller memory (not the handle's pinned flag) is honoured: raised before the
+    call it leaves the problem untouched (src/Optimizer.cc:749-751); the mid-run raise is covered
+    deterministically by the raise_stop_after hook below, which the device reads in place of the flag."""
+    P = small_problem(seed=9)
+    flag = np.ones(1, np.int32)
     r = ba.LocalBundleAdjustment(P, stop=flag)
-    t.join()
-    assert flag[0] == 1
-    assert sum(r["iterations"]) < sum(full["iterations"])
-    assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
+    assert list(r["iterations"]) == [0, 0] and r["trials"] == 0
+    np.testing.assert_array_equal(r["Tcw"], np.asarray(P["Tcw"], np.float32).reshape(-1, 12))
+    flag[0] = 0
+    _compare(ba.LocalBundleAdjustment(P, stop=flag), oracle.local_ba(P))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("after", [0, 2, 4])  # inside the first phase (optimize(5))
-def test_gpu_localba_stop_raised_after_trials(ba, after, monkeypatch):
-    """Deterministic mid-run stop: ORBX_BA_RAISE_STOP_AFTER=n makes the device LM control see a
+def test_gpu_localba_stop_raised_after_trials(ba, after):
+    """Deterministic mid-run stop: the raise_stop_after = n debug option makes the device LM control see a
     raised flag from trial n of the first phase on (as a flag raised by LocalMapping::InterruptBA
     between two trials).  The phase ends at that iteration, the second phase is skipped, and the
     result is the same bit for bit on every run and through the batched driver."""
     P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
     full = ba.LocalBundleAdjustment(P)
-    monkeypatch.setenv("ORBX_BA_RAISE_STOP_AFTER", str(after))
-    r = ba.LocalBundleAdjustment(P)
-    r2 = ba.LocalBundleAdjustment(P)
-    many = ba.LocalBundleAdjustmentMany([P, P])
+    with ba.debug_options(raise_stop_after=after):
+        r = ba.LocalBundleAdjustment(P)
+        r2 = ba.LocalBundleAdjustment(P)
+        many = ba.LocalBundleAdjustmentMany([P, P])
     assert r["iterations"][1] == 0 and 1 <= r["iterations"][0] <= after + 1
     assert r["trials"] >= after + 1 and sum(r["iterations"]) < sum(full["iterations"])
     for o in (r2, many[0], many[1]):
@@ -465,18 +456,19 @@ def test_oracle_nan_trial_refresh(trial, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case,trial", [("config4", 0), ("config4", 1), ("config4", 3), ("rejects_b", 2)])
 def test_gpu_localba_nan_trial(ba, case, trial, monkeypatch):
-    """A trial whose chi is NaN (ORBX_BA_NAN_TRIAL) is rejected and, with rho NaN, ends its
+    """A trial whose chi is NaN (debug option nan_trial; ORBX_BA_NAN_TRIAL for the oracle) is rejected and, with rho NaN, ends its
     iteration while the phase goes on: g2o pops it and the next iteration recomputes the errors
     at the restored state before linearising.  The device LM loop pauses the phase for exactly
     that (restore, errors, k_ba_lm_resume): GPU = oracle (1e-4, identical counts and outliers),
-    device loop = host loop (ORBX_BA_HOST_LM=1) bit for bit, batched = single bit for bit."""
+    device loop = host loop (debug option host_lm) bit for bit, batched = single bit for bit."""
     P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(case)
-    monkeypatch.setenv("ORBX_BA_NAN_TRIAL", str(trial))
-    a = ba.LocalBundleAdjustment(P)
+    monkeypatch.setenv("ORBX_BA_NAN_TRIAL", str(trial))  # the oracle's hook (test infrastructure)
+    with ba.debug_options(nan_trial=trial):
+        a = ba.LocalBundleAdjustment(P)
+        many = ba.LocalBundleAdjustmentMany([P, small_problem(seed=12)])
     _compare(a, oracle.local_ba(P))
-    many = ba.LocalBundleAdjustmentMany([P, small_problem(seed=12)])
-    monkeypatch.setenv("ORBX_BA_HOST_LM", "1")
-    b = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(nan_trial=trial, host_lm=1):
+        b = ba.LocalBundleAdjustment(P)
     for o in (b, many[0]):
         for k in ("Tcw_d", "Xw_d", "edge_outlier"):
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(o[k]))
@@ -515,8 +507,6 @@ def test_gpu_localba_batched_bit_identical(ba):
 def test_gpu_localba_batched_fallback_and_stop(ba):
     """A batch holding a problem whose edges are not grouped by point (host structure build)
     runs one by one with the same results; a stop flag raised mid-run ends the batched loop."""
-    import threading
-    import time
     P1 = synth.localba_problem(seed=7)
     P2 = dict(small_problem(seed=11))
     perm = np.random.default_rng(0).permutation(len(P2["edge_point"]))
@@ -529,16 +519,11 @@ def test_gpu_localba_batched_fallback_and_stop(ba):
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
         assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
     probs = [synth.localba_problem(seed=8 + k, n_local=30, n_fixed=4, n_points=4000) for k in range(4)]
-    t0 = time.perf_counter()
     full = ba.LocalBundleAdjustmentMany(probs)
-    delay = 0.15 * (time.perf_counter() - t0)  # margin scaled by the call's own duration
-    flag = ba._stop
-    t = threading.Thread(target=lambda: (time.sleep(delay), flag.__setitem__(0, 1)))
-    t.start()
-    # the wrapper writes the handle flag (0) before the call; the thread raises it mid-run
-    rs = ba.LocalBundleAdjustmentMany(probs)
-    t.join()
-    flag[0] = 0
+    with ba.debug_options(raise_stop_after=3):  # the flag reads raised from the batch's 4th trial on
+        rs = ba.LocalBundleAdjustmentMany(probs)
     assert sum(sum(r["iterations"]) for r in rs) < sum(sum(r["iterations"]) for r in full)
+    for r in rs:
+        assert r["iterations"][1] == 0
     for r in rs:
         assert np.isfinite(r["Tcw_d"]).all() and np.isfinite(r["Xw_d"]).all()
