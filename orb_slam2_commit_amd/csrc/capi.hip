@@ -27,6 +27,8 @@
 
 namespace orbx {
 hipError_t upload_constants(const int* umax16, const int* gauss7);
+hipError_t launch_blur(const Geometry& Gh, const Geometry* Gd, const int* tile_level, const BatchPtrs& B, int n_img,
+                       hipStream_t st);
 hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells, const int* tile_level,
                                  const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B, int n_img,
                                  orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t st,
@@ -459,7 +461,6 @@ orbx_status ensure_batch(orbx_extractor* h, const Plan& P, int n) {
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
   chk(h->pyr.ensure((size_t)G.pyr_bytes * n + 256));
-  chk(h->blur.ensure((size_t)G.blur_bytes * n + 256));
   chk(h->cand.ensure((size_t)G.cand_total * n));
   chk(h->kpos.ensure((size_t)G.cand_total * n));
   chk(h->knode.ensure((size_t)G.cand_total * n));
@@ -949,6 +950,13 @@ extern "C" long long orbx_debug_copy(orbx_extractor* h, int what, int image, int
       const LevelGeom& L = G.lv[arg];
       bytes = (size_t)L.w * L.h;
       if (dst && cap >= bytes) {
+        // the extraction blurs only each keypoint's patch (k_describe); the whole blurred levels of
+        // the last batch are made here, on demand, from its pyramid
+        if (h->blur.ensure((size_t)G.blur_bytes * h->last_n + 256) != hipSuccess) return ORBX_ERR_HIP;
+        const BatchPtrs B = batch_ptrs(h, h->last_in, h->last_pitch);
+        if (launch_blur(G, P.dG.p, P.dtiles.p, B, h->last_n, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+          return ORBX_ERR_HIP;
         const uint8_t* b = h->blur.p + (size_t)image * G.blur_bytes + L.boff;
         if (hipMemcpy2D(dst, L.w, b, L.bstride, L.w, L.h, hipMemcpyDeviceToHost) != hipSuccess) return ORBX_ERR_HIP;
       }

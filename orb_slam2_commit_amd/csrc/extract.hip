@@ -4,14 +4,17 @@
 //
 //   k_resize   x(nlevels-1)  ComputePyramid            src/ORBextractor.cc:1215-1250
 //   k_fast                   per-cell FAST + fallback  src/ORBextractor.cc:843-915
-//   k_blur                   GaussianBlur 7x7 s=2      src/ORBextractor.cc:1186-1190
 //   k_octree                 DistributeOctTree         src/ORBextractor.cc:562-815
-//   k_describe               IC_Angle + rBRIEF + scale src/ORBextractor.cc:77-152,1192-1207
+//   k_describe               IC_Angle + patch GaussianBlur 7x7 s=2 + rBRIEF + scale
+//                                                      src/ORBextractor.cc:77-152,1186-1207
+//   (k_blur                  whole-level GaussianBlur, debug only: ORBX_DBG_BLUR_LEVEL)
 //
 // Integer/byte work throughout (HBM-bound); the only float math is the
 // orientation/rotation and it is compiled without FP contraction so it rounds
 // exactly like the CPU path.
 #include <hip/hip_runtime.h>
+
+#include <utility>
 
 #include "orbx_device.h"
 #include "orbx_internal.h"
@@ -42,6 +45,9 @@ __constant__ double c_sincos[23] = {
 
 
 constexpr int BS = 256;
+
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------- block scan
 // Exclusive scan of a[0..n) in LDS (in place); returns the total. All NT threads call.
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, c
 // GaussianBlur(7x7, sigma=2, BORDER_REFLECT_101), OpenCV 3.2 8U fixed point:
 // integer kernel {k0..k6} (x256), exact integer row+column sums, then
 // rint(acc/65536) on SIMD column groups (x < w&~3) and (acc+2^15)>>16 on the
-// scalar tail; saturate to u8.  128x128 output tile per block, staged in LDS.
+// scalar tail; saturate to u8 (the integer kernel {18,34,49,55,49,34,18} sums to 257).  128x128 output tile per block, staged in LDS.
 __constant__ int c_gauss[7];
 
 __device__ __forceinline__ int reflect101(int p, int n) {
@@ -279,9 +285,11 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 // the <= 3 reflected columns each side are patched from LDS afterwards).
 // Thread = 4 columns x a 16-row strip: row sums (byte dot products) go into a
 // 7-row register window that slides down the strip; the column taps are exact
-// f32 FMAs on the row sums with the weights pre-scaled by 2^-16 (every partial
-// sum is an integer multiple of 2^-16 below 2^8, exact in f32), so
-// v_rndne_f32 is rint(acc/65536) and v_cvt_pk_u8_f32 packs the byte.
+// packed-f32 FMAs on the row sums with the weights pre-scaled by 2^-16 (every
+// partial sum is an integer multiple of 2^-16 below 2^8, exact in f32), rounded
+// by the 1.5*2^23 add and packed by byte permutes: ~10 VALU per output (18.6
+// with per-column byte aligns, v_rndne / v_med3 / v_cvt_pk_u8 per output; the
+// kernel is VALU-issue-bound).
 constexpr int kBIn = kBlurTileW + 16;  // input tile row stride (bytes, 16-B multiple)
 constexpr int kBStrip = 16;            // output rows per thread
 __global__ __launch_bounds__(BS, 8) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
@@ -368,63 +376,89 @@ __global__ __launch_bounds__(BS, 8) void k_blur(const Geometry* __restrict__ G, 
   const int ys = (tid / (kBlurTileW / 4)) * kBStrip;  // strip's first output row in the tile
   const int xg = x0 + 4 * g;
   if (xg >= w || y0 + ys >= h) return;
-  const int k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
-  // horizontal taps as byte dot products (exact integers, weights < 256):
-  // output col j of the group needs tile bytes j+1..j+7 of the 12 bytes
-  // [a b c]; lo = bytes j+1..j+4 (k0 k1 k2 k3), hi = bytes j+5..j+8 (k2 k1 k0 0)
-  const uint32_t wlo = (uint32_t)k0 | (uint32_t)k1 << 8 | (uint32_t)k2 << 16 | (uint32_t)k3 << 24;
-  const uint32_t whi = (uint32_t)k2 | (uint32_t)k1 << 8 | (uint32_t)k0 << 16;
+  const uint32_t k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
+  // horizontal taps as byte dot products (exact integers, weights < 256) straight on the three
+  // aligned dwords [a b c] = tile bytes 4g .. 4g+11: output col j of the group takes bytes
+  // j+1 .. j+7, i.e. ten v_dot4_u32_u8 with the taps pre-shifted into the word each byte sits in
+  // (no byte-align step).  The accumulator starts at 0x4B000000, so the sum comes out as the f32
+  // bits of 2^23 + s (s <= 257*255 < 2^23) and one packed subtract per two columns converts it.
+  auto W4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) { return b0 | b1 << 8 | b2 << 16 | b3 << 24; };
+  const uint32_t wa0 = W4(0, k0, k1, k2), wb0 = W4(k3, k2, k1, k0);
+  const uint32_t wa1 = W4(0, 0, k0, k1), wb1 = W4(k2, k3, k2, k1), wc1 = W4(k0, 0, 0, 0);
+  const uint32_t wa2 = W4(0, 0, 0, k0), wb2 = W4(k1, k2, k3, k2), wc2 = W4(k1, k0, 0, 0);
+  const uint32_t wb3 = W4(k0, k1, k2, k3), wc3 = W4(k2, k1, k0, 0);
   const float f0 = (float)k0 * (1.f / 65536.f), f1 = (float)k1 * (1.f / 65536.f), f2 = (float)k2 * (1.f / 65536.f),
               f3 = (float)k3 * (1.f / 65536.f);
-  // row sums (<= 257*255, exact in f32) of output cols xg..xg+3 on tile row ty
-  auto rowsum = [&](int ty, float (&o)[4]) {
+  const float2v F0 = {f0, f0}, F1 = {f1, f1}, F2 = {f2, f2}, F3 = {f3, f3};
+  const float2v two23 = {8388608.0f, 8388608.0f}, magic = {12582912.0f, 12582912.0f};
+  // row sums (<= 257*255, exact in f32) of output cols xg..xg+3 on tile row ty, as two f32 pairs
+  auto rowsum = [&](int ty, float2v (&o)[2]) {
     const uint32_t* r32 = (const uint32_t*)&tin[ty * kBIn + 4 * g];
     const uint32_t a = r32[0], b = r32[1], c = r32[2];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t lo = j < 3 ? __builtin_amdgcn_alignbyte(b, a, j + 1) : b;
-      const uint32_t hi = j < 3 ? __builtin_amdgcn_alignbyte(c, b, j + 1) : c;
-      o[j] = (float)__builtin_amdgcn_udot4(lo, wlo, __builtin_amdgcn_udot4(hi, whi, 0u, false), false);
-    }
+    constexpr uint32_t bias = 0x4B000000u;  // f32 2^23
+    const uint32_t s0 = __builtin_amdgcn_udot4(b, wb0, __builtin_amdgcn_udot4(a, wa0, bias, false), false);
+    const uint32_t s1 = __builtin_amdgcn_udot4(
+        c, wc1, __builtin_amdgcn_udot4(b, wb1, __builtin_amdgcn_udot4(a, wa1, bias, false), false), false);
+    const uint32_t s2 = __builtin_amdgcn_udot4(
+        c, wc2, __builtin_amdgcn_udot4(b, wb2, __builtin_amdgcn_udot4(a, wa2, bias, false), false), false);
+    const uint32_t s3 = __builtin_amdgcn_udot4(c, wc3, __builtin_amdgcn_udot4(b, wb3, bias, false), false);
+    o[0] = (float2v){__uint_as_float(s0), __uint_as_float(s1)} - two23;
+    o[1] = (float2v){__uint_as_float(s2), __uint_as_float(s3)} - two23;
   };
-  float win[7][4];
+  // 7-row ring indexed by compile-time (r + i) % 7 in the unrolled loop: no register moves
+  float2v win[7][2];
 #pragma unroll
   for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
   const int simd_w = w & ~3;
   const bool all_simd = xg + 3 < simd_w;  // the whole group takes the SSE2 rounding
+  const bool full = xg + 4 <= w;
+  // stores through a buffer resource over the level's blurred rows: rows past h fall outside
+  // num_records and are dropped; the row step is a scalar offset
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, h * bs, 0x00020000);
+  const uint32_t voff = (uint32_t)((y0 + ys) * bs + xg);
 #pragma unroll
   for (int r = 0; r < kBStrip; r++) {
-    rowsum(ys + r + 6, win[6]);
-    const int y = y0 + ys + r;
-    if (y < h) {
-      uint32_t packed = 0;
+    rowsum(ys + r + 6, win[(r + 6) % 7]);
+    // column taps on packed f32 pairs, each element exactly the scalar chain
+    // fma(f3, w3, fma(f2, w2+w4, fma(f1, w1+w5, f0*(w0+w6)))) = acc / 2^16 (integer sums below
+    // 2^24 scaled by a power of two); + 1.5*2^23 rounds it half-to-even (the SSE2 groups'
+    // rint), leaving the integer in the low bits
+    float2v acc[2];
+    uint32_t rb[4];
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+      const float2v w0 = win[r % 7][hh], w1 = win[(r + 1) % 7][hh], w2 = win[(r + 2) % 7][hh],
+                    w3 = win[(r + 3) % 7][hh], w4 = win[(r + 4) % 7][hh], w5 = win[(r + 5) % 7][hh],
+                    w6 = win[(r + 6) % 7][hh];
+      acc[hh] = __builtin_elementwise_fma(
+          F3, w3, __builtin_elementwise_fma(F2, w2 + w4, __builtin_elementwise_fma(F1, w1 + w5, F0 * (w0 + w6))));
+      const float2v rr = acc[hh] + magic;
+      rb[2 * hh] = __float_as_uint(rr.x);
+      rb[2 * hh + 1] = __float_as_uint(rr.y);
+    }
+    // low halves as u16 pairs, saturated to 255 (the kernel sums to 257), then the low bytes
+    u16x2 p01 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(rb[1], rb[0], 0x05040100u));
+    u16x2 p23 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(rb[3], rb[2], 0x05040100u));
+    const u16x2 cap = {255, 255};
+    p01 = __builtin_elementwise_min(p01, cap);
+    p23 = __builtin_elementwise_min(p23, cap);
+    uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01), 0x06040200u);
+    if (!all_simd) {
+      // the row's scalar tail (x >= w & ~3): (acc + 2^15) >> 16
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        // acc / 2^16 exactly (integer sums below 2^24 scaled by a power of two)
-        const float acc = __builtin_fmaf(f3, win[3][j],
-                                         __builtin_fmaf(f2, win[2][j] + win[4][j],
-                                                        __builtin_fmaf(f1, win[1][j] + win[5][j],
-                                                                       f0 * (win[0][j] + win[6][j]))));
-        float v;
-        if (all_simd || xg + j < simd_w) {
-          v = __builtin_rintf(acc);  // SSE2 groups: rint(acc / 2^16), ties to even
-        } else {
-          const int ai = (int)(acc * 65536.f);  // scalar tail: (acc + 2^15) >> 16
-          v = (float)((ai + (1 << 15)) >> 16);
+        if (xg + j >= simd_w) {
+          const float aj = j == 0 ? acc[0].x : j == 1 ? acc[0].y : j == 2 ? acc[1].x : acc[1].y;
+          const int v = min(((int)(aj * 65536.f) + (1 << 15)) >> 16, 255);
+          packed = (packed & ~(0xFFu << (8 * j))) | ((uint32_t)v << (8 * j));
         }
-        packed = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(v, 0.f, 255.f), j, packed);
-      }
-      uint8_t* d = dst + (size_t)y * bs + xg;
-      if (xg + 4 <= w) {
-        *(uint32_t*)d = packed;
-      } else {
-        for (int j = 0; j < w - xg; j++) d[j] = (uint8_t)(packed >> (8 * j));
       }
     }
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) win[i][j] = win[i + 1][j];
+    if (full) {
+      __builtin_amdgcn_raw_buffer_store_b32(packed, rd, voff, r * bs, 0);
+    } else {
+      for (int j = 0; j < w - xg; j++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(packed >> (8 * j)), rd, voff + j, r * bs, 0);
+    }
   }
 }
 
@@ -1205,169 +1239,327 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
          __builtin_amdgcn_readlane(v, 63);
 }
 
-typedef float float2v __attribute__((ext_vector_type(2)));
 
-// describe's staged blurred patch: rotated bit_pattern_31_ points stay within
-// radius 18.39, so |row|, |col| <= 18 after cvRound
+// describe's blurred patch: rotated bit_pattern_31_ points stay within radius 18.39, so
+// |row|, |col| <= 18 after cvRound: a 37 x 37 patch around the keypoint
 constexpr int kPatchR = 18;
-constexpr int kPatchRows = 2 * kPatchR + 1;            // 37
-constexpr int kPatchCh = 4;  // 16-B chunks per staged row: 16-aligned start, 37 bytes + up to 15 of slack
-constexpr int kPatchRowCh = 5;  // LDS row stride in chunks: 80 B = 20 dwords, so the rotated samples'
-                                // rows spread over the banks (a 64-B stride folds every 4th row together)
-constexpr int kPatchIt = (kPatchRows * kPatchCh + 63) / 64;
+constexpr int kPatchRows = 2 * kPatchR + 1;  // 37
+constexpr int kPS = 80;  // LDS row stride of the staged patches (bytes): 20 dwords, so the rotated
+                         // samples' rows spread over the banks (a 64-B stride folds every 4th row)
+// the raw patch the blur of that patch reads: rows y-21..y+21, 16-B chunks from the 16-aligned
+// column xs = (x - 21) & ~15 (x - 21 - xs <= 15, + 43 bytes <= 58: four chunks per row)
+constexpr int kRawR = kPatchR + 3;           // 21
+constexpr int kRawRows = 2 * kRawR + 1;      // 43
+constexpr int kRawCh = 4;
+constexpr int kRawIt = (kRawRows * kRawCh + 63) / 64;  // 3 chunks per lane
+constexpr int kDescLds = (kRawRows + kPatchRows) * kPS + 256;  // bytes per wave (+ descriptor words)
+// blur work split: lane = (column pair g < 19, row strip s < 3 of 13 / 13 / 11 output rows)
+constexpr int kBlurPairs = (kPatchRows + 1) / 2;  // 19
+constexpr int kBlurStrip = 13;
 
-// One wave per keypoint: IC_Angle on the raw level (src/ORBextractor.cc:77-105),
-// computeOrbDescriptor on the blurred level (:110-152), then the keypoint
-// record in level-major output order with pt *= mvScaleFactor[l] (:1201-1207).
-// The keypoint index is wave-uniform (readfirstlane), so the level lookup and
-// the octree entry are scalar loads and every image access is a uniform base
-// plus a 32-bit lane offset.
+constexpr int kDescK = 8;  // keypoints per wave
+static_assert(kDescK * 8 <= 64, "one descriptor dword per lane");
+
+// f(std::integral_constant<int, 0>{}) ... f(<N-1>): compile-time lane indices in an unrolled loop
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+__device__ __forceinline__ const uint8_t* lane_ptr(const uint8_t* p, int j) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)a, j), hi = __builtin_amdgcn_readlane((uint32_t)(a >> 32), j);
+  return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float lane_f(float v, int j) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+}
+
+// k_describe: IC_Angle (src/ORBextractor.cc:77-105), the level's GaussianBlur (:1186-1190)
+// restricted to each keypoint's 37 x 37 sampling patch, computeOrbDescriptor (:110-152) and the
+// keypoint record in level-major output order with pt *= mvScaleFactor[l] (:1201-1207).
+//
+// The blurred level is never materialised: every blurred pixel the 256 rotated pairs can touch
+// lies in the patch, and GaussianBlur's output at a pixel depends only on the 7 x 7 raw pixels
+// around it (REFLECT_101 at the level border), so blurring the 43 x 43 raw neighbourhood in LDS
+// gives the same bytes as blurring the level and reading them back -- without the level-sized
+// write and the two level-sized reads (1.5 + 0.7 GB per 256-frame step).
+//
+// kDescK keypoints per wave (consecutive output indices):
+//   1. lane j finds keypoint i0 + j's level and loads its octree entry and level record;
+//   2. the IC_Angle boxes of all kDescK keypoints and the raw patches of the first two are issued
+//      together; the moments are wave sums per keypoint (v_dot4 on circle-masked 16-B rows);
+//   3. fastAtan2 and the deterministic sin/cos run once, lane j for keypoint j;
+//   4. per keypoint: raw patch -> LDS (reflected border columns patched), the patch two ahead
+//      issued, the 37 x 37 blur (exact integer row sums by v_dot4, packed-f32 column taps, the
+//      SSE2 / scalar-tail rounding of the output column) -> LDS, then the 256 rotated pairs with
+//      pair p in lane p & 63: ballot k = descriptor bits 64k .. 64k+63, staged in LDS;
+//   5. one coalesced store of the kDescK descriptors (lane = dword) and the keypoint records.
 __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                  int32_t* __restrict__ counts, int kp_cap) {
-  // rBRIEF pattern as floats, once per block; each wave's 37 x 37 blurred patch
-  // (rows y-18..y+18, 16-aligned columns from (x-18) & ~15) staged with
-  // 16-B buffer loads, so the 512 rotated samples are LDS gathers rather
-  // than ~30 cache lines per global gather instruction
-  __shared__ float4 s_pat[256];
-  __shared__ uint4 s_patch[BS / 64][kPatchRows * kPatchRowCh];
+  __shared__ __align__(16) uint8_t s_desc[BS / 64][kDescLds];
   const int2 bi = xcd_block2();
   const int img = bi.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // the pattern's load is issued beside the level counts' and staged after them, so the block's
-  // barrier waits for both round trips at once (it used to wait for the pattern alone first)
-  const float4 patv = reinterpret_cast<const float4*>(c_pattern_f)[threadIdx.x];
-  const int i = __builtin_amdgcn_readfirstlane(bi.x * (BS / 64) + wv);
+  const int i0 = __builtin_amdgcn_readfirstlane((bi.x * (BS / 64) + wv) * kDescK);
   const int nl = G->nlevels;
-  // level of keypoint i: per-level counts as independent scalar loads, then an
-  // unrolled scan in scalar registers (no dependent load chain, no indexing)
+  // per-level counts as independent scalar loads
   const int* oc = B.oct_count + (size_t)img * nl;
   int cnt[kMaxLevelsPlan];
 #pragma unroll
   for (int ll = 0; ll < kMaxLevelsPlan; ll++) cnt[ll] = ll < nl ? oc[ll] : 0;
-  int total = 0, l = 0, first = 0;
+  int total = 0;
+#pragma unroll
+  for (int ll = 0; ll < kMaxLevelsPlan; ll++) total += cnt[ll];
+  if (bi.x == 0 && threadIdx.x == 0) counts[img] = total;
+  // the rBRIEF pairs of this lane (p = lane + 64k), reused for every keypoint of the wave
+  float4 pat[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) pat[k] = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * k];
+  if (i0 >= total) return;  // wave-uniform: the DPP sums below see a full wave
+  const int nk = min(kDescK, total - i0);
+  // 1. lane j: keypoint i0 + min(j, nk - 1) (lanes past nk repeat the last one; never written)
+  const int i = i0 + min(lane, nk - 1);
+  int l = 0, first = 0, acc = 0;
 #pragma unroll
   for (int ll = 0; ll < kMaxLevelsPlan; ll++) {
-    if (i >= total) {  // last level whose start is <= i
+    if (i >= acc) {  // last level whose start is <= i
       l = ll;
-      first = total;
+      first = acc;
     }
-    total += cnt[ll];
+    acc += cnt[ll];
   }
-  if (bi.x == 0 && threadIdx.x == 0) counts[img] = total;
-  s_pat[threadIdx.x] = patv;
-  __syncthreads();
-  if (i >= total) return;  // wave-uniform: the DPP sums below see a full wave
   const LevelGeom& L = G->lv[l];
   const uint32_t v = B.oct[(size_t)img * G->oct_total + L.oct_off + (i - first)];
+  const int w = L.w, h = L.h;
+  const float lscale = L.scale, lsize = L.kp_size;
   const int x = v & 0xFFF, y = (v >> 12) & 0xFFF, score = v >> 24;
-  const int w = L.w;
-  const uint8_t* blur = B.blur + (size_t)img * G->blur_bytes + L.boff;  // uniform
-  const int bs = L.bstride;
-  const int x0 = (x - kPatchR) & ~15;  // x - 18 >= 1: keypoints sit >= 19 px inside the level
-  // 16-B chunks from a 16-aligned column: with the 16-byte row stride a chunk is wholly inside
-  // its row or wholly past the row's end (and, in the last row, past num_records: zeros)
-  uint32_t pv[kPatchIt][4];
-  {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(blur + (size_t)(y - kPatchR) * bs + x0), (short)0, kPatchRows * bs, 0x00020000);
+  const uint8_t* lvl = level_ptr(*G, B, img, l);
+  // IC box origin (x - 15, y - 15); keypoints sit >= 19 px inside the level, so the box is too
+  const uint8_t* icp = lvl + (size_t)(y - 15) * w + (x - 15);
+
+  // 2. IC boxes of every keypoint, then the first two raw patches
+  const int r = lane >> 1, hh = lane & 1;
+  uint32_t q[kDescK][4];
 #pragma unroll
-    for (int k = 0; k < kPatchIt; k++) {
-      const int q = lane + 64 * k, r = q >> 2, j = q & 3;
-      const uint32_t off = q < kPatchRows * kPatchCh ? (uint32_t)(r * bs + 16 * j) : 0x80000000u;
-      const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-      pv[k][0] = v4[0];
-      pv[k][1] = v4[1];
-      pv[k][2] = v4[2];
-      pv[k][3] = v4[3];
+  for (int j = 0; j < kDescK; j++) {
+    const int wj = __builtin_amdgcn_readlane(w, j);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)lane_ptr(icp, j), (short)0, 31 * wj, 0x00020000);
+    const uint32_t off = lane < 62 ? (uint32_t)(r * wj + 16 * hh) : 0x80000000u;
+    const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    q[j][0] = t[0];
+    q[j][1] = t[1];
+    q[j][2] = t[2];
+    q[j][3] = t[3];
+  }
+  // raw patch of keypoint j: lane chunk c = lane + 64k is (row c >> 2, 16-B column block c & 3);
+  // rows reflected (REFLECT_101), columns outside the level patched in LDS afterwards
+  uint32_t pv[2][kRawIt][4];
+  auto load_patch = [&](int j, uint32_t (&dst)[kRawIt][4]) {
+    const int wj = __builtin_amdgcn_readlane(w, j), hj = __builtin_amdgcn_readlane(h, j);
+    const int xj = __builtin_amdgcn_readlane(x, j), yj = __builtin_amdgcn_readlane(y, j);
+    const int xs = (xj - kRawR) & ~15;
+    const int nrec = wj * hj;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)lane_ptr(lvl, j), (short)0, nrec, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < kRawIt; k++) {
+      const int c = lane + 64 * k, rr = c >> 2, cc = c & 3;
+      const int o = reflect101(yj - kRawR + rr, hj) * wj + xs + 16 * cc;  // may be < 0 in row 0
+      dst[k][0] = dst[k][1] = dst[k][2] = dst[k][3] = 0;
+      if (c < kRawRows * kRawCh) {
+        if (o + 16 <= nrec) {  // o < 0 wraps past num_records: zeros (only reflected columns)
+          const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)o, 0, 0);
+          dst[k][0] = t[0];
+          dst[k][1] = t[1];
+          dst[k][2] = t[2];
+          dst[k][3] = t[3];
+        } else {
+          // a chunk straddling the level's last byte: byte loads, each range-checked on its own
+#pragma unroll
+          for (int b = 0; b < 16; b++)
+            dst[k][b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(o + b), 0, 0) << (8 * (b & 3));
+        }
+      }
     }
-  }
-  // IC_Angle (src/ORBextractor.cc:77-105) on the raw level
-  const uint8_t* raw = level_ptr(*G, B, img, l);
-  int m01 = 0, m10 = 0;
+  };
+  load_patch(0, pv[0]);
+  if (kDescK > 1) load_patch(1, pv[1]);
+  // moments: lane (r, hh) holds the 16 bytes at columns 16hh .. 16hh + 15 of box row r, masked to
+  // the circle; s0 = sum I, s1 = sum b * I, m01 = (r - 15) s0, m10 = s1 + (16hh - 15) s0 (integers:
+  // exact in any order).  Keypoint j's sums land in lane j.
+  int M01 = 0, M10 = 0;
   {
-    // lane (r, h) takes the 16 bytes at columns 16h .. 16h + 15 of box row r (x - 15 ..,
-    // y - 15 ..) with ONE unaligned 16-B buffer load (the box is always inside the level),
-    // masks them to the circle and sums by v_dot4_u32_u8: s0 = sum I, s1 = sum b * I.  Then
-    // m01 = v * s0 and m10 = sum (16h + b - 15) I = s1 + (16h - 15) s0 (integers: exact in any order)
-    const int r = lane >> 1, h = lane & 1;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(raw + (size_t)(y - 15) * w + (x - 15)), (short)0, 31 * w, 0x00020000);
-    const uint32_t off = lane < 62 ? (uint32_t)(r * w + 16 * h) : 0x80000000u;
-    const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
     const uint4 mk = c_icmask[lane];
-    const uint32_t I0 = q[0] & mk.x, I1 = q[1] & mk.y, I2 = q[2] & mk.z, I3 = q[3] & mk.w;
-    uint32_t s0 = __builtin_amdgcn_udot4(I0, 0x01010101u, 0u, false);
-    s0 = __builtin_amdgcn_udot4(I1, 0x01010101u, s0, false);
-    s0 = __builtin_amdgcn_udot4(I2, 0x01010101u, s0, false);
-    s0 = __builtin_amdgcn_udot4(I3, 0x01010101u, s0, false);
-    uint32_t s1 = __builtin_amdgcn_udot4(I0, 0x03020100u, 0u, false);
-    s1 = __builtin_amdgcn_udot4(I1, 0x07060504u, s1, false);
-    s1 = __builtin_amdgcn_udot4(I2, 0x0B0A0908u, s1, false);
-    s1 = __builtin_amdgcn_udot4(I3, 0x0F0E0D0Cu, s1, false);
-    m01 = (r - 15) * (int)s0;
-    m10 = (int)s1 + (16 * h - 15) * (int)s0;
+    static_for<kDescK>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const uint32_t I0 = q[j][0] & mk.x, I1 = q[j][1] & mk.y, I2 = q[j][2] & mk.z, I3 = q[j][3] & mk.w;
+      uint32_t s0 = __builtin_amdgcn_udot4(I0, 0x01010101u, 0u, false);
+      s0 = __builtin_amdgcn_udot4(I1, 0x01010101u, s0, false);
+      s0 = __builtin_amdgcn_udot4(I2, 0x01010101u, s0, false);
+      s0 = __builtin_amdgcn_udot4(I3, 0x01010101u, s0, false);
+      uint32_t s1 = __builtin_amdgcn_udot4(I0, 0x03020100u, 0u, false);
+      s1 = __builtin_amdgcn_udot4(I1, 0x07060504u, s1, false);
+      s1 = __builtin_amdgcn_udot4(I2, 0x0B0A0908u, s1, false);
+      s1 = __builtin_amdgcn_udot4(I3, 0x0F0E0D0Cu, s1, false);
+      const int m01 = wave_sum_dpp((r - 15) * (int)s0);
+      const int m10 = wave_sum_dpp((int)s1 + (16 * hh - 15) * (int)s0);
+      M01 = lane == j ? m01 : M01;
+      M10 = lane == j ? m10 : M10;
+    });
   }
-  m01 = wave_sum_dpp(m01);
-  m10 = wave_sum_dpp(m10);
-  const float angle = fast_atan2((float)m01, (float)m10);
+  // 3. orientation of keypoint j in lane j
+  const float angle = fast_atan2((float)M01, (float)M10);
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float sn, cs;
   sincos_det(angle * factorPI, c_sincos, &sn, &cs);
-  const float a = cs, b = sn;
+
+  // blur constants (see k_blur): taps pre-shifted into the dot4 words, 2^-16-scaled column taps
+  const uint32_t k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
+  auto W4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) { return b0 | b1 << 8 | b2 << 16 | b3 << 24; };
+  const uint32_t wl0 = W4(k0, k1, k2, k3), wh0 = W4(k2, k1, k0, 0);  // output col 2g: bytes sb .. sb+6
+  const uint32_t wl1 = W4(0, k0, k1, k2), wh1 = W4(k3, k2, k1, k0);  // output col 2g+1: bytes sb+1 .. sb+7
+  const float f0 = (float)k0 * (1.f / 65536.f), f1 = (float)k1 * (1.f / 65536.f), f2 = (float)k2 * (1.f / 65536.f),
+              f3 = (float)k3 * (1.f / 65536.f);
+  const float2v F0 = {f0, f0}, F1 = {f1, f1}, F2 = {f2, f2}, F3 = {f3, f3};
+  const float2v two23 = {8388608.0f, 8388608.0f}, magic = {12582912.0f, 12582912.0f};
+  const int bg = lane % kBlurPairs, bst = lane / kBlurPairs;  // column pair, row strip (lanes < 57)
+  const bool blur_lane = lane < 3 * kBlurPairs;
+
+  // 4. per keypoint
+  uint8_t* raw = s_desc[wv];
+  uint8_t* pb = s_desc[wv] + kRawRows * kPS;
+  constexpr uint32_t corr = (uint32_t)(kPatchR * kPS + kPatchR) - (0x400000u * (uint32_t)kPS + 0x4B400000u);
+  const float2v magic_s = {12582912.0f, 12582912.0f};
+  // the descriptors' 64-bit words, staged per wave and stored by lane = dword at the end
+  uint64_t* sdw = reinterpret_cast<uint64_t*>(s_desc[wv] + (kRawRows + kPatchRows) * kPS);
+  static_for<kDescK>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    if (j >= nk) return;  // wave-uniform
+    uint32_t (&cur)[kRawIt][4] = pv[j & 1];
+    const int wj = __builtin_amdgcn_readlane(w, j), xj = __builtin_amdgcn_readlane(x, j);
+    const int xs = (xj - kRawR) & ~15;
 #pragma unroll
-  for (int k = 0; k < kPatchIt; k++)
-    if (lane + 64 * k < kPatchRows * kPatchCh)
-      s_patch[wv][((lane + 64 * k) >> 2) * kPatchRowCh + ((lane + 64 * k) & 3)] = make_uint4(pv[k][0], pv[k][1], pv[k][2], pv[k][3]);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint8_t* patch = reinterpret_cast<const uint8_t*>(s_patch[wv]);
-  constexpr int PS = 16 * kPatchRowCh;  // patch row stride (bytes)
-  // Rotated pattern point (px, py) -> pixel (y + r, x + c) with
-  //   r = cvRound(px*b + py*a), c = cvRound(px*a - py*b)    (src/ORBextractor.cc:119-125)
-  // Both coordinates ride in packed-f32 lanes.  Each sum is rounded exactly as
-  // the scalar expression (products, then the add / subtract); adding 1.5*2^23
-  // rounds it to an integer half-to-even (|sum| < 2^22), leaving 0x4B400000 + r
-  // in the bits.  A 24-bit mad on the raw bits ((0x400000 + r) * bs, low 24 bits
-  // sign-extended) plus the uniform correction gives the 32-bit pixel offset.
-  const float2v ba = {b, a}, ab = {a, b}, magic = {12582912.0f, 12582912.0f};
-  const uint32_t corr = (uint32_t)(kPatchR * PS + (x - x0)) - (0x400000u * (uint32_t)PS + 0x4B400000u);
-  int bits = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int pair = lane * 4 + k;  // bit (pair & 7) of byte pair >> 3
-    const float4 pp = s_pat[pair];  // points 2*pair, 2*pair + 1
-    int t[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const float px = e ? pp.z : pp.x, py = e ? pp.w : pp.y;
-      const float2v P = (float2v){px, px} * ba;  // {px*b, px*a}
-      const float2v Q = (float2v){py, -py} * ab;  // {py*a, -(py*b)}: negation is exact
-      const float2v M = (P + Q) + magic;
-      const uint32_t mr = __float_as_uint(M.x), mc = __float_as_uint(M.y);
-      t[e] = patch[(uint32_t)__mul24((int)mr, PS) + mc + corr];
+    for (int k = 0; k < kRawIt; k++) {
+      const int c = lane + 64 * k;
+      if (c < kRawRows * kRawCh)
+        *(uint4*)(raw + (c >> 2) * kPS + 16 * (c & 3)) = make_uint4(cur[k][0], cur[k][1], cur[k][2], cur[k][3]);
     }
-    bits |= (t[0] < t[1]) << k;
-  }
-  const int other = __builtin_amdgcn_mov_dpp(bits, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]: lane ^ 1
-  uint8_t* d = desc + ((size_t)img * kp_cap + i) * 32;
-  if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(bits | (other << 4));
-  if (lane == 0) {
+    if (j + 2 < kDescK && j + 2 < nk) load_patch(j + 2, cur);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // columns outside the level (x - 21 < 0 or x + 21 >= w): REFLECT_101 copies of columns inside
+    // it (sources and targets disjoint, so one pass)
+    if (xj - kRawR < 0 || xj + kRawR >= wj) {
+      for (int e = lane; e < kRawRows * 4; e += 64) {
+        const int rr = e >> 2, k = e & 3;
+        const int col = k < 2 ? xj - kRawR + k : xj + kRawR - 1 + (k - 2);  // two per side
+        if (col < 0 || col >= wj) raw[rr * kPS + col - xs] = raw[rr * kPS + reflect101(col, wj) - xs];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // the 37 x 37 blur: output (row ro, col cc) = level pixel (y - 18 + ro, x - 18 + cc), taps on
+    // raw rows ro .. ro+6 and raw bytes o + cc .. o + cc + 6 (o = x - 21 - xs)
+    if (blur_lane) {
+      const int o = xj - kRawR - xs;
+      const int sb = o + 2 * bg, sh = sb & 3;
+      const uint8_t* rb0 = raw + bst * kBlurStrip * kPS + (sb & ~3);
+      auto rowsum = [&](int t) -> float2v {
+        const uint32_t* r32 = (const uint32_t*)(rb0 + t * kPS);
+        const uint32_t a = r32[0], b = r32[1], c = r32[2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(b, a, sh), hi = __builtin_amdgcn_alignbyte(c, b, sh);
+        constexpr uint32_t bias = 0x4B000000u;  // f32 2^23: the sum comes out as the bits of 2^23 + s
+        const uint32_t s0 = __builtin_amdgcn_udot4(hi, wh0, __builtin_amdgcn_udot4(lo, wl0, bias, false), false);
+        const uint32_t s1 = __builtin_amdgcn_udot4(hi, wh1, __builtin_amdgcn_udot4(lo, wl1, bias, false), false);
+        return (float2v){__uint_as_float(s0), __uint_as_float(s1)} - two23;
+      };
+      const int simd_w = wj & ~3;
+      const int X0 = xj - kPatchR + 2 * bg;  // level column of output col 2g
+      const bool tail = X0 + 1 >= simd_w;     // a column of the pair takes the scalar-tail rounding
+      const int nrows = bst < 2 ? kBlurStrip : kPatchRows - 2 * kBlurStrip;
+      float2v win[7];
+#pragma unroll
+      for (int t = 0; t < 6; t++) win[t] = rowsum(t);
+#pragma unroll
+      for (int t = 0; t < kBlurStrip; t++) {
+        win[(t + 6) % 7] = rowsum(t + 6);
+        const float2v w0 = win[t % 7], w1 = win[(t + 1) % 7], w2 = win[(t + 2) % 7], w3 = win[(t + 3) % 7],
+                      w4 = win[(t + 4) % 7], w5 = win[(t + 5) % 7], w6 = win[(t + 6) % 7];
+        // exactly the scalar chain fma(f3, w3, fma(f2, w2+w4, fma(f1, w1+w5, f0*(w0+w6)))) per element
+        const float2v accv = __builtin_elementwise_fma(
+            F3, w3, __builtin_elementwise_fma(F2, w2 + w4, __builtin_elementwise_fma(F1, w1 + w5, F0 * (w0 + w6))));
+        const float2v rr = accv + magic_s;  // rint (half-to-even) into the low bits
+        uint32_t pk = __builtin_amdgcn_perm(__float_as_uint(rr.y), __float_as_uint(rr.x), 0x05040100u);
+        u16x2 p2 = __builtin_bit_cast(u16x2, pk);
+        p2 = __builtin_elementwise_min(p2, (u16x2){255, 255});  // the kernel sums to 257
+        uint32_t px2 = __builtin_bit_cast(uint32_t, p2);
+        if (tail) {
+          // the row's scalar tail (x >= w & ~3): (acc + 2^15) >> 16
+          const int v0 = min(((int)(accv.x * 65536.f) + (1 << 15)) >> 16, 255);
+          const int v1 = min(((int)(accv.y * 65536.f) + (1 << 15)) >> 16, 255);
+          if (X0 >= simd_w) px2 = (px2 & 0xFFFF0000u) | (uint32_t)v0;
+          px2 = (px2 & 0x0000FFFFu) | ((uint32_t)v1 << 16);
+        }
+        if (t < nrows)
+          *(uint16_t*)(pb + (bst * kBlurStrip + t) * kPS + 2 * bg) = (uint16_t)(px2 | (px2 >> 8));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // rotated pattern point (px, py) -> patch pixel (18 + r, 18 + c) with
+    //   r = cvRound(px*b + py*a), c = cvRound(px*a - py*b)    (src/ORBextractor.cc:119-125)
+    // Both coordinates ride in packed-f32 lanes.  Each sum is rounded exactly as the scalar
+    // expression (products, then the add / subtract); adding 1.5*2^23 rounds it to an integer
+    // half-to-even (|sum| < 2^22), leaving 0x4B400000 + r in the bits.  A 24-bit mad on the raw
+    // bits ((0x400000 + r) * kPS, low 24 bits sign-extended) plus a constant gives the offset.
+    const float a = lane_f(cs, j), b = lane_f(sn, j);
+    const float2v ba = {b, a}, ab = {a, b};
+    static_for<4>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      int t[2];
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const float px = e ? pat[k].z : pat[k].x, py = e ? pat[k].w : pat[k].y;
+        const float2v P = (float2v){px, px} * ba;   // {px*b, px*a}
+        const float2v Q = (float2v){py, -py} * ab;  // {py*a, -(py*b)}: negation is exact
+        const float2v M = (P + Q) + magic;
+        const uint32_t mr = __float_as_uint(M.x), mc = __float_as_uint(M.y);
+        t[e] = pb[(uint32_t)__mul24((int)mr, kPS) + mc + corr];
+      }
+      // bits 64k .. 64k + 63 of the descriptor: every lane stores the same wave-uniform word
+      sdw[4 * j + k] = __ballot(t[0] < t[1]);
+    });
+    // the next keypoint's patches overwrite these: every lane's reads come first
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  });
+  // 5. output: descriptors (lane = dword) and keypoint records (lane = keypoint)
+  const size_t o0 = (size_t)img * kp_cap + i0;
+  if (lane < 8 * nk) reinterpret_cast<uint32_t*>(desc + o0 * 32)[lane] = reinterpret_cast<const uint32_t*>(sdw)[lane];
+  if (lane < nk) {
     orbx_keypoint kp;
     float fx = (float)x, fy = (float)y;
     if (l != 0) {
-      fx *= L.scale;
-      fy *= L.scale;
+      fx *= lscale;
+      fy *= lscale;
     }
     kp.x = fx;
     kp.y = fy;
-    kp.size = L.kp_size;
+    kp.size = lsize;
     kp.angle = angle;
     kp.response = (float)score;
     kp.octave = l;
     kp.class_id = -1;
-    kps[(size_t)img * kp_cap + i] = kp;
+    kps[o0 + lane] = kp;
   }
 }
 
@@ -1410,19 +1602,25 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   } else {
     (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
   }
-  T->begin(st);
-  hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
-  T->end(ST_BLUR, st);
+  // no k_blur here: k_describe blurs each keypoint's patch itself (the blurred levels are a
+  // debug product, launch_blur)
   if (Gh.ncells > 0) {
     const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap, Gh.oct_kcap);
     T->begin(st);
     hipLaunchKernelGGL(k_octree, dim3(n_img, Gh.nlevels), dim3(OBS), smem, st, Gd, cells, B);
     T->end(ST_OCTREE, st);
   }
-  const int nb = (Gh.max_kps + BS / 64 - 1) / (BS / 64);
+  const int nb = (Gh.max_kps + BS / 64 * kDescK - 1) / (BS / 64 * kDescK);
   T->begin(st);
   hipLaunchKernelGGL(k_describe, dim3(max(nb, 1), n_img), dim3(BS), 0, st, Gd, B, kps, desc, counts, kp_cap);
   T->end(ST_DESCRIBE, st);
+  return hipGetLastError();
+}
+
+// The blurred levels of n_img images (ORBX_DBG_BLUR_LEVEL; the extraction itself never writes them)
+hipError_t launch_blur(const Geometry& Gh, const Geometry* Gd, const int* tile_level, const BatchPtrs& B, int n_img,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
   return hipGetLastError();
 }
 

@@ -461,6 +461,14 @@ def _fuse_expected(fr, pts, best, cand_obs, occ_obs, nother):
             kf_mp[i] = ("P", k)
             obs[("P", k)]["K"] = i
 
+    # MapPoint::nObs: AddObservation adds 2 for a stereo observation (mvuRight >= 0) else 1; Replace
+    # (src/MapPoint.cc:179-221) clears the replaced point's observations but not its nObs
+    nobs = {e: cnt(e) for e in obs}
+
+    def add_obs(y, kf, idx):
+        obs[y][kf] = idx
+        nobs[y] += (2 if ur[idx] >= 0 else 1) if kf == "K" else 1
+
     def replace(x, y):
         o = obs[x]
         obs[x] = {}
@@ -472,7 +480,7 @@ def _fuse_expected(fr, pts, best, cand_obs, occ_obs, nother):
             else:
                 if kf == "K":
                     kf_mp[idx] = y
-                obs[y][kf] = idx
+                add_obs(y, kf, idx)
     nf = 0
     for k in range(n_p):
         b = int(best[k])
@@ -487,12 +495,12 @@ def _fuse_expected(fr, pts, best, cand_obs, occ_obs, nother):
                 else:
                     replace(m, a)
         else:
-            obs[a]["K"] = b
+            add_obs(a, "K", b)
             kf_mp[b] = a
         nf += 1
     code = [-1 if e is None else (e[1] if e[0] == "P" else -100 - e[1]) for e in kf_mp]
     ents = [("P", k) for k in range(n_p)] + [("Q", q) for q in range(len(occ_feats))]
-    return nf, np.array(code, np.int32), np.array([bad[e] for e in ents], np.uint8), np.array([cnt(e) for e in ents])
+    return nf, np.array(code, np.int32), np.array([bad[e] for e in ents], np.uint8), np.array([nobs[e] for e in ents])
 
 
 @pytest.mark.gpu
