@@ -1252,12 +1252,17 @@ constexpr int kRawR = kPatchR + 3;           // 21
 constexpr int kRawRows = 2 * kRawR + 1;      // 43
 constexpr int kRawCh = 4;
 constexpr int kRawIt = (kRawRows * kRawCh + 63) / 64;  // 3 chunks per lane
-constexpr int kDescLds = (kRawRows + kPatchRows) * kPS + 256;  // bytes per wave (+ descriptor words)
+// bytes per wave: (raw patch +) blurred patch + the descriptor words
+constexpr int kDescLds = (ORBX_DESC_FUSED ? kRawRows + kPatchRows : kPatchRows) * kPS + 256;
+constexpr int kPatchIt = (kPatchRows * kRawCh + 63) / 64;  // blurred-level patch: 3 chunks per lane
 // blur work split: lane = (column pair g < 19, row strip s < 3 of 13 / 13 / 11 output rows)
 constexpr int kBlurPairs = (kPatchRows + 1) / 2;  // 19
 constexpr int kBlurStrip = 13;
 
-constexpr int kDescK = 8;  // keypoints per wave
+#ifndef ORBX_DESC_K
+#define ORBX_DESC_K 8
+#endif
+constexpr int kDescK = ORBX_DESC_K;  // keypoints per wave
 static_assert(kDescK * 8 <= 64, "one descriptor dword per lane");
 
 // f(std::integral_constant<int, 0>{}) ... f(<N-1>): compile-time lane indices in an unrolled loop
@@ -1359,8 +1364,34 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   }
   // raw patch of keypoint j: lane chunk c = lane + 64k is (row c >> 2, 16-B column block c & 3);
   // rows reflected (REFLECT_101), columns outside the level patched in LDS afterwards
+  static_assert(kRawIt == kPatchIt, "one register set for both patch forms");
+#if !ORBX_DESC_FUSED
+  // the blurred level's patch: rows y-18..y+18, 16-B chunks from the 16-aligned column x0
+  const int bs = L.bstride;
+  const int x0 = (x - kPatchR) & ~15;
+  const uint8_t* pbl = B.blur + (size_t)img * G->blur_bytes + L.boff + (size_t)(y - kPatchR) * bs + x0;
+  constexpr int PS = kPS;
+  const uint32_t corr_l = (uint32_t)(kPatchR * PS + (x - x0)) - (0x400000u * (uint32_t)PS + 0x4B400000u);
+#endif
   uint32_t pv[2][kRawIt][4];
   auto load_patch = [&](int j, uint32_t (&dst)[kRawIt][4]) {
+#if !ORBX_DESC_FUSED
+    const int bsj = __builtin_amdgcn_readlane(bs, j);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)lane_ptr(pbl, j), (short)0, kPatchRows * bsj, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < kPatchIt; k++) {
+      // 16-B chunks from a 16-aligned column: with the 16-byte row stride a chunk is wholly inside
+      // its row or wholly past the row's end (and, in the last row, past num_records: zeros)
+      const int c = lane + 64 * k;
+      const uint32_t off = c < kPatchRows * kRawCh ? (uint32_t)((c >> 2) * bsj + 16 * (c & 3)) : 0x80000000u;
+      const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      dst[k][0] = t[0];
+      dst[k][1] = t[1];
+      dst[k][2] = t[2];
+      dst[k][3] = t[3];
+    }
+#else
     const int wj = __builtin_amdgcn_readlane(w, j), hj = __builtin_amdgcn_readlane(h, j);
     const int xj = __builtin_amdgcn_readlane(x, j), yj = __builtin_amdgcn_readlane(y, j);
     const int xs = (xj - kRawR) & ~15;
@@ -1386,6 +1417,7 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
         }
       }
     }
+#endif
   };
   load_patch(0, pv[0]);
   if (kDescK > 1) load_patch(1, pv[1]);
@@ -1431,16 +1463,30 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   const bool blur_lane = lane < 3 * kBlurPairs;
 
   // 4. per keypoint
+#if ORBX_DESC_FUSED
   uint8_t* raw = s_desc[wv];
   uint8_t* pb = s_desc[wv] + kRawRows * kPS;
   constexpr uint32_t corr = (uint32_t)(kPatchR * kPS + kPatchR) - (0x400000u * (uint32_t)kPS + 0x4B400000u);
+#else
+  uint8_t* pb = s_desc[wv];
+#endif
   const float2v magic_s = {12582912.0f, 12582912.0f};
   // the descriptors' 64-bit words, staged per wave and stored by lane = dword at the end
-  uint64_t* sdw = reinterpret_cast<uint64_t*>(s_desc[wv] + (kRawRows + kPatchRows) * kPS);
+  uint64_t* sdw = reinterpret_cast<uint64_t*>(s_desc[wv] + kDescLds - 256);
   static_for<kDescK>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     if (j >= nk) return;  // wave-uniform
     uint32_t (&cur)[kRawIt][4] = pv[j & 1];
+#if !ORBX_DESC_FUSED
+#pragma unroll
+    for (int k = 0; k < kPatchIt; k++) {
+      const int c = lane + 64 * k;
+      if (c < kPatchRows * kRawCh)
+        *(uint4*)(pb + (c >> 2) * kPS + 16 * (c & 3)) = make_uint4(cur[k][0], cur[k][1], cur[k][2], cur[k][3]);
+    }
+    if (j + 2 < kDescK && j + 2 < nk) load_patch(j + 2, cur);
+    const uint32_t corr = __builtin_amdgcn_readlane(corr_l, j);
+#else
     const int wj = __builtin_amdgcn_readlane(w, j), xj = __builtin_amdgcn_readlane(x, j);
     const int xs = (xj - kRawR) & ~15;
 #pragma unroll
@@ -1511,6 +1557,7 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
           *(uint16_t*)(pb + (bst * kBlurStrip + t) * kPS + 2 * bg) = (uint16_t)(px2 | (px2 >> 8));
       }
     }
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1602,15 +1649,18 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   } else {
     (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
   }
-  // no k_blur here: k_describe blurs each keypoint's patch itself (the blurred levels are a
-  // debug product, launch_blur)
+  if (!ORBX_DESC_FUSED) {  // (fused: k_describe blurs each keypoint's patch itself; launch_blur on request)
+    T->begin(st);
+    hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
+    T->end(ST_BLUR, st);
+  }
   if (Gh.ncells > 0) {
     const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap, Gh.oct_kcap);
     T->begin(st);
     hipLaunchKernelGGL(k_octree, dim3(n_img, Gh.nlevels), dim3(OBS), smem, st, Gd, cells, B);
     T->end(ST_OCTREE, st);
   }
-  const int nb = (Gh.max_kps + BS / 64 * kDescK - 1) / (BS / 64 * kDescK);
+  const int nb = (Gh.max_kps + BS / 64 * kDescK - 1) / (BS / 64 * kDescK);  // kDescK keypoints per wave
   T->begin(st);
   hipLaunchKernelGGL(k_describe, dim3(max(nb, 1), n_img), dim3(BS), 0, st, Gd, B, kps, desc, counts, kp_cap);
   T->end(ST_DESCRIBE, st);

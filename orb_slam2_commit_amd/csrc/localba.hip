@@ -1567,8 +1567,8 @@ __host__ __device__ inline int ldlt_pan_rows(int N) { return ldlt_np4(N) + 8; }
 // the lanes of a wave reading different row groups spread over the LDS banks
 __host__ __device__ inline int ldlt_prow(int i) { return (i >> 2) * 34 + (i & 3) * 8; }
 __host__ __device__ inline int ldlt_pan_arr(int N) { return ldlt_pan_rows(N) / 4 * 34; }
-inline size_t ldlt_pan_smem(int N) {
-  return ((size_t)N * (N - 1) / 2 + 3 * (size_t)ldlt_pan_arr(N) + N) * sizeof(double);
+inline size_t ldlt_pan_smem(int N) {  // (+ the look-ahead's second L / V panel set)
+  return ((size_t)N * (N - 1) / 2 + 5 * (size_t)ldlt_pan_arr(N) + N) * sizeof(double);
 }
 // (one tile per thread: with two the trailing update doubles and the panel kernel loses to the
 // column-step one, e.g. 91 us at N = 126)
@@ -1590,6 +1590,8 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   double* Lp = Pn + PA;                         // panel L (scaled)
   double* Vp = Lp + PA;                         // panel V = L D (unscaled)
   double* ys = Vp + PA;                         // [N] y = D^-1 L^-1 b
+  double* Lp2 = ys + N;                         // the look-ahead's second L / V set
+  double* Vp2 = Lp2 + PA;
   double a[TPT][4][4];
   int ti[TPT], tk[TPT];
   LDLT_TS(0);
@@ -1619,6 +1621,7 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   }
   // (the tile loads above are in flight while the panel arrays are cleared)
   for (int j = tid; j < 3 * PA; j += NT) Pn[j] = 0.0;  // padding rows / columns stay finite
+  for (int j = tid; j < 2 * PA; j += NT) Lp2[j] = 0.0;
   __syncthreads();
 #pragma unroll
   for (int t = 0; t < TPT; t++) {
@@ -1633,9 +1636,9 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   }
   __syncthreads();
   LDLT_TS(1);
-  for (int M = 0; 2 * M < Tc; M++) {
+  // B: the panel rows of panel M into (Lq, Vq)
+  auto panel_rows = [&](int M, double* Lq, double* Vq) {
     const int c0 = 8 * M, w = min(8, N - c0);
-    // B: panel rows
     const int i = c0 + tid;
     if (i <= N) {
       double Dm[36], u[8];
@@ -1676,8 +1679,8 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
         }
       }
       if (tid == 0 && zero) fail = 1;
-      double2_t* lo = reinterpret_cast<double2_t*>(Lp + ldlt_prow(i));
-      double2_t* vo = reinterpret_cast<double2_t*>(Vp + ldlt_prow(i));
+      double2_t* lo = reinterpret_cast<double2_t*>(Lq + ldlt_prow(i));
+      double2_t* vo = reinterpret_cast<double2_t*>(Vq + ldlt_prow(i));
 #pragma unroll
       for (int h = 0; h < 4; h++) {
         lo[h] = double2_t{L[2 * h], L[2 * h + 1]};
@@ -1694,14 +1697,15 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
           if (q < w) ys[c0 + q] = L[q];
       }
     }
-    __syncthreads();
-    LDLT_TS(2 + 2 * M);
-    // C: trailing tiles
+  };
+  // C: the register tiles in tile columns [tlo, thi) right of panel M take A -= L_rows V_cols^T;
+  // the tiles of the next panel (tile columns 2M+2, 2M+3) publish themselves
+  auto trailing = [&](int M, const double* Lq, const double* Vq, int tlo, int thi) {
 #pragma unroll
     for (int t = 0; t < TPT; t++) {
-      if (tk[t] >= 2 * M + 2) {
-        const double* lr = Lp + 34 * ti[t];
-        const double* vr = Vp + 34 * tk[t];
+      if (tk[t] >= 2 * M + 2 && tk[t] >= tlo && tk[t] < thi) {
+        const double* lr = Lq + 34 * ti[t];
+        const double* vr = Vq + 34 * tk[t];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           double Lv[4][4], Vv[4][4];
@@ -1730,9 +1734,36 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
         }
       }
     }
+  };
+#ifdef ORBX_LDLT_NO_LOOKAHEAD
+  for (int M = 0; 2 * M < Tc; M++) {
+    panel_rows(M, Lp, Vp);
+    __syncthreads();
+    LDLT_TS(2 + 2 * M);
+    trailing(M, Lp, Vp, 0, Tc);
     __syncthreads();
     LDLT_TS(3 + 2 * M);
   }
+#else
+  // Look-ahead by one panel: the next panel's two tile columns take panel M's update first and
+  // publish; then panel M+1's rows (the redundant 8x8 factor chain) run while every other tile
+  // takes panel M's update.  L / V of consecutive panels alternate between two LDS sets (the
+  // trailing update of panel M still reads its set while panel M+1's rows fill the other).  Each
+  // tile sees the same updates in the same order as without look-ahead: bit-identical.
+  panel_rows(0, Lp, Vp);
+  __syncthreads();
+  for (int M = 0; 2 * M < Tc; M++) {
+    double* Lc = (M & 1) ? Lp2 : Lp;
+    double* Vc = (M & 1) ? Vp2 : Vp;
+    trailing(M, Lc, Vc, 2 * M + 2, 2 * M + 4);
+    __syncthreads();
+    LDLT_TS(2 + 2 * M);
+    if (2 * (M + 1) < Tc) panel_rows(M + 1, (M & 1) ? Lp : Lp2, (M & 1) ? Vp : Vp2);
+    trailing(M, Lc, Vc, 2 * M + 4, Tc);
+    __syncthreads();
+    LDLT_TS(3 + 2 * M);
+  }
+#endif
   if (fail) {
     if (tid == 0) D.scal[2] = 0.0;
     return;

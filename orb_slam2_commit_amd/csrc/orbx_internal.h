@@ -18,6 +18,12 @@ namespace orbx {
 constexpr int kMaxLevelsPlan = 16;
 constexpr int kEdgeThresholdHost = 19;  // EDGE_THRESHOLD, src/ORBextractor.cc:74
 
+// k_describe form: 1 = each keypoint's 37x37 patch blurred inside k_describe from the raw level (no
+// blurred level materialised), 0 = k_blur writes the blurred levels and k_describe samples them
+#ifndef ORBX_DESC_FUSED
+#define ORBX_DESC_FUSED 0
+#endif
+
 struct LevelGeom {
   int w, h;
   long long off;    // offset of level in per-image pyramid buffer (levels >= 1)
@@ -77,7 +83,12 @@ struct ResizeY {
   int16_t b0, b1;
 };
 
-constexpr int kBlurTileW = 128, kBlurTileH = 128;
+#ifndef ORBX_BLUR_TW  // k_blur output tile (256 threads: TW/4 column groups x 16-row strips)
+#define ORBX_BLUR_TW 128
+#define ORBX_BLUR_TH 128
+#endif
+constexpr int kBlurTileW = ORBX_BLUR_TW, kBlurTileH = ORBX_BLUR_TH;
+static_assert(kBlurTileW / 4 * (kBlurTileH / 16) == 256, "k_blur: one thread per 4 columns x 16 rows");
 
 // Device pointers for one batch.
 struct BatchPtrs {

@@ -20,6 +20,7 @@
 namespace orbx {
 
 constexpr int SBS = 256;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
 
@@ -142,6 +143,9 @@ constexpr int kSadIt = (11 * kSadDw + 63) / 64;
 // row-group loop spilled and was slower (0.55-0.60)
 __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
   __shared__ uint32_t s_sad[SBS / 64][11 * kSadDw];
+#ifndef ORBX_SAD_BYTES
+  __shared__ uint32_t s_sw[SBS / 64][66 + 2 * 121];  // u16-pair forms of the staged patch and strip
+#endif
   const int2 bi = xcd_block2();
   const int f = bi.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
@@ -251,20 +255,68 @@ __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geo
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(sp);
+    const uint32_t aL0 = (uint32_t)(uintptr_t)rowL0, aR0 = (uint32_t)(uintptr_t)rowR0;
+    auto lpix = [&](int dy, int dx) -> int { return sb[4 * kSadDw * dy + ((aL0 + (uint32_t)(dy * lw)) & 3) + dx]; };
+    auto rpix = [&](int dy, int dx) -> int {  // strip column dx
+      return sb[4 * (kSadDw * dy + kSadDwL) + ((aR0 + (uint32_t)(dy * lw)) & 3) + dx];
+    };
     int part = 0;
+#ifndef ORBX_SAD_BYTES
+    {
+      // SAD term |(L - Lc) - (R - Rc)| = |(L + Rc) - (R + Lc)|: both sides in [0, 510], so two
+      // pixels per v_sad_u16 on u16 pairs.  The staged bytes become, in this wave's slot: the left
+      // patch as pairs (2k, 2k+1) (11 x 6 dwords, pad 0) and the strip + Lc twice, as pairs
+      // (2k, 2k+1) and (2k+1, 2k+2) (11 x 11 dwords each), so every lane's pair reads are aligned.
+      // Lanes 0..54: offset s = lane % 11 (inc = s - 5), rows g, g+5, g+10 (g = lane / 11).
+      uint32_t* l16 = s_sw[wid];
+      uint32_t* re16 = l16 + 66;
+      uint32_t* ro16 = re16 + 121;
+      const uint32_t Lc = (uint32_t)lpix(w, w);
+      for (int q = lane; q < 66; q += 64) {
+        const int r = q / 6, k = q - r * 6;
+        l16[q] = (uint32_t)lpix(r, 2 * k) | (2 * k + 1 <= 2 * w ? (uint32_t)lpix(r, 2 * k + 1) << 16 : 0u);
+      }
+      for (int q = lane; q < 121; q += 64) {
+        const int r = q / 11, k = q - r * 11;
+        const uint32_t a = (uint32_t)rpix(r, 2 * k) + Lc;
+        const uint32_t b = (2 * k + 1 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 1) : 0u) + Lc;
+        const uint32_t c = (2 * k + 2 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 2) : 0u) + Lc;
+        re16[q] = a | b << 16;
+        ro16[q] = b | c << 16;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int ll = lane < 55 ? lane : 0;
+      const int so = ll % 11, g = ll / 11;
+      const uint32_t rc = (uint32_t)rpix(w, so + w);  // Rc = strip column inc + 2w
+      const u16x2 rc2 = {(uint16_t)rc, (uint16_t)rc};
+      const uint32_t* rrow = ((so & 1) ? ro16 : re16) + (so >> 1);  // pair (so + 2p, so + 2p + 1) at p
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int dy = min(g + 5 * k, 2 * w);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int p2 = 0; p2 < 6; p2++) {
+          uint32_t lp = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, l16[dy * 6 + p2]) + rc2);
+          uint32_t rp = rrow[dy * 11 + p2];
+          if (p2 == 5) {  // pixel 11 of the pair does not exist
+            lp &= 0xFFFFu;
+            rp &= 0xFFFFu;
+          }
+          acc = __builtin_amdgcn_sad_u16(lp, rp, acc);
+        }
+        part += (g + 5 * k < 2 * w + 1) ? (int)acc : 0;
+      }
+      if (lane >= 55) part = 0;
+    }
+#else
     {
       // lanes 0..54: inc = lane % 11, rows g, g+5, g+10 (g = lane / 11); rows >= 11
       // clamped and masked
       const int ll = lane < 55 ? lane : 0;
       const int inc = ll % 11 - L;
       const int g = ll / 11;
-      const uint32_t aL0 = (uint32_t)(uintptr_t)rowL0, aR0 = (uint32_t)(uintptr_t)rowR0;
-      auto lpix = [&](int dy, int dx) -> int {
-        return sb[4 * kSadDw * dy + ((aL0 + (uint32_t)(dy * lw)) & 3) + dx];
-      };
-      auto rpix = [&](int dy, int dx) -> int {  // strip column dx
-        return sb[4 * (kSadDw * dy + kSadDwL) + ((aR0 + (uint32_t)(dy * lw)) & 3) + dx];
-      };
       const int cL = lpix(w, w);
       const int cR = rpix(w, inc + 2 * w);
       // one row group at a time: 22 staged bytes live instead of 66 (registers bound occupancy)
@@ -287,6 +339,7 @@ __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geo
       }
       if (lane >= 55) part = 0;
     }
+#endif
     const int src = lane < 11 ? lane : 0;
     int sad = __shfl(part, src, 64) + __shfl(part, src + 11, 64) + __shfl(part, src + 22, 64) +
               __shfl(part, src + 33, 64) + __shfl(part, src + 44, 64);

@@ -208,6 +208,13 @@ def test_gpu_track_motion_model_and_local_map(gpu):
         o1 = oracle.search_by_projection(fr, pts, 1, th=7.0, check_ori=True, mono=False, last_Tcw=Tg[j])
         if o1["nmatches"] < 20:
             o1 = oracle.search_by_projection(fr, pts, 1, th=14.0, check_ori=True, mono=False, last_Tcw=Tg[j])
+        if not int(r["nmatches"][j]) == o1["nmatches"] > 100:  # diagnostics (printed with the failure)
+            print("motion diag", dict(j=j, gpu=int(r["nmatches"][j]), oracle=o1["nmatches"], n=n, nl=nl,
+                                      ok=int(ok.sum()), dep=int((Z_all[lf, :nl] > 0).sum()),
+                                      kl_x=kl["x"][:4].tolist(), kc_x=kc["x"][:4].tolist(),
+                                      pos=P["pos"][ok][:2].tolist(), Tg=np.asarray(Tg[j]).tolist(),
+                                      Twc=np.asarray(Twc[j]).tolist(), sf=sf.tolist(), r={k: np.asarray(v).tolist()
+                                      for k, v in r.items()}, stream=str(torch.cuda.current_stream())))
         assert int(r["nmatches"][j]) == o1["nmatches"] > 100
         np.testing.assert_array_equal(h(mt.fout1[j, :n]), o1["frame_out"])
         fmap = np.where(o1["frame_out"] >= 0, o1["frame_out"], -1)
