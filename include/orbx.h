@@ -66,6 +66,11 @@ typedef int orbx_status;
 #define ORBX_ERR_SIZE (-5)       /* image geometry outside supported range    */
 #define ORBX_ERR_STATE (-6)      /* call requires a previous extraction       */
 
+/* stream argument of the handle-owning device entry points (extractor, vocabulary): NULL picks the
+ * handle's own (non-blocking) stream, this value the device's legacy null stream, which is what a
+ * caller on PyTorch's default stream must pass so its own work stays ordered with the library's. */
+#define ORBX_STREAM_NULL ((void*)1)
+
 /* Layout-identical to cv::KeyPoint (28 bytes). class_id is always -1. */
 typedef struct {
   float x, y, size, angle, response;
@@ -107,7 +112,8 @@ orbx_status orbx_pyramid_level(orbx_extractor* h, int image, int level, uint8_t*
 /* Device-resident batch: n_images u8 images of width x height, image i at
  * d_images + i*image_pitch (row stride = width).  Outputs on device: image i
  * writes d_counts[i] keypoints to d_kps + i*kp_capacity and descriptors to
- * d_desc + i*kp_capacity*32.  stream: hipStream_t (NULL = the handle's own).
+ * d_desc + i*kp_capacity*32.  stream: hipStream_t (NULL = the handle's own; ORBX_STREAM_NULL = the
+ * device's legacy null stream, e.g. PyTorch's default stream).
  * Asynchronous; the input buffer must stay alive until the stream completes
  * and, for orbx_stereo_* on the same batch, until those complete too
  * (level 0 of the pyramid is the input itself). */
@@ -209,7 +215,8 @@ orbx_status orbx_voc_transform(orbx_voc* v, const uint8_t* desc, const int32_t* 
  * for every frame of the batch at once): set s is rows s*stride .. s*stride + count[s*count_step]-1
  * of d_desc (at most cap <= 8192 rows; the stereo batch's left images: stride = 2*cap,
  * count_step = 2).  Outputs as above with set_off[s] = s*cap (fv_off of set s starts at
- * s*(cap+1)).  All pointers device pointers, queued on `stream` (NULL: the vocabulary's own),
+ * s*(cap+1)).  All pointers device pointers, queued on `stream` (NULL: the vocabulary's own;
+ * ORBX_STREAM_NULL: the device's legacy null stream),
  * no host synchronisation. */
 orbx_status orbx_voc_transform_device(orbx_voc* v, const uint8_t* d_desc, int cap, long long stride,
                                       const int32_t* d_count, int count_step, int n_sets, int levelsup,

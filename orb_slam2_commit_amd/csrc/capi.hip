@@ -503,7 +503,9 @@ orbx_status run_extract(orbx_extractor* h, Plan* P, int n, const uint8_t* d_in, 
   return ORBX_OK;
 }
 
-hipStream_t pick_stream(orbx_extractor* h, void* s) { return s ? (hipStream_t)s : h->stream; }
+hipStream_t pick_stream(orbx_extractor* h, void* s) {
+  return s == ORBX_STREAM_NULL ? (hipStream_t)0 : s ? (hipStream_t)s : h->stream;
+}
 
 // 64-bit fingerprint of n keypoint records and their descriptors (multiply-xorshift over 32-bit
 // words, a few microseconds for 2,000 keypoints): orbx_stereo_match uses the device copies of the

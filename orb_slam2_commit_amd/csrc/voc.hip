@@ -525,7 +525,7 @@ orbx_status orbx_voc_transform_device(orbx_voc* v, const uint8_t* d_desc, int ca
   if (cap > orbx::kVocMaxSet) return ORBX_ERR_SIZE;
   if (v->empty) return ORBX_ERR_STATE;
   if (hipSetDevice(v->device) != hipSuccess) return ORBX_ERR_HIP;
-  hipStream_t st = stream ? (hipStream_t)stream : v->st;
+  hipStream_t st = stream == ORBX_STREAM_NULL ? (hipStream_t)0 : stream ? (hipStream_t)stream : v->st;
   const size_t nt = (size_t)n_sets * cap;
   if (nt > (size_t)0x7FFFFFFF) return ORBX_ERR_SIZE;
   const size_t need = a256(4 * nt) + a256(8 * nt) + a256(4 * nt);  // word | weight | nid

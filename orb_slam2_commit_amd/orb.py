@@ -128,7 +128,7 @@ class ORBextractor:
         n, h, w = images.shape
         cap = kps.shape[1]
         check(_lib.lib().orbx_extract_batch_device(self._h, n, ptr(images), w, h, h * w, ptr(kps), ptr(desc),
-                                                   ptr(counts), cap, _stream_ptr(stream)),
+                                                   ptr(counts), cap, _stream_ptr(stream, True)),
               "orbx_extract_batch_device")
 
     def stereo_frames_device(self, images, kps, desc, counts, bf, baseline, uright, depth, nmatches, stream=None):
@@ -137,16 +137,20 @@ class ORBextractor:
         cap = kps.shape[1]
         check(_lib.lib().orbx_stereo_frames_device(self._h, n2 // 2, ptr(images), w, h, h * w, ptr(kps), ptr(desc),
                                                    ptr(counts), cap, C.c_float(bf), C.c_float(baseline),
-                                                   ptr(uright), ptr(depth), ptr(nmatches), _stream_ptr(stream)),
+                                                   ptr(uright), ptr(depth), ptr(nmatches), _stream_ptr(stream, True)),
               "orbx_stereo_frames_device")
 
 
-def _stream_ptr(stream):
+def _stream_ptr(stream, handle_api=False):
+    """hipStream_t of a torch stream.  For the handle-owning entry points (extractor, vocabulary) NULL
+    would pick the handle's own non-blocking stream, so torch's legacy default stream (cuda_stream 0) is
+    passed as ORBX_STREAM_NULL to keep the caller's work on that stream ordered with the library's."""
     if stream is None:
         return None
-    if hasattr(stream, "cuda_stream"):
-        return C.c_void_p(stream.cuda_stream)
-    return C.c_void_p(int(stream))
+    s = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    if s == 0 and handle_api:
+        return C.c_void_p(1)  # ORBX_STREAM_NULL
+    return C.c_void_p(s)
 
 
 def compute_stereo_matches(extractor_left, extractor_right, kps_left, desc_left, kps_right, desc_right, bf,

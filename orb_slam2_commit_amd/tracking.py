@@ -72,7 +72,8 @@ class TrackBatch:
         # 1. Frame::ComputeBoW on every left image (src/Frame.cc ComputeBoW)
         check(L.orbx_voc_transform_device(self.voc._h, ptr(desc), cap, 2 * cap, ptr(counts), 2, B, self.levelsup,
                                           ptr(self.bow_words), ptr(self.bow_values), ptr(self.n_bow),
-                                          ptr(self.fv_nodes), ptr(self.fv_off), ptr(self.fv_feat), ptr(self.n_fv), sp),
+                                          ptr(self.fv_nodes), ptr(self.fv_off), ptr(self.fv_feat), ptr(self.n_fv),
+                                          C.c_void_p(st.cuda_stream or 1)),  # 1 = ORBX_STREAM_NULL
               "orbx_voc_transform_device")
         if ev:
             ev[1].record(st)

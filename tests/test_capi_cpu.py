@@ -81,3 +81,19 @@ def test_ctypes_layouts_match_the_c_abi():
         assert L.orbx_sizeof(name.encode()) == C.sizeof(cls), name
     assert L.orbx_sizeof(b"orbx_keypoint") == _lib.KEYPOINT_DTYPE.itemsize == 28
     assert L.orbx_sizeof(b"no_such_type") == -1
+
+
+def test_handle_stream_sentinel():
+    """torch's legacy default stream (cuda_stream 0) reaches the handle-owning entry points as
+    ORBX_STREAM_NULL (1), not NULL (= the handle's own non-blocking stream, unordered with the caller's
+    work); other streams and the plain-stream entry points pass through unchanged."""
+    from types import SimpleNamespace
+
+    from orb_slam2_commit_amd.orb import _stream_ptr
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "orbx.h")).read()
+    assert re.search(r"#define ORBX_STREAM_NULL \(\(void\*\)1\)", hdr)
+    null, other = SimpleNamespace(cuda_stream=0), SimpleNamespace(cuda_stream=0x5000)
+    assert _stream_ptr(null, True).value == 1
+    assert _stream_ptr(null).value is None
+    assert _stream_ptr(other, True).value == 0x5000 and _stream_ptr(other).value == 0x5000
+    assert _stream_ptr(None, True) is None
