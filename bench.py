@@ -185,11 +185,7 @@ def s8d_stage_bytes(stage, n_img, n_frames, P, kps_per_img, acc_per_frame):
         return n_img * sP
     if stage == "k_blur":  # (debug launches only) blur read + write of every level
         return n_img * 2 * sP
-    if stage == "k_describe":
-        # orientation read + blur read (both of the raw level; the kernel blurs each keypoint's
-        # patch itself) + 28 + 32 B out.  §8(d)'s blur write and blurred read (2*sum(P)) are moved
-        # by no kernel -- the blurred level is never materialised -- so, like the 2*P0 input copy,
-        # they appear only in the whole-step figure
+    if stage == "k_describe":  # orientation read of the raw level + rBRIEF read of the blurred level + 60 B out
         return n_img * (2 * sP + 60 * kps_per_img)
     if stage == "stereo":  # k_stereo_prep + k_stereo_match + k_stereo_finalize together: B_st
         return n_frames * s8d_stereo_frame(kps_per_img, kps_per_img, acc_per_frame)

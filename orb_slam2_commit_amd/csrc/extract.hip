@@ -5,9 +5,10 @@
 //   k_resize   x(nlevels-1)  ComputePyramid            src/ORBextractor.cc:1215-1250
 //   k_fast                   per-cell FAST + fallback  src/ORBextractor.cc:843-915
 //   k_octree                 DistributeOctTree         src/ORBextractor.cc:562-815
-//   k_describe               IC_Angle + patch GaussianBlur 7x7 s=2 + rBRIEF + scale
+//   k_describe               IC_Angle + rBRIEF on the blurred level + scale
 //                                                      src/ORBextractor.cc:77-152,1186-1207
-//   (k_blur                  whole-level GaussianBlur, debug only: ORBX_DBG_BLUR_LEVEL)
+//   k_blur                   whole-level GaussianBlur 7x7 s=2 (ORBX_DESC_FUSED=1: not launched,
+//                            k_describe blurs each keypoint's patch; ORBX_DBG_BLUR_LEVEL makes it)
 //
 // Integer/byte work throughout (HBM-bound); the only float math is the
 // orientation/rotation and it is compiled without FP contraction so it rounds
