@@ -5,9 +5,9 @@
 //   k_stereo_prep     per frame: right keypoints sorted by (octave, y) -- replaces
 //                     the reference's row-band table (:564-590); the candidate
 //                     set of a left keypoint is then 3 contiguous ranges.
-//   k_stereo_match    one wave per left keypoint: band Hamming argmin (strict <,
-//                     lowest index), 11x11 SAD over +-5 px on the unblurred
-//                     pyramid level, parabola, depth (:600-770).
+//   k_stereo_match    16 lanes per left keypoint (four per wave in parallel): band
+//                     Hamming argmin (strict <, lowest index), 11x11 SAD over +-5 px
+//                     on the unblurred pyramid level, parabola, depth (:600-770).
 //   k_stereo_finalize per frame: median SAD by 2-pass radix select, reject
 //                     SAD >= 1.5*1.4*median (:774-787).
 #include <hip/hip_runtime.h>
@@ -129,244 +129,199 @@ __global__ __launch_bounds__(PBS) void k_stereo_prep(StereoArgs A, const Geometr
   }
 }
 
-// 16 left keypoints per 4-wave block (4 per wave): 128 per block left the
-// waves walking 32 keypoints each in series (0.39 ms/step; 16: 0.29 ms)
-constexpr int kKpsPerBlock = 16;
-// SAD staging per wave: 11 rows x (4 left + 6 right) dwords
+// 16 left keypoints per 4-wave block (one per 16-lane quarter)
+constexpr int kKpsPerBlock = SBS / 16;
+// SAD staging per keypoint: 11 rows x (4 left + 6 right) dwords
 constexpr int kSadDwL = 4, kSadDwR = 6, kSadDw = kSadDwL + kSadDwR;
-constexpr int kSadIt = (11 * kSadDw + 63) / 64;
 
-// No LDS: candidate ranges come from the row table, (x, index) pairs from the
-// sorted array, so occupancy is bounded by registers only.
-// 8 waves per SIMD: 64 VGPRs (the SAD holds one row group's 22 staged bytes at a time, not all
-// three): 0.539 -> 0.488 ms per step against 79 VGPRs / 6 waves; capping registers without the
-// row-group loop spilled and was slower (0.55-0.60)
-__global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
-  __shared__ uint32_t s_sad[SBS / 64][11 * kSadDw];
-#ifndef ORBX_SAD_BYTES
-  __shared__ uint32_t s_sw[SBS / 64][66 + 2 * 121];  // u16-pair forms of the staged patch and strip
-#endif
+// k_stereo_match: the four left keypoints of a wave run in PARALLEL, one per 16-lane quarter
+// (q = lane >> 4), 16 per 256-thread block: each keypoint's chain of dependent round trips
+// (keypoint + candidate ranges -> candidates' (x, index) and descriptors -> SAD rows) overlaps the
+// other three.  One keypoint per wave, four in series, took 0.388 ms per step against 0.225 here
+// (profiles/r04/ab_stereo_quarters.txt).  Per keypoint (src/Frame.cc:600-770): strict-min Hamming
+// over the candidate ranges (key dist<<12 | index, the winner's x carried by the key's lane); the
+// 11x11 left patch and 11x21 right strip staged in the quarter's LDS slot; SAD term
+// |(L - Lc) - (R - Rc)| = |(L + Rc) - (R + Lc)| on u16 pairs (two pixels per v_sad_u16), lane
+// s < 11 of the quarter summing offset s - 5 over the 11 rows; parabola; depth.  Quarter
+// reductions are DPP row rotations (a DPP row is 16 lanes); a quarter leaves early on its own
+// (its lanes agree).  LDS 26.1 KB per block: 6 blocks (24 waves) per CU.
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {  // min over the lane's 16-lane row
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false));  // row_ror:2
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false));  // row_ror:1
+  return v;
+}
+
+__global__ __launch_bounds__(SBS, 6) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
+  constexpr int NQ = SBS / 16;                // quarters (keypoints) per block
+  __shared__ uint32_t s_raw[NQ][11 * kSadDw];  // per quarter: 11 rows x (4 left + 6 right) dwords
+  __shared__ uint32_t s_sw[NQ][66 + 2 * 121];  // per quarter: u16-pair forms of the patch and strip
   const int2 bi = xcd_block2();
-  const int f = bi.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int f = bi.y, tid = threadIdx.x, lane = tid & 63, ql = lane & 15, qb = tid >> 4;
   const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
-  const int base = bi.x * kKpsPerBlock;
-  if (base >= nL) return;
+  const int iL = bi.x * NQ + qb;
+  if (iL >= nL) return;
   const int2* rxi = A.rxi + (size_t)f * kMaxStereoKps;
   const uint4* rdR = A.rdesc + (size_t)f * kMaxStereoKps * 2;
   const orbx_keypoint* kL = A.kpL + (size_t)f * A.kL_stride;
-  const uint8_t* dL = A.dL + (size_t)f * A.kL_stride * 32;
   const int limg = f * A.l_step + A.l_off, rimg = f * A.r_step + A.r_off;
-  for (int iL = base + wid; iL < min(nL, base + kKpsPerBlock); iL += SBS / 64) {
-    const orbx_keypoint kp = kL[iL];
-    const uint4 lrg = A.lrange[(size_t)f * A.maxL + iL];  // issued beside the keypoint (k_stereo_prep)
-    const int levelL = kp.octave;
-    const float uL = kp.x;
-    const float minU = uL - A.maxD, maxU = uL - A.minD;
-    float* outU = A.uR + (size_t)f * A.out_stride + iL;
-    float* outD = A.depth + (size_t)f * A.out_stride + iL;
-    int* outS = A.sad + (size_t)f * A.out_stride + iL;
-    if (lane == 0) {
-      *outU = -1.0f;
-      *outD = -1.0f;
-      *outS = -1;
-    }
-    if (maxU < 0) continue;
-    // candidate ranges per octave (vRowIndices[vL], octaves levelL-1..levelL+1)
-    const uint32_t t3[3] = {lrg.x, lrg.y, lrg.z};
-    int rb[3], re[3];
+  const orbx_keypoint kp = kL[iL];
+  const uint4 lrg = A.lrange[(size_t)f * A.maxL + iL];
+  uint64_t ld[4];
+  {
+    const uint64_t* p = (const uint64_t*)(A.dL + ((size_t)f * A.kL_stride + iL) * 32);
+    ld[0] = p[0]; ld[1] = p[1]; ld[2] = p[2]; ld[3] = p[3];
+  }
+  const int levelL = kp.octave;
+  const float uL = kp.x;
+  const float minU = uL - A.maxD, maxU = uL - A.minD;
+  float* outU = A.uR + (size_t)f * A.out_stride + iL;
+  float* outD = A.depth + (size_t)f * A.out_stride + iL;
+  int* outS = A.sad + (size_t)f * A.out_stride + iL;
+  if (ql == 0) {
+    *outU = -1.0f;
+    *outD = -1.0f;
+    *outS = -1;
+  }
+  if (maxU < 0) return;
+  const uint32_t t3[3] = {lrg.x, lrg.y, lrg.z};
+  int rb[3], re[3];
 #pragma unroll
-    for (int q = 0; q < 3; q++) {
-      rb[q] = (int)(t3[q] & 0xFFFF);
-      re[q] = (int)(t3[q] >> 16);
+  for (int q = 0; q < 3; q++) {
+    rb[q] = (int)(t3[q] & 0xFFFF);
+    re[q] = (int)(t3[q] >> 16);
+  }
+  const int n0 = re[0] - rb[0], n1 = re[1] - rb[1], n2 = re[2] - rb[2];
+  const int K = n0 + n1 + n2;
+  uint32_t best = 0xFFFFFFFFu;
+  float bestX = 0.f;
+  for (int j = ql; j < K; j += 16) {
+    const int pos = j < n0 ? rb[0] + j : (j < n0 + n1 ? rb[1] + (j - n0) : rb[2] + (j - n0 - n1));
+    const int2 xi = rxi[pos];
+    const uint4 r0 = rdR[2 * pos], r1 = rdR[2 * pos + 1];
+    const float uR = __int_as_float(xi.x);
+    if (!(uR >= minU && uR <= maxU)) continue;
+    const uint64_t rd[4] = {(uint64_t)r0.x | ((uint64_t)r0.y << 32), (uint64_t)r0.z | ((uint64_t)r0.w << 32),
+                            (uint64_t)r1.x | ((uint64_t)r1.y << 32), (uint64_t)r1.z | ((uint64_t)r1.w << 32)};
+    const int dist = hamming256(ld, rd);
+    const uint32_t key = ((uint32_t)dist << 12) | (uint32_t)xi.y;
+    if (key < best) {
+      best = key;
+      bestX = uR;
     }
-    const int n0 = re[0] - rb[0], n1 = re[1] - rb[1], n2 = re[2] - rb[2];
-    const int K = n0 + n1 + n2;
-    uint64_t ld[4];
-    {
-      const uint64_t* p = (const uint64_t*)(dL + (size_t)iL * 32);
-      ld[0] = p[0]; ld[1] = p[1]; ld[2] = p[2]; ld[3] = p[3];
+  }
+  const uint32_t wbest = row_min_u32(best);
+  const int bestDist = wbest == 0xFFFFFFFFu ? 100 : (int)(wbest >> 12);
+  if (bestDist >= 75) return;  // thOrbDist = (TH_HIGH+TH_LOW)/2 (also < TH_HIGH)
+  const LevelGeom& Lv = G->lv[levelL];
+  const uint64_t om = __ballot(best == wbest) >> (lane & 48);
+  const int owner = (lane & 48) + __builtin_ctzll(om & 0xFFFF);
+  const float uR0 = __shfl(bestX, owner, 64);
+  const float sf = A.inv_scale[levelL];
+  const float scaleduL = __builtin_roundf(kp.x * sf);
+  const float scaledvL = __builtin_roundf(kp.y * sf);
+  const float scaleduR0 = __builtin_roundf(uR0 * sf);
+  const int w = 5, L = 5;
+  const float iniu = scaleduR0 + L - w;
+  const float endu = scaleduR0 + L + w + 1;
+  if (iniu < 0 || endu >= Lv.w) return;
+  if (scaleduR0 - 2 * w < 0 || scaledvL - w < 0 || scaledvL + w >= Lv.h || scaleduL - w < 0 ||
+      scaleduL + w >= Lv.w)
+    return;
+  const uint8_t* imL = level_ptr(*G, A.BL, limg, levelL);
+  const uint8_t* imR = level_ptr(*G, A.BR, rimg, levelL);
+  const int lw = Lv.w;
+  const int cy = (int)scaledvL, cxL = (int)scaleduL, cxR0 = (int)scaleduR0;
+  uint32_t* sp = s_raw[qb];
+  const uint8_t* rowL0 = imL + (size_t)(cy - w) * lw + (cxL - w);
+  const uint8_t* rowR0 = imR + (size_t)(cy - w) * lw + (cxR0 - 2 * w);
+  {
+    constexpr int IT = (11 * kSadDw + 15) / 16;
+    uint32_t sv[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const int q = ql + 16 * k, r = q / kSadDw, j = q - r * kSadDw;
+      const bool left = j < kSadDwL;
+      const uintptr_t a = (uintptr_t)((left ? rowL0 : rowR0) + (size_t)r * lw);
+      const int jj = left ? j : j - kSadDwL, need = left ? 2 * w + 1 : 4 * w + 1;
+      sv[k] = 0;
+      if (q < 11 * kSadDw && 4 * jj < (int)(a & 3) + need) sv[k] = *((const uint32_t*)(a & ~(uintptr_t)3) + jj);
     }
-    // candidate (x, index) and descriptor loads are independent (both in sorted
-    // order); the winner's x travels with its key, so no kR[bestIdxR] load follows
-    uint32_t best = 0xFFFFFFFFu;
-    float bestX = 0.f;
-    for (int j = lane; j < K; j += 64) {
-      const int pos = j < n0 ? rb[0] + j : (j < n0 + n1 ? rb[1] + (j - n0) : rb[2] + (j - n0 - n1));
-      const int2 xi = rxi[pos];
-      const uint4 r0 = rdR[2 * pos], r1 = rdR[2 * pos + 1];
-      const float uR = __int_as_float(xi.x);
-      if (!(uR >= minU && uR <= maxU)) continue;
-      const uint64_t rd[4] = {(uint64_t)r0.x | ((uint64_t)r0.y << 32), (uint64_t)r0.z | ((uint64_t)r0.w << 32),
-                              (uint64_t)r1.x | ((uint64_t)r1.y << 32), (uint64_t)r1.z | ((uint64_t)r1.w << 32)};
-      const int dist = hamming256(ld, rd);
-      const uint32_t key = ((uint32_t)dist << 12) | (uint32_t)xi.y;
-      if (key < best) {
-        best = key;
-        bestX = uR;
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (ql + 16 * k < 11 * kSadDw) sp[ql + 16 * k] = sv[k];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(sp);
+  const uint32_t aL0 = (uint32_t)(uintptr_t)rowL0, aR0 = (uint32_t)(uintptr_t)rowR0;
+  auto lpix = [&](int dy, int dx) -> int { return sb[4 * kSadDw * dy + ((aL0 + (uint32_t)(dy * lw)) & 3) + dx]; };
+  auto rpix = [&](int dy, int dx) -> int {
+    return sb[4 * (kSadDw * dy + kSadDwL) + ((aR0 + (uint32_t)(dy * lw)) & 3) + dx];
+  };
+  uint32_t* l16 = s_sw[qb];
+  uint32_t* re16 = l16 + 66;
+  uint32_t* ro16 = re16 + 121;
+  const uint32_t Lc = (uint32_t)lpix(w, w);
+  for (int q = ql; q < 66; q += 16) {
+    const int r = q / 6, k = q - r * 6;
+    l16[q] = (uint32_t)lpix(r, 2 * k) | (2 * k + 1 <= 2 * w ? (uint32_t)lpix(r, 2 * k + 1) << 16 : 0u);
+  }
+  for (int q = ql; q < 121; q += 16) {
+    const int r = q / 11, k = q - r * 11;
+    const uint32_t a = (uint32_t)rpix(r, 2 * k) + Lc;
+    const uint32_t b = (2 * k + 1 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 1) : 0u) + Lc;
+    const uint32_t c = (2 * k + 2 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 2) : 0u) + Lc;
+    re16[q] = a | b << 16;
+    ro16[q] = b | c << 16;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int so = ql < 11 ? ql : 0;
+  const uint32_t rc = (uint32_t)rpix(w, so + w);  // Rc = strip column inc + 2w
+  const u16x2 rc2 = {(uint16_t)rc, (uint16_t)rc};
+  const uint32_t* rrow = ((so & 1) ? ro16 : re16) + (so >> 1);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int dy = 0; dy < 2 * w + 1; dy++) {
+#pragma unroll
+    for (int p2 = 0; p2 < 6; p2++) {
+      uint32_t lp = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, l16[dy * 6 + p2]) + rc2);
+      uint32_t rp = rrow[dy * 11 + p2];
+      if (p2 == 5) {
+        lp &= 0xFFFFu;
+        rp &= 0xFFFFu;
       }
+      acc = __builtin_amdgcn_sad_u16(lp, rp, acc);
     }
-    const uint32_t wbest = wave_min_u32(best);
-    const int bestDist = wbest == 0xFFFFFFFFu ? 100 : (int)(wbest >> 12);
-    if (bestDist >= 75) continue;  // thOrbDist = (TH_HIGH+TH_LOW)/2 (also < TH_HIGH)
-    // SAD refinement on the unblurred level kpL.octave
-    const LevelGeom& Lv = G->lv[levelL];
-    const int owner = __builtin_ctzll(__ballot(best == wbest));
-    const float uR0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bestX), owner));
-    const float sf = A.inv_scale[levelL];
-    const float scaleduL = __builtin_roundf(kp.x * sf);
-    const float scaledvL = __builtin_roundf(kp.y * sf);
-    const float scaleduR0 = __builtin_roundf(uR0 * sf);
-    const int w = 5, L = 5;
-    const float iniu = scaleduR0 + L - w;
-    const float endu = scaleduR0 + L + w + 1;
-    if (iniu < 0 || endu >= Lv.w) continue;
-    // the reference asserts (cv::Mat::colRange/rowRange) when a patch leaves
-    // the level; unreachable for keypoints >= 16 px inside their level
-    if (scaleduR0 - 2 * w < 0 || scaledvL - w < 0 || scaledvL + w >= Lv.h || scaleduL - w < 0 ||
-        scaleduL + w >= Lv.w)
-      continue;
-    const uint8_t* imL = level_ptr(*G, A.BL, limg, levelL);
-    const uint8_t* imR = level_ptr(*G, A.BR, rimg, levelL);
-    const int lw = Lv.w;
-    const int cy = (int)scaledvL, cxL = (int)scaleduL, cxR0 = (int)scaleduR0;
-    // Stage the 11x11 left patch (columns cxL-5..cxL+5) and the 11x21 right
-    // strip (cxR0-10..cxR0+10) of rows cy-5..cy+5 in this wave's LDS slot:
-    // aligned dword loads, each row keeping its byte shift (rows are packed at
-    // the level width), dwords wholly past a row's bytes not loaded.
-    uint32_t* sp = s_sad[wid];
-    const uint8_t* rowL0 = imL + (size_t)(cy - w) * lw + (cxL - w);
-    const uint8_t* rowR0 = imR + (size_t)(cy - w) * lw + (cxR0 - 2 * w);
-    {
-      uint32_t sv[kSadIt];
-#pragma unroll
-      for (int k = 0; k < kSadIt; k++) {
-        const int q = lane + 64 * k, r = q / kSadDw, j = q - r * kSadDw;
-        const bool left = j < kSadDwL;
-        const uintptr_t a = (uintptr_t)((left ? rowL0 : rowR0) + (size_t)r * lw);
-        const int jj = left ? j : j - kSadDwL, need = left ? 2 * w + 1 : 4 * w + 1;
-        sv[k] = 0;
-        if (q < (2 * w + 1) * kSadDw && 4 * jj < (int)(a & 3) + need) sv[k] = *((const uint32_t*)(a & ~(uintptr_t)3) + jj);
-      }
-#pragma unroll
-      for (int k = 0; k < kSadIt; k++)
-        if (lane + 64 * k < (2 * w + 1) * kSadDw) sp[lane + 64 * k] = sv[k];
+  }
+  const int sad = (int)acc;
+  // first strict minimum over inc = -5..5 (quarter lanes 0..10)
+  const uint32_t skey = row_min_u32(ql < 11 ? ((uint32_t)sad << 4) | (uint32_t)ql : 0xFFFFFFFFu);
+  const int bix = (int)(skey & 15);
+  const int bestSad = (int)(skey >> 4);
+  const int bestinc = bix - L;
+  const int qbase = lane & 48;
+  const float d1 = (float)__shfl(sad, qbase + max(bix - 1, 0), 64);
+  const float d3 = (float)__shfl(sad, qbase + min(bix + 1, 15), 64);
+  if (bestinc == -L || bestinc == L) return;
+  const float d2 = (float)bestSad;
+  const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+  if (deltaR < -1 || deltaR > 1) return;
+  float bestuR = Lv.scale * ((float)scaleduR0 + (float)bestinc + deltaR);
+  float disparity = uL - bestuR;
+  if (disparity >= A.minD && disparity < A.maxD) {
+    if (disparity <= 0) {
+      disparity = 0.01f;
+      bestuR = uL - 0.01f;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint8_t* sb = reinterpret_cast<const uint8_t*>(sp);
-    const uint32_t aL0 = (uint32_t)(uintptr_t)rowL0, aR0 = (uint32_t)(uintptr_t)rowR0;
-    auto lpix = [&](int dy, int dx) -> int { return sb[4 * kSadDw * dy + ((aL0 + (uint32_t)(dy * lw)) & 3) + dx]; };
-    auto rpix = [&](int dy, int dx) -> int {  // strip column dx
-      return sb[4 * (kSadDw * dy + kSadDwL) + ((aR0 + (uint32_t)(dy * lw)) & 3) + dx];
-    };
-    int part = 0;
-#ifndef ORBX_SAD_BYTES
-    {
-      // SAD term |(L - Lc) - (R - Rc)| = |(L + Rc) - (R + Lc)|: both sides in [0, 510], so two
-      // pixels per v_sad_u16 on u16 pairs.  The staged bytes become, in this wave's slot: the left
-      // patch as pairs (2k, 2k+1) (11 x 6 dwords, pad 0) and the strip + Lc twice, as pairs
-      // (2k, 2k+1) and (2k+1, 2k+2) (11 x 11 dwords each), so every lane's pair reads are aligned.
-      // Lanes 0..54: offset s = lane % 11 (inc = s - 5), rows g, g+5, g+10 (g = lane / 11).
-      uint32_t* l16 = s_sw[wid];
-      uint32_t* re16 = l16 + 66;
-      uint32_t* ro16 = re16 + 121;
-      const uint32_t Lc = (uint32_t)lpix(w, w);
-      for (int q = lane; q < 66; q += 64) {
-        const int r = q / 6, k = q - r * 6;
-        l16[q] = (uint32_t)lpix(r, 2 * k) | (2 * k + 1 <= 2 * w ? (uint32_t)lpix(r, 2 * k + 1) << 16 : 0u);
-      }
-      for (int q = lane; q < 121; q += 64) {
-        const int r = q / 11, k = q - r * 11;
-        const uint32_t a = (uint32_t)rpix(r, 2 * k) + Lc;
-        const uint32_t b = (2 * k + 1 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 1) : 0u) + Lc;
-        const uint32_t c = (2 * k + 2 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 2) : 0u) + Lc;
-        re16[q] = a | b << 16;
-        ro16[q] = b | c << 16;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int ll = lane < 55 ? lane : 0;
-      const int so = ll % 11, g = ll / 11;
-      const uint32_t rc = (uint32_t)rpix(w, so + w);  // Rc = strip column inc + 2w
-      const u16x2 rc2 = {(uint16_t)rc, (uint16_t)rc};
-      const uint32_t* rrow = ((so & 1) ? ro16 : re16) + (so >> 1);  // pair (so + 2p, so + 2p + 1) at p
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const int dy = min(g + 5 * k, 2 * w);
-        uint32_t acc = 0;
-#pragma unroll
-        for (int p2 = 0; p2 < 6; p2++) {
-          uint32_t lp = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, l16[dy * 6 + p2]) + rc2);
-          uint32_t rp = rrow[dy * 11 + p2];
-          if (p2 == 5) {  // pixel 11 of the pair does not exist
-            lp &= 0xFFFFu;
-            rp &= 0xFFFFu;
-          }
-          acc = __builtin_amdgcn_sad_u16(lp, rp, acc);
-        }
-        part += (g + 5 * k < 2 * w + 1) ? (int)acc : 0;
-      }
-      if (lane >= 55) part = 0;
-    }
-#else
-    {
-      // lanes 0..54: inc = lane % 11, rows g, g+5, g+10 (g = lane / 11); rows >= 11
-      // clamped and masked
-      const int ll = lane < 55 ? lane : 0;
-      const int inc = ll % 11 - L;
-      const int g = ll / 11;
-      const int cL = lpix(w, w);
-      const int cR = rpix(w, inc + 2 * w);
-      // one row group at a time: 22 staged bytes live instead of 66 (registers bound occupancy)
-#pragma unroll 1
-      for (int k = 0; k < 3; k++) {
-        const int dy = min(g + 5 * k, 2 * w);
-        int pv[2 * w + 1], qv[2 * w + 1];
-#pragma unroll
-        for (int dx = 0; dx < 2 * w + 1; dx++) {
-          pv[dx] = lpix(dy, dx);
-          qv[dx] = rpix(dy, inc + w + dx);
-        }
-        int rowsad = 0;
-#pragma unroll
-        for (int dx = 0; dx < 2 * w + 1; dx++) {
-          const int a = pv[dx] - cL, c = qv[dx] - cR;
-          rowsad += a > c ? a - c : c - a;
-        }
-        part += (g + 5 * k < 2 * w + 1) ? rowsad : 0;
-      }
-      if (lane >= 55) part = 0;
-    }
-#endif
-    const int src = lane < 11 ? lane : 0;
-    int sad = __shfl(part, src, 64) + __shfl(part, src + 11, 64) + __shfl(part, src + 22, 64) +
-              __shfl(part, src + 33, 64) + __shfl(part, src + 44, 64);
-    // first strict minimum over inc = -5..5 (lanes 0..10)
-    uint32_t skey = lane < 11 ? ((uint32_t)sad << 4) | (uint32_t)lane : 0xFFFFFFFFu;
-    skey = wave_min_u32(skey);
-    const int bi = (int)(skey & 15);
-    const int bestSad = (int)(skey >> 4);
-    const int bestinc = bi - L;
-    if (bestinc == -L || bestinc == L) continue;
-    const float d1 = (float)__shfl(sad, bi - 1, 64);
-    const float d2 = (float)bestSad;
-    const float d3 = (float)__shfl(sad, bi + 1, 64);
-    const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
-    if (deltaR < -1 || deltaR > 1) continue;
-    float bestuR = Lv.scale * ((float)scaleduR0 + (float)bestinc + deltaR);
-    float disparity = uL - bestuR;
-    if (disparity >= A.minD && disparity < A.maxD) {
-      if (disparity <= 0) {
-        disparity = 0.01f;
-        bestuR = uL - 0.01f;
-      }
-      if (lane == 0) {
-        *outD = A.bf / disparity;
-        *outU = bestuR;
-        *outS = bestSad;
-      }
+    if (ql == 0) {
+      *outD = A.bf / disparity;
+      *outU = bestuR;
+      *outS = bestSad;
     }
   }
 }
