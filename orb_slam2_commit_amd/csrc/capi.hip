@@ -360,6 +360,38 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
     while (kc > 64 && (long long)octree_smem_host(node_cap, cell_cap, (int)kc) > 160 * 1024 - 1024) kc -= 64;
     G.oct_kcap = (int)kc;
   }
+  // k_octree launch groups: the levels with more than 0.4 x level 0's pixels as 512-thread blocks
+  // with the 50 KB budget above (three per CU), the smaller ones as 256-thread blocks in <= 24 KB
+  // (six per CU: their blocks are short and barrier-bound, so more of them in flight is what pays;
+  // 0.231 -> 0.212 ms per step; 128-thread blocks, other budgets and splits measured no better,
+  // profiles/r04/ab_octree_groups.txt)
+  {
+    const long long P0 = (long long)G.lv[0].w * G.lv[0].h;
+    int split = 1;
+    while (split < p.nlevels && (long long)G.lv[split].w * G.lv[split].h * 10 > 4 * P0) split++;
+    auto group = [&](int l0, int l1, int nt, long long budget, OctGroup& g) {
+      g.l0 = l0;
+      g.l1 = l1;
+      g.nt = nt;
+      g.node_cap = 64;
+      g.cell_cap = 1;
+      int mc = 1;
+      for (int l = l0; l < l1; l++) {
+        g.node_cap = std::max(g.node_cap, (G.lv[l].oct_cap + 63) / 64 * 64);
+        g.cell_cap = std::max(g.cell_cap, G.lv[l].cell_end - G.lv[l].cell_begin);
+        mc = std::max(mc, G.lv[l].cand_cap);
+      }
+      const long long base = (long long)octree_smem_host(g.node_cap, g.cell_cap, 0);
+      long long kc = (budget - 512 - base) / 6;
+      kc = std::max(kc, 1024LL) & ~63LL;
+      kc = std::min(kc, (long long)(mc + 63) / 64 * 64);
+      while (kc > 64 && (long long)octree_smem_host(g.node_cap, g.cell_cap, (int)kc) > 160 * 1024 - 1024) kc -= 64;
+      g.kcap = (int)kc;
+    };
+    G.n_og = 0;
+    group(0, split, 512, 50 * 1024, G.og[G.n_og++]);
+    if (split < p.nlevels) group(split, p.nlevels, 256, 24 * 1024, G.og[G.n_og++]);
+  }
   return ORBX_OK;
 }
 
@@ -449,7 +481,12 @@ orbx_status get_plan(orbx_extractor* h, int W, int H, Plan** out) {
   if (e == hipSuccess && !P->yt.empty())
     e = hipMemcpy(P->dyt.p, P->yt.data(), P->yt.size() * sizeof(ResizeY), hipMemcpyHostToDevice);
   if (e != hipSuccess) return ORBX_ERR_HIP;
-  e = octree_set_smem_limit(octree_smem_host(P->G.node_cap, P->G.cell_cap, P->G.oct_kcap));
+  {
+    size_t mx = 0;
+    for (int g = 0; g < P->G.n_og; g++)
+      mx = std::max(mx, octree_smem_host(P->G.og[g].node_cap, P->G.og[g].cell_cap, P->G.og[g].kcap));
+    e = octree_set_smem_limit(mx);
+  }
   if (e != hipSuccess) return ORBX_ERR_HIP;
   *out = P.get();
   h->plans[key] = std::move(P);

@@ -787,18 +787,19 @@ __host__ __device__ inline size_t octree_smem_bytes(int NC, int cell_cap, int kc
   return b;
 }
 
-// octree block size: the split rounds loop over every candidate of the level
-// (thousands at level 0); 512 threads beat 256 (0.42 -> 0.38 ms per 256 frames),
-// 1024 halves the resident blocks per CU and loses (0.71)
-constexpr int OBS = 512;
-// phase 2 sorts up to this many splittable nodes by rank (M^2 / OBS compares per thread), more by
+// octree block size NT per launch group (Geometry::og): the split rounds loop over every candidate
+// of the level (thousands at levels 0-2: 512 threads there, 512 beat 256 for a single launch, 0.42
+// -> 0.38 ms per 256 frames, and 1024 halved the resident blocks per CU, 0.71); the upper levels
+// run as 256-thread blocks with a smaller LDS footprint, so more of them share a CU
+// phase 2 sorts up to this many splittable nodes by rank (M^2 / NT compares per thread), more by
 // the bitonic network
 constexpr int kOctRankSortMax = 1024;
 
+template <int NT>
 __device__ __forceinline__ void bitonic_sort_desc(uint64_t* k, int n) {
   for (int size = 2; size <= n; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < n / 2; i += OBS) {
+      for (int i = threadIdx.x; i < n / 2; i += NT) {
         const int lo = 2 * i - (i & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;
@@ -842,9 +843,9 @@ struct OctCands {
   }
 };
 
-template <class F>
+template <int NT, class F>
 __device__ __forceinline__ void oct_cands(int T, const OctCands& c, F f) {
-  for (int k = threadIdx.x; k < T; k += OBS) {
+  for (int k = threadIdx.x; k < T; k += NT) {
     const uint32_t n0 = c.nd(k);
     uint32_t n = n0;
     f(k, c.pos(k), n);
@@ -862,15 +863,16 @@ __device__ unsigned int* oct_probe_buf;
 #define OCT_TS(v)
 #endif
 
-__global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k_octree(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
-                                               BatchPtrs B) {
+template <int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void k_octree(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
+                                               BatchPtrs B, OctGroup grp) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   // level-major grid (images fastest): every image's level-0 block (the longest) is dispatched
   // first and the short top levels last, so the kernel's tail is short blocks (longest first;
   // image-major order left one level-0 block per image until the end: 0.302 -> 0.232 ms per step)
-  const int img = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+  const int img = blockIdx.x, l = grp.l0 + blockIdx.y, tid = threadIdx.x;
   const LevelGeom& L = G->lv[l];
-  const int NC = G->node_cap;
+  const int NC = grp.node_cap;
   const int NP2 = next_pow2(NC);
   OctSmem s;
   {
@@ -888,15 +890,15 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     s.sb = (int*)p; p += NC * 4;
     p = (unsigned char*)(((uintptr_t)p + 7) & ~(uintptr_t)7);
     s.key = (uint64_t*)p; p += (size_t)NP2 * 8;
-    s.cpre = (int*)p; p += (G->cell_cap + 1) * 4;
+    s.cpre = (int*)p; p += (grp.cell_cap + 1) * 4;
     s.ctrl = (int*)p; p += 8 * 4;
-    s.kp = (uint32_t*)p; p += (size_t)G->oct_kcap * 4;
+    s.kp = (uint32_t*)p; p += (size_t)grp.kcap * 4;
     s.kn = (uint16_t*)p;
   }
   uint32_t* oct_out = B.oct + (size_t)img * G->oct_total + L.oct_off;
   int* oct_cnt = B.oct_count + (size_t)img * G->nlevels + l;
   const size_t kbase = (size_t)img * G->cand_total + L.cand_begin;
-  OctCands oc{s.kp, s.kn, G->oct_kcap, B.kpos + kbase, (uint32_t*)B.knode + kbase};
+  OctCands oc{s.kp, s.kn, grp.kcap, B.kpos + kbase, (uint32_t*)B.knode + kbase};
 
   OCT_TS(ot0);
 #ifdef ORBX_OCT_PROBE
@@ -905,9 +907,9 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
 #endif
   // 1. candidates of this level in vToDistributeKeys order (cells row-major)
   const int ncl = L.cell_end - L.cell_begin;
-  for (int c = tid; c < ncl; c += OBS) s.cpre[c] = B.cell_count[(size_t)img * G->ncells + L.cell_begin + c];
+  for (int c = tid; c < ncl; c += NT) s.cpre[c] = B.cell_count[(size_t)img * G->ncells + L.cell_begin + c];
   __syncthreads();
-  const int T = block_exclusive_scan<OBS>(s.cpre, ncl);
+  const int T = block_exclusive_scan<NT>(s.cpre, ncl);
   if (tid == 0) s.cpre[ncl] = T;
   if (T == 0) {
     if (tid == 0) *oct_cnt = 0;
@@ -916,7 +918,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   const int nIni = L.nIni;
   const float hX = L.hX;
   const int minBX = L.minBX, minBY = L.minBY;
-  for (int i = tid; i < nIni; i += OBS) s.ccnt[i] = 0;
+  for (int i = tid; i < nIni; i += NT) s.ccnt[i] = 0;
   __syncthreads();
   const uint32_t* cand = B.cand + (size_t)img * G->cand_total;
   auto put_cand = [&](int k, uint32_t v) {
@@ -927,10 +929,10 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     oc.set(k, pos, (uint32_t)root);
     atomicAdd(&s.ccnt[root], 1);
   };
-  if (ncl >= OBS / 2) {
+  if (ncl >= NT / 2) {
     // many cells (the dense levels): one thread per cell walks its survivors (candidate
     // k = cpre[c] + i), four loads in flight at a time
-    for (int c = tid; c < ncl; c += OBS) {
+    for (int c = tid; c < ncl; c += NT) {
       const int k0 = s.cpre[c], n = s.cpre[c + 1] - k0;
       const uint32_t* src = cand + cells[L.cell_begin + c].cand_off;
       int i = 0;
@@ -945,7 +947,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
   } else {
     // few cells with many survivors each: one thread per candidate, its cell by binary search
-    for (int k = tid; k < T; k += OBS) {
+    for (int k = tid; k < T; k += NT) {
       int lo = 0, hi = ncl - 1;  // last c with cpre[c] <= k
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -957,10 +959,10 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   __syncthreads();
   OCT_TS(ot1);
   // 2. roots -> list (empty roots erased, src/ORBextractor.cc:604-615)
-  for (int i = tid; i < nIni; i += OBS) s.sa[i] = s.ccnt[i] > 0 ? 1 : 0;
+  for (int i = tid; i < nIni; i += NT) s.sa[i] = s.ccnt[i] > 0 ? 1 : 0;
   __syncthreads();
-  int S = block_exclusive_scan<OBS>(s.sa, nIni);
-  for (int i = tid; i < nIni; i += OBS) {
+  int S = block_exclusive_scan<NT>(s.sa, nIni);
+  for (int i = tid; i < nIni; i += NT) {
     if (s.ccnt[i] > 0) {
       const int ni = s.sa[i];
       s.x0[ni] = (int16_t)(int)(hX * (float)i);
@@ -973,11 +975,11 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
   }
   __syncthreads();
-  oct_cands(T, oc, [&](int, uint32_t, uint32_t& nd) { nd = (uint32_t)s.nidx[nd]; });
+  oct_cands<NT>(T, oc, [&](int, uint32_t, uint32_t& nd) { nd = (uint32_t)s.nidx[nd]; });
   // child counters of the next round are cleared by the pass that precedes that
   // round's opening barrier (here, and after each round's remap): one barrier
   // per round fewer than a separate clear
-  for (int i = tid; i < S * 4; i += OBS) s.ccnt[i] = 0;
+  for (int i = tid; i < S * 4; i += NT) s.ccnt[i] = 0;
   OCT_TS(ot2);
   int cur = 0;
   int seqBase = nIni;
@@ -1001,7 +1003,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
 #endif
     const int nb = cur ^ 1;
     // kp pass A: child digit of every keypoint whose node splits (count > 1)
-    oct_cands(T, oc, [&](int, uint32_t v, uint32_t& nd) {
+    oct_cands<NT>(T, oc, [&](int, uint32_t v, uint32_t& nd) {
       const int n = (int)(nd & 0x3FFF);
       if ((s.cnt + cur * NC)[n] > 1) {
         const int nx0 = (s.x0 + cur * NC)[n], ny0 = (s.y0 + cur * NC)[n];
@@ -1019,7 +1021,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
       // split every node with > 1 keypoint, in list order.  One scan of packed
       // (children | kept << 16 | expandable children << 32) gives each node its
       // child and kept positions and the round's totals.
-      for (int i = tid; i < S; i += OBS) {
+      for (int i = tid; i < S; i += NT) {
         const bool split = (s.cnt + cur * NC)[i] > 1;
         uint64_t v = split ? 0 : (1ull << 16);
         if (split)
@@ -1030,11 +1032,11 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
         s.key[i] = v;
       }
       __syncthreads();
-      const uint64_t tot = block_scan_excl<OBS, uint64_t>(s.key, S);
+      const uint64_t tot = block_scan_excl<NT, uint64_t>(s.key, S);
       C = (int)(tot & 0xFFFF);
       const int Sg = (int)((tot >> 16) & 0xFFFF);
       const int nexp = (int)(tot >> 32);
-      for (int i = tid; i < S; i += OBS) {
+      for (int i = tid; i < S; i += NT) {
         const uint64_t pre = s.key[i];
         if ((s.cnt + cur * NC)[i] > 1) {
           const int nx0 = (s.x0 + cur * NC)[i], ny0 = (s.y0 + cur * NC)[i], nx1 = (s.x1 + cur * NC)[i], ny1 = (s.y1 + cur * NC)[i];
@@ -1066,12 +1068,12 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
         }
       }
       __syncthreads();  // children / cidx / nidx written before the candidates remap
-      oct_cands(T, oc, [&](int, uint32_t, uint32_t& nd) {
+      oct_cands<NT>(T, oc, [&](int, uint32_t, uint32_t& nd) {
         const int n = (int)(nd & 0x3FFF);
         nd = (uint32_t)((s.cnt + cur * NC)[n] > 1 ? s.cidx[n * 4 + (nd >> 14)] : s.nidx[n]);
       });
       Snew = C + Sg;
-      for (int i = tid; i < Snew * 4; i += OBS) s.ccnt[i] = 0;
+      for (int i = tid; i < Snew * 4; i += NT) s.ccnt[i] = 0;
       seqBase += C;
       const bool finish = Snew >= N || Snew == S;
       S = Snew;
@@ -1080,13 +1082,13 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
       if (Snew + 3 * nexp > N) phase = 2;
     } else {
       // phase 2: split the largest (size, seq) first until the list reaches N
-      for (int i = tid; i < S; i += OBS) s.sa[i] = (s.cnt + cur * NC)[i] > 1 ? 1 : 0;
+      for (int i = tid; i < S; i += NT) s.sa[i] = (s.cnt + cur * NC)[i] > 1 ? 1 : 0;
       __syncthreads();
-      const int M = block_exclusive_scan<OBS>(s.sa, S);
+      const int M = block_exclusive_scan<NT>(s.sa, S);
       const int P2 = next_pow2(max(M, 2));
-      for (int i = tid; i < P2; i += OBS) s.key[i] = 0;
+      for (int i = tid; i < P2; i += NT) s.key[i] = 0;
       __syncthreads();
-      for (int i = tid; i < S; i += OBS)
+      for (int i = tid; i < S; i += NT)
         if ((s.cnt + cur * NC)[i] > 1)
           s.key[s.sa[i]] = ((uint64_t)(s.cnt + cur * NC)[i] << 43) | ((uint64_t)(s.seq + cur * NC)[i] << 13) | (uint64_t)i;
       __syncthreads();
@@ -1094,7 +1096,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
         // descending order by rank (keys are distinct: they carry the node index): key j goes to
         // #{keys > key j}; one pass over the M keys per key instead of log2(P2)^2/2 barrier stages
         uint64_t* tmp = reinterpret_cast<uint64_t*>(s.cidx);  // cidx is rewritten below
-        for (int j = tid; j < M; j += OBS) {
+        for (int j = tid; j < M; j += NT) {
           const uint64_t x = s.key[j];
           int r = 0;
 #pragma unroll 4
@@ -1102,13 +1104,13 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
           tmp[r] = x;
         }
         __syncthreads();
-        for (int j = tid; j < M; j += OBS) s.key[j] = tmp[j];
+        for (int j = tid; j < M; j += NT) s.key[j] = tmp[j];
         __syncthreads();
       } else {
-        bitonic_sort_desc(s.key, P2);
+        bitonic_sort_desc<NT>(s.key, P2);
       }
       if (tid == 0) s.ctrl[1] = M - 1;
-      for (int j = tid; j < M; j += OBS) {
+      for (int j = tid; j < M; j += NT) {
         const int n = (int)(s.key[j] & 0x1FFF);
         int nc = 0;
         for (int d = 0; d < 4; d++) nc += s.ccnt[n * 4 + d] > 0;
@@ -1116,8 +1118,8 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
       }
       __syncthreads();
       // inclusive prefix of growth; first j reaching N
-      block_exclusive_scan<OBS>(s.sb, M);  // exclusive
-      for (int j = tid; j < M; j += OBS) {
+      block_exclusive_scan<NT>(s.sb, M);  // exclusive
+      for (int j = tid; j < M; j += NT) {
         const int n = (int)(s.key[j] & 0x1FFF);
         int nc = 0;
         for (int d = 0; d < 4; d++) nc += s.ccnt[n * 4 + d] > 0;
@@ -1126,7 +1128,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
       __syncthreads();
       const int m = s.ctrl[1];
       // children positions in processing order j = 0..m
-      for (int j = tid; j < M; j += OBS) {
+      for (int j = tid; j < M; j += NT) {
         int nc = 0;
         if (j <= m) {
           const int n = (int)(s.key[j] & 0x1FFF);
@@ -1134,18 +1136,18 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
         }
         s.sb[j] = nc;
       }
-      for (int i = tid; i < S; i += OBS) s.nidx[i] = -1;  // -1: processed marker set below
+      for (int i = tid; i < S; i += NT) s.nidx[i] = -1;  // -1: processed marker set below
       __syncthreads();
-      C = block_exclusive_scan<OBS>(s.sb, M);
-      for (int j = tid; j <= m; j += OBS) {
+      C = block_exclusive_scan<NT>(s.sb, M);
+      for (int j = tid; j <= m; j += NT) {
         const int n = (int)(s.key[j] & 0x1FFF);
         s.nidx[n] = -2;  // processed
       }
       __syncthreads();
-      for (int i = tid; i < S; i += OBS) s.sa[i] = s.nidx[i] == -2 ? 0 : 1;
+      for (int i = tid; i < S; i += NT) s.sa[i] = s.nidx[i] == -2 ? 0 : 1;
       __syncthreads();
-      const int rest = block_exclusive_scan<OBS>(s.sa, S);
-      for (int j = tid; j <= m; j += OBS) {
+      const int rest = block_exclusive_scan<NT>(s.sa, S);
+      for (int j = tid; j <= m; j += NT) {
         const int i = (int)(s.key[j] & 0x1FFF);
         const int nx0 = (s.x0 + cur * NC)[i], ny0 = (s.y0 + cur * NC)[i], nx1 = (s.x1 + cur * NC)[i], ny1 = (s.y1 + cur * NC)[i];
         const int hx = (int)__builtin_ceilf((float)(nx1 - nx0) / 2);
@@ -1165,7 +1167,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
           s.cidx[i * 4 + d] = (int16_t)ni;
         }
       }
-      for (int i = tid; i < S; i += OBS) {
+      for (int i = tid; i < S; i += NT) {
         if (s.nidx[i] == -2) continue;
         const int ni = C + s.sa[i];
         (s.x0 + nb * NC)[ni] = (s.x0 + cur * NC)[i];
@@ -1177,13 +1179,13 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
         s.nidx[i] = (int16_t)ni;
       }
       __syncthreads();
-      oct_cands(T, oc, [&](int, uint32_t, uint32_t& nd) {
+      oct_cands<NT>(T, oc, [&](int, uint32_t, uint32_t& nd) {
         const int n = (int)(nd & 0x3FFF);
         const int ni = s.nidx[n];  // -2: n was split this round
         nd = (uint32_t)(ni == -2 ? s.cidx[n * 4 + (nd >> 14)] : ni);
       });
       Snew = C + rest;
-      for (int i = tid; i < Snew * 4; i += OBS) s.ccnt[i] = 0;
+      for (int i = tid; i < Snew * 4; i += NT) s.ccnt[i] = 0;
       seqBase += C;
       const bool finish = Snew >= N || Snew == S;
       S = Snew;
@@ -1193,9 +1195,9 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   }
   __syncthreads();
   // 3. best response per node: max score, then lowest candidate index
-  for (int i = tid; i < S; i += OBS) s.key[i] = 0;
+  for (int i = tid; i < S; i += NT) s.key[i] = 0;
   __syncthreads();
-  oct_cands(T, oc, [&](int k, uint32_t v, uint32_t& nd) {
+  oct_cands<NT>(T, oc, [&](int k, uint32_t v, uint32_t& nd) {
     const uint32_t x = (v & 0xFFF) + minBX, y = ((v >> 12) & 0xFFF) + minBY;
     const uint64_t key = ((uint64_t)(v >> 24) << 56) | ((uint64_t)(0xFFFFFFu - (uint32_t)k) << 24) |
                          (uint64_t)((y << 12) | x);
@@ -1203,7 +1205,7 @@ __global__ __launch_bounds__(OBS) __attribute__((amdgpu_waves_per_eu(6))) void k
   });
   __syncthreads();
   const int nout = min(S, L.oct_cap);
-  for (int i = tid; i < nout; i += OBS) {
+  for (int i = tid; i < nout; i += NT) {
     const uint64_t key = s.key[i];
     oct_out[i] = ((uint32_t)(key >> 56) << 24) | (uint32_t)(key & 0xFFFFFF);
   }
@@ -1310,7 +1312,18 @@ __device__ __forceinline__ float lane_f(float v, int j) {
 //      SSE2 / scalar-tail rounding of the output column) -> LDS, then the 256 rotated pairs with
 //      pair p in lane p & 63: ballot k = descriptor bits 64k .. 64k+63, staged in LDS;
 //   5. one coalesced store of the kDescK descriptors (lane = dword) and the keypoint records.
-__global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
+#ifndef ORBX_DESC_PAT_LATE
+#define ORBX_DESC_PAT_LATE 0
+#endif
+#ifndef ORBX_DESC_WPE
+#define ORBX_DESC_WPE 0
+#endif
+#if ORBX_DESC_WPE
+#define ORBX_DESC_ATTR __attribute__((amdgpu_waves_per_eu(ORBX_DESC_WPE)))
+#else
+#define ORBX_DESC_ATTR
+#endif
+__global__ __launch_bounds__(BS) ORBX_DESC_ATTR void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                  int32_t* __restrict__ counts, int kp_cap) {
   __shared__ __align__(16) uint8_t s_desc[BS / 64][kDescLds];
@@ -1329,9 +1342,11 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   for (int ll = 0; ll < kMaxLevelsPlan; ll++) total += cnt[ll];
   if (bi.x == 0 && threadIdx.x == 0) counts[img] = total;
   // the rBRIEF pairs of this lane (p = lane + 64k), reused for every keypoint of the wave
+#if !ORBX_DESC_PAT_LATE
   float4 pat[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) pat[k] = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * k];
+#endif
   if (i0 >= total) return;  // wave-uniform: the DPP sums below see a full wave
   const int nk = min(kDescK, total - i0);
   // 1. lane j: keypoint i0 + min(j, nk - 1) (lanes past nk repeat the last one; never written)
@@ -1475,6 +1490,12 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
       M10 = lane == j ? m10 : M10;
     });
   }
+#if ORBX_DESC_PAT_LATE
+  // the rBRIEF pairs of this lane, loaded once the IC boxes' registers are free
+  float4 pat[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) pat[k] = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * k];
+#endif
   // 3. orientation of keypoint j in lane j
   const float angle = fast_atan2((float)M01, (float)M10);
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
@@ -1684,9 +1705,16 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
     T->end(ST_BLUR, st);
   }
   if (Gh.ncells > 0) {
-    const size_t smem = octree_smem_bytes(Gh.node_cap, Gh.cell_cap, Gh.oct_kcap);
     T->begin(st);
-    hipLaunchKernelGGL(k_octree, dim3(n_img, Gh.nlevels), dim3(OBS), smem, st, Gd, cells, B);
+    // (launch order of the groups measured flat)
+    for (int gi = 0; gi < Gh.n_og; gi++) {
+      const OctGroup& og = Gh.og[gi];
+      const size_t smem = octree_smem_bytes(og.node_cap, og.cell_cap, og.kcap);
+      if (og.nt == 512)
+        hipLaunchKernelGGL(k_octree<512>, dim3(n_img, og.l1 - og.l0), dim3(512), smem, st, Gd, cells, B, og);
+      else
+        hipLaunchKernelGGL(k_octree<256>, dim3(n_img, og.l1 - og.l0), dim3(256), smem, st, Gd, cells, B, og);
+    }
     T->end(ST_OCTREE, st);
   }
   const int nb = (Gh.max_kps + BS / 64 * kDescK - 1) / (BS / 64 * kDescK);  // kDescK keypoints per wave
@@ -1706,7 +1734,9 @@ hipError_t launch_blur(const Geometry& Gh, const Geometry* Gd, const int* tile_l
 size_t octree_smem_host(int NC, int cell_cap, int kcap) { return octree_smem_bytes(NC, cell_cap, kcap); }
 
 hipError_t octree_set_smem_limit(size_t bytes) {
-  return hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  hipError_t e = hipFuncSetAttribute((const void*)k_octree<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_octree<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 }  // namespace orbx

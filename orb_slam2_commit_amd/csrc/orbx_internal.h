@@ -42,6 +42,14 @@ struct LevelGeom {
   int tile_begin, tiles_x, tiles_y;  // blur tiles
 };
 
+// k_octree launch group: levels [l0, l1) as NT-thread blocks with LDS sized for those levels
+struct OctGroup {
+  int l0, l1, nt;
+  int node_cap;  // LDS node capacity (max over the group's levels, multiple of 64)
+  int cell_cap;  // max cells of one level
+  int kcap;      // candidates of a level kept in LDS (the rest in global scratch)
+};
+
 struct Geometry {
   int nlevels, width, height;
   int ini_th, min_th;
@@ -51,6 +59,8 @@ struct Geometry {
   int node_cap;   // octree LDS node capacity (max over levels, multiple of 64)
   int cell_cap;   // max cells in one level
   int oct_kcap;   // octree: candidates of a level kept in LDS (the rest in global scratch)
+  OctGroup og[2];  // k_octree launch groups (levels 0..split-1 at 512 threads, the rest at 256)
+  int n_og;
   // k_fast launch groups (consecutive cell ranges, one launch each) with their LDS layout, sized by
   // the group's largest cell: row stride s of the window tile and the score map (40, 48 or 80),
   // region rows per compass instruction rp (2 when the group's cells are <= 32 wide)
