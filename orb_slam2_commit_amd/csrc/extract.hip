@@ -1312,18 +1312,7 @@ __device__ __forceinline__ float lane_f(float v, int j) {
 //      SSE2 / scalar-tail rounding of the output column) -> LDS, then the 256 rotated pairs with
 //      pair p in lane p & 63: ballot k = descriptor bits 64k .. 64k+63, staged in LDS;
 //   5. one coalesced store of the kDescK descriptors (lane = dword) and the keypoint records.
-#ifndef ORBX_DESC_PAT_LATE
-#define ORBX_DESC_PAT_LATE 0
-#endif
-#ifndef ORBX_DESC_WPE
-#define ORBX_DESC_WPE 0
-#endif
-#if ORBX_DESC_WPE
-#define ORBX_DESC_ATTR __attribute__((amdgpu_waves_per_eu(ORBX_DESC_WPE)))
-#else
-#define ORBX_DESC_ATTR
-#endif
-__global__ __launch_bounds__(BS) ORBX_DESC_ATTR void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
+__global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                  int32_t* __restrict__ counts, int kp_cap) {
   __shared__ __align__(16) uint8_t s_desc[BS / 64][kDescLds];
@@ -1342,11 +1331,9 @@ __global__ __launch_bounds__(BS) ORBX_DESC_ATTR void k_describe(const Geometry* 
   for (int ll = 0; ll < kMaxLevelsPlan; ll++) total += cnt[ll];
   if (bi.x == 0 && threadIdx.x == 0) counts[img] = total;
   // the rBRIEF pairs of this lane (p = lane + 64k), reused for every keypoint of the wave
-#if !ORBX_DESC_PAT_LATE
   float4 pat[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) pat[k] = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * k];
-#endif
   if (i0 >= total) return;  // wave-uniform: the DPP sums below see a full wave
   const int nk = min(kDescK, total - i0);
   // 1. lane j: keypoint i0 + min(j, nk - 1) (lanes past nk repeat the last one; never written)
@@ -1490,12 +1477,6 @@ __global__ __launch_bounds__(BS) ORBX_DESC_ATTR void k_describe(const Geometry* 
       M10 = lane == j ? m10 : M10;
     });
   }
-#if ORBX_DESC_PAT_LATE
-  // the rBRIEF pairs of this lane, loaded once the IC boxes' registers are free
-  float4 pat[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) pat[k] = reinterpret_cast<const float4*>(c_pattern_f)[lane + 64 * k];
-#endif
   // 3. orientation of keypoint j in lane j
   const float angle = fast_atan2((float)M01, (float)M10);
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
