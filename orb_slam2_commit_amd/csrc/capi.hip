@@ -335,6 +335,10 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
     }
   }
   if (G.rz_rows > kRzMaxRows || (size_t)G.rz_rows * (G.rz_stride + 2 * kRzTW) > 64 * 1024) return ORBX_ERR_SIZE;
+  G.rz_lc = 0;
+  while ((1 << G.rz_lc) < G.rz_stride / 16) G.rz_lc++;
+  // every footprint row must be loaded: rows per thread = ceil(rz_rows / (256 >> rz_lc)) <= the kernel's 4
+  if (G.rz_lc > 8 || (G.rz_rows + (256 >> G.rz_lc) - 1) / (256 >> G.rz_lc) > (kRzMaxRows + 15) / 16) return ORBX_ERR_SIZE;
   G.pyr_bytes = (pyr + 255) & ~255LL;
   G.blur_bytes = (blur + 255) & ~255LL;
   G.ncells = (int)P.cells.size();

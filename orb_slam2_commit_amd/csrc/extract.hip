@@ -191,40 +191,37 @@ __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, c
     const int i = (tid + k * BS) / (kRzTW / 4);
     yv[k] = Y[i < ny ? i : 0];
   }
-  // 1. footprint -> LDS (up to kRzLd chunk loads per thread issued before their LDS stores)
+  // 1. footprint -> LDS: lane = (row, 16-B chunk) with a power-of-two lane count per row (the
+  //    widest span's chunks; no division), all of a thread's chunk loads issued before their stores
   {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, swh, 0x00020000);
-    const int nch = (span + 15) >> 4, total = nrows * nch;
-    constexpr int kRzLd = 4;
-    for (int q0 = 0; q0 < total; q0 += kRzLd * BS) {
-      uint4 v[kRzLd];
+    const int nch = (span + 15) >> 4;
+    const int lc = G->rz_lc;  // log2(chunk lanes per row)
+    const int c = tid & ((1 << lc) - 1), r0 = tid >> lc, rstep = BS >> lc;
+    constexpr int kRzLd = (kRzMaxRows + 15) / 16;  // >= rows per thread when >= 16 rows per step
+    uint4 v[kRzLd];
 #pragma unroll
-      for (int u = 0; u < kRzLd; u++) {
-        const int q = q0 + u * BS + tid;
-        v[u] = make_uint4(0, 0, 0, 0);
-        if (q < total) {
-          const int r = q / nch, c = q - r * nch;
-          const int o = (ry0 + r) * S.w + cx0 + 16 * c;
-          if (o + 16 <= swh) {
-            const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-            v[u] = make_uint4(t[0], t[1], t[2], t[3]);
-          } else {  // last bytes of the level: byte loads, each range-checked (outside -> 0, never used)
-            uint32_t w4[4] = {0, 0, 0, 0};
+    for (int u = 0; u < kRzLd; u++) {
+      const int r = r0 + u * rstep;
+      const int o = (ry0 + r) * S.w + cx0 + 16 * c;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (r < nrows && c < nch) {
+        if (o + 16 <= swh) {
+          const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+          v[u] = make_uint4(t[0], t[1], t[2], t[3]);
+        } else {  // last bytes of the level: byte loads, each range-checked (outside -> 0, never used)
+          uint32_t w4[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int b = 0; b < 16; b++)
-              w4[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + b, 0, 0) << (8 * (b & 3));
-            v[u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-          }
+          for (int b = 0; b < 16; b++)
+            w4[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + b, 0, 0) << (8 * (b & 3));
+          v[u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
       }
+    }
 #pragma unroll
-      for (int u = 0; u < kRzLd; u++) {
-        const int q = q0 + u * BS + tid;
-        if (q < total) {
-          const int r = q / nch, c = q - r * nch;
-          *(uint4*)&tin[r * stride + 16 * c] = v[u];
-        }
-      }
+    for (int u = 0; u < kRzLd; u++) {
+      const int r = r0 + u * rstep;
+      if (r < nrows && c < nch) *(uint4*)&tin[r * stride + 16 * c] = v[u];
     }
   }
   __syncthreads();

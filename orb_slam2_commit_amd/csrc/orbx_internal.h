@@ -70,6 +70,7 @@ struct Geometry {
   int n_fg;
   int rz_rows;    // k_resize: max source rows staged per 128x16 output tile
   int rz_stride;  // k_resize: LDS row stride of the staged footprint (16-B chunks covering the widest span)
+  int rz_lc;      // k_resize: log2 of the lanes per footprint row (>= the widest span's 16-B chunks)
 };
 
 constexpr int kRzTW = 128, kRzTH = 32;  // k_resize output tile

@@ -130,3 +130,50 @@ def test_bench_batch_slots_match_oracle(gpu):
         assert np.array_equal(uR[f, :nL].view(np.uint32), ouR.view(np.uint32)), f
         assert np.array_equal(dep[f, :nL].view(np.uint32), odep.view(np.uint32)), f
         assert int(nm[f]) == int((ouR >= 0).sum()), f
+
+
+def test_stereo_frames_device_ragged(gpu):
+    """A device batch with ragged and empty frames: a blank left image (no left keypoints), a blank
+    right image (every left keypoint unmatched), a low-texture pair (a left count that is no multiple
+    of the 16 keypoints a match block takes) beside a textured pair -- each frame equal to the oracle,
+    the empty ones writing nothing past their counts and zero matches."""
+    import torch
+    w, h = 1241, 376
+    blank = np.full((h, w), 128, np.uint8)
+    L0, R0 = synth.stereo_pair(61, w, h)
+    L3, R3 = synth.stereo_pair(62, w, h)
+    rng = np.random.default_rng(9)
+    soft = (blank.astype(np.int16) + rng.integers(-12, 13, (h, w))).clip(0, 255).astype(np.uint8)
+    pairs = [(L0, R0), (blank, R0), (L0, blank), (soft, np.roll(soft, -7, axis=1)), (L3, R3)]
+    n = len(pairs)
+    imgs = np.stack([im for pr in pairs for im in pr])
+    ex = ORBextractor(2000, 1.2, 8, 20, 7)
+    cap = ex.max_keypoints(w, h)
+    d = torch.from_numpy(imgs).to(gpu)
+    kps = torch.zeros((2 * n, cap, 28), dtype=torch.uint8, device=gpu)
+    desc = torch.zeros((2 * n, cap, 32), dtype=torch.uint8, device=gpu)
+    cnt = torch.zeros(2 * n, dtype=torch.int32, device=gpu)
+    uR = torch.full((n, cap), 7.0, dtype=torch.float32, device=gpu)
+    dep = torch.full((n, cap), 7.0, dtype=torch.float32, device=gpu)
+    nm = torch.full((n,), -5, dtype=torch.int32, device=gpu)
+    ex.stereo_frames_device(d, kps, desc, cnt, KITTI_BF, KITTI_BF / KITTI_FX, uR, dep, nm,
+                            torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    p = oracle.params(2000, 1.2, 8, 20, 7)
+    cnt_h, uR_h, dep_h, nm_h = cnt.cpu().numpy(), uR.cpu().numpy(), dep.cpu().numpy(), nm.cpu().numpy()
+    counts = []
+    for f in range(n):
+        oL, oR = oracle.extract(p, pairs[f][0]), oracle.extract(p, pairs[f][1])
+        nL = int(cnt_h[2 * f])
+        assert nL == len(oL.keypoints) and int(cnt_h[2 * f + 1]) == len(oR.keypoints), f
+        counts.append((nL, len(oR.keypoints)))
+        if nL:
+            ouR, odep = oracle.stereo_match(p, oL, oR, KITTI_BF, KITTI_BF / KITTI_FX)
+            assert np.array_equal(uR_h[f, :nL].view(np.uint32), ouR.view(np.uint32)), f
+            assert np.array_equal(dep_h[f, :nL].view(np.uint32), odep.view(np.uint32)), f
+            assert int(nm_h[f]) == int((ouR >= 0).sum()), f
+        else:
+            assert int(nm_h[f]) == 0, f
+        assert (uR_h[f, nL:] == 7.0).all() and (dep_h[f, nL:] == 7.0).all(), f  # nothing past the count
+    assert counts[1][0] == 0 and counts[2][1] == 0 and int(nm_h[2]) == 0
+    assert counts[3][0] % 16 != 0 or counts[0][0] % 16 != 0
