@@ -25,6 +25,11 @@ def load(path, counter):
     return acc
 
 
+# bench stages timed as ONE event per step though they run as several launches (k_fast: LDS launch
+# groups; k_octree: level groups; k_describe: k_orient + k_rbrief): bytes summed over the step
+STEP_STAGES = ("k_fast", "k_octree", "k_describe")
+
+
 def main(d, head, batch="256"):
     f = load(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     w = load(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -33,13 +38,13 @@ def main(d, head, batch="256"):
     for k in sorted(set(f) | set(w)):
         n = max(len(f.get(k, [])), len(w.get(k, [])), 1)
         total = 2.0 * sum(f.get(k, [])) * 1024 + sum(w.get(k, [])) * 1024
-        per_event = total / steps if k == "k_fast" else total / n
+        per_event = total / steps if k in STEP_STAGES else total / n
         out[k] = int(per_event)
         disp[k] = n
     json.dump(dict(source="tools/traffic_now.sh + tools/traffic_json.py", head=head, batch=int(batch),
                    per_launch_bytes=out, dispatches=disp, steps=steps,
-                   note="2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per bench stage event (k_fast: per step, "
-                        "summed over its launch groups; others: per dispatch)"), sys.stdout, indent=1)
+                   note="2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per bench stage event (k_fast, k_octree, "
+                        "k_describe: per step, summed over their launches; others: per dispatch)"), sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
