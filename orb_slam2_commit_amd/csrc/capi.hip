@@ -165,9 +165,12 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
     if (L.w < 1 || L.h < 1 || L.w > 4095 || L.h > 4095) return ORBX_ERR_SIZE;
     L.off = l == 0 ? 0 : pyr;
     if (l > 0) pyr += (long long)L.w * L.h;
+    // blurred level: tiles of 8 rows x 16 bytes (128 B), tile (ty, tx) at (ty * bstride/16 + tx) * 128,
+    // row y of a tile at 16 * (y & 7): a 37x37 patch k_describe gathers covers 5-6 x 3-4 such
+    // 128-B tiles (~20) against ~48 128-B lines in a row-major layout
     L.bstride = (L.w + 15) & ~15;
     L.boff = blur;
-    blur += ((long long)L.bstride * L.h + 255) & ~255LL;
+    blur += ((long long)L.bstride * ((L.h + 7) & ~7) + 255) & ~255LL;
     L.minBX = L.minBY = kEdgeThresholdHost - 3;
     L.maxBX = L.w - kEdgeThresholdHost + 3;
     L.maxBY = L.h - kEdgeThresholdHost + 3;
@@ -1003,7 +1006,12 @@ extern "C" long long orbx_debug_copy(orbx_extractor* h, int what, int image, int
             hipStreamSynchronize(h->stream) != hipSuccess)
           return ORBX_ERR_HIP;
         const uint8_t* b = h->blur.p + (size_t)image * G.blur_bytes + L.boff;
-        if (hipMemcpy2D(dst, L.w, b, L.bstride, L.w, L.h, hipMemcpyDeviceToHost) != hipSuccess) return ORBX_ERR_HIP;
+        std::vector<uint8_t> tiles((size_t)L.bstride * ((L.h + 7) & ~7));
+        if (hipMemcpy(tiles.data(), b, tiles.size(), hipMemcpyDeviceToHost) != hipSuccess) return ORBX_ERR_HIP;
+        uint8_t* o = static_cast<uint8_t*>(dst);
+        for (int yy = 0; yy < L.h; yy++)
+          for (int xx = 0; xx < L.w; xx++)
+            o[(size_t)yy * L.w + xx] = tiles[((size_t)(yy >> 3) * (L.bstride >> 4) + (xx >> 4)) * 128 + (yy & 7) * 16 + (xx & 15)];
       }
       return (long long)bytes;
     }

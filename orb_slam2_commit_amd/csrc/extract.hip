@@ -287,10 +287,17 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 // partial sum is an integer multiple of 2^-16 below 2^8, exact in f32), rounded
 // by the 1.5*2^23 add and packed by byte permutes: ~10 VALU per output (18.6
 // with per-column byte aligns, v_rndne / v_med3 / v_cvt_pk_u8 per output; the
-// kernel is VALU-issue-bound).
+// kernel is VALU-issue-bound).  A strip's 16 packed output dwords stay in
+// registers until the whole tile is done, then go through the (no longer
+// needed) input tile in LDS in the tiled blurred-level order (8x16-B tiles)
+// and out as whole 128-B tiles of b128 stores.  7 waves per SIMD: 68 VGPRs,
+// no scratch (8 spills 12 B per lane for the same time, profiles/r04/ab_blur_tiled.txt).
 constexpr int kBIn = kBlurTileW + 16;  // input tile row stride (bytes, 16-B multiple)
 constexpr int kBStrip = 16;            // output rows per thread
-__global__ __launch_bounds__(BS, 8) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
+#ifndef ORBX_BLUR_WPE
+#define ORBX_BLUR_WPE 7
+#endif
+__global__ __launch_bounds__(BS, ORBX_BLUR_WPE) void k_blur(const Geometry* __restrict__ G, const int* __restrict__ tile_level,
                                              BatchPtrs B) {
   constexpr int TR = kBlurTileH + 6;
   __shared__ __align__(16) uint8_t tin[(TR + 1) * kBIn];
@@ -373,7 +380,9 @@ __global__ __launch_bounds__(BS, 8) void k_blur(const Geometry* __restrict__ G, 
   const int g = tid & (kBlurTileW / 4 - 1);
   const int ys = (tid / (kBlurTileW / 4)) * kBStrip;  // strip's first output row in the tile
   const int xg = x0 + 4 * g;
-  if (xg >= w || y0 + ys >= h) return;
+  // (threads past the level compute nothing but stay for the barriers of the tile write-out)
+  const bool active = xg < w && y0 + ys < h;
+  uint32_t outv[kBStrip];
   const uint32_t k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
   // horizontal taps as byte dot products (exact integers, weights < 256) straight on the three
   // aligned dwords [a b c] = tile bytes 4g .. 4g+11: output col j of the group takes bytes
@@ -405,15 +414,13 @@ __global__ __launch_bounds__(BS, 8) void k_blur(const Geometry* __restrict__ G, 
   };
   // 7-row ring indexed by compile-time (r + i) % 7 in the unrolled loop: no register moves
   float2v win[7][2];
+  if (active) {
 #pragma unroll
   for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
   const int simd_w = w & ~3;
   const bool all_simd = xg + 3 < simd_w;  // the whole group takes the SSE2 rounding
   const bool full = xg + 4 <= w;
-  // stores through a buffer resource over the level's blurred rows: rows past h fall outside
-  // num_records and are dropped; the row step is a scalar offset
-  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, h * bs, 0x00020000);
-  const uint32_t voff = (uint32_t)((y0 + ys) * bs + xg);
+
 #pragma unroll
   for (int r = 0; r < kBStrip; r++) {
     rowsum(ys + r + 6, win[(r + 6) % 7]);
@@ -452,10 +459,35 @@ __global__ __launch_bounds__(BS, 8) void k_blur(const Geometry* __restrict__ G, 
         }
       }
     }
-    if (full) {
-      __builtin_amdgcn_raw_buffer_store_b32(packed, rd, voff, r * bs, 0);
-    } else {
-      for (int j = 0; j < w - xg; j++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(packed >> (8 * j)), rd, voff + j, r * bs, 0);
+    outv[r] = packed;
+  }
+  }  // active
+  // Write-out in the level's tile layout (8 rows x 16 bytes = 128-B tiles, the layout k_describe
+  // gathers from): the outputs go to LDS (the input tile is no longer read) in tile order, then
+  // leave as whole 128-B lines, 16 B per lane: the block's 128 x 128 outputs are 16 tile rows of
+  // 8 consecutive tiles (1 KB each).  Columns past w and rows past h land in the level's padding.
+  __syncthreads();
+  if (active) {
+#pragma unroll
+    for (int r = 0; r < kBStrip; r++) {
+      const int yr = ys + r, c = 4 * g;
+      *(uint32_t*)&tin[((yr >> 3) * (kBlurTileW / 16) + (c >> 4)) * 128 + (yr & 7) * 16 + (c & 15)] = outv[r];
+    }
+  }
+  __syncthreads();
+  {
+    const int ntx = bs >> 4, nty = (h + 7) >> 3;
+    const int tx0 = x0 >> 4, ty0 = y0 >> 3;
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, nty * ntx * 128, 0x00020000);
+    constexpr int kTiles = (kBlurTileW / 16) * (kBlurTileH / 8), kChunks = kTiles * 8;  // 16-B chunks
+#pragma unroll
+    for (int k = 0; k < kChunks / BS; k++) {
+      const int q = tid + k * BS, t = q >> 3, tr = t / (kBlurTileW / 16), tc = t - tr * (kBlurTileW / 16);
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *(const u32x4*)&tin[q * 16];
+      if (tx0 + tc < ntx && ty0 + tr < nty)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rd, (uint32_t)(((ty0 + tr) * ntx + tx0 + tc) * 128 + (q & 7) * 16), 0, 0);
     }
   }
 }
@@ -1376,7 +1408,7 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   // the blurred level's patch: rows y-18..y+18, 16-B chunks from the 16-aligned column x0
   const int bs = L.bstride;
   const int x0 = (x - kPatchR) & ~15;
-  const uint8_t* pbl = B.blur + (size_t)img * G->blur_bytes + L.boff + (size_t)(y - kPatchR) * bs + x0;
+  const uint8_t* pbl = B.blur + (size_t)img * G->blur_bytes + L.boff;  // the level's tiles
   constexpr int PS = kPS;
   const uint32_t corr_l = (uint32_t)(kPatchR * PS + (x - x0)) - (0x400000u * (uint32_t)PS + 0x4B400000u);
 #endif
@@ -1401,18 +1433,20 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   int pdst[2][kPatchLd];  // LDS byte offset of each loaded chunk (-1: none)
   auto load_patch = [&](int j, uint32_t (&dst)[kPatchLd][4], int (&dofs)[kPatchLd]) {
 #if !ORBX_DESC_FUSED
-    const int bsj = __builtin_amdgcn_readlane(bs, j);
-    const int aj = (__builtin_amdgcn_readlane(x, j) - kPatchR) & 15;
+    const int bt8 = __builtin_amdgcn_readlane(bs, j) * 8, hj = __builtin_amdgcn_readlane(h, j);
+    const int xj = __builtin_amdgcn_readlane(x, j), y0j = __builtin_amdgcn_readlane(y, j) - kPatchR;
+    const int aj = (xj - kPatchR) & 15, tx0 = (xj - kPatchR) >> 4;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)lane_ptr(pbl, j), (short)0, kPatchRows * bsj, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)lane_ptr(pbl, j), (short)0, ((hj + 7) >> 3) * bt8, 0x00020000);
 #pragma unroll
     for (int k = 0; k < kPatchLd; k++) {
-      // 16-B chunks from a 16-aligned column: with the 16-byte row stride a chunk is wholly inside
-      // its row or wholly past the row's end (and, in the last row, past num_records: zeros)
+      // 16-B chunks at 16-aligned columns: each is one row of an 8 x 16 tile (blur_tile_off), so the
+      // chunks of eight patch rows in a column share one 128-B line
       const int lo = (kPatchR + aj - shw[k]) >> 4, hi = (kPatchR + aj + shw[k]) >> 4;
       const int ch = lo + skk[k];
       const bool ok = srow[k] >= 0 && ch <= hi;
-      const uint32_t off = ok ? (uint32_t)(srow[k] * bsj + 16 * ch) : 0x80000000u;
+      const int yy = y0j + srow[k];
+      const uint32_t off = ok ? (uint32_t)((yy >> 3) * bt8 + (tx0 + ch) * 128 + (yy & 7) * 16) : 0x80000000u;
       dofs[k] = ok ? srow[k] * kPS + 16 * ch : -1;
       const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
       dst[k][0] = t[0];

@@ -4,7 +4,8 @@
 // HBM layout per image (all u8, row-major, stride = level width):
 //   level 0            : the caller's input image itself (never copied)
 //   pyramid  (levels>=1): pyr  + img*pyr_bytes  + lv[l].off
-//   blurred  (all levels): blur + img*blur_bytes + lv[l].boff, row stride lv[l].bstride
+//   blurred  (all levels): blur + img*blur_bytes + lv[l].boff, 8x16-byte tiles (128 B each),
+//                          tile (ty, tx) at (ty * bstride/16 + tx) * 128, row y&7 at 16 * (y & 7)
 //   FAST candidates     : cand + img*cand_total + cells[c].cand_off   (u32 score<<24|y<<12|x)
 //   octree output       : oct  + img*oct_total  + lv[l].oct_off        (same packing, list order)
 #pragma once
@@ -28,7 +29,7 @@ struct LevelGeom {
   int w, h;
   long long off;    // offset of level in per-image pyramid buffer (levels >= 1)
   long long boff;   // offset of level in per-image blurred buffer (256-B aligned)
-  int bstride;      // blurred row stride (multiple of 16 bytes)
+  int bstride;      // blurred level width rounded to 16 (tile columns = bstride / 16)
   int minBX, minBY, maxBX, maxBY;  // FAST border box, src/ORBextractor.cc:829-832
   int cell_begin, cell_end;        // range in the cell table (row-major)
   int cand_begin, cand_cap;        // candidate slots of the level in the per-image buffer

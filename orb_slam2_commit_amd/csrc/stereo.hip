@@ -144,7 +144,7 @@ constexpr int kSadDwL = 4, kSadDwR = 6, kSadDw = kSadDwL + kSadDwR;
 // |(L - Lc) - (R - Rc)| = |(L + Rc) - (R + Lc)| on u16 pairs (two pixels per v_sad_u16), lane
 // s < 11 of the quarter summing offset s - 5 over the 11 rows; parabola; depth.  Quarter
 // reductions are DPP row rotations (a DPP row is 16 lanes); a quarter leaves early on its own
-// (its lanes agree).  LDS 26.1 KB per block: 6 blocks (24 waves) per CU.
+// (its lanes agree).  LDS 19.0 KB per block: 8 blocks (32 waves) per CU.
 __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {  // min over the lane's 16-lane row
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
@@ -153,10 +153,10 @@ __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {  // min over the l
   return v;
 }
 
-__global__ __launch_bounds__(SBS, 6) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
+__global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
   constexpr int NQ = SBS / 16;                // quarters (keypoints) per block
   __shared__ uint32_t s_raw[NQ][11 * kSadDw];  // per quarter: 11 rows x (4 left + 6 right) dwords
-  __shared__ uint32_t s_sw[NQ][66 + 2 * 121];  // per quarter: u16-pair forms of the patch and strip
+  __shared__ uint32_t s_sw[NQ][66 + 121];  // per quarter: u16-pair forms of the patch and strip
   const int2 bi = xcd_block2();
   const int f = bi.y, tid = threadIdx.x, lane = tid & 63, ql = lane & 15, qb = tid >> 4;
   const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
@@ -263,7 +263,6 @@ __global__ __launch_bounds__(SBS, 6) void k_stereo_match(StereoArgs A, const Geo
   };
   uint32_t* l16 = s_sw[qb];
   uint32_t* re16 = l16 + 66;
-  uint32_t* ro16 = re16 + 121;
   const uint32_t Lc = (uint32_t)lpix(w, w);
   for (int q = ql; q < 66; q += 16) {
     const int r = q / 6, k = q - r * 6;
@@ -273,9 +272,7 @@ __global__ __launch_bounds__(SBS, 6) void k_stereo_match(StereoArgs A, const Geo
     const int r = q / 11, k = q - r * 11;
     const uint32_t a = (uint32_t)rpix(r, 2 * k) + Lc;
     const uint32_t b = (2 * k + 1 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 1) : 0u) + Lc;
-    const uint32_t c = (2 * k + 2 <= 4 * w ? (uint32_t)rpix(r, 2 * k + 2) : 0u) + Lc;
     re16[q] = a | b << 16;
-    ro16[q] = b | c << 16;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -283,14 +280,20 @@ __global__ __launch_bounds__(SBS, 6) void k_stereo_match(StereoArgs A, const Geo
   const int so = ql < 11 ? ql : 0;
   const uint32_t rc = (uint32_t)rpix(w, so + w);  // Rc = strip column inc + 2w
   const u16x2 rc2 = {(uint16_t)rc, (uint16_t)rc};
-  const uint32_t* rrow = ((so & 1) ? ro16 : re16) + (so >> 1);
+  // strip pairs (so + 2p, so + 2p + 1): the even-aligned pairs re16[so/2 + p] themselves, or for an odd
+  // offset the middle halves of two neighbours (one v_alignbyte; the odd-aligned copy is not stored)
+  const uint32_t* rrow = re16 + (so >> 1);
+  const uint32_t sh = (uint32_t)(so & 1) * 2;
   uint32_t acc = 0;
 #pragma unroll
   for (int dy = 0; dy < 2 * w + 1; dy++) {
+    uint32_t wv[7];
+#pragma unroll
+    for (int t = 0; t < 7; t++) wv[t] = rrow[dy * 11 + t];  // (the 7th may run into the next row: used only when odd)
 #pragma unroll
     for (int p2 = 0; p2 < 6; p2++) {
       uint32_t lp = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, l16[dy * 6 + p2]) + rc2);
-      uint32_t rp = rrow[dy * 11 + p2];
+      uint32_t rp = __builtin_amdgcn_alignbyte(wv[p2 + 1], wv[p2], sh);
       if (p2 == 5) {
         lp &= 0xFFFFu;
         rp &= 0xFFFFu;
