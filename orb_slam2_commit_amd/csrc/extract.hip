@@ -419,6 +419,8 @@ __global__ __launch_bounds__(BS, ORBX_BLUR_WPE) void k_blur(const Geometry* __re
   for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
   const int simd_w = w & ~3;
   const bool all_simd = xg + 3 < simd_w;  // the whole group takes the SSE2 rounding
+  // wave-uniform: the per-row tail fix-up below is a scalar branch (no exec-mask juggling per row)
+  const bool wave_tail = __builtin_amdgcn_ballot_w64(!all_simd) != 0;
   const bool full = xg + 4 <= w;
 
 #pragma unroll
@@ -448,15 +450,14 @@ __global__ __launch_bounds__(BS, ORBX_BLUR_WPE) void k_blur(const Geometry* __re
     p01 = __builtin_elementwise_min(p01, cap);
     p23 = __builtin_elementwise_min(p23, cap);
     uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01), 0x06040200u);
-    if (!all_simd) {
-      // the row's scalar tail (x >= w & ~3): (acc + 2^15) >> 16
+    if (wave_tail) {
+      // the row's scalar tail (x >= w & ~3): (acc + 2^15) >> 16, selected per lane and column
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        if (xg + j >= simd_w) {
-          const float aj = j == 0 ? acc[0].x : j == 1 ? acc[0].y : j == 2 ? acc[1].x : acc[1].y;
-          const int v = min(((int)(aj * 65536.f) + (1 << 15)) >> 16, 255);
-          packed = (packed & ~(0xFFu << (8 * j))) | ((uint32_t)v << (8 * j));
-        }
+        const float aj = j == 0 ? acc[0].x : j == 1 ? acc[0].y : j == 2 ? acc[1].x : acc[1].y;
+        const int v = min(((int)(aj * 65536.f) + (1 << 15)) >> 16, 255);
+        const uint32_t fixed = (packed & ~(0xFFu << (8 * j))) | ((uint32_t)v << (8 * j));
+        packed = xg + j >= simd_w ? fixed : packed;
       }
     }
     outv[r] = packed;
