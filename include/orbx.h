@@ -399,6 +399,19 @@ orbx_status orbx_pnp_iterate_many(orbx_pnp* const* solvers, int n, int n_iterati
  *                        bestIdx when bestDist <= TH_LOW, *nmatches = nFused.  The caller then
  *                        applies Replace/AddObservation in point order, :1057-1086, re-querying
  *                        any later point whose descriptor a Replace recomputed)
+ *   ORBX_PROJ_SIM3       SearchByProjection(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&,
+ *                        vector<MapPoint*>& vpMatched, th)   src/ORBmatcher.cc:327-440
+ *                        (LoopClosing::ComputeSim3, src/LoopClosing.cc:504; f = the KeyFrame with
+ *                        f.Tcw = the 4x4 Sim3 Scw, bounds = its int mnMinX.. as float; occ[i] != 0 =
+ *                        vpMatched[i] on entry; flags bit0 = !isBad() && not in vpMatched;
+ *                        frame_out[i] = k: vpMatched[i] = point k; *nmatches = nmatches)
+ *   ORBX_PROJ_FUSE_SIM3  the matching half of Fuse(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&,
+ *                        th, vector<MapPoint*>& vpReplacePoint)   src/ORBmatcher.cc:1094-1236
+ *                        (LoopClosing::SearchAndFuse, src/LoopClosing.cc:837; f as for SIM3, occ
+ *                        unused; flags bit0 = !isBad() && !spAlreadyFound.count(pMP) with
+ *                        spAlreadyFound = pKF->GetMapPoints() at entry; point_match[k] = bestIdx
+ *                        when bestDist <= TH_LOW, *nmatches = nFused; the caller applies the
+ *                        replace / AddMapPoint block, :1210-1229, in point order)
  * The current Frame (orbx_proj_frame) and the projected MapPoints are SoA
  * arrays the caller gathers from its object graph; the Frame's mvpMapPoints
  * on entry is summarised per feature as occ[i]: 0 NULL, 1 a MapPoint with
@@ -409,6 +422,8 @@ orbx_status orbx_pnp_iterate_many(orbx_pnp* const* solvers, int n, int n_iterati
 #define ORBX_PROJ_LAST_FRAME 1
 #define ORBX_PROJ_KEYFRAME 2
 #define ORBX_PROJ_FUSE 3
+#define ORBX_PROJ_SIM3 4
+#define ORBX_PROJ_FUSE_SIM3 5
 #define ORBX_PROJ_MAX_FEATURES 8192 /* Frame::N per problem */
 
 typedef struct {
@@ -436,11 +451,12 @@ typedef struct {
   const uint8_t* flags;     /* bit0 = the point takes part (LOCAL: mbTrackInView && !isBad(), or with
                                frustum: mnLastFrameSeen != mnId && !isBad(); LAST_FRAME: pMP &&
                                !mvbOutlier[i]; KEYFRAME: pMP && !isBad() && !sAlreadyFound.count(pMP);
-                               FUSE: pMP && !isBad() && !IsInKeyFrame(pKF));
+                               FUSE: pMP && !isBad() && !IsInKeyFrame(pKF); SIM3: !isBad() &&
+                               !spAlreadyFound.count(pMP));
                                bit1 = Observations() > 0 */
-  const float* pos;         /* GetWorldPos(), n_points x 3 (frustum, LAST_FRAME, KEYFRAME, FUSE) */
-  const float* normal;      /* GetNormal(), n_points x 3 (frustum, FUSE) */
-  const float* dist_minmax; /* mfMinDistance, mfMaxDistance, n_points x 2 (frustum, KEYFRAME, FUSE) */
+  const float* pos;         /* GetWorldPos(), n_points x 3 (frustum, LAST_FRAME, KEYFRAME, FUSE*, SIM3) */
+  const float* normal;      /* GetNormal(), n_points x 3 (frustum, FUSE*, SIM3) */
+  const float* dist_minmax; /* mfMinDistance, mfMaxDistance, n_points x 2 (frustum, KEYFRAME, FUSE*, SIM3) */
   const float* angle;       /* LastFrame.mvKeysUn[i].angle / pKF->mvKeysUn[i].angle (LAST_FRAME, KEYFRAME) */
   const int32_t* octave;    /* LastFrame.mvKeys[i].octave (LAST_FRAME) */
   float* track;             /* LOCAL, n_points x 4: mTrackProjX, mTrackProjY, mTrackProjXR, mTrackViewCos

@@ -13,6 +13,8 @@
 //   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)      src/ORBmatcher.cc:1489-1646
 //   ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist)  src/ORBmatcher.cc:1648-1795
 //   ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th), matching half     src/ORBmatcher.cc:944-1054
+//   ORBmatcher::SearchByProjection(KeyFrame*, Scw, vector<MapPoint*>, vpMatched, th)  src/ORBmatcher.cc:327-440
+//   ORBmatcher::Fuse(KeyFrame*, Scw, vector<MapPoint*>, th, vpReplacePoint), matching half  :1094-1236
 //
 // OpenCV arithmetic restated (parity vs the genuine library is unpinned; the
 // reference ships no fixture for any of this):
@@ -495,6 +497,84 @@ int fuse(const oracle_proj_problem& P) {
   return nFused;
 }
 
+// SearchByProjection(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, vector<MapPoint*>& vpMatched,
+// th), src/ORBmatcher.cc:327-440 (LoopClosing::ComputeSim3, src/LoopClosing.cc:504).  F.Tcw holds
+// the 4x4 Sim3 Scw.  sRcw/scw and col(3)/scw are Mat / double: MatOp_AddEx -> convertTo(alpha =
+// 1/scw) -> cvtScale_<float,float,float>, i.e. x * (float)(1.0/scw) + 0.0f in float; scw =
+// sqrt(row0.dot(row0)) (Mat::dot: double products summed left to right) rounded to float.
+// vpMatched on entry is F.occ (nonzero = a MapPoint); flags bit0 = !isBad() && !spAlreadyFound.
+void sim3_decompose(const float* S, float* T) {
+  double d = (double)S[0] * S[0];
+  d = d + (double)S[1] * S[1];
+  d = d + (double)S[2] * S[2];
+  const float scw = (float)std::sqrt(d);
+  const float a = (float)(1.0 / (double)scw);
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 4; c++) T[4 * r + c] = S[4 * r + c] * a + 0.0f;
+  T[12] = T[13] = T[14] = 0.0f;
+  T[15] = 1.0f;
+}
+
+// kind 4: SearchByProjection(KeyFrame*, Scw, ...) (src/ORBmatcher.cc:327-440); kind 5: the matching
+// half of Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint) (:1094-1236): no "already matched" state
+// in the candidate loop, invz = 1.0/z in double, flags bit0 = !isBad() && !spAlreadyFound.count(pMP)
+// (pKF->GetMapPoints() at entry); point_match[i] = bestIdx, the return value nFused.  The caller
+// applies the replace / AddMapPoint block (:1210-1229) in point order.
+int sim3(const oracle_proj_problem& P) {
+  const bool fuse = P.kind == 5;
+  const oracle_proj_frame& F = P.f;
+  Frame fr(F);
+  Occupancy occ(F);
+  float T[16], Ow[3];
+  sim3_decompose(F.Tcw, T);
+  camera_centre(T, Ow);  // -Rcw.t()*tcw: GEMM_1_T, double sum
+  int nmatches = 0;
+  for (int i = 0; i < P.n_points; i++) {
+    P.point_match[i] = -1;
+    if (!(P.flags[i] & 1)) continue;  // pMP->isBad() || spAlreadyFound.count(pMP)
+    const float* X = P.pos + 3 * i;
+    float c[3];
+    mat3x1(T, X, c);
+    if (c[2] < 0.0) continue;
+    const float invz = fuse ? (float)(1.0 / (double)c[2]) : 1 / c[2];
+    const float x = c[0] * invz, y = c[1] * invz;
+    const float u = F.fx * x + F.cx, v = F.fy * y + F.cy;
+    if (!(u >= F.min_x && u < F.max_x && v >= F.min_y && v < F.max_y)) continue;  // KeyFrame::IsInImage
+    const float maxDistance = 1.2f * P.dist_minmax[2 * i + 1], minDistance = 0.8f * P.dist_minmax[2 * i];
+    const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+    const float dist = norm3(PO);
+    if (dist < minDistance || dist > maxDistance) continue;
+    const float* Pn = P.normal + 3 * i;
+    double dot = (double)PO[0] * Pn[0];
+    dot = dot + (double)PO[1] * Pn[1];
+    dot = dot + (double)PO[2] * Pn[2];
+    if (dot < 0.5 * dist) continue;
+    const int nPredictedLevel = predict_scale(P.dist_minmax[2 * i + 1], dist, F.log_scale_factor, F.nlevels);
+    const float radius = P.th * F.scale_factors[nPredictedLevel];
+    const std::vector<int> cand = fr.area(u, v, radius);  // KeyFrame::GetFeaturesInArea, no level filter
+    if (cand.empty()) continue;
+    const uint8_t* dMP = P.desc + 32 * (size_t)i;
+    int bestDist = 256, bestIdx = -1;
+    for (int idx : cand) {
+      if (!fuse && occ.who[idx] != -1) continue;  // vpMatched[idx]
+      const int kpLevel = F.keys_un[idx].octave;
+      if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+      const int d = hamming(dMP, F.desc + 32 * (size_t)idx);
+      if (d < bestDist) {
+        bestDist = d;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= 50) {  // TH_LOW
+      occ.who[bestIdx] = i;  // vpMatched[bestIdx] = pMP (Fuse: frame_out = the last point matched there)
+      P.point_match[i] = bestIdx;
+      nmatches++;
+    }
+  }
+  write_out(P, occ);
+  return nmatches;
+}
+
 }  // namespace
 
 extern "C" {
@@ -506,6 +586,8 @@ int oracle_search_by_projection(const oracle_proj_problem* P) {
     case 1: return last_frame(*P);
     case 2: return keyframe(*P);
     case 3: return fuse(*P);
+    case 4:
+    case 5: return sim3(*P);
     default: return -1;
   }
 }

@@ -421,7 +421,6 @@ __global__ __launch_bounds__(BS, ORBX_BLUR_WPE) void k_blur(const Geometry* __re
   const bool all_simd = xg + 3 < simd_w;  // the whole group takes the SSE2 rounding
   // wave-uniform: the per-row tail fix-up below is a scalar branch (no exec-mask juggling per row)
   const bool wave_tail = __builtin_amdgcn_ballot_w64(!all_simd) != 0;
-  const bool full = xg + 4 <= w;
 
 #pragma unroll
   for (int r = 0; r < kBStrip; r++) {

@@ -1,6 +1,8 @@
 // projection.hip -- ORBmatcher::SearchByProjection, the three overloads run on
 // every tracked frame (src/ORBmatcher.cc:46-142 local map, :1489-1646 last
-// frame, :1648-1795 keyframe) and the matching half of Fuse (:944-1054), with
+// frame, :1648-1795 keyframe), the matching half of Fuse (:944-1054) and the
+// loop-closing SearchByProjection(KeyFrame*, Scw, ...) (:327-440) and Fuse(KeyFrame*, Scw, ...)
+// (:1094-1236, matching half), with
 // Frame::AssignFeaturesToGrid /
 // GetFeaturesInArea (src/Frame.cc:254-271, 388-453) and, for the local map,
 // Frame::isInFrustum (src/Frame.cc:315-375) fused in front.  One block per
@@ -164,9 +166,10 @@ __device__ Query setup_query(const ProjProblem& P, int i, const float* Tcw, cons
   const float* X = P.pos + 3 * i;
   float c[3];
   mat3x1(Tcw, X, c);
-  if (P.kind == ORBX_PROJ_FUSE) {  // src/ORBmatcher.cc:960-1006
+  if (P.kind == ORBX_PROJ_FUSE || P.kind == ORBX_PROJ_SIM3 || P.kind == ORBX_PROJ_FUSE_SIM3) {
+    // src/ORBmatcher.cc:960-1006, :352-391, :1117-1160
     if (c[2] < 0.0f) return q;
-    const float invz = 1 / c[2];
+    const float invz = P.kind == ORBX_PROJ_FUSE_SIM3 ? (float)(1.0 / (double)c[2]) : 1 / c[2];
     const float x = c[0] * invz, y = c[1] * invz;
     const float u = F.fx * x + F.cx, v = F.fy * y + F.cy;
     if (!(u >= F.min_x && u < F.max_x && v >= F.min_y && v < F.max_y)) return q;  // KeyFrame::IsInImage
@@ -256,7 +259,21 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   const int nF = P.f_n_dev ? min(max(*P.f_n_dev, 0), F.n) : F.n;
   const int nP = P.n_points_dev ? min(max(*P.n_points_dev, 0), P.n_points) : P.n_points;
   __shared__ float s_Tcw[16];
-  if (tid < 16) s_Tcw[tid] = P.Tcw_dev ? P.Tcw_dev[tid] : F.Tcw[tid];
+  if (tid < 16) {
+    const float* S = P.Tcw_dev ? P.Tcw_dev : F.Tcw;
+    if (P.kind == ORBX_PROJ_SIM3 || P.kind == ORBX_PROJ_FUSE_SIM3) {
+      // Scw -> [Rcw | tcw] = [sRcw | t] / scw (src/ORBmatcher.cc:335-339): scw = sqrt(row0.dot(row0))
+      // (double products summed left to right, rounded to float); Mat / double is convertTo(alpha =
+      // 1/scw): x * (float)alpha + 0.0f in float.  Every one of the 16 threads derives scw itself.
+      double d = (double)S[0] * S[0];
+      d = d + (double)S[1] * S[1];
+      d = d + (double)S[2] * S[2];
+      const float a = (float)(1.0 / (double)(float)__builtin_sqrt(d));
+      s_Tcw[tid] = tid < 12 ? S[tid] * a + 0.0f : (tid == 15 ? 1.0f : 0.0f);
+    } else {
+      s_Tcw[tid] = S[tid];
+    }
+  }
   int* s_fw = (int*)s_keys;
 
   // ---- Frame::AssignFeaturesToGrid as a sort of (cell << 13 | index) ----
@@ -360,8 +377,11 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   const int g = tid / kGroup, gl = tid % kGroup;
   constexpr int kGroups = PBS / kGroup;
   const bool local = P.kind == ORBX_PROJ_LOCAL;
-  const bool kf = P.kind == ORBX_PROJ_KEYFRAME;
-  const bool fuse = P.kind == ORBX_PROJ_FUSE;  // no "already matched" state: one sweep
+  // KEYFRAME and SIM3: any MapPoint on the feature blocks it, and every match blocks later points
+  const bool kf = P.kind == ORBX_PROJ_KEYFRAME || P.kind == ORBX_PROJ_SIM3;
+  // no "already matched" state: one sweep (FUSE also gates candidates by reprojection error)
+  const bool fuse = P.kind == ORBX_PROJ_FUSE || P.kind == ORBX_PROJ_FUSE_SIM3;
+  const bool gate = P.kind == ORBX_PROJ_FUSE;
   for (int sweep = 0; sweep <= nP + 1; sweep++) {
     if (tid == 0) s_changed = 0;
     __syncthreads();
@@ -395,7 +415,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
             if (check && (oct < q.min_level || (q.max_level >= 0 && oct > q.max_level))) continue;
             const float dx = kp.x - q.x, dy = kp.y - q.y;
             if (!(__builtin_fabsf(dx) < q.r && __builtin_fabsf(dy) < q.r)) continue;
-            if (fuse) {  // reprojection error gate, src/ORBmatcher.cc:1018-1042
+            if (gate) {  // reprojection error gate, src/ORBmatcher.cc:1018-1042
               const float isg = F.inv_level_sigma2[oct];
               const float urf = F.u_right ? F.u_right[idx] : -1.0f;
               const float ex = q.x - kp.x, ey = q.y - kp.y;
@@ -407,7 +427,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
                 const float e2 = ex * ex + ey * ey;
                 if (e2 * isg > 5.99) continue;
               }
-            } else {
+            } else if (!fuse) {
               const int o = F.occ ? F.occ[idx] : 0;
               if ((kf ? o != 0 : o == 2) || s_fw[idx] < i) continue;
             }
@@ -469,7 +489,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
     s_drop = 0;
   }
   __syncthreads();
-  const bool rot = !local && !fuse && P.check_ori;
+  const bool rot = !local && !fuse && P.kind != ORBX_PROJ_SIM3 && P.check_ori;
   int cnt = 0;
   for (int i = tid; i < nP; i += PBS) {
     const int m = P.point_match[i];
@@ -539,7 +559,7 @@ orbx_status proj_status(hipError_t e) { return e == hipSuccess ? ORBX_OK : ORBX_
 
 // Host-side argument checks shared by both entry points (the kernel assumes them).
 orbx_status proj_check(const orbx_proj_problem& p, bool host) {
-  if (p.kind < ORBX_PROJ_LOCAL || p.kind > ORBX_PROJ_FUSE) return ORBX_ERR_ARG;
+  if (p.kind < ORBX_PROJ_LOCAL || p.kind > ORBX_PROJ_FUSE_SIM3) return ORBX_ERR_ARG;
   if (p.f.n < 0 || p.n_points < 0) return ORBX_ERR_ARG;
   if (p.f.n > ORBX_PROJ_MAX_FEATURES) return ORBX_ERR_CAPACITY;
   if (p.f.nlevels < 1 || p.f.nlevels > 16) return ORBX_ERR_ARG;
@@ -563,6 +583,8 @@ orbx_status proj_check(const orbx_proj_problem& p, bool host) {
             if ((p.flags[i] & 1) && (p.octave[i] < 0 || p.octave[i] >= p.f.nlevels)) return ORBX_ERR_ARG;
         break;
       case ORBX_PROJ_FUSE:
+      case ORBX_PROJ_SIM3:
+      case ORBX_PROJ_FUSE_SIM3:
         if (!p.pos || !p.normal || !p.dist_minmax) return ORBX_ERR_ARG;
         break;
       default:

@@ -294,6 +294,29 @@ class ORBmatcher:
         o = _run_projection(self, pKF, vpMapPoints, PROJ_FUSE, th=th)
         return int(o["nmatches"][0]), o["point_match"]
 
+    def SearchByProjectionSim3(self, pKF, Scw, vpPoints, th=10):
+        """SearchByProjection(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, vector<MapPoint*>&
+        vpMatched, th) -- src/ORBmatcher.cc:327-440 (LoopClosing::ComputeSim3, src/LoopClosing.cc:504).
+        pKF: frame dict of the KeyFrame (bounds = its int mnMinX.., occ[i] != 0 = vpMatched[i] on
+        entry); Scw: 4x4 Sim3; vpPoints: points dict (pos, normal, dist_minmax, desc, flags bit0 =
+        !isBad() && not already in vpMatched).  Returns (nmatches, frame_out, point_match);
+        frame_out[i] = k: vpMatched[i] = point k, -1 unchanged."""
+        F = dict(pKF)
+        F["Tcw"] = np.asarray(Scw, np.float32).reshape(4, 4)
+        o = _run_projection(self, F, vpPoints, PROJ_SIM3, th=float(th))
+        return int(o["nmatches"][0]), o["frame_out"], o["point_match"]
+
+    def FuseSim3(self, pKF, Scw, vpPoints, th=4.0):
+        """The matching half of Fuse(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, th,
+        vector<MapPoint*>& vpReplacePoint) -- src/ORBmatcher.cc:1094-1236 (LoopClosing::SearchAndFuse).
+        vpPoints flags bit0 = !isBad() && not in pKF->GetMapPoints().  Returns (nFused,
+        bestIdx[n_points] (-1 = none)); the caller applies the replace / AddMapPoint block
+        (:1210-1229) in point order."""
+        F = dict(pKF)
+        F["Tcw"] = np.asarray(Scw, np.float32).reshape(4, 4)
+        o = _run_projection(self, F, vpPoints, PROJ_FUSE_SIM3, th=float(th))
+        return int(o["nmatches"][0]), o["point_match"]
+
     def SearchForTriangulation(self, prob, bOnlyStereo=False):
         """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) --
         src/ORBmatcher.cc:738-925.  prob: dict(kf1, kf2 (keys_un, desc, u_right, has_mp, node_id,
@@ -326,7 +349,7 @@ class ORBmatcher:
         return int(d[0]) if n == 1 else d
 
 
-PROJ_LOCAL, PROJ_LAST_FRAME, PROJ_KEYFRAME, PROJ_FUSE = 0, 1, 2, 3
+PROJ_LOCAL, PROJ_LAST_FRAME, PROJ_KEYFRAME, PROJ_FUSE, PROJ_SIM3, PROJ_FUSE_SIM3 = 0, 1, 2, 3, 4, 5
 
 
 def _f32(x):

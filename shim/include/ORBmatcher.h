@@ -12,6 +12,9 @@
 //   SearchForTriangulation(KeyFrame*, KeyFrame*, F12, vMatchedPairs, bOnlyStereo) include/ORBmatcher.h:134
 //                                                       (src/ORBmatcher.cc:738-925)
 //   Fuse(KeyFrame*, const vector<MapPoint*>&, th)                       include/ORBmatcher.h:148
+//   SearchByProjection(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, vector<MapPoint*>&, th)
+//                                                                       include/ORBmatcher.h:99
+//   Fuse(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, th, vector<MapPoint*>&)  include/ORBmatcher.h:153
 //                                                       (src/ORBmatcher.cc:918-1092)
 // DescriptorDistance of one pair stays on the host (a GPU launch per pair would cost more than the
 // popcounts); every other member runs its matching on the MI355X (orbx_search_by_bow_*,
@@ -43,6 +46,12 @@ class ORBmatcher {
   // Tracking::Relocalization: a candidate KeyFrame's MapPoints not found yet
   int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std::set<MapPoint*>& sAlreadyFound,
                          const float th, const int ORBdist);
+  // LoopClosing::ComputeSim3: the loop MapPoints into the current KeyFrame through a Sim3
+  int SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
+                         std::vector<MapPoint*>& vpMatched, int th);
+  // LoopClosing::SearchAndFuse: the loop MapPoints into a corrected KeyFrame through its Sim3
+  int Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints, float th,
+           std::vector<MapPoint*>& vpReplacePoint);
   // LocalMapping::CreateNewMapPoints
   int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
                              std::vector<std::pair<size_t, size_t>>& vMatchedPairs, const bool bOnlyStereo);

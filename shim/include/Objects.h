@@ -148,6 +148,7 @@ class KeyFrame {
     std::unique_lock<std::mutex> lock(mMutexFeatures);
     return mvpMapPoints;
   }
+  std::set<MapPoint*> GetMapPoints();           // src/KeyFrame.cc GetMapPoints: the non-bad MapPoints
   MapPoint* GetMapPoint(const size_t& idx) {     // src/KeyFrame.cc GetMapPoint
     std::unique_lock<std::mutex> lock(mMutexFeatures);
     return mvpMapPoints[idx];

@@ -690,6 +690,105 @@ int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, c
   return nFused;
 }
 
+int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
+                                   std::vector<MapPoint*>& vpMatched, int th) {
+  // src/ORBmatcher.cc:327-440 (caller LoopClosing::ComputeSim3, src/LoopClosing.cc:504): one
+  // ORBX_PROJ_SIM3 problem; vpMatched on entry blocks its features (occ) and its MapPoints
+  // (spAlreadyFound), the kernel's sweeps reproduce the in-order "vpMatched[idx]" skips
+  const int n = (int)vpPoints.size();
+  cv::Mat desc;
+  orbx_proj_problem p;
+  std::memset(&p, 0, sizeof(p));
+  p.kind = ORBX_PROJ_SIM3;
+  p.th = (float)th;
+  p.f = fuse_frame(pKF, desc);
+  copy_mat44(Scw, p.f.Tcw);
+  std::vector<int8_t> occ(pKF->N > 0 ? pKF->N : 1, 0);
+  std::set<MapPoint*> found;
+  for (int i = 0; i < pKF->N && i < (int)vpMatched.size(); i++)
+    if (vpMatched[i]) {
+      occ[i] = 1;
+      found.insert(vpMatched[i]);
+    }
+  p.f.occ = occ.data();
+  ProjPoints P(n);
+  for (int k = 0; k < n; k++) {
+    MapPoint* pMP = vpPoints[k];
+    if (!pMP || pMP->isBad() || found.count(pMP)) continue;
+    P.flags[k] = 1;
+    copy_desc(pMP, &P.desc[32 * (size_t)k]);
+    copy_pos(pMP, &P.pos[3 * (size_t)k]);
+    const cv::Mat nrm = pMP->GetNormal();
+    for (int c = 0; c < 3; c++) P.normal[3 * (size_t)k + c] = nrm.empty() ? 0.f : nrm.at<float>(c, 0);
+    copy_dist(pMP, &P.dist[2 * (size_t)k]);
+  }
+  P.fill(p, n);
+  std::vector<int32_t> frame_out(pKF->N > 0 ? pKF->N : 1, -1);
+  int32_t nm = 0;
+  p.frame_out = frame_out.data();
+  p.nmatches = &nm;
+  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection (Sim3)");
+  for (int i = 0; i < pKF->N && i < (int)vpMatched.size(); i++)
+    if (frame_out[i] >= 0) vpMatched[i] = vpPoints[frame_out[i]];
+  return nm;
+}
+
+std::set<MapPoint*> KeyFrame::GetMapPoints() {
+  std::unique_lock<std::mutex> lock(mMutexFeatures);
+  std::set<MapPoint*> s;
+  for (MapPoint* pMP : mvpMapPoints)
+    if (pMP && !pMP->isBad()) s.insert(pMP);
+  return s;
+}
+
+int ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints, float th,
+                     std::vector<MapPoint*>& vpReplacePoint) {
+  // src/ORBmatcher.cc:1094-1236 (caller LoopClosing::SearchAndFuse, src/LoopClosing.cc:837).  The
+  // candidate loop reads no state the loop writes, so every point is matched in one launch
+  // (ORBX_PROJ_FUSE_SIM3); the replace / AddMapPoint block then runs here in point order.
+  const std::set<MapPoint*> found = pKF->GetMapPoints();
+  const int n = (int)vpPoints.size();
+  cv::Mat desc;
+  orbx_proj_problem p;
+  std::memset(&p, 0, sizeof(p));
+  p.kind = ORBX_PROJ_FUSE_SIM3;
+  p.th = th;
+  p.f = fuse_frame(pKF, desc);
+  copy_mat44(Scw, p.f.Tcw);
+  ProjPoints P(n);
+  for (int k = 0; k < n; k++) {
+    MapPoint* pMP = vpPoints[k];
+    if (!pMP || pMP->isBad() || found.count(pMP)) continue;
+    P.flags[k] = 1;
+    copy_desc(pMP, &P.desc[32 * (size_t)k]);
+    copy_pos(pMP, &P.pos[3 * (size_t)k]);
+    const cv::Mat nrm = pMP->GetNormal();
+    for (int c = 0; c < 3; c++) P.normal[3 * (size_t)k + c] = nrm.empty() ? 0.f : nrm.at<float>(c, 0);
+    copy_dist(pMP, &P.dist[2 * (size_t)k]);
+  }
+  P.fill(p, n);
+  std::vector<int32_t> frame_out(pKF->N > 0 ? pKF->N : 1, -1);
+  int32_t nm = 0;
+  p.frame_out = frame_out.data();
+  p.nmatches = &nm;
+  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection (Fuse Sim3)");
+  int nFused = 0;
+  for (int i = 0; i < n; i++) {
+    const int bestIdx = P.point_match[i];
+    if (bestIdx < 0) continue;
+    MapPoint* pMP = vpPoints[i];
+    MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
+    if (pMPinKF) {
+      if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
+    } else {
+      pMP->AddObservation(pKF, bestIdx);
+      pKF->AddMapPoint(pMP, bestIdx);
+    }
+    nFused++;
+  }
+  return nFused;
+}
+
 int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
                                        std::vector<std::pair<size_t, size_t>>& vMatchedPairs, const bool bOnlyStereo) {
   // src/ORBmatcher.cc:738-925 (caller LocalMapping::CreateNewMapPoints, src/LocalMapping.cc:363)

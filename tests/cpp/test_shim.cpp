@@ -10,6 +10,8 @@
 //                       Tracking::Relocalization's candidate loop
 //   proj    IN OUT      ORBmatcher::SearchByProjection x3 (local map / last frame / KeyFrame)
 //   fuse    IN OUT      ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th) incl. Replace / AddObservation
+//   sim3    IN OUT      ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)
+//   fusesim3 IN OUT     ORBmatcher::Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint)
 //   tri     IN OUT      ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, F12, pairs, bOnlyStereo)
 //   pose    IN OUT      Optimizer::PoseOptimization(Frame*)
 //   distinct IN OUT     MapPoint::ComputeDistinctiveDescriptors
@@ -926,6 +928,135 @@ static int mode_fuse(const char* in, const char* out) {
   return 0;
 }
 
+// SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th).  pKF is the payload frame.  vpMatched
+// on entry holds its occupied features: the first of them take the odd-index candidates with bit0
+// off (so those are in spAlreadyFound), the rest their own entry MapPoints; even-index candidates
+// with bit0 off are bad.
+static void keyframe_from_frame(const Frame& F, KeyFrame& K) {
+  K.mnId = 1000;
+  K.N = F.N;
+  K.mvKeysUn = F.mvKeysUn;
+  K.mDescriptors = F.mDescriptors;
+  K.mvuRight = F.mvuRight;
+  K.mvpMapPoints.assign(F.N, nullptr);
+  K.mnMinX = (int)Frame::mnMinX;
+  K.mnMaxX = (int)Frame::mnMaxX;
+  K.mnMinY = (int)Frame::mnMinY;
+  K.mnMaxY = (int)Frame::mnMaxY;
+  K.mfGridElementWidthInv = Frame::mfGridElementWidthInv;
+  K.mfGridElementHeightInv = Frame::mfGridElementHeightInv;
+  K.mnScaleLevels = F.mnScaleLevels;
+  K.mvScaleFactors = F.mvScaleFactors;
+  K.mvLevelSigma2 = F.mvLevelSigma2;
+  K.mvInvLevelSigma2 = F.mvInvLevelSigma2;
+  K.mfLogScaleFactor = F.mfLogScaleFactor;
+  K.fx = Frame::fx;
+  K.fy = Frame::fy;
+  K.cx = Frame::cx;
+  K.cy = Frame::cy;
+  K.mbf = F.mbf;
+  K.mb = F.mb;
+  K.SetPose(F.mTcw);
+}
+
+// The candidates of a Sim3 mode, and the entry MapPoints of the KeyFrame's occupied features: the first
+// occupied features take the odd-index candidates with bit0 off, the rest their own entry MapPoints.
+// Every other candidate with bit0 off is bad, so bit0 is exactly "!isBad() && not already there".
+static void sim3_points(const FramePayload& fp, const PointPayload& P, std::vector<std::unique_ptr<MapPoint>>& cands,
+                        std::vector<MapPoint*>& pts, std::vector<MapPoint*>& entry) {
+  const Frame& F = fp.F;
+  pts.assign(P.n, nullptr);
+  for (int k = 0; k < P.n; k++) {
+    cands.emplace_back(new MapPoint());
+    MapPoint& m = *cands.back();
+    make_point(m, P, k);
+    m.mbBad = !(P.flags[k] & 1);  // cleared below for the candidates that become entry MapPoints
+    pts[k] = &m;
+  }
+  entry.assign(F.N, nullptr);
+  int kk = 1;
+  for (int i = 0; i < F.N; i++) {
+    if (!F.mvpMapPoints[i]) continue;
+    while (kk < P.n && (P.flags[kk] & 1)) kk += 2;
+    if (kk < P.n) {
+      entry[i] = pts[kk];
+      pts[kk]->mbBad = false;
+      kk += 2;
+    } else {
+      entry[i] = F.mvpMapPoints[i];
+    }
+  }
+}
+
+// MapPoint -> code: candidate k, -1000 - i for the entry MapPoint of feature i, -1 NULL
+static int sim3_code(const MapPoint* m, const std::vector<MapPoint*>& pts, const std::vector<MapPoint*>& entry) {
+  if (!m) return -1;
+  for (size_t k = 0; k < pts.size(); k++)
+    if (pts[k] == m) return (int)k;
+  for (size_t i = 0; i < entry.size(); i++)
+    if (entry[i] == m) return -1000 - (int)i;
+  return -2;
+}
+
+static int mode_sim3(const char* in, const char* out) {
+  Reader r(in);
+  const int th = r.get<int32_t>();
+  cv::Mat Scw(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) Scw.at<float>(i / 4, i % 4) = r.get<float>();
+  FramePayload fp;
+  read_frame(r, fp);
+  PointPayload P;
+  read_points(r, P);
+  const Frame& F = fp.F;
+  KeyFrame K;
+  keyframe_from_frame(F, K);
+  std::vector<std::unique_ptr<MapPoint>> cands;
+  std::vector<MapPoint*> pts, vpMatched;
+  sim3_points(fp, P, cands, pts, vpMatched);
+  const std::vector<MapPoint*> entry(vpMatched);
+  ORBmatcher matcher;
+  const int nm = matcher.SearchByProjection(&K, Scw, pts, vpMatched, th);
+  Writer o(out);
+  o.put<int32_t>(nm);
+  // vpMatched afterwards: candidate k, -1000 - i the entry MapPoint of feature i, -1 NULL
+  for (int i = 0; i < F.N; i++) o.put<int32_t>(sim3_code(vpMatched[i], pts, entry));
+  std::printf("sim3 ok: %d matches\n", nm);
+  return 0;
+}
+
+// Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint): pKF's MapPoints are the entry MapPoints of
+// sim3_points (those of features i with i % 3 == 0 that are not candidates are bad).  Out: nFused,
+// vpReplacePoint per point and pKF's MapPoints per feature afterwards, as sim3_code codes.
+static int mode_fusesim3(const char* in, const char* out) {
+  Reader r(in);
+  const float th = r.get<float>();
+  cv::Mat Scw(4, 4, CV_32F);
+  for (int i = 0; i < 16; i++) Scw.at<float>(i / 4, i % 4) = r.get<float>();
+  FramePayload fp;
+  read_frame(r, fp);
+  PointPayload P;
+  read_points(r, P);
+  const Frame& F = fp.F;
+  KeyFrame K;
+  keyframe_from_frame(F, K);
+  std::vector<std::unique_ptr<MapPoint>> cands;
+  std::vector<MapPoint*> pts, entry;
+  sim3_points(fp, P, cands, pts, entry);
+  for (int i = 0; i < F.N; i++) {
+    K.mvpMapPoints[i] = entry[i];
+    if (entry[i] && i % 3 == 0 && sim3_code(entry[i], pts, entry) < -1) entry[i]->mbBad = true;
+  }
+  std::vector<MapPoint*> rep(P.n, nullptr);
+  ORBmatcher matcher;
+  const int nf = matcher.Fuse(&K, Scw, pts, th, rep);
+  Writer o(out);
+  o.put<int32_t>(nf);
+  for (int k = 0; k < P.n; k++) o.put<int32_t>(sim3_code(rep[k], pts, entry));
+  for (int i = 0; i < F.N; i++) o.put<int32_t>(sim3_code(K.mvpMapPoints[i], pts, entry));
+  std::printf("fusesim3 ok: %d fused\n", nf);
+  return 0;
+}
+
 // SearchForTriangulation(KeyFrame*, KeyFrame*, F12, vMatchedPairs, bOnlyStereo)
 static void read_tri_kf(Reader& r, KeyFrame& K) {
   K.N = r.get<int32_t>();
@@ -1136,6 +1267,8 @@ int main(int argc, char** argv) {
     if (m == "pnp") return mode_pnp(argv[2], argv[3]);
     if (m == "proj") return mode_proj(argv[2], argv[3]);
     if (m == "fuse") return mode_fuse(argv[2], argv[3]);
+    if (m == "sim3") return mode_sim3(argv[2], argv[3]);
+    if (m == "fusesim3") return mode_fusesim3(argv[2], argv[3]);
     if (m == "tri") return mode_tri(argv[2], argv[3]);
     if (m == "pose") return mode_pose(argv[2], argv[3]);
     if (m == "distinct") return mode_distinct(argv[2], argv[3]);

@@ -73,6 +73,12 @@ def test_shim_exports_reference_classes(exe):
                 "unsigned long> > >&, bool)",
                 "ORB_SLAM2::ORBmatcher::Fuse(ORB_SLAM2::KeyFrame*, std::vector<ORB_SLAM2::MapPoint*, "
                 "std::allocator<ORB_SLAM2::MapPoint*> > const&, float)",
+                "ORB_SLAM2::ORBmatcher::SearchByProjection(ORB_SLAM2::KeyFrame*, cv::Mat, "
+                "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> > const&, "
+                "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&, int)",
+                "ORB_SLAM2::ORBmatcher::Fuse(ORB_SLAM2::KeyFrame*, cv::Mat, std::vector<ORB_SLAM2::MapPoint*, "
+                "std::allocator<ORB_SLAM2::MapPoint*> > const&, float, std::vector<ORB_SLAM2::MapPoint*, "
+                "std::allocator<ORB_SLAM2::MapPoint*> >&)",
                 "ORB_SLAM2::Optimizer::PoseOptimization(ORB_SLAM2::Frame*)",
                 "ORB_SLAM2::MapPoint::ComputeDistinctiveDescriptors()",
                 "ORB_SLAM2::Frame::ComputeBoW()",
@@ -535,6 +541,84 @@ def test_shim_fuse(gpu, exe, tmp_path, seed, th):
     np.testing.assert_array_equal(code, ecode)
     np.testing.assert_array_equal(rec["bad"], ebad)
     np.testing.assert_array_equal(rec["nobs"], ecnt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,th", [(0, 10), (1, 3), (2, 5)])
+def test_shim_search_by_projection_sim3(gpu, exe, tmp_path, variant, th):
+    """ORBmatcher::SearchByProjection(KeyFrame*, cv::Mat Scw, vpPoints, vpMatched, th)
+    (include/ORBmatcher.h:99, LoopClosing::ComputeSim3): vpMatched afterwards equals the oracle's,
+    feature for feature -- entry entries kept (their MapPoints in spAlreadyFound when they are
+    candidates), new matches set -- and the return value."""
+    fr = synth.projection_frame(720 + variant, n=1800, p_occ=(0.1, 0.15))
+    pts = synth.projection_points(721 + variant, fr, 3, n_points=1500, pool=0.3)
+    Scw = _scaled(fr, [1.7, 0.35, 2.9][variant])
+    ref = oracle.search_by_projection(dict(fr, Tcw=Scw), pts, 4, th=float(th))
+    payload = struct.pack("<i", th) + Scw.reshape(16).tobytes() + _frame_bytes(fr) + _points_bytes(pts)
+    out = _run(exe, "sim3", payload, tmp_path)
+    nm = struct.unpack_from("<i", out, 0)[0]
+    state = np.frombuffer(out, np.int32, offset=4)
+    want = _sim3_entry(pts, fr)
+    fo = ref["frame_out"]
+    want = np.where(fo >= 0, fo, want)
+    assert nm == ref["nmatches"] and nm > 50
+    np.testing.assert_array_equal(state, want)
+
+
+def _sim3_entry(pts, fr):
+    """test_shim.cpp sim3_points: the entry MapPoint code per feature (candidate k, -1000 - i, -1)."""
+    flags, occ = np.asarray(pts["flags"]), np.asarray(fr["occ"])
+    want = np.full(len(occ), -1, np.int32)
+    kk = 1
+    for i in np.nonzero(occ != 0)[0]:
+        while kk < len(flags) and (flags[kk] & 1):
+            kk += 2
+        if kk < len(flags):
+            want[i] = kk
+            kk += 2
+        else:
+            want[i] = -1000 - i
+    return want
+
+
+def _scaled(fr, s):
+    S = np.array(fr["Tcw"], np.float32).copy()
+    S[:3, :] = (S[:3, :].astype(np.float64) * s).astype(np.float32)
+    return S
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,th", [(0, 4.0), (1, 1.0), (2, 7.0)])
+def test_shim_fuse_sim3(gpu, exe, tmp_path, variant, th):
+    """ORBmatcher::Fuse(KeyFrame*, cv::Mat Scw, vpPoints, th, vpReplacePoint) (include/ORBmatcher.h:153,
+    LoopClosing::SearchAndFuse): matches on the MI355X, then the replace / AddMapPoint block in point
+    order -- vpReplacePoint per point, pKF's MapPoints per feature afterwards and nFused equal the
+    reference loop's (restated here on the oracle's matches), bad entry MapPoints included."""
+    fr = synth.projection_frame(730 + variant, n=1800, p_occ=(0.1, 0.15))
+    pts = synth.projection_points(731 + variant, fr, 3, n_points=1500, pool=0.3)
+    Scw = _scaled(fr, [0.6, 1.9, 3.3][variant])
+    ref = oracle.search_by_projection(dict(fr, Tcw=Scw), pts, 5, th=th)
+    payload = struct.pack("<f", th) + Scw.reshape(16).tobytes() + _frame_bytes(fr) + _points_bytes(pts)
+    out = _run(exe, "fusesim3", payload, tmp_path)
+    nf = struct.unpack_from("<i", out, 0)[0]
+    npnt, nfeat = len(pts["desc"]), len(fr["desc"])
+    rep = np.frombuffer(out, np.int32, npnt, 4)
+    kf = np.frombuffer(out, np.int32, nfeat, 4 + 4 * npnt)
+    want_kf = _sim3_entry(pts, fr)
+    bad = {c for c in want_kf if c <= -1000 and (-1000 - c) % 3 == 0}
+    want_rep = np.full(npnt, -1, np.int32)
+    for i, m in enumerate(ref["point_match"]):
+        if m < 0:
+            continue
+        if want_kf[m] != -1:
+            if want_kf[m] not in bad:
+                want_rep[i] = want_kf[m]
+        else:
+            want_kf[m] = i
+    assert nf == ref["nmatches"] and nf > 50
+    assert (want_rep >= 0).sum() > 0 and (want_rep <= -1000).sum() > 0
+    np.testing.assert_array_equal(rep, want_rep)
+    np.testing.assert_array_equal(kf, want_kf)
 
 
 def _tri_kf_bytes(d):
