@@ -37,6 +37,7 @@
  *                                                               src/ORBmatcher.cc:46-142, 1489-1795, include/ORBmatcher.h:64-95
  *   orbx_search_by_projection_device   batch of the above (one block per problem)
  *   orbx_search_for_triangulation  ORBmatcher::SearchForTriangulation src/ORBmatcher.cc:738-925, include/ORBmatcher.h:134
+ *   orbx_search_by_sim3            ORBmatcher::SearchBySim3 src/ORBmatcher.cc:1238-1487, include/ORBmatcher.h:139
  *   orbx_pose_optimization     Optimizer::PoseOptimization     src/Optimizer.cc:287-528, include/Optimizer.h:71
  *   orbx_pose_optimization_device      batch of the above (one block per frame)
  *   orbx_distinctive_descriptors[_device]  MapPoint::ComputeDistinctiveDescriptors src/MapPoint.cc:249-320
@@ -412,6 +413,10 @@ orbx_status orbx_pnp_iterate_many(orbx_pnp* const* solvers, int n, int n_iterati
  *                        spAlreadyFound = pKF->GetMapPoints() at entry; point_match[k] = bestIdx
  *                        when bestDist <= TH_LOW, *nmatches = nFused; the caller applies the
  *                        replace / AddMapPoint block, :1210-1229, in point order)
+ *   ORBX_PROJ_BY_SIM3    one direction of SearchBySim3 (src/ORBmatcher.cc:1283-1340; orbx_search_by_sim3
+ *                        below runs both): f = the other KeyFrame (its own Tcw unused), f.Tcw = the
+ *                        points' KeyFrame pose [Riw | tiw], last_Tcw = [sRji | tji]; flags bit0 =
+ *                        pMP && !vbAlreadyMatched && !isBad(); point_match[k] = bestIdx (<= TH_HIGH)
  * The current Frame (orbx_proj_frame) and the projected MapPoints are SoA
  * arrays the caller gathers from its object graph; the Frame's mvpMapPoints
  * on entry is summarised per feature as occ[i]: 0 NULL, 1 a MapPoint with
@@ -424,6 +429,7 @@ orbx_status orbx_pnp_iterate_many(orbx_pnp* const* solvers, int n, int n_iterati
 #define ORBX_PROJ_FUSE 3
 #define ORBX_PROJ_SIM3 4
 #define ORBX_PROJ_FUSE_SIM3 5
+#define ORBX_PROJ_BY_SIM3 6
 #define ORBX_PROJ_MAX_FEATURES 8192 /* Frame::N per problem */
 
 typedef struct {
@@ -488,6 +494,33 @@ orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int device);
 /* Batched, device-resident: problems[] is a HOST array whose pointers are
  * device pointers; one launch for the whole batch, stream-ordered. */
 orbx_status orbx_search_by_projection_device(const orbx_proj_problem* problems, int n, void* stream);
+
+/* ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12, s12, R12,
+ * t12, th) -- src/ORBmatcher.cc:1238-1487, include/ORBmatcher.h:139 (caller LoopClosing::ComputeSim3,
+ * src/LoopClosing.cc:422).  kf1 / kf2: the KeyFrames (keys_un, desc, bounds = int mnMinX.. as float,
+ * grid, levels, fx.., Tcw = GetPose()); per feature i of KF j the MapPoint GetMapPointMatches()[i]:
+ * descj/posj/dist_minmaxj (MapPoint descriptor, world position, mfMinDistance/mfMaxDistance) and flagsj
+ * bit0 = pMP && !vbAlreadyMatchedj[i] && !pMP->isBad() (vbAlreadyMatched from vpMatches12 on entry,
+ * :1262-1273).  match12[i1] = idx2 where the two directions agree (vpMatches12[i1] =
+ * vpMapPoints2[idx2]), -1 elsewhere; *nfound = nFound. */
+typedef struct {
+  orbx_proj_frame kf1, kf2;
+  const uint8_t* desc1;
+  const float* pos1;
+  const float* dist_minmax1;
+  const uint8_t* flags1;
+  const uint8_t* desc2;
+  const float* pos2;
+  const float* dist_minmax2;
+  const uint8_t* flags2;
+  float s12;
+  float R12[9];   /* row-major */
+  float t12[3];
+  float th;
+  int32_t* match12; /* kf1.n */
+  int32_t* nfound;
+} orbx_sim3_problem;
+orbx_status orbx_search_by_sim3(const orbx_sim3_problem* p, int device); /* host pointers */
 
 /* ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12,
  * vector<pair<size_t,size_t>>&, bOnlyStereo) -- src/ORBmatcher.cc:738-925,

@@ -56,6 +56,14 @@ class ProjProblem(C.Structure):
                [(k, C.c_void_p) for k in ("frame_out", "point_match", "nmatches")]
 
 
+class Sim3Problem(C.Structure):
+    _fields_ = [("kf1", ProjFrame), ("kf2", ProjFrame)] + \
+               [(k, C.c_void_p) for k in ("desc1", "pos1", "dist_minmax1", "flags1", "desc2", "pos2", "dist_minmax2",
+                                          "flags2")] + \
+               [("s12", C.c_float), ("R12", C.c_float * 9), ("t12", C.c_float * 3), ("th", C.c_float),
+                ("match12", C.c_void_p), ("nfound", C.c_void_p)]
+
+
 class PoseProblem(C.Structure):
     _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p)] + \
                [(k, C.c_float) for k in ("fx", "fy", "cx", "cy", "bf")] + \
@@ -510,6 +518,33 @@ def search_by_projection(frame, points, kind, th, nnratio=0.6, check_ori=True, m
     if kind == 0:
         out["track"], out["track_level"] = track, level
     return out
+
+
+def search_by_sim3(kf1, kf2, pts1, pts2, s12, R12, t12, th):
+    """SearchBySim3 reference: kfj = projection_frame dicts (Tcw = GetPose()), ptsj = per-feature MapPoint
+    arrays (desc, pos, dist_minmax, flags).  Returns (nFound, match12[N1])."""
+    f1, k1 = _proj_frame(kf1)
+    f2, k2 = _proj_frame(kf2)
+    p = Sim3Problem()
+    p.kf1, p.kf2 = f1, f2
+    keep = []
+    for j, pts in ((1, pts1), (2, pts2)):
+        for k, dt in (("desc", np.uint8), ("pos", np.float32), ("dist_minmax", np.float32), ("flags", np.uint8)):
+            a = np.ascontiguousarray(pts[k], dt)
+            keep.append(a)
+            setattr(p, "%s%d" % (k, j), _p(a))
+    p.s12, p.th = float(s12), float(th)
+    R = np.asarray(R12, np.float32).reshape(9)
+    t = np.asarray(t12, np.float32).reshape(3)
+    for i in range(9):
+        p.R12[i] = float(R[i])
+    for i in range(3):
+        p.t12[i] = float(t[i])
+    m = np.zeros(max(1, f1.n), np.int32)
+    nf = np.zeros(1, np.int32)
+    p.match12, p.nfound = _p(m), _p(nf)
+    lib().oracle_search_by_sim3(C.byref(p))
+    return int(nf[0]), m[:f1.n]
 
 
 def features_in_area(frame, x, y, r, min_level=-1, max_level=-1):

@@ -200,6 +200,27 @@ typedef struct {
 
 int oracle_search_by_projection(const oracle_proj_problem* p);
 
+/* ORBmatcher::SearchBySim3 (src/ORBmatcher.cc:1238-1487); layout identical to orbx_sim3_problem. */
+typedef struct {
+  oracle_proj_frame kf1, kf2;
+  const uint8_t* desc1;
+  const float* pos1;
+  const float* dist_minmax1;
+  const uint8_t* flags1;
+  const uint8_t* desc2;
+  const float* pos2;
+  const float* dist_minmax2;
+  const uint8_t* flags2;
+  float s12;
+  float R12[9];
+  float t12[3];
+  float th;
+  int32_t* match12;
+  int32_t* nfound;
+} oracle_sim3_problem;
+
+int oracle_search_by_sim3(const oracle_sim3_problem* p);
+
 /* Optimizer::PoseOptimization (src/Optimizer.cc:287-528); layout identical to
  * orbx_pose_problem in include/orbx.h. */
 typedef struct {

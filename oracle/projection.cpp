@@ -15,6 +15,7 @@
 //   ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th), matching half     src/ORBmatcher.cc:944-1054
 //   ORBmatcher::SearchByProjection(KeyFrame*, Scw, vector<MapPoint*>, vpMatched, th)  src/ORBmatcher.cc:327-440
 //   ORBmatcher::Fuse(KeyFrame*, Scw, vector<MapPoint*>, th, vpReplacePoint), matching half  :1094-1236
+//   ORBmatcher::SearchBySim3(KeyFrame*, KeyFrame*, vpMatches12, s12, R12, t12, th)  :1238-1487
 //
 // OpenCV arithmetic restated (parity vs the genuine library is unpinned; the
 // reference ships no fixture for any of this):
@@ -28,6 +29,7 @@
 //     by the float assignment; Mat::dot likewise sums double products.
 //   * std::log(float) in PredictScale: log_det() below, a double evaluation
 //     rounded once to float (shared operation sequence with the GPU).
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -575,9 +577,82 @@ int sim3(const oracle_proj_problem& P) {
   return nmatches;
 }
 
+// ORBmatcher::SearchBySim3, src/ORBmatcher.cc:1238-1487.  Matrix algebra as OpenCV 3.2 evaluates it:
+// s12*R12 and (1.0/s12)*R12.t() are convertTo(alpha) (x * (float)alpha + 0.0f, the transpose first);
+// -sR21*t12 is cv::gemm's small-matrix path with alpha = -1; A*x + b of 3x1 Mats is mat3x1.
+// One direction: the MapPoints of KeyFrame `own` (per feature i, flags bit0 = pMP && !vbAlreadyMatched
+// && !isBad()) into KeyFrame `other` through [sR | t]; vnMatch[i] = bestIdx (bestDist <= TH_HIGH).
+void sim3_direction(const oracle_proj_frame& own, const oracle_proj_frame& other, const uint8_t* desc,
+                    const float* pos, const float* dmm, const uint8_t* flags, const float* A, float th,
+                    std::vector<int>& vnMatch) {
+  Frame fr(other);
+  vnMatch.assign(own.n, -1);
+  for (int i = 0; i < own.n; i++) {
+    if (!(flags[i] & 1)) continue;
+    const float* X = pos + 3 * i;
+    float c1[3], c2[3];
+    mat3x1(own.Tcw, X, c1);  // R1w*p3Dw + t1w
+    mat3x1(A, c1, c2);       // sR21*p3Dc1 + t21
+    if (c2[2] < 0.0) continue;
+    const float invz = (float)(1.0 / (double)c2[2]);
+    const float x = c2[0] * invz, y = c2[1] * invz;
+    const float u = other.fx * x + other.cx, v = other.fy * y + other.cy;
+    if (!(u >= other.min_x && u < other.max_x && v >= other.min_y && v < other.max_y)) continue;  // IsInImage
+    const float maxDistance = 1.2f * dmm[2 * i + 1], minDistance = 0.8f * dmm[2 * i];
+    const float dist3D = norm3(c2);
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    const int nPredictedLevel = predict_scale(dmm[2 * i + 1], dist3D, other.log_scale_factor, other.nlevels);
+    const float radius = th * other.scale_factors[nPredictedLevel];
+    const std::vector<int> cand = fr.area(u, v, radius);
+    if (cand.empty()) continue;
+    int bestDist = INT_MAX, bestIdx = -1;
+    for (int idx : cand) {
+      const int oct = other.keys_un[idx].octave;
+      if (oct < nPredictedLevel - 1 || oct > nPredictedLevel) continue;
+      const int d = hamming(desc + 32 * (size_t)i, other.desc + 32 * (size_t)idx);
+      if (d < bestDist) {
+        bestDist = d;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= kThHigh) vnMatch[i] = bestIdx;
+  }
+}
+
+int search_by_sim3(const oracle_sim3_problem& P) {
+  float sR12[16], sR21[16];
+  const float a12 = (float)(double)P.s12, a21 = (float)(1.0 / (double)P.s12);
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      sR12[4 * r + c] = P.R12[3 * r + c] * a12 + 0.0f;  // s12*R12
+      sR21[4 * r + c] = P.R12[3 * c + r] * a21 + 0.0f;  // (1.0/s12)*R12.t()
+    }
+  for (int r = 0; r < 3; r++) {
+    sR12[4 * r + 3] = P.t12[r];
+    const float t0 = sR21[4 * r] * P.t12[0] + sR21[4 * r + 1] * P.t12[1] + sR21[4 * r + 2] * P.t12[2];
+    sR21[4 * r + 3] = (float)((double)t0 * -1.0);  // t21 = -sR21*t12
+  }
+  std::vector<int> vnMatch1, vnMatch2;
+  sim3_direction(P.kf1, P.kf2, P.desc1, P.pos1, P.dist_minmax1, P.flags1, sR21, P.th, vnMatch1);
+  sim3_direction(P.kf2, P.kf1, P.desc2, P.pos2, P.dist_minmax2, P.flags2, sR12, P.th, vnMatch2);
+  int nFound = 0;
+  for (int i1 = 0; i1 < P.kf1.n; i1++) {
+    P.match12[i1] = -1;
+    const int idx2 = vnMatch1[i1];
+    if (idx2 >= 0 && vnMatch2[idx2] == i1) {
+      P.match12[i1] = idx2;
+      nFound++;
+    }
+  }
+  *P.nfound = nFound;
+  return nFound;
+}
+
 }  // namespace
 
 extern "C" {
+
+int oracle_search_by_sim3(const oracle_sim3_problem* P) { return P ? search_by_sim3(*P) : -1; }
 
 int oracle_search_by_projection(const oracle_proj_problem* P) {
   if (!P) return -1;

@@ -94,6 +94,14 @@ class ProjProblem(C.Structure):
                 ("Tcw_dev", C.c_void_p), ("gate", C.c_void_p), ("gate_below", C.c_int)]
 
 
+class Sim3Problem(C.Structure):
+    _fields_ = [("kf1", ProjFrame), ("kf2", ProjFrame)] + \
+               [(k, C.c_void_p) for k in ("desc1", "pos1", "dist_minmax1", "flags1", "desc2", "pos2", "dist_minmax2",
+                                          "flags2")] + \
+               [("s12", C.c_float), ("R12", C.c_float * 9), ("t12", C.c_float * 3), ("th", C.c_float),
+                ("match12", C.c_void_p), ("nfound", C.c_void_p)]
+
+
 class PoseProblem(C.Structure):
     _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p),
                 ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
@@ -198,6 +206,7 @@ SIGNATURES = {
     "orbx_frame_points_device": ([C.POINTER(FramePoints), C.c_int, P], C.c_int),
     "orbx_track_step_device": ([C.POINTER(TrackStep), C.c_int, P], C.c_int),
     "orbx_search_by_projection": ([C.POINTER(ProjProblem), C.c_int], C.c_int),
+    "orbx_search_by_sim3": ([C.POINTER(Sim3Problem), C.c_int], C.c_int),
     "orbx_search_by_projection_device": ([C.POINTER(ProjProblem), C.c_int, P], C.c_int),
     "orbx_pose_optimization": ([C.POINTER(PoseProblem), C.c_int], C.c_int),
     "orbx_pose_optimization_device": ([C.POINTER(PoseProblem), C.c_int, P], C.c_int),

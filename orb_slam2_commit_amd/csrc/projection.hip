@@ -2,7 +2,7 @@
 // every tracked frame (src/ORBmatcher.cc:46-142 local map, :1489-1646 last
 // frame, :1648-1795 keyframe), the matching half of Fuse (:944-1054) and the
 // loop-closing SearchByProjection(KeyFrame*, Scw, ...) (:327-440) and Fuse(KeyFrame*, Scw, ...)
-// (:1094-1236, matching half), with
+// (:1094-1236, matching half), and both directions of SearchBySim3 (:1238-1487), with
 // Frame::AssignFeaturesToGrid /
 // GetFeaturesInArea (src/Frame.cc:254-271, 388-453) and, for the local map,
 // Frame::isInFrustum (src/Frame.cc:315-375) fused in front.  One block per
@@ -165,6 +165,29 @@ __device__ Query setup_query(const ProjProblem& P, int i, const float* Tcw, cons
   if (!(fl & 1)) return q;
   const float* X = P.pos + 3 * i;
   float c[3];
+  if (P.kind == ORBX_PROJ_BY_SIM3) {  // one direction of SearchBySim3, src/ORBmatcher.cc:1283-1340
+    float c1[3];
+    mat3x1(Tcw, X, c1);          // R1w*p3Dw + t1w (the point's own KeyFrame)
+    mat3x1(P.last_Tcw, c1, c);   // sR21*p3Dc1 + t21
+    if (c[2] < 0.0f) return q;
+    const float invz = (float)(1.0 / (double)c[2]);
+    const float x = c[0] * invz, y = c[1] * invz;
+    const float u = F.fx * x + F.cx, v = F.fy * y + F.cy;
+    if (!(u >= F.min_x && u < F.max_x && v >= F.min_y && v < F.max_y)) return q;  // KeyFrame::IsInImage
+    const float d3 = norm3(c);
+    const float dmin = P.dist_minmax[2 * i], dmax = P.dist_minmax[2 * i + 1];
+    if (d3 < 0.8f * dmin || d3 > 1.2f * dmax) return q;
+    const int lvl = predict_scale(dmax, d3, F.log_scale_factor, F.nlevels);
+    q.r = P.th * F.scale_factors[lvl];
+    q.x = u;
+    q.y = v;
+    q.min_level = lvl - 1;
+    q.max_level = lvl;
+    q.ur_th = -1.0f;
+    q.th = kThHigh;
+    q.active = true;
+    return q;
+  }
   mat3x1(Tcw, X, c);
   if (P.kind == ORBX_PROJ_FUSE || P.kind == ORBX_PROJ_SIM3 || P.kind == ORBX_PROJ_FUSE_SIM3) {
     // src/ORBmatcher.cc:960-1006, :352-391, :1117-1160
@@ -380,7 +403,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   // KEYFRAME and SIM3: any MapPoint on the feature blocks it, and every match blocks later points
   const bool kf = P.kind == ORBX_PROJ_KEYFRAME || P.kind == ORBX_PROJ_SIM3;
   // no "already matched" state: one sweep (FUSE also gates candidates by reprojection error)
-  const bool fuse = P.kind == ORBX_PROJ_FUSE || P.kind == ORBX_PROJ_FUSE_SIM3;
+  const bool fuse = P.kind == ORBX_PROJ_FUSE || P.kind == ORBX_PROJ_FUSE_SIM3 || P.kind == ORBX_PROJ_BY_SIM3;
   const bool gate = P.kind == ORBX_PROJ_FUSE;
   for (int sweep = 0; sweep <= nP + 1; sweep++) {
     if (tid == 0) s_changed = 0;
@@ -559,7 +582,7 @@ orbx_status proj_status(hipError_t e) { return e == hipSuccess ? ORBX_OK : ORBX_
 
 // Host-side argument checks shared by both entry points (the kernel assumes them).
 orbx_status proj_check(const orbx_proj_problem& p, bool host) {
-  if (p.kind < ORBX_PROJ_LOCAL || p.kind > ORBX_PROJ_FUSE_SIM3) return ORBX_ERR_ARG;
+  if (p.kind < ORBX_PROJ_LOCAL || p.kind > ORBX_PROJ_BY_SIM3) return ORBX_ERR_ARG;
   if (p.f.n < 0 || p.n_points < 0) return ORBX_ERR_ARG;
   if (p.f.n > ORBX_PROJ_MAX_FEATURES) return ORBX_ERR_CAPACITY;
   if (p.f.nlevels < 1 || p.f.nlevels > 16) return ORBX_ERR_ARG;
@@ -581,6 +604,9 @@ orbx_status proj_check(const orbx_proj_problem& p, bool host) {
         if (host)
           for (int i = 0; i < p.n_points; i++)
             if ((p.flags[i] & 1) && (p.octave[i] < 0 || p.octave[i] >= p.f.nlevels)) return ORBX_ERR_ARG;
+        break;
+      case ORBX_PROJ_BY_SIM3:
+        if (!p.pos || !p.dist_minmax) return ORBX_ERR_ARG;
         break;
       case ORBX_PROJ_FUSE:
       case ORBX_PROJ_SIM3:
@@ -689,4 +715,71 @@ extern "C" orbx_status orbx_search_by_projection_device(const orbx_proj_problem*
   if (e == hipSuccess) e = orbx::launch_search_by_projection(dP, n, st);
   const hipError_t e2 = hipFreeAsync(dP, st);
   return proj_status(e != hipSuccess ? e : e2);
+}
+
+namespace {
+// sR12 = s12*R12, sR21 = (1.0/s12)*R12.t(), t21 = -sR21*t12 (src/ORBmatcher.cc:1252-1254): a Mat times
+// a scalar is convertTo(alpha) -- x * (float)alpha + 0.0f in float; R12.t() scaled is transpose then
+// convertTo; -A*b is cv::gemm's small-matrix path (float dot, then (float)((double)t0 * -1.0))
+void sim3_pair(float s12, const float* R12, const float* t12, float* sR12_t12, float* sR21_t21) {
+  const float a12 = (float)(double)s12, a21 = (float)(1.0 / (double)s12);
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) {
+      sR12_t12[4 * r + c] = R12[3 * r + c] * a12 + 0.0f;
+      sR21_t21[4 * r + c] = R12[3 * c + r] * a21 + 0.0f;
+    }
+    sR12_t12[4 * r + 3] = t12[r];
+  }
+  for (int r = 0; r < 3; r++) {
+    const float t0 = sR21_t21[4 * r] * t12[0] + sR21_t21[4 * r + 1] * t12[1] + sR21_t21[4 * r + 2] * t12[2];
+    sR21_t21[4 * r + 3] = (float)((double)t0 * -1.0);
+  }
+  for (int k = 12; k < 16; k++) sR12_t12[k] = sR21_t21[k] = k == 15 ? 1.0f : 0.0f;
+}
+}  // namespace
+
+extern "C" orbx_status orbx_search_by_sim3(const orbx_sim3_problem* p, int device) {
+  if (!p || !p->match12 || !p->nfound) return ORBX_ERR_ARG;
+  const int N1 = p->kf1.n, N2 = p->kf2.n;
+  if (N1 < 0 || N2 < 0) return ORBX_ERR_ARG;
+  if (!(p->s12 > 0.0f) && !(p->s12 < 0.0f)) return ORBX_ERR_ARG;  // 1/s12
+  float A12[16], A21[16];
+  sim3_pair(p->s12, p->R12, p->t12, A12, A21);
+  // direction 1: KF1's MapPoints into KF2 (points = KF1 features), direction 2: KF2's into KF1
+  std::vector<int32_t> m1(N1 > 0 ? N1 : 1, -1), m2(N2 > 0 ? N2 : 1, -1);
+  std::vector<int32_t> fo1(N2 > 0 ? N2 : 1), fo2(N1 > 0 ? N1 : 1);
+  int32_t n1 = 0, n2 = 0;
+  for (int d = 0; d < 2; d++) {
+    orbx_proj_problem q;
+    std::memset(&q, 0, sizeof(q));
+    q.kind = ORBX_PROJ_BY_SIM3;
+    q.f = d == 0 ? p->kf2 : p->kf1;
+    q.f.occ = nullptr;
+    const orbx_proj_frame& own = d == 0 ? p->kf1 : p->kf2;  // the points' KeyFrame: R1w|t1w or R2w|t2w
+    std::memcpy(q.f.Tcw, own.Tcw, sizeof(q.f.Tcw));
+    std::memcpy(q.last_Tcw, d == 0 ? A21 : A12, sizeof(q.last_Tcw));
+    q.n_points = d == 0 ? N1 : N2;
+    q.desc = d == 0 ? p->desc1 : p->desc2;
+    q.flags = d == 0 ? p->flags1 : p->flags2;
+    q.pos = d == 0 ? p->pos1 : p->pos2;
+    q.dist_minmax = d == 0 ? p->dist_minmax1 : p->dist_minmax2;
+    q.th = p->th;
+    q.frame_out = d == 0 ? fo1.data() : fo2.data();
+    q.point_match = d == 0 ? m1.data() : m2.data();
+    q.nmatches = d == 0 ? &n1 : &n2;
+    const orbx_status st = orbx_search_by_projection(&q, device);
+    if (st != ORBX_OK) return st;
+  }
+  // mutual check (:1466-1482)
+  int nFound = 0;
+  for (int i1 = 0; i1 < N1; i1++) {
+    const int idx2 = m1[i1];
+    p->match12[i1] = -1;
+    if (idx2 >= 0 && idx2 < N2 && m2[idx2] == i1) {
+      p->match12[i1] = idx2;
+      nFound++;
+    }
+  }
+  *p->nfound = nFound;
+  return ORBX_OK;
 }

@@ -317,6 +317,31 @@ class ORBmatcher:
         o = _run_projection(self, F, vpPoints, PROJ_FUSE_SIM3, th=float(th))
         return int(o["nmatches"][0]), o["point_match"]
 
+    def SearchBySim3(self, pKF1, pKF2, pts1, pts2, s12, R12, t12, th=7.5):
+        """SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12, s12, R12, t12, th)
+        -- src/ORBmatcher.cc:1238-1487 (LoopClosing::ComputeSim3).  pKFj: frame dicts (Tcw = GetPose());
+        ptsj: the KeyFrame's GetMapPointMatches() as per-feature arrays (desc, pos, dist_minmax, flags bit0
+        = pMP && !vbAlreadyMatched && !isBad()).  Returns (nFound, match12[N1]: the KF2 feature whose
+        MapPoint becomes vpMatches12[i1], -1 none)."""
+        f1, k1 = _host_proj_frame(pKF1)
+        f2, k2 = _host_proj_frame(pKF2)
+        p = _lib.Sim3Problem()
+        p.kf1, p.kf2 = f1, f2
+        keep = [k1, k2]
+        for j, pts in ((1, pts1), (2, pts2)):
+            for k, dt in (("desc", np.uint8), ("pos", np.float32), ("dist_minmax", np.float32), ("flags", np.uint8)):
+                a = np.ascontiguousarray(pts[k], dt)
+                keep.append(a)
+                setattr(p, "%s%d" % (k, j), ptr(a))
+        p.s12, p.th = float(s12), float(th)
+        p.R12[:] = _f32(R12).reshape(9).tolist()
+        p.t12[:] = _f32(t12).reshape(3).tolist()
+        m = np.zeros(max(1, f1.n), np.int32)
+        nf = np.zeros(1, np.int32)
+        p.match12, p.nfound = ptr(m), ptr(nf)
+        check(_lib.lib().orbx_search_by_sim3(C.byref(p), self.device), "orbx_search_by_sim3")
+        return int(nf[0]), m[:f1.n]
+
     def SearchForTriangulation(self, prob, bOnlyStereo=False):
         """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) --
         src/ORBmatcher.cc:738-925.  prob: dict(kf1, kf2 (keys_un, desc, u_right, has_mp, node_id,
@@ -404,6 +429,14 @@ def proj_problem(frame, points, kind, th, nnratio=0.6, check_ori=True, mono=Fals
     p.frame_out, p.point_match, p.nmatches = (ptr(outputs["frame_out"]), ptr(outputs["point_match"]),
                                               ptr(outputs["nmatches"]))
     return p, outputs
+
+
+def _host_proj_frame(frame):
+    """An orbx_proj_frame over host copies of a frame dict's arrays; returns (frame, keep-alive)."""
+    fr = _host_frame(frame)
+    p, _ = proj_problem(fr, dict(desc=np.zeros((0, 32), np.uint8), flags=np.zeros(0, np.uint8)), PROJ_KEYFRAME,
+                        th=1.0, outputs=dict(frame_out=None, point_match=None, nmatches=None))
+    return p.f, fr
 
 
 def _host_points(points):

@@ -733,6 +733,60 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector
   return nm;
 }
 
+int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12, const float& s12,
+                             const cv::Mat& R12, const cv::Mat& t12, const float th) {
+  // src/ORBmatcher.cc:1238-1487 (caller LoopClosing::ComputeSim3, src/LoopClosing.cc:422): both
+  // directions on the GPU (orbx_search_by_sim3), vbAlreadyMatched1/2 from vpMatches12 here (:1262-1273)
+  const std::vector<MapPoint*> vp1 = pKF1->GetMapPointMatches(), vp2 = pKF2->GetMapPointMatches();
+  const int N1 = (int)vp1.size(), N2 = (int)vp2.size();
+  std::vector<char> am1(N1, 0), am2(N2, 0);
+  for (int i = 0; i < N1 && i < (int)vpMatches12.size(); i++) {
+    MapPoint* pMP = vpMatches12[i];
+    if (!pMP) continue;
+    am1[i] = 1;
+    const int idx2 = pMP->GetIndexInKeyFrame(pKF2);
+    if (idx2 >= 0 && idx2 < N2) am2[idx2] = 1;
+  }
+  orbx_sim3_problem p;
+  std::memset(&p, 0, sizeof(p));
+  cv::Mat d1, d2;
+  p.kf1 = fuse_frame(pKF1, d1);
+  p.kf2 = fuse_frame(pKF2, d2);
+  ProjPoints P1(N1), P2(N2);
+  auto side = [](const std::vector<MapPoint*>& vp, const std::vector<char>& am, ProjPoints& P) {
+    for (size_t i = 0; i < vp.size(); i++) {
+      MapPoint* pMP = vp[i];
+      if (!pMP || am[i] || pMP->isBad()) continue;
+      P.flags[i] = 1;
+      copy_desc(pMP, &P.desc[32 * i]);
+      copy_pos(pMP, &P.pos[3 * i]);
+      copy_dist(pMP, &P.dist[2 * i]);
+    }
+  };
+  side(vp1, am1, P1);
+  side(vp2, am2, P2);
+  p.desc1 = P1.desc.data();
+  p.pos1 = P1.pos.data();
+  p.dist_minmax1 = P1.dist.data();
+  p.flags1 = P1.flags.data();
+  p.desc2 = P2.desc.data();
+  p.pos2 = P2.pos.data();
+  p.dist_minmax2 = P2.dist.data();
+  p.flags2 = P2.flags.data();
+  p.s12 = s12;
+  for (int i = 0; i < 9; i++) p.R12[i] = R12.at<float>(i / 3, i % 3);
+  for (int i = 0; i < 3; i++) p.t12[i] = t12.at<float>(i, 0);
+  p.th = th;
+  std::vector<int32_t> m12(N1 > 0 ? N1 : 1, -1);
+  int32_t nf = 0;
+  p.match12 = m12.data();
+  p.nfound = &nf;
+  check(orbx_search_by_sim3(&p, mDevice), "orbx_search_by_sim3");
+  for (int i1 = 0; i1 < N1; i1++)
+    if (m12[i1] >= 0) vpMatches12[i1] = vp2[m12[i1]];
+  return nf;
+}
+
 std::set<MapPoint*> KeyFrame::GetMapPoints() {
   std::unique_lock<std::mutex> lock(mMutexFeatures);
   std::set<MapPoint*> s;

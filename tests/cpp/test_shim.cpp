@@ -12,6 +12,7 @@
 //   fuse    IN OUT      ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>, th) incl. Replace / AddObservation
 //   sim3    IN OUT      ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)
 //   fusesim3 IN OUT     ORBmatcher::Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint)
+//   bysim3  IN OUT      ORBmatcher::SearchBySim3(KeyFrame*, KeyFrame*, vpMatches12, s12, R12, t12, th)
 //   tri     IN OUT      ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, F12, pairs, bOnlyStereo)
 //   pose    IN OUT      Optimizer::PoseOptimization(Frame*)
 //   distinct IN OUT     MapPoint::ComputeDistinctiveDescriptors
@@ -1057,6 +1058,77 @@ static int mode_fusesim3(const char* in, const char* out) {
   return 0;
 }
 
+// SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th): both KeyFrames are the payload frame (two
+// frame records), feature i of KeyFrame j holds point i of points payload j.  Points with bit0 off:
+// i % 3 == 0 NULL, == 1 bad, == 2 "already matched" -- KF1's such features take vpMatches12 entries
+// pointing at KF2's such MapPoints in order (observed by KF2 there; KF2's left over are bad, KF1's left
+// over point at a MapPoint outside KF2).  Out: nFound, vpMatches12 per KF1 feature (KF2 feature
+// index of the MapPoint, -2 one outside KF2, -1 NULL).
+static int mode_bysim3(const char* in, const char* out) {
+  Reader r(in);
+  const float th = r.get<float>(), s12 = r.get<float>();
+  cv::Mat R12(3, 3, CV_32F), t12(3, 1, CV_32F);
+  for (int i = 0; i < 9; i++) R12.at<float>(i / 3, i % 3) = r.get<float>();
+  for (int i = 0; i < 3; i++) t12.at<float>(i, 0) = r.get<float>();
+  FramePayload fp1, fp2;
+  read_frame(r, fp1);
+  read_frame(r, fp2);
+  PointPayload P1, P2;
+  read_points(r, P1);
+  read_points(r, P2);
+  KeyFrame K1, K2;
+  keyframe_from_frame(fp1.F, K1);
+  keyframe_from_frame(fp2.F, K2);
+  K2.mnId = 1001;
+  std::vector<std::unique_ptr<MapPoint>> own;
+  auto fill = [&](KeyFrame& K, const PointPayload& P, std::vector<MapPoint*>& mp) {
+    mp.assign(K.N, nullptr);
+    for (int i = 0; i < K.N && i < P.n; i++) {
+      if (!(P.flags[i] & 1) && i % 3 == 0) continue;  // NULL
+      own.emplace_back(new MapPoint());
+      MapPoint& m = *own.back();
+      make_point(m, P, i);
+      m.mbBad = !(P.flags[i] & 1) && i % 3 == 1;
+      mp[i] = &m;
+      K.mvpMapPoints[i] = &m;
+    }
+  };
+  std::vector<MapPoint*> mp1, mp2;
+  fill(K1, P1, mp1);
+  fill(K2, P2, mp2);
+  std::vector<int> targets;  // KF2's "already matched" features
+  for (int j = 0; j < K2.N && j < P2.n; j++)
+    if (!(P2.flags[j] & 1) && j % 3 == 2) targets.push_back(j);
+  std::vector<MapPoint*> vpMatches12(K1.N, nullptr);
+  own.emplace_back(new MapPoint());
+  MapPoint* outside = own.back().get();
+  size_t t = 0;
+  for (int i = 0; i < K1.N && i < P1.n; i++) {
+    if ((P1.flags[i] & 1) || i % 3 != 2) continue;
+    if (t < targets.size()) {
+      MapPoint* m = mp2[targets[t]];
+      m->AddObservation(&K2, targets[t]);
+      vpMatches12[i] = m;
+      t++;
+    } else {
+      vpMatches12[i] = outside;
+    }
+  }
+  for (; t < targets.size(); t++) mp2[targets[t]]->mbBad = true;
+  ORBmatcher matcher;
+  const int nf = matcher.SearchBySim3(&K1, &K2, vpMatches12, s12, R12, t12, th);
+  Writer o(out);
+  o.put<int32_t>(nf);
+  for (int i = 0; i < K1.N; i++) {
+    int v = vpMatches12[i] ? -2 : -1;
+    for (int j = 0; j < K2.N && v == -2; j++)
+      if (mp2[j] == vpMatches12[i]) v = j;
+    o.put<int32_t>(v);
+  }
+  std::printf("bysim3 ok: %d found\n", nf);
+  return 0;
+}
+
 // SearchForTriangulation(KeyFrame*, KeyFrame*, F12, vMatchedPairs, bOnlyStereo)
 static void read_tri_kf(Reader& r, KeyFrame& K) {
   K.N = r.get<int32_t>();
@@ -1269,6 +1341,7 @@ int main(int argc, char** argv) {
     if (m == "fuse") return mode_fuse(argv[2], argv[3]);
     if (m == "sim3") return mode_sim3(argv[2], argv[3]);
     if (m == "fusesim3") return mode_fusesim3(argv[2], argv[3]);
+    if (m == "bysim3") return mode_bysim3(argv[2], argv[3]);
     if (m == "tri") return mode_tri(argv[2], argv[3]);
     if (m == "pose") return mode_pose(argv[2], argv[3]);
     if (m == "distinct") return mode_distinct(argv[2], argv[3]);

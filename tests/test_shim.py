@@ -10,6 +10,7 @@ each compared with the oracle exactly as the ctypes-level tests do.
 import os
 import struct
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -76,6 +77,9 @@ def test_shim_exports_reference_classes(exe):
                 "ORB_SLAM2::ORBmatcher::SearchByProjection(ORB_SLAM2::KeyFrame*, cv::Mat, "
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> > const&, "
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&, int)",
+                "ORB_SLAM2::ORBmatcher::SearchBySim3(ORB_SLAM2::KeyFrame*, ORB_SLAM2::KeyFrame*, "
+                "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&, float const&, "
+                "cv::Mat const&, cv::Mat const&, float)",
                 "ORB_SLAM2::ORBmatcher::Fuse(ORB_SLAM2::KeyFrame*, cv::Mat, std::vector<ORB_SLAM2::MapPoint*, "
                 "std::allocator<ORB_SLAM2::MapPoint*> > const&, float, std::vector<ORB_SLAM2::MapPoint*, "
                 "std::allocator<ORB_SLAM2::MapPoint*> >&)",
@@ -619,6 +623,36 @@ def test_shim_fuse_sim3(gpu, exe, tmp_path, variant, th):
     assert (want_rep >= 0).sum() > 0 and (want_rep <= -1000).sum() > 0
     np.testing.assert_array_equal(rep, want_rep)
     np.testing.assert_array_equal(kf, want_kf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,s12,th", [(0, 1.1, 7.5), (1, 0.93, 7.5)])
+def test_shim_search_by_sim3(gpu, exe, tmp_path, seed, s12, th):
+    """ORBmatcher::SearchBySim3(KeyFrame*, KeyFrame*, vpMatches12, s12, R12, t12, th)
+    (include/ORBmatcher.h:139): vbAlreadyMatched1/2 from vpMatches12 on entry (GetIndexInKeyFrame),
+    NULL and bad MapPoints skipped, both directions on the MI355X, vpMatches12 afterwards equal to the
+    oracle's cross-checked matches, entry entries kept."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_projection import _sim3_pair_case
+    kf1, kf2, p1, p2, s, R12, t12 = _sim3_pair_case(980 + seed, n=1500, s12=s12)
+    nf_ref, m12 = oracle.search_by_sim3(kf1, kf2, p1, p2, s, R12, t12, th)
+    payload = (struct.pack("<ff", th, float(s)) + np.asarray(R12, np.float32).tobytes()
+               + np.asarray(t12, np.float32).tobytes() + _frame_bytes(kf1) + _frame_bytes(kf2)
+               + _points_bytes(p1) + _points_bytes(p2))
+    out = _run(exe, "bysim3", payload, tmp_path)
+    nf = struct.unpack_from("<i", out, 0)[0]
+    state = np.frombuffer(out, np.int32, offset=4)
+    f1, f2 = np.asarray(p1["flags"]), np.asarray(p2["flags"])
+    targets = [j for j in range(len(f2)) if not (f2[j] & 1) and j % 3 == 2]
+    want = np.full(len(f1), -1, np.int32)
+    t = 0
+    for i in range(len(f1)):
+        if not (f1[i] & 1) and i % 3 == 2:
+            want[i] = targets[t] if t < len(targets) else -2
+            t += 1
+    want = np.where(m12 >= 0, m12, want)
+    assert nf == nf_ref > 100
+    np.testing.assert_array_equal(state, want)
 
 
 def _tri_kf_bytes(d):
