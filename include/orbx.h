@@ -38,6 +38,7 @@
  *   orbx_search_by_projection_device   batch of the above (one block per problem)
  *   orbx_search_for_triangulation  ORBmatcher::SearchForTriangulation src/ORBmatcher.cc:738-925, include/ORBmatcher.h:134
  *   orbx_search_by_sim3            ORBmatcher::SearchBySim3 src/ORBmatcher.cc:1238-1487, include/ORBmatcher.h:139
+ *   orbx_search_for_initialization ORBmatcher::SearchForInitialization src/ORBmatcher.cc:442-587, include/ORBmatcher.h:130
  *   orbx_pose_optimization     Optimizer::PoseOptimization     src/Optimizer.cc:287-528, include/Optimizer.h:71
  *   orbx_pose_optimization_device      batch of the above (one block per frame)
  *   orbx_distinctive_descriptors[_device]  MapPoint::ComputeDistinctiveDescriptors src/MapPoint.cc:249-320
@@ -521,6 +522,24 @@ typedef struct {
   int32_t* nfound;
 } orbx_sim3_problem;
 orbx_status orbx_search_by_sim3(const orbx_sim3_problem* p, int device); /* host pointers */
+
+/* ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
+ * vector<int>& vnMatches12, int windowSize) -- src/ORBmatcher.cc:442-587, include/ORBmatcher.h:130
+ * (caller Tracking::MonocularInitialization, src/Tracking.cc:711).  f1: keys_un (octave >= 0, angle), desc; f2: keys_un,
+ * desc and the grid fields (min_x, min_y, grid_inv_w/h); the other frame fields are unused.
+ * prev_matched: f1.n (x, y) pairs, updated in place as vbPrevMatched; match12[i1] = vnMatches12[i1];
+ * nnratio = the ORBmatcher's mfNNratio (0.9 in the reference's initializer), check_ori =
+ * mbCheckOrientation.  n1, n2 <= ORBX_PROJ_MAX_FEATURES. */
+typedef struct {
+  orbx_proj_frame f1, f2;
+  float* prev_matched;
+  int window;
+  float nnratio;
+  int check_ori;
+  int32_t* match12;
+  int32_t* nmatches;
+} orbx_init_problem;
+orbx_status orbx_search_for_initialization(const orbx_init_problem* p, int device); /* host pointers */
 
 /* ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, cv::Mat F12,
  * vector<pair<size_t,size_t>>&, bOnlyStereo) -- src/ORBmatcher.cc:738-925,

@@ -64,6 +64,11 @@ class Sim3Problem(C.Structure):
                 ("match12", C.c_void_p), ("nfound", C.c_void_p)]
 
 
+class InitProblem(C.Structure):
+    _fields_ = [("f1", ProjFrame), ("f2", ProjFrame), ("prev_matched", C.c_void_p), ("window", C.c_int),
+                ("nnratio", C.c_float), ("check_ori", C.c_int), ("match12", C.c_void_p), ("nmatches", C.c_void_p)]
+
+
 class PoseProblem(C.Structure):
     _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p)] + \
                [(k, C.c_float) for k in ("fx", "fy", "cx", "cy", "bf")] + \
@@ -545,6 +550,21 @@ def search_by_sim3(kf1, kf2, pts1, pts2, s12, R12, t12, th):
     p.match12, p.nfound = _p(m), _p(nf)
     lib().oracle_search_by_sim3(C.byref(p))
     return int(nf[0]), m[:f1.n]
+
+
+def search_for_initialization(f1, f2, prev_matched, window=100, nnratio=0.9, check_ori=True):
+    """SearchForInitialization reference: returns (nmatches, vnMatches12[N1], vbPrevMatched[N1,2])."""
+    a, k1 = _proj_frame(f1)
+    b, k2 = _proj_frame(f2)
+    p = InitProblem()
+    p.f1, p.f2 = a, b
+    prev = np.ascontiguousarray(prev_matched, np.float32).reshape(-1, 2).copy()
+    m = np.zeros(max(1, a.n), np.int32)
+    nm = np.zeros(1, np.int32)
+    p.prev_matched, p.window, p.nnratio, p.check_ori = _p(prev), int(window), float(nnratio), int(bool(check_ori))
+    p.match12, p.nmatches = _p(m), _p(nm)
+    lib().oracle_search_for_initialization(C.byref(p))
+    return int(nm[0]), m[:a.n], prev
 
 
 def features_in_area(frame, x, y, r, min_level=-1, max_level=-1):

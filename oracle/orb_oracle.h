@@ -221,6 +221,20 @@ typedef struct {
 
 int oracle_search_by_sim3(const oracle_sim3_problem* p);
 
+/* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:442-587); layout identical to
+ * orbx_init_problem. */
+typedef struct {
+  oracle_proj_frame f1, f2;
+  float* prev_matched;
+  int window;
+  float nnratio;
+  int check_ori;
+  int32_t* match12;
+  int32_t* nmatches;
+} oracle_init_problem;
+
+int oracle_search_for_initialization(const oracle_init_problem* p);
+
 /* Optimizer::PoseOptimization (src/Optimizer.cc:287-528); layout identical to
  * orbx_pose_problem in include/orbx.h. */
 typedef struct {

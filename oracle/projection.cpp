@@ -16,6 +16,7 @@
 //   ORBmatcher::SearchByProjection(KeyFrame*, Scw, vector<MapPoint*>, vpMatched, th)  src/ORBmatcher.cc:327-440
 //   ORBmatcher::Fuse(KeyFrame*, Scw, vector<MapPoint*>, th, vpReplacePoint), matching half  :1094-1236
 //   ORBmatcher::SearchBySim3(KeyFrame*, KeyFrame*, vpMatches12, s12, R12, t12, th)  :1238-1487
+//   ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)  :442-587
 //
 // OpenCV arithmetic restated (parity vs the genuine library is unpinned; the
 // reference ships no fixture for any of this):
@@ -648,9 +649,82 @@ int search_by_sim3(const oracle_sim3_problem& P) {
   return nFound;
 }
 
+// ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize),
+// src/ORBmatcher.cc:442-587, statement by statement (level-0 F1 keypoints only; the window search is
+// F2.GetFeaturesInArea(x, y, w, 0, 0); a feature taken by a later F1 keypoint with a smaller
+// distance drops the earlier match; rotHist holds every accepted match, dropped ones included).
+int search_for_initialization(const oracle_init_problem& P) {
+  const oracle_proj_frame& F1 = P.f1;
+  const oracle_proj_frame& F2 = P.f2;
+  Frame fr2(F2);
+  int nmatches = 0;
+  std::vector<int> vnMatches12(F1.n, -1);
+  std::vector<int> rotHist[kHisto];
+  std::vector<int> vMatchedDistance(F2.n, INT_MAX), vnMatches21(F2.n, -1);
+  for (int i1 = 0; i1 < F1.n; i1++) {
+    const oracle_keypoint& kp1 = F1.keys_un[i1];
+    const int level1 = kp1.octave;
+    if (level1 > 0) continue;
+    const std::vector<int> vIndices2 =
+        fr2.area(P.prev_matched[2 * i1], P.prev_matched[2 * i1 + 1], (float)P.window, level1, level1);
+    if (vIndices2.empty()) continue;
+    const uint8_t* d1 = F1.desc + 32 * (size_t)i1;
+    int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+    for (int i2 : vIndices2) {
+      const int dist = hamming(d1, F2.desc + 32 * (size_t)i2);
+      if (vMatchedDistance[i2] <= dist) continue;
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestIdx2 = i2;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= 50) {  // TH_LOW
+      if (bestDist < (float)bestDist2 * P.nnratio) {
+        if (vnMatches21[bestIdx2] >= 0) {
+          vnMatches12[vnMatches21[bestIdx2]] = -1;
+          nmatches--;
+        }
+        vnMatches12[i1] = bestIdx2;
+        vnMatches21[bestIdx2] = i1;
+        vMatchedDistance[bestIdx2] = bestDist;
+        nmatches++;
+        if (P.check_ori) rotHist[rot_bin(F1.keys_un[i1].angle, F2.keys_un[bestIdx2].angle)].push_back(i1);
+      }
+    }
+  }
+  if (P.check_ori) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, ind1, ind2, ind3);
+    for (int i = 0; i < kHisto; i++) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (int idx1 : rotHist[i])
+        if (vnMatches12[idx1] >= 0) {
+          vnMatches12[idx1] = -1;
+          nmatches--;
+        }
+    }
+  }
+  for (int i1 = 0; i1 < F1.n; i1++) {
+    P.match12[i1] = vnMatches12[i1];
+    if (vnMatches12[i1] >= 0) {
+      P.prev_matched[2 * i1] = F2.keys_un[vnMatches12[i1]].x;
+      P.prev_matched[2 * i1 + 1] = F2.keys_un[vnMatches12[i1]].y;
+    }
+  }
+  *P.nmatches = nmatches;
+  return nmatches;
+}
+
 }  // namespace
 
 extern "C" {
+
+int oracle_search_for_initialization(const oracle_init_problem* P) {
+  return P ? search_for_initialization(*P) : -1;
+}
 
 int oracle_search_by_sim3(const oracle_sim3_problem* P) { return P ? search_by_sim3(*P) : -1; }
 

@@ -102,6 +102,11 @@ class Sim3Problem(C.Structure):
                 ("match12", C.c_void_p), ("nfound", C.c_void_p)]
 
 
+class InitProblem(C.Structure):
+    _fields_ = [("f1", ProjFrame), ("f2", ProjFrame), ("prev_matched", C.c_void_p), ("window", C.c_int),
+                ("nnratio", C.c_float), ("check_ori", C.c_int), ("match12", C.c_void_p), ("nmatches", C.c_void_p)]
+
+
 class PoseProblem(C.Structure):
     _fields_ = [("n", C.c_int), ("obs", C.c_void_p), ("Xw", C.c_void_p), ("inv_sigma2", C.c_void_p),
                 ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
@@ -207,6 +212,7 @@ SIGNATURES = {
     "orbx_track_step_device": ([C.POINTER(TrackStep), C.c_int, P], C.c_int),
     "orbx_search_by_projection": ([C.POINTER(ProjProblem), C.c_int], C.c_int),
     "orbx_search_by_sim3": ([C.POINTER(Sim3Problem), C.c_int], C.c_int),
+    "orbx_search_for_initialization": ([C.POINTER(InitProblem), C.c_int], C.c_int),
     "orbx_search_by_projection_device": ([C.POINTER(ProjProblem), C.c_int, P], C.c_int),
     "orbx_pose_optimization": ([C.POINTER(PoseProblem), C.c_int], C.c_int),
     "orbx_pose_optimization_device": ([C.POINTER(PoseProblem), C.c_int, P], C.c_int),

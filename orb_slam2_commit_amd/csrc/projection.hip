@@ -567,6 +567,259 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   if (tid == 0) *P.nmatches = s_count - s_drop;
 }
 
+// ---- ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:442-587) ----
+// The reference walks F1's level-0 keypoints in order; keypoint i1 skips every candidate i2 whose
+// vMatchedDistance <= dist, and an accepted match takes i2 from its earlier holder (vnMatches21).
+// vMatchedDistance before i1's turn is md_i1(f) = min{dist_j : j < i1 accepted at f} (a later
+// acceptance at f needs a strictly smaller distance), so i1's choice is a function of the choices of
+// j < i1 only and the sweeps of k_search_by_projection reach the sequential answer: every sweep
+// evaluates all keypoints against the previous sweep's choices, held as a sorted (f << 13 | j) list
+// with per-feature prefix minima of the distance (md lookup = one binary search, only for features
+// with a chooser), until no choice changes.  The last chooser of a feature keeps it; the rotation
+// histogram counts every acceptance (dropped ones included), as rotHist does.
+// Dynamic LDS: sort keys (max(pow2(N1), pow2(N2)) x 4 B), cell starts, F2 grid positions, prefix
+// minima (pow2(N1) x 2 B), has-chooser bitmap.
+constexpr int IBS = 1024;
+constexpr int kInitMaxHeld = kMaxF / IBS;  // sorted-list positions per thread in the final pass
+
+__host__ __device__ inline int pow2_at_least(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+__host__ __device__ inline size_t init_smem_bytes(int n1, int n2) {
+  const int ns1 = pow2_at_least(n1), ns2 = pow2_at_least(n2), nk = ns1 > ns2 ? ns1 : ns2;
+  return (size_t)nk * 4 + (size_t)(kCells + 1) * 4 + (size_t)((n2 + 1) & ~1) * 2 + (size_t)ns1 * 2 +
+         (size_t)((n2 + 31) / 32) * 4;
+}
+
+template <class T>
+__device__ void bitonic_asc(T* k, int n) {
+  for (int size = 2; size <= n; size <<= 1)
+    for (int j = size >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < (n >> 1); t += blockDim.x) {
+        const int lo = 2 * t - (t & (j - 1)), hi = lo + j;
+        const T a = k[lo], b = k[hi];
+        if ((a > b) == ((lo & size) == 0)) {
+          k[lo] = b;
+          k[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(IBS) void k_search_for_initialization(const orbx_init_problem* __restrict__ probs) {
+  extern __shared__ __align__(16) uint8_t ismem[];
+  __shared__ int s_changed, s_count;
+  __shared__ int s_hist[32], s_sel[3];
+  const orbx_init_problem& P = probs[blockIdx.x];
+  const orbx_proj_frame& F1 = P.f1;
+  const orbx_proj_frame& F2 = P.f2;
+  const int n1 = F1.n, n2 = F2.n, tid = threadIdx.x;
+  const int ns1 = pow2_at_least(n1), ns2 = pow2_at_least(n2), nk = ns1 > ns2 ? ns1 : ns2;
+  uint32_t* s_keys = (uint32_t*)ismem;
+  int* s_start = (int*)(s_keys + nk);
+  uint16_t* s_pos = (uint16_t*)(s_start + kCells + 1);
+  uint16_t* s_pmin = s_pos + ((n2 + 1) & ~1);
+  uint32_t* s_has = (uint32_t*)(s_pmin + ns1);
+  int32_t* choice = P.match12;  // dist << 16 | i2 per F1 keypoint across the sweeps, -1 none
+
+  // ---- F2's level-0 keypoints into the grid (GetFeaturesInArea(x, y, w, 0, 0) sees only those) ----
+  for (int i = tid; i < ns2; i += IBS) {
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < n2) {
+      const orbx_keypoint kp = F2.keys_un[i];
+      const int px = (int)__builtin_roundf((kp.x - F2.min_x) * F2.grid_inv_w);
+      const int py = (int)__builtin_roundf((kp.y - F2.min_y) * F2.grid_inv_h);
+      if (kp.octave == 0 && px >= 0 && px < ORBX_GRID_COLS && py >= 0 && py < ORBX_GRID_ROWS)
+        key = ((uint32_t)(px * ORBX_GRID_ROWS + py) << 13) | (uint32_t)i;
+    }
+    s_keys[i] = key;
+  }
+  __syncthreads();
+  bitonic_asc(s_keys, ns2);
+  for (int c = tid; c <= kCells; c += IBS) {
+    const uint32_t target = (uint32_t)c << 13;
+    int lo = 0, hi = ns2;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (s_keys[m] < target) lo = m + 1; else hi = m;
+    }
+    s_start[c] = lo;
+  }
+  for (int i = tid; i < n2; i += IBS) s_pos[i] = (uint16_t)(s_keys[i] & 0x1FFF);
+  __syncthreads();
+  // no chooser before the first sweep
+  for (int p = tid; p < ns1; p += IBS) s_keys[p] = 0xFFFFFFFFu;
+  for (int w = tid; w < (n2 + 31) / 32; w += IBS) s_has[w] = 0;
+  for (int i = tid; i < n1; i += IBS) choice[i] = -1;
+  if (tid < 32) s_hist[tid] = 0;
+  __threadfence_block();
+  __syncthreads();
+
+  const int g = tid / kGroup, gl = tid % kGroup;
+  constexpr int kGroups = IBS / kGroup;
+  const float r = (float)P.window;
+  for (int sweep = 0; sweep <= n1 + 1; sweep++) {
+    if (tid == 0) s_changed = 0;
+    __syncthreads();
+    int changed = 0;
+    for (int i = g; i < n1; i += kGroups) {
+      int m = -1;
+      if (F1.keys_un[i].octave == 0) {
+        const float x = P.prev_matched[2 * i], y = P.prev_matched[2 * i + 1];
+        int x0 = max(0, (int)__builtin_floorf((x - F2.min_x - r) * F2.grid_inv_w));
+        const int x1 = min(ORBX_GRID_COLS - 1, (int)__builtin_ceilf((x - F2.min_x + r) * F2.grid_inv_w));
+        const int y0 = max(0, (int)__builtin_floorf((y - F2.min_y - r) * F2.grid_inv_h));
+        const int y1 = min(ORBX_GRID_ROWS - 1, (int)__builtin_ceilf((y - F2.min_y + r) * F2.grid_inv_h));
+        if (x0 >= ORBX_GRID_COLS || x1 < 0 || y0 >= ORBX_GRID_ROWS || y1 < 0) x0 = x1 + 1;
+        uint64_t dq[4];
+        {
+          const uint64_t* d = (const uint64_t*)(F1.desc + (size_t)i * 32);
+          dq[0] = d[0]; dq[1] = d[1]; dq[2] = d[2]; dq[3] = d[3];
+        }
+        uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+        for (int ix = x0; ix <= x1; ix++) {
+          const int c0 = ix * ORBX_GRID_ROWS;
+          const int pend = s_start[c0 + y1 + 1];
+          for (int p = s_start[c0 + y0] + gl; p < pend; p += kGroup) {
+            const int idx = s_pos[p];
+            const orbx_keypoint& kp = F2.keys_un[idx];
+            if (!(__builtin_fabsf(kp.x - x) < r && __builtin_fabsf(kp.y - y) < r)) continue;
+            const uint64_t* d = (const uint64_t*)(F2.desc + (size_t)idx * 32);
+            const uint64_t dd[4] = {d[0], d[1], d[2], d[3]};
+            const int dist = hamming256(dq, dd);
+            if ((s_has[idx >> 5] >> (idx & 31)) & 1) {  // vMatchedDistance[idx] <= dist: skip
+              const uint32_t key = ((uint32_t)idx << 13) | (uint32_t)i;
+              int lo = 0, hi = ns1;
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_keys[mid] < key) lo = mid + 1; else hi = mid;
+              }
+              if (lo > 0 && (s_keys[lo - 1] >> 13) == (uint32_t)idx && (int)s_pmin[lo - 1] <= dist) continue;
+            }
+            const uint32_t k = ((uint32_t)dist << 16) | (uint32_t)p;
+            if (k < m1) {
+              m2 = m1;
+              m1 = k;
+            } else if (k < m2) {
+              m2 = k;
+            }
+          }
+        }
+        const uint32_t b1 = group_min(m1);
+        const uint32_t b2 = group_min(m1 == b1 ? m2 : m1);
+        if (b1 != 0xFFFFFFFFu) {
+          const int d1 = (int)(b1 >> 16);
+          const int d2 = b2 == 0xFFFFFFFFu ? INT_MAX : (int)(b2 >> 16);
+          if (d1 <= 50 && (float)d1 < (float)d2 * P.nnratio) m = (d1 << 16) | (int)s_pos[b1 & 0xFFFF];
+        }
+      }
+      if (gl == 0) {
+        if (choice[i] != m) changed = 1;
+        choice[i] = m;
+      }
+    }
+    if (changed) s_changed = 1;
+    __threadfence_block();
+    __syncthreads();
+    if (!s_changed) break;
+    // the choosers of this sweep, sorted by (feature, keypoint), with per-feature prefix minima
+    for (int p = tid; p < ns1; p += IBS) {
+      uint32_t key = 0xFFFFFFFFu;
+      if (p < n1) {
+        const int c = choice[p];
+        if (c >= 0) key = ((uint32_t)(c & 0xFFFF) << 13) | (uint32_t)p;
+      }
+      s_keys[p] = key;
+    }
+    for (int w = tid; w < (n2 + 31) / 32; w += IBS) s_has[w] = 0;
+    __syncthreads();
+    bitonic_asc(s_keys, ns1);
+    for (int p = tid; p < ns1; p += IBS) {
+      const uint32_t key = s_keys[p];
+      if (key == 0xFFFFFFFFu) continue;
+      const uint32_t f = key >> 13;
+      int d = choice[key & 0x1FFF] >> 16;
+      for (int q = p - 1; q >= 0 && (s_keys[q] >> 13) == f; q--) d = min(d, choice[s_keys[q] & 0x1FFF] >> 16);
+      s_pmin[p] = (uint16_t)d;
+      atomicOr(&s_has[f >> 5], 1u << (f & 31));
+    }
+    __syncthreads();
+  }
+
+  // ---- final: a feature's last chooser keeps it; rotation histogram over every acceptance ----
+  // (the list in s_keys is the final choices': the last sweep changed nothing)
+  int held_i[kInitMaxHeld], held_fin[kInitMaxHeld], held_bin[kInitMaxHeld];
+  if (tid == 0) s_count = 0;
+#pragma unroll
+  for (int k = 0; k < kInitMaxHeld; k++) {
+    const int p = tid + k * IBS;
+    held_i[k] = -1;
+    held_fin[k] = -1;
+    held_bin[k] = -1;
+    if (p < ns1) {
+      const uint32_t key = s_keys[p];
+      if (key != 0xFFFFFFFFu) {
+        const int i = (int)(key & 0x1FFF), i2 = choice[i] & 0xFFFF;
+        const bool last = p + 1 == ns1 || (s_keys[p + 1] >> 13) != (key >> 13);
+        held_i[k] = i;
+        held_fin[k] = last ? i2 : -1;
+        if (P.check_ori) {
+          held_bin[k] = rot_bin(F1.keys_un[i].angle, F2.keys_un[i2].angle);
+          atomicAdd(&s_hist[held_bin[k]], 1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (P.check_ori && tid == 0) {  // ComputeThreeMaxima
+    int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+    for (int b = 0; b < 30; b++) {
+      const int sz = s_hist[b];
+      if (sz > m1) {
+        m3 = m2; m2 = m1; m1 = sz;
+        i3 = i2; i2 = i1; i1 = b;
+      } else if (sz > m2) {
+        m3 = m2; m2 = sz;
+        i3 = i2; i2 = b;
+      } else if (sz > m3) {
+        m3 = sz;
+        i3 = b;
+      }
+    }
+    if (m2 < 0.1f * (float)m1) {
+      i2 = -1;
+      i3 = -1;
+    } else if (m3 < 0.1f * (float)m1) {
+      i3 = -1;
+    }
+    s_sel[0] = i1;
+    s_sel[1] = i2;
+    s_sel[2] = i3;
+  }
+  __syncthreads();
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < kInitMaxHeld; k++) {
+    const int i = held_i[k];
+    if (i < 0) continue;
+    int out = held_fin[k];
+    if (P.check_ori && held_bin[k] != s_sel[0] && held_bin[k] != s_sel[1] && held_bin[k] != s_sel[2]) out = -1;
+    P.match12[i] = out;
+    if (out >= 0) {
+      const orbx_keypoint kp = F2.keys_un[out];
+      P.prev_matched[2 * i] = kp.x;
+      P.prev_matched[2 * i + 1] = kp.y;
+      cnt++;
+    }
+  }
+  atomicAdd(&s_count, cnt);
+  __syncthreads();
+  if (tid == 0) *P.nmatches = s_count;
+}
+
 hipError_t launch_search_by_projection(const ProjProblem* d_probs, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_search_by_projection, dim3(n), dim3(PBS), 0, st, d_probs);
@@ -781,5 +1034,79 @@ extern "C" orbx_status orbx_search_by_sim3(const orbx_sim3_problem* p, int devic
     }
   }
   *p->nfound = nFound;
+  return ORBX_OK;
+}
+
+extern "C" orbx_status orbx_search_for_initialization(const orbx_init_problem* p, int device) {
+  if (!p || !p->match12 || !p->nmatches || !p->prev_matched) return ORBX_ERR_ARG;
+  const int n1 = p->f1.n, n2 = p->f2.n;
+  if (n1 < 0 || n2 < 0) return ORBX_ERR_ARG;
+  if (n1 > ORBX_PROJ_MAX_FEATURES || n2 > ORBX_PROJ_MAX_FEATURES) return ORBX_ERR_CAPACITY;
+  if ((n1 > 0 && (!p->f1.keys_un || !p->f1.desc)) || (n2 > 0 && (!p->f2.keys_un || !p->f2.desc))) return ORBX_ERR_ARG;
+  if (p->window < 0) return ORBX_ERR_ARG;
+  for (int i = 0; i < n1; i++)
+    if (p->f1.keys_un[i].octave < 0) return ORBX_ERR_ARG;  // GetFeaturesInArea(.., level1, level1) needs level1 >= 0
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_NODEV;
+  if (device < 0 || device >= ndev || hipSetDevice(device) != hipSuccess) return ORBX_ERR_ARG;
+  size_t off = 0;
+  auto at = [&](size_t bytes) {
+    off = (off + 255) & ~(size_t)255;
+    const size_t a = off;
+    off += bytes;
+    return a;
+  };
+  const size_t a_k1 = at((size_t)n1 * sizeof(orbx_keypoint)), a_d1 = at((size_t)n1 * 32);
+  const size_t a_k2 = at((size_t)n2 * sizeof(orbx_keypoint)), a_d2 = at((size_t)n2 * 32);
+  const size_t a_prev = at((size_t)n1 * 8), a_m = at((size_t)n1 * 4 + 4), a_nm = at(4);
+  const size_t a_prob = at(sizeof(orbx_init_problem));
+  orbx::ScratchGuard g(device);
+  if (!g.l || g.l->reserve(off, off) != hipSuccess) return ORBX_ERR_HIP;
+  uint8_t* h = g.l->h;
+  uint8_t* d = g.l->d;
+  std::memset(h, 0, off);
+  if (n1) {
+    std::memcpy(h + a_k1, p->f1.keys_un, (size_t)n1 * sizeof(orbx_keypoint));
+    std::memcpy(h + a_d1, p->f1.desc, (size_t)n1 * 32);
+    std::memcpy(h + a_prev, p->prev_matched, (size_t)n1 * 8);
+  }
+  if (n2) {
+    std::memcpy(h + a_k2, p->f2.keys_un, (size_t)n2 * sizeof(orbx_keypoint));
+    std::memcpy(h + a_d2, p->f2.desc, (size_t)n2 * 32);
+  }
+  orbx_init_problem q = *p;
+  q.f1.keys_un = (const orbx_keypoint*)(d + a_k1);
+  q.f1.desc = d + a_d1;
+  q.f2.keys_un = (const orbx_keypoint*)(d + a_k2);
+  q.f2.desc = d + a_d2;
+  q.f1.u_right = q.f2.u_right = nullptr;
+  q.f1.occ = q.f2.occ = nullptr;
+  q.prev_matched = (float*)(d + a_prev);
+  q.match12 = (int32_t*)(d + a_m);
+  q.nmatches = (int32_t*)(d + a_nm);
+  std::memcpy(h + a_prob, &q, sizeof(q));
+  hipStream_t st = g.l->st;
+  const size_t smem = orbx::init_smem_bytes(n1, n2);
+  static bool attr = false;  // the kernel's dynamic LDS may exceed the 64 KB default
+  hipError_t e = hipSuccess;
+  if (!attr) {
+    e = hipFuncSetAttribute((const void*)orbx::k_search_for_initialization, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+    attr = e == hipSuccess;
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(orbx::k_search_for_initialization, dim3(1), dim3(orbx::IBS), smem, st,
+                       (const orbx_init_problem*)(d + a_prob));
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(h + a_prev, d + a_prev, a_prob - a_prev, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = g.l->sync();
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  if (n1) {
+    std::memcpy(p->prev_matched, h + a_prev, (size_t)n1 * 8);
+    std::memcpy(p->match12, h + a_m, (size_t)n1 * 4);
+  }
+  std::memcpy(p->nmatches, h + a_nm, 4);
   return ORBX_OK;
 }

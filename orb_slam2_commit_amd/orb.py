@@ -317,6 +317,26 @@ class ORBmatcher:
         o = _run_projection(self, F, vpPoints, PROJ_FUSE_SIM3, th=float(th))
         return int(o["nmatches"][0]), o["point_match"]
 
+    def SearchForInitialization(self, F1, F2, vbPrevMatched, windowSize=10):
+        """SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
+        vector<int>& vnMatches12, windowSize) -- src/ORBmatcher.cc:442-587 (Tracking::
+        MonocularInitialization: ORBmatcher(0.9, true), windowSize 100).  F1, F2: frame dicts
+        (keys_un, desc; F2's grid fields).  Returns (nmatches, vnMatches12[N1], vbPrevMatched[N1, 2]
+        updated)."""
+        f1, k1 = _host_proj_frame(F1)
+        f2, k2 = _host_proj_frame(F2)
+        p = _lib.InitProblem()
+        p.f1, p.f2 = f1, f2
+        prev = np.ascontiguousarray(vbPrevMatched, np.float32).reshape(-1, 2).copy()
+        assert len(prev) == f1.n
+        m = np.zeros(max(1, f1.n), np.int32)
+        nm = np.zeros(1, np.int32)
+        p.prev_matched, p.window = ptr(prev), int(windowSize)
+        p.nnratio, p.check_ori = float(self.mfNNratio), int(bool(self.mbCheckOrientation))
+        p.match12, p.nmatches = ptr(m), ptr(nm)
+        check(_lib.lib().orbx_search_for_initialization(C.byref(p), self.device), "orbx_search_for_initialization")
+        return int(nm[0]), m[:f1.n], prev
+
     def SearchBySim3(self, pKF1, pKF2, pts1, pts2, s12, R12, t12, th=7.5):
         """SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12, s12, R12, t12, th)
         -- src/ORBmatcher.cc:1238-1487 (LoopClosing::ComputeSim3).  pKFj: frame dicts (Tcw = GetPose());

@@ -736,3 +736,132 @@ def test_gpu_search_by_sim3(gpu, seed, s12, th):
     got = ORBmatcher().SearchBySim3(kf1, kf2, p1, p2, s, R12, t12, th)
     assert got[0] == ref[0] > 100
     np.testing.assert_array_equal(got[1], ref[1])
+
+
+# ------------------------------------------------------------------ SearchForInitialization (:442-587)
+def _init_case(seed, n=1500, shift=(6.0, -3.0), noise=1.0, max_p=0.3, extra=0.3):
+    """F1 = a synthetic frame; F2 = its keypoints moved by `shift` + noise with 0..max_p of each
+    descriptor's bits flipped, a fraction `extra` of random features added, in shuffled order (so the
+    grid order differs from F1's); vbPrevMatched = F1's keypoints (Tracking::MonocularInitialization)."""
+    f1 = synth.projection_frame(seed, n=n, p_occ=(0.0, 0.0))
+    r = np.random.default_rng(seed + 7)
+    k1 = f1["keys_un"]
+    ne = int(n * extra)
+    keys = np.concatenate([k1.copy(), k1[r.integers(0, n, ne)].copy()])
+    keys["x"][:n] += np.float32(shift[0]) + r.normal(0, noise, n).astype(np.float32)
+    keys["y"][:n] += np.float32(shift[1]) + r.normal(0, noise, n).astype(np.float32)
+    keys["x"][n:] = r.uniform(f1["min_x"], f1["max_x"], ne).astype(np.float32)
+    keys["y"][n:] = r.uniform(f1["min_y"], f1["max_y"], ne).astype(np.float32)
+    keys["angle"] = (keys["angle"] + r.normal(0, 4.0, len(keys))).astype(np.float32) % np.float32(360.0)
+    desc = np.concatenate([np.asarray(f1["desc"], np.uint8), r.integers(0, 256, (ne, 32), dtype=np.uint8)])
+    mask = r.random((n + ne, 256)) < r.uniform(0.0, max_p, (n + ne, 1))
+    desc = desc ^ np.packbits(mask, axis=1, bitorder="little")
+    perm = r.permutation(n + ne)
+    f2 = dict(f1, keys_un=keys[perm], desc=desc[perm], occ=None, u_right=None)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    return f1, f2, prev
+
+
+def py_search_for_initialization(f1, f2, prev, window=100, nnratio=0.9, check_ori=True):
+    F2 = PyFrame(f2)
+    k1, k2 = f1["keys_un"], f2["keys_un"]
+    n1, n2 = len(k1), len(k2)
+    m12 = [-1] * n1
+    m21 = [-1] * n2
+    md = [1 << 31] * n2
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for i1 in range(n1):
+        if k1["octave"][i1] > 0:
+            continue
+        cand = F2.area(prev[i1, 0], prev[i1, 1], f32(window), 0, 0)
+        if not cand:
+            continue
+        b, b2, bi = 1 << 31, 1 << 31, -1
+        for i2 in cand:
+            d = _ham(f1["desc"][i1], f2["desc"][i2])
+            if md[i2] <= d:
+                continue
+            if d < b:
+                b2, b, bi = b, d, i2
+            elif d < b2:
+                b2 = d
+        if b <= 50 and f32(b) < f32(f32(b2) * f32(nnratio)):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                nm -= 1
+            m12[i1], m21[bi], md[bi] = bi, i1, b
+            nm += 1
+            if check_ori:
+                hist[_rot_bin(k1["angle"][i1], k2["angle"][bi])].append(i1)
+    if check_ori:
+        sel = _three_max([len(h) for h in hist])
+        for b_ in range(30):
+            if b_ in sel:
+                continue
+            for i1 in hist[b_]:
+                if m12[i1] >= 0:
+                    m12[i1] = -1
+                    nm -= 1
+    out = prev.copy()
+    for i1 in range(n1):
+        if m12[i1] >= 0:
+            out[i1] = (k2["x"][m12[i1]], k2["y"][m12[i1]])
+    return nm, np.array(m12, np.int32), out
+
+
+@pytest.mark.parametrize("seed,window,check", [(0, 100, True), (1, 30, True), (2, 100, False)])
+def test_init_oracle_vs_python_restatement(seed, window, check):
+    f1, f2, prev = _init_case(1000 + seed, n=500)
+    got = oracle.search_for_initialization(f1, f2, prev, window, 0.9, check)
+    ref = py_search_for_initialization(f1, f2, prev, window, 0.9, check)
+    assert got[0] == ref[0] > 20
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(got[2].view(np.uint32), ref[2].view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,window,check,n", [(0, 100, True, 2000), (1, 30, True, 2000), (2, 100, False, 2000),
+                                                 (3, 100, True, 4000), (4, 10, True, 1000)])
+def test_gpu_search_for_initialization(gpu, seed, window, check, n):
+    """orbx_search_for_initialization equals the sequential oracle: vnMatches12, vbPrevMatched (f32
+    bits) and nmatches, with the vMatchedDistance skips, vnMatches21 take-overs and the rotation check."""
+    from orb_slam2_commit_amd import ORBmatcher
+    f1, f2, prev = _init_case(1200 + seed, n=n)
+    ref = oracle.search_for_initialization(f1, f2, prev, window, 0.9, check)
+    got = ORBmatcher(0.9, check).SearchForInitialization(f1, f2, prev, window)
+    assert got[0] == ref[0] > 20
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(got[2].view(np.uint32), ref[2].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_search_for_initialization_edges(gpu):
+    """Empty frames, no level-0 keypoint, a crowded window where every F1 keypoint competes for the
+    same few F2 features (long take-over chains, many sweeps)."""
+    from orb_slam2_commit_amd import ORBmatcher
+    m = ORBmatcher(0.9, True)
+    f1, f2, prev = _init_case(1300, n=800)
+    e1 = dict(f1, keys_un=f1["keys_un"][:0], desc=f1["desc"][:0])
+    assert m.SearchForInitialization(e1, f2, prev[:0], 100)[0] == 0
+    e2 = dict(f2, keys_un=f2["keys_un"][:0], desc=f2["desc"][:0])
+    r = m.SearchForInitialization(f1, e2, prev, 100)
+    assert r[0] == 0 and (r[1] == -1).all()
+    hi = dict(f1, keys_un=f1["keys_un"].copy())
+    hi["keys_un"]["octave"] = 1
+    assert m.SearchForInitialization(hi, f2, prev, 100)[0] == 0
+    # crowd: F2 = 40 features near one spot, every F1 keypoint's window covers them
+    r_ = np.random.default_rng(5)
+    k2 = f2["keys_un"][:40].copy()
+    k2["x"] = np.float32(600) + r_.normal(0, 5, 40).astype(np.float32)
+    k2["y"] = np.float32(180) + r_.normal(0, 5, 40).astype(np.float32)
+    k2["octave"] = 0
+    src = r_.integers(0, len(f1["desc"]), 40)
+    d2 = np.asarray(f1["desc"], np.uint8)[src] ^ np.packbits(r_.random((40, 256)) < 0.05, axis=1, bitorder="little")
+    crowd = dict(f2, keys_un=k2, desc=d2)
+    pc = np.tile(np.array([[600.0, 180.0]], np.float32), (len(f1["desc"]), 1))
+    ref = oracle.search_for_initialization(f1, crowd, pc, 100, 0.9, True)
+    got = m.SearchForInitialization(f1, crowd, pc, 100)
+    assert got[0] == ref[0]
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(got[2].view(np.uint32), ref[2].view(np.uint32))
