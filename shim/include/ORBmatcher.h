@@ -16,6 +16,7 @@
 //                                                                       include/ORBmatcher.h:99
 //   Fuse(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, th, vector<MapPoint*>&)  include/ORBmatcher.h:153
 //   SearchBySim3(KeyFrame*, KeyFrame*, vector<MapPoint*>&, s12, R12, t12, th)     include/ORBmatcher.h:139
+//   SearchForInitialization(Frame&, Frame&, vector<Point2f>&, vector<int>&, windowSize) include/ORBmatcher.h:130
 //                                                       (src/ORBmatcher.cc:918-1092)
 // DescriptorDistance of one pair stays on the host (a GPU launch per pair would cost more than the
 // popcounts); every other member runs its matching on the MI355X (orbx_search_by_bow_*,
@@ -53,6 +54,9 @@ class ORBmatcher {
   // LoopClosing::SearchAndFuse: the loop MapPoints into a corrected KeyFrame through its Sim3
   int Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints, float th,
            std::vector<MapPoint*>& vpReplacePoint);
+  // Tracking::MonocularInitialization: F1's level-0 keypoints in windows around vbPrevMatched in F2
+  int SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
+                              std::vector<int>& vnMatches12, int windowSize = 10);
   // LoopClosing::ComputeSim3: matches between two KeyFrames' MapPoints through a Sim3, both ways
   int SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12, const float& s12,
                    const cv::Mat& R12, const cv::Mat& t12, const float th);

@@ -733,6 +733,36 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector
   return nm;
 }
 
+int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Point2f>& vbPrevMatched,
+                                        std::vector<int>& vnMatches12, int windowSize) {
+  // src/ORBmatcher.cc:442-587 (caller Tracking::MonocularInitialization, src/Tracking.cc:711)
+  std::vector<int8_t> occ1, occ2;
+  cv::Mat d1, d2;
+  orbx_init_problem p;
+  std::memset(&p, 0, sizeof(p));
+  p.f1 = proj_frame(F1, occ1, d1);
+  p.f2 = proj_frame(F2, occ2, d2);
+  const int n1 = F1.N;
+  std::vector<float> prev(2 * (size_t)(n1 > 0 ? n1 : 1), 0.f);
+  for (int i = 0; i < n1 && i < (int)vbPrevMatched.size(); i++) {
+    prev[2 * i] = vbPrevMatched[i].x;
+    prev[2 * i + 1] = vbPrevMatched[i].y;
+  }
+  std::vector<int32_t> m(n1 > 0 ? n1 : 1, -1);
+  int32_t nm = 0;
+  p.prev_matched = prev.data();
+  p.window = windowSize;
+  p.nnratio = mfNNratio;
+  p.check_ori = mbCheckOrientation ? 1 : 0;
+  p.match12 = m.data();
+  p.nmatches = &nm;
+  check(orbx_search_for_initialization(&p, mDevice), "orbx_search_for_initialization");
+  vnMatches12.assign(m.begin(), m.begin() + n1);
+  for (int i = 0; i < n1 && i < (int)vbPrevMatched.size(); i++)
+    if (m[i] >= 0) vbPrevMatched[i] = cv::Point2f(prev[2 * i], prev[2 * i + 1]);
+  return nm;
+}
+
 int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12, const float& s12,
                              const cv::Mat& R12, const cv::Mat& t12, const float th) {
   // src/ORBmatcher.cc:1238-1487 (caller LoopClosing::ComputeSim3, src/LoopClosing.cc:422): both

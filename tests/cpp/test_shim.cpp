@@ -13,6 +13,7 @@
 //   sim3    IN OUT      ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)
 //   fusesim3 IN OUT     ORBmatcher::Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint)
 //   bysim3  IN OUT      ORBmatcher::SearchBySim3(KeyFrame*, KeyFrame*, vpMatches12, s12, R12, t12, th)
+//   init    IN OUT      ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
 //   tri     IN OUT      ORBmatcher::SearchForTriangulation(KeyFrame*, KeyFrame*, F12, pairs, bOnlyStereo)
 //   pose    IN OUT      Optimizer::PoseOptimization(Frame*)
 //   distinct IN OUT     MapPoint::ComputeDistinctiveDescriptors
@@ -1129,6 +1130,35 @@ static int mode_bysim3(const char* in, const char* out) {
   return 0;
 }
 
+// SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) with ORBmatcher(nnratio, check).
+// Out: nmatches, vnMatches12, vbPrevMatched (x, y floats).
+static int mode_init(const char* in, const char* out) {
+  Reader r(in);
+  const int window = r.get<int32_t>();
+  const float nn = r.get<float>();
+  const int check = r.get<int32_t>();
+  FramePayload fp1, fp2;
+  read_frame(r, fp1);
+  read_frame(r, fp2);
+  std::vector<cv::Point2f> prev(fp1.F.N);
+  for (int i = 0; i < fp1.F.N; i++) {
+    const float x = r.get<float>();
+    prev[i] = cv::Point2f(x, r.get<float>());
+  }
+  std::vector<int> m12;
+  ORBmatcher matcher(nn, check != 0);
+  const int nm = matcher.SearchForInitialization(fp1.F, fp2.F, prev, m12, window);
+  Writer o(out);
+  o.put<int32_t>(nm);
+  for (int i = 0; i < fp1.F.N; i++) o.put<int32_t>(m12[i]);
+  for (int i = 0; i < fp1.F.N; i++) {
+    o.put<float>(prev[i].x);
+    o.put<float>(prev[i].y);
+  }
+  std::printf("init ok: %d matches\n", nm);
+  return 0;
+}
+
 // SearchForTriangulation(KeyFrame*, KeyFrame*, F12, vMatchedPairs, bOnlyStereo)
 static void read_tri_kf(Reader& r, KeyFrame& K) {
   K.N = r.get<int32_t>();
@@ -1342,6 +1372,7 @@ int main(int argc, char** argv) {
     if (m == "sim3") return mode_sim3(argv[2], argv[3]);
     if (m == "fusesim3") return mode_fusesim3(argv[2], argv[3]);
     if (m == "bysim3") return mode_bysim3(argv[2], argv[3]);
+    if (m == "init") return mode_init(argv[2], argv[3]);
     if (m == "tri") return mode_tri(argv[2], argv[3]);
     if (m == "pose") return mode_pose(argv[2], argv[3]);
     if (m == "distinct") return mode_distinct(argv[2], argv[3]);

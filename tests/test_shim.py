@@ -77,6 +77,8 @@ def test_shim_exports_reference_classes(exe):
                 "ORB_SLAM2::ORBmatcher::SearchByProjection(ORB_SLAM2::KeyFrame*, cv::Mat, "
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> > const&, "
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&, int)",
+                "ORB_SLAM2::ORBmatcher::SearchForInitialization(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, "
+                "std::vector<cv::Point2f, std::allocator<cv::Point2f> >&, std::vector<int, std::allocator<int> >&, int)",
                 "ORB_SLAM2::ORBmatcher::SearchBySim3(ORB_SLAM2::KeyFrame*, ORB_SLAM2::KeyFrame*, "
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&, float const&, "
                 "cv::Mat const&, cv::Mat const&, float)",
@@ -653,6 +655,28 @@ def test_shim_search_by_sim3(gpu, exe, tmp_path, seed, s12, th):
     want = np.where(m12 >= 0, m12, want)
     assert nf == nf_ref > 100
     np.testing.assert_array_equal(state, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,window,check", [(0, 100, True), (1, 50, False)])
+def test_shim_search_for_initialization(gpu, exe, tmp_path, seed, window, check):
+    """ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+    (include/ORBmatcher.h:130, Tracking::MonocularInitialization): vnMatches12, vbPrevMatched and the
+    return value equal the sequential oracle's."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_projection import _init_case
+    f1, f2, prev = _init_case(1400 + seed, n=2000)
+    nm_ref, m_ref, prev_ref = oracle.search_for_initialization(f1, f2, prev, window, 0.9, check)
+    payload = (struct.pack("<ifi", window, 0.9, int(check)) + _frame_bytes(f1) + _frame_bytes(f2)
+               + np.ascontiguousarray(prev, np.float32).tobytes())
+    out = _run(exe, "init", payload, tmp_path)
+    n1 = len(f1["desc"])
+    nm = struct.unpack_from("<i", out, 0)[0]
+    m12 = np.frombuffer(out, np.int32, n1, 4)
+    pv = np.frombuffer(out, np.float32, 2 * n1, 4 + 4 * n1).reshape(-1, 2)
+    assert nm == nm_ref > 20
+    np.testing.assert_array_equal(m12, m_ref)
+    np.testing.assert_array_equal(pv.view(np.uint32), prev_ref.view(np.uint32))
 
 
 def _tri_kf_bytes(d):
