@@ -1087,13 +1087,9 @@ extern "C" orbx_status orbx_search_for_initialization(const orbx_init_problem* p
   std::memcpy(h + a_prob, &q, sizeof(q));
   hipStream_t st = g.l->st;
   const size_t smem = orbx::init_smem_bytes(n1, n2);
-  static bool attr = false;  // the kernel's dynamic LDS may exceed the 64 KB default
-  hipError_t e = hipSuccess;
-  if (!attr) {
-    e = hipFuncSetAttribute((const void*)orbx::k_search_for_initialization, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-    attr = e == hipSuccess;
-  }
+  // the dynamic LDS reaches ~79 KB at 8192 features (above the 64 KB default)
+  hipError_t e = hipFuncSetAttribute((const void*)orbx::k_search_for_initialization,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e == hipSuccess) e = hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(orbx::k_search_for_initialization, dim3(1), dim3(orbx::IBS), smem, st,
