@@ -590,7 +590,7 @@ long long orbx_sizeof(const char* type) {
   ORBX_SIZEOF(orbx_rand_state) ORBX_SIZEOF(orbx_proj_frame) ORBX_SIZEOF(orbx_proj_problem)
   ORBX_SIZEOF(orbx_tri_kf) ORBX_SIZEOF(orbx_tri_problem) ORBX_SIZEOF(orbx_pose_problem)
   ORBX_SIZEOF(orbx_track_gather) ORBX_SIZEOF(orbx_frame_points) ORBX_SIZEOF(orbx_track_step)
-  ORBX_SIZEOF(orbx_camera)
+  ORBX_SIZEOF(orbx_camera) ORBX_SIZEOF(orbx_sim3_problem) ORBX_SIZEOF(orbx_init_problem)
 #undef ORBX_SIZEOF
   return -1;
 }
