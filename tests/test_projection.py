@@ -865,3 +865,56 @@ def test_gpu_search_for_initialization_edges(gpu):
     assert got[0] == ref[0]
     np.testing.assert_array_equal(got[1], ref[1])
     np.testing.assert_array_equal(got[2].view(np.uint32), ref[2].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_projection_sim3_device_sized(gpu):
+    """The Sim3 kinds through orbx_search_by_projection_device with device-resident sizes and pose
+    (f_n_dev, n_points_dev, Tcw_dev = the Sim3, decomposed on the device): equal to the oracle on the
+    truncated problem, and a gated problem leaves its outputs untouched."""
+    import ctypes as C
+    import torch
+    from orb_slam2_commit_amd import _lib
+    from orb_slam2_commit_amd.orb import proj_problem
+
+    fr = synth.projection_frame(1500, n=2000)
+    pts = synth.projection_points(1501, fr, 3, n_points=2500)
+    f4 = _sim3(fr, 1)
+    nf, npnt = 1700, 2100  # device-side sizes below the capacities
+    trunc_fr = dict(f4, keys_un=f4["keys_un"][:nf], desc=f4["desc"][:nf], occ=np.asarray(f4["occ"])[:nf],
+                    u_right=None if f4.get("u_right") is None else np.asarray(f4["u_right"])[:nf])
+    trunc_pts = {k: (v[:npnt] if isinstance(v, np.ndarray) else v) for k, v in pts.items()}
+    probs, keep, refs = [], [], []
+    for kind, th, gate in ((4, 10.0, 0), (5, 4.0, 0), (4, 10.0, 30)):
+        refs.append((kind, oracle.search_by_projection(trunc_fr, trunc_pts, kind, th=th)))
+        dfr = dict(f4)
+        dfr["Tcw"] = np.eye(4, dtype=np.float32)  # replaced by Tcw_dev
+        for k in ("keys_un", "desc", "u_right", "occ"):
+            if f4.get(k) is not None:
+                dfr[k] = torch.from_numpy(np.ascontiguousarray(f4[k]).view(np.uint8)).to(gpu)
+        dpts = {k: (torch.from_numpy(np.ascontiguousarray(v)).to(gpu) if isinstance(v, np.ndarray) else v)
+                for k, v in pts.items()}
+        outs = dict(frame_out=torch.full((len(f4["desc"]),), 77, dtype=torch.int32, device=gpu),
+                    point_match=torch.full((len(pts["desc"]),), 77, dtype=torch.int32, device=gpu),
+                    nmatches=torch.full((1,), 77, dtype=torch.int32, device=gpu))
+        p, _ = proj_problem(dfr, dpts, kind, th=th, outputs=outs)
+        sizes = torch.tensor([nf, npnt, gate], dtype=torch.int32, device=gpu)
+        T = torch.from_numpy(np.ascontiguousarray(f4["Tcw"], np.float32).reshape(16)).to(gpu)
+        p.f_n_dev, p.n_points_dev = sizes.data_ptr(), sizes.data_ptr() + 4
+        p.Tcw_dev, p.gate, p.gate_below = T.data_ptr(), sizes.data_ptr() + 8, 20
+        probs.append(p)
+        keep.append((dfr, dpts, outs, sizes, T))
+    arr = (_lib.ProjProblem * len(probs))(*probs)
+    s = torch.cuda.current_stream()
+    _lib.check(_lib.lib().orbx_search_by_projection_device(arr, len(probs), C.c_void_p(s.cuda_stream)), "batch")
+    torch.cuda.synchronize()
+    for (kind, ref), (_, _, outs, sizes, _) in zip(refs, keep):
+        got_fo = outs["frame_out"].cpu().numpy()
+        got_pm = outs["point_match"].cpu().numpy()
+        got_nm = int(outs["nmatches"].cpu()[0])
+        if int(sizes[2]) >= 20:  # gated: untouched
+            assert got_nm == 77 and (got_fo == 77).all() and (got_pm == 77).all()
+            continue
+        assert got_nm == ref["nmatches"] > 50
+        np.testing.assert_array_equal(got_pm[:npnt], ref["point_match"])
+        np.testing.assert_array_equal(got_fo[:nf], ref["frame_out"])
