@@ -812,7 +812,7 @@ int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoin
   p.match12 = m12.data();
   p.nfound = &nf;
   check(orbx_search_by_sim3(&p, mDevice), "orbx_search_by_sim3");
-  for (int i1 = 0; i1 < N1; i1++)
+  for (int i1 = 0; i1 < N1 && i1 < (int)vpMatches12.size(); i1++)
     if (m12[i1] >= 0) vpMatches12[i1] = vp2[m12[i1]];
   return nf;
 }
@@ -863,7 +863,7 @@ int ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& v
     MapPoint* pMP = vpPoints[i];
     MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
     if (pMPinKF) {
-      if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
+      if (!pMPinKF->isBad() && i < (int)vpReplacePoint.size()) vpReplacePoint[i] = pMPinKF;
     } else {
       pMP->AddObservation(pKF, bestIdx);
       pKF->AddMapPoint(pMP, bestIdx);
