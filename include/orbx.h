@@ -13,6 +13,10 @@
  *   orbx_extractor_scale_tables GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
  *                               GetInverseScaleSigmaSquares     include/ORBextractor.h:85-103
  *   orbx_extractor_get_levels   GetLevels                       include/ORBextractor.h:81
+ *   orbx_extractor_tables       protected mnFeaturesPerLevel/umax/pattern
+ *                                                               src/ORBextractor.cc:416-490, include/ORBextractor.h:118,132,135
+ *   orbx_extractor_set_pyramid_readback
+ *                               mvImagePyramid refreshed by every operator()  src/ORBextractor.cc:1215-1250
  *   orbx_extract                ORBextractor::operator()        src/ORBextractor.cc:1138-1211, include/ORBextractor.h:77-78
  *   orbx_pyramid_level          public mvImagePyramid[level]    include/ORBextractor.h:104 (read at src/Frame.cc:556,681,694,700)
  *   orbx_extract_batch_device   frame-batch form of operator() (one launch per stage for n images)
@@ -96,6 +100,17 @@ int orbx_extractor_get_levels(const orbx_extractor* h);
 /* Any output pointer may be NULL; arrays hold nlevels floats. */
 orbx_status orbx_extractor_scale_tables(const orbx_extractor* h, float* scale, float* inv_scale,
                                         float* sigma2, float* inv_sigma2);
+/* The constructor's remaining tables (src/ORBextractor.cc:416-490; the protected members
+ * mnFeaturesPerLevel, umax and pattern of include/ORBextractor.h:118,132,135): features_per_level
+ * holds nlevels ints, umax 16 (HALF_PATCH_SIZE + 1), pattern 1024 (the 512 (x, y) sample points of the
+ * 256 rBRIEF pairs, bit_pattern_31_).  Any pointer may be NULL. */
+orbx_status orbx_extractor_tables(const orbx_extractor* h, int* features_per_level, int* umax, int* pattern);
+/* mvImagePyramid readback (include/ORBextractor.h:104; the reference rebuilds it on every operator()
+ * call, src/ORBextractor.cc:1215-1250).  With on != 0 every orbx_extract also copies the pyramid it
+ * built into pinned host memory in the same stream, before its single synchronisation, and
+ * orbx_pyramid_level(h, 0, l, ...) then reads that copy with no device call.  Off by default (a
+ * caller that never reads the levels on the host does not pay the copy). */
+orbx_status orbx_extractor_set_pyramid_readback(orbx_extractor* h, int on);
 /* Upper bound on keypoints per image for this geometry (size kps/desc buffers with it). */
 int orbx_extractor_max_keypoints(orbx_extractor* h, int width, int height);
 

@@ -178,6 +178,8 @@ SIGNATURES = {
     "orbx_extractor_destroy": ([P], None),
     "orbx_extractor_get_levels": ([P], C.c_int),
     "orbx_extractor_scale_tables": ([P, P, P, P, P], C.c_int),
+    "orbx_extractor_tables": ([P, P, P, P], C.c_int),
+    "orbx_extractor_set_pyramid_readback": ([P, C.c_int], C.c_int),
     "orbx_extractor_max_keypoints": ([P, C.c_int, C.c_int], C.c_int),
     "orbx_extract": ([P, P, C.c_int, C.c_int, C.c_size_t, P, C.c_int, P, C.POINTER(C.c_int)], C.c_int),
     "orbx_pyramid_level": ([P, C.c_int, C.c_int, P, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),

@@ -442,8 +442,25 @@ struct orbx_extractor {
   bool last_host = false;
   int last_fp_n = 0;
   uint64_t last_fp = 0;
+  // mvImagePyramid readback (orbx_extractor_set_pyramid_readback): level 0 (the packed input) then
+  // levels 1.. exactly as packed on the device, in pinned memory; valid for the last orbx_extract
+  bool pyr_readback = false;
+  bool hpyr_valid = false;
+  uint8_t* hpyr = nullptr;
+  size_t hpyr_cap = 0, hpyr_l0 = 0;
   ~orbx_extractor() {
     if (hstage) (void)hipHostFree(hstage);
+    if (hpyr) (void)hipHostFree(hpyr);
+  }
+  hipError_t ensure_hpyr(size_t bytes) {
+    if (bytes <= hpyr_cap && hpyr) return hipSuccess;
+    if (hpyr) (void)hipHostFree(hpyr);
+    hpyr = nullptr;
+    hpyr_cap = 0;
+    const size_t cap = (bytes + 4095) & ~(size_t)4095;
+    hipError_t e = hipHostMalloc((void**)&hpyr, cap, hipHostMallocDefault);
+    if (e == hipSuccess) hpyr_cap = cap;
+    return e;
   }
   hipError_t ensure_stage(size_t bytes) {
     if (bytes <= hstage_cap && hstage) return hipSuccess;
@@ -544,6 +561,7 @@ orbx_status run_extract(orbx_extractor* h, Plan* P, int n, const uint8_t* d_in, 
   h->last_pitch = pitch;
   h->last_n = n;
   h->last_host = false;  // orbx_extract sets it again after its readback
+  h->hpyr_valid = false;
   return ORBX_OK;
 }
 
@@ -649,6 +667,27 @@ orbx_status orbx_extractor_scale_tables(const orbx_extractor* h, float* scale, f
   return ORBX_OK;
 }
 
+orbx_status orbx_extractor_tables(const orbx_extractor* h, int* features_per_level, int* umax, int* pattern) {
+  if (!h) return ORBX_ERR_ARG;
+  static const int8_t kPattern[512 * 2] = {
+#include "brief_pattern_31.inc"
+  };
+  for (int i = 0; i < h->params.nlevels; i++)
+    if (features_per_level) features_per_level[i] = h->tables.nfeat[i];
+  for (int v = 0; v < 16; v++)
+    if (umax) umax[v] = h->tables.umax[v];
+  for (int i = 0; i < 1024; i++)
+    if (pattern) pattern[i] = kPattern[i];
+  return ORBX_OK;
+}
+
+orbx_status orbx_extractor_set_pyramid_readback(orbx_extractor* h, int on) {
+  if (!h) return ORBX_ERR_ARG;
+  h->pyr_readback = on != 0;
+  if (!h->pyr_readback) h->hpyr_valid = false;
+  return ORBX_OK;
+}
+
 int orbx_extractor_max_keypoints(orbx_extractor* h, int width, int height) {
   if (!h) return ORBX_ERR_ARG;
   Plan* P = nullptr;
@@ -686,8 +725,20 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
   uint8_t* d_desc = h->out.p + h->out_desc;
   s = run_extract(h, P, 1, h->in.p, npx, d_kps, d_desc, d_count, kcap, st);
   if (s != ORBX_OK) return s;
+  const bool pyr = h->pyr_readback;
+  if (pyr) {
+    // mvImagePyramid (src/ORBextractor.cc:1215-1250 rebuilds it on every call): levels 1.. leave in
+    // one more D2H behind the output block; level 0 is the staged input, copied on the host while
+    // the kernels run
+    h->hpyr_l0 = (npx + 255) & ~(size_t)255;
+    if (h->ensure_hpyr(h->hpyr_l0 + (size_t)P->G.pyr_bytes) != hipSuccess) return ORBX_ERR_HIP;
+  }
   // count, keypoints and descriptors in ONE copy, then the stream's only synchronisation
   chk(hipMemcpyAsync(h->hstage, h->out.p, h->out_bytes, hipMemcpyDeviceToHost, st));
+  if (pyr && P->G.nlevels > 1)
+    chk(hipMemcpyAsync(h->hpyr + h->hpyr_l0, h->pyr.p, (size_t)P->G.pyr_bytes, hipMemcpyDeviceToHost, st));
+  if (pyr)  // from the caller's image (hstage is the output's destination by now)
+    for (int y = 0; y < height; y++) std::memcpy(h->hpyr + (size_t)y * width, img + (size_t)y * stride, width);
   chk(hipStreamSynchronize(st));
   if (e != hipSuccess) return ORBX_ERR_HIP;
   const int32_t cnt = *(const int32_t*)h->hstage;
@@ -699,6 +750,7 @@ orbx_status orbx_extract(orbx_extractor* h, const uint8_t* img, int width, int h
     if (desc) std::memcpy(desc, h->hstage + h->out_desc, (size_t)32 * cnt);
   }
   h->last_host = true;
+  h->hpyr_valid = pyr;
   h->last_fp_n = cnt;
   h->last_fp = keypoint_fingerprint(hk, h->hstage + h->out_desc, cnt);
   return ORBX_OK;
@@ -715,6 +767,12 @@ orbx_status orbx_pyramid_level(orbx_extractor* h, int image, int level, uint8_t*
   if (height) *height = hh;
   if (!dst) return ORBX_OK;
   if (dst_stride < (size_t)w) return ORBX_ERR_ARG;
+  if (h->hpyr_valid && image == 0) {
+    // staged by the last orbx_extract: a host copy, no device call
+    const uint8_t* src = level == 0 ? h->hpyr : h->hpyr + h->hpyr_l0 + G.lv[level].off;
+    for (int y = 0; y < hh; y++) std::memcpy(dst + (size_t)y * dst_stride, src + (size_t)y * w, w);
+    return ORBX_OK;
+  }
   if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
   BatchPtrs B = batch_ptrs(h, h->last_in, h->last_pitch);
   const uint8_t* src = level_ptr(G, B, image, level);

@@ -10,12 +10,14 @@
 #include "Objects.h"
 #include "opencv_min.hpp"
 #include "orbx.h"
+#include "orbx_shim.h"
 
 namespace ORB_SLAM2 {
 
 class ORBVocabulary {
  public:
-  explicit ORBVocabulary(int device = 0) : mDevice(device) {}
+  // the reference's `new ORBVocabulary()` (System.cc); the tree goes to device gOrbxDevice when loaded
+  ORBVocabulary() = default;
   ~ORBVocabulary();
   ORBVocabulary(const ORBVocabulary&) = delete;
   ORBVocabulary& operator=(const ORBVocabulary&) = delete;
@@ -36,7 +38,6 @@ class ORBVocabulary {
   orbx_voc* gpu() const { return mpGpu; }
 
  private:
-  int mDevice;
   orbx_voc* mpGpu = nullptr;
   int32_t mInfo[6] = {0, 0, 0, 0, 0, 0};
 };

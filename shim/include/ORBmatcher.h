@@ -1,5 +1,5 @@
 // ORBmatcher.h -- drop-in ORB_SLAM2::ORBmatcher for the hot-path members over liborbx.so:
-//   ORBmatcher(nnratio, checkOri)                 include/ORBmatcher.h:48
+//   ORBmatcher(nnratio, checkOri)                 include/ORBmatcher.h:47
 //   static DescriptorDistance(a, b)               include/ORBmatcher.h:50 (src/ORBmatcher.cc:1844-1860)
 //   SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches)  include/ORBmatcher.h:114 (src/ORBmatcher.cc:175-325)
 //   SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12)     include/ORBmatcher.h:116 (src/ORBmatcher.cc:589-736)
@@ -17,7 +17,8 @@
 //   Fuse(KeyFrame*, cv::Mat Scw, const vector<MapPoint*>&, th, vector<MapPoint*>&)  include/ORBmatcher.h:153
 //   SearchBySim3(KeyFrame*, KeyFrame*, vector<MapPoint*>&, s12, R12, t12, th)     include/ORBmatcher.h:139
 //   SearchForInitialization(Frame&, Frame&, vector<Point2f>&, vector<int>&, windowSize) include/ORBmatcher.h:130
-//                                                       (src/ORBmatcher.cc:918-1092)
+//                                                       (src/ORBmatcher.cc:442-587)
+// Every member runs on device gOrbxDevice (orbx_shim.h); the layout is the reference's two members.
 // DescriptorDistance of one pair stays on the host (a GPU launch per pair would cost more than the
 // popcounts); every other member runs its matching on the MI355X (orbx_search_by_bow_*,
 // orbx_search_by_projection, orbx_search_for_triangulation) and applies the result to the object
@@ -34,7 +35,7 @@ namespace ORB_SLAM2 {
 
 class ORBmatcher {
  public:
-  ORBmatcher(float nnratio = 0.6, bool checkOri = true, int device = 0);
+  ORBmatcher(float nnratio = 0.6, bool checkOri = true);
 
   static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b);
 
@@ -73,7 +74,6 @@ class ORBmatcher {
  protected:
   float mfNNratio;
   bool mbCheckOrientation;
-  int mDevice;
 };
 
 }  // namespace ORB_SLAM2

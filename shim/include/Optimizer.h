@@ -54,14 +54,13 @@ class Optimizer {
   // with >= 3 correspondences, pFrame->SetPose; returns the inlier count (0 below 3 matches).
   int static PoseOptimization(Frame* pFrame);
   // include/Optimizer.h:61.  pbStopFlag: the reference's bool* (NULL allowed), polled before the
-  // run and between LM trials.  Runs on device mnDevice.  Throws std::runtime_error on a library
+  // run and between LM trials.  Runs on device gOrbxDevice.  Throws std::runtime_error on a library
   // error (the object graph is then left as it was).
   void static LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap);
   // The explicit-problem form.  Throws std::runtime_error on a library error.
   void static LocalBundleAdjustment(const LocalBAProblem& problem, bool* pbStopFlag, LocalBAResult& result,
                                     int device = 0);
 
-  static int mnDevice;  // device of the graph form (default 0)
   // test hook: called with the window the graph form gathered, before it runs (NULL: none)
   static void (*mpfnGatheredHook)(const LocalBAProblem& problem, const std::vector<KeyFrame*>& cameras);
 };

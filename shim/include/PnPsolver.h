@@ -36,7 +36,6 @@ class PnPsolver {
   cv::Mat iterate(int nIterations, bool& bNoMore, std::vector<bool>& vbInliers, int& nInliers);
 
   static void SeedRandom(unsigned int seed);  // the shared stream (srand)
-  static int mnDevice;                        // device new solvers run on (default 0)
 
  private:
   void ensure_solver();

@@ -27,11 +27,16 @@ namespace cv {
 
 typedef unsigned char uchar;
 
-struct Point2f {
-  float x = 0.f, y = 0.f;
-  Point2f() = default;
-  Point2f(float x_, float y_) : x(x_), y(y_) {}
+// cv::Point_<T> with OpenCV's typedefs, so signatures mangle as they do against the real header
+template <class T>
+struct Point_ {
+  T x = T(), y = T();
+  Point_() = default;
+  Point_(T x_, T y_) : x(x_), y(y_) {}
 };
+typedef Point_<int> Point2i;
+typedef Point_<float> Point2f;
+typedef Point2i Point;
 
 // cv::KeyPoint: 28 bytes, field order pt, size, angle, response, octave, class_id
 class KeyPoint {

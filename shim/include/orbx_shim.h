@@ -1,7 +1,7 @@
-// orbx_shim.h -- shim-wide settings for the members that have no device of their own
-// (MapPoint::ComputeDistinctiveDescriptors, Frame::ComputeImageBounds / UndistortKeyPoints):
-// they run on device gOrbxDevice (default 0).  ORBmatcher, Optimizer, PnPsolver and
-// ORBVocabulary keep their own device settings.
+// orbx_shim.h -- the shim-wide device: the reference's constructors take no device, so
+// ORBextractor, ORBmatcher, ORBVocabulary, MapPoint::ComputeDistinctiveDescriptors and
+// Frame::ComputeImageBounds / UndistortKeyPoints, PnPsolver and Optimizer's graph forms run on device
+// gOrbxDevice (default 0; set it before constructing the objects).
 #pragma once
 
 namespace ORB_SLAM2 {

@@ -47,12 +47,11 @@ static void check(orbx_status s, const char* what) {
 static cv::Mat continuous(const cv::Mat& m) { return m.isContinuous() ? m : m.clone(); }
 
 // ------------------------------------------------------------------ ORBextractor
-ORBextractor::ORBextractor(int nfeatures_, float scaleFactor_, int nlevels_, int iniThFAST_, int minThFAST_,
-                           int device)
+ORBextractor::ORBextractor(int nfeatures_, float scaleFactor_, int nlevels_, int iniThFAST_, int minThFAST_)
     : nfeatures(nfeatures_), scaleFactor(scaleFactor_), nlevels(nlevels_), iniThFAST(iniThFAST_),
       minThFAST(minThFAST_) {
   orbx_extractor_params p{nfeatures, scaleFactor_, nlevels, iniThFAST, minThFAST};
-  check(orbx_extractor_create(&p, device, &mpGpu), "orbx_extractor_create");
+  check(orbx_extractor_create(&p, gOrbxDevice, &mpGpu), "orbx_extractor_create");
   mvScaleFactor.resize(nlevels);
   mvInvScaleFactor.resize(nlevels);
   mvLevelSigma2.resize(nlevels);
@@ -60,6 +59,14 @@ ORBextractor::ORBextractor(int nfeatures_, float scaleFactor_, int nlevels_, int
   check(orbx_extractor_scale_tables(mpGpu, mvScaleFactor.data(), mvInvScaleFactor.data(), mvLevelSigma2.data(),
                                     mvInvLevelSigma2.data()),
         "orbx_extractor_scale_tables");
+  // the constructor's other tables (src/ORBextractor.cc:433-490): quotas, the IC_Angle circle, pattern
+  mnFeaturesPerLevel.resize(nlevels);
+  umax.resize(16);  // HALF_PATCH_SIZE + 1
+  std::vector<int> pts(1024);
+  check(orbx_extractor_tables(mpGpu, mnFeaturesPerLevel.data(), umax.data(), pts.data()), "orbx_extractor_tables");
+  pattern.resize(512);
+  for (int i = 0; i < 512; i++) pattern[i] = cv::Point(pts[2 * i], pts[2 * i + 1]);
+  check(orbx_extractor_set_pyramid_readback(mpGpu, 1), "orbx_extractor_set_pyramid_readback");
   mvImagePyramid.resize(nlevels);
 }
 
@@ -69,6 +76,15 @@ ORBextractor::~ORBextractor() {
 
 void ORBextractor::operator()(cv::InputArray _image, cv::InputArray, std::vector<cv::KeyPoint>& _keypoints,
                               cv::OutputArray _descriptors) {
+  Extract(_image, _keypoints, _descriptors, true);
+}
+
+void ORBextractor::ExtractForFrame(const cv::Mat& image, std::vector<cv::KeyPoint>& keypoints, cv::Mat& descriptors) {
+  Extract(image, keypoints, descriptors, false);
+}
+
+void ORBextractor::Extract(cv::InputArray _image, std::vector<cv::KeyPoint>& _keypoints,
+                           cv::OutputArray _descriptors, bool pyramid) {
   if (_image.empty()) return;  // src/ORBextractor.cc:1141
   cv::Mat image = _image.getMat();
   if (image.type() != CV_8UC1) throw std::invalid_argument("ORBextractor: image must be CV_8UC1");  // :1145
@@ -77,6 +93,7 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray, std::vector
   _keypoints.resize(cap);
   cv::Mat desc(cap > 0 ? cap : 1, 32, CV_8U);
   int n = 0;
+  check(orbx_extractor_set_pyramid_readback(mpGpu, pyramid ? 1 : 0), "orbx_extractor_set_pyramid_readback");
   check(orbx_extract(mpGpu, image.data, image.cols, image.rows, image.step,
                      reinterpret_cast<orbx_keypoint*>(_keypoints.data()), cap, desc.data, &n),
         "orbx_extract");
@@ -88,14 +105,18 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray, std::vector
     cv::Mat& out = _descriptors.getMatRef();
     for (int i = 0; i < n; i++) std::memcpy(out.ptr<uint8_t>(i), desc.ptr<uint8_t>(i), 32);
   }
-  if (mbDownloadPyramid) {
-    for (int l = 0; l < nlevels; l++) {
-      int w = 0, h = 0;
-      check(orbx_pyramid_level(mpGpu, 0, l, nullptr, 0, &w, &h), "orbx_pyramid_level");
-      mvImagePyramid[l].create(h, w, CV_8U);
-      check(orbx_pyramid_level(mpGpu, 0, l, mvImagePyramid[l].data, mvImagePyramid[l].step, &w, &h),
-            "orbx_pyramid_level");
+  for (int l = 0; l < nlevels; l++) {
+    if (!pyramid) {
+      mvImagePyramid[l].release();
+      continue;
     }
+    // new Mats every call, as ComputePyramid assigns fresh ones (an older level a caller kept stays
+    // intact); the copy comes from the pinned readback orbx_extract already waited for
+    int w = 0, h = 0;
+    check(orbx_pyramid_level(mpGpu, 0, l, nullptr, 0, &w, &h), "orbx_pyramid_level");
+    cv::Mat m(h, w, CV_8U);
+    check(orbx_pyramid_level(mpGpu, 0, l, m.data, m.step, &w, &h), "orbx_pyramid_level");
+    mvImagePyramid[l] = m;
   }
 }
 
@@ -235,9 +256,9 @@ void KeyFrame::ComputeBoW() {  // src/KeyFrame.cc:65-80
 
 void Frame::ExtractORB(int flag, const cv::Mat& im) {
   if (flag == 0)
-    (*mpORBextractorLeft)(im, cv::Mat(), mvKeys, mDescriptors);
+    mpORBextractorLeft->ExtractForFrame(im, mvKeys, mDescriptors);
   else
-    (*mpORBextractorRight)(im, cv::Mat(), mvKeysRight, mDescriptorsRight);
+    mpORBextractorRight->ExtractForFrame(im, mvKeysRight, mDescriptorsRight);
 }
 
 void Frame::UndistortKeyPoints() {
@@ -254,7 +275,7 @@ void Frame::UndistortKeyPoints() {
   for (int i = 0; i < 5; i++) cam.dist[i] = i < nd ? mDistCoef.ptr<float>(0)[i] : 0.f;
   mvKeysUn.resize(N);
   check(orbx_undistort_keypoints(reinterpret_cast<const orbx_keypoint*>(mvKeys.data()), N, &cam,
-                                 reinterpret_cast<orbx_keypoint*>(mvKeysUn.data()), 0),
+                                 reinterpret_cast<orbx_keypoint*>(mvKeysUn.data()), gOrbxDevice),
         "orbx_undistort_keypoints");
 }
 
@@ -282,8 +303,7 @@ const int ORBmatcher::TH_HIGH = 100;
 const int ORBmatcher::TH_LOW = 50;
 const int ORBmatcher::HISTO_LENGTH = 30;
 
-ORBmatcher::ORBmatcher(float nnratio, bool checkOri, int device)
-    : mfNNratio(nnratio), mbCheckOrientation(checkOri), mDevice(device) {}
+ORBmatcher::ORBmatcher(float nnratio, bool checkOri) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
 
 int ORBmatcher::DescriptorDistance(const cv::Mat& a, const cv::Mat& b) {
   // src/ORBmatcher.cc:1844-1860: popcount of the 256-bit XOR (the bit-trick sum there is a popcount)
@@ -339,7 +359,7 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpM
   const orbx_bow_side sa = a.side((int)pKF->mvKeysUn.size(), true), sb = b.side(F.N, false);
   std::vector<int32_t> match(F.N > 0 ? F.N : 1, -1);
   int n = 0;
-  check(orbx_search_by_bow_kf_f(&sa, &sb, mfNNratio, mbCheckOrientation, match.data(), &n, mDevice),
+  check(orbx_search_by_bow_kf_f(&sa, &sb, mfNNratio, mbCheckOrientation, match.data(), &n, gOrbxDevice),
         "orbx_search_by_bow_kf_f");
   for (int i = 0; i < F.N; i++)
     if (match[i] >= 0) vpMapPointMatches[i] = vpMapPointsKF[match[i]];
@@ -357,7 +377,7 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint
   const orbx_bow_side sa = a.side(n1, true), sb = b.side(n2, true);
   std::vector<int32_t> match(n1 > 0 ? n1 : 1, -1);
   int n = 0;
-  check(orbx_search_by_bow_kf_kf(&sa, &sb, mfNNratio, mbCheckOrientation, match.data(), &n, mDevice),
+  check(orbx_search_by_bow_kf_kf(&sa, &sb, mfNNratio, mbCheckOrientation, match.data(), &n, gOrbxDevice),
         "orbx_search_by_bow_kf_kf");
   for (int i = 0; i < n1 && i < (int)vpMatches12.size(); i++)
     if (match[i] >= 0) vpMatches12[i] = vpMapPoints2[match[i]];
@@ -509,7 +529,7 @@ int ORBmatcher::SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMap
   int32_t nm = 0;
   p.frame_out = frame_out.data();
   p.nmatches = &nm;
-  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection");
+  check(orbx_search_by_projection(&p, gOrbxDevice), "orbx_search_by_projection");
   apply_frame_out(F, frame_out, vpMapPoints);
   return nm;
 }
@@ -541,7 +561,7 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
   int32_t nm = 0;
   p.frame_out = frame_out.data();
   p.nmatches = &nm;
-  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection");
+  check(orbx_search_by_projection(&p, gOrbxDevice), "orbx_search_by_projection");
   apply_frame_out(CurrentFrame, frame_out, LastFrame.mvpMapPoints);
   return nm;
 }
@@ -574,7 +594,7 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std
   int32_t nm = 0;
   p.frame_out = frame_out.data();
   p.nmatches = &nm;
-  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection");
+  check(orbx_search_by_projection(&p, gOrbxDevice), "orbx_search_by_projection");
   apply_frame_out(CurrentFrame, frame_out, vpMPs);
   return nm;
 }
@@ -653,7 +673,7 @@ int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, c
   std::vector<int> all(n);
   for (int i = 0; i < n; i++) all[i] = i;
   std::vector<int32_t> best;
-  fuse_match(pKF, vpMapPoints, all, th, mDevice, best);
+  fuse_match(pKF, vpMapPoints, all, th, gOrbxDevice, best);
   std::set<MapPoint*> touched;  // MapPoints an earlier Replace modified
   int nFused = 0;
   for (int i = 0; i < n; i++) {
@@ -662,7 +682,7 @@ int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, c
     int bestIdx = best[i];
     if (touched.count(pMP)) {
       std::vector<int32_t> b1;
-      fuse_match(pKF, vpMapPoints, std::vector<int>{i}, th, mDevice, b1);
+      fuse_match(pKF, vpMapPoints, std::vector<int>{i}, th, gOrbxDevice, b1);
       bestIdx = b1[0];
     }
     if (bestIdx < 0) continue;
@@ -727,7 +747,7 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector
   int32_t nm = 0;
   p.frame_out = frame_out.data();
   p.nmatches = &nm;
-  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection (Sim3)");
+  check(orbx_search_by_projection(&p, gOrbxDevice), "orbx_search_by_projection (Sim3)");
   for (int i = 0; i < pKF->N && i < (int)vpMatched.size(); i++)
     if (frame_out[i] >= 0) vpMatched[i] = vpPoints[frame_out[i]];
   return nm;
@@ -756,7 +776,7 @@ int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, std::vector<cv::Po
   p.check_ori = mbCheckOrientation ? 1 : 0;
   p.match12 = m.data();
   p.nmatches = &nm;
-  check(orbx_search_for_initialization(&p, mDevice), "orbx_search_for_initialization");
+  check(orbx_search_for_initialization(&p, gOrbxDevice), "orbx_search_for_initialization");
   vnMatches12.assign(m.begin(), m.begin() + n1);
   for (int i = 0; i < n1 && i < (int)vbPrevMatched.size(); i++)
     if (m[i] >= 0) vbPrevMatched[i] = cv::Point2f(prev[2 * i], prev[2 * i + 1]);
@@ -811,7 +831,7 @@ int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoin
   int32_t nf = 0;
   p.match12 = m12.data();
   p.nfound = &nf;
-  check(orbx_search_by_sim3(&p, mDevice), "orbx_search_by_sim3");
+  check(orbx_search_by_sim3(&p, gOrbxDevice), "orbx_search_by_sim3");
   for (int i1 = 0; i1 < N1 && i1 < (int)vpMatches12.size(); i1++)
     if (m12[i1] >= 0) vpMatches12[i1] = vp2[m12[i1]];
   return nf;
@@ -855,7 +875,7 @@ int ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& v
   int32_t nm = 0;
   p.frame_out = frame_out.data();
   p.nmatches = &nm;
-  check(orbx_search_by_projection(&p, mDevice), "orbx_search_by_projection (Fuse Sim3)");
+  check(orbx_search_by_projection(&p, gOrbxDevice), "orbx_search_by_projection (Fuse Sim3)");
   int nFused = 0;
   for (int i = 0; i < n; i++) {
     const int bestIdx = P.point_match[i];
@@ -921,7 +941,7 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F
   int32_t nm = 0;
   p.match12 = m12.data();
   p.nmatches = &nm;
-  check(orbx_search_for_triangulation(&p, mDevice), "orbx_search_for_triangulation");
+  check(orbx_search_for_triangulation(&p, gOrbxDevice), "orbx_search_for_triangulation");
   vMatchedPairs.clear();
   vMatchedPairs.reserve(nm);
   for (int i = 0; i < pKF1->N; i++)
@@ -968,7 +988,7 @@ bool ORBVocabulary::loadFromText(const std::string& text) {
     orbx_voc_destroy(mpGpu);
     mpGpu = nullptr;
   }
-  check(orbx_voc_load_text(text.data(), text.size(), mDevice, &mpGpu), "orbx_voc_load_text");
+  check(orbx_voc_load_text(text.data(), text.size(), gOrbxDevice, &mpGpu), "orbx_voc_load_text");
   check(orbx_voc_info(mpGpu, mInfo), "orbx_voc_info");
   return true;
 }
@@ -1013,7 +1033,6 @@ void ORBVocabulary::transform(const std::vector<cv::Mat>& features, DBoW2::BowVe
 }
 
 // ------------------------------------------------------------------ PnPsolver
-int PnPsolver::mnDevice = 0;
 
 namespace {
 // the process-wide stream DUtils::Random::RandomInt draws from (glibc rand(), seed 1)
@@ -1071,7 +1090,7 @@ void PnPsolver::ensure_solver() {
   const int n = (int)mvSigma2.size();
   const orbx_pnp_problem prob{n, n ? mvP3Dw.data() : nullptr, n ? mvP2D.data() : nullptr,
                               n ? mvSigma2.data() : nullptr, fu, fv, uc, vc};
-  check(orbx_pnp_create(&prob, &mParams, mnDevice, &mpGpu), "orbx_pnp_create");
+  check(orbx_pnp_create(&prob, &mParams, gOrbxDevice, &mpGpu), "orbx_pnp_create");
   int mi = 0;
   float eps = 0;
   check(orbx_pnp_get_params(mpGpu, &mi, &mRansacMaxIts, &eps), "orbx_pnp_get_params");
@@ -1110,7 +1129,6 @@ cv::Mat PnPsolver::iterate(int nIterations, bool& bNoMore, std::vector<bool>& vb
 }
 
 // ------------------------------------------------------------------ Optimizer
-int Optimizer::mnDevice = 0;
 void (*Optimizer::mpfnGatheredHook)(const LocalBAProblem&, const std::vector<KeyFrame*>&) = nullptr;
 
 int Optimizer::PoseOptimization(Frame* pFrame) {
@@ -1152,7 +1170,7 @@ int Optimizer::PoseOptimization(Frame* pFrame) {
   p.Tcw_out = T;
   p.outlier = outlier.data();
   p.ngood = &ngood;
-  check(orbx_pose_optimization(&p, mnDevice), "orbx_pose_optimization");
+  check(orbx_pose_optimization(&p, gOrbxDevice), "orbx_pose_optimization");
   for (int k = 0; k < n; k++) pFrame->mvbOutlier[idx[k]] = outlier[k] != 0;
   cv::Mat pose(4, 4, CV_32F);
   for (int i = 0; i < 16; i++) pose.at<float>(i / 4, i % 4) = T[i];
@@ -1238,7 +1256,7 @@ void Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap
   // :747-751: a stop requested before the optimisation leaves the map untouched
   if (pbStopFlag && *pbStopFlag) return;
   LocalBAResult R;
-  LocalBundleAdjustment(P, pbStopFlag, R, mnDevice);
+  LocalBundleAdjustment(P, pbStopFlag, R, gOrbxDevice);
   // the flag may have gone up between the check above and the library's own poll: the library then
   // skipped optimize(5), and the reference would have returned here with the map untouched (:749-751)
   if (!R.ran) return;

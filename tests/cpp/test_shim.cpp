@@ -114,6 +114,13 @@ static int mode_abi() {
   for (int i = 0; i < 32; i++) manual += __builtin_popcount((unsigned)(a.at<uint8_t>(1, i) ^ a.at<uint8_t>(3, i)));
   REQUIRE(ORBmatcher::DescriptorDistance(a.row(1), a.row(3)) == manual);
   REQUIRE(ORBmatcher::TH_LOW == 50 && ORBmatcher::TH_HIGH == 100 && ORBmatcher::HISTO_LENGTH == 30);
+  // the reference's layouts: ORBmatcher holds {float mfNNratio; bool mbCheckOrientation;}
+  // (include/ORBmatcher.h:175-177); cv::Point is Point_<int>
+  REQUIRE(sizeof(ORBmatcher) == 8 && sizeof(cv::Point) == 8 && sizeof(cv::Point2f) == 8);
+  {
+    ORBmatcher dflt;  // ORBmatcher(float nnratio=0.6, bool checkOri=true), include/ORBmatcher.h:47
+    (void)dflt;
+  }
   // GPU-backed members fail loudly without a device (never a silent CPU path)
   if (orbx_device_count() <= 0) {
     REQUIRE(throws_runtime([] { ORBextractor ex(1000, 1.2f, 8, 20, 7); }));
@@ -154,8 +161,6 @@ static int mode_stereo(const char* in, const char* out) {
   const float bf = r.get<float>(), fx = r.get<float>();
   std::vector<uint8_t> L = r.vec<uint8_t>((size_t)w * h), R = r.vec<uint8_t>((size_t)w * h);
   ORBextractor exL(nf, sf, nl, ini, mn), exR(nf, sf, nl, ini, mn);
-  REQUIRE(!exL.mbDownloadPyramid);  // off by default: the stereo matcher reads the device copy
-  exL.mbDownloadPyramid = true;     // this test also checks the host copy
   cv::Mat imL(h, w, CV_8U, L.data()), imR(h, w, CV_8U, R.data());
   cv::Mat K(3, 3, CV_32F), dist(4, 1, CV_32F);
   std::memset(K.data, 0, 36);
@@ -177,6 +182,23 @@ static int mode_stereo(const char* in, const char* out) {
   for (size_t i = 0; i < F.mvKeysRight.size(); i++) o.raw(F.mDescriptorsRight.ptr<uint8_t>((int)i), 32);
   o.raw(F.mvuRight.data(), F.mvuRight.size() * 4);
   o.raw(F.mvDepth.data(), F.mvDepth.size() * 4);
+  // Frame reads the device pyramids, so its extractions leave mvImagePyramid empty (never stale)
+  for (int l = 0; l < nl; l++) REQUIRE(exL.mvImagePyramid[l].empty());
+  // operator() itself refreshes mvImagePyramid on every call (src/ORBextractor.cc:1215-1250): first
+  // on the right image, then on the left one, whose levels must be the left image's
+  {
+    std::vector<cv::KeyPoint> kr, kl;
+    cv::Mat dr, dl;
+    exL(imR, cv::Mat(), kr, dr);
+    REQUIRE((int)exL.mvImagePyramid.size() == nl && exL.mvImagePyramid[0].cols == w && exL.mvImagePyramid[0].rows == h);
+    REQUIRE(std::memcmp(exL.mvImagePyramid[0].data, R.data(), (size_t)w * h) == 0);
+    const cv::Mat keep = exL.mvImagePyramid[1];  // a level a caller kept survives the next call
+    std::vector<uint8_t> keep_bytes(keep.data, keep.data + (size_t)keep.rows * keep.step);
+    exL(imL, cv::Mat(), kl, dl);
+    REQUIRE(kl.size() == F.mvKeys.size() && std::memcmp(kl.data(), F.mvKeys.data(), kl.size() * 28) == 0);
+    REQUIRE(keep.data != exL.mvImagePyramid[1].data &&
+            std::memcmp(keep.data, keep_bytes.data(), keep_bytes.size()) == 0);
+  }
   // the host copy of the left pyramid (mvImagePyramid)
   for (int l = 0; l < nl; l++) {
     const cv::Mat& m = exL.mvImagePyramid[l];

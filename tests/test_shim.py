@@ -46,7 +46,8 @@ def test_shim_abi(exe):
 
 def test_shim_exports_reference_classes(exe):
     out = subprocess.check_output(["nm", "-DC", "--defined-only", os.path.join(ROOT, "shim", "liborbx_shim.so")]).decode()
-    for sym in ["ORB_SLAM2::ORBextractor::ORBextractor(int, float, int, int, int, int)",
+    for sym in ["ORB_SLAM2::ORBextractor::ORBextractor(int, float, int, int, int)",
+                "ORB_SLAM2::ORBmatcher::ORBmatcher(float, bool)",
                 "ORB_SLAM2::ORBextractor::operator()(cv::_InputArray const&, cv::_InputArray const&, "
                 "std::vector<cv::KeyPoint, std::allocator<cv::KeyPoint> >&, cv::_OutputArray const&)",
                 "ORB_SLAM2::ORBmatcher::DescriptorDistance(cv::Mat const&, cv::Mat const&)",
@@ -78,7 +79,7 @@ def test_shim_exports_reference_classes(exe):
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> > const&, "
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&, int)",
                 "ORB_SLAM2::ORBmatcher::SearchForInitialization(ORB_SLAM2::Frame&, ORB_SLAM2::Frame&, "
-                "std::vector<cv::Point2f, std::allocator<cv::Point2f> >&, std::vector<int, std::allocator<int> >&, int)",
+                "std::vector<cv::Point_<float>, std::allocator<cv::Point_<float> > >&, std::vector<int, std::allocator<int> >&, int)",
                 "ORB_SLAM2::ORBmatcher::SearchBySim3(ORB_SLAM2::KeyFrame*, ORB_SLAM2::KeyFrame*, "
                 "std::vector<ORB_SLAM2::MapPoint*, std::allocator<ORB_SLAM2::MapPoint*> >&, float const&, "
                 "cv::Mat const&, cv::Mat const&, float)",
@@ -96,6 +97,9 @@ def test_shim_exports_reference_classes(exe):
                 "ORB_SLAM2::ORBVocabulary::transform(std::vector<cv::Mat, std::allocator<cv::Mat> > const&, "
                 "DBoW2::BowVector&, DBoW2::FeatureVector&, int) const"]:
         assert sym in out, sym
+    # no device argument in the reference constructors (include/ORBextractor.h:61, include/ORBmatcher.h:47)
+    assert "ORB_SLAM2::ORBextractor::ORBextractor(int, float, int, int, int, int)" not in out
+    assert "ORB_SLAM2::ORBmatcher::ORBmatcher(float, bool, int)" not in out
 
 
 # ------------------------------------------------------------------------------------------ GPU
