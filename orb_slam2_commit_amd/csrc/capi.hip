@@ -29,8 +29,7 @@ namespace orbx {
 hipError_t upload_constants(const int* umax16, const int* gauss7);
 hipError_t launch_blur(const Geometry& Gh, const Geometry* Gd, const int* tile_level, const BatchPtrs& B, int n_img,
                        hipStream_t st);
-hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells, const FastStrip* strips,
-                                 const int* tile_level,
+hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells, const int* tile_level,
                                  const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B, int n_img,
                                  orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap, hipStream_t st,
                                  StageTimer* T);
@@ -130,13 +129,11 @@ void gaussian_int_kernel(int k[7]) {
 struct Plan {
   Geometry G{};
   std::vector<CellInfo> cells;
-  std::vector<FastStrip> strips;
   std::vector<int> tile_level;
   std::vector<ResizeX> xt;
   std::vector<ResizeY> yt;
   DevBuf<Geometry> dG;
   DevBuf<CellInfo> dcells;
-  DevBuf<FastStrip> dstrips;
   DevBuf<int> dtiles;
   DevBuf<ResizeX> dxt;
   DevBuf<ResizeY> dyt;
@@ -326,70 +323,6 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
       G.n_fg = 2;
     }
   }
-  // k_fast strips: each cell row of a level split into ceil(n / K) strips of near-equal cell counts,
-  // K = floor(250 / wCell), so a strip's region plus the 3-pixel margins fits the 256 columns one
-  // wave holds (64 lanes x 4); the kernel finds a pixel's cell as 3 + j * wcell, so every cell of a
-  // strip but the last must be exactly wcell wide (the reference's layout: only a row's last cell is
-  // clipped, src/ORBextractor.cc:862-869) -- checked here
-  {
-    int hmax = 1;
-    for (int l = 0; l < p.nlevels; l++) {
-      const LevelGeom& L = G.lv[l];
-      for (int c = L.cell_begin; c < L.cell_end;) {
-        int e = c;
-        while (e < L.cell_end && P.cells[e].y0 == P.cells[c].y0) e++;
-        const int n = e - c, wc = P.cells[c].x1 - P.cells[c].x0 + 1;
-        const int K = std::max(1, 250 / wc), ns = (n + K - 1) / K;
-        for (int q = 0; q < ns; q++) {
-          const int a = c + n * q / ns, b = c + n * (q + 1) / ns;
-          const CellInfo& A = P.cells[a];
-          FastStrip S{};
-          S.level = (int16_t)l;
-          S.ncell = (int16_t)(b - a);
-          S.y0 = A.y0;
-          S.h = (int16_t)(A.y1 - A.y0 + 1);
-          S.xs = (int16_t)(A.x0 - 3);
-          S.wcell = (int16_t)(A.x1 - A.x0 + 1);
-          S.cxl = (int16_t)(P.cells[b - 1].x1 - S.xs);
-          S.cell0 = a;
-          S.lw = L.w;
-          S.lh = L.h;
-          S.loff = (int)L.off;
-          for (int k = a; k < b; k++) {
-            const CellInfo& C = P.cells[k];
-            const bool ok = C.y0 == A.y0 && C.y1 == A.y1 && C.x0 == A.x0 + (k - a) * S.wcell &&
-                            (k + 1 < b ? C.x1 == C.x0 + S.wcell - 1 : C.x1 <= C.x0 + S.wcell - 1);
-            if (!ok) return ORBX_ERR_SIZE;
-          }
-          if (S.cxl + 3 > 255 || S.h > 64) return ORBX_ERR_SIZE;
-          hmax = std::max(hmax, (int)S.h);
-          P.strips.push_back(S);
-        }
-        c = e;
-      }
-    }
-    // two launch groups: strips no taller than the median level's cells first (stable order)
-    std::vector<int> hs;
-    for (const FastStrip& S : P.strips) hs.push_back(S.h);
-    std::vector<int> sorted_h = hs;
-    std::sort(sorted_h.begin(), sorted_h.end());
-    const int hsplit = sorted_h.empty() ? 0 : sorted_h[sorted_h.size() / 2];
-    std::stable_partition(P.strips.begin(), P.strips.end(), [&](const FastStrip& S) { return S.h <= hsplit; });
-    int na = 0, ha = 1, hb = 1;
-    for (const FastStrip& S : P.strips) {
-      if (S.h <= hsplit) {
-        na++;
-        ha = std::max(ha, (int)S.h);
-      } else {
-        hb = std::max(hb, (int)S.h);
-      }
-    }
-    G.n_strips = (int)P.strips.size();
-    G.n_sg = 0;
-    if (na > 0) G.sg[G.n_sg++] = {0, na, (int)fast_strip_smem_bytes(ha)};
-    if (G.n_strips > na) G.sg[G.n_sg++] = {na, G.n_strips - na, (int)fast_strip_smem_bytes(hb)};
-    (void)hmax;
-  }
   // k_resize staging bound: source footprint of every 128x16 output tile
   G.rz_rows = 1;
   G.rz_stride = 16;
@@ -482,7 +415,7 @@ struct orbx_extractor {
   long long bytes_pyr = 0, bytes_blur = 0, n_cand = 0, n_oct = 0, n_cells = 0;
   DevBuf<uint8_t> pyr, blur;
   DevBuf<uint32_t> cand, kpos, oct;
-  DevBuf<int> cell_count, knode, oct_count, fast_fb;
+  DevBuf<int> cell_count, knode, oct_count;
   // host-API staging: the input image, and ONE output block [count | keypoints | descriptors]
   // (orbx_extract reads it back with one copy; orbx_stereo_match reads it in place)
   DevBuf<uint8_t> in, out;
@@ -559,15 +492,12 @@ orbx_status get_plan(orbx_extractor* h, int W, int H, Plan** out) {
   hipError_t e;
   if ((e = P->dG.ensure(1)) != hipSuccess) return ORBX_ERR_HIP;
   if ((e = P->dcells.ensure(P->cells.size())) != hipSuccess) return ORBX_ERR_HIP;
-  if ((e = P->dstrips.ensure(P->strips.size())) != hipSuccess) return ORBX_ERR_HIP;
   if ((e = P->dtiles.ensure(P->tile_level.size())) != hipSuccess) return ORBX_ERR_HIP;
   if ((e = P->dxt.ensure(P->xt.size())) != hipSuccess) return ORBX_ERR_HIP;
   if ((e = P->dyt.ensure(P->yt.size())) != hipSuccess) return ORBX_ERR_HIP;
   e = hipMemcpy(P->dG.p, &P->G, sizeof(Geometry), hipMemcpyHostToDevice);
   if (e == hipSuccess && !P->cells.empty())
     e = hipMemcpy(P->dcells.p, P->cells.data(), P->cells.size() * sizeof(CellInfo), hipMemcpyHostToDevice);
-  if (e == hipSuccess && !P->strips.empty())
-    e = hipMemcpy(P->dstrips.p, P->strips.data(), P->strips.size() * sizeof(FastStrip), hipMemcpyHostToDevice);
   if (e == hipSuccess && !P->tile_level.empty())
     e = hipMemcpy(P->dtiles.p, P->tile_level.data(), P->tile_level.size() * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess && !P->xt.empty())
@@ -597,7 +527,6 @@ orbx_status ensure_batch(orbx_extractor* h, const Plan& P, int n) {
   chk(h->kpos.ensure((size_t)G.cand_total * n));
   chk(h->knode.ensure((size_t)G.cand_total * n));
   chk(h->cell_count.ensure((size_t)std::max(G.ncells, 1) * n));
-  chk(h->fast_fb.ensure((size_t)std::max(G.ncells, 1) * n));
   chk(h->oct.ensure((size_t)G.oct_total * n));
   chk(h->oct_count.ensure((size_t)G.nlevels * n));
   return hip_status(e);
@@ -611,7 +540,6 @@ BatchPtrs batch_ptrs(orbx_extractor* h, const uint8_t* in, size_t pitch) {
   B.blur = h->blur.p;
   B.cand = h->cand.p;
   B.cell_count = h->cell_count.p;
-  B.fast_fb = h->fast_fb.p;
   B.kpos = h->kpos.p;
   B.knode = h->knode.p;
   B.oct = h->oct.p;
@@ -625,7 +553,7 @@ orbx_status run_extract(orbx_extractor* h, Plan* P, int n, const uint8_t* d_in, 
   orbx_status s = ensure_batch(h, *P, n);
   if (s != ORBX_OK) return s;
   BatchPtrs B = batch_ptrs(h, d_in, pitch);
-  hipError_t e = launch_extract_stages(P->G, P->dG.p, P->dcells.p, P->dstrips.p, P->dtiles.p, P->dxt.p, P->dyt.p, B, n, d_kps,
+  hipError_t e = launch_extract_stages(P->G, P->dG.p, P->dcells.p, P->dtiles.p, P->dxt.p, P->dyt.p, B, n, d_kps,
                                        d_desc, d_counts, kp_cap, st, &h->timer);
   if (e != hipSuccess) return ORBX_ERR_HIP;
   h->last_plan = P;

@@ -586,22 +586,17 @@ __device__ unsigned int* fast_probe_buf;
 #define ORBX_FAST_CPW 2
 #endif
 constexpr int kFastCPW = ORBX_FAST_CPW;  // FAST cells per wave
-// FB: the cells k_fast_strip left to this kernel instead of a cell range (a flag per cell, B.fast_fb):
-// 1 = the whole cell (its strip's survivors overflowed the LDS list), 2 = only the minThFAST pass
-// (no survivor at iniThFAST); S/RP then fit the widest cell
-template <int S, int RP, bool FB = false>
+template <int S, int RP>
 __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B, int grp) {
-  // dynamic LDS sized by the launch group's largest cell (G->fg[grp]), or the widest possible (FB)
+  // dynamic LDS sized by the launch group's largest cell (G->fg[grp])
   extern __shared__ __align__(16) uint8_t fast_smem[];
-  const int tile_bytes = FB ? (((kMaxCell + 6) * S + 15) & ~15) : G->fg[grp].tile_bytes;
-  const int map_bytes = FB ? (((kMaxCell + 2) * S + 15) & ~15) : G->fg[grp].map_bytes;
+  const int tile_bytes = G->fg[grp].tile_bytes, map_bytes = G->fg[grp].map_bytes;
   uint8_t* tile = fast_smem;
   uint8_t* smap = fast_smem + tile_bytes;
   uint16_t* list = (uint16_t*)(fast_smem + tile_bytes + map_bytes);
   const int2 bi = xcd_block2();
-  int img = bi.y;
-  const int lane = threadIdx.x;
+  const int img = bi.y, lane = threadIdx.x;
   // 1. window -> registers -> LDS: lane = (row, 16-B chunk); window pixel (r, col) lands at tile[r*S + col]
   constexpr int CPR = (S + 15) / 16, RPI = 64 / CPR;
   constexpr int KMAX = (kMaxCell + 6 + RPI - 1) / RPI;
@@ -629,51 +624,26 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   };
   // kFastCPW cells per wave, one after another; the next cell's window loads are issued before the
   // current cell's work, so their latency hides behind it
-  const int cell0 = FB ? 0 : G->fg[grp].c0 + bi.x * kFastCPW, cend = FB ? 0 : G->fg[grp].c1;
-  // FB: this block's cells are bi.x * 64 + k * 64 * gridDim.x + lane; the flagged ones one by one
-  const int* fbl = B.fast_fb + (size_t)img * G->ncells;
-  int fb_base = bi.x * 64, fb_flag = 0;
-  uint64_t fb_m = 0;
-  CellInfo cn;
+  const int cell0 = G->fg[grp].c0 + bi.x * kFastCPW, cend = G->fg[grp].c1;
+  CellInfo cn = cells[cell0];
   uint32_t vn[KMAX][4];
-  if (!FB) {
-    cn = cells[cell0];
-    load_window(cn, vn);
-  }
-  for (int q = 0; FB || q < kFastCPW; q++) {
-  int cell, mode = 0;
-  if (FB) {
-    while (fb_m == 0 && fb_base < G->ncells) {  // wave-uniform
-      const int cl = fb_base + lane;
-      fb_flag = cl < G->ncells ? fbl[cl] : 0;
-      fb_m = __ballot(fb_flag != 0);
-      if (fb_m == 0) fb_base += 64 * gridDim.x;
-    }
-    if (fb_m == 0) break;
-    const int k = __builtin_ctzll(fb_m);
-    fb_m &= fb_m - 1;
-    cell = fb_base + k;
-    mode = __builtin_amdgcn_readlane(fb_flag, k) - 1;
-    if (fb_m == 0) fb_base += 64 * gridDim.x;
-    cn = cells[cell];
-    load_window(cn, vn);
-  } else {
-    cell = cell0 + q;
-    if (cell >= cend) break;  // wave-uniform
-  }
+  load_window(cn, vn);
+  for (int q = 0; q < kFastCPW; q++) {
+  const int cell = cell0 + q;
+  if (cell >= cend) break;  // wave-uniform
   const CellInfo c = cn;
   uint32_t v[KMAX][4];
 #pragma unroll
   for (int k = 0; k < KMAX; k++)
 #pragma unroll
     for (int e = 0; e < 4; e++) v[k][e] = vn[k][e];
-  if (!FB && q + 1 < kFastCPW && cell + 1 < cend) {
+  if (q + 1 < kFastCPW && cell + 1 < cend) {
     cn = cells[cell + 1];
     load_window(cn, vn);
   }
   const int W = c.x1 - c.x0 + 1, H = c.y1 - c.y0 + 1, TH = H + 6;
   FAST_TS(0);
-  __syncthreads();  // the previous cell's tile / map / list reads are done
+  if (q > 0) __syncthreads();  // the previous cell's tile / map / list reads are done
   {
     // zero the score map (its border row/column stands for "outside the region")
     for (int i = lane * 16; i < map_bytes; i += 64 * 16) *(uint4*)(smap + i) = make_uint4(0, 0, 0, 0);
@@ -771,7 +741,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   // FAST at iniThFAST only (src/ORBextractor.cc:892): the map then holds exactly the corners at
   // iniThFAST, which is all NMS at iniThFAST looks at (a weaker neighbour never beats a centre)
   FAST_TS(1);
-  int nc = mode == 1 ? 0 : detect(ini);
+  int nc = detect(ini);
   FAST_TS(2);
   // 4. survivors at iniThFAST (verdict kept in bit 15 of the list entry)
   int cnt = 0;
@@ -822,286 +792,6 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   }
 #endif
   }  // cells of this wave
-}
-
-#ifndef ORBX_FAST_STRIP
-#define ORBX_FAST_STRIP 1
-#endif
-// ------------------------------------------------------------ FAST by strips
-// One 256-thread block per strip: up to 8 consecutive FAST cells of one cell row (FastStrip), a window
-// of up to 256 columns x (H + 6) rows.  Per pixel the work is the cell windows' cv::FAST(window, t,
-// nonmax) of src/ORBextractor.cc:843-915; a pixel's corner test and score do not depend on its
-// window (the cell regions partition the strip's region), so only NMS at the cell seams and the
-// per-cell threshold choice are per cell:
-//   1. the window -> LDS (16-B buffer loads at the unaligned row positions, all in flight), rows at a
-//      272-B stride (a 256-B stride put every row of a 7x7 ring on one bank: 350M conflict cycles);
-//   2. compass test at tc = min(iniThFAST, minThFAST) for every pixel from registers: wave w sweeps a
-//      band of rows, lane L owns strip columns 4L .. 4L+3 as two u16 pairs per row (v_perm unpacks)
-//      and keeps the 7 rows a centre row needs in a register ring; the +-3 column taps are byte
-//      permutes of the row's dword and its neighbours'; min/max/saturating differences as v_pk_*_u16
-//      on two pixels per instruction;
-//   3. the survivors compacted block-wide (wave scans of per-lane counts), cornerScore<16>+1 for them
-//      from the LDS tile (ring_score1), the corners at tc compacted in place;
-//   4. the tile becomes the score map (the window is no longer read), strict 3x3 NMS of every corner
-//      against its own cell's region (neighbours across a cell seam or outside the region count as
-//      0) at iniThFAST and at minThFAST: two survivor bitmaps;
-//   5. per cell (wave w takes cells w, w+4, ...; lane = region row) the survivors at iniThFAST, or at
-//      minThFAST when there are none (the reference's second FAST call, :892-900), are written
-//      row-major into the cell's slots.  A strip whose survivors overflow the LDS list (kStripCap)
-//      leaves its cells to k_fast<.., true> (a flag per cell in B.fast_fb).
-constexpr int kStripNT = 256;
-constexpr int kTS = 272, kTS4 = kTS / 4;  // tile row stride (bytes, dwords)
-
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-  return v;
-}
-
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-  uint32_t d;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
-
-__global__ __launch_bounds__(kStripNT) void k_fast_strip(const Geometry* __restrict__ G,
-                                                         const CellInfo* __restrict__ cells,
-                                                         const FastStrip* __restrict__ strips, int strip0,
-                                                         BatchPtrs B) {
-  extern __shared__ __align__(16) uint8_t fs_smem[];
-  __shared__ int s_wtot[4];
-  const int2 bi = xcd_block2();
-  const FastStrip s = strips[strip0 + bi.x];
-  const int img = bi.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int H = s.h, T = H + 6;
-  uint8_t* tile = fs_smem;  // T rows x kTS; rows 0 .. H-1 become the score map after step 3
-  const uint32_t* tile32 = (const uint32_t*)fs_smem;
-  uint16_t* list = (uint16_t*)(fs_smem + T * kTS);  // kStripCap survivors (row << 8 | column)
-  uint8_t* lsc = (uint8_t*)(list + kStripCap);      // the corners' S+1
-  uint32_t* bmi = (uint32_t*)(lsc + kStripCap);     // survivors at iniThFAST: H rows x 256 bits
-  uint32_t* bmm = bmi + H * 8;                      // survivors at minThFAST
-  // 1. window -> LDS
-  {
-    const uint8_t* lvl = s.level == 0 ? B.in + (size_t)img * B.in_pitch : B.pyr + (size_t)img * G->pyr_bytes + s.loff;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)lvl, (short)0, s.lw * s.lh, 0x00020000);
-    const int lr = tid >> 4, lc = tid & 15;
-    const int rowb = (s.y0 - 3) * s.lw + s.xs + 16 * lc;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    constexpr int KP = (kMaxCell + 6 + 15) / 16;
-    u32x4 v[KP];
-#pragma unroll
-    for (int k = 0; k < KP; k++) {
-      const int r = 16 * k + lr;
-      v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, r < T ? (uint32_t)(rowb + r * s.lw) : 0x80000000u, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < KP; k++) {
-      const int r = 16 * k + lr;
-      if (r < T) *(u32x4*)(tile + r * kTS + 16 * lc) = v[k];
-    }
-    for (int i = tid; i < 2 * H * 8; i += kStripNT) bmi[i] = 0;
-  }
-  __syncthreads();
-  const int ini = min(max(G->ini_th, 0), 255), mint = min(max(G->min_th, 0), 255), tc = min(ini, mint);
-  const uint32_t tt = (uint32_t)tc * 0x10001u;
-  // 2. compass survivors of this wave's band: rows b0 .. b1-1 in blocks of 8 (bit 4i + k of block
-  //    word q: row b0 + 8q + i, column 4 * lane + k)
-  const int Bh = (((H + 3) >> 2) + 3) & ~3, b0 = min(H, wave * Bh), b1 = min(H, b0 + Bh);
-  uint32_t mw[2] = {0, 0};  // Bh <= 16 rows
-  if (b0 < b1) {
-    uint32_t rmask = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) rmask |= (4 * lane + k >= 3 && 4 * lane + k <= s.cxl) ? (1u << k) : 0u;
-    auto unpack_lo = [](uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0c010c00u); };
-    auto unpack_hi = [](uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0c030c02u); };
-    auto u16 = [](uint32_t v) { return __builtin_bit_cast(u16x2, v); };
-    auto w32 = [](u16x2 v) { return __builtin_bit_cast(uint32_t, v); };
-    uint32_t UA[8], UB[8];
-#pragma unroll
-    for (int t = 0; t < 6; t++) {
-      const uint32_t o = tile32[(b0 + t) * kTS4 + lane];
-      UA[t] = unpack_lo(o);
-      UB[t] = unpack_hi(o);
-    }
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      if (8 * q >= b1 - b0) break;  // wave-uniform
-      const int r8 = b0 + 8 * q;
-      uint32_t m = 0;
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        if (i == 4 && r8 + 4 >= b1) break;  // wave-uniform: the band ends at a multiple of 4 rows
-        // rows past the band (at most 3) read LDS inside the allocation and are masked
-        const int r = r8 + i, tn = r + 6, t = r + 3;
-        const uint32_t on = tile32[tn * kTS4 + lane];
-        const uint32_t prev = tile32[t * kTS4 + lane - 1], own = tile32[t * kTS4 + lane], next = tile32[t * kTS4 + lane + 1];
-        UA[(i + 6) & 7] = unpack_lo(on);
-        UB[(i + 6) & 7] = unpack_hi(on);
-        const u16x2 cA = u16(UA[(i + 3) & 7]), cB = u16(UB[(i + 3) & 7]);
-        const u16x2 p0A = u16(UA[(i + 6) & 7]), p0B = u16(UB[(i + 6) & 7]), p8A = u16(UA[i & 7]), p8B = u16(UB[i & 7]);
-        const u16x2 p4A = u16(__builtin_amdgcn_perm(next, own, 0x0c040c03u));
-        const u16x2 p4B = u16(__builtin_amdgcn_perm(next, own, 0x0c060c05u));
-        const u16x2 p12A = u16(__builtin_amdgcn_perm(own, prev, 0x0c020c01u));
-        const u16x2 p12B = u16(__builtin_amdgcn_perm(own, prev, 0x0c040c03u));
-        // compass: min(max(p0,p8), max(p4,p12)) > c+t or max(min(p0,p8), min(p4,p12)) < c-t
-        const u16x2 hiA = __builtin_elementwise_min(__builtin_elementwise_max(p0A, p8A), __builtin_elementwise_max(p4A, p12A));
-        const u16x2 hiB = __builtin_elementwise_min(__builtin_elementwise_max(p0B, p8B), __builtin_elementwise_max(p4B, p12B));
-        const u16x2 loA = __builtin_elementwise_max(__builtin_elementwise_min(p0A, p8A), __builtin_elementwise_min(p4A, p12A));
-        const u16x2 loB = __builtin_elementwise_max(__builtin_elementwise_min(p0B, p8B), __builtin_elementwise_min(p4B, p12B));
-        const u16x2 dA = __builtin_elementwise_max(__builtin_elementwise_sub_sat(hiA, cA), __builtin_elementwise_sub_sat(cA, loA));
-        const u16x2 dB = __builtin_elementwise_max(__builtin_elementwise_sub_sat(hiB, cB), __builtin_elementwise_sub_sat(cB, loB));
-        // (d - t)_sat clamped to 1 per pixel: bits 0 / 16 of A, 2 / 18 of B
-        const uint32_t hA = pk_min_u16(w32(__builtin_elementwise_sub_sat(dA, u16(tt))), 0x10001u);
-        const uint32_t hB = pk_min_u16(w32(__builtin_elementwise_sub_sat(dB, u16(tt))), 0x10001u);
-        const uint32_t y = hA | (hB << 2);
-        m |= ((y | (y >> 15)) & rmask) << (4 * i);
-      }
-      mw[q] = m;
-    }
-    // rows past b1 in the last block
-    const int nb = b1 - b0;
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const int left = nb - 8 * q;
-      mw[q] = left >= 8 ? mw[q] : left <= 0 ? 0u : (mw[q] & ((1u << (4 * left)) - 1));
-    }
-  }
-  // 3. survivors -> list (block order: wave, lane, row, column), their scores, corners in place
-  const int cnt = __builtin_popcount(mw[0]) + __builtin_popcount(mw[1]);
-  const int incl = wave_incl_scan(cnt);
-  if (lane == 63) s_wtot[wave] = incl;
-  __syncthreads();
-  int o = incl - cnt, n = 0;
-#pragma unroll
-  for (int w = 0; w < 4; w++) {
-    const int t = s_wtot[w];
-    o += w < wave ? t : 0;
-    n += t;
-  }
-  if (n > kStripCap) {  // block-uniform: the whole strip goes to the worklist pass
-    if (tid < s.ncell) B.fast_fb[(size_t)img * G->ncells + s.cell0 + tid] = 1;
-    return;
-  }
-#pragma unroll
-  for (int q = 0; q < 2; q++) {
-    uint32_t m = mw[q];
-    const int rb = (b0 + 8 * q) << 8, cb = 4 * lane;
-    while (m) {
-      const int b = __builtin_ctz(m);
-      list[o++] = (uint16_t)(rb + ((b >> 2) << 8) + cb + (b & 3));
-      m &= m - 1;
-    }
-  }
-  __syncthreads();
-  int nc = 0;
-  for (int i0 = 0; i0 < n; i0 += kStripNT) {
-    const int i = i0 + tid;
-    int e = 0, sc1 = 0;
-    bool corner = false;
-    if (i < n) {
-      e = list[i];
-      sc1 = ring_score1<kTS>(tile + (e >> 8) * kTS + (e & 255) - 3);
-      corner = sc1 > tc;
-    }
-    const uint64_t m = __ballot(corner);
-    __syncthreads();  // every read of this round is done (s_wtot reused, list written in place)
-    if (lane == 0) s_wtot[wave] = __popcll(m);
-    __syncthreads();
-    int cb = nc, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      const int t = s_wtot[w];
-      cb += w < wave ? t : 0;
-      tot += t;
-    }
-    if (corner) {
-      list[cb + lane_rank(m)] = (uint16_t)e;
-      lsc[cb + lane_rank(m)] = (uint8_t)sc1;
-    }
-    nc += tot;
-  }
-  __syncthreads();
-  // 4. the window's rows 0 .. H-1 become the score map (S+1 of the corners, 0 elsewhere)
-  for (int i = tid; i < (H * kTS) / 16; i += kStripNT) *(uint4*)(tile + 16 * i) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  for (int i = tid; i < nc; i += kStripNT) {
-    const int e = list[i];
-    tile[(e >> 8) * kTS + (e & 255)] = lsc[i];
-  }
-  __syncthreads();
-  {
-    const float invw = 1.0f / (float)s.wcell;
-    const int ti = ini + 1, tm = mint + 1;
-    for (int i = tid; i < nc; i += kStripNT) {
-      const int e = list[i], r = e >> 8, cx = e & 255, p = r * kTS + cx;
-      const int sc = lsc[i];
-      const int j = (int)(((float)(cx - 3) + 0.5f) * invw);
-      const int cx0 = 3 + j * s.wcell, cx1 = min(cx0 + s.wcell - 1, (int)s.cxl);
-      const bool L = cx > cx0, Rt = cx < cx1, U = r > 0, D = r < H - 1;
-      const int pu = U ? p - kTS : p, pd = D ? p + kTS : p;
-      int mx = 0;
-      if (L) mx = max(mx, (int)tile[p - 1]);
-      if (Rt) mx = max(mx, (int)tile[p + 1]);
-      if (U) {
-        mx = max(mx, (int)tile[pu]);
-        if (L) mx = max(mx, (int)tile[pu - 1]);
-        if (Rt) mx = max(mx, (int)tile[pu + 1]);
-      }
-      if (D) {
-        mx = max(mx, (int)tile[pd]);
-        if (L) mx = max(mx, (int)tile[pd - 1]);
-        if (Rt) mx = max(mx, (int)tile[pd + 1]);
-      }
-      const uint32_t bit = 1u << (cx & 31);
-      if (sc >= ti && sc > 1 && !(mx >= max(ti, sc))) atomicOr(&bmi[r * 8 + (cx >> 5)], bit);
-      if (sc >= tm && sc > 1 && !(mx >= max(tm, sc))) atomicOr(&bmm[r * 8 + (cx >> 5)], bit);
-    }
-  }
-  __syncthreads();
-  // 5. per cell, row-major into the cell's slots (lane = region row)
-  const int r = lane;
-  const bool rv = r < H;
-  for (int j = wave; j < s.ncell; j += 4) {
-    const int cell = s.cell0 + j;
-    const CellInfo cc = cells[cell];
-    const int cx0 = cc.x0 - s.xs, cx1 = cc.x1 - s.xs, w = cx0 >> 5, sh = cx0 & 31;
-    const uint64_t lenm = (1ull << (cx1 - cx0 + 1)) - 1;
-    auto seg = [&](const uint32_t* bm) -> uint64_t {
-      if (!rv) return 0;
-      const uint32_t* q = bm + r * 8;
-      const uint32_t d0 = q[w], d1 = w + 1 < 8 ? q[w + 1] : 0u, d2 = w + 2 < 8 ? q[w + 2] : 0u;
-      const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh), hi = __builtin_amdgcn_alignbit(d2, d1, sh);
-      return (((uint64_t)hi << 32) | lo) & lenm;
-    };
-    uint64_t sg = seg(bmi);
-    int c = __popcll(sg);
-    int ic = wave_incl_scan(c);
-    int tot = __builtin_amdgcn_readlane(ic, 63);
-    if (tot == 0) {  // wave-uniform: the cell's minThFAST survivors
-      sg = seg(bmm);
-      c = __popcll(sg);
-      ic = wave_incl_scan(c);
-      tot = __builtin_amdgcn_readlane(ic, 63);
-    }
-    uint32_t* out = B.cand + (size_t)img * G->cand_total + cc.cand_off;
-    int oo = ic - c;
-    while (sg) {
-      const int b = __builtin_ctzll(sg);
-      const int cx = cx0 + b;
-      if (oo < cc.cap)
-        out[oo] = ((uint32_t)(tile[r * kTS + cx] - 1) << 24) | ((uint32_t)(s.y0 + r) << 12) | (uint32_t)(s.xs + cx);
-      oo++;
-      sg &= sg - 1;
-    }
-    if (lane == 0) {
-      B.cell_count[(size_t)img * G->ncells + cell] = min(tot, cc.cap);
-      B.fast_fb[(size_t)img * G->ncells + cell] = 0;
-    }
-  }
 }
 
 // ----------------------------------------------------------------- octree
@@ -2025,13 +1715,8 @@ hipError_t upload_constants(const int* umax16, const int* gauss7) {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_gauss), gauss7, 7 * sizeof(int));
 }
 
-// k_fast<80, 1, true>'s LDS: window tile, score map and compass list of the widest cell
-inline size_t fast_fb_smem() {
-  return (size_t)(((kMaxCell + 6) * 80 + 15) & ~15) + (((kMaxCell + 2) * 80 + 15) & ~15) + 2 * kMaxCell * kMaxCell;
-}
-
 hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const CellInfo* cells,
-                                 const FastStrip* strips, const int* tile_level, const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B,
+                                 const int* tile_level, const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B,
                                  int n_img, orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap,
                                  hipStream_t st, StageTimer* T) {
   for (int l = 1; l < Gh.nlevels; l++) {
@@ -2040,16 +1725,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
     hipLaunchKernelGGL(k_resize, grid, dim3(BS), (size_t)Gh.rz_rows * (Gh.rz_stride + 2 * kRzTW), st, Gd, xt, yt, B, l);
     T->end(ST_RESIZE, st);
   }
-  if (Gh.ncells > 0 && ORBX_FAST_STRIP) {
-    T->begin(st);
-    for (int g = 0; g < Gh.n_sg; g++) {
-      const Geometry::StripGroup& SG = Gh.sg[g];
-      if (SG.n > 0)
-        hipLaunchKernelGGL(k_fast_strip, dim3(SG.n, n_img), dim3(kStripNT), SG.smem, st, Gd, cells, strips, SG.s0, B);
-    }
-    hipLaunchKernelGGL((k_fast<80, 1, true>), dim3(kFastFbBlocks, n_img), dim3(64), fast_fb_smem(), st, Gd, cells, B, 0);
-    T->end(ST_FAST, st);
-  } else if (Gh.ncells > 0) {
+  if (Gh.ncells > 0) {
     T->begin(st);
     for (int g = 0; g < Gh.n_fg; g++) {
       const Geometry::FastGroup& F = Gh.fg[g];

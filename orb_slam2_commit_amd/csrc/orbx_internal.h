@@ -69,13 +69,6 @@ struct Geometry {
     int c0, c1, s, rp, tile_bytes, map_bytes, smem;
   } fg[2];
   int n_fg;
-  int n_strips;     // k_fast strips (FastStrip table)
-  // k_fast_strip launch groups: strips [s0, s0 + n) with the LDS of their tallest strip (the short
-  // strips of most levels apart from the few taller ones, so more blocks fit a CU)
-  struct StripGroup {
-    int s0, n, smem;
-  } sg[2];
-  int n_sg;
   int rz_rows;    // k_resize: max source rows staged per 128x16 output tile
   int rz_stride;  // k_resize: LDS row stride of the staged footprint (16-B chunks covering the widest span)
   int rz_lc;      // k_resize: log2 of the lanes per footprint row (>= the widest span's 16-B chunks)
@@ -92,25 +85,6 @@ struct CellInfo {
                  // k_fast finds its window from this one record, no dependent geometry load
   int pad2;
 };
-
-// k_fast strip: up to 8 consecutive FAST cells of one cell row of one level (their detection regions
-// partition the strip's region columns; all share the region rows)
-struct FastStrip {
-  int16_t level, ncell;  // cells cell0 .. cell0 + ncell - 1
-  int16_t y0, h;         // region rows y0 .. y0 + h - 1 (level coordinates)
-  int16_t xs, wcell;     // window's first column (= the first cell's x0 - 3); cell width (all but the last)
-  int16_t cxl, pad;      // last region column, strip coordinates (x - xs)
-  int cell0;
-  int lw, lh, loff;      // the level's width, height and offset in an image's pyramid block (level > 0)
-};
-
-constexpr int kStripCap = 3072;    // k_fast strip kernel: compass survivors of a strip held in LDS
-constexpr int kFastFbBlocks = 16;  // k_fast worklist pass: blocks per image
-// its LDS: the (H + 6) x 272-B window (the score map overlays it), the survivor list (u16 position +
-// u8 score), two H x 256-bit NMS survivor bitmaps
-__host__ __device__ inline size_t fast_strip_smem_bytes(int hmax) {
-  return (size_t)(hmax + 6) * 272 + (size_t)kStripCap * 3 + (size_t)2 * hmax * 32;
-}
 
 struct ResizeX {  // horizontal tap of one output column
   int sx0, sx1;
@@ -136,7 +110,6 @@ struct BatchPtrs {
   uint8_t* blur;
   uint32_t* cand;
   int* cell_count;
-  int* fast_fb;     // k_fast worklist: per image and cell, 0 = done by k_fast_strip, 1 + mode = k_fast<.., true>
   uint32_t* kpos;   // octree scratch
   int* knode;
   uint32_t* oct;
