@@ -901,7 +901,9 @@ def main():
     L.orbx_debug_copy(ex._h, 2, 0, 0, _lib.ptr(cc), cc.nbytes)
     cand_per_img = float(cc.sum())  # noqa: F841 -- FAST survivors (reported)
     P = [w * h for (w, h) in level_sizes(W, H, ex.GetInverseScaleFactors())]
-    dom = max(stages, key=lambda k: stages[k][0]) if stages else None
+    # the dominant stage among those with SURVEY 8(d) bytes (k_octree has none; the three stereo
+    # kernels are one stage, charged B_st together with their summed time)
+    dom = None
     traffic_all, traffic_src = {}, None
     if os.path.exists(args.traffic):
         try:
@@ -950,16 +952,21 @@ def main():
         tr = sum(traffic_all.get(k, 0) for k in st_k) or None
         stage_hbm["stereo"] = stage_entry("stereo", ev_s, 1, rp, tr)
         stage_hbm["stereo"]["kernels"] = {k: round(stages[k][0] / stages[k][1], 4) for k in st_k}
+    cands = {k: v for k, v in stage_hbm.items() if v.get("s8d_bytes_per_event")}
+    if cands:
+        dom = max(cands, key=lambda k: cands[k]["ms_per_step"])
+        if dom == "stereo":
+            stages = dict(stages, stereo=(sum(stages[k][0] / stages[k][1] for k in st_k), 1))
     roofline = None
     if dom:
         ms_tot, nl = stages[dom]
         avg_s = ms_tot / nl / 1e3
-        ent = stage_hbm.get(dom) or stage_hbm.get("stereo")
+        ent = stage_hbm[dom]
         nbytes = ent["s8d_bytes_per_event"]
         achieved = nbytes / avg_s / 1e9
         roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 5), frac_rocprof=ent.get("frac_rocprof"),
-                        traffic=traffic_all.get(dom), traffic_source=traffic_src, rocprof_source=rp_src,
+                        traffic=ent.get("traffic_per_event"), traffic_source=traffic_src, rocprof_source=rp_src,
                         algorithmic_bytes_per_launch=int(nbytes), avg_launch_ms=round(avg_s * 1e3, 4),
                         bytes_definition="SURVEY 8(d) terms of this kernel only, per timer event over the batch "
                                          "(k_fast: sum(P) per image; no intermediates)")

@@ -462,6 +462,12 @@ typedef struct {
   float log_scale_factor;          /* mfLogScaleFactor */
   float fx, fy, cx, cy, bf, b;     /* fx, fy, cx, cy, mbf, mb */
   float Tcw[16];                   /* mTcw, row-major 4x4 */
+  /* the bounds the feature grid was built with, when they differ from min_x / min_y: a KeyFrame keeps
+   * integer mnMinX / mnMinY (include/KeyFrame.h, GetFeaturesInArea's cell range, IsInImage) while its
+   * mGrid is the Frame's, built from the float Frame::mnMinX / mnMinY (src/Frame.cc:388-395 PosInGrid);
+   * grid_min_set = 0: the grid uses min_x / min_y */
+  float grid_min_x, grid_min_y;
+  int grid_min_set;
 } orbx_proj_frame;
 
 typedef struct {
@@ -626,8 +632,8 @@ orbx_status orbx_pose_optimization_device(const orbx_pose_problem* problems, int
 /* Tracking::TrackReferenceKeyFrame's gather (src/Tracking.cc:910-969) between SearchByBoW(KF, F)
  * and PoseOptimization(&F), on a device batch: PoseOptimization's edge per current-frame feature
  * with a MapPoint, in feature order (src/Optimizer.cc:318-410).  The reference KeyFrame's MapPoints
- * are its stereo points as StereoInitialization / CreateNewKeyFrame create them
- * (src/Tracking.cc:640-668, 1515-1555): feature k has one iff kf_depth[k] > 0, at
+ * are its stereo points as StereoInitialization creates them (src/Tracking.cc:590-668): feature k has
+ * one iff kf_depth[k] > 0, at
  * Frame::UnprojectStereo(k) (src/Frame.cc:823-839: mvKeysUn[k], mRwc*x3Dc+mOw -- cv::gemm with the
  * addend on OpenCV 3.2's small-matrix path: the dot product in float, then a float add) with pose Twc.
  * (KeyFrame::UnprojectStereo, src/KeyFrame.cc:758-780, reads mvKeys instead; the two agree whenever
@@ -651,8 +657,10 @@ typedef struct {
 } orbx_track_gather;
 orbx_status orbx_track_gather_device(const orbx_track_gather* problems, int n, void* stream);
 
-/* The MapPoints a stereo frame creates (StereoInitialization / CreateNewKeyFrame, src/Tracking.cc:640-668,
- * 1515-1555: one per feature with mvDepth > 0) as the SoA a SearchByProjection problem takes, for the
+/* The MapPoints StereoInitialization creates (src/Tracking.cc:590-668: one per feature with mvDepth > 0;
+ * CreateNewKeyFrame, :1311-1401, and UpdateLastFrame, :971-1040, instead stop at the first point past
+ * mThDepth once more than 100 exist, so this models an initial keyframe as the last frame) as the SoA
+ * a SearchByProjection problem takes, for the
  * frame's features 0..N-1 (point i = feature i, the frame's descriptors are the points' descriptors):
  *   pos      Frame::UnprojectStereo(i) (src/Frame.cc:823-839) with pose Twc
  *   normal, dist_minmax  MapPoint::UpdateNormalAndDepth with the one observation (src/MapPoint.cc

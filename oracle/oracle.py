@@ -44,7 +44,8 @@ class ProjFrame(C.Structure):
                                                                  "grid_inv_h")] + \
                [("nlevels", C.c_int), ("scale_factors", C.c_float * 16), ("inv_level_sigma2", C.c_float * 16)] + \
                [(k, C.c_float) for k in ("log_scale_factor", "fx", "fy", "cx", "cy", "bf", "b")] + \
-               [("Tcw", C.c_float * 16)]
+               [("Tcw", C.c_float * 16), ("grid_min_x", C.c_float), ("grid_min_y", C.c_float),
+                ("grid_min_set", C.c_int)]
 
 
 class ProjProblem(C.Structure):
@@ -478,6 +479,8 @@ def _proj_frame(fr):
     for k in ("min_x", "max_x", "min_y", "max_y", "grid_inv_w", "grid_inv_h", "log_scale_factor", "fx", "fy", "cx",
               "cy", "bf", "b"):
         setattr(f, k, float(fr[k]))
+    if fr.get("grid_min_x") is not None:
+        f.grid_min_x, f.grid_min_y, f.grid_min_set = float(fr["grid_min_x"]), float(fr["grid_min_y"]), 1
     f.nlevels = int(fr["nlevels"])
     isg = fr.get("inv_level_sigma2")
     for i in range(f.nlevels):

@@ -175,6 +175,9 @@ typedef struct {
   float log_scale_factor;
   float fx, fy, cx, cy, bf, b;
   float Tcw[16];
+  float grid_min_x, grid_min_y;  /* the grid's bounds when grid_min_set (a KeyFrame: the Frame's float
+                                    mnMinX/mnMinY, while min_x/min_y are its integer copies) */
+  int grid_min_set;
 } oracle_proj_frame;
 
 typedef struct {

@@ -122,8 +122,11 @@ struct Frame {
   explicit Frame(const oracle_proj_frame& f) : F(f) {
     for (int i = 0; i < F.n; i++) {  // AssignFeaturesToGrid
       const oracle_keypoint& kp = F.keys_un[i];
-      const int px = (int)std::round((kp.x - F.min_x) * F.grid_inv_w);
-      const int py = (int)std::round((kp.y - F.min_y) * F.grid_inv_h);
+      // PosInGrid (src/Frame.cc:388-395) with the bounds the grid was built with: a KeyFrame's mGrid is
+      // its Frame's (float mnMinX/mnMinY), GetFeaturesInArea below uses the KeyFrame's integer copies
+      const float gx0 = F.grid_min_set ? F.grid_min_x : F.min_x, gy0 = F.grid_min_set ? F.grid_min_y : F.min_y;
+      const int px = (int)std::round((kp.x - gx0) * F.grid_inv_w);
+      const int py = (int)std::round((kp.y - gy0) * F.grid_inv_h);
       if (px < 0 || px >= kCols || py < 0 || py >= kRows) continue;
       grid[px][py].push_back(i);
     }

@@ -80,7 +80,8 @@ class ProjFrame(C.Structure):
                 ("scale_factors", C.c_float * 16), ("inv_level_sigma2", C.c_float * 16),
                 ("log_scale_factor", C.c_float), ("fx", C.c_float),
                 ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float), ("b", C.c_float),
-                ("Tcw", C.c_float * 16)]
+                ("Tcw", C.c_float * 16), ("grid_min_x", C.c_float), ("grid_min_y", C.c_float),
+                ("grid_min_set", C.c_int)]
 
 
 class ProjProblem(C.Structure):

@@ -306,8 +306,8 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
     uint32_t key = 0xFFFFFFFFu;
     if (i < nF) {
       const orbx_keypoint kp = F.keys_un[i];
-      const int px = (int)__builtin_roundf((kp.x - F.min_x) * F.grid_inv_w);
-      const int py = (int)__builtin_roundf((kp.y - F.min_y) * F.grid_inv_h);
+      const int px = (int)__builtin_roundf((kp.x - (F.grid_min_set ? F.grid_min_x : F.min_x)) * F.grid_inv_w);
+      const int py = (int)__builtin_roundf((kp.y - (F.grid_min_set ? F.grid_min_y : F.min_y)) * F.grid_inv_h);
       if (px >= 0 && px < ORBX_GRID_COLS && py >= 0 && py < ORBX_GRID_ROWS)
         key = ((uint32_t)(px * ORBX_GRID_ROWS + py) << 13) | (uint32_t)i;
     }
@@ -630,8 +630,8 @@ __global__ __launch_bounds__(IBS) void k_search_for_initialization(const orbx_in
     uint32_t key = 0xFFFFFFFFu;
     if (i < n2) {
       const orbx_keypoint kp = F2.keys_un[i];
-      const int px = (int)__builtin_roundf((kp.x - F2.min_x) * F2.grid_inv_w);
-      const int py = (int)__builtin_roundf((kp.y - F2.min_y) * F2.grid_inv_h);
+      const int px = (int)__builtin_roundf((kp.x - (F2.grid_min_set ? F2.grid_min_x : F2.min_x)) * F2.grid_inv_w);
+      const int py = (int)__builtin_roundf((kp.y - (F2.grid_min_set ? F2.grid_min_y : F2.min_y)) * F2.grid_inv_h);
       if (kp.octave == 0 && px >= 0 && px < ORBX_GRID_COLS && py >= 0 && py < ORBX_GRID_ROWS)
         key = ((uint32_t)(px * ORBX_GRID_ROWS + py) << 13) | (uint32_t)i;
     }

@@ -425,6 +425,8 @@ def proj_problem(frame, points, kind, th, nnratio=0.6, check_ori=True, mono=Fals
     for k in ("min_x", "max_x", "min_y", "max_y", "grid_inv_w", "grid_inv_h", "log_scale_factor", "fx", "fy",
               "cx", "cy", "bf", "b"):
         setattr(f, k, float(frame[k]))
+    if frame.get("grid_min_x") is not None:  # a KeyFrame's grid: the Frame's float bounds
+        f.grid_min_x, f.grid_min_y, f.grid_min_set = float(frame["grid_min_x"]), float(frame["grid_min_y"]), 1
     f.nlevels = int(frame["nlevels"])
     sf = np.zeros(16, np.float32)
     sf[:f.nlevels] = frame["scale_factors"][:f.nlevels]

@@ -371,7 +371,10 @@ class MotionTrackBatch:
         if timings is not None:  # GPU time per phase: search (last frame), gather+pose 1, local search, pose 2
             timings.append((ev[0].elapsed_time(ev[1]) / 1e3, ev[1].elapsed_time(ev[3]) / 1e3,
                             ev[3].elapsed_time(ev[4]) / 1e3, ev[4].elapsed_time(ev[5]) / 1e3))
-        return dict(nmatches=res[0], ngood_motion=res[1], lost=res[2], local_matches=res[3], inliers=res[4])
+        # a lost frame skipped the local search (its gate), so its nm2 slot still holds an older call's
+        # count: report 0 for it, as the reference never runs TrackLocalMap on it
+        local = np.where(res[2] != 0, 0, res[3])
+        return dict(nmatches=res[0], ngood_motion=res[1], lost=res[2], local_matches=local, inliers=res[4])
 
 
 def log_scale_factor(scale_factor):

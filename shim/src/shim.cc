@@ -617,6 +617,11 @@ orbx_proj_frame fuse_frame(KeyFrame* pKF, cv::Mat& desc) {
   f.max_y = (float)pKF->mnMaxY;
   f.grid_inv_w = pKF->mfGridElementWidthInv;
   f.grid_inv_h = pKF->mfGridElementHeightInv;
+  // mGrid came from the Frame (KeyFrame.cc constructor), built with the float Frame::mnMinX/mnMinY;
+  // the KeyFrame's own (integer) copies above give GetFeaturesInArea's cell range and IsInImage
+  f.grid_min_x = Frame::mnMinX;
+  f.grid_min_y = Frame::mnMinY;
+  f.grid_min_set = 1;
   set_levels(f, pKF->mnScaleLevels, pKF->mvScaleFactors, pKF->mvInvLevelSigma2);
   f.log_scale_factor = pKF->mfLogScaleFactor;
   f.fx = pKF->fx;

@@ -75,8 +75,11 @@ class PyFrame:
         self.grid = [[[] for _ in range(48)] for _ in range(64)]
         for i in range(len(k)):
             # PosInGrid's round() is half-away-from-zero
-            vx = float(f32(f32(k["x"][i] - fr["min_x"]) * fr["grid_inv_w"]))
-            vy = float(f32(f32(k["y"][i] - fr["min_y"]) * fr["grid_inv_h"]))
+            # a KeyFrame's grid is its Frame's, built with the float bounds (grid_min_*); its
+            # GetFeaturesInArea below uses the KeyFrame's integer copies (min_x / min_y)
+            gx0, gy0 = fr.get("grid_min_x", fr["min_x"]), fr.get("grid_min_y", fr["min_y"])
+            vx = float(f32(f32(k["x"][i] - f32(gx0)) * fr["grid_inv_w"]))
+            vy = float(f32(f32(k["y"][i] - f32(gy0)) * fr["grid_inv_h"]))
             px = int(math.floor(abs(vx) + 0.5)) * (1 if vx >= 0 else -1)
             py = int(math.floor(abs(vy) + 0.5)) * (1 if vy >= 0 else -1)
             if 0 <= px < 64 and 0 <= py < 48:
@@ -412,6 +415,18 @@ def _kw(kind, fr, variant=0):
             dict(th=3.0, orb_dist=50)][variant % 4]
 
 
+def _kf_frame(fr):
+    """fr as a KeyFrame of an undistorted camera: the Frame's bounds are fractional (float statics,
+    ComputeImageBounds), the KeyFrame keeps them as ints (include/KeyFrame.h: const int mnMinX ..), and
+    its mGrid is the Frame's, built from the float bounds with the float cell inverses."""
+    gx0, gy0 = np.float32(fr["min_x"] - 1.63), np.float32(fr["min_y"] + 0.71)
+    gx1, gy1 = np.float32(fr["max_x"] + 0.38), np.float32(fr["max_y"] - 0.47)
+    return dict(fr, grid_min_x=gx0, grid_min_y=gy0, min_x=float(int(gx0)), min_y=float(int(gy0)),
+                max_x=float(int(gx1)), max_y=float(int(gy1)),
+                grid_inv_w=np.float32(np.float32(64) / np.float32(gx1 - gx0)),
+                grid_inv_h=np.float32(np.float32(48) / np.float32(gy1 - gy0)))
+
+
 def _same(a, b, kind, frustum=False):
     assert a["nmatches"] == b["nmatches"], (a["nmatches"], b["nmatches"])
     assert np.array_equal(a["point_match"], b["point_match"])
@@ -437,6 +452,28 @@ def test_oracle_vs_python_restatement(kind, variant):
     ref = py_search(fr, pts, kind, limit=limit, **pk)
     _same(got, ref, kind, kw.get("frustum", False))
     assert got["nmatches"] > 0
+
+
+@pytest.mark.parametrize("kind", [3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 3])
+def test_oracle_keyframe_grid_bounds(kind, variant):
+    """KeyFrame problems (Fuse, the Sim3 projections) on a distorted camera: the grid from the Frame's
+    float bounds, the search window and IsInImage from the KeyFrame's integer bounds."""
+    fr = _kf_frame(synth.projection_frame(30 + variant, n=400, width=300, height=200))
+    pts = synth.projection_points(40 + variant, fr, min(kind, 3), n_points=250, pool=0.3)
+    if kind >= 4:
+        fr = _sim3(fr, variant)
+    kw = _kw(kind, fr, variant)
+    got = oracle.search_by_projection(fr, pts, kind, **kw)
+    pk = dict(kw)
+    limit = pk.pop("view_cos_limit", 0.5)
+    _same(got, py_search(fr, pts, kind, limit=limit, **pk), kind)
+    assert got["nmatches"] > 0
+    # the grid bounds matter: the same frame with the grid built from the integer bounds enumerates
+    # some features from other cells
+    g0 = PyFrame(fr).grid
+    g1 = PyFrame({k: v for k, v in fr.items() if not k.startswith("grid_min")}).grid
+    assert g0 != g1
 
 
 def test_features_in_area_vs_bruteforce():
@@ -530,6 +567,19 @@ def test_gpu_projection_kitti(gpu, kind, variant):
     ref = oracle.search_by_projection(fr, pts, kind, **kw)
     got = _gpu(fr, pts, kind, **dict(kw))
     _same(got, ref, kind, kw.get("frustum", False))
+    assert ref["nmatches"] > 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [3, 4, 5])
+def test_gpu_projection_keyframe_grid_bounds(gpu, kind):
+    fr = _kf_frame(synth.projection_frame(140 + kind, n=2000))
+    pts = synth.projection_points(240 + kind, fr, min(kind, 3), n_points=3000)
+    if kind >= 4:
+        fr = _sim3(fr, 1)
+    kw = _kw(kind, fr, 0)
+    ref = oracle.search_by_projection(fr, pts, kind, **kw)
+    _same(_gpu(fr, pts, kind, **dict(kw)), ref, kind)
     assert ref["nmatches"] > 100
 
 
