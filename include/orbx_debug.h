@@ -32,21 +32,16 @@ int orbx_debug_ldlt(const double* S, const double* b, int N, double* x, int reps
 int orbx_debug_ldlt_ex(const double* S, const double* b, int N, double* x, int reps, float* ms, int kind,
                        unsigned long long* stamps);
 
-/* LocalBA test / A-B options of one solver handle (tests and tools only; a production caller never
- * sets them: the default, all zero with nan_trial = raise_stop_after = -1, is the shipped behaviour).
- * Every setting keeps the results bit-identical except the two hooks, which reproduce rare events
- * deterministically: nan_trial (the chi2 of that trial of each phase reads NaN, the reference's
- * rho-NaN rejection) and raise_stop_after (the stop flag reads raised after that many trials). */
+/* LocalBA test options of one solver handle (tests and tools only; a production caller never sets
+ * them: ldlt = AUTO with nan_trial = raise_stop_after = -1 is the shipped behaviour).  ldlt forces
+ * one of the reduced-system kernels the library ships for other sizes (so each is tested at every
+ * size it can take); the two hooks reproduce rare events deterministically: nan_trial (the chi2 of
+ * that trial of each phase reads NaN, the reference's rho-NaN rejection) and raise_stop_after (the
+ * stop flag reads raised after that many trials). */
 #define ORBX_BA_LDLT_AUTO 0    /* 8-wide panels (N < 128), column-step (N <= 192), blocked MFMA beyond */
 #define ORBX_BA_LDLT_COLUMN 1  /* the column-step kernel wherever it fits */
 #define ORBX_BA_LDLT_BLOCKED 2 /* the blocked MFMA kernel */
 typedef struct {
-  int host_lm;          /* the host-controlled LM loop instead of k_ba_lm_control */
-  int no_spec;          /* host loop: no speculative linearisation */
-  int host_struct;      /* the per-phase edge structure built on the host */
-  int no_fuse;          /* k_ba_linearize / point_sum / point_schur instead of k_ba_lin_schur */
-  int no_camfold;       /* k_ba_cam_sum / cam_fin launched, not folded into k_ba_pairs / schur_fin */
-  int no_psfold;        /* k_ba_point_schur launched on the trials that do not relinearise */
   int ldlt;             /* ORBX_BA_LDLT_* */
   int nan_trial;        /* -1 off */
   int raise_stop_after; /* -1 off */

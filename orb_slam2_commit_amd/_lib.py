@@ -154,9 +154,7 @@ class TrackGather(C.Structure):
 
 
 class BaDebugOptions(C.Structure):  # include/orbx_debug.h orbx_ba_debug_options
-    _fields_ = [("host_lm", C.c_int), ("no_spec", C.c_int), ("host_struct", C.c_int), ("no_fuse", C.c_int),
-                ("no_camfold", C.c_int), ("no_psfold", C.c_int), ("ldlt", C.c_int), ("nan_trial", C.c_int),
-                ("raise_stop_after", C.c_int), ("trace", C.c_int)]
+    _fields_ = [("ldlt", C.c_int), ("nan_trial", C.c_int), ("raise_stop_after", C.c_int), ("trace", C.c_int)]
 
 
 class Camera(C.Structure):

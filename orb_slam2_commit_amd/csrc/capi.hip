@@ -522,7 +522,7 @@ orbx_status ensure_batch(orbx_extractor* h, const Plan& P, int n) {
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
   chk(h->pyr.ensure((size_t)G.pyr_bytes * n + 256));
-  if (!ORBX_DESC_FUSED) chk(h->blur.ensure((size_t)G.blur_bytes * n + 256));
+  chk(h->blur.ensure((size_t)G.blur_bytes * n + 256));
   chk(h->cand.ensure((size_t)G.cand_total * n));
   chk(h->kpos.ensure((size_t)G.cand_total * n));
   chk(h->knode.ensure((size_t)G.cand_total * n));
@@ -1055,9 +1055,8 @@ extern "C" long long orbx_debug_copy(orbx_extractor* h, int what, int image, int
       const LevelGeom& L = G.lv[arg];
       bytes = (size_t)L.w * L.h;
       if (dst && cap >= bytes) {
-        // with ORBX_DESC_FUSED the extraction blurs only each keypoint's patch (k_describe): the
-        // whole blurred levels of the last batch are made here, on demand, from its pyramid (without
-        // it they exist already; re-blurring the same pyramid rewrites the same bytes)
+        // the blurred levels of the last batch, re-blurred from its pyramid (the same bytes k_blur
+        // wrote; the batch that follows may have reused the buffer)
         if (h->blur.ensure((size_t)G.blur_bytes * h->last_n + 256) != hipSuccess) return ORBX_ERR_HIP;
         const BatchPtrs B = batch_ptrs(h, h->last_in, h->last_pitch);
         if (launch_blur(G, P.dG.p, P.dtiles.p, B, h->last_n, h->stream) != hipSuccess ||

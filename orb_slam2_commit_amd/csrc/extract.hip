@@ -7,8 +7,7 @@
 //   k_octree                 DistributeOctTree         src/ORBextractor.cc:562-815
 //   k_describe               IC_Angle + rBRIEF on the blurred level + scale
 //                                                      src/ORBextractor.cc:77-152,1186-1207
-//   k_blur                   whole-level GaussianBlur 7x7 s=2 (ORBX_DESC_FUSED=1: not launched,
-//                            k_describe blurs each keypoint's patch; ORBX_DBG_BLUR_LEVEL makes it)
+//   k_blur                   whole-level GaussianBlur 7x7 s=2 into 8 x 16-B tiles (k_describe samples them)
 //
 // Integer/byte work throughout (HBM-bound); the only float math is the
 // orientation/rotation and it is compiled without FP contraction so it rounds
@@ -1306,24 +1305,14 @@ constexpr int kPatchR = 18;
 constexpr int kPatchRows = 2 * kPatchR + 1;  // 37
 constexpr int kPS = 80;  // LDS row stride of the staged patches (bytes): 20 dwords, so the rotated
                          // samples' rows spread over the banks (a 64-B stride folds every 4th row)
-// the raw patch the blur of that patch reads: rows y-21..y+21, 16-B chunks from the 16-aligned
-// column xs = (x - 21) & ~15 (x - 21 - xs <= 15, + 43 bytes <= 58: four chunks per row)
-constexpr int kRawR = kPatchR + 3;           // 21
-constexpr int kRawRows = 2 * kRawR + 1;      // 43
-constexpr int kRawCh = 4;
-constexpr int kRawIt = (kRawRows * kRawCh + 63) / 64;  // 3 chunks per lane
-// bytes per wave: (raw patch +) blurred patch + the descriptor words
-constexpr int kDescLds = (ORBX_DESC_FUSED ? kRawRows + kPatchRows : kPatchRows) * kPS + 256;
-constexpr int kPatchIt = (kPatchRows * kRawCh + 63) / 64;  // blurred-level patch: 3 chunks per lane
+// bytes per wave: the blurred patch + the descriptor words
+constexpr int kDescLds = kPatchRows * kPS + 256;
 // half-width hw(r) of patch row r = 0..36 (row offset r - 18) the rotated pattern can reach
 // describe patch slots: slot s -> (row << 2 | k-th chunk of the row's span), 2 / 3 / 4 slots per row
 // (the most 16-B chunks the row's span covers over the 16 alignments), 124 slots, 0xFF past them
 __constant__ uint8_t c_patch_slot[128] = {0,1,4,5,8,9,10,12,13,14,16,17,18,20,21,22,24,25,26,28,29,30,32,33,34,36,37,38,40,41,42,43,44,45,46,47,48,49,50,51,52,53,54,55,56,57,58,59,60,61,62,63,64,65,66,67,68,69,70,71,72,73,74,75,76,77,78,79,80,81,82,83,84,85,86,87,88,89,90,91,92,93,94,95,96,97,98,99,100,101,102,103,104,105,106,107,108,109,110,112,113,114,116,117,118,120,121,122,124,125,126,128,129,130,132,133,134,136,137,138,140,141,144,145,255,255,255,255};
 __constant__ int c_patch_hw[kPatchRows] = {6,  8,  10, 11, 12, 13, 14, 15, 16, 16, 17, 17, 18, 18, 18, 18, 18, 18, 18,
                                            18, 18, 18, 18, 18, 18, 17, 17, 16, 16, 15, 14, 13, 12, 11, 10, 8,  6};
-// blur work split: lane = (column pair g < 19, row strip s < 3 of 13 / 13 / 11 output rows)
-constexpr int kBlurPairs = (kPatchRows + 1) / 2;  // 19
-constexpr int kBlurStrip = 13;
 
 #ifndef ORBX_DESC_K
 #define ORBX_DESC_K 8
@@ -1349,25 +1338,18 @@ __device__ __forceinline__ float lane_f(float v, int j) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
 }
 
-// k_describe: IC_Angle (src/ORBextractor.cc:77-105), the level's GaussianBlur (:1186-1190)
-// restricted to each keypoint's 37 x 37 sampling patch, computeOrbDescriptor (:110-152) and the
-// keypoint record in level-major output order with pt *= mvScaleFactor[l] (:1201-1207).
-//
-// The blurred level is never materialised: every blurred pixel the 256 rotated pairs can touch
-// lies in the patch, and GaussianBlur's output at a pixel depends only on the 7 x 7 raw pixels
-// around it (REFLECT_101 at the level border), so blurring the 43 x 43 raw neighbourhood in LDS
-// gives the same bytes as blurring the level and reading them back -- without the level-sized
-// write and the two level-sized reads (1.5 + 0.7 GB per 256-frame step).
+// k_describe: IC_Angle (src/ORBextractor.cc:77-105), computeOrbDescriptor (:110-152) on the blurred
+// level k_blur wrote (:1186-1190), and the keypoint record in level-major output order with
+// pt *= mvScaleFactor[l] (:1201-1207).
 //
 // kDescK keypoints per wave (consecutive output indices):
 //   1. lane j finds keypoint i0 + j's level and loads its octree entry and level record;
-//   2. the IC_Angle boxes of all kDescK keypoints and the raw patches of the first two are issued
-//      together; the moments are wave sums per keypoint (v_dot4 on circle-masked 16-B rows);
+//   2. the IC_Angle boxes of all kDescK keypoints and the blurred patches of the first two are
+//      issued together; the moments are wave sums per keypoint (v_dot4 on circle-masked 16-B rows);
 //   3. fastAtan2 and the deterministic sin/cos run once, lane j for keypoint j;
-//   4. per keypoint: raw patch -> LDS (reflected border columns patched), the patch two ahead
-//      issued, the 37 x 37 blur (exact integer row sums by v_dot4, packed-f32 column taps, the
-//      SSE2 / scalar-tail rounding of the output column) -> LDS, then the 256 rotated pairs with
-//      pair p in lane p & 63: ballot k = descriptor bits 64k .. 64k+63, staged in LDS;
+//   4. per keypoint: the blurred patch (only the pixels a rotated pair can reach) -> LDS, the patch
+//      two ahead issued, then the 256 rotated pairs with pair p in lane p & 63: ballot k =
+//      descriptor bits 64k .. 64k+63, staged in LDS;
 //   5. one coalesced store of the kDescK descriptors (lane = dword) and the keypoint records.
 __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G, BatchPtrs B,
                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
@@ -1413,7 +1395,7 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   // IC box origin (x - 15, y - 15); keypoints sit >= 19 px inside the level, so the box is too
   const uint8_t* icp = lvl + (size_t)(y - 15) * w + (x - 15);
 
-  // 2. IC boxes of every keypoint, then the first two raw patches
+  // 2. IC boxes of every keypoint, then the first two blurred patches
   const int r = lane >> 1, hh = lane & 1;
   uint32_t q[kDescK][4];
 #pragma unroll
@@ -1428,19 +1410,13 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
     q[j][2] = t[2];
     q[j][3] = t[3];
   }
-  // raw patch of keypoint j: lane chunk c = lane + 64k is (row c >> 2, 16-B column block c & 3);
-  // rows reflected (REFLECT_101), columns outside the level patched in LDS afterwards
-  static_assert(kRawIt == kPatchIt, "one register set for both patch forms");
-  constexpr int kPatchLd = ORBX_DESC_FUSED ? kRawIt : 2;  // 16-B loads per lane per patch
-#if !ORBX_DESC_FUSED
+  constexpr int kPatchLd = 2;  // 16-B loads per lane per patch
   // the blurred level's patch: rows y-18..y+18, 16-B chunks from the 16-aligned column x0
   const int bs = L.bstride;
   const int x0 = (x - kPatchR) & ~15;
   const uint8_t* pbl = B.blur + (size_t)img * G->blur_bytes + L.boff;  // the level's tiles
   constexpr int PS = kPS;
   const uint32_t corr_l = (uint32_t)(kPatchR * PS + (x - x0)) - (0x400000u * (uint32_t)PS + 0x4B400000u);
-#endif
-#if !ORBX_DESC_FUSED
   // Only the blurred pixels a rotated pattern point can land on are loaded: a point of radius rho
   // rounds to (r, c) with (|r| - 1/2)^2 + (|c| - 1/2)^2 <= rho^2 <= 338 (the pattern's largest
   // rho^2), so row r needs |c| <= hw(r) (c_patch_hw; equal to the brute-force reach of the pattern
@@ -1456,11 +1432,9 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
     skk[k] = e & 3;
     shw[k] = c_patch_hw[e == 0xFF ? 0 : e >> 2];
   }
-#endif
   uint32_t pv[2][kPatchLd][4];
   int pdst[2][kPatchLd];  // LDS byte offset of each loaded chunk (-1: none)
   auto load_patch = [&](int j, uint32_t (&dst)[kPatchLd][4], int (&dofs)[kPatchLd]) {
-#if !ORBX_DESC_FUSED
     const int bt8 = __builtin_amdgcn_readlane(bs, j) * 8, hj = __builtin_amdgcn_readlane(h, j);
     const int xj = __builtin_amdgcn_readlane(x, j), y0j = __builtin_amdgcn_readlane(y, j) - kPatchR;
     const int aj = (xj - kPatchR) & 15, tx0 = (xj - kPatchR) >> 4;
@@ -1482,34 +1456,6 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
       dst[k][2] = t[2];
       dst[k][3] = t[3];
     }
-#else
-    (void)dofs;
-    const int wj = __builtin_amdgcn_readlane(w, j), hj = __builtin_amdgcn_readlane(h, j);
-    const int xj = __builtin_amdgcn_readlane(x, j), yj = __builtin_amdgcn_readlane(y, j);
-    const int xs = (xj - kRawR) & ~15;
-    const int nrec = wj * hj;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)lane_ptr(lvl, j), (short)0, nrec, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < kRawIt; k++) {
-      const int c = lane + 64 * k, rr = c >> 2, cc = c & 3;
-      const int o = reflect101(yj - kRawR + rr, hj) * wj + xs + 16 * cc;  // may be < 0 in row 0
-      dst[k][0] = dst[k][1] = dst[k][2] = dst[k][3] = 0;
-      if (c < kRawRows * kRawCh) {
-        if (o + 16 <= nrec) {  // o < 0 wraps past num_records: zeros (only reflected columns)
-          const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)o, 0, 0);
-          dst[k][0] = t[0];
-          dst[k][1] = t[1];
-          dst[k][2] = t[2];
-          dst[k][3] = t[3];
-        } else {
-          // a chunk straddling the level's last byte: byte loads, each range-checked on its own
-#pragma unroll
-          for (int b = 0; b < 16; b++)
-            dst[k][b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(o + b), 0, 0) << (8 * (b & 3));
-        }
-      }
-    }
-#endif
   };
   load_patch(0, pv[0], pdst[0]);
   if (kDescK > 1) load_patch(1, pv[1], pdst[1]);
@@ -1542,27 +1488,10 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
   float sn, cs;
   sincos_det(angle * factorPI, c_sincos, &sn, &cs);
 
-  // blur constants (see k_blur): taps pre-shifted into the dot4 words, 2^-16-scaled column taps
-  const uint32_t k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
-  auto W4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) { return b0 | b1 << 8 | b2 << 16 | b3 << 24; };
-  const uint32_t wl0 = W4(k0, k1, k2, k3), wh0 = W4(k2, k1, k0, 0);  // output col 2g: bytes sb .. sb+6
-  const uint32_t wl1 = W4(0, k0, k1, k2), wh1 = W4(k3, k2, k1, k0);  // output col 2g+1: bytes sb+1 .. sb+7
-  const float f0 = (float)k0 * (1.f / 65536.f), f1 = (float)k1 * (1.f / 65536.f), f2 = (float)k2 * (1.f / 65536.f),
-              f3 = (float)k3 * (1.f / 65536.f);
-  const float2v F0 = {f0, f0}, F1 = {f1, f1}, F2 = {f2, f2}, F3 = {f3, f3};
-  const float2v two23 = {8388608.0f, 8388608.0f}, magic = {12582912.0f, 12582912.0f};
-  const int bg = lane % kBlurPairs, bst = lane / kBlurPairs;  // column pair, row strip (lanes < 57)
-  const bool blur_lane = lane < 3 * kBlurPairs;
+  const float2v magic = {12582912.0f, 12582912.0f};  // 1.5 * 2^23: round half to even
 
   // 4. per keypoint
-#if ORBX_DESC_FUSED
-  uint8_t* raw = s_desc[wv];
-  uint8_t* pb = s_desc[wv] + kRawRows * kPS;
-  constexpr uint32_t corr = (uint32_t)(kPatchR * kPS + kPatchR) - (0x400000u * (uint32_t)kPS + 0x4B400000u);
-#else
   uint8_t* pb = s_desc[wv];
-#endif
-  const float2v magic_s = {12582912.0f, 12582912.0f};
   // the descriptors' 64-bit words, staged per wave and stored by lane = dword at the end
   uint64_t* sdw = reinterpret_cast<uint64_t*>(s_desc[wv] + kDescLds - 256);
   static_for<kDescK>([&](auto jc) {
@@ -1570,84 +1499,11 @@ __global__ __launch_bounds__(BS) void k_describe(const Geometry* __restrict__ G,
     if (j >= nk) return;  // wave-uniform
     uint32_t (&cur)[kPatchLd][4] = pv[j & 1];
     int (&cdst)[kPatchLd] = pdst[j & 1];
-#if !ORBX_DESC_FUSED
 #pragma unroll
     for (int k = 0; k < kPatchLd; k++)
       if (cdst[k] >= 0) *(uint4*)(pb + cdst[k]) = make_uint4(cur[k][0], cur[k][1], cur[k][2], cur[k][3]);
     if (j + 2 < kDescK && j + 2 < nk) load_patch(j + 2, cur, cdst);
     const uint32_t corr = __builtin_amdgcn_readlane(corr_l, j);
-#else
-    const int wj = __builtin_amdgcn_readlane(w, j), xj = __builtin_amdgcn_readlane(x, j);
-    const int xs = (xj - kRawR) & ~15;
-#pragma unroll
-    for (int k = 0; k < kRawIt; k++) {
-      const int c = lane + 64 * k;
-      if (c < kRawRows * kRawCh)
-        *(uint4*)(raw + (c >> 2) * kPS + 16 * (c & 3)) = make_uint4(cur[k][0], cur[k][1], cur[k][2], cur[k][3]);
-    }
-    if (j + 2 < kDescK && j + 2 < nk) load_patch(j + 2, cur, cdst);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // columns outside the level (x - 21 < 0 or x + 21 >= w): REFLECT_101 copies of columns inside
-    // it (sources and targets disjoint, so one pass)
-    if (xj - kRawR < 0 || xj + kRawR >= wj) {
-      for (int e = lane; e < kRawRows * 4; e += 64) {
-        const int rr = e >> 2, k = e & 3;
-        const int col = k < 2 ? xj - kRawR + k : xj + kRawR - 1 + (k - 2);  // two per side
-        if (col < 0 || col >= wj) raw[rr * kPS + col - xs] = raw[rr * kPS + reflect101(col, wj) - xs];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    // the 37 x 37 blur: output (row ro, col cc) = level pixel (y - 18 + ro, x - 18 + cc), taps on
-    // raw rows ro .. ro+6 and raw bytes o + cc .. o + cc + 6 (o = x - 21 - xs)
-    if (blur_lane) {
-      const int o = xj - kRawR - xs;
-      const int sb = o + 2 * bg, sh = sb & 3;
-      const uint8_t* rb0 = raw + bst * kBlurStrip * kPS + (sb & ~3);
-      auto rowsum = [&](int t) -> float2v {
-        const uint32_t* r32 = (const uint32_t*)(rb0 + t * kPS);
-        const uint32_t a = r32[0], b = r32[1], c = r32[2];
-        const uint32_t lo = __builtin_amdgcn_alignbyte(b, a, sh), hi = __builtin_amdgcn_alignbyte(c, b, sh);
-        constexpr uint32_t bias = 0x4B000000u;  // f32 2^23: the sum comes out as the bits of 2^23 + s
-        const uint32_t s0 = __builtin_amdgcn_udot4(hi, wh0, __builtin_amdgcn_udot4(lo, wl0, bias, false), false);
-        const uint32_t s1 = __builtin_amdgcn_udot4(hi, wh1, __builtin_amdgcn_udot4(lo, wl1, bias, false), false);
-        return (float2v){__uint_as_float(s0), __uint_as_float(s1)} - two23;
-      };
-      const int simd_w = wj & ~3;
-      const int X0 = xj - kPatchR + 2 * bg;  // level column of output col 2g
-      const bool tail = X0 + 1 >= simd_w;     // a column of the pair takes the scalar-tail rounding
-      const int nrows = bst < 2 ? kBlurStrip : kPatchRows - 2 * kBlurStrip;
-      float2v win[7];
-#pragma unroll
-      for (int t = 0; t < 6; t++) win[t] = rowsum(t);
-#pragma unroll
-      for (int t = 0; t < kBlurStrip; t++) {
-        win[(t + 6) % 7] = rowsum(t + 6);
-        const float2v w0 = win[t % 7], w1 = win[(t + 1) % 7], w2 = win[(t + 2) % 7], w3 = win[(t + 3) % 7],
-                      w4 = win[(t + 4) % 7], w5 = win[(t + 5) % 7], w6 = win[(t + 6) % 7];
-        // exactly the scalar chain fma(f3, w3, fma(f2, w2+w4, fma(f1, w1+w5, f0*(w0+w6)))) per element
-        const float2v accv = __builtin_elementwise_fma(
-            F3, w3, __builtin_elementwise_fma(F2, w2 + w4, __builtin_elementwise_fma(F1, w1 + w5, F0 * (w0 + w6))));
-        const float2v rr = accv + magic_s;  // rint (half-to-even) into the low bits
-        uint32_t pk = __builtin_amdgcn_perm(__float_as_uint(rr.y), __float_as_uint(rr.x), 0x05040100u);
-        u16x2 p2 = __builtin_bit_cast(u16x2, pk);
-        p2 = __builtin_elementwise_min(p2, (u16x2){255, 255});  // the kernel sums to 257
-        uint32_t px2 = __builtin_bit_cast(uint32_t, p2);
-        if (tail) {
-          // the row's scalar tail (x >= w & ~3): (acc + 2^15) >> 16
-          const int v0 = min(((int)(accv.x * 65536.f) + (1 << 15)) >> 16, 255);
-          const int v1 = min(((int)(accv.y * 65536.f) + (1 << 15)) >> 16, 255);
-          if (X0 >= simd_w) px2 = (px2 & 0xFFFF0000u) | (uint32_t)v0;
-          px2 = (px2 & 0x0000FFFFu) | ((uint32_t)v1 << 16);
-        }
-        if (t < nrows)
-          *(uint16_t*)(pb + (bst * kBlurStrip + t) * kPS + 2 * bg) = (uint16_t)(px2 | (px2 >> 8));
-      }
-    }
-#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1739,7 +1595,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   } else {
     (void)hipMemsetAsync(B.oct_count, 0, sizeof(int) * Gh.nlevels * n_img, st);
   }
-  if (!ORBX_DESC_FUSED) {  // (fused: k_describe blurs each keypoint's patch itself; launch_blur on request)
+  {
     T->begin(st);
     hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
     T->end(ST_BLUR, st);

@@ -295,7 +295,6 @@ struct BaDev {
   double* scal;    // scalars: [0] chi at iteration start, [1] chi after the trial, [2] solve ok, [3] max diag, [4] LM scale
   const LmState* lm;  // device LM state: gates the trial's kernels and carries lambda (null: host control)
   int nan_trial;      // debug (ORBX_BA_NAN_TRIAL): this trial's chi is NaN; -1 off
-  int host_trial;     // host-controlled loop: the trial being queued (the device loop counts its own)
   int raise_after;    // debug (ORBX_BA_RAISE_STOP_AFTER): the device raises the stop mirror after this many trials; -1 off
 };
 
@@ -448,7 +447,7 @@ __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, 
       chi = rho[0];
     }
     // debug hook (ORBX_BA_NAN_TRIAL): the given trial's chi is NaN, i.e. rho is NaN
-    if (dst == 1 && k == 0 && D.nan_trial >= 0 && (D.lm ? D.lm->trials : D.host_trial) == D.nan_trial)
+    if (dst == 1 && k == 0 && D.nan_trial >= 0 && D.lm && D.lm->trials == D.nan_trial)
       chi = __builtin_nan("");
   }
   block_partial(chi, D.scal + 8 + dst * D.nbe);
@@ -1002,15 +1001,14 @@ __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
 // (k1, k2) order).  Blocks b >= nblk: sum of cf over pose b - nblk's positions
 // (the Schur rhs correction).  Chunk partials -> gpart; k_ba_schur_fin sums
 // them in chunk order (deterministic).
-// device-LM trials fold k_ba_cam_sum / k_ba_cam_fin into k_ba_pairs / k_ba_schur_fin (debug option
-// no_camfold launches them as before; results are bit-identical either way)
-static bool camfold_on() { return !ba_opts().no_camfold; }
+// device-LM trials fold k_ba_cam_sum / k_ba_cam_fin into k_ba_pairs / k_ba_schur_fin (the entry
+// linearisation of a phase still launches them)
 // device-LM value of BaDev::fused: 2 = k_ba_lin_schur also takes the non-relinearising trials'
-// point side and k_ba_point_schur is not launched (debug option no_psfold: launched).  A problem without
-// free poses keeps 1 (k_ba_point_schur flags its empty reduced system).
+// point side and k_ba_point_schur is not launched.  A problem without free poses keeps 1
+// (k_ba_point_schur flags its empty reduced system).
 static int fused_mode(int nbf, int nposes) {
   if (nbf <= 0) return 0;
-  return nposes > 0 && !ba_opts().no_psfold ? 2 : 1;
+  return nposes > 0 ? 2 : 1;
 }
 
 // pose-term chunk partials of a camfold trial, after the pair and rhs partials
@@ -2685,17 +2683,11 @@ struct LocalBA {
   double* rb_host = nullptr;       // pinned readback block
   int rb_cap = 0;
   hipEvent_t rb_ev = nullptr;      // recorded after the readback copy (the wait skips later work)
-  // Two sets of the linearisation outputs the LM trial reads.  While the host
-  // waits for a trial's readback, the next iteration's linearisation at the
-  // trial state is already running into the other set; an accepted trial (the
-  // common case) then starts its next iteration on that set, a rejected one
-  // keeps the current set untouched.
+  // the linearisation outputs the LM trials read
   struct LinSet {
     double *Hpl, *Hll, *bl, *dmax_p, *Hpp, *bp;
   };
-  LinSet lin[2] = {};
-  int lin_cur = 0;
-  DBuf<double> Hpl2, Hll2, bl2, dmax2, Hpp2, bp2;
+  LinSet lin0 = {};
   LocalBA() = default;
   LocalBA(const LocalBA&) = delete;
   LocalBA& operator=(const LocalBA&) = delete;
@@ -2929,12 +2921,6 @@ struct LocalBA {
     BA_CHECK(c.dmax_p.alloc(npa + nposes));
     BA_CHECK(c.Hpp.alloc(36 * (size_t)nposes));
     BA_CHECK(c.bp.alloc(N));
-    BA_CHECK(Hpl2.alloc(18 * (size_t)na));
-    BA_CHECK(Hll2.alloc(9 * (size_t)npa));
-    BA_CHECK(bl2.alloc(3 * (size_t)npa));
-    BA_CHECK(dmax2.alloc(npa + nposes));
-    BA_CHECK(Hpp2.alloc(36 * (size_t)nposes));
-    BA_CHECK(bp2.alloc(N));
     if (!rb_ev) BA_CHECK(hipEventCreateWithFlags(&rb_ev, hipEventDisableTiming));
     BA_CHECK(c.xp.alloc(N));
     BA_CHECK(c.bs.alloc(N));
@@ -2982,10 +2968,8 @@ struct LocalBA {
     D.xp = c.xp.p;
     D.bs = c.bs.p;
     D.S = c.S.p;
-    lin[0] = LinSet{c.Hpl.p, c.Hll.p, c.bl.p, c.dmax_p.p, c.Hpp.p, c.bp.p};
-    lin[1] = LinSet{Hpl2.p, Hll2.p, bl2.p, dmax2.p, Hpp2.p, bp2.p};
-    lin_cur = 0;
-    use_lin(D, lin[0]);
+    lin0 = LinSet{c.Hpl.p, c.Hll.p, c.bl.p, c.dmax_p.p, c.Hpp.p, c.bp.p};
+    use_lin(D, lin0);
     return ORBX_OK;
   }
 
@@ -3022,113 +3006,8 @@ struct LocalBA {
     return hipSuccess;
   }
 
-  // SparseOptimizer::optimize + OptimizationAlgorithmLevenberg::solve.  One
-  // host readback per LM trial (plus one for lambda init per phase); the
-  // accept/reject logic runs on the host on exactly the reference's doubles.
-  orbx_status optimize(int iterations, const StopFlag& stop, hipStream_t st, int* iters, double* final_chi) {
-    double lambda = 0, ni = 2;
-    int nBad = 0;
-    int it = 0;
-    const size_t N = 6 * (size_t)D.nposes;
-    if (ldlt_np((int)N) > kLdltMaxNp) return ORBX_ERR_SIZE;
-    LdltPlan ldlt;
-    BA_CHECK(ldlt.prepare((int)N));
-    D.ldlt_pan = ldlt.pan ? 1 : 0;
-    if (!ldlt.col && !ldlt.in_lds) {
-      BA_CHECK(c.Sw.alloc((size_t)ldlt_np((int)N) * ldlt_np((int)N)));
-      D.Sw = c.Sw.p;
-    }
-    const int gp = std::max((D.npa + D.nposes + LBS - 1) / LBS, 1);
-    const int ga = std::max((D.na + LBS - 1) / LBS, 1);
-    double sc[5];
-    int ptrial = 0;  // trials of this phase (the ORBX_BA_NAN_TRIAL hook counts per phase, as the device loop)
-    const bool spec_on = !ba_opts().no_spec;
-    bool spec_ready = false;  // the other LinSet holds the linearisation at the current state
-    double spec_chi = 0;      // its chi (the accepted trial's)
-    for (int i = 0; i < iterations && !(stop()); i++) {
-      const bool from_spec = spec_ready;
-      if (from_spec) {
-        lin_cur ^= 1;
-        use_lin(D, lin[lin_cur]);
-      } else {
-        BA_CHECK(errors(st, 1, 0));  // computeActiveErrors; activeRobustChi2 -> scal[0]
-        linearize(D, st);
-      }
-      spec_ready = false;
-      BA_CHECK(hipGetLastError());
-      if (i == 0) {
-        hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D.dmax_p, D.npa + D.nposes, D.scal + 3, 1);
-        BA_CHECK(read_scalars(sc, st));
-        lambda = 1e-5 * sc[3];  // computeLambdaInit: tau * max |H_jj|
-        ni = 2;
-        nBad = 0;
-      }
-      double currentChi = 0, iniChi = 0;
-      double rho = 0;
-      int qmax = 0;
-      do {
-        hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, D, lambda);
-        if (D.nposes > 0) {
-          hipLaunchKernelGGL(k_ba_pairs, dim3(D.nblk + D.nposes, D.gsplit), dim3(kPB), 0, st, D);
-          hipLaunchKernelGGL(k_ba_schur_fin, dim3(D.nblk + D.nposes), dim3(64), 0, st, D, lambda);
-          ldlt.launch(D, st);
-        }
-        hipLaunchKernelGGL(k_ba_update, dim3(D.nbu), dim3(LBS), 0, st, D, lambda);
-        D.host_trial = ptrial++;
-        BA_CHECK(errors(st, 1, 1));
-        BA_CHECK(start_read(st));
-        bool launched = false;
-        if (spec_on && i + 1 < iterations) {  // next iteration's linearisation at the trial state
-          BaDev Ds = D;
-          use_lin(Ds, lin[lin_cur ^ 1]);
-          linearize(Ds, st);
-          BA_CHECK(hipGetLastError());
-          launched = true;
-        }
-        BA_CHECK(finish_read(sc));
-        if (qmax == 0) currentChi = iniChi = from_spec ? spec_chi : sc[0];
-        const bool ok2 = sc[2] != 0.0;
-        trials++;
-        const double tempChi = ok2 ? sc[1] : std::numeric_limits<double>::max();
-        rho = currentChi - tempChi;
-        double scale = ok2 ? sc[4] : 0.0;
-        scale += 1e-3;
-        rho /= scale;
-        if (rho > 0 && std::isfinite(tempChi)) {
-          double alpha = 1. - lm_cube(2 * rho - 1);
-          alpha = std::min(alpha, 2. / 3.);
-          const double scaleFactor = std::max(1. / 3., alpha);
-          lambda *= scaleFactor;
-          ni = 2;
-          currentChi = tempChi;
-          spec_ready = launched;
-          spec_chi = tempChi;
-        } else {
-          lambda *= ni;
-          ni *= 2;
-          spec_ready = false;
-          if (ok2) hipLaunchKernelGGL(k_ba_restore, dim3(gp), dim3(LBS), 0, st, D);
-          BA_CHECK(hipGetLastError());
-        }
-        qmax++;
-      } while (rho < 0 && qmax < 10 && !(stop()));
-      ++it;
-      if (qmax == 10 || rho == 0) break;
-      if ((iniChi - currentChi) * 1e3 < iniChi)
-        nBad++;
-      else
-        nBad = 0;
-      if (nBad >= 3) break;
-    }
-    *iters = it;
-    BA_CHECK(errors(st, 0, 0));  // activeRobustChi2 of the stored errors
-    BA_CHECK(read_scalars(sc, st));
-    if (final_chi) *final_chi = sc[0];
-    return ORBX_OK;
-  }
-
-  // The same optimize() with the LM control on the device: the entry
-  // linearisation and lambda init, then trials queued back to back --
+  // SparseOptimizer::optimize + OptimizationAlgorithmLevenberg::solve with the LM control on the
+  // device: the entry linearisation and lambda init, then trials queued back to back --
   // (gated) linearisation, Schur, solve, update (which first pops a rejected
   // trial), errors, k_ba_lm_control -- with no host round trip between them,
   // and one gated restore when the phase ends on a rejection.  The host
@@ -3158,7 +3037,7 @@ struct LocalBA {
     BaDev Dg = D;
     Dg.lm = c.lm.p;
     Dg.fused = fused_mode(D.nbf, D.nposes);
-    Dg.camfold = camfold_on() ? 1 : 0;
+    Dg.camfold = 1;
     int it = 0;
     if (!(stop())) {  // the loop head's first poll (i = 0)
       hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, D0, 1, 0);
@@ -3286,7 +3165,6 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
   // test hooks (off unless orbx_debug_ba_options set them): a NaN trial, a device-raised stop flag
   D.nan_trial = ba_opts().nan_trial;
   D.raise_after = ba_opts().raise_stop_after;
-  D.host_trial = 0;
   Ctx& c = L.c;
   const int nc = pb->n_cams, np = pb->n_points, ne = pb->n_edges;
   D.nc = nc;
@@ -3305,10 +3183,10 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
     max_run = std::max(max_run, run);
     L.ccnt[pb->edge_cam[e]]++;
   }
-  // the fused point side needs every point's positions inside one block (debug option no_fuse: split)
-  L.fuse_ok = grouped && max_run <= kFuseMaxDeg && !ba_opts().no_fuse;
-  L.dev_struct = grouped && nc <= kStructMaxNc && (ne + kTileE - 1) / kTileE <= kStructMaxTiles &&
-                 !ba_opts().host_struct;
+  // the fused point side needs every point's positions inside one block (else the three kernels)
+  L.fuse_ok = grouped && max_run <= kFuseMaxDeg;
+  // the structure on the device when the edges arrive grouped by point (else the host build)
+  L.dev_struct = grouped && nc <= kStructMaxNc && (ne + kTileE - 1) / kTileE <= kStructMaxTiles;
   if (L.dev_struct) {  // phase-1 sizes: the launches need no readback
     int nposes = 0, maxc = 0;
     for (int i = 0; i < nc; i++)
@@ -3481,13 +3359,13 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   res->chi2[0] = res->chi2[1] = 0;
   const int ge = (ne + LBS - 1) / LBS;
   bool ran = false;
-  // LM control on the device unless the stop flag cannot be mapped (or ORBX_BA_HOST_LM=1)
+  // LM control on the device; the stop flag it polls lives in pinned, device-mapped memory
   DevStop dstop{nullptr, nullptr};
   L.unmap_stop();
   L.hook_stopped = false;
-  const bool dev_lm = !ba_opts().host_lm && L.map_stop(stop, &dstop);
+  if (!L.map_stop(stop, &dstop)) return ORBX_ERR_HIP;
   auto optimize = [&](int iterations, int* iters, double* chi) {
-    return dev_lm ? L.optimize_dev(iterations, stop, dstop, st, iters, chi) : L.optimize(iterations, stop, st, iters, chi);
+    return L.optimize_dev(iterations, stop, dstop, st, iters, chi);
   };
   if (!(stop())) {  // src/Optimizer.cc:749-751
     ran = true;
@@ -3581,7 +3459,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
     if (!lpan.pan) return ORBX_ERR_SIZE;
     BA_CHECK(lpan.prepare_many());
   }
-  const bool camfold = camfold_on();
+  const bool camfold = true;
   int n_ps = 0, n_psfold = 0;  // problems that launch k_ba_point_schur / whose k_ba_lin_schur takes it
   if (B.cap < K) {
     if (B.lm_host) (void)hipHostFree(B.lm_host);
@@ -3703,7 +3581,8 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
   }
   DevStop dstop{nullptr, nullptr};
   for (int i = 0; i < K; i++) Ls[i]->unmap_stop();
-  bool batch = !ba_opts().host_lm && Ls[0]->map_stop(stop, &dstop);
+  if (!Ls[0]->map_stop(stop, &dstop)) return ORBX_ERR_HIP;
+  bool batch = true;
   for (int i = 0; i < K; i++) batch &= Ls[i]->dev_struct;
   if (!batch) {  // one by one (intake again inside: the arenas are reused)
     for (int i = 0; i < K; i++) {
@@ -3764,7 +3643,7 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
 }  // namespace orbx
 
 namespace orbx {
-constexpr orbx_ba_debug_options kBaOptsDefault = {0, 0, 0, 0, 0, 0, ORBX_BA_LDLT_AUTO, -1, -1, 0};
+constexpr orbx_ba_debug_options kBaOptsDefault = {ORBX_BA_LDLT_AUTO, -1, -1, 0};
 thread_local const orbx_ba_debug_options* t_ba_opts = nullptr;
 inline const orbx_ba_debug_options& ba_opts() { return t_ba_opts ? *t_ba_opts : kBaOptsDefault; }
 struct BaOptScope {  // the handle's options for this call on this thread

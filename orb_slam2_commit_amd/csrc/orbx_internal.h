@@ -19,12 +19,6 @@ namespace orbx {
 constexpr int kMaxLevelsPlan = 16;
 constexpr int kEdgeThresholdHost = 19;  // EDGE_THRESHOLD, src/ORBextractor.cc:74
 
-// k_describe form: 1 = each keypoint's 37x37 patch blurred inside k_describe from the raw level (no
-// blurred level materialised), 0 = k_blur writes the blurred levels and k_describe samples them
-#ifndef ORBX_DESC_FUSED
-#define ORBX_DESC_FUSED 0
-#endif
-
 struct LevelGeom {
   int w, h;
   long long off;    // offset of level in per-image pyramid buffer (levels >= 1)

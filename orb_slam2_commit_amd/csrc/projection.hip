@@ -33,6 +33,7 @@
 // loads per point group), so the batch is the unit of throughput.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstring>
 #include <vector>
@@ -268,20 +269,12 @@ __device__ __forceinline__ uint32_t group_min(uint32_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem* __restrict__ probs) {
-  __shared__ uint32_t s_keys[kMaxF];  // grid sort keys, then first-writer / final occupant table
-  __shared__ uint16_t s_pos[kMaxF];   // sorted position -> feature index
-  __shared__ int s_start[kCells + 1];
-  __shared__ int s_hist[32];
-  __shared__ int s_sel[3];
-  __shared__ int s_changed, s_count, s_drop;
-  const ProjProblem& P = probs[blockIdx.x];
+// ---- the kernel's phases as block-wide device functions (shared by the batched one-block-per-problem
+// kernel and the split single-problem kernels below) ----
+
+// the pose the points project with: Tcw, or for the Sim3 kinds [Rcw | tcw] = [sRcw | t] / scw
+__device__ __forceinline__ void proj_pose(const ProjProblem& P, float* s_Tcw, int tid) {
   const orbx_proj_frame& F = P.f;
-  const int tid = threadIdx.x;
-  if (P.gate && !(*P.gate < P.gate_below)) return;  // block-uniform: the problem is skipped whole
-  const int nF = P.f_n_dev ? min(max(*P.f_n_dev, 0), F.n) : F.n;
-  const int nP = P.n_points_dev ? min(max(*P.n_points_dev, 0), P.n_points) : P.n_points;
-  __shared__ float s_Tcw[16];
   if (tid < 16) {
     const float* S = P.Tcw_dev ? P.Tcw_dev : F.Tcw;
     if (P.kind == ORBX_PROJ_SIM3 || P.kind == ORBX_PROJ_FUSE_SIM3) {
@@ -297,12 +290,30 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
       s_Tcw[tid] = S[tid];
     }
   }
-  int* s_fw = (int*)s_keys;
+}
 
-  // ---- Frame::AssignFeaturesToGrid as a sort of (cell << 13 | index) ----
+// camera centre and the last-frame direction flags (after proj_pose's writes are visible)
+__device__ __forceinline__ void proj_centre(const ProjProblem& P, const float* s_Tcw, float* Ow, bool& fwd, bool& bwd) {
+  if (P.kind == ORBX_PROJ_FUSE)
+    camera_centre_kf(s_Tcw, Ow);  // pKF->GetCameraCenter() (src/ORBmatcher.cc:928)
+  else
+    camera_centre(s_Tcw, Ow);
+  fwd = bwd = false;
+  if (P.kind == ORBX_PROJ_LAST_FRAME) {
+    float tlc[3];
+    mat3x1(P.last_Tcw, Ow, tlc);  // twc = Ow
+    fwd = tlc[2] > P.f.b && !P.mono;
+    bwd = -tlc[2] > P.f.b && !P.mono;
+  }
+}
+
+// Frame::AssignFeaturesToGrid as a sort of (cell << 13 | index): s_pos[sorted position] = feature,
+// s_start[c] = first sorted position of cell c (s_keys is the sort's scratch); ends with a barrier
+template <int NT>
+__device__ void proj_grid(const orbx_proj_frame& F, int nF, uint32_t* s_keys, uint16_t* s_pos, int* s_start, int tid) {
   int nsort = 1;
   while (nsort < nF) nsort <<= 1;
-  for (int i = tid; i < nsort; i += PBS) {
+  for (int i = tid; i < nsort; i += NT) {
     uint32_t key = 0xFFFFFFFFu;
     if (i < nF) {
       const orbx_keypoint kp = F.keys_un[i];
@@ -316,7 +327,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   __syncthreads();
   for (int k = 2; k <= nsort; k <<= 1) {  // bitonic sort, ascending
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = tid; t < (nsort >> 1); t += PBS) {
+      for (int t = tid; t < (nsort >> 1); t += NT) {
         const int lo = 2 * t - (t & (j - 1));
         const int hi = lo + j;
         const uint32_t a = s_keys[lo], b = s_keys[hi];
@@ -329,7 +340,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
       __syncthreads();
     }
   }
-  for (int c = tid; c <= kCells; c += PBS) {  // s_start[c] = lower_bound(c << 13)
+  for (int c = tid; c <= kCells; c += NT) {  // s_start[c] = lower_bound(c << 13)
     const uint32_t target = (uint32_t)c << 13;
     int lo = 0, hi = nsort;
     while (lo < hi) {
@@ -338,190 +349,203 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
     }
     s_start[c] = lo;
   }
-  for (int i = tid; i < nF; i += PBS) s_pos[i] = (uint16_t)(s_keys[i] & 0x1FFF);
-  if (tid < 32) s_hist[tid] = 0;
+  for (int i = tid; i < nF; i += NT) s_pos[i] = (uint16_t)(s_keys[i] & 0x1FFF);
   __syncthreads();
+}
 
-  float Ow[3];
-  if (P.kind == ORBX_PROJ_FUSE)
-    camera_centre_kf(s_Tcw, Ow);  // pKF->GetCameraCenter() (src/ORBmatcher.cc:928)
-  else
-    camera_centre(s_Tcw, Ow);
-  bool fwd = false, bwd = false;
-  if (P.kind == ORBX_PROJ_LAST_FRAME) {
-    float tlc[3];
-    mat3x1(P.last_Tcw, Ow, tlc);  // twc = Ow
-    fwd = tlc[2] > F.b && !P.mono;
-    bwd = -tlc[2] > F.b && !P.mono;
-  }
-
-  // ---- Tracking::SearchLocalPoints: isInFrustum(pMP, limit) for every point ----
-  if (P.kind == ORBX_PROJ_LOCAL && P.frustum) {
-    for (int i = tid; i < nP; i += PBS) {
-      int lvl = -1;
-      float* tr = P.track + 4 * i;
-      if (P.flags[i] & 1) {
-        const float* X = P.pos + 3 * i;
-        float c[3];
-        mat3x1(s_Tcw, X, c);
-        if (!(c[2] < 0.0f)) {
-          const float invz = 1.0f / c[2];
-          const float u = F.fx * c[0] * invz + F.cx;
-          const float v = F.fy * c[1] * invz + F.cy;
-          if (!(u < F.min_x || u > F.max_x) && !(v < F.min_y || v > F.max_y) && u == u && v == v) {
-            const float dmin = P.dist_minmax[2 * i], dmax = P.dist_minmax[2 * i + 1];
-            const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
-            const float dist = norm3(PO);
-            if (!(dist < 0.8f * dmin || dist > 1.2f * dmax)) {
-              const float* Pn = P.normal + 3 * i;
-              double dot = (double)PO[0] * Pn[0];
-              dot = dot + (double)PO[1] * Pn[1];
-              dot = dot + (double)PO[2] * Pn[2];
-              const float vc = (float)(dot / dist);
-              if (!(vc < P.view_cos_limit)) {
-                lvl = predict_scale(dmax, dist, F.log_scale_factor, F.nlevels);
-                tr[0] = u;
-                tr[1] = v;
-                tr[2] = u - F.bf * invz;
-                tr[3] = vc;
-              }
-            }
+// Tracking::SearchLocalPoints' isInFrustum(pMP, limit) for point i
+__device__ __forceinline__ void proj_frustum(const ProjProblem& P, int i, const float* s_Tcw, const float* Ow) {
+  const orbx_proj_frame& F = P.f;
+  int lvl = -1;
+  float* tr = P.track + 4 * i;
+  if (P.flags[i] & 1) {
+    const float* X = P.pos + 3 * i;
+    float c[3];
+    mat3x1(s_Tcw, X, c);
+    if (!(c[2] < 0.0f)) {
+      const float invz = 1.0f / c[2];
+      const float u = F.fx * c[0] * invz + F.cx;
+      const float v = F.fy * c[1] * invz + F.cy;
+      if (!(u < F.min_x || u > F.max_x) && !(v < F.min_y || v > F.max_y) && u == u && v == v) {
+        const float dmin = P.dist_minmax[2 * i], dmax = P.dist_minmax[2 * i + 1];
+        const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+        const float dist = norm3(PO);
+        if (!(dist < 0.8f * dmin || dist > 1.2f * dmax)) {
+          const float* Pn = P.normal + 3 * i;
+          double dot = (double)PO[0] * Pn[0];
+          dot = dot + (double)PO[1] * Pn[1];
+          dot = dot + (double)PO[2] * Pn[2];
+          const float vc = (float)(dot / dist);
+          if (!(vc < P.view_cos_limit)) {
+            lvl = predict_scale(dmax, dist, F.log_scale_factor, F.nlevels);
+            tr[0] = u;
+            tr[1] = v;
+            tr[2] = u - F.bf * invz;
+            tr[3] = vc;
           }
         }
       }
-      P.track_level[i] = lvl;
     }
-    __threadfence_block();
   }
-  for (int i = tid; i < nF; i += PBS) s_fw[i] = INT_MAX;
-  __syncthreads();
+  P.track_level[i] = lvl;
+}
 
-  // ---- sweeps to the sequential fixed point ----
-  const int g = tid / kGroup, gl = tid % kGroup;
-  constexpr int kGroups = PBS / kGroup;
-  const bool local = P.kind == ORBX_PROJ_LOCAL;
+struct ProjMode {
+  bool local, kf, fuse, gate;
+};
+__device__ __forceinline__ ProjMode proj_mode(const ProjProblem& P) {
+  ProjMode M;
+  M.local = P.kind == ORBX_PROJ_LOCAL;
   // KEYFRAME and SIM3: any MapPoint on the feature blocks it, and every match blocks later points
-  const bool kf = P.kind == ORBX_PROJ_KEYFRAME || P.kind == ORBX_PROJ_SIM3;
+  M.kf = P.kind == ORBX_PROJ_KEYFRAME || P.kind == ORBX_PROJ_SIM3;
   // no "already matched" state: one sweep (FUSE also gates candidates by reprojection error)
-  const bool fuse = P.kind == ORBX_PROJ_FUSE || P.kind == ORBX_PROJ_FUSE_SIM3 || P.kind == ORBX_PROJ_BY_SIM3;
-  const bool gate = P.kind == ORBX_PROJ_FUSE;
-  for (int sweep = 0; sweep <= nP + 1; sweep++) {
-    if (tid == 0) s_changed = 0;
+  M.fuse = P.kind == ORBX_PROJ_FUSE || P.kind == ORBX_PROJ_FUSE_SIM3 || P.kind == ORBX_PROJ_BY_SIM3;
+  M.gate = P.kind == ORBX_PROJ_FUSE;
+  return M;
+}
+
+// One point's match by a kGroup-lane group (the result is valid in every lane of the group) against
+// the first-writer table fw of the previous sweep
+__device__ __forceinline__ int proj_point(const ProjProblem& P, int i, int gl, const float* s_Tcw, const float* Ow,
+                                          bool fwd, bool bwd, const uint16_t* s_pos, const int* s_start,
+                                          const int* fw, const ProjMode& M) {
+  const orbx_proj_frame& F = P.f;
+  const Query q = setup_query(P, i, s_Tcw, Ow, fwd, bwd);
+  int m = -1;
+  if (!q.active) return m;
+  uint64_t dq[4];
+  {
+    const uint64_t* d = (const uint64_t*)(P.desc + (size_t)i * 32);
+    dq[0] = d[0]; dq[1] = d[1]; dq[2] = d[2]; dq[3] = d[3];
+  }
+  uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+  int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+  {  // Frame::GetFeaturesInArea cell range, src/Frame.cc:395-413
+    x0 = max(0, (int)__builtin_floorf((q.x - F.min_x - q.r) * F.grid_inv_w));
+    x1 = min(ORBX_GRID_COLS - 1, (int)__builtin_ceilf((q.x - F.min_x + q.r) * F.grid_inv_w));
+    y0 = max(0, (int)__builtin_floorf((q.y - F.min_y - q.r) * F.grid_inv_h));
+    y1 = min(ORBX_GRID_ROWS - 1, (int)__builtin_ceilf((q.y - F.min_y + q.r) * F.grid_inv_h));
+    if (x0 >= ORBX_GRID_COLS || x1 < 0 || y0 >= ORBX_GRID_ROWS || y1 < 0) x1 = x0 - 1;
+  }
+  const bool check = q.min_level > 0 || q.max_level >= 0;
+  for (int ix = x0; ix <= x1; ix++) {
+    const int c0 = ix * ORBX_GRID_ROWS;
+    const int pend = s_start[c0 + y1 + 1];
+    for (int p = s_start[c0 + y0] + gl; p < pend; p += kGroup) {
+      const int idx = s_pos[p];
+      const orbx_keypoint& kp = F.keys_un[idx];
+      const int oct = kp.octave;
+      if (check && (oct < q.min_level || (q.max_level >= 0 && oct > q.max_level))) continue;
+      const float dx = kp.x - q.x, dy = kp.y - q.y;
+      if (!(__builtin_fabsf(dx) < q.r && __builtin_fabsf(dy) < q.r)) continue;
+      if (M.gate) {  // reprojection error gate, src/ORBmatcher.cc:1018-1042
+        const float isg = F.inv_level_sigma2[oct];
+        const float urf = F.u_right ? F.u_right[idx] : -1.0f;
+        const float ex = q.x - kp.x, ey = q.y - kp.y;
+        if (urf >= 0) {
+          const float er = q.ur - urf;
+          const float e2 = ex * ex + ey * ey + er * er;
+          if (e2 * isg > 7.8) continue;
+        } else {
+          const float e2 = ex * ex + ey * ey;
+          if (e2 * isg > 5.99) continue;
+        }
+      } else if (!M.fuse) {
+        const int o = F.occ ? F.occ[idx] : 0;
+        if ((M.kf ? o != 0 : o == 2) || fw[idx] < i) continue;
+      }
+      if (q.ur_th >= 0.0f && F.u_right) {
+        const float urf = F.u_right[idx];
+        if (urf > 0 && __builtin_fabsf(q.ur - urf) > q.ur_th) continue;
+      }
+      const uint64_t* d = (const uint64_t*)(F.desc + (size_t)idx * 32);
+      const uint64_t x[4] = {d[0], d[1], d[2], d[3]};
+      const uint32_t key = ((uint32_t)hamming256(dq, x) << 16) | (uint32_t)p;
+      if (key < m1) {
+        m2 = m1;
+        m1 = key;
+      } else if (key < m2) {
+        m2 = key;
+      }
+    }
+  }
+  const uint32_t b1 = group_min(m1);
+  const uint32_t b2 = group_min(m1 == b1 ? m2 : m1);
+  if (b1 != 0xFFFFFFFFu) {
+    const int d1 = (int)(b1 >> 16);
+    if (d1 <= q.th) {
+      const int i1 = s_pos[b1 & 0xFFFF];
+      bool ok = true;
+      if (M.local) {  // ratio only when best and second share a level, src/ORBmatcher.cc:127-131
+        const int l1 = F.keys_un[i1].octave;
+        const int l2 = b2 == 0xFFFFFFFFu ? -1 : F.keys_un[s_pos[b2 & 0xFFFF]].octave;
+        const int d2 = b2 == 0xFFFFFFFFu ? 256 : (int)(b2 >> 16);
+        if (l1 == l2 && (float)d1 > P.nnratio * (float)d2) ok = false;
+      }
+      if (ok) m = i1;
+    }
+  }
+  return m;
+}
+
+// The sweeps to the sequential fixed point inside one block, from sweep `first` on, with the
+// first-writer table s_fw already holding sweep `first`'s input
+template <int NT>
+__device__ void proj_sweeps(const ProjProblem& P, int nF, int nP, const float* s_Tcw, const float* Ow, bool fwd,
+                            bool bwd, const uint16_t* s_pos, const int* s_start, int* s_fw, int* s_changed,
+                            int first, int tid) {
+  const ProjMode M = proj_mode(P);
+  const int g = tid / kGroup, gl = tid % kGroup;
+  constexpr int kGroups = NT / kGroup;
+  for (int sweep = first; sweep <= nP + 1; sweep++) {
+    if (tid == 0) *s_changed = 0;
     __syncthreads();
     int changed = 0;
     for (int i = g; i < nP; i += kGroups) {
-      const Query q = setup_query(P, i, s_Tcw, Ow, fwd, bwd);
-      int m = -1;
-      if (q.active) {
-        uint64_t dq[4];
-        {
-          const uint64_t* d = (const uint64_t*)(P.desc + (size_t)i * 32);
-          dq[0] = d[0]; dq[1] = d[1]; dq[2] = d[2]; dq[3] = d[3];
-        }
-        uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
-        int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
-        {  // Frame::GetFeaturesInArea cell range, src/Frame.cc:395-413
-          x0 = max(0, (int)__builtin_floorf((q.x - F.min_x - q.r) * F.grid_inv_w));
-          x1 = min(ORBX_GRID_COLS - 1, (int)__builtin_ceilf((q.x - F.min_x + q.r) * F.grid_inv_w));
-          y0 = max(0, (int)__builtin_floorf((q.y - F.min_y - q.r) * F.grid_inv_h));
-          y1 = min(ORBX_GRID_ROWS - 1, (int)__builtin_ceilf((q.y - F.min_y + q.r) * F.grid_inv_h));
-          if (x0 >= ORBX_GRID_COLS || x1 < 0 || y0 >= ORBX_GRID_ROWS || y1 < 0) x1 = x0 - 1;
-        }
-        const bool check = q.min_level > 0 || q.max_level >= 0;
-        for (int ix = x0; ix <= x1; ix++) {
-          const int c0 = ix * ORBX_GRID_ROWS;
-          const int pend = s_start[c0 + y1 + 1];
-          for (int p = s_start[c0 + y0] + gl; p < pend; p += kGroup) {
-            const int idx = s_pos[p];
-            const orbx_keypoint& kp = F.keys_un[idx];
-            const int oct = kp.octave;
-            if (check && (oct < q.min_level || (q.max_level >= 0 && oct > q.max_level))) continue;
-            const float dx = kp.x - q.x, dy = kp.y - q.y;
-            if (!(__builtin_fabsf(dx) < q.r && __builtin_fabsf(dy) < q.r)) continue;
-            if (gate) {  // reprojection error gate, src/ORBmatcher.cc:1018-1042
-              const float isg = F.inv_level_sigma2[oct];
-              const float urf = F.u_right ? F.u_right[idx] : -1.0f;
-              const float ex = q.x - kp.x, ey = q.y - kp.y;
-              if (urf >= 0) {
-                const float er = q.ur - urf;
-                const float e2 = ex * ex + ey * ey + er * er;
-                if (e2 * isg > 7.8) continue;
-              } else {
-                const float e2 = ex * ex + ey * ey;
-                if (e2 * isg > 5.99) continue;
-              }
-            } else if (!fuse) {
-              const int o = F.occ ? F.occ[idx] : 0;
-              if ((kf ? o != 0 : o == 2) || s_fw[idx] < i) continue;
-            }
-            if (q.ur_th >= 0.0f && F.u_right) {
-              const float urf = F.u_right[idx];
-              if (urf > 0 && __builtin_fabsf(q.ur - urf) > q.ur_th) continue;
-            }
-            const uint64_t* d = (const uint64_t*)(F.desc + (size_t)idx * 32);
-            const uint64_t x[4] = {d[0], d[1], d[2], d[3]};
-            const uint32_t key = ((uint32_t)hamming256(dq, x) << 16) | (uint32_t)p;
-            if (key < m1) {
-              m2 = m1;
-              m1 = key;
-            } else if (key < m2) {
-              m2 = key;
-            }
-          }
-        }
-        const uint32_t b1 = group_min(m1);
-        const uint32_t b2 = group_min(m1 == b1 ? m2 : m1);
-        if (b1 != 0xFFFFFFFFu) {
-          const int d1 = (int)(b1 >> 16);
-          if (d1 <= q.th) {
-            const int i1 = s_pos[b1 & 0xFFFF];
-            bool ok = true;
-            if (local) {  // ratio only when best and second share a level, src/ORBmatcher.cc:127-131
-              const int l1 = F.keys_un[i1].octave;
-              const int l2 = b2 == 0xFFFFFFFFu ? -1 : F.keys_un[s_pos[b2 & 0xFFFF]].octave;
-              const int d2 = b2 == 0xFFFFFFFFu ? 256 : (int)(b2 >> 16);
-              if (l1 == l2 && (float)d1 > P.nnratio * (float)d2) ok = false;
-            }
-            if (ok) m = i1;
-          }
-        }
-      }
+      const int m = proj_point(P, i, gl, s_Tcw, Ow, fwd, bwd, s_pos, s_start, s_fw, M);
       if (gl == 0) {
         if (sweep == 0 || P.point_match[i] != m) changed = 1;
         P.point_match[i] = m;
       }
     }
-    if (changed) s_changed = 1;
+    if (changed) *s_changed = 1;
     __threadfence_block();
     __syncthreads();
-    if (!s_changed || fuse) break;
+    if (!*s_changed || M.fuse) break;
     // first blocking writer per feature from this sweep's matches
-    for (int f = tid; f < nF; f += PBS) s_fw[f] = INT_MAX;
+    for (int f = tid; f < nF; f += NT) s_fw[f] = INT_MAX;
     __syncthreads();
-    for (int i = tid; i < nP; i += PBS) {
+    for (int i = tid; i < nP; i += NT) {
       const int m = P.point_match[i];
-      if (m >= 0 && (kf || (P.flags[i] & 2))) atomicMin(&s_fw[m], i);
+      if (m >= 0 && (M.kf || (P.flags[i] & 2))) atomicMin(&s_fw[m], i);
     }
     __syncthreads();
   }
+}
 
-  // ---- final occupant (last writer), rotation consistency, count ----
-  for (int f = tid; f < nF; f += PBS) s_fw[f] = -1;
+// Final occupant (last writer), rotation consistency (ComputeThreeMaxima), frame_out and the count
+template <int NT>
+__device__ void proj_final(const ProjProblem& P, int nF, int nP, int* s_fw, int* s_hist, int* s_sel, int* s_count,
+                           int* s_drop, int tid) {
+  const orbx_proj_frame& F = P.f;
+  const ProjMode M = proj_mode(P);
+  for (int f = tid; f < nF; f += NT) s_fw[f] = -1;
+  if (tid < 32) s_hist[tid] = 0;
   if (tid == 0) {
-    s_count = 0;
-    s_drop = 0;
+    *s_count = 0;
+    *s_drop = 0;
   }
   __syncthreads();
-  const bool rot = !local && !fuse && P.kind != ORBX_PROJ_SIM3 && P.check_ori;
+  const bool rot = !M.local && !M.fuse && P.kind != ORBX_PROJ_SIM3 && P.check_ori;
   int cnt = 0;
-  for (int i = tid; i < nP; i += PBS) {
+  for (int i = tid; i < nP; i += NT) {
     const int m = P.point_match[i];
     if (m < 0) continue;
     cnt++;
     atomicMax(&s_fw[m], i);
     if (rot) atomicAdd(&s_hist[rot_bin(P.angle[i], F.keys_un[m].angle)], 1);
   }
-  atomicAdd(&s_count, cnt);
+  atomicAdd(s_count, cnt);
   __syncthreads();
   if (rot && tid == 0) {  // ComputeThreeMaxima, src/ORBmatcher.cc:1797-1839
     int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
@@ -551,7 +575,7 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
   __syncthreads();
   if (rot) {
     int drop = 0;
-    for (int i = tid; i < nP; i += PBS) {
+    for (int i = tid; i < nP; i += NT) {
       const int m = P.point_match[i];
       if (m < 0) continue;
       const int b = rot_bin(P.angle[i], F.keys_un[m].angle);
@@ -560,11 +584,160 @@ __global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem*
         drop++;
       }
     }
-    atomicAdd(&s_drop, drop);
+    atomicAdd(s_drop, drop);
     __syncthreads();
   }
-  for (int f = tid; f < nF; f += PBS) P.frame_out[f] = s_fw[f];
-  if (tid == 0) *P.nmatches = s_count - s_drop;
+  for (int f = tid; f < nF; f += NT) P.frame_out[f] = s_fw[f];
+  if (tid == 0) *P.nmatches = *s_count - *s_drop;
+}
+
+__device__ __forceinline__ int proj_nF(const ProjProblem& P) {
+  return P.f_n_dev ? min(max(*P.f_n_dev, 0), P.f.n) : P.f.n;
+}
+__device__ __forceinline__ int proj_nP(const ProjProblem& P) {
+  return P.n_points_dev ? min(max(*P.n_points_dev, 0), P.n_points) : P.n_points;
+}
+
+// One block per problem (batches: the chip fills with problems)
+__global__ __launch_bounds__(PBS) void k_search_by_projection(const ProjProblem* __restrict__ probs) {
+  __shared__ uint32_t s_keys[kMaxF];  // grid sort keys, then first-writer / final occupant table
+  __shared__ uint16_t s_pos[kMaxF];   // sorted position -> feature index
+  __shared__ int s_start[kCells + 1];
+  __shared__ int s_hist[32];
+  __shared__ int s_sel[3];
+  __shared__ int s_changed, s_count, s_drop;
+  __shared__ float s_Tcw[16];
+  const ProjProblem& P = probs[blockIdx.x];
+  const int tid = threadIdx.x;
+  if (P.gate && !(*P.gate < P.gate_below)) return;  // block-uniform: the problem is skipped whole
+  const int nF = proj_nF(P), nP = proj_nP(P);
+  proj_pose(P, s_Tcw, tid);
+  proj_grid<PBS>(P.f, nF, s_keys, s_pos, s_start, tid);
+  int* s_fw = (int*)s_keys;
+  float Ow[3];
+  bool fwd, bwd;
+  proj_centre(P, s_Tcw, Ow, fwd, bwd);
+  if (P.kind == ORBX_PROJ_LOCAL && P.frustum) {
+    for (int i = tid; i < nP; i += PBS) proj_frustum(P, i, s_Tcw, Ow);
+    __threadfence_block();
+  }
+  for (int i = tid; i < nF; i += PBS) s_fw[i] = INT_MAX;
+  __syncthreads();
+  proj_sweeps<PBS>(P, nF, nP, s_Tcw, Ow, fwd, bwd, s_pos, s_start, s_fw, &s_changed, 0, tid);
+  proj_final<PBS>(P, nF, nP, s_fw, s_hist, s_sel, &s_count, &s_drop, tid);
+}
+
+// ---- one problem split over many blocks (the host C-ABI's single call) ----
+// A single problem in one block keeps one CU busy for the whole call (1 ms at 2,000 features /
+// 3,000 points).  Split: k_proj_split_prep builds the grid once into global scratch (block 0) and
+// runs isInFrustum over all blocks; each sweep is one launch of kProjSplitBlocks blocks, every block a
+// slice of the points against the previous sweep's first-writer table (triple-buffered in global
+// memory: sweep s reads fw[s % 3], takes atomicMin into fw[(s+1) % 3], clears fw[(s+2) % 3]); a sweep
+// whose predecessor changed nothing returns at once.  k_proj_split_final (one block) finishes any
+// sweeps still needed in the single-block way, then the final phase.  Same fixed point, so the
+// same answer as k_search_by_projection bit for bit.
+constexpr int kProjSplitSweeps = 3;  // sweep launches before the final kernel takes over
+struct ProjSplit {
+  uint16_t* pos;   // [kMaxF]
+  int* start;      // [kCells + 1]
+  int* fw;         // [3][kMaxF]
+  int* changed;    // [kProjSplitSweeps]
+};
+
+__global__ __launch_bounds__(PBS) void k_proj_split_prep(const ProjProblem* __restrict__ probs, ProjSplit S) {
+  __shared__ uint32_t s_keys[kMaxF];
+  __shared__ uint16_t s_pos[kMaxF];
+  __shared__ int s_start[kCells + 1];
+  __shared__ float s_Tcw[16];
+  const ProjProblem& P = probs[0];
+  const int tid = threadIdx.x, nF = proj_nF(P), nP = proj_nP(P);
+  const int gt = blockIdx.x * PBS + tid, gs = gridDim.x * PBS;
+  for (int f = gt; f < nF; f += gs) {
+    S.fw[f] = INT_MAX;
+    S.fw[kMaxF + f] = INT_MAX;
+  }
+  if (gt < kProjSplitSweeps) S.changed[gt] = 0;
+  if (P.kind == ORBX_PROJ_LOCAL && P.frustum) {
+    proj_pose(P, s_Tcw, tid);
+    __syncthreads();
+    float Ow[3];
+    bool fwd, bwd;
+    proj_centre(P, s_Tcw, Ow, fwd, bwd);
+    for (int i = gt; i < nP; i += gs) proj_frustum(P, i, s_Tcw, Ow);
+  }
+  if (blockIdx.x == 0) {
+    proj_grid<PBS>(P.f, nF, s_keys, s_pos, s_start, tid);
+    for (int i = tid; i < nF; i += PBS) S.pos[i] = s_pos[i];
+    for (int c = tid; c <= kCells; c += PBS) S.start[c] = s_start[c];
+  }
+}
+
+__global__ __launch_bounds__(PBS) void k_proj_split_sweep(const ProjProblem* __restrict__ probs, ProjSplit S,
+                                                          int sweep) {
+  __shared__ int s_fw[kMaxF];
+  __shared__ uint16_t s_pos[kMaxF];
+  __shared__ int s_start[kCells + 1];
+  __shared__ float s_Tcw[16];
+  const ProjProblem& P = probs[0];
+  if (sweep > 0 && !__atomic_load_n(&S.changed[sweep - 1], __ATOMIC_RELAXED)) return;  // converged
+  const int tid = threadIdx.x, nF = proj_nF(P), nP = proj_nP(P);
+  const int* fwr = S.fw + (sweep % 3) * kMaxF;
+  int* fwn = S.fw + ((sweep + 1) % 3) * kMaxF;
+  int* fwc = S.fw + ((sweep + 2) % 3) * kMaxF;
+  proj_pose(P, s_Tcw, tid);
+  for (int i = tid; i < nF; i += PBS) {
+    s_fw[i] = fwr[i];
+    s_pos[i] = S.pos[i];
+  }
+  for (int c = tid; c <= kCells; c += PBS) s_start[c] = S.start[c];
+  const int gt = blockIdx.x * PBS + tid, gs = gridDim.x * PBS;
+  for (int f = gt; f < nF; f += gs) fwc[f] = INT_MAX;
+  __syncthreads();
+  float Ow[3];
+  bool fwd, bwd;
+  proj_centre(P, s_Tcw, Ow, fwd, bwd);
+  const ProjMode M = proj_mode(P);
+  const int g = blockIdx.x * (PBS / kGroup) + tid / kGroup, gl = tid % kGroup, G = gridDim.x * (PBS / kGroup);
+  int changed = 0;
+  for (int i = g; i < nP; i += G) {
+    const int m = proj_point(P, i, gl, s_Tcw, Ow, fwd, bwd, s_pos, s_start, s_fw, M);
+    if (gl == 0) {
+      if (sweep == 0 || P.point_match[i] != m) changed = 1;
+      P.point_match[i] = m;
+      if (!M.fuse && m >= 0 && (M.kf || (P.flags[i] & 2))) atomicMin(&fwn[m], i);
+    }
+  }
+  if (changed) S.changed[sweep] = 1;
+}
+
+__global__ __launch_bounds__(PBS) void k_proj_split_final(const ProjProblem* __restrict__ probs, ProjSplit S) {
+  __shared__ int s_fw[kMaxF];
+  __shared__ uint16_t s_pos[kMaxF];
+  __shared__ int s_start[kCells + 1];
+  __shared__ int s_hist[32];
+  __shared__ int s_sel[3];
+  __shared__ int s_changed, s_count, s_drop;
+  __shared__ float s_Tcw[16];
+  const ProjProblem& P = probs[0];
+  const int tid = threadIdx.x, nF = proj_nF(P), nP = proj_nP(P);
+  const ProjMode M = proj_mode(P);
+  // the split sweeps stop at kProjSplitSweeps; a problem still changing goes on here, from the
+  // state they left (point_match of the last sweep, its first writers in fw[kProjSplitSweeps % 3])
+  if (!M.fuse && S.changed[kProjSplitSweeps - 1]) {  // block-uniform
+    proj_pose(P, s_Tcw, tid);
+    const int* fwr = S.fw + (kProjSplitSweeps % 3) * kMaxF;
+    for (int i = tid; i < nF; i += PBS) {
+      s_fw[i] = fwr[i];
+      s_pos[i] = S.pos[i];
+    }
+    for (int c = tid; c <= kCells; c += PBS) s_start[c] = S.start[c];
+    __syncthreads();
+    float Ow[3];
+    bool fwd, bwd;
+    proj_centre(P, s_Tcw, Ow, fwd, bwd);
+    proj_sweeps<PBS>(P, nF, nP, s_Tcw, Ow, fwd, bwd, s_pos, s_start, s_fw, &s_changed, kProjSplitSweeps, tid);
+  }
+  proj_final<PBS>(P, nF, nP, s_fw, s_hist, s_sel, &s_count, &s_drop, tid);
 }
 
 // ---- ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:442-587) ----
@@ -609,23 +782,29 @@ __device__ void bitonic_asc(T* k, int n) {
     }
 }
 
-__global__ __launch_bounds__(IBS) void k_search_for_initialization(const orbx_init_problem* __restrict__ probs) {
-  extern __shared__ __align__(16) uint8_t ismem[];
-  __shared__ int s_changed, s_count;
-  __shared__ int s_hist[32], s_sel[3];
-  const orbx_init_problem& P = probs[blockIdx.x];
-  const orbx_proj_frame& F1 = P.f1;
-  const orbx_proj_frame& F2 = P.f2;
-  const int n1 = F1.n, n2 = F2.n, tid = threadIdx.x;
+// ---- its phases as block-wide device functions (the one-block kernel and the split single call) ----
+struct InitLds {  // dynamic LDS views
+  uint32_t* keys;   // grid sort scratch, then the sorted chooser list (ns1)
+  int* start;       // [kCells + 1]
+  uint16_t* pos;    // F2 sorted positions
+  uint16_t* pmin;   // per list position: prefix minimum of the distance over the feature's choosers
+  uint32_t* has;    // feature has a chooser
+};
+__device__ __forceinline__ InitLds init_lds(uint8_t* ismem, int n1, int n2) {
   const int ns1 = pow2_at_least(n1), ns2 = pow2_at_least(n2), nk = ns1 > ns2 ? ns1 : ns2;
-  uint32_t* s_keys = (uint32_t*)ismem;
-  int* s_start = (int*)(s_keys + nk);
-  uint16_t* s_pos = (uint16_t*)(s_start + kCells + 1);
-  uint16_t* s_pmin = s_pos + ((n2 + 1) & ~1);
-  uint32_t* s_has = (uint32_t*)(s_pmin + ns1);
-  int32_t* choice = P.match12;  // dist << 16 | i2 per F1 keypoint across the sweeps, -1 none
+  InitLds S;
+  S.keys = (uint32_t*)ismem;
+  S.start = (int*)(S.keys + nk);
+  S.pos = (uint16_t*)(S.start + kCells + 1);
+  S.pmin = S.pos + ((n2 + 1) & ~1);
+  S.has = (uint32_t*)(S.pmin + ns1);
+  return S;
+}
 
-  // ---- F2's level-0 keypoints into the grid (GetFeaturesInArea(x, y, w, 0, 0) sees only those) ----
+// F2's level-0 keypoints into the grid (GetFeaturesInArea(x, y, w, 0, 0) sees only those)
+__device__ void init_grid(const orbx_init_problem& P, const InitLds& S, int tid) {
+  const orbx_proj_frame& F2 = P.f2;
+  const int n2 = F2.n, ns2 = pow2_at_least(n2);
   for (int i = tid; i < ns2; i += IBS) {
     uint32_t key = 0xFFFFFFFFu;
     if (i < n2) {
@@ -635,124 +814,146 @@ __global__ __launch_bounds__(IBS) void k_search_for_initialization(const orbx_in
       if (kp.octave == 0 && px >= 0 && px < ORBX_GRID_COLS && py >= 0 && py < ORBX_GRID_ROWS)
         key = ((uint32_t)(px * ORBX_GRID_ROWS + py) << 13) | (uint32_t)i;
     }
-    s_keys[i] = key;
+    S.keys[i] = key;
   }
   __syncthreads();
-  bitonic_asc(s_keys, ns2);
+  bitonic_asc(S.keys, ns2);
   for (int c = tid; c <= kCells; c += IBS) {
     const uint32_t target = (uint32_t)c << 13;
     int lo = 0, hi = ns2;
     while (lo < hi) {
       const int m = (lo + hi) >> 1;
-      if (s_keys[m] < target) lo = m + 1; else hi = m;
+      if (S.keys[m] < target) lo = m + 1; else hi = m;
     }
-    s_start[c] = lo;
+    S.start[c] = lo;
   }
-  for (int i = tid; i < n2; i += IBS) s_pos[i] = (uint16_t)(s_keys[i] & 0x1FFF);
+  for (int i = tid; i < n2; i += IBS) S.pos[i] = (uint16_t)(S.keys[i] & 0x1FFF);
   __syncthreads();
-  // no chooser before the first sweep
-  for (int p = tid; p < ns1; p += IBS) s_keys[p] = 0xFFFFFFFFu;
-  for (int w = tid; w < (n2 + 31) / 32; w += IBS) s_has[w] = 0;
-  for (int i = tid; i < n1; i += IBS) choice[i] = -1;
-  if (tid < 32) s_hist[tid] = 0;
-  __threadfence_block();
-  __syncthreads();
+}
 
+// F1 keypoint i's choice (dist << 16 | i2, or -1) by a kGroup-lane group against the previous
+// sweep's chooser list
+__device__ __forceinline__ int init_point(const orbx_init_problem& P, const InitLds& S, int i, int gl) {
+  const orbx_proj_frame& F1 = P.f1;
+  const orbx_proj_frame& F2 = P.f2;
+  const int ns1 = pow2_at_least(F1.n);
+  const float r = (float)P.window;
+  int m = -1;
+  if (F1.keys_un[i].octave != 0) return m;
+  const float x = P.prev_matched[2 * i], y = P.prev_matched[2 * i + 1];
+  int x0 = max(0, (int)__builtin_floorf((x - F2.min_x - r) * F2.grid_inv_w));
+  const int x1 = min(ORBX_GRID_COLS - 1, (int)__builtin_ceilf((x - F2.min_x + r) * F2.grid_inv_w));
+  const int y0 = max(0, (int)__builtin_floorf((y - F2.min_y - r) * F2.grid_inv_h));
+  const int y1 = min(ORBX_GRID_ROWS - 1, (int)__builtin_ceilf((y - F2.min_y + r) * F2.grid_inv_h));
+  if (x0 >= ORBX_GRID_COLS || x1 < 0 || y0 >= ORBX_GRID_ROWS || y1 < 0) x0 = x1 + 1;
+  uint64_t dq[4];
+  {
+    const uint64_t* d = (const uint64_t*)(F1.desc + (size_t)i * 32);
+    dq[0] = d[0]; dq[1] = d[1]; dq[2] = d[2]; dq[3] = d[3];
+  }
+  uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+  for (int ix = x0; ix <= x1; ix++) {
+    const int c0 = ix * ORBX_GRID_ROWS;
+    const int pend = S.start[c0 + y1 + 1];
+    for (int p = S.start[c0 + y0] + gl; p < pend; p += kGroup) {
+      const int idx = S.pos[p];
+      const orbx_keypoint& kp = F2.keys_un[idx];
+      if (!(__builtin_fabsf(kp.x - x) < r && __builtin_fabsf(kp.y - y) < r)) continue;
+      const uint64_t* d = (const uint64_t*)(F2.desc + (size_t)idx * 32);
+      const uint64_t dd[4] = {d[0], d[1], d[2], d[3]};
+      const int dist = hamming256(dq, dd);
+      if ((S.has[idx >> 5] >> (idx & 31)) & 1) {  // vMatchedDistance[idx] <= dist: skip
+        const uint32_t key = ((uint32_t)idx << 13) | (uint32_t)i;
+        int lo = 0, hi = ns1;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (S.keys[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        if (lo > 0 && (S.keys[lo - 1] >> 13) == (uint32_t)idx && (int)S.pmin[lo - 1] <= dist) continue;
+      }
+      const uint32_t k = ((uint32_t)dist << 16) | (uint32_t)p;
+      if (k < m1) {
+        m2 = m1;
+        m1 = k;
+      } else if (k < m2) {
+        m2 = k;
+      }
+    }
+  }
+  const uint32_t b1 = group_min(m1);
+  const uint32_t b2 = group_min(m1 == b1 ? m2 : m1);
+  if (b1 != 0xFFFFFFFFu) {
+    const int d1 = (int)(b1 >> 16);
+    const int d2 = b2 == 0xFFFFFFFFu ? INT_MAX : (int)(b2 >> 16);
+    if (d1 <= 50 && (float)d1 < (float)d2 * P.nnratio) m = (d1 << 16) | (int)S.pos[b1 & 0xFFFF];
+  }
+  return m;
+}
+
+// the choosers of the current choices, sorted by (feature, keypoint), with per-feature prefix minima
+__device__ void init_list(const orbx_init_problem& P, const InitLds& S, int tid) {
+  const int n1 = P.f1.n, n2 = P.f2.n, ns1 = pow2_at_least(n1);
+  const int32_t* choice = P.match12;
+  for (int p = tid; p < ns1; p += IBS) {
+    uint32_t key = 0xFFFFFFFFu;
+    if (p < n1) {
+      const int c = choice[p];
+      if (c >= 0) key = ((uint32_t)(c & 0xFFFF) << 13) | (uint32_t)p;
+    }
+    S.keys[p] = key;
+  }
+  for (int w = tid; w < (n2 + 31) / 32; w += IBS) S.has[w] = 0;
+  __syncthreads();
+  bitonic_asc(S.keys, ns1);
+  for (int p = tid; p < ns1; p += IBS) {
+    const uint32_t key = S.keys[p];
+    if (key == 0xFFFFFFFFu) continue;
+    const uint32_t f = key >> 13;
+    int d = choice[key & 0x1FFF] >> 16;
+    for (int q = p - 1; q >= 0 && (S.keys[q] >> 13) == f; q--) d = min(d, choice[S.keys[q] & 0x1FFF] >> 16);
+    S.pmin[p] = (uint16_t)d;
+    atomicOr(&S.has[f >> 5], 1u << (f & 31));
+  }
+  __syncthreads();
+}
+
+// sweeps inside one block from sweep `first` on (S holds the list of the choices before it)
+__device__ void init_sweeps(const orbx_init_problem& P, const InitLds& S, int* s_changed, int first, int tid) {
+  const int n1 = P.f1.n;
+  int32_t* choice = P.match12;
   const int g = tid / kGroup, gl = tid % kGroup;
   constexpr int kGroups = IBS / kGroup;
-  const float r = (float)P.window;
-  for (int sweep = 0; sweep <= n1 + 1; sweep++) {
-    if (tid == 0) s_changed = 0;
+  for (int sweep = first; sweep <= n1 + 1; sweep++) {
+    if (tid == 0) *s_changed = 0;
     __syncthreads();
     int changed = 0;
     for (int i = g; i < n1; i += kGroups) {
-      int m = -1;
-      if (F1.keys_un[i].octave == 0) {
-        const float x = P.prev_matched[2 * i], y = P.prev_matched[2 * i + 1];
-        int x0 = max(0, (int)__builtin_floorf((x - F2.min_x - r) * F2.grid_inv_w));
-        const int x1 = min(ORBX_GRID_COLS - 1, (int)__builtin_ceilf((x - F2.min_x + r) * F2.grid_inv_w));
-        const int y0 = max(0, (int)__builtin_floorf((y - F2.min_y - r) * F2.grid_inv_h));
-        const int y1 = min(ORBX_GRID_ROWS - 1, (int)__builtin_ceilf((y - F2.min_y + r) * F2.grid_inv_h));
-        if (x0 >= ORBX_GRID_COLS || x1 < 0 || y0 >= ORBX_GRID_ROWS || y1 < 0) x0 = x1 + 1;
-        uint64_t dq[4];
-        {
-          const uint64_t* d = (const uint64_t*)(F1.desc + (size_t)i * 32);
-          dq[0] = d[0]; dq[1] = d[1]; dq[2] = d[2]; dq[3] = d[3];
-        }
-        uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
-        for (int ix = x0; ix <= x1; ix++) {
-          const int c0 = ix * ORBX_GRID_ROWS;
-          const int pend = s_start[c0 + y1 + 1];
-          for (int p = s_start[c0 + y0] + gl; p < pend; p += kGroup) {
-            const int idx = s_pos[p];
-            const orbx_keypoint& kp = F2.keys_un[idx];
-            if (!(__builtin_fabsf(kp.x - x) < r && __builtin_fabsf(kp.y - y) < r)) continue;
-            const uint64_t* d = (const uint64_t*)(F2.desc + (size_t)idx * 32);
-            const uint64_t dd[4] = {d[0], d[1], d[2], d[3]};
-            const int dist = hamming256(dq, dd);
-            if ((s_has[idx >> 5] >> (idx & 31)) & 1) {  // vMatchedDistance[idx] <= dist: skip
-              const uint32_t key = ((uint32_t)idx << 13) | (uint32_t)i;
-              int lo = 0, hi = ns1;
-              while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (s_keys[mid] < key) lo = mid + 1; else hi = mid;
-              }
-              if (lo > 0 && (s_keys[lo - 1] >> 13) == (uint32_t)idx && (int)s_pmin[lo - 1] <= dist) continue;
-            }
-            const uint32_t k = ((uint32_t)dist << 16) | (uint32_t)p;
-            if (k < m1) {
-              m2 = m1;
-              m1 = k;
-            } else if (k < m2) {
-              m2 = k;
-            }
-          }
-        }
-        const uint32_t b1 = group_min(m1);
-        const uint32_t b2 = group_min(m1 == b1 ? m2 : m1);
-        if (b1 != 0xFFFFFFFFu) {
-          const int d1 = (int)(b1 >> 16);
-          const int d2 = b2 == 0xFFFFFFFFu ? INT_MAX : (int)(b2 >> 16);
-          if (d1 <= 50 && (float)d1 < (float)d2 * P.nnratio) m = (d1 << 16) | (int)s_pos[b1 & 0xFFFF];
-        }
-      }
+      const int m = init_point(P, S, i, gl);
       if (gl == 0) {
         if (choice[i] != m) changed = 1;
         choice[i] = m;
       }
     }
-    if (changed) s_changed = 1;
+    if (changed) *s_changed = 1;
     __threadfence_block();
     __syncthreads();
-    if (!s_changed) break;
-    // the choosers of this sweep, sorted by (feature, keypoint), with per-feature prefix minima
-    for (int p = tid; p < ns1; p += IBS) {
-      uint32_t key = 0xFFFFFFFFu;
-      if (p < n1) {
-        const int c = choice[p];
-        if (c >= 0) key = ((uint32_t)(c & 0xFFFF) << 13) | (uint32_t)p;
-      }
-      s_keys[p] = key;
-    }
-    for (int w = tid; w < (n2 + 31) / 32; w += IBS) s_has[w] = 0;
-    __syncthreads();
-    bitonic_asc(s_keys, ns1);
-    for (int p = tid; p < ns1; p += IBS) {
-      const uint32_t key = s_keys[p];
-      if (key == 0xFFFFFFFFu) continue;
-      const uint32_t f = key >> 13;
-      int d = choice[key & 0x1FFF] >> 16;
-      for (int q = p - 1; q >= 0 && (s_keys[q] >> 13) == f; q--) d = min(d, choice[s_keys[q] & 0x1FFF] >> 16);
-      s_pmin[p] = (uint16_t)d;
-      atomicOr(&s_has[f >> 5], 1u << (f & 31));
-    }
-    __syncthreads();
+    if (!*s_changed) break;
+    init_list(P, S, tid);
   }
+}
 
-  // ---- final: a feature's last chooser keeps it; rotation histogram over every acceptance ----
-  // (the list in s_keys is the final choices': the last sweep changed nothing)
+// final: a feature's last chooser keeps it; rotation histogram over every acceptance (S.keys holds
+// the final choices' list: the last sweep changed nothing)
+__device__ void init_final(const orbx_init_problem& P, const InitLds& S, int* s_hist, int* s_sel, int* s_count,
+                           int tid) {
+  const orbx_proj_frame& F1 = P.f1;
+  const orbx_proj_frame& F2 = P.f2;
+  const int ns1 = pow2_at_least(F1.n);
+  const int32_t* choice = P.match12;
   int held_i[kInitMaxHeld], held_fin[kInitMaxHeld], held_bin[kInitMaxHeld];
-  if (tid == 0) s_count = 0;
+  if (tid == 0) *s_count = 0;
+  if (tid < 32) s_hist[tid] = 0;
+  __syncthreads();
 #pragma unroll
   for (int k = 0; k < kInitMaxHeld; k++) {
     const int p = tid + k * IBS;
@@ -760,10 +961,10 @@ __global__ __launch_bounds__(IBS) void k_search_for_initialization(const orbx_in
     held_fin[k] = -1;
     held_bin[k] = -1;
     if (p < ns1) {
-      const uint32_t key = s_keys[p];
+      const uint32_t key = S.keys[p];
       if (key != 0xFFFFFFFFu) {
         const int i = (int)(key & 0x1FFF), i2 = choice[i] & 0xFFFF;
-        const bool last = p + 1 == ns1 || (s_keys[p + 1] >> 13) != (key >> 13);
+        const bool last = p + 1 == ns1 || (S.keys[p + 1] >> 13) != (key >> 13);
         held_i[k] = i;
         held_fin[k] = last ? i2 : -1;
         if (P.check_ori) {
@@ -815,14 +1016,172 @@ __global__ __launch_bounds__(IBS) void k_search_for_initialization(const orbx_in
       cnt++;
     }
   }
-  atomicAdd(&s_count, cnt);
+  atomicAdd(s_count, cnt);
   __syncthreads();
-  if (tid == 0) *P.nmatches = s_count;
+  if (tid == 0) *P.nmatches = *s_count;
+}
+
+// no chooser before the first sweep
+__device__ void init_clear(const orbx_init_problem& P, const InitLds& S, int tid) {
+  const int n1 = P.f1.n, n2 = P.f2.n, ns1 = pow2_at_least(n1);
+  for (int p = tid; p < ns1; p += IBS) S.keys[p] = 0xFFFFFFFFu;
+  for (int w = tid; w < (n2 + 31) / 32; w += IBS) S.has[w] = 0;
+  for (int i = tid; i < n1; i += IBS) P.match12[i] = -1;
+  __threadfence_block();
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(IBS) void k_search_for_initialization(const orbx_init_problem* __restrict__ probs) {
+  extern __shared__ __align__(16) uint8_t ismem[];
+  __shared__ int s_changed, s_count;
+  __shared__ int s_hist[32], s_sel[3];
+  const orbx_init_problem& P = probs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const InitLds S = init_lds(ismem, P.f1.n, P.f2.n);
+  init_grid(P, S, tid);
+  init_clear(P, S, tid);
+  init_sweeps(P, S, &s_changed, 0, tid);
+  init_final(P, S, s_hist, s_sel, &s_count, tid);
+}
+
+// ---- one problem over many blocks (the host single call): the F2 grid once (k_init_split_prep,
+// one block), each sweep one launch over kInitSplitBlocks-sized slices of F1 against the chooser
+// list in global memory, the list of a changed sweep rebuilt by one block (k_init_split_list); after
+// kInitSplitSweeps sweeps k_init_split_final (one block) goes on in the single-block way where the
+// choices still change, then the final phase.  Same fixed point: the same answer bit for bit.
+constexpr int kInitSplitSweeps = 3;
+struct InitSplit {
+  uint32_t* keys;   // [kMaxF] the chooser list
+  uint16_t* pmin;   // [kMaxF]
+  uint32_t* has;    // [kMaxF / 32]
+  uint16_t* pos;    // [kMaxF]
+  int* start;       // [kCells + 1]
+  int* changed;     // [kInitSplitSweeps]
+};
+constexpr size_t kInitSplitBytes = 4 * (size_t)kMaxF + 2 * kMaxF + kMaxF / 8 + 2 * kMaxF + 4 * (kCells + 1) + 64 + 6 * 256;
+inline InitSplit init_split_at(uint8_t* d) {
+  size_t o = 0;
+  auto take = [&](size_t b) {
+    uint8_t* p = d + o;
+    o += (b + 255) & ~(size_t)255;
+    return p;
+  };
+  InitSplit S;
+  S.keys = (uint32_t*)take(4 * (size_t)kMaxF);
+  S.pmin = (uint16_t*)take(2 * kMaxF);
+  S.has = (uint32_t*)take(kMaxF / 8);
+  S.pos = (uint16_t*)take(2 * kMaxF);
+  S.start = (int*)take(4 * (kCells + 1));
+  S.changed = (int*)take(64);
+  return S;
+}
+// LDS view S <- global state G (the grid; the list when `list`)
+__device__ void init_load(const orbx_init_problem& P, const InitLds& S, const InitSplit& G, bool list, int tid) {
+  const int n1 = P.f1.n, n2 = P.f2.n, ns1 = pow2_at_least(n1);
+  for (int c = tid; c <= kCells; c += IBS) S.start[c] = G.start[c];
+  for (int i = tid; i < n2; i += IBS) S.pos[i] = G.pos[i];
+  if (list) {
+    for (int p = tid; p < ns1; p += IBS) {
+      S.keys[p] = G.keys[p];
+      S.pmin[p] = G.pmin[p];
+    }
+    for (int w = tid; w < (n2 + 31) / 32; w += IBS) S.has[w] = G.has[w];
+  }
+  __syncthreads();
+}
+__device__ void init_store_list(const orbx_init_problem& P, const InitLds& S, const InitSplit& G, int tid) {
+  const int n1 = P.f1.n, n2 = P.f2.n, ns1 = pow2_at_least(n1);
+  for (int p = tid; p < ns1; p += IBS) {
+    G.keys[p] = S.keys[p];
+    G.pmin[p] = S.pmin[p];
+  }
+  for (int w = tid; w < (n2 + 31) / 32; w += IBS) G.has[w] = S.has[w];
+}
+
+__global__ __launch_bounds__(IBS) void k_init_split_prep(const orbx_init_problem* __restrict__ probs, InitSplit G) {
+  extern __shared__ __align__(16) uint8_t ismem[];
+  const orbx_init_problem& P = probs[0];
+  const int tid = threadIdx.x;
+  const InitLds S = init_lds(ismem, P.f1.n, P.f2.n);
+  init_grid(P, S, tid);
+  for (int c = tid; c <= kCells; c += IBS) G.start[c] = S.start[c];
+  for (int i = tid; i < P.f2.n; i += IBS) G.pos[i] = S.pos[i];
+  init_clear(P, S, tid);
+  init_store_list(P, S, G, tid);
+  if (tid < kInitSplitSweeps) G.changed[tid] = 0;
+}
+
+__global__ __launch_bounds__(IBS) void k_init_split_sweep(const orbx_init_problem* __restrict__ probs, InitSplit G,
+                                                          int sweep) {
+  extern __shared__ __align__(16) uint8_t ismem[];
+  const orbx_init_problem& P = probs[0];
+  if (sweep > 0 && !G.changed[sweep - 1]) return;  // converged
+  const int tid = threadIdx.x;
+  const InitLds S = init_lds(ismem, P.f1.n, P.f2.n);
+  init_load(P, S, G, true, tid);
+  int32_t* choice = P.match12;
+  const int g = blockIdx.x * (IBS / kGroup) + tid / kGroup, gl = tid % kGroup, NG = gridDim.x * (IBS / kGroup);
+  int changed = 0;
+  for (int i = g; i < P.f1.n; i += NG) {
+    const int m = init_point(P, S, i, gl);
+    if (gl == 0) {
+      if (choice[i] != m) changed = 1;
+      choice[i] = m;
+    }
+  }
+  if (changed) G.changed[sweep] = 1;
+}
+
+__global__ __launch_bounds__(IBS) void k_init_split_list(const orbx_init_problem* __restrict__ probs, InitSplit G,
+                                                         int sweep) {
+  extern __shared__ __align__(16) uint8_t ismem[];
+  const orbx_init_problem& P = probs[0];
+  if (!G.changed[sweep]) return;  // unchanged: the stored list is this sweep's too
+  const int tid = threadIdx.x;
+  const InitLds S = init_lds(ismem, P.f1.n, P.f2.n);
+  init_list(P, S, tid);
+  init_store_list(P, S, G, tid);
+}
+
+__global__ __launch_bounds__(IBS) void k_init_split_final(const orbx_init_problem* __restrict__ probs, InitSplit G) {
+  extern __shared__ __align__(16) uint8_t ismem[];
+  __shared__ int s_changed, s_count;
+  __shared__ int s_hist[32], s_sel[3];
+  const orbx_init_problem& P = probs[0];
+  const int tid = threadIdx.x;
+  const InitLds S = init_lds(ismem, P.f1.n, P.f2.n);
+  init_load(P, S, G, true, tid);
+  if (G.changed[kInitSplitSweeps - 1]) init_sweeps(P, S, &s_changed, kInitSplitSweeps, tid);  // block-uniform
+  init_final(P, S, s_hist, s_sel, &s_count, tid);
 }
 
 hipError_t launch_search_by_projection(const ProjProblem* d_probs, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_search_by_projection, dim3(n), dim3(PBS), 0, st, d_probs);
+  return hipGetLastError();
+}
+
+// scratch bytes of one split problem (ProjSplit), 256-B aligned parts
+constexpr size_t kProjSplitBytes = 2 * kMaxF + 256 + (kCells + 1) * 4 + 256 + 3 * (size_t)kMaxF * 4 + 256 + 256;
+inline ProjSplit proj_split_at(uint8_t* d) {
+  ProjSplit S;
+  S.pos = (uint16_t*)d;
+  S.start = (int*)(d + 2 * kMaxF + 256);
+  S.fw = (int*)(d + 2 * kMaxF + 256 + (kCells + 1) * 4 + 256);
+  S.changed = (int*)(d + 2 * kMaxF + 256 + (kCells + 1) * 4 + 256 + 3 * (size_t)kMaxF * 4 + 256);
+  return S;
+}
+
+// One problem over many blocks (the host single call); kind, nP from the host copy of the problem
+hipError_t launch_search_by_projection_split(const ProjProblem* d_prob, int kind, int nP, uint8_t* d_scratch,
+                                             hipStream_t st) {
+  const ProjSplit S = proj_split_at(d_scratch);
+  const int nb = std::min(64, std::max(1, (nP + PBS / kGroup - 1) / (PBS / kGroup)));
+  const bool fuse = kind == ORBX_PROJ_FUSE || kind == ORBX_PROJ_FUSE_SIM3 || kind == ORBX_PROJ_BY_SIM3;
+  hipLaunchKernelGGL(k_proj_split_prep, dim3(nb), dim3(PBS), 0, st, d_prob, S);
+  for (int s = 0; s < (fuse ? 1 : kProjSplitSweeps); s++)
+    hipLaunchKernelGGL(k_proj_split_sweep, dim3(nb), dim3(PBS), 0, st, d_prob, S, s);
+  hipLaunchKernelGGL(k_proj_split_final, dim3(1), dim3(PBS), 0, st, d_prob, S);
   return hipGetLastError();
 }
 
@@ -912,10 +1271,11 @@ extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int
   const size_t a_pm = reserve(nullptr, nP * 4);
   const size_t a_nm = reserve(nullptr, 4);
   const size_t a_prob = reserve(nullptr, sizeof(orbx_proj_problem));
+  const size_t a_split = reserve(nullptr, orbx::kProjSplitBytes);  // device-only scratch (not copied)
   orbx::ScratchGuard g(device);  // pooled lease: no per-call allocation (orbx_scratch.h)
   if (!g.l || g.l->reserve(off, off) != hipSuccess) return ORBX_ERR_HIP;
   uint8_t* hst = g.l->h;
-  std::memset(hst, 0, off);
+  std::memset(hst, 0, a_split);  // (the split scratch is device-only)
   for (const Item& it : items)
     if (it.src && it.bytes) std::memcpy(hst + it.at, it.src, it.bytes);
   uint8_t* d = g.l->d;
@@ -939,8 +1299,10 @@ extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int
   std::memcpy(hst + a_prob, &q, sizeof(q));
   hipStream_t st = g.l->st;
   const size_t o_out = local ? a_trk : a_fout;  // outputs are contiguous up to the descriptor
-  hipError_t e = hipMemcpyAsync(d, hst, off, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = orbx::launch_search_by_projection((const orbx::ProjProblem*)(d + a_prob), 1, st);
+  hipError_t e = hipMemcpyAsync(d, hst, a_split, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = orbx::launch_search_by_projection_split((const orbx::ProjProblem*)(d + a_prob), p->kind, p->n_points,
+                                                d + a_split, st);
   if (e == hipSuccess) e = hipMemcpyAsync(hst + o_out, d + o_out, a_prob - o_out, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = g.l->sync();
   if (e != hipSuccess) return proj_status(e);
@@ -1060,11 +1422,12 @@ extern "C" orbx_status orbx_search_for_initialization(const orbx_init_problem* p
   const size_t a_k2 = at((size_t)n2 * sizeof(orbx_keypoint)), a_d2 = at((size_t)n2 * 32);
   const size_t a_prev = at((size_t)n1 * 8), a_m = at((size_t)n1 * 4 + 4), a_nm = at(4);
   const size_t a_prob = at(sizeof(orbx_init_problem));
+  const size_t a_split = at(orbx::kInitSplitBytes);  // device-only scratch
   orbx::ScratchGuard g(device);
   if (!g.l || g.l->reserve(off, off) != hipSuccess) return ORBX_ERR_HIP;
   uint8_t* h = g.l->h;
   uint8_t* d = g.l->d;
-  std::memset(h, 0, off);
+  std::memset(h, 0, a_split);
   if (n1) {
     std::memcpy(h + a_k1, p->f1.keys_un, (size_t)n1 * sizeof(orbx_keypoint));
     std::memcpy(h + a_d1, p->f1.desc, (size_t)n1 * 32);
@@ -1088,12 +1451,22 @@ extern "C" orbx_status orbx_search_for_initialization(const orbx_init_problem* p
   hipStream_t st = g.l->st;
   const size_t smem = orbx::init_smem_bytes(n1, n2);
   // the dynamic LDS reaches ~79 KB at 8192 features (above the 64 KB default)
-  hipError_t e = hipFuncSetAttribute((const void*)orbx::k_search_for_initialization,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  if (e == hipSuccess) e = hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, st);
+  hipError_t e = hipSuccess;
+  for (const void* k : {(const void*)orbx::k_init_split_prep, (const void*)orbx::k_init_split_sweep,
+                        (const void*)orbx::k_init_split_list, (const void*)orbx::k_init_split_final})
+    if (e == hipSuccess) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (e == hipSuccess) e = hipMemcpyAsync(d, h, a_split, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(orbx::k_search_for_initialization, dim3(1), dim3(orbx::IBS), smem, st,
-                       (const orbx_init_problem*)(d + a_prob));
+    // one problem over many blocks: ~64 F1 keypoints per block per sweep
+    const orbx_init_problem* dp = (const orbx_init_problem*)(d + a_prob);
+    const orbx::InitSplit S = orbx::init_split_at(d + a_split);
+    const int nb = std::min(64, std::max(1, (n1 + orbx::IBS / orbx::kGroup - 1) / (orbx::IBS / orbx::kGroup)));
+    hipLaunchKernelGGL(orbx::k_init_split_prep, dim3(1), dim3(orbx::IBS), smem, st, dp, S);
+    for (int s = 0; s < orbx::kInitSplitSweeps; s++) {
+      hipLaunchKernelGGL(orbx::k_init_split_sweep, dim3(nb), dim3(orbx::IBS), smem, st, dp, S, s);
+      hipLaunchKernelGGL(orbx::k_init_split_list, dim3(1), dim3(orbx::IBS), smem, st, dp, S, s);
+    }
+    hipLaunchKernelGGL(orbx::k_init_split_final, dim3(1), dim3(orbx::IBS), smem, st, dp, S);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemcpyAsync(h + a_prev, d + a_prev, a_prob - a_prev, hipMemcpyDeviceToHost, st);

@@ -565,10 +565,9 @@ class Optimizer:
             self._stop = None
 
     def set_debug_options(self, **kw):
-        """Test / A-B options of this solver handle (include/orbx_debug.h, orbx_ba_debug_options:
-        host_lm, no_spec, host_struct, no_fuse, no_camfold, no_psfold, ldlt, nan_trial,
-        raise_stop_after, trace); no arguments restore the production defaults."""
-        o = _lib.BaDebugOptions(0, 0, 0, 0, 0, 0, 0, -1, -1, 0)
+        """Test options of this solver handle (include/orbx_debug.h, orbx_ba_debug_options: ldlt,
+        nan_trial, raise_stop_after, trace); no arguments restore the production defaults."""
+        o = _lib.BaDebugOptions(0, -1, -1, 0)
         for k, v in kw.items():
             if k not in dict(o._fields_):
                 raise TypeError("unknown LocalBA debug option %r" % k)

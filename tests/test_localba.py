@@ -237,68 +237,11 @@ def test_gpu_localba_stop_and_degenerate(ba):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,kw", [(7, {}), (10, {}), (8, dict(n_local=30, n_fixed=4, n_points=4000))])
-def test_gpu_localba_speculative_linearization_bit_identical(ba, seed, kw):
-    """Linearising the next iteration into the second buffer set while the host reads a
-    trial back (default) gives bit-identical poses, points, outlier flags and LM counts
-    to the in-line path (debug options host_lm + no_spec)."""
-    P = synth.localba_problem(seed=seed, **kw)
-    a = ba.LocalBundleAdjustment(P)
-    with ba.debug_options(host_lm=1):
-        h = ba.LocalBundleAdjustment(P)
-    with ba.debug_options(host_lm=1, no_spec=1):
-        b = ba.LocalBundleAdjustment(P)
-    for o in (h, b):
-        for k in ("Tcw_d", "Xw_d", "edge_outlier"):
-            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(o[k]))
-        assert list(a["iterations"]) == list(o["iterations"]) and a["trials"] == o["trials"]
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(REJECT_CASES))
 def test_gpu_localba_rejections_match_oracle(ba, name):
-    """Rejected trials (pop + lambda *= ni, with a speculative linearisation launched on the
-    trial state that is then discarded) and the _nBad early stop: GPU = oracle, and the
-    speculative path = the in-line path (debug options host_lm + no_spec) bit for bit."""
+    """Rejected trials (pop + lambda *= ni) and the _nBad early stop: GPU = oracle."""
     P = reject_problem(name)
-    a = ba.LocalBundleAdjustment(P)
-    _compare(a, oracle.local_ba(P))
-    with ba.debug_options(host_lm=1, no_spec=1):
-        b = ba.LocalBundleAdjustment(P)
-    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
-        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
-    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", ["config4", "small", "many_kfs", "no_outliers", "all_fixed", "empty", "one_edge"])
-def test_gpu_localba_device_structure_bit_identical(ba, case):
-    """The per-phase active-edge structure built on the device (k_ba_struct: point
-    segments, pose indices, pose-grouped positions, pair-table offsets) gives
-    bit-identical poses, points, outlier flags and LM counts to the host build
-    (debug option host_struct), both phases (phase 2 reads the outlier flags on the device)."""
-    if case == "config4":
-        P = synth.localba_problem(seed=7)
-    elif case == "many_kfs":
-        P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
-    elif case == "no_outliers":
-        P = small_problem(seed=6, outlier_frac=0.0)
-    else:
-        P = dict(small_problem(seed=12))
-        if case == "all_fixed":
-            P["fixed"] = np.ones(len(P["fixed"]), np.uint8)
-        elif case in ("empty", "one_edge"):
-            n = 0 if case == "empty" else 1
-            for k in ("edge_point", "edge_cam", "obs", "inv_sigma2"):
-                P[k] = np.ascontiguousarray(np.asarray(P[k])[:n])
-    a = ba.LocalBundleAdjustment(P)
-    with ba.debug_options(host_struct=1):
-        b = ba.LocalBundleAdjustment(P)
-    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
-        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
-    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
-    if case in ("config4", "small"):
-        _compare(a, oracle.local_ba(P))
+    _compare(ba.LocalBundleAdjustment(P), oracle.local_ba(P))
 
 
 @pytest.mark.gpu
@@ -347,59 +290,6 @@ def test_gpu_reduced_system_ldlt_zero_pivot(gpu, kernel):
     rc = _lib.lib().orbx_debug_ldlt_ex(_lib.ptr(S), _lib.ptr(np.ones(N)), N, _lib.ptr(x), 1, C.byref(ms),
                                        LDLT_KIND[kernel], None)
     assert rc == _lib.ORBX_ERR_STATE if hasattr(_lib, "ORBX_ERR_STATE") else rc == -6
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", ["config4", "rejects"])
-def test_gpu_localba_fused_point_side_bit_identical(ba, case):
-    """The fused point side of iteration-start trials (k_ba_lin_schur: linearisation, point sums,
-    D^-1 and B D^-1 in one kernel) gives the same bits, iterations and trials as the three
-    separate kernels (debug option no_fuse)."""
-    P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(sorted(REJECT_CASES)[0])
-    a = ba.LocalBundleAdjustment(P)
-    with ba.debug_options(no_fuse=1):
-        b = ba.LocalBundleAdjustment(P)
-    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
-        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
-    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", ["config4", "rejects"])
-@pytest.mark.parametrize("switch", ["no_camfold", "no_psfold"])
-def test_gpu_localba_trial_folds_bit_identical(ba, case, switch):
-    """Device-LM trials sum the pose terms inside k_ba_pairs and finish Hpp / b_p inside
-    k_ba_schur_fin (no k_ba_cam_sum / k_ba_cam_fin launches), and k_ba_lin_schur also does the
-    point side of trials that do not relinearise (no k_ba_point_schur launch): same bits,
-    iterations and trials as with the separate kernels (debug options no_camfold / no_psfold)."""
-    P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(sorted(REJECT_CASES)[0])
-    a = ba.LocalBundleAdjustment(P)
-    with ba.debug_options(**{switch: 1}):
-        b = ba.LocalBundleAdjustment(P)
-    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
-        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
-    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", ["config4", "many_kfs"] + sorted(REJECT_CASES))
-def test_gpu_localba_device_lm_bit_identical(ba, case):
-    """LM control on the device (k_ba_lm_control: accept/reject, lambda, the trial budget,
-    rho == 0 and _nBad, trials queued without a host round trip) gives the same bits,
-    iterations and trials as the host-controlled loop (debug option host_lm)."""
-    if case == "config4":
-        P = synth.localba_problem(seed=7)
-    elif case == "many_kfs":
-        P = synth.localba_problem(seed=8, n_local=30, n_fixed=4, n_points=4000)
-    else:
-        P = reject_problem(case)
-    a = ba.LocalBundleAdjustment(P)
-    with ba.debug_options(host_lm=1):
-        b = ba.LocalBundleAdjustment(P)
-    for k in ("Tcw_d", "Xw_d", "edge_outlier"):
-        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
-    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
-    assert a["chi2"] == b["chi2"]
 
 
 @pytest.mark.gpu
@@ -460,16 +350,14 @@ def test_gpu_localba_nan_trial(ba, case, trial, monkeypatch):
     iteration while the phase goes on: g2o pops it and the next iteration recomputes the errors
     at the restored state before linearising.  The device LM loop pauses the phase for exactly
     that (restore, errors, k_ba_lm_resume): GPU = oracle (1e-4, identical counts and outliers),
-    device loop = host loop (debug option host_lm) bit for bit, batched = single bit for bit."""
+    batched = single bit for bit."""
     P = synth.localba_problem(seed=7) if case == "config4" else reject_problem(case)
     monkeypatch.setenv("ORBX_BA_NAN_TRIAL", str(trial))  # the oracle's hook (test infrastructure)
     with ba.debug_options(nan_trial=trial):
         a = ba.LocalBundleAdjustment(P)
         many = ba.LocalBundleAdjustmentMany([P, small_problem(seed=12)])
     _compare(a, oracle.local_ba(P))
-    with ba.debug_options(nan_trial=trial, host_lm=1):
-        b = ba.LocalBundleAdjustment(P)
-    for o in (b, many[0]):
+    for o in (many[0],):
         for k in ("Tcw_d", "Xw_d", "edge_outlier"):
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(o[k]))
         assert list(a["iterations"]) == list(o["iterations"]) and a["trials"] == o["trials"]
