@@ -153,6 +153,14 @@ __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {  // min over the l
   return v;
 }
 
+#ifdef ORBX_STEREO_ROWS_PROBE
+// Probe build only (tools/stereo_floor.sh): the row origins of every keypoint that reaches the SAD
+// staging, and k_stereo_rows_only, which loads exactly those 11 + 11 rows and nothing else -- its
+// FETCH_SIZE is the sector-granular floor of the refinement's reads.
+constexpr int kProbeFrames = 256, kProbeKps = 2048;
+__device__ uint2 g_rows_probe[kProbeFrames * kProbeKps];  // (rowL0 - imL, rowR0 - imR + 1), 0: not staged
+#endif
+
 __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
   constexpr int NQ = SBS / 16;                // quarters (keypoints) per block
   __shared__ uint32_t s_raw[NQ][11 * kSadDw];  // per quarter: 11 rows x (4 left + 6 right) dwords
@@ -236,6 +244,10 @@ __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geo
   uint32_t* sp = s_raw[qb];
   const uint8_t* rowL0 = imL + (size_t)(cy - w) * lw + (cxL - w);
   const uint8_t* rowR0 = imR + (size_t)(cy - w) * lw + (cxR0 - 2 * w);
+#ifdef ORBX_STEREO_ROWS_PROBE
+  if (ql == 0 && f < kProbeFrames && iL < kProbeKps)
+    g_rows_probe[f * kProbeKps + iL] = make_uint2((uint32_t)(rowL0 - imL), (uint32_t)(rowR0 - imR) + 1u);
+#endif
   {
     constexpr int IT = (11 * kSadDw + 15) / 16;
     uint32_t sv[IT];
@@ -414,6 +426,35 @@ __global__ __launch_bounds__(SBS) void k_hamming(const uint8_t* __restrict__ a, 
   out[i] = hamming256(x, y);
 }
 
+#ifdef ORBX_STEREO_ROWS_PROBE
+// one lane per left keypoint: the staged rows exactly as k_stereo_match loads them (11 rows of 4 left
+// and 6 right dwords at the 4-aligned row starts, bytes outside the span skipped as there)
+__global__ __launch_bounds__(256) void k_stereo_rows_only(StereoArgs A, const Geometry* __restrict__ G,
+                                                          uint32_t* sink) {
+  const int f = blockIdx.y, iL = blockIdx.x * 256 + threadIdx.x;
+  const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
+  if (iL >= nL || f >= kProbeFrames || iL >= kProbeKps) return;
+  const uint2 rec = g_rows_probe[f * kProbeKps + iL];
+  g_rows_probe[f * kProbeKps + iL] = make_uint2(0u, 0u);
+  if (rec.y == 0) return;
+  const orbx_keypoint kp = (A.kpL + (size_t)f * A.kL_stride)[iL];
+  const LevelGeom& Lv = G->lv[kp.octave];
+  const int limg = f * A.l_step + A.l_off, rimg = f * A.r_step + A.r_off;
+  const uint8_t* rowL0 = level_ptr(*G, A.BL, limg, kp.octave) + rec.x;
+  const uint8_t* rowR0 = level_ptr(*G, A.BR, rimg, kp.octave) + (rec.y - 1u);
+  uint32_t x = 0;
+  for (int r = 0; r < 11; r++) {
+    for (int side = 0; side < 2; side++) {
+      const uintptr_t a = (uintptr_t)((side ? rowR0 : rowL0) + (size_t)r * Lv.w);
+      const int need = side ? 21 : 11, nd = side ? kSadDwR : kSadDwL;
+      for (int jj = 0; jj < nd; jj++)
+        if (4 * jj < (int)(a & 3) + need) x ^= *((const uint32_t*)(a & ~(uintptr_t)3) + jj);
+    }
+  }
+  if (x == 0x9E3779B9u) sink[0] = x;  // keeps the loads
+}
+#endif
+
 hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, int maxL, hipStream_t st,
                          StageTimer* T) {
   T->begin(st);
@@ -426,6 +467,10 @@ hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, 
   T->begin(st);
   hipLaunchKernelGGL(k_stereo_finalize, dim3(n_frames), dim3(SBS), 0, st, A);
   T->end(ST_STEREO_FINAL, st);
+#ifdef ORBX_STEREO_ROWS_PROBE
+  hipLaunchKernelGGL(k_stereo_rows_only, dim3((maxL + 255) / 256, n_frames), dim3(256), 0, st, A, Gd,
+                     (uint32_t*)A.nmatches);
+#endif
   return hipGetLastError();
 }
 
