@@ -21,8 +21,6 @@
 //   k_ba_lm_control  the LM verdict on the device: partials summed in block order,
 //                    accept/reject, lambda/ni, trial budget, _nBad, stop flag polled
 //                    through host-mapped memory; gates the next trial's kernels
-//                    (ORBX_BA_HOST_LM=1: the same decisions on the host, one
-//                    readback per trial)
 // Every reduction has a fixed partition and order: results are run-to-run
 // identical, with no cross-block atomics (an agent-scope release/acquire per
 // block costs an L2 writeback/invalidate on the multi-XCD part).
@@ -1757,6 +1755,7 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
     __syncthreads();
     LDLT_TS(2 + 2 * M);
     if (2 * (M + 1) < Tc) panel_rows(M + 1, (M & 1) ? Lp : Lp2, (M & 1) ? Vp : Vp2);
+    LDLT_TS(32 + M);  // (thread 0 is always a panel-row thread: the rows' chain ends here)
     trailing(M, Lc, Vc, 2 * M + 4, Tc);
     __syncthreads();
     LDLT_TS(3 + 2 * M);
@@ -1767,12 +1766,16 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
     return;
   }
   if (tid >= 64) return;
-  // L^T x = y in 8-row blocks from the bottom: the block's eight y values (final once the rows
-  // below are done) are read out of their lanes, every lane solves the 8x8 unit upper system
-  // L_KK^T x_K = y_K the same way, then rows above take y_i -= sum_u L[k0+u][i] x_u.  A block's
-  // entries are loaded while the previous block runs (two register sets, the loop unrolled by
-  // two); loads are clamped to written entries and need no masks: rows past N have x = 0, and
-  // lanes at or below the block keep their value by a select.
+  // L^T x = y one row at a time from the bottom: x_k = y_k (final once every row below is done) is
+  // read out of its lane and each lane takes y_i -= L[k][i] x_k for its rows i < k.  Per row the
+  // dependent chain is one lane read and one FMA; rows are loaded eight ahead (the lgkmcnt window
+  // is 15) and the reads run past row k's k entries into the next rows or the panel arrays
+  // (written LDS): they are masked where they are used -- a select right after a load would wait
+  // for it there -- and the loops have no branches, so the waits stay per group of eight rows.
+  // Two phases by the 64-row group of k, so that each row needs no select of its y register and
+  // phase 2 (k < 64) leaves the upper group alone.
+  // (The 8-row blocked form -- readlanes of a block, an 8x8 unit triangular solve, two register
+  // sets of 44 LDS reads -- took 1.5k cycles per block, 24k of the kernel's 100k at N = 120.)
   const int lane = tid;
   double y[R];
 #pragma unroll
@@ -1780,63 +1783,48 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
     const int i = lane + 64 * r;
     y[r] = i < N ? ys[i] : 0.0;
   }
-  const int nb = (N + 7) / 8;
-  // (row k's reads run past its k entries into the next rows or the panel arrays after the
-  // factor -- LDS that is written and finite; those terms are discarded by the selects below)
-  auto load_blk = [&](int K, double (&Lkk)[28], double (&Lr)[8][R]) {
-    const int k0 = 8 * K;
+  static_assert(R == 2, "the two-phase row loop below: rows 64.. then 0..63");
+  auto row_ptr = [&](int k) { return Lpk + (size_t)max(k, 1) * (max(k, 1) - 1) / 2; };
+  constexpr int kAhead = 8;  // rows loaded ahead (<= 15 LDS reads in flight)
+  LDLT_TS(48);
+  // phase 1: rows k = K1 .. 64 (K1 >= N - 1; rows k >= N have x_k = y_k = 0 and change nothing):
+  // x_k sits in y[1]; rows i < 64 always take the update, rows i >= 64 only when i < k
+  {
+    const int K1 = 64 + 8 * ((max(N - 64, 0) + 7) / 8) - 1;
+    double L0[kAhead], L1[kAhead];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int k = k0 + u;
-      const double* Lk = Lpk + k * (k - 1) / 2;
-#pragma unroll
-      for (int v = 0; v < u; v++) Lkk[ldlt_tri(u - 1, v)] = Lk[k0 + v];  // L[k0+u][k0+v]
-#pragma unroll
-      for (int r = 0; r < R; r++) Lr[u][r] = Lk[lane + 64 * r];  // L[k0+u][i]
+    for (int u = 0; u < kAhead; u++) {
+      const double* Lk = row_ptr(K1 - u);
+      L0[u] = Lk[lane];
+      L1[u] = Lk[lane + 64];
     }
-  };
-  auto solve_blk = [&](int K, const double (&Lkk)[28], const double (&Lr)[8][R]) {
-    const int k0 = 8 * K, rb = k0 >> 6;  // the block's rows sit in y[rb] (8 | 64)
-    double x[8];
-    const double yb = rb == 0 ? y[0] : R == 2 || rb == 1 ? y[1] : y[R - 1];
+    for (int k0 = K1; k0 >= 64; k0 -= kAhead) {
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const double xv = readlane_d(yb, (k0 + u) & 63);
-      x[u] = k0 + u < N ? xv : 0.0;  // rows past N (their x stays out of every sum)
-    }
-#pragma unroll
-    for (int u = 6; u >= 0; u--)
-#pragma unroll
-      for (int v = 7; v > u; v--) x[u] = __builtin_fma(-Lkk[ldlt_tri(v - 1, u)], x[v], x[u]);
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int i = lane + 64 * r;
-      double s0 = Lr[0][r] * x[0], s1 = Lr[1][r] * x[1];
-      s0 = __builtin_fma(Lr[2][r], x[2], s0);
-      s1 = __builtin_fma(Lr[3][r], x[3], s1);
-      s0 = __builtin_fma(Lr[4][r], x[4], s0);
-      s1 = __builtin_fma(Lr[5][r], x[5], s1);
-      s0 = __builtin_fma(Lr[6][r], x[6], s0);
-      s1 = __builtin_fma(Lr[7][r], x[7], s1);
-      const double yn = y[r] - (s0 + s1);
-      y[r] = i < k0 ? yn : y[r];
-      if (r == rb) {  // uniform: the block's own rows take x
-        const int u = lane & 7;
-        double xv = x[0];
-#pragma unroll
-        for (int w = 1; w < 8; w++) xv = u == w ? x[w] : xv;
-        y[r] = ((lane ^ k0) & ~7 & 63) == 0 ? xv : y[r];
+      for (int u = 0; u < kAhead; u++) {
+        const int k = k0 - u;
+        const double xk = readlane_d(y[1], k - 64);
+        y[0] = __builtin_fma(-L0[u], xk, y[0]);
+        y[1] = __builtin_fma(lane + 64 < k ? -L1[u] : 0.0, xk, y[1]);
+        const double* Lk = row_ptr(k - kAhead);  // (rows below 64 of the next group: unused)
+        L0[u] = Lk[lane];
+        L1[u] = Lk[lane + 64];
       }
     }
-  };
-  double LkA[28], LrA[8][R], LkB[28], LrB[8][R];
-  load_blk(nb - 1, LkA, LrA);
-  for (int K = nb - 1; K >= 0; K -= 2) {
-    if (K >= 1) load_blk(K - 1, LkB, LrB);
-    solve_blk(K, LkA, LrA);
-    if (K < 1) break;
-    if (K >= 2) load_blk(K - 2, LkA, LrA);
-    solve_blk(K - 1, LkB, LrB);
+  }
+  // phase 2: rows k = 63 .. 0, x_k in y[0]; rows i >= 64 are final
+  {
+    double L0[kAhead];
+#pragma unroll
+    for (int u = 0; u < kAhead; u++) L0[u] = row_ptr(63 - u)[lane];
+    for (int k0 = 63; k0 >= 0; k0 -= kAhead) {
+#pragma unroll
+      for (int u = 0; u < kAhead; u++) {
+        const int k = k0 - u;
+        const double xk = readlane_d(y[0], k);
+        y[0] = __builtin_fma(lane < k ? -L0[u] : 0.0, xk, y[0]);
+        L0[u] = row_ptr(k - kAhead)[lane];  // (k - kAhead < 1: unused)
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < R; r++)
@@ -1928,6 +1916,11 @@ struct LdltPlan {
 };
 
 constexpr int kUpCh = 2048;  // k_ba_update: positions per LDS chunk (48 KB)
+// k_ba_update: points per block (all LBS threads form the position products): 64 points take one
+// round of position products per block and four times the blocks (10.8 -> 7.4 us at config 4;
+// 32 points: 7.0 us, within the spread)
+constexpr int kUpPts = 64;
+static_assert(kUpPts <= LBS, "one thread per point");
 // back-substitution + update (push first) + LM scale, skipped when the solve failed
 // (scal[2] == 0).  Blocks: the active poses first (their se3 exp chains then overlap the point
 // blocks), then LBS active points per block; one LM-scale partial per block.
@@ -1980,8 +1973,8 @@ __device__ __forceinline__ void k_ba_update_body(const BaDev& D, double lambda) 
       }
     }
   } else {
-    const int i0 = (blockIdx.x - npb) * LBS, i = i0 + threadIdx.x, i1 = min(i0 + LBS, D.npa);
-    const bool pt = i < D.npa;
+    const int i0 = (blockIdx.x - npb) * kUpPts, i = i0 + threadIdx.x, i1 = min(i0 + kUpPts, D.npa);
+    const bool pt = (int)threadIdx.x < kUpPts && i < D.npa;
     const int ic = pt ? i : i0;  // (i0 < npa in a point block) loads stay in range
     // everything that depends on neither the solve's flag nor the LM state, issued first
     const int p = D.pt_id[ic];
@@ -2109,6 +2102,39 @@ __device__ inline double seq_sum_wave(const double* p, int n) {
   return s;
 }
 
+// Two such sums at once (same orders and bits as two seq_sum_wave calls): both arrays' loads are
+// in flight together and lane 0 adds the first while lane 1 adds the second (valid in lane 0).
+__device__ inline void seq_sum2_wave(const double* p, int n, const double* q, int m, double& sp, double& sq) {
+  __shared__ double buf[2][512];
+  double s = 0;
+  const int len = max(n, m);
+  for (int base = 0; base < len; base += 512) {
+    const int cn = min(512, n - base), cm = min(512, m - base);  // (may be <= 0)
+    double vp[8], vq[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {  // clamped, unpredicated loads: all sixteen in flight at once
+      const int i = threadIdx.x + 64 * u;
+      vp[u] = p[max(min(base + i, n - 1), 0)];
+      vq[u] = q[max(min(base + i, m - 1), 0)];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int i = threadIdx.x + 64 * u;
+      if (i < cn) buf[0][i] = vp[u];
+      if (i < cm) buf[1][i] = vq[u];
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const double* bb = buf[threadIdx.x];
+      const int c = threadIdx.x == 0 ? cn : cm;
+      for (int i = 0; i < c; i++) s += bb[i];
+    }
+    __syncthreads();
+  }
+  sp = s;
+  sq = __shfl(s, 1, 64);
+}
+
 __device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations) {
   LmState* L = const_cast<LmState*>(D.lm);
   const double a = seq_sum_wave(D.scal + 8, D.nbe);
@@ -2143,8 +2169,8 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
   // serves both of the loop's polls below; a flag raised after it is seen at the next trial)
   const bool st = stop() || (D.raise_after >= 0 && L->trials >= D.raise_after);  // (+ test hook)
   const double* p = D.scal + 8;
-  const double b = seq_sum_wave(p + D.nbe, D.nbe);
-  const double u = seq_sum_wave(p + 2 * D.nbe, nbu);
+  double b, u;
+  seq_sum2_wave(p + D.nbe, D.nbe, p + 2 * D.nbe, nbu, b, u);
   if (threadIdx.x != 0) return;
   L->rejected = 0;
   const bool ok2 = D.scal[2] != 0.0;
@@ -2934,7 +2960,7 @@ struct LocalBA {
     D.gpart = c.gpart.p;
     // readback block: scal[0..7], then errors partials (2 slots of nbe), then update partials
     D.nbe = std::max((na + LBS - 1) / LBS, 1);
-    nbu = std::max((nposes + LBS - 1) / LBS + (npa + LBS - 1) / LBS, 1);  // k_ba_update: pose blocks, then point blocks
+    nbu = std::max((nposes + LBS - 1) / LBS + (npa + kUpPts - 1) / kUpPts, 1);  // k_ba_update: pose blocks, then point blocks
     D.nbu = nbu;
     n_rb = 8 + 2 * D.nbe + nbu;
     BA_CHECK(c.scal.alloc(n_rb));

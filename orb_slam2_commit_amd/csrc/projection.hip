@@ -643,13 +643,25 @@ struct ProjSplit {
   int* fw;         // [3][kMaxF]
   int* changed;    // [kProjSplitSweeps]
 };
+// scratch bytes of one split problem (ProjSplit), 256-B aligned parts; problem z of a launch
+// (blockIdx.z, the problems of one host call: SearchBySim3's two directions) at z * kProjSplitBytes
+constexpr size_t kProjSplitBytes = 2 * kMaxF + 256 + (kCells + 1) * 4 + 256 + 3 * (size_t)kMaxF * 4 + 256 + 256;
+__host__ __device__ inline ProjSplit proj_split_at(uint8_t* d) {
+  ProjSplit S;
+  S.pos = (uint16_t*)d;
+  S.start = (int*)(d + 2 * kMaxF + 256);
+  S.fw = (int*)(d + 2 * kMaxF + 256 + (kCells + 1) * 4 + 256);
+  S.changed = (int*)(d + 2 * kMaxF + 256 + (kCells + 1) * 4 + 256 + 3 * (size_t)kMaxF * 4 + 256);
+  return S;
+}
 
-__global__ __launch_bounds__(PBS) void k_proj_split_prep(const ProjProblem* __restrict__ probs, ProjSplit S) {
+__global__ __launch_bounds__(PBS) void k_proj_split_prep(const ProjProblem* __restrict__ probs, uint8_t* scratch) {
   __shared__ uint32_t s_keys[kMaxF];
   __shared__ uint16_t s_pos[kMaxF];
   __shared__ int s_start[kCells + 1];
   __shared__ float s_Tcw[16];
-  const ProjProblem& P = probs[0];
+  const ProjProblem& P = probs[blockIdx.z];
+  const ProjSplit S = proj_split_at(scratch + blockIdx.z * kProjSplitBytes);
   const int tid = threadIdx.x, nF = proj_nF(P), nP = proj_nP(P);
   const int gt = blockIdx.x * PBS + tid, gs = gridDim.x * PBS;
   for (int f = gt; f < nF; f += gs) {
@@ -672,13 +684,14 @@ __global__ __launch_bounds__(PBS) void k_proj_split_prep(const ProjProblem* __re
   }
 }
 
-__global__ __launch_bounds__(PBS) void k_proj_split_sweep(const ProjProblem* __restrict__ probs, ProjSplit S,
+__global__ __launch_bounds__(PBS) void k_proj_split_sweep(const ProjProblem* __restrict__ probs, uint8_t* scratch,
                                                           int sweep) {
   __shared__ int s_fw[kMaxF];
   __shared__ uint16_t s_pos[kMaxF];
   __shared__ int s_start[kCells + 1];
   __shared__ float s_Tcw[16];
-  const ProjProblem& P = probs[0];
+  const ProjProblem& P = probs[blockIdx.z];
+  const ProjSplit S = proj_split_at(scratch + blockIdx.z * kProjSplitBytes);
   if (sweep > 0 && !__atomic_load_n(&S.changed[sweep - 1], __ATOMIC_RELAXED)) return;  // converged
   const int tid = threadIdx.x, nF = proj_nF(P), nP = proj_nP(P);
   const int* fwr = S.fw + (sweep % 3) * kMaxF;
@@ -710,7 +723,7 @@ __global__ __launch_bounds__(PBS) void k_proj_split_sweep(const ProjProblem* __r
   if (changed) S.changed[sweep] = 1;
 }
 
-__global__ __launch_bounds__(PBS) void k_proj_split_final(const ProjProblem* __restrict__ probs, ProjSplit S) {
+__global__ __launch_bounds__(PBS) void k_proj_split_final(const ProjProblem* __restrict__ probs, uint8_t* scratch) {
   __shared__ int s_fw[kMaxF];
   __shared__ uint16_t s_pos[kMaxF];
   __shared__ int s_start[kCells + 1];
@@ -718,7 +731,8 @@ __global__ __launch_bounds__(PBS) void k_proj_split_final(const ProjProblem* __r
   __shared__ int s_sel[3];
   __shared__ int s_changed, s_count, s_drop;
   __shared__ float s_Tcw[16];
-  const ProjProblem& P = probs[0];
+  const ProjProblem& P = probs[blockIdx.z];
+  const ProjSplit S = proj_split_at(scratch + blockIdx.z * kProjSplitBytes);
   const int tid = threadIdx.x, nF = proj_nF(P), nP = proj_nP(P);
   const ProjMode M = proj_mode(P);
   // the split sweeps stop at kProjSplitSweeps; a problem still changing goes on here, from the
@@ -1161,27 +1175,21 @@ hipError_t launch_search_by_projection(const ProjProblem* d_probs, int n, hipStr
   return hipGetLastError();
 }
 
-// scratch bytes of one split problem (ProjSplit), 256-B aligned parts
-constexpr size_t kProjSplitBytes = 2 * kMaxF + 256 + (kCells + 1) * 4 + 256 + 3 * (size_t)kMaxF * 4 + 256 + 256;
-inline ProjSplit proj_split_at(uint8_t* d) {
-  ProjSplit S;
-  S.pos = (uint16_t*)d;
-  S.start = (int*)(d + 2 * kMaxF + 256);
-  S.fw = (int*)(d + 2 * kMaxF + 256 + (kCells + 1) * 4 + 256);
-  S.changed = (int*)(d + 2 * kMaxF + 256 + (kCells + 1) * 4 + 256 + 3 * (size_t)kMaxF * 4 + 256);
-  return S;
-}
-
-// One problem over many blocks (the host single call); kind, nP from the host copy of the problem
-hipError_t launch_search_by_projection_split(const ProjProblem* d_prob, int kind, int nP, uint8_t* d_scratch,
-                                             hipStream_t st) {
-  const ProjSplit S = proj_split_at(d_scratch);
-  const int nb = std::min(64, std::max(1, (nP + PBS / kGroup - 1) / (PBS / kGroup)));
-  const bool fuse = kind == ORBX_PROJ_FUSE || kind == ORBX_PROJ_FUSE_SIM3 || kind == ORBX_PROJ_BY_SIM3;
-  hipLaunchKernelGGL(k_proj_split_prep, dim3(nb), dim3(PBS), 0, st, d_prob, S);
+// nprob problems (d_prob[0..nprob), scratch z at d_scratch + z * kProjSplitBytes), each split over
+// many blocks: the host single calls.  kinds / nP from the host copies of the problems.
+hipError_t launch_search_by_projection_split(const ProjProblem* d_prob, const int* kinds, const int* nPs, int nprob,
+                                             uint8_t* d_scratch, hipStream_t st) {
+  int nPmax = 0;
+  bool fuse = true;
+  for (int z = 0; z < nprob; z++) {
+    nPmax = std::max(nPmax, nPs[z]);
+    fuse = fuse && (kinds[z] == ORBX_PROJ_FUSE || kinds[z] == ORBX_PROJ_FUSE_SIM3 || kinds[z] == ORBX_PROJ_BY_SIM3);
+  }
+  const int nb = std::min(64, std::max(1, (nPmax + PBS / kGroup - 1) / (PBS / kGroup)));
+  hipLaunchKernelGGL(k_proj_split_prep, dim3(nb, 1, nprob), dim3(PBS), 0, st, d_prob, d_scratch);
   for (int s = 0; s < (fuse ? 1 : kProjSplitSweeps); s++)
-    hipLaunchKernelGGL(k_proj_split_sweep, dim3(nb), dim3(PBS), 0, st, d_prob, S, s);
-  hipLaunchKernelGGL(k_proj_split_final, dim3(1), dim3(PBS), 0, st, d_prob, S);
+    hipLaunchKernelGGL(k_proj_split_sweep, dim3(nb, 1, nprob), dim3(PBS), 0, st, d_prob, d_scratch, s);
+  hipLaunchKernelGGL(k_proj_split_final, dim3(1, 1, nprob), dim3(PBS), 0, st, d_prob, d_scratch);
   return hipGetLastError();
 }
 
@@ -1234,16 +1242,19 @@ orbx_status proj_check(const orbx_proj_problem& p, bool host) {
 
 }  // namespace
 
-extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int device) {
-  if (!p) return ORBX_ERR_ARG;
-  const orbx_status chk = proj_check(*p, true);
-  if (chk != ORBX_OK) return chk;
+namespace {
+// The host single calls: n problems (1, or SearchBySim3's two directions) staged in one pooled
+// arena -- every problem's inputs, then every problem's outputs, then the n device descriptors,
+// then the device-only split scratch -- one upload, one split launch set over blockIdx.z, one
+// download of the outputs, one sync.
+orbx_status proj_run_host(const orbx_proj_problem* const* ps, int n, int device) {
+  for (int z = 0; z < n; z++) {
+    const orbx_status chk = proj_check(*ps[z], true);
+    if (chk != ORBX_OK) return chk;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_NODEV;
   if (device < 0 || device >= ndev || hipSetDevice(device) != hipSuccess) return ORBX_ERR_ARG;
-  const size_t nF = (size_t)p->f.n, nP = (size_t)p->n_points;
-  const bool local = p->kind == ORBX_PROJ_LOCAL;
-  // one arena: inputs, outputs, problem descriptor
   size_t off = 0;
   struct Item { const void* src; size_t bytes; size_t at; };
   std::vector<Item> items;
@@ -1254,66 +1265,100 @@ extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int
     off += bytes;
     return at;
   };
-  const size_t a_keys = reserve(p->f.keys_un, nF * sizeof(orbx_keypoint));
-  const size_t a_fdesc = reserve(p->f.desc, nF * 32);
-  const size_t a_ur = p->f.u_right ? reserve(p->f.u_right, nF * 4) : 0;
-  const size_t a_occ = p->f.occ ? reserve(p->f.occ, nF) : 0;
-  const size_t a_desc = reserve(p->desc, nP * 32);
-  const size_t a_flags = reserve(p->flags, nP);
-  const size_t a_pos = p->pos ? reserve(p->pos, nP * 12) : 0;
-  const size_t a_nrm = p->normal ? reserve(p->normal, nP * 12) : 0;
-  const size_t a_dmm = p->dist_minmax ? reserve(p->dist_minmax, nP * 8) : 0;
-  const size_t a_ang = p->angle ? reserve(p->angle, nP * 4) : 0;
-  const size_t a_oct = p->octave ? reserve(p->octave, nP * 4) : 0;
-  const size_t a_trk = local ? reserve(p->frustum ? nullptr : p->track, nP * 16) : 0;
-  const size_t a_lvl = local ? reserve(p->frustum ? nullptr : p->track_level, nP * 4) : 0;
-  const size_t a_fout = reserve(nullptr, nF * 4);
-  const size_t a_pm = reserve(nullptr, nP * 4);
-  const size_t a_nm = reserve(nullptr, 4);
-  const size_t a_prob = reserve(nullptr, sizeof(orbx_proj_problem));
-  const size_t a_split = reserve(nullptr, orbx::kProjSplitBytes);  // device-only scratch (not copied)
+  struct Lay {
+    size_t keys, fdesc, ur, occ, desc, flags, pos, nrm, dmm, ang, oct, trk, lvl, fout, pm, nm;
+  };
+  Lay L[2];
+  for (int z = 0; z < n; z++) {  // inputs
+    const orbx_proj_problem* p = ps[z];
+    const size_t nF = (size_t)p->f.n, nP = (size_t)p->n_points;
+    Lay& a = L[z];
+    a.keys = reserve(p->f.keys_un, nF * sizeof(orbx_keypoint));
+    a.fdesc = reserve(p->f.desc, nF * 32);
+    a.ur = p->f.u_right ? reserve(p->f.u_right, nF * 4) : 0;
+    a.occ = p->f.occ ? reserve(p->f.occ, nF) : 0;
+    a.desc = reserve(p->desc, nP * 32);
+    a.flags = reserve(p->flags, nP);
+    a.pos = p->pos ? reserve(p->pos, nP * 12) : 0;
+    a.nrm = p->normal ? reserve(p->normal, nP * 12) : 0;
+    a.dmm = p->dist_minmax ? reserve(p->dist_minmax, nP * 8) : 0;
+    a.ang = p->angle ? reserve(p->angle, nP * 4) : 0;
+    a.oct = p->octave ? reserve(p->octave, nP * 4) : 0;
+  }
+  off = (off + 255) & ~(size_t)255;
+  const size_t o_out = off;  // outputs are contiguous from here up to the descriptors
+  for (int z = 0; z < n; z++) {
+    const orbx_proj_problem* p = ps[z];
+    const size_t nF = (size_t)p->f.n, nP = (size_t)p->n_points;
+    const bool local = p->kind == ORBX_PROJ_LOCAL;
+    Lay& a = L[z];
+    a.trk = local ? reserve(p->frustum ? nullptr : p->track, nP * 16) : 0;  // (in / out)
+    a.lvl = local ? reserve(p->frustum ? nullptr : p->track_level, nP * 4) : 0;
+    a.fout = reserve(nullptr, nF * 4);
+    a.pm = reserve(nullptr, nP * 4);
+    a.nm = reserve(nullptr, 4);
+  }
+  const size_t a_prob = reserve(nullptr, sizeof(orbx_proj_problem) * n);
+  const size_t a_split = reserve(nullptr, orbx::kProjSplitBytes * n);  // device-only scratch (not copied)
   orbx::ScratchGuard g(device);  // pooled lease: no per-call allocation (orbx_scratch.h)
   if (!g.l || g.l->reserve(off, off) != hipSuccess) return ORBX_ERR_HIP;
   uint8_t* hst = g.l->h;
-  std::memset(hst, 0, a_split);  // (the split scratch is device-only)
+  std::memset(hst, 0, a_split);
   for (const Item& it : items)
     if (it.src && it.bytes) std::memcpy(hst + it.at, it.src, it.bytes);
   uint8_t* d = g.l->d;
-  orbx_proj_problem q = *p;
-  q.f.keys_un = (const orbx_keypoint*)(d + a_keys);
-  q.f.desc = d + a_fdesc;
-  q.f.u_right = p->f.u_right ? (const float*)(d + a_ur) : nullptr;
-  q.f.occ = p->f.occ ? (const int8_t*)(d + a_occ) : nullptr;
-  q.desc = d + a_desc;
-  q.flags = d + a_flags;
-  q.pos = p->pos ? (const float*)(d + a_pos) : nullptr;
-  q.normal = p->normal ? (const float*)(d + a_nrm) : nullptr;
-  q.dist_minmax = p->dist_minmax ? (const float*)(d + a_dmm) : nullptr;
-  q.angle = p->angle ? (const float*)(d + a_ang) : nullptr;
-  q.octave = p->octave ? (const int32_t*)(d + a_oct) : nullptr;
-  q.track = local ? (float*)(d + a_trk) : nullptr;
-  q.track_level = local ? (int32_t*)(d + a_lvl) : nullptr;
-  q.frame_out = (int32_t*)(d + a_fout);
-  q.point_match = (int32_t*)(d + a_pm);
-  q.nmatches = (int32_t*)(d + a_nm);
-  std::memcpy(hst + a_prob, &q, sizeof(q));
+  int kinds[2], nPs[2];
+  for (int z = 0; z < n; z++) {
+    const orbx_proj_problem* p = ps[z];
+    const Lay& a = L[z];
+    const bool local = p->kind == ORBX_PROJ_LOCAL;
+    orbx_proj_problem q = *p;
+    q.f.keys_un = (const orbx_keypoint*)(d + a.keys);
+    q.f.desc = d + a.fdesc;
+    q.f.u_right = p->f.u_right ? (const float*)(d + a.ur) : nullptr;
+    q.f.occ = p->f.occ ? (const int8_t*)(d + a.occ) : nullptr;
+    q.desc = d + a.desc;
+    q.flags = d + a.flags;
+    q.pos = p->pos ? (const float*)(d + a.pos) : nullptr;
+    q.normal = p->normal ? (const float*)(d + a.nrm) : nullptr;
+    q.dist_minmax = p->dist_minmax ? (const float*)(d + a.dmm) : nullptr;
+    q.angle = p->angle ? (const float*)(d + a.ang) : nullptr;
+    q.octave = p->octave ? (const int32_t*)(d + a.oct) : nullptr;
+    q.track = local ? (float*)(d + a.trk) : nullptr;
+    q.track_level = local ? (int32_t*)(d + a.lvl) : nullptr;
+    q.frame_out = (int32_t*)(d + a.fout);
+    q.point_match = (int32_t*)(d + a.pm);
+    q.nmatches = (int32_t*)(d + a.nm);
+    std::memcpy(hst + a_prob + z * sizeof(orbx_proj_problem), &q, sizeof(q));
+    kinds[z] = p->kind;
+    nPs[z] = p->n_points;
+  }
   hipStream_t st = g.l->st;
-  const size_t o_out = local ? a_trk : a_fout;  // outputs are contiguous up to the descriptor
   hipError_t e = hipMemcpyAsync(d, hst, a_split, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
-    e = orbx::launch_search_by_projection_split((const orbx::ProjProblem*)(d + a_prob), p->kind, p->n_points,
-                                                d + a_split, st);
+    e = orbx::launch_search_by_projection_split((const orbx::ProjProblem*)(d + a_prob), kinds, nPs, n, d + a_split, st);
   if (e == hipSuccess) e = hipMemcpyAsync(hst + o_out, d + o_out, a_prob - o_out, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = g.l->sync();
   if (e != hipSuccess) return proj_status(e);
-  if (nF) std::memcpy(p->frame_out, hst + a_fout, nF * 4);
-  if (nP) std::memcpy(p->point_match, hst + a_pm, nP * 4);
-  std::memcpy(p->nmatches, hst + a_nm, 4);
-  if (local && p->frustum && nP) {
-    std::memcpy(p->track, hst + a_trk, nP * 16);
-    std::memcpy(p->track_level, hst + a_lvl, nP * 4);
+  for (int z = 0; z < n; z++) {
+    const orbx_proj_problem* p = ps[z];
+    const Lay& a = L[z];
+    const size_t nF = (size_t)p->f.n, nP = (size_t)p->n_points;
+    if (nF) std::memcpy(p->frame_out, hst + a.fout, nF * 4);
+    if (nP) std::memcpy(p->point_match, hst + a.pm, nP * 4);
+    std::memcpy(p->nmatches, hst + a.nm, 4);
+    if (p->kind == ORBX_PROJ_LOCAL && p->frustum && nP) {
+      std::memcpy(p->track, hst + a.trk, nP * 16);
+      std::memcpy(p->track_level, hst + a.lvl, nP * 4);
+    }
   }
   return ORBX_OK;
+}
+}  // namespace
+
+extern "C" orbx_status orbx_search_by_projection(const orbx_proj_problem* p, int device) {
+  if (!p) return ORBX_ERR_ARG;
+  return proj_run_host(&p, 1, device);
 }
 
 extern "C" orbx_status orbx_search_by_projection_device(const orbx_proj_problem* problems, int n, void* stream) {
@@ -1364,8 +1409,9 @@ extern "C" orbx_status orbx_search_by_sim3(const orbx_sim3_problem* p, int devic
   std::vector<int32_t> m1(N1 > 0 ? N1 : 1, -1), m2(N2 > 0 ? N2 : 1, -1);
   std::vector<int32_t> fo1(N2 > 0 ? N2 : 1), fo2(N1 > 0 ? N1 : 1);
   int32_t n1 = 0, n2 = 0;
+  orbx_proj_problem qs[2];
   for (int d = 0; d < 2; d++) {
-    orbx_proj_problem q;
+    orbx_proj_problem& q = qs[d];
     std::memset(&q, 0, sizeof(q));
     q.kind = ORBX_PROJ_BY_SIM3;
     q.f = d == 0 ? p->kf2 : p->kf1;
@@ -1382,9 +1428,10 @@ extern "C" orbx_status orbx_search_by_sim3(const orbx_sim3_problem* p, int devic
     q.frame_out = d == 0 ? fo1.data() : fo2.data();
     q.point_match = d == 0 ? m1.data() : m2.data();
     q.nmatches = d == 0 ? &n1 : &n2;
-    const orbx_status st = orbx_search_by_projection(&q, device);
-    if (st != ORBX_OK) return st;
   }
+  const orbx_proj_problem* qp[2] = {&qs[0], &qs[1]};
+  const orbx_status st = proj_run_host(qp, 2, device);  // both directions in one upload / launch set
+  if (st != ORBX_OK) return st;
   // mutual check (:1466-1482)
   int nFound = 0;
   for (int i1 = 0; i1 < N1; i1++) {
