@@ -154,11 +154,18 @@ __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {  // min over the l
 }
 
 #ifdef ORBX_STEREO_ROWS_PROBE
-// Probe build only (tools/stereo_floor.sh): the row origins of every keypoint that reaches the SAD
-// staging, and k_stereo_rows_only, which loads exactly those 11 + 11 rows and nothing else -- its
-// FETCH_SIZE is the sector-granular floor of the refinement's reads.
-constexpr int kProbeFrames = 256, kProbeKps = 2048;
+// Probe build only (tools/stereo_floor.py): the row origins of every keypoint that reaches the SAD
+// staging (k_stereo_match records them), then
+//   k_stereo_rows_only  the staging loads alone, in k_stereo_match's grid, block order and lane
+//                       pattern (its FETCH_SIZE: what those reads cost as the match kernel issues them)
+//   k_stereo_rows_mark  every 64-B sector those reads touch, marked once in per-buffer bitmaps, and
+//   k_stereo_rows_count the marked sectors and 128-B lines counted: the unique-sector floor of the
+//                       refinement's reads (orbx_debug_stereo_floor reads the totals).
+constexpr int kProbeFrames = 512, kProbeKps = 2048;
 __device__ uint2 g_rows_probe[kProbeFrames * kProbeKps];  // (rowL0 - imL, rowR0 - imR + 1), 0: not staged
+constexpr int kProbeWords = 1 << 20;                      // per bitmap: 32M sectors (2 GiB of image)
+__device__ uint32_t g_probe_bits[4][kProbeWords];         // L input, L pyramid, R input, R pyramid
+__device__ unsigned long long g_probe_count[3];           // sectors, lines, staged keypoints
 #endif
 
 __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geometry* __restrict__ G) {
@@ -192,6 +199,9 @@ __global__ __launch_bounds__(SBS, 8) void k_stereo_match(StereoArgs A, const Geo
     *outD = -1.0f;
     *outS = -1;
   }
+#ifdef ORBX_STEREO_ROWS_PROBE
+  if (ql == 0 && f < kProbeFrames && iL < kProbeKps) g_rows_probe[f * kProbeKps + iL] = make_uint2(0u, 0u);
+#endif
   if (maxU < 0) return;
   const uint32_t t3[3] = {lrg.x, lrg.y, lrg.z};
   int rb[3], re[3];
@@ -427,31 +437,81 @@ __global__ __launch_bounds__(SBS) void k_hamming(const uint8_t* __restrict__ a, 
 }
 
 #ifdef ORBX_STEREO_ROWS_PROBE
-// one lane per left keypoint: the staged rows exactly as k_stereo_match loads them (11 rows of 4 left
-// and 6 right dwords at the 4-aligned row starts, bytes outside the span skipped as there)
-__global__ __launch_bounds__(256) void k_stereo_rows_only(StereoArgs A, const Geometry* __restrict__ G,
-                                                          uint32_t* sink) {
-  const int f = blockIdx.y, iL = blockIdx.x * 256 + threadIdx.x;
-  const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
-  if (iL >= nL || f >= kProbeFrames || iL >= kProbeKps) return;
+// the staged reads of keypoint (f, iL): calls fn(side, level 0?, dword address) for each dword k_stereo_match
+// loads (11 rows x 4 left / 6 right dwords at the 4-aligned row starts, dwords past the span skipped)
+template <typename Fn>
+__device__ inline void probe_rows(const StereoArgs& A, const Geometry* G, int f, int iL, int ql, Fn fn) {
   const uint2 rec = g_rows_probe[f * kProbeKps + iL];
-  g_rows_probe[f * kProbeKps + iL] = make_uint2(0u, 0u);
   if (rec.y == 0) return;
   const orbx_keypoint kp = (A.kpL + (size_t)f * A.kL_stride)[iL];
-  const LevelGeom& Lv = G->lv[kp.octave];
   const int limg = f * A.l_step + A.l_off, rimg = f * A.r_step + A.r_off;
   const uint8_t* rowL0 = level_ptr(*G, A.BL, limg, kp.octave) + rec.x;
   const uint8_t* rowR0 = level_ptr(*G, A.BR, rimg, kp.octave) + (rec.y - 1u);
+  const int lw = G->lv[kp.octave].w, w = 5;
+  constexpr int IT = (11 * kSadDw + 15) / 16;
+#pragma unroll
+  for (int k = 0; k < IT; k++) {
+    const int q = ql + 16 * k, r = q / kSadDw, j = q - r * kSadDw;
+    const bool left = j < kSadDwL;
+    const uintptr_t a = (uintptr_t)((left ? rowL0 : rowR0) + (size_t)r * lw);
+    const int jj = left ? j : j - kSadDwL, need = left ? 2 * w + 1 : 4 * w + 1;
+    if (q < 11 * kSadDw && 4 * jj < (int)(a & 3) + need)
+      fn(left ? 0 : 1, kp.octave == 0, (a & ~(uintptr_t)3) + 4 * (uintptr_t)jj);
+  }
+}
+
+__global__ __launch_bounds__(SBS) void k_stereo_rows_only(StereoArgs A, const Geometry* __restrict__ G, uint32_t* sink) {
+  constexpr int NQ = SBS / 16;
+  const int2 bi = xcd_block2();
+  const int f = bi.y, tid = threadIdx.x, ql = tid & 15, qb = tid >> 4;
+  const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
+  const int iL = bi.x * NQ + qb;
+  if (iL >= nL || f >= kProbeFrames || iL >= kProbeKps) return;
   uint32_t x = 0;
-  for (int r = 0; r < 11; r++) {
-    for (int side = 0; side < 2; side++) {
-      const uintptr_t a = (uintptr_t)((side ? rowR0 : rowL0) + (size_t)r * Lv.w);
-      const int need = side ? 21 : 11, nd = side ? kSadDwR : kSadDwL;
-      for (int jj = 0; jj < nd; jj++)
-        if (4 * jj < (int)(a & 3) + need) x ^= *((const uint32_t*)(a & ~(uintptr_t)3) + jj);
+  probe_rows(A, G, f, iL, ql, [&](int, bool, uintptr_t a) { x ^= *(const uint32_t*)a; });
+  if (x == 0x9E3779B9u) sink[0] = x;  // keeps the loads
+}
+
+// bitmap slot of a dword address: which buffer (level 0 = the input images, else the pyramid) of
+// which side, and the 64-B sector index from the buffer's start
+__device__ inline void probe_mark(const StereoArgs& A, int side, bool l0, uintptr_t a) {
+  const BatchPtrs& B = side ? A.BR : A.BL;
+  const int m = 2 * side + (l0 ? 0 : 1);
+  const uintptr_t off = a - (l0 ? (uintptr_t)B.in : (uintptr_t)B.pyr);
+  const unsigned long long sec = off >> 6;
+  if (sec < 32ull * kProbeWords) atomicOr(&g_probe_bits[m][sec >> 5], 1u << (sec & 31));
+}
+
+__global__ __launch_bounds__(SBS) void k_stereo_rows_mark(StereoArgs A, const Geometry* __restrict__ G) {
+  constexpr int NQ = SBS / 16;
+  const int f = blockIdx.y, tid = threadIdx.x, ql = tid & 15, qb = tid >> 4;
+  const int nL = min(A.nL[(size_t)f * A.n_stride_L], A.maxL);
+  const int iL = blockIdx.x * NQ + qb;
+  if (iL >= nL || f >= kProbeFrames || iL >= kProbeKps) return;
+  if (ql == 0 && g_rows_probe[f * kProbeKps + iL].y) atomicAdd(&g_probe_count[2], 1ull);
+  probe_rows(A, G, f, iL, ql, [&](int side, bool l0, uintptr_t a) { probe_mark(A, side, l0, a); });
+}
+
+// counts the marked sectors and 128-B lines and clears the bitmaps for the next call
+__global__ __launch_bounds__(256) void k_stereo_rows_count() {
+  unsigned long long s = 0, l = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < 4 * kProbeWords; i += gridDim.x * 256) {
+    uint32_t* wp = &g_probe_bits[i / kProbeWords][i % kProbeWords];
+    const uint32_t v = *wp;
+    if (v) {
+      s += __popc(v);
+      l += __popc((v | (v >> 1)) & 0x55555555u);
+      *wp = 0;
     }
   }
-  if (x == 0x9E3779B9u) sink[0] = x;  // keeps the loads
+  for (int o = 32; o > 0; o >>= 1) {  // wave sums, one atomic per wave
+    s += __shfl_down(s, o, 64);
+    l += __shfl_down(l, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (s || l)) {
+    atomicAdd(&g_probe_count[0], s);
+    atomicAdd(&g_probe_count[1], l);
+  }
 }
 #endif
 
@@ -468,8 +528,9 @@ hipError_t launch_stereo(const StereoArgs& A, const Geometry* Gd, int n_frames, 
   hipLaunchKernelGGL(k_stereo_finalize, dim3(n_frames), dim3(SBS), 0, st, A);
   T->end(ST_STEREO_FINAL, st);
 #ifdef ORBX_STEREO_ROWS_PROBE
-  hipLaunchKernelGGL(k_stereo_rows_only, dim3((maxL + 255) / 256, n_frames), dim3(256), 0, st, A, Gd,
-                     (uint32_t*)A.nmatches);
+  hipLaunchKernelGGL(k_stereo_rows_only, dim3(max(nb, 1), n_frames), dim3(SBS), 0, st, A, Gd, (uint32_t*)A.nmatches);
+  hipLaunchKernelGGL(k_stereo_rows_mark, dim3(max(nb, 1), n_frames), dim3(SBS), 0, st, A, Gd);
+  hipLaunchKernelGGL(k_stereo_rows_count, dim3(1024), dim3(256), 0, st);
 #endif
   return hipGetLastError();
 }
@@ -481,3 +542,16 @@ hipError_t launch_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* ou
 }
 
 }  // namespace orbx
+
+#ifdef ORBX_STEREO_ROWS_PROBE
+// probe builds only: totals since the last call (64-B sectors, 128-B lines, staged keypoints), reset
+extern "C" int orbx_debug_stereo_floor(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  unsigned long long h[3] = {0, 0, 0};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(orbx::g_probe_count), sizeof(h)) != hipSuccess) return -1;
+  const unsigned long long z[3] = {0, 0, 0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(orbx::g_probe_count), z, sizeof(z)) != hipSuccess) return -1;
+  for (int i = 0; i < 3; i++) out[i] = h[i];
+  return 0;
+}
+#endif
