@@ -1085,14 +1085,12 @@ __global__ __launch_bounds__(kPB) void k_ba_pairs_many(const BaDev* __restrict__
 // Reduced system from the chunk partials: blocks b < nblk write Hschur block
 // (c1, c2) = [c1==c2](Hpp + lambda I) - pair sum (both triangles, so every
 // entry of S is written); blocks b >= nblk write bs = bp - sum cf.
-__device__ __forceinline__ void k_ba_schur_fin_body(const BaDev& D, double lambda) {
-  if (lm_skip(D) || (int)blockIdx.x >= D.nblk + D.nposes) return;
-  lambda = lm_lambda(D, lambda);
-  const int j = threadIdx.x, S = D.gsplit;
+__device__ inline void schur_fin_block(const BaDev& D, int blk, int j, double lambda) {
+  const int S = D.gsplit;
   const bool cam = D.camfold && !lm_skip_lin(D);  // k_ba_cam_fin's sums (chunk order) done here
   const double* camp = D.gpart + cam_part_off(D);
-  if ((int)blockIdx.x >= D.nblk) {
-    const int ci = blockIdx.x - D.nblk;
+  if (blk >= D.nblk) {
+    const int ci = blk - D.nblk;
     if (j < 6) {
       double t = 0;
       for (int c = 0; c < S; c++) t += D.gpart[(size_t)D.nblk * S * 36 + ((size_t)ci * S + c) * 6 + j];
@@ -1110,9 +1108,9 @@ __device__ __forceinline__ void k_ba_schur_fin_body(const BaDev& D, double lambd
   }
   if (j >= 36) return;
   int c1;
-  const int c2 = tri_decode(blockIdx.x, D.nposes, c1);
+  const int c2 = tri_decode(blk, D.nposes, c1);
   double v = 0;
-  for (int c = 0; c < S; c++) v += D.gpart[((size_t)blockIdx.x * S + c) * 36 + j];
+  for (int c = 0; c < S; c++) v += D.gpart[((size_t)blk * S + c) * 36 + j];
   const int N = 6 * D.nposes;
   const int r = j / 6, c = j % 6;
   double sv;
@@ -1132,6 +1130,10 @@ __device__ __forceinline__ void k_ba_schur_fin_body(const BaDev& D, double lambd
     D.S[(size_t)(6 * c2 + c) * N + 6 * c1 + r] = sv;
   }
   D.S[(size_t)(6 * c1 + r) * N + 6 * c2 + c] = sv;
+}
+__device__ __forceinline__ void k_ba_schur_fin_body(const BaDev& D, double lambda) {
+  if (lm_skip(D) || (int)blockIdx.x >= D.nblk + D.nposes) return;
+  schur_fin_block(D, blockIdx.x, threadIdx.x, lm_lambda(D, lambda));
 }
 __global__ __launch_bounds__(64) void k_ba_schur_fin(BaDev D, double lambda) { k_ba_schur_fin_body(D, lambda); }
 __global__ __launch_bounds__(64) void k_ba_schur_fin_many(const BaDev* __restrict__ Ds, double lambda) {
@@ -1552,19 +1554,26 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_col_many(const BaDev* __restrict
 //      diagonal block and its own row from LDS, factors the diagonal block in registers (every
 //      such thread the same way: no cross-lane broadcast on the pivot chain) and solves its row:
 //      L_i (scaled) and V_i = L_i D (unscaled) to LDS, L_i also into the packed factor;
-//   C  every register tile right of the panel takes A -= L_rows V_cols^T (8 FMAs per entry, the
-//      tile stays in registers: only the panel rows move through LDS), and the tiles of the next
-//      panel publish themselves.
+//   C  every register tile right of the next panel takes A -= L_rows V_cols^T (8 FMAs per entry,
+//      the tile stays in registers: only the panel rows move through LDS); the tiles of the panel
+//      after next publish themselves once updated and leave the registers;
+//   A  (before B of panel M+1) panel M's update of panel M+1's eight columns, in LDS, by every
+//      thread: two entries of one row each, so it costs ~16 FMAs per thread instead of the
+//      128 of a register tile's look-ahead in one wave (1.5k cycles per panel).
+// Panel values are double-buffered (panel M+1 in one buffer while panel M+2 is published into the
+// other) and so are L / V (panel M's are read by C while B writes panel M+1's).  Every entry sees
+// the same updates in the same order as the register path: results are unchanged bit for bit.
 // Two barriers per eight pivots.  The augmented row ends as y = D^-1 L^-1 b, and wave 0 solves
 // L^T x = y.  Failure rule as the other kernels: an exactly zero pivot fails the solve.
-// LDS: packed strictly-lower L (N(N-1)/2), the panel values / L / V ((Np+8) x 8 each), y (N).
+// LDS: packed strictly-lower L (N(N-1)/2), two panel-value, two L and two V arrays ((Np+8) x 8
+// each), y (N).
 __host__ __device__ inline int ldlt_pan_rows(int N) { return ldlt_np4(N) + 8; }
 // panel arrays: rows of 8 doubles in groups of four, each group padded to 34 doubles, so that
 // the lanes of a wave reading different row groups spread over the LDS banks
 __host__ __device__ inline int ldlt_prow(int i) { return (i >> 2) * 34 + (i & 3) * 8; }
 __host__ __device__ inline int ldlt_pan_arr(int N) { return ldlt_pan_rows(N) / 4 * 34; }
-inline size_t ldlt_pan_smem(int N) {  // (+ the look-ahead's second L / V panel set)
-  return ((size_t)N * (N - 1) / 2 + 5 * (size_t)ldlt_pan_arr(N) + N) * sizeof(double);
+inline size_t ldlt_pan_smem(int N) {
+  return ((size_t)N * (N - 1) / 2 + 6 * (size_t)ldlt_pan_arr(N) + N) * sizeof(double);
 }
 // (one tile per thread: with two the trailing update doubles and the panel kernel loses to the
 // column-step one, e.g. 91 us at N = 126)
@@ -1586,8 +1595,9 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   double* Lp = Pn + PA;                         // panel L (scaled)
   double* Vp = Lp + PA;                         // panel V = L D (unscaled)
   double* ys = Vp + PA;                         // [N] y = D^-1 L^-1 b
-  double* Lp2 = ys + N;                         // the look-ahead's second L / V set
+  double* Lp2 = ys + N;                         // the second L / V set
   double* Vp2 = Lp2 + PA;
+  double* Pn2 = Vp2 + PA;                       // the second panel-value buffer
   double a[TPT][4][4];
   int ti[TPT], tk[TPT];
   LDLT_TS(0);
@@ -1617,14 +1627,15 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   }
   // (the tile loads above are in flight while the panel arrays are cleared)
   for (int j = tid; j < 3 * PA; j += NT) Pn[j] = 0.0;  // padding rows / columns stay finite
-  for (int j = tid; j < 2 * PA; j += NT) Lp2[j] = 0.0;
+  for (int j = tid; j < 3 * PA; j += NT) Lp2[j] = 0.0;
   __syncthreads();
 #pragma unroll
-  for (int t = 0; t < TPT; t++) {
-    if (tk[t] >= 0 && tk[t] < 2) {
+  for (int t = 0; t < TPT; t++) {  // panels 0 and 1 (tile columns 0..3) publish and leave the registers
+    if (tk[t] >= 0 && tk[t] < 4) {
+      double* P = tk[t] < 2 ? Pn : Pn2;
 #pragma unroll
       for (int p = 0; p < 4; p++) {
-        double2_t* dst = reinterpret_cast<double2_t*>(Pn + ldlt_prow(4 * ti[t] + p) + 4 * tk[t]);
+        double2_t* dst = reinterpret_cast<double2_t*>(P + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] & 1));
         dst[0] = double2_t{a[t][p][0], a[t][p][1]};
         dst[1] = double2_t{a[t][p][2], a[t][p][3]};
       }
@@ -1633,21 +1644,21 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   __syncthreads();
   LDLT_TS(1);
   // B: the panel rows of panel M into (Lq, Vq)
-  auto panel_rows = [&](int M, double* Lq, double* Vq) {
+  auto panel_rows = [&](int M, const double* Pq, double* Lq, double* Vq) {
     const int c0 = 8 * M, w = min(8, N - c0);
     const int i = c0 + tid;
     if (i <= N) {
       double Dm[36], u[8];
 #pragma unroll
       for (int r = 0; r < 8; r++) {
-        const double2_t* src = reinterpret_cast<const double2_t*>(Pn + ldlt_prow(c0 + r));
+        const double2_t* src = reinterpret_cast<const double2_t*>(Pq + ldlt_prow(c0 + r));
         const double2_t v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
         const double row[8] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
 #pragma unroll
         for (int c = 0; c <= r; c++) Dm[ldlt_tri(r, c)] = row[c];
       }
       {
-        const double2_t* src = reinterpret_cast<const double2_t*>(Pn + ldlt_prow(i));
+        const double2_t* src = reinterpret_cast<const double2_t*>(Pq + ldlt_prow(i));
         const double2_t v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
         u[0] = v0.x, u[1] = v0.y, u[2] = v1.x, u[3] = v1.y, u[4] = v2.x, u[5] = v2.y, u[6] = v3.x, u[7] = v3.y;
       }
@@ -1694,12 +1705,12 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
       }
     }
   };
-  // C: the register tiles in tile columns [tlo, thi) right of panel M take A -= L_rows V_cols^T;
-  // the tiles of the next panel (tile columns 2M+2, 2M+3) publish themselves
-  auto trailing = [&](int M, const double* Lq, const double* Vq, int tlo, int thi) {
+  // C: the register tiles right of panel M+1 (tile columns >= 2M+4) take A -= L_rows V_cols^T;
+  // those of panel M+2 (tile columns 2M+4, 2M+5) then publish themselves into Pq and retire
+  auto trailing = [&](int M, const double* Lq, const double* Vq, double* Pq) {
 #pragma unroll
     for (int t = 0; t < TPT; t++) {
-      if (tk[t] >= 2 * M + 2 && tk[t] >= tlo && tk[t] < thi) {
+      if (tk[t] >= 2 * M + 4) {
         const double* lr = Lq + 34 * ti[t];
         const double* vr = Vq + 34 * tk[t];
 #pragma unroll
@@ -1720,10 +1731,10 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
 #pragma unroll
               for (int q = 0; q < 4; q++) a[t][p][q] = __builtin_fma(-Lv[p][s], Vv[q][s], a[t][p][q]);
         }
-        if (tk[t] < 2 * M + 4) {  // the next panel publishes itself
+        if (tk[t] < 2 * M + 6) {  // panel M+2 publishes itself
 #pragma unroll
           for (int p = 0; p < 4; p++) {
-            double2_t* dst = reinterpret_cast<double2_t*>(Pn + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] - 2 * M - 2));
+            double2_t* dst = reinterpret_cast<double2_t*>(Pq + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] & 1));
             dst[0] = double2_t{a[t][p][0], a[t][p][1]};
             dst[1] = double2_t{a[t][p][2], a[t][p][3]};
           }
@@ -1731,36 +1742,45 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
       }
     }
   };
-#ifdef ORBX_LDLT_NO_LOOKAHEAD
-  for (int M = 0; 2 * M < Tc; M++) {
-    panel_rows(M, Lp, Vp);
-    __syncthreads();
-    LDLT_TS(2 + 2 * M);
-    trailing(M, Lp, Vp, 0, Tc);
-    __syncthreads();
-    LDLT_TS(3 + 2 * M);
-  }
-#else
-  // Look-ahead by one panel: the next panel's two tile columns take panel M's update first and
-  // publish; then panel M+1's rows (the redundant 8x8 factor chain) run while every other tile
-  // takes panel M's update.  L / V of consecutive panels alternate between two LDS sets (the
-  // trailing update of panel M still reads its set while panel M+1's rows fill the other).  Each
-  // tile sees the same updates in the same order as without look-ahead: bit-identical.
-  panel_rows(0, Lp, Vp);
+  // A: panel M's update of panel M+1's values in Pq (rows c1 = 8(M+1) .. N, eight columns): thread
+  // -> (row c1 + tid / 4, columns 2 (tid % 4), +1), the s = 0..7 FMAs in the register path's order
+  auto lookahead = [&](const double* Lq, const double* Vq, double* Pq, int c1) {
+    const int i = c1 + tid / 4, j0 = 2 * (tid & 3);
+    if (i <= N) {
+      const double2_t* ls = reinterpret_cast<const double2_t*>(Lq + ldlt_prow(i));
+      const double2_t* va = reinterpret_cast<const double2_t*>(Vq + ldlt_prow(c1 + j0));
+      const double2_t* vb = reinterpret_cast<const double2_t*>(Vq + ldlt_prow(c1 + j0 + 1));
+      double2_t* dst = reinterpret_cast<double2_t*>(Pq + ldlt_prow(i) + j0);
+      double2_t x = *dst;
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const double2_t l = ls[h], u = va[h], v = vb[h];
+        x.x = __builtin_fma(-l.x, u.x, x.x);
+        x.y = __builtin_fma(-l.x, v.x, x.y);
+        x.x = __builtin_fma(-l.y, u.y, x.x);
+        x.y = __builtin_fma(-l.y, v.y, x.y);
+      }
+      *dst = x;
+    }
+  };
+  static_assert(NT / 4 >= 120, "one look-ahead pass covers rows 8 .. N of a panel (N < 128)");
+  panel_rows(0, Pn, Lp, Vp);
   __syncthreads();
   for (int M = 0; 2 * M < Tc; M++) {
-    double* Lc = (M & 1) ? Lp2 : Lp;
+    double* Lc = (M & 1) ? Lp2 : Lp;  // panel M's L / V
     double* Vc = (M & 1) ? Vp2 : Vp;
-    trailing(M, Lc, Vc, 2 * M + 2, 2 * M + 4);
+    double* Pnext = (M & 1) ? Pn : Pn2;  // panel M+1's values (then panel M+3's)
+    double* Pafter = (M & 1) ? Pn2 : Pn;  // panel M+2's values, published by C below
+    const bool more = 2 * (M + 1) < Tc;
+    if (more) lookahead(Lc, Vc, Pnext, 8 * (M + 1));
     __syncthreads();
     LDLT_TS(2 + 2 * M);
-    if (2 * (M + 1) < Tc) panel_rows(M + 1, (M & 1) ? Lp : Lp2, (M & 1) ? Vp : Vp2);
+    if (more) panel_rows(M + 1, Pnext, (M & 1) ? Lp : Lp2, (M & 1) ? Vp : Vp2);
     LDLT_TS(32 + M);  // (thread 0 is always a panel-row thread: the rows' chain ends here)
-    trailing(M, Lc, Vc, 2 * M + 4, Tc);
+    trailing(M, Lc, Vc, Pafter);
     __syncthreads();
     LDLT_TS(3 + 2 * M);
   }
-#endif
   if (fail) {
     if (tid == 0) D.scal[2] = 0.0;
     return;
