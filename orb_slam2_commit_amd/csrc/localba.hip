@@ -1087,17 +1087,32 @@ __global__ __launch_bounds__(kPB) void k_ba_pairs_many(const BaDev* __restrict__
 // entry of S is written); blocks b >= nblk write bs = bp - sum cf.
 __device__ inline void schur_fin_block(const BaDev& D, int blk, int j, double lambda) {
   const int S = D.gsplit;
+  // sum of the S chunk partials at p, p + stride, ... in chunk order; loads issued in groups of 8
+  // (clamped, not predicated) before their adds
+  auto psum = [&](const double* p, size_t stride) {
+    double t = 0;
+    for (int c0 = 0; c0 < S; c0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const double* q = p + (size_t)min(c0 + e, S - 1) * stride;
+        v[e] = *q;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if (c0 + e < S) t += v[e];
+    }
+    return t;
+  };
   const bool cam = D.camfold && !lm_skip_lin(D);  // k_ba_cam_fin's sums (chunk order) done here
   const double* camp = D.gpart + cam_part_off(D);
   if (blk >= D.nblk) {
     const int ci = blk - D.nblk;
     if (j < 6) {
-      double t = 0;
-      for (int c = 0; c < S; c++) t += D.gpart[(size_t)D.nblk * S * 36 + ((size_t)ci * S + c) * 6 + j];
+      const double t = psum(D.gpart + (size_t)D.nblk * S * 36 + (size_t)ci * S * 6 + j, 6);
       double bp;
       if (cam) {
-        bp = 0;
-        for (int c = 0; c < S; c++) bp += camp[((size_t)ci * S + c) * 27 + 21 + j];
+        bp = psum(camp + (size_t)ci * S * 27 + 21 + j, 27);
         D.bp[6 * ci + j] = bp;
       } else {
         bp = D.bp[6 * ci + j];
@@ -1109,8 +1124,7 @@ __device__ inline void schur_fin_block(const BaDev& D, int blk, int j, double la
   if (j >= 36) return;
   int c1;
   const int c2 = tri_decode(blk, D.nposes, c1);
-  double v = 0;
-  for (int c = 0; c < S; c++) v += D.gpart[((size_t)blk * S + c) * 36 + j];
+  const double v = psum(D.gpart + (size_t)blk * S * 36 + j, 36);
   const int N = 6 * D.nposes;
   const int r = j / 6, c = j % 6;
   double sv;
@@ -1118,8 +1132,7 @@ __device__ inline void schur_fin_block(const BaDev& D, int blk, int j, double la
     double h;
     if (cam) {
       const int lo = min(r, c), hi = max(r, c);
-      h = 0;
-      for (int q = 0; q < S; q++) h += camp[((size_t)c1 * S + q) * 27 + lo * 6 - (lo * (lo - 1)) / 2 + (hi - lo)];
+      h = psum(camp + (size_t)c1 * S * 27 + lo * 6 - (lo * (lo - 1)) / 2 + (hi - lo), 27);
       D.Hpp[36 * c1 + j] = h;
     } else {
       h = D.Hpp[36 * c1 + j];
@@ -1567,11 +1580,18 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_col_many(const BaDev* __restrict
 // L^T x = y.  Failure rule as the other kernels: an exactly zero pivot fails the solve.
 // LDS: packed strictly-lower L (N(N-1)/2), two panel-value, two L and two V arrays ((Np+8) x 8
 // each), y (N).
+#ifndef ORBX_LDLT_PW
+#define ORBX_LDLT_PW 8
+#endif
+constexpr int kPW = ORBX_LDLT_PW;  // panel width (pivots per panel): 4 or 8
+static_assert(kPW == 4 || kPW == 8, "panels of one or two tile columns");
+constexpr int kTPP = kPW / 4;      // tile columns per panel
 __host__ __device__ inline int ldlt_pan_rows(int N) { return ldlt_np4(N) + 8; }
-// panel arrays: rows of 8 doubles in groups of four, each group padded to 34 doubles, so that
+// panel arrays: rows of kPW doubles in groups of four, each group padded by 2 doubles, so that
 // the lanes of a wave reading different row groups spread over the LDS banks
-__host__ __device__ inline int ldlt_prow(int i) { return (i >> 2) * 34 + (i & 3) * 8; }
-__host__ __device__ inline int ldlt_pan_arr(int N) { return ldlt_pan_rows(N) / 4 * 34; }
+constexpr int kPG = 4 * kPW + 2;
+__host__ __device__ inline int ldlt_prow(int i) { return (i >> 2) * kPG + (i & 3) * kPW; }
+__host__ __device__ inline int ldlt_pan_arr(int N) { return ldlt_pan_rows(N) / 4 * kPG; }
 inline size_t ldlt_pan_smem(int N) {
   return ((size_t)N * (N - 1) / 2 + 6 * (size_t)ldlt_pan_arr(N) + N) * sizeof(double);
 }
@@ -1630,12 +1650,12 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   for (int j = tid; j < 3 * PA; j += NT) Lp2[j] = 0.0;
   __syncthreads();
 #pragma unroll
-  for (int t = 0; t < TPT; t++) {  // panels 0 and 1 (tile columns 0..3) publish and leave the registers
-    if (tk[t] >= 0 && tk[t] < 4) {
-      double* P = tk[t] < 2 ? Pn : Pn2;
+  for (int t = 0; t < TPT; t++) {  // panels 0 and 1 publish and leave the registers
+    if (tk[t] >= 0 && tk[t] < 2 * kTPP) {
+      double* P = tk[t] < kTPP ? Pn : Pn2;
 #pragma unroll
       for (int p = 0; p < 4; p++) {
-        double2_t* dst = reinterpret_cast<double2_t*>(P + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] & 1));
+        double2_t* dst = reinterpret_cast<double2_t*>(P + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] % kTPP));
         dst[0] = double2_t{a[t][p][0], a[t][p][1]};
         dst[1] = double2_t{a[t][p][2], a[t][p][3]};
       }
@@ -1645,81 +1665,89 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
   LDLT_TS(1);
   // B: the panel rows of panel M into (Lq, Vq)
   auto panel_rows = [&](int M, const double* Pq, double* Lq, double* Vq) {
-    const int c0 = 8 * M, w = min(8, N - c0);
+    constexpr int W = kPW, H = kPW / 2;  // (H: double2 per panel row)
+    const int c0 = W * M, w = min(W, N - c0);
     const int i = c0 + tid;
     if (i <= N) {
-      double Dm[36], u[8];
+      double Dm[W * (W + 1) / 2], u[W];
 #pragma unroll
-      for (int r = 0; r < 8; r++) {
+      for (int r = 0; r < W; r++) {
         const double2_t* src = reinterpret_cast<const double2_t*>(Pq + ldlt_prow(c0 + r));
-        const double2_t v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
-        const double row[8] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
+        double row[W];
+#pragma unroll
+        for (int h = 0; h < H; h++) {
+          const double2_t v = src[h];
+          row[2 * h] = v.x, row[2 * h + 1] = v.y;
+        }
 #pragma unroll
         for (int c = 0; c <= r; c++) Dm[ldlt_tri(r, c)] = row[c];
       }
       {
         const double2_t* src = reinterpret_cast<const double2_t*>(Pq + ldlt_prow(i));
-        const double2_t v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
-        u[0] = v0.x, u[1] = v0.y, u[2] = v1.x, u[3] = v1.y, u[4] = v2.x, u[5] = v2.y, u[6] = v3.x, u[7] = v3.y;
+#pragma unroll
+        for (int h = 0; h < H; h++) {
+          const double2_t v = src[h];
+          u[2 * h] = v.x, u[2 * h + 1] = v.y;
+        }
       }
-      double L[8], V[8];
+      double L[W], V[W];
       bool zero = false;
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
+      for (int q = 0; q < W; q++) {
         L[q] = 0.0;
         V[q] = 0.0;
         if (q < w) {  // uniform
           const double d = Dm[ldlt_tri(q, q)];
           zero |= d == 0.0;
           const double rq = rcp_nr(d);
-          double lq[8];
+          double lq[W];
 #pragma unroll
-          for (int r = q + 1; r < 8; r++) lq[r] = Dm[ldlt_tri(r, q)] * rq;
+          for (int r = q + 1; r < W; r++) lq[r] = Dm[ldlt_tri(r, q)] * rq;
 #pragma unroll
-          for (int r = q + 1; r < 8; r++)
+          for (int r = q + 1; r < W; r++)
 #pragma unroll
             for (int c = q + 1; c <= r; c++) Dm[ldlt_tri(r, c)] = __builtin_fma(-lq[r], Dm[ldlt_tri(c, q)], Dm[ldlt_tri(r, c)]);
           V[q] = u[q];
           L[q] = u[q] * rq;
 #pragma unroll
-          for (int c = q + 1; c < 8; c++) u[c] = __builtin_fma(-L[q], Dm[ldlt_tri(c, q)], u[c]);
+          for (int c = q + 1; c < W; c++) u[c] = __builtin_fma(-L[q], Dm[ldlt_tri(c, q)], u[c]);
         }
       }
       if (tid == 0 && zero) fail = 1;
       double2_t* lo = reinterpret_cast<double2_t*>(Lq + ldlt_prow(i));
       double2_t* vo = reinterpret_cast<double2_t*>(Vq + ldlt_prow(i));
 #pragma unroll
-      for (int h = 0; h < 4; h++) {
+      for (int h = 0; h < H; h++) {
         lo[h] = double2_t{L[2 * h], L[2 * h + 1]};
         vo[h] = double2_t{V[2 * h], V[2 * h + 1]};
       }
       if (i < N) {
         double* lrow = Lpk + (size_t)i * (i - 1) / 2 + c0;
 #pragma unroll
-        for (int q = 0; q < 8; q++)
+        for (int q = 0; q < W; q++)
           if (c0 + q < i && q < w) lrow[q] = L[q];
       } else {
 #pragma unroll
-        for (int q = 0; q < 8; q++)
+        for (int q = 0; q < W; q++)
           if (q < w) ys[c0 + q] = L[q];
       }
     }
   };
-  // C: the register tiles right of panel M+1 (tile columns >= 2M+4) take A -= L_rows V_cols^T;
-  // those of panel M+2 (tile columns 2M+4, 2M+5) then publish themselves into Pq and retire
+  // C: the register tiles right of panel M+1 take A -= L_rows V_cols^T; those of panel M+2 then
+  // publish themselves into Pq and retire
   auto trailing = [&](int M, const double* Lq, const double* Vq, double* Pq) {
 #pragma unroll
     for (int t = 0; t < TPT; t++) {
-      if (tk[t] >= 2 * M + 4) {
-        const double* lr = Lq + 34 * ti[t];
-        const double* vr = Vq + 34 * tk[t];
+      if (tk[t] >= kTPP * (M + 2)) {
+        const double* lr = Lq + kPG * ti[t];
+        const double* vr = Vq + kPG * tk[t];
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < kTPP; h++) {
           double Lv[4][4], Vv[4][4];
 #pragma unroll
           for (int p = 0; p < 4; p++) {
-            const double2_t* ls = reinterpret_cast<const double2_t*>(lr + 8 * p + 4 * h);
-            const double2_t* vs = reinterpret_cast<const double2_t*>(vr + 8 * p + 4 * h);
+            const double2_t* ls = reinterpret_cast<const double2_t*>(lr + kPW * p + 4 * h);
+            const double2_t* vs = reinterpret_cast<const double2_t*>(vr + kPW * p + 4 * h);
             const double2_t l0 = ls[0], l1 = ls[1], v0 = vs[0], v1 = vs[1];
             Lv[p][0] = l0.x, Lv[p][1] = l0.y, Lv[p][2] = l1.x, Lv[p][3] = l1.y;
             Vv[p][0] = v0.x, Vv[p][1] = v0.y, Vv[p][2] = v1.x, Vv[p][3] = v1.y;
@@ -1731,10 +1759,10 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
 #pragma unroll
               for (int q = 0; q < 4; q++) a[t][p][q] = __builtin_fma(-Lv[p][s], Vv[q][s], a[t][p][q]);
         }
-        if (tk[t] < 2 * M + 6) {  // panel M+2 publishes itself
+        if (tk[t] < kTPP * (M + 3)) {  // panel M+2 publishes itself
 #pragma unroll
           for (int p = 0; p < 4; p++) {
-            double2_t* dst = reinterpret_cast<double2_t*>(Pq + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] & 1));
+            double2_t* dst = reinterpret_cast<double2_t*>(Pq + ldlt_prow(4 * ti[t] + p) + 4 * (tk[t] % kTPP));
             dst[0] = double2_t{a[t][p][0], a[t][p][1]};
             dst[1] = double2_t{a[t][p][2], a[t][p][3]};
           }
@@ -1742,37 +1770,47 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
       }
     }
   };
-  // A: panel M's update of panel M+1's values in Pq (rows c1 = 8(M+1) .. N, eight columns): thread
-  // -> (row c1 + tid / 4, columns 2 (tid % 4), +1), the s = 0..7 FMAs in the register path's order
+  // A: panel M's update of panel M+1's values in Pq (rows c1 = kPW (M+1) .. N, kPW columns):
+  // thread -> (row c1 + tid / 4, columns CPT (tid % 4) .. +CPT-1), the s = 0..kPW-1 FMAs in the
+  // register path's order
   auto lookahead = [&](const double* Lq, const double* Vq, double* Pq, int c1) {
-    const int i = c1 + tid / 4, j0 = 2 * (tid & 3);
+    constexpr int CPT = kPW / 4;
+    const int i = c1 + tid / 4, j0 = CPT * (tid & 3);
     if (i <= N) {
       const double2_t* ls = reinterpret_cast<const double2_t*>(Lq + ldlt_prow(i));
-      const double2_t* va = reinterpret_cast<const double2_t*>(Vq + ldlt_prow(c1 + j0));
-      const double2_t* vb = reinterpret_cast<const double2_t*>(Vq + ldlt_prow(c1 + j0 + 1));
-      double2_t* dst = reinterpret_cast<double2_t*>(Pq + ldlt_prow(i) + j0);
-      double2_t x = *dst;
+      double* dst = Pq + ldlt_prow(i) + j0;
+      double x[CPT];
+      const double2_t* vr[CPT];
 #pragma unroll
-      for (int h = 0; h < 4; h++) {
-        const double2_t l = ls[h], u = va[h], v = vb[h];
-        x.x = __builtin_fma(-l.x, u.x, x.x);
-        x.y = __builtin_fma(-l.x, v.x, x.y);
-        x.x = __builtin_fma(-l.y, u.y, x.x);
-        x.y = __builtin_fma(-l.y, v.y, x.y);
+      for (int c = 0; c < CPT; c++) {
+        x[c] = dst[c];
+        vr[c] = reinterpret_cast<const double2_t*>(Vq + ldlt_prow(c1 + j0 + c));
       }
-      *dst = x;
+#pragma unroll
+      for (int h = 0; h < kPW / 2; h++) {
+        const double2_t l = ls[h];
+        double2_t v[CPT];
+#pragma unroll
+        for (int c = 0; c < CPT; c++) v[c] = vr[c][h];
+#pragma unroll
+        for (int c = 0; c < CPT; c++) x[c] = __builtin_fma(-l.x, v[c].x, x[c]);
+#pragma unroll
+        for (int c = 0; c < CPT; c++) x[c] = __builtin_fma(-l.y, v[c].y, x[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < CPT; c++) dst[c] = x[c];
     }
   };
-  static_assert(NT / 4 >= 120, "one look-ahead pass covers rows 8 .. N of a panel (N < 128)");
+  static_assert(NT / 4 >= 124, "one look-ahead pass covers rows kPW .. N of a panel (N < 128)");
   panel_rows(0, Pn, Lp, Vp);
   __syncthreads();
-  for (int M = 0; 2 * M < Tc; M++) {
+  for (int M = 0; kTPP * M < Tc; M++) {
     double* Lc = (M & 1) ? Lp2 : Lp;  // panel M's L / V
     double* Vc = (M & 1) ? Vp2 : Vp;
     double* Pnext = (M & 1) ? Pn : Pn2;  // panel M+1's values (then panel M+3's)
     double* Pafter = (M & 1) ? Pn2 : Pn;  // panel M+2's values, published by C below
-    const bool more = 2 * (M + 1) < Tc;
-    if (more) lookahead(Lc, Vc, Pnext, 8 * (M + 1));
+    const bool more = kTPP * (M + 1) < Tc;
+    if (more) lookahead(Lc, Vc, Pnext, kPW * (M + 1));
     __syncthreads();
     LDLT_TS(2 + 2 * M);
     if (more) panel_rows(M + 1, Pnext, (M & 1) ? Lp : Lp2, (M & 1) ? Vp : Vp2);
