@@ -72,13 +72,13 @@ def parse():
     ap.add_argument("--track-steps", type=int, default=5, help="steps of the extract+match+track leg (0: skip)")
     ap.add_argument("--c3-steps", type=int, default=3, help="config-3 (EuRoC + PnP RANSAC) steps per rank (0: skip)")
     ap.add_argument("--c3-batch", type=int, default=128, help="config-3 frames (sequences) per step per GPU")
-    ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r04_sq_counters.json"),
+    ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r05_sq_counters.json"),
                     help="SQ counter summary (tools/pmc_kernel.sh + tools/sq_summary.py) for issue fractions")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/profile.sh + tools/parse_prof.py); null if absent")
-    ap.add_argument("--rocprof", default=os.path.join(ROOT, "profiles", "r04_rocprof_stages.json"),
+    ap.add_argument("--rocprof", default=os.path.join(ROOT, "profiles", "r05_rocprof_stages.json"),
                     help="per-stage kernel time per step from rocprofv3 --stats (tools/rocprof_stages.py)")
-    ap.add_argument("--ba-traffic", default=os.path.join(ROOT, "profiles", "r04_localba_traffic.json"),
+    ap.add_argument("--ba-traffic", default=os.path.join(ROOT, "profiles", "r05_localba_traffic.json"),
                     help="LocalBA PMC bytes per LM iteration (tools/ba_traffic.py); null if absent")
     return ap.parse_args()
 
