@@ -80,6 +80,8 @@ def parse():
                     help="per-stage kernel time per step from rocprofv3 --stats (tools/rocprof_stages.py)")
     ap.add_argument("--ba-traffic", default=os.path.join(ROOT, "profiles", "r05_localba_traffic.json"),
                     help="LocalBA PMC bytes per LM iteration (tools/ba_traffic.py); null if absent")
+    ap.add_argument("--stereo-floor", default=os.path.join(ROOT, "profiles", "r05_stereo_floor.json"),
+                    help="measured sector floor of the stereo stage (tools/stereo_floor.py); null if absent")
     return ap.parse_args()
 
 
@@ -952,6 +954,18 @@ def main():
         tr = sum(traffic_all.get(k, 0) for k in st_k) or None
         stage_hbm["stereo"] = stage_entry("stereo", ev_s, 1, rp, tr)
         stage_hbm["stereo"]["kernels"] = {k: round(stages[k][0] / stages[k][1], 4) for k in st_k}
+        # the measured floor (unique 64-B sectors of the staged keypoints' 22 SAD rows + the non-row
+        # part of B_st), per frame from its profile run, scaled to this step's frames
+        try:
+            with open(args.stereo_floor) as f:
+                fl = json.load(f)["floor"]
+            per_frame = (fl["floor_bytes_64B_sectors"] + fl["B_st_bytes"] - fl["rows_bytes_compact"]) / fl["frames_per_step"]
+            floor_b = per_frame * B
+            stage_hbm["stereo"]["sector_floor_bytes_per_event"] = int(floor_b)
+            stage_hbm["stereo"]["traffic_vs_sector_floor"] = round(tr / floor_b, 3) if tr else None
+            stage_hbm["stereo"]["sector_floor_source"] = os.path.relpath(args.stereo_floor, ROOT)
+        except (OSError, KeyError, ValueError):
+            stage_hbm["stereo"]["sector_floor_bytes_per_event"] = None
     cands = {k: v for k, v in stage_hbm.items() if v.get("s8d_bytes_per_event")}
     if cands:
         dom = max(cands, key=lambda k: cands[k]["ms_per_step"])
