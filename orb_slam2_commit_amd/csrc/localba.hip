@@ -975,11 +975,12 @@ __device__ inline int tri_decode(int b, int n, int& c1) {
 // order), the first position k2 of the same point on pose c2, flagged when
 // the point has more than one.
 __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
+  const int2 bxy = xcd_block2();  // (as k_ba_pairs: one pose chunk's blocks on one XCD)
   int c1;
-  const int c2 = tri_decode(blockIdx.x, D.nposes, c1);
+  const int c2 = tri_decode(bxy.x, D.nposes, c1);
   int lo, hi;
-  chunk_range(D.cam_off[c1], D.cam_off[c1 + 1], blockIdx.y, gridDim.y, lo, hi);
-  int* tab = D.ptab + D.boff[blockIdx.x] - D.cam_off[c1];
+  chunk_range(D.cam_off[c1], D.cam_off[c1 + 1], bxy.y, gridDim.y, lo, hi);
+  int* tab = D.ptab + D.boff[bxy.x] - D.cam_off[c1];
   for (int t = lo + threadIdx.x; t < hi; t += kPB) {
     const int i = D.pos_pt[D.cam_pos[t]];
     const int s = D.pt_off[i], e = D.pt_off[i + 1];
