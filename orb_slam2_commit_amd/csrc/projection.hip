@@ -1248,6 +1248,7 @@ namespace {
 // then the device-only split scratch -- one upload, one split launch set over blockIdx.z, one
 // download of the outputs, one sync.
 orbx_status proj_run_host(const orbx_proj_problem* const* ps, int n, int device) {
+  if (n < 1 || n > 2) return ORBX_ERR_ARG;  // (one problem, or SearchBySim3's two directions)
   for (int z = 0; z < n; z++) {
     const orbx_status chk = proj_check(*ps[z], true);
     if (chk != ORBX_OK) return chk;
