@@ -342,28 +342,6 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
   while ((1 << G.rz_lc) < G.rz_stride / 16) G.rz_lc++;
   // every footprint row must be loaded: rows per thread = ceil(rz_rows / (256 >> rz_lc)) <= the kernel's 4
   if (G.rz_lc > 8 || (G.rz_rows + (256 >> G.rz_lc) - 1) / (256 >> G.rz_lc) > (kRzMaxRows + 15) / 16) return ORBX_ERR_SIZE;
-  // k_resize_blur staging bound: source footprint of every extended 128 x kRbTH tile (rows
-  // y0-3 .. y0+kRbTH+2, columns x0-4 .. x0+139, clamped to the level); levels too large for its LDS
-  // budget keep k_resize + k_blur (rb_rows = 0)
-  G.rb_rows = 1;
-  G.rb_stride = 16;
-  for (int l = 1; l < G.nlevels; l++) {
-    const LevelGeom& L = G.lv[l];
-    for (int oy = 0; oy < L.h; oy += kRbTH) {
-      const int r0 = std::max(oy - 3, 0), r1 = std::min(oy + kRbTH + 2, L.h - 1);
-      G.rb_rows = std::max(G.rb_rows, P.yt[L.ytab_off + r1].sy1 - P.yt[L.ytab_off + r0].sy0 + 1);
-    }
-    for (int ox = 0; ox < L.w; ox += kBlurTileW) {
-      const int c0 = std::max(ox - 4, 0), c1 = std::min(ox + kRbEW - 5, L.w - 1);
-      const int span = P.xt[L.xtab_off + c1].sx1 - P.xt[L.xtab_off + c0].sx0 + 1;
-      G.rb_stride = std::max(G.rb_stride, (span + 15) / 16 * 16);
-    }
-  }
-  G.rb_lc = 0;
-  while ((1 << G.rb_lc) < G.rb_stride / 16) G.rb_lc++;
-  if (G.rb_rows > kRbMaxRows || G.rb_lc > 8 || resize_blur_smem(G.rb_rows, G.rb_stride) > 64 * 1024 ||
-      (G.rb_rows + (256 >> G.rb_lc) - 1) / (256 >> G.rb_lc) > (kRbMaxRows + 15) / 16)
-    G.rb_rows = 0;
   G.pyr_bytes = (pyr + 255) & ~255LL;
   G.blur_bytes = (blur + 255) & ~255LL;
   G.ncells = (int)P.cells.size();

@@ -275,126 +275,6 @@ __device__ __forceinline__ int reflect101(int p, int n) {
   return p;
 }
 
-constexpr int kBIn = kBlurTileW + 16;  // input tile row stride (bytes, 16-B multiple)
-constexpr int kBStrip = 16;            // output rows per thread
-
-// GaussianBlur 7x7 of SR output rows x 4 columns (xg .. xg+3 of a level of width w) from an LDS
-// tile of row stride kBIn whose column 0 is the tile's x0 - 4 and row 0 its y0 - 3: thread column
-// group g (tile columns 4g .. 4g+11 read), strip rows ys .. ys+SR+5.  One packed dword per row.
-template <int SR>
-__device__ __forceinline__ void blur_strip(const uint8_t* tin, int g, int ys, int xg, int w, uint32_t (&outv)[SR]) {
-  const uint32_t k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
-  // horizontal taps as byte dot products (exact integers, weights < 256) straight on the three
-  // aligned dwords [a b c] = tile bytes 4g .. 4g+11: output col j of the group takes bytes
-  // j+1 .. j+7, i.e. ten v_dot4_u32_u8 with the taps pre-shifted into the word each byte sits in
-  // (no byte-align step).  The accumulator starts at 0x4B000000, so the sum comes out as the f32
-  // bits of 2^23 + s (s <= 257*255 < 2^23) and one packed subtract per two columns converts it.
-  auto W4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) { return b0 | b1 << 8 | b2 << 16 | b3 << 24; };
-  const uint32_t wa0 = W4(0, k0, k1, k2), wb0 = W4(k3, k2, k1, k0);
-  const uint32_t wa1 = W4(0, 0, k0, k1), wb1 = W4(k2, k3, k2, k1), wc1 = W4(k0, 0, 0, 0);
-  const uint32_t wa2 = W4(0, 0, 0, k0), wb2 = W4(k1, k2, k3, k2), wc2 = W4(k1, k0, 0, 0);
-  const uint32_t wb3 = W4(k0, k1, k2, k3), wc3 = W4(k2, k1, k0, 0);
-  const float f0 = (float)k0 * (1.f / 65536.f), f1 = (float)k1 * (1.f / 65536.f), f2 = (float)k2 * (1.f / 65536.f),
-              f3 = (float)k3 * (1.f / 65536.f);
-  const float2v F0 = {f0, f0}, F1 = {f1, f1}, F2 = {f2, f2}, F3 = {f3, f3};
-  const float2v two23 = {8388608.0f, 8388608.0f}, magic = {12582912.0f, 12582912.0f};
-  // row sums (<= 257*255, exact in f32) of output cols xg..xg+3 on tile row ty, as two f32 pairs
-  auto rowsum = [&](int ty, float2v (&o)[2]) {
-    const uint32_t* r32 = (const uint32_t*)&tin[ty * kBIn + 4 * g];
-    const uint32_t a = r32[0], b = r32[1], c = r32[2];
-    constexpr uint32_t bias = 0x4B000000u;  // f32 2^23
-    const uint32_t s0 = __builtin_amdgcn_udot4(b, wb0, __builtin_amdgcn_udot4(a, wa0, bias, false), false);
-    const uint32_t s1 = __builtin_amdgcn_udot4(
-        c, wc1, __builtin_amdgcn_udot4(b, wb1, __builtin_amdgcn_udot4(a, wa1, bias, false), false), false);
-    const uint32_t s2 = __builtin_amdgcn_udot4(
-        c, wc2, __builtin_amdgcn_udot4(b, wb2, __builtin_amdgcn_udot4(a, wa2, bias, false), false), false);
-    const uint32_t s3 = __builtin_amdgcn_udot4(c, wc3, __builtin_amdgcn_udot4(b, wb3, bias, false), false);
-    o[0] = (float2v){__uint_as_float(s0), __uint_as_float(s1)} - two23;
-    o[1] = (float2v){__uint_as_float(s2), __uint_as_float(s3)} - two23;
-  };
-  // 7-row ring indexed by compile-time (r + i) % 7 in the unrolled loop: no register moves
-  float2v win[7][2];
-#pragma unroll
-  for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
-  const int simd_w = w & ~3;
-  const bool all_simd = xg + 3 < simd_w;  // the whole group takes the SSE2 rounding
-  // wave-uniform: the per-row tail fix-up below is a scalar branch (no exec-mask juggling per row)
-  const bool wave_tail = __builtin_amdgcn_ballot_w64(!all_simd) != 0;
-
-#pragma unroll
-  for (int r = 0; r < SR; r++) {
-    rowsum(ys + r + 6, win[(r + 6) % 7]);
-    // column taps on packed f32 pairs, each element exactly the scalar chain
-    // fma(f3, w3, fma(f2, w2+w4, fma(f1, w1+w5, f0*(w0+w6)))) = acc / 2^16 (integer sums below
-    // 2^24 scaled by a power of two); + 1.5*2^23 rounds it half-to-even (the SSE2 groups'
-    // rint), leaving the integer in the low bits
-    float2v acc[2];
-    uint32_t rb[4];
-#pragma unroll
-    for (int hh = 0; hh < 2; hh++) {
-      const float2v w0 = win[r % 7][hh], w1 = win[(r + 1) % 7][hh], w2 = win[(r + 2) % 7][hh],
-                    w3 = win[(r + 3) % 7][hh], w4 = win[(r + 4) % 7][hh], w5 = win[(r + 5) % 7][hh],
-                    w6 = win[(r + 6) % 7][hh];
-      acc[hh] = __builtin_elementwise_fma(
-          F3, w3, __builtin_elementwise_fma(F2, w2 + w4, __builtin_elementwise_fma(F1, w1 + w5, F0 * (w0 + w6))));
-      const float2v rr = acc[hh] + magic;
-      rb[2 * hh] = __float_as_uint(rr.x);
-      rb[2 * hh + 1] = __float_as_uint(rr.y);
-    }
-    // low halves as u16 pairs, saturated to 255 (the kernel sums to 257), then the low bytes
-    u16x2 p01 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(rb[1], rb[0], 0x05040100u));
-    u16x2 p23 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(rb[3], rb[2], 0x05040100u));
-    const u16x2 cap = {255, 255};
-    p01 = __builtin_elementwise_min(p01, cap);
-    p23 = __builtin_elementwise_min(p23, cap);
-    uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01), 0x06040200u);
-    if (wave_tail) {
-      // the row's scalar tail (x >= w & ~3): (acc + 2^15) >> 16, selected per lane and column
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const float aj = j == 0 ? acc[0].x : j == 1 ? acc[0].y : j == 2 ? acc[1].x : acc[1].y;
-        const int v = min(((int)(aj * 65536.f) + (1 << 15)) >> 16, 255);
-        const uint32_t fixed = (packed & ~(0xFFu << (8 * j))) | ((uint32_t)v << (8 * j));
-        packed = xg + j >= simd_w ? fixed : packed;
-      }
-    }
-    outv[r] = packed;
-  }
-}
-
-// Write-out of a blurred 128 x TH tile in the level's tile layout (8 rows x 16 bytes = 128-B tiles,
-// the layout k_describe gathers from): the outputs go to LDS (stage, >= 128 * TH bytes, free to
-// overwrite) in tile order, then leave as whole 128-B lines, 16 B per lane.  Columns past w and
-// rows past h land in the level's padding.
-template <int TH>
-__device__ __forceinline__ void blur_tile_out(uint8_t* stage, const uint32_t (&outv)[TH / 8], bool active, int g, int ys,
-                                              uint8_t* dst, int bs, int h, int x0, int y0, int tid) {
-  constexpr int SR = TH / 8;
-  if (active) {
-#pragma unroll
-    for (int r = 0; r < SR; r++) {
-      const int yr = ys + r, c = 4 * g;
-      *(uint32_t*)&stage[((yr >> 3) * (kBlurTileW / 16) + (c >> 4)) * 128 + (yr & 7) * 16 + (c & 15)] = outv[r];
-    }
-  }
-  __syncthreads();
-  {
-    const int ntx = bs >> 4, nty = (h + 7) >> 3;
-    const int tx0 = x0 >> 4, ty0 = y0 >> 3;
-    const __amdgpu_buffer_rsrc_t rd =
-        __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, nty * ntx * 128, 0x00020000);
-    constexpr int kTiles = (kBlurTileW / 16) * (TH / 8), kChunks = kTiles * 8;  // 16-B chunks
-#pragma unroll
-    for (int k = 0; k < kChunks / BS; k++) {
-      const int q = tid + k * BS, t = q >> 3, tr = t / (kBlurTileW / 16), tc = t - tr * (kBlurTileW / 16);
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 v = *(const u32x4*)&stage[q * 16];
-      if (tx0 + tc < ntx && ty0 + tr < nty)
-        __builtin_amdgcn_raw_buffer_store_b128(v, rd, (uint32_t)(((ty0 + tr) * ntx + tx0 + tc) * 128 + (q & 7) * 16), 0, 0);
-    }
-  }
-}
-
 // Tile of kBlurTileW x kBlurTileH (128 x 128) outputs per 256-thread block.
 // Input tile col 0 = x0-4 so that every 4-output group reads 3 aligned LDS
 // dwords.  The tile arrives as 16-B buffer loads at the (unaligned) source row
@@ -411,6 +291,8 @@ __device__ __forceinline__ void blur_tile_out(uint8_t* stage, const uint32_t (&o
 // needed) input tile in LDS in the tiled blurred-level order (8x16-B tiles)
 // and out as whole 128-B tiles of b128 stores.  7 waves per SIMD: 68 VGPRs,
 // no scratch (8 spills 12 B per lane for the same time, profiles/r04/ab_blur_tiled.txt).
+constexpr int kBIn = kBlurTileW + 16;  // input tile row stride (bytes, 16-B multiple)
+constexpr int kBStrip = 16;            // output rows per thread
 #ifndef ORBX_BLUR_WPE
 #define ORBX_BLUR_WPE 7
 #endif
@@ -500,164 +382,113 @@ __global__ __launch_bounds__(BS, ORBX_BLUR_WPE) void k_blur(const Geometry* __re
   // (threads past the level compute nothing but stay for the barriers of the tile write-out)
   const bool active = xg < w && y0 + ys < h;
   uint32_t outv[kBStrip];
-  if (active) blur_strip<kBStrip>(tin, g, ys, xg, w, outv);
-  __syncthreads();  // the outputs are staged over the input tile
-  blur_tile_out<kBlurTileH>(tin, outv, active, g, ys, dst, bs, h, x0, y0, tid);
-}
+  const uint32_t k0 = c_gauss[0], k1 = c_gauss[1], k2 = c_gauss[2], k3 = c_gauss[3];
+  // horizontal taps as byte dot products (exact integers, weights < 256) straight on the three
+  // aligned dwords [a b c] = tile bytes 4g .. 4g+11: output col j of the group takes bytes
+  // j+1 .. j+7, i.e. ten v_dot4_u32_u8 with the taps pre-shifted into the word each byte sits in
+  // (no byte-align step).  The accumulator starts at 0x4B000000, so the sum comes out as the f32
+  // bits of 2^23 + s (s <= 257*255 < 2^23) and one packed subtract per two columns converts it.
+  auto W4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) { return b0 | b1 << 8 | b2 << 16 | b3 << 24; };
+  const uint32_t wa0 = W4(0, k0, k1, k2), wb0 = W4(k3, k2, k1, k0);
+  const uint32_t wa1 = W4(0, 0, k0, k1), wb1 = W4(k2, k3, k2, k1), wc1 = W4(k0, 0, 0, 0);
+  const uint32_t wa2 = W4(0, 0, 0, k0), wb2 = W4(k1, k2, k3, k2), wc2 = W4(k1, k0, 0, 0);
+  const uint32_t wb3 = W4(k0, k1, k2, k3), wc3 = W4(k2, k1, k0, 0);
+  const float f0 = (float)k0 * (1.f / 65536.f), f1 = (float)k1 * (1.f / 65536.f), f2 = (float)k2 * (1.f / 65536.f),
+              f3 = (float)k3 * (1.f / 65536.f);
+  const float2v F0 = {f0, f0}, F1 = {f1, f1}, F2 = {f2, f2}, F3 = {f3, f3};
+  const float2v two23 = {8388608.0f, 8388608.0f}, magic = {12582912.0f, 12582912.0f};
+  // row sums (<= 257*255, exact in f32) of output cols xg..xg+3 on tile row ty, as two f32 pairs
+  auto rowsum = [&](int ty, float2v (&o)[2]) {
+    const uint32_t* r32 = (const uint32_t*)&tin[ty * kBIn + 4 * g];
+    const uint32_t a = r32[0], b = r32[1], c = r32[2];
+    constexpr uint32_t bias = 0x4B000000u;  // f32 2^23
+    const uint32_t s0 = __builtin_amdgcn_udot4(b, wb0, __builtin_amdgcn_udot4(a, wa0, bias, false), false);
+    const uint32_t s1 = __builtin_amdgcn_udot4(
+        c, wc1, __builtin_amdgcn_udot4(b, wb1, __builtin_amdgcn_udot4(a, wa1, bias, false), false), false);
+    const uint32_t s2 = __builtin_amdgcn_udot4(
+        c, wc2, __builtin_amdgcn_udot4(b, wb2, __builtin_amdgcn_udot4(a, wa2, bias, false), false), false);
+    const uint32_t s3 = __builtin_amdgcn_udot4(c, wc3, __builtin_amdgcn_udot4(b, wb3, bias, false), false);
+    o[0] = (float2v){__uint_as_float(s0), __uint_as_float(s1)} - two23;
+    o[1] = (float2v){__uint_as_float(s2), __uint_as_float(s3)} - two23;
+  };
+  // 7-row ring indexed by compile-time (r + i) % 7 in the unrolled loop: no register moves
+  float2v win[7][2];
+  if (active) {
+#pragma unroll
+  for (int r = 0; r < 6; r++) rowsum(ys + r, win[r]);
+  const int simd_w = w & ~3;
+  const bool all_simd = xg + 3 < simd_w;  // the whole group takes the SSE2 rounding
+  // wave-uniform: the per-row tail fix-up below is a scalar branch (no exec-mask juggling per row)
+  const bool wave_tail = __builtin_amdgcn_ballot_w64(!all_simd) != 0;
 
-// ---------------------------------------------------------- resize + blur
-// Levels >= 1: ComputePyramid's resize of level l-1 (src/ORBextractor.cc:1215-1250) and the blur
-// of level l that operator() runs before the descriptors (src/ORBextractor.cc:1186-1190) in ONE
-// pass over a 128 x kRbTH output tile, so the blur no longer re-reads the level from HBM:
-//   1. the source footprint of the tile's EXTENDED level region -- rows y0-3 .. y0+kRbTH+2 and
-//      columns x0-4 .. x0+139, each taken at its BORDER_REFLECT_101 position inside the level
-//      (clamped into the tile's own range where no output needs it) -- as 16-B loads to LDS;
-//   2. the horizontal resize pass of every footprint row for the 144 extended columns (int16,
-//      4 columns per item, the taps of a thread's 4 columns loaded once);
-//   3. the vertical pass for every extended row -> the level's u8 tile in LDS (row stride kBIn,
-//      column 0 = x0-4, row 0 = y0-3: k_blur's input tile layout, reflection included), the
-//      interior rows/columns also stored to the level in HBM (FAST, the next level, IC_Angle);
-//   4. k_blur's strips (blur_strip) on that tile and its 128-B tile write-out (blur_tile_out).
-// Every value is the same per-pixel formula as k_resize / k_blur, so both outputs are bit-identical
-// to the two-kernel path.  Level 0's blur stays in k_blur (it reads the input image).
-constexpr int kRbG = kBIn / 4;             // 4-column groups of the extended width (36)
-constexpr int kRbGR = BS / kRbG;           // rows per step of the group-mapped passes (7)
-constexpr int kRbVIt = (kRbER + kRbGR - 1) / kRbGR;  // vertical items per thread
-static_assert(kBlurTileW == 128 && kBIn == kRbEW && kRbTH % 8 == 0 && kRbTH >= 8, "k_resize_blur tile shape");
-
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
-
-__global__ __launch_bounds__(BS) void k_resize_blur(const Geometry* __restrict__ G, const ResizeX* __restrict__ xt,
-                                                    const ResizeY* __restrict__ yt, BatchPtrs B, int l) {
-  extern __shared__ __align__(16) uint8_t rb_smem[];
-  const LevelGeom& L = G->lv[l];
-  const LevelGeom& S = G->lv[l - 1];
-  const int3 bi = xcd_block3();
-  const int img = bi.z, tid = threadIdx.x;
-  const int w = L.w, h = L.h;
-  const int x0 = bi.x * kBlurTileW, y0 = bi.y * kRbTH;
-  const int nx = min(kBlurTileW, w - x0), ny = min(kRbTH, h - y0);
-  // extended region, mapped into the level: reflect101, then clamped into [cmin, cmax] x [rmin, rmax]
-  // (the range every needed position lands in; the clamp only touches positions no output reads)
-  const int cmin = max(x0 - 4, 0), cmax = min(x0 + kBIn - 5, w - 1);
-  const int rmin = max(y0 - 3, 0), rmax = min(y0 + kRbTH + 2, h - 1);
-  const ResizeX* X = xt + L.xtab_off;
-  const ResizeY* Y = yt + L.ytab_off;
-  const int cx0 = X[cmin].sx0, span = X[cmax].sx1 - cx0 + 1;
-  const int ry0 = Y[rmin].sy0, nrows = Y[rmax].sy1 - ry0 + 1;
-  const int stride = G->rb_stride;
-  uint8_t* tin = rb_smem;  // footprint; then the extended level tile (tl)
-  int16_t* hb = (int16_t*)(rb_smem + (max(G->rb_rows * stride, (kRbER + 1) * kBIn) + 15) / 16 * 16);  // [rows][kBIn]
-  uint8_t* tl = rb_smem;
-  const uint8_t* src = level_ptr(*G, B, img, l - 1);
-  const int swh = S.w * S.h;
-  // the taps of this thread's 4 columns (group gq) and vertical rows, loaded beside the footprint
-  const int gq = tid % kRbG, rq = tid / kRbG;
-  const bool qok = rq < kRbGR;
-  ResizeX xc[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) xc[j] = X[clampi(reflect101(x0 - 4 + 4 * gq + j, w), cmin, cmax)];
-  ResizeY yv[kRbVIt];
+  for (int r = 0; r < kBStrip; r++) {
+    rowsum(ys + r + 6, win[(r + 6) % 7]);
+    // column taps on packed f32 pairs, each element exactly the scalar chain
+    // fma(f3, w3, fma(f2, w2+w4, fma(f1, w1+w5, f0*(w0+w6)))) = acc / 2^16 (integer sums below
+    // 2^24 scaled by a power of two); + 1.5*2^23 rounds it half-to-even (the SSE2 groups'
+    // rint), leaving the integer in the low bits
+    float2v acc[2];
+    uint32_t rb[4];
 #pragma unroll
-  for (int k = 0; k < kRbVIt; k++) {
-    const int er = rq + k * kRbGR;
-    yv[k] = Y[clampi(reflect101(y0 - 3 + min(er, kRbER - 1), h), rmin, rmax)];
-  }
-  // 1. footprint -> LDS (k_resize's staging)
-  {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, swh, 0x00020000);
-    const int nch = (span + 15) >> 4;
-    const int lc = G->rb_lc;
-    const int c = tid & ((1 << lc) - 1), r0 = tid >> lc, rstep = BS >> lc;
-    constexpr int kLd = (kRbMaxRows + 15) / 16;
-    uint4 v[kLd];
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int r = r0 + u * rstep;
-      const int o = (ry0 + r) * S.w + cx0 + 16 * c;
-      v[u] = make_uint4(0, 0, 0, 0);
-      if (r < nrows && c < nch) {
-        if (o + 16 <= swh) {
-          const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-          v[u] = make_uint4(t[0], t[1], t[2], t[3]);
-        } else {  // last bytes of the level: byte loads, each range-checked (outside -> 0, never used)
-          uint32_t w4[4] = {0, 0, 0, 0};
-#pragma unroll
-          for (int b = 0; b < 16; b++)
-            w4[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + b, 0, 0) << (8 * (b & 3));
-          v[u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        }
-      }
+    for (int hh = 0; hh < 2; hh++) {
+      const float2v w0 = win[r % 7][hh], w1 = win[(r + 1) % 7][hh], w2 = win[(r + 2) % 7][hh],
+                    w3 = win[(r + 3) % 7][hh], w4 = win[(r + 4) % 7][hh], w5 = win[(r + 5) % 7][hh],
+                    w6 = win[(r + 6) % 7][hh];
+      acc[hh] = __builtin_elementwise_fma(
+          F3, w3, __builtin_elementwise_fma(F2, w2 + w4, __builtin_elementwise_fma(F1, w1 + w5, F0 * (w0 + w6))));
+      const float2v rr = acc[hh] + magic;
+      rb[2 * hh] = __float_as_uint(rr.x);
+      rb[2 * hh + 1] = __float_as_uint(rr.y);
     }
-#pragma unroll
-    for (int u = 0; u < kLd; u++) {
-      const int r = r0 + u * rstep;
-      if (r < nrows && c < nch) *(uint4*)&tin[r * stride + 16 * c] = v[u];
-    }
-  }
-  __syncthreads();
-  // 2. horizontal pass: item = (footprint row, 4 extended columns)
-  if (qok) {
-    int s0[4], s1[4], a0[4], a1[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      s0[j] = xc[j].sx0 - cx0;
-      s1[j] = xc[j].sx1 - cx0;
-      a0[j] = xc[j].a0;
-      a1[j] = xc[j].a1;
-    }
-    for (int r = rq; r < nrows; r += kRbGR) {
-      const uint8_t* t = tin + r * stride;
-      uint32_t hv[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) hv[j] = (uint32_t)(uint16_t)(int16_t)((t[s0[j]] * a0[j] + t[s1[j]] * a1[j]) >> 4);
-      *(uint2*)&hb[r * kBIn + 4 * gq] = make_uint2(hv[0] | hv[1] << 16, hv[2] | hv[3] << 16);
-    }
-  }
-  __syncthreads();
-  // 3. vertical pass: item = (extended row, 4 extended columns) -> tl; interior -> the level
-  {
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(B.pyr + (size_t)img * G->pyr_bytes + L.off), (short)0, w * h, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < kRbVIt; k++) {
-      const int er = rq + k * kRbGR;
-      if (!qok || er >= kRbER) continue;
-      const ResizeY y = yv[k];
-      const uint32_t B0 = (uint32_t)y.b0 << 16, B1 = (uint32_t)y.b1 << 16;
-      const uint2 p0 = *(const uint2*)&hb[(y.sy0 - ry0) * kBIn + 4 * gq];
-      const uint2 p1 = *(const uint2*)&hb[(y.sy1 - ry0) * kBIn + 4 * gq];
-      const uint32_t h0[4] = {p0.x & 0xFFFF, p0.x >> 16, p0.y & 0xFFFF, p0.y >> 16};
-      const uint32_t h1[4] = {p1.x & 0xFFFF, p1.x >> 16, p1.y & 0xFFFF, p1.y >> 16};
-      uint32_t packed = 0;
+    // low halves as u16 pairs, saturated to 255 (the kernel sums to 257), then the low bytes
+    u16x2 p01 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(rb[1], rb[0], 0x05040100u));
+    u16x2 p23 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(rb[3], rb[2], 0x05040100u));
+    const u16x2 cap = {255, 255};
+    p01 = __builtin_elementwise_min(p01, cap);
+    p23 = __builtin_elementwise_min(p23, cap);
+    uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01), 0x06040200u);
+    if (wave_tail) {
+      // the row's scalar tail (x >= w & ~3): (acc + 2^15) >> 16, selected per lane and column
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const uint32_t v = (__umulhi(B0, h0[j]) + __umulhi(B1, h1[j]) + 2) >> 2;
-        packed |= v << (8 * j);
+        const float aj = j == 0 ? acc[0].x : j == 1 ? acc[0].y : j == 2 ? acc[1].x : acc[1].y;
+        const int v = min(((int)(aj * 65536.f) + (1 << 15)) >> 16, 255);
+        const uint32_t fixed = (packed & ~(0xFFu << (8 * j))) | ((uint32_t)v << (8 * j));
+        packed = xg + j >= simd_w ? fixed : packed;
       }
-      *(uint32_t*)&tl[er * kBIn + 4 * gq] = packed;
-      const int i = er - 3, cg = 4 * (gq - 1);  // interior row / first column in the tile
-      if (i >= 0 && i < ny && gq >= 1 && cg < nx) {
-        const int o = (y0 + i) * w + x0 + cg;
-        if (cg + 4 <= nx) {
-          __builtin_amdgcn_raw_buffer_store_b32(packed, rd, o, 0, 0);
-        } else {
-          for (int j = 0; j < nx - cg; j++) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(packed >> (8 * j)), rd, o + j, 0, 0);
-        }
-      }
+    }
+    outv[r] = packed;
+  }
+  }  // active
+  // Write-out in the level's tile layout (8 rows x 16 bytes = 128-B tiles, the layout k_describe
+  // gathers from): the outputs go to LDS (the input tile is no longer read) in tile order, then
+  // leave as whole 128-B lines, 16 B per lane: the block's 128 x 128 outputs are 16 tile rows of
+  // 8 consecutive tiles (1 KB each).  Columns past w and rows past h land in the level's padding.
+  __syncthreads();
+  if (active) {
+#pragma unroll
+    for (int r = 0; r < kBStrip; r++) {
+      const int yr = ys + r, c = 4 * g;
+      *(uint32_t*)&tin[((yr >> 3) * (kBlurTileW / 16) + (c >> 4)) * 128 + (yr & 7) * 16 + (c & 15)] = outv[r];
     }
   }
   __syncthreads();
-  // 4. blur of the tile's 128 x kRbTH outputs from tl, staged over hb (no longer read) for the write-out
-  constexpr int SR = kRbTH / 8;
-  const int g = tid & (kBlurTileW / 4 - 1);
-  const int ys = (tid / (kBlurTileW / 4)) * SR;
-  const int xg = x0 + 4 * g;
-  const bool active = xg < w && y0 + ys < h;
-  uint32_t outv[SR];
-  if (active) blur_strip<SR>(tl, g, ys, xg, w, outv);
-  blur_tile_out<kRbTH>((uint8_t*)hb, outv, active, g, ys, B.blur + (size_t)img * G->blur_bytes + L.boff, L.bstride, h,
-                       x0, y0, tid);
+  {
+    const int ntx = bs >> 4, nty = (h + 7) >> 3;
+    const int tx0 = x0 >> 4, ty0 = y0 >> 3;
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, nty * ntx * 128, 0x00020000);
+    constexpr int kTiles = (kBlurTileW / 16) * (kBlurTileH / 8), kChunks = kTiles * 8;  // 16-B chunks
+#pragma unroll
+    for (int k = 0; k < kChunks / BS; k++) {
+      const int q = tid + k * BS, t = q >> 3, tr = t / (kBlurTileW / 16), tc = t - tr * (kBlurTileW / 16);
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *(const u32x4*)&tin[q * 16];
+      if (tx0 + tc < ntx && ty0 + tr < nty)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rd, (uint32_t)(((ty0 + tr) * ntx + tx0 + tc) * 128 + (q & 7) * 16), 0, 0);
+    }
+  }
 }
 
 // ------------------------------------------------------------------- FAST
@@ -1744,18 +1575,10 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
                                  const int* tile_level, const ResizeX* xt, const ResizeY* yt, const BatchPtrs& B,
                                  int n_img, orbx_keypoint* kps, uint8_t* desc, int32_t* counts, int kp_cap,
                                  hipStream_t st, StageTimer* T) {
-  // levels >= 1: resize + blur in one pass per level (k_resize_blur) when its footprint fits LDS,
-  // else k_resize per level and k_blur over every level's tiles below
-  const bool fused = Gh.rb_rows > 0;
   for (int l = 1; l < Gh.nlevels; l++) {
+    dim3 grid((Gh.lv[l].w + kRzTW - 1) / kRzTW, (Gh.lv[l].h + kRzTH - 1) / kRzTH, n_img);
     T->begin(st);
-    if (fused) {
-      dim3 grid((Gh.lv[l].w + kBlurTileW - 1) / kBlurTileW, (Gh.lv[l].h + kRbTH - 1) / kRbTH, n_img);
-      hipLaunchKernelGGL(k_resize_blur, grid, dim3(BS), resize_blur_smem(Gh.rb_rows, Gh.rb_stride), st, Gd, xt, yt, B, l);
-    } else {
-      dim3 grid((Gh.lv[l].w + kRzTW - 1) / kRzTW, (Gh.lv[l].h + kRzTH - 1) / kRzTH, n_img);
-      hipLaunchKernelGGL(k_resize, grid, dim3(BS), (size_t)Gh.rz_rows * (Gh.rz_stride + 2 * kRzTW), st, Gd, xt, yt, B, l);
-    }
+    hipLaunchKernelGGL(k_resize, grid, dim3(BS), (size_t)Gh.rz_rows * (Gh.rz_stride + 2 * kRzTW), st, Gd, xt, yt, B, l);
     T->end(ST_RESIZE, st);
   }
   if (Gh.ncells > 0) {
@@ -1774,9 +1597,7 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   }
   {
     T->begin(st);
-    // (level 0's tiles come first in the tile list)
-    const int nt = fused ? Gh.lv[0].tiles_x * Gh.lv[0].tiles_y : Gh.ntiles;
-    hipLaunchKernelGGL(k_blur, dim3(nt, n_img), dim3(BS), 0, st, Gd, tile_level, B);
+    hipLaunchKernelGGL(k_blur, dim3(Gh.ntiles, n_img), dim3(BS), 0, st, Gd, tile_level, B);
     T->end(ST_BLUR, st);
   }
   if (Gh.ncells > 0) {

@@ -66,14 +66,10 @@ struct Geometry {
   int rz_rows;    // k_resize: max source rows staged per 128x16 output tile
   int rz_stride;  // k_resize: LDS row stride of the staged footprint (16-B chunks covering the widest span)
   int rz_lc;      // k_resize: log2 of the lanes per footprint row (>= the widest span's 16-B chunks)
-  int rb_rows;    // k_resize_blur: max source rows of an extended tile's footprint (0: not used)
-  int rb_stride;  // k_resize_blur: LDS row stride of the staged footprint
-  int rb_lc;      // k_resize_blur: log2 of the lanes per footprint row
 };
 
 constexpr int kRzTW = 128, kRzTH = 32;  // k_resize output tile
 constexpr int kRzMaxRows = 64;
-constexpr int kRbMaxRows = 96;  // k_resize_blur footprint rows (host-checked)
 
 struct CellInfo {
   int16_t level, pad;
@@ -99,19 +95,6 @@ struct ResizeY {
 #endif
 constexpr int kBlurTileW = ORBX_BLUR_TW, kBlurTileH = ORBX_BLUR_TH;
 static_assert(kBlurTileW / 4 * (kBlurTileH / 16) == 256, "k_blur: one thread per 4 columns x 16 rows");
-
-// k_resize_blur: 128 x kRbTH output tiles of a level >= 1 over an extended (kRbTH + 6) x kRbEW region
-#ifndef ORBX_RB_TH
-#define ORBX_RB_TH 32
-#endif
-constexpr int kRbTH = ORBX_RB_TH;
-constexpr int kRbER = kRbTH + 6;            // extended rows y0-3 .. y0+kRbTH+2
-constexpr int kRbEW = kBlurTileW + 16;      // extended columns x0-4 .. x0+139 (k_blur's input tile stride)
-// dynamic LDS: the footprint (rows x stride; later the extended level tile) then the int16 rows
-__host__ __device__ inline size_t resize_blur_smem(int rows, int stride) {
-  const size_t tin = (size_t)rows * stride, tl = (size_t)(kRbER + 1) * kRbEW;
-  return ((tin > tl ? tin : tl) + 15) / 16 * 16 + (size_t)rows * kRbEW * 2;
-}
 
 // Device pointers for one batch.
 struct BatchPtrs {
