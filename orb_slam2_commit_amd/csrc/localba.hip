@@ -2709,24 +2709,33 @@ struct Ctx {
 
 // Pinned host staging buffer + one device arena: arrays are laid out with
 // take(), filled through host(), and sent with one async copy.
+// A pinned host block and its device twin, carved by take() in the same offsets.  mapped: no
+// twin -- dbuf is the device's view of the pinned block itself, so kernels write results straight
+// into host memory (no copy, no copy engine hand-off after the last kernel)
 struct Arena {
   uint8_t* hbuf = nullptr;
   uint8_t* dbuf = nullptr;
   size_t cap = 0, off = 0;
-  ~Arena() {
+  bool mapped = false;
+  explicit Arena(bool m = false) : mapped(m) {}
+  ~Arena() { release(); }
+  void release() {
     if (hbuf) (void)hipHostFree(hbuf);
-    if (dbuf) (void)hipFree(dbuf);
+    if (dbuf && !mapped) (void)hipFree(dbuf);
+    hbuf = dbuf = nullptr;
   }
   hipError_t reserve(size_t bytes) {
     off = 0;
     if (bytes <= cap && hbuf) return hipSuccess;
-    if (hbuf) (void)hipHostFree(hbuf);
-    if (dbuf) (void)hipFree(dbuf);
-    hbuf = dbuf = nullptr;
+    release();
     cap = bytes + bytes / 4 + 4096;
-    hipError_t e = hipHostMalloc((void**)&hbuf, cap, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipMalloc((void**)&dbuf, cap);
-    if (e != hipSuccess) cap = 0;
+    hipError_t e = hipHostMalloc((void**)&hbuf, cap, mapped ? hipHostMallocMapped : hipHostMallocDefault);
+    if (e == hipSuccess)
+      e = mapped ? hipHostGetDevicePointer((void**)&dbuf, hbuf, 0) : hipMalloc((void**)&dbuf, cap);
+    if (e != hipSuccess) {
+      release();
+      cap = 0;
+    }
     return e;
   }
   template <class T>
@@ -2746,7 +2755,9 @@ struct Arena {
     if (!v.empty()) std::memcpy(host(d), v.data(), v.size() * sizeof(T));
     return d;
   }
-  hipError_t upload(hipStream_t st) { return off ? hipMemcpyAsync(dbuf, hbuf, off, hipMemcpyHostToDevice, st) : hipSuccess; }
+  hipError_t upload(hipStream_t st) {
+    return off && !mapped ? hipMemcpyAsync(dbuf, hbuf, off, hipMemcpyHostToDevice, st) : hipSuccess;
+  }
 };
 
 inline size_t arena_bytes(std::initializer_list<size_t> sizes) {
@@ -2759,9 +2770,11 @@ struct LocalBA {
   BaDev D{};
   Ctx c;  // device buffers, kept across calls (grow only)
   Arena prob_arena, struct_arena;
-  // result write-back: one device arena (flags, poses, points) read back by ONE copy into pinned
-  // memory, then host copies into the caller's arrays (pageable copies each block the host)
-  Arena wb_arena;
+  // result write-back: k_ba_outliers / k_ba_export write the flags, poses and points straight
+  // into a mapped pinned block, then host copies into the caller's arrays.  (A device arena read
+  // back by one copy measured 81 us of copy-engine hand-off after k_ba_export plus the 11 us copy
+  // per call, profiles/r05/localba_timeline_*.txt)
+  Arena wb_arena{true};
   struct Wb {
     double *Tcw_d, *Xw_d;
     float *Tcw, *Xw;
@@ -3405,8 +3418,8 @@ orbx_status ba_writeback(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       for (int i = 0; i < 3 * np; i++) res->Xw_d[i] = pb->Xw[i];
     return ORBX_OK;
   }
-  // :817-847 vToErase, then the poses and points; everything lands in the write-back arena and
-  // leaves in one copy (ba_writeback_finish moves it into the caller's arrays after the sync)
+  // :817-847 vToErase, then the poses and points; everything lands in the mapped write-back arena
+  // (ba_writeback_finish moves it into the caller's arrays after the sync)
   Arena& A = L.wb_arena;
   BA_CHECK(A.reserve(arena_bytes({res->Tcw_d ? 12 * sizeof(double) * nc : 0, res->Xw_d ? 3 * sizeof(double) * np : 0,
                                   12 * sizeof(float) * nc, 3 * sizeof(float) * np, (size_t)ne})));
@@ -3420,7 +3433,6 @@ orbx_status ba_writeback(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   const int gx = (std::max(nc, np) + LBS - 1) / LBS;
   hipLaunchKernelGGL(k_ba_export, dim3(std::max(gx, 1)), dim3(LBS), 0, st, D, w.Tcw, w.Xw, w.Tcw_d, w.Xw_d);
   BA_CHECK(hipGetLastError());
-  BA_CHECK(hipMemcpyAsync(A.hbuf, A.dbuf, A.off, hipMemcpyDeviceToHost, st));
   return ORBX_OK;
 }
 

@@ -13,12 +13,15 @@ def main(reps=10):
     P = synth.localba_problem(seed=7)
     o = Optimizer(0)
     r = o.LocalBundleAdjustment(P)  # warm-up (allocations, code load)
+    ts = []
     t0 = time.perf_counter()
     for _ in range(reps):
+        t1 = time.perf_counter()
         r = o.LocalBundleAdjustment(P)
+        ts.append(time.perf_counter() - t1)
     dt = (time.perf_counter() - t0) / reps
     its = sum(r["iterations"])
-    print(json.dumps(dict(ms_per_call=dt * 1e3, iterations=r["iterations"], trials=r["trials"],
+    print(json.dumps(dict(ms_per_call=dt * 1e3, median_ms=float(np.median(ts)) * 1e3, iterations=r["iterations"], trials=r["trials"],
                           iters_per_s=its / dt, trials_per_s=r["trials"] / dt,
                           edges=int(len(P["edge_point"])))))
 
