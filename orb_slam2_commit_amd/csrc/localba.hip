@@ -33,7 +33,9 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -292,6 +294,12 @@ struct BaDev {
   int nbu;         // k_ba_update blocks (its LM-scale partials)
   double* scal;    // scalars: [0] chi at iteration start, [1] chi after the trial, [2] solve ok, [3] max diag, [4] LM scale
   const LmState* lm;  // device LM state: gates the trial's kernels and carries lambda (null: host control)
+  // phase-end readout (set on the last k_ba_errors launch of a phase only): the launch also writes
+  // its block partials, block 0 the rest of the readback block and *lm_copy, into mapped pinned
+  // memory (rb_out, lm_out), so the host reads them after one event with no copy launches
+  double* rb_out;
+  LmState* lm_out;
+  const LmState* lm_copy;
   int nan_trial;      // debug (ORBX_BA_NAN_TRIAL): this trial's chi is NaN; -1 off
   int raise_after;    // debug (ORBX_BA_RAISE_STOP_AFTER): the device raises the stop mirror after this many trials; -1 off
 };
@@ -368,10 +376,13 @@ __device__ inline double block_sum1(double v, double* red /* LDS [LBS/64] */) {
 // Block partial of a grid-wide sum: stored to out[blockIdx.x]; the host adds
 // the partials in block order after its one readback per LM trial (fixed
 // order, no cross-block synchronisation on the device).
-__device__ inline void block_partial(double v, double* out) {
+__device__ inline void block_partial(double v, double* out, double* out2 = nullptr) {
   __shared__ double red[LBS / 64];
   const double bs = block_sum1(v, red);
-  if (threadIdx.x == 0) out[blockIdx.x] = bs;
+  if (threadIdx.x == 0) {
+    out[blockIdx.x] = bs;
+    if (out2) out2[blockIdx.x] = bs;
+  }
 }
 
 __device__ inline void edge_error(const BaDev& D, int e, double err[3], double& chi2) {
@@ -448,7 +459,19 @@ __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, 
     if (dst == 1 && k == 0 && D.nan_trial >= 0 && D.lm && D.lm->trials == D.nan_trial)
       chi = __builtin_nan("");
   }
-  block_partial(chi, D.scal + 8 + dst * D.nbe);
+  block_partial(chi, D.scal + 8 + dst * D.nbe, D.rb_out ? D.rb_out + 8 + dst * D.nbe : nullptr);
+  if (D.rb_out && blockIdx.x == 0) {
+    // the readback block's other entries (written by earlier launches), then the LM state
+    const int n_rb = 8 + 2 * D.nbe + D.nbu;
+    for (int i = threadIdx.x; i < n_rb; i += LBS)
+      if (i < 8 + dst * D.nbe || i >= 8 + (dst + 1) * D.nbe) D.rb_out[i] = D.scal[i];
+    if (D.lm_out) {
+      constexpr int kW = sizeof(LmState) / 4;
+      static_assert(sizeof(LmState) % 4 == 0, "LmState copied as words");
+      if (threadIdx.x < kW)
+        reinterpret_cast<uint32_t*>(D.lm_out)[threadIdx.x] = reinterpret_cast<const uint32_t*>(D.lm_copy)[threadIdx.x];
+    }
+  }
 }
 __global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute, int dst) { k_ba_errors_body(D, recompute, dst); }
 __global__ __launch_bounds__(LBS) void k_ba_errors_many(const BaDev* __restrict__ Ds, int recompute, int dst) {
@@ -1905,6 +1928,22 @@ __global__ __launch_bounds__(NT) void k_ba_ldlt_pan_many(const BaDev* __restrict
   k_ba_ldlt_pan_body<TPT, NT, R>(Ds[blockIdx.z]);
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device), raised only when a larger
+// size is asked for: the runtime call costs microseconds and used to sit between the launches of
+// every LM phase (the device idled behind it)
+inline hipError_t set_smem_attr(const void* fn, size_t bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(mu);
+  size_t& have = done[{fn, dev}];
+  if (bytes <= have) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) have = bytes;
+  return e;
+}
+
 // Launch plan for the reduced system: the 8-wide panel kernel (N < 128), the column-step kernel while
 // the packed factor fits LDS, else the 16-wide blocked MFMA kernel (LDS or global).  The debug options
 // (orbx_debug_ba_options) can force the column-step or the blocked kernel where they fit, for tests.
@@ -1921,7 +1960,7 @@ struct LdltPlan {
       nt = 512;
       tpt = 1;
       smem = ldlt_pan_smem(N);
-      return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+      return set_smem_attr(kernel_ptr(), smem);
     }
     col = ldlt_col_fits(N) && ba_opts().ldlt != ORBX_BA_LDLT_BLOCKED;
     if (col) {
@@ -1938,7 +1977,7 @@ struct LdltPlan {
       in_lds = ldlt_np(N) <= kLdltLdsNp;
       smem = ldlt_smem_bytes(N, in_lds);
     }
-    return hipFuncSetAttribute(kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    return set_smem_attr(kernel_ptr(), smem);
   }
   const void* kernel_ptr() const {
     if (pan) return (const void*)k_ba_ldlt_pan<1, 512, 2>;
@@ -1963,7 +2002,7 @@ struct LdltPlan {
                     : tpt == 4 ? (const void*)k_ba_ldlt_col_many<4, 256> : (const void*)k_ba_ldlt_col_many<8, 256>;
   }
   hipError_t prepare_many() const {
-    return hipFuncSetAttribute(many_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    return set_smem_attr(many_ptr(), smem);
   }
   void launch_many(const BaDev* Ds, int K, hipStream_t st) const {
     hipLaunchKernelGGL(reinterpret_cast<void (*)(const BaDev*)>(const_cast<void*>(many_ptr())), dim3(1, 1, K),
@@ -2785,7 +2824,8 @@ struct LocalBA {
   std::vector<uint8_t> level;  // 0/1 per edge
   int trials = 0;
   int nbu = 1, n_rb = 8;           // k_ba_update blocks; doubles in the readback block
-  double* rb_host = nullptr;       // pinned readback block
+  double* rb_host = nullptr;       // pinned readback block (mapped: rb_map is the device's view)
+  double* rb_map = nullptr;
   int rb_cap = 0;
   hipEvent_t rb_ev = nullptr;      // recorded after the readback copy (the wait skips later work)
   // the linearisation outputs the LM trials read
@@ -2848,7 +2888,8 @@ struct LocalBA {
   bool dev_struct = false;  // k_ba_struct_* build the arrays (edges grouped by point, nc <= kStructMaxNc)
   const uint8_t* dfix = nullptr;  // device copy of the fixed flags
   DBuf<int> sbuf;                 // k_ba_struct_* tiles and outputs, sized for the whole edge list
-  int* sint_host = nullptr;       // pinned: k_ba_struct_scan's five sizes
+  int* sint_host = nullptr;       // pinned, mapped: k_ba_struct_scan's five sizes (written there directly)
+  int* sint_map = nullptr;
   int sizes1[5] = {0, 0, 0, 0, 0};  // phase-1 sizes (all edges active), counted on the host
   orbx_status build_structure(int lvl, hipStream_t st) {
     if (dev_struct) return build_structure_dev(lvl, st, lvl < 0 ? sizes1 : nullptr);
@@ -2971,7 +3012,10 @@ struct LocalBA {
     const int ntiles = (ne + kTileE - 1) / kTileE;
     const size_t nb = (size_t)nc * (nc + 1) / 2 + 1;
     BA_CHECK(sbuf.alloc(8 * (size_t)ntiles + (size_t)ntiles * nc + 6 * (size_t)ne + 1 + 3 * (size_t)nc + 1 + nb + 8));
-    if (!sint_host) BA_CHECK(hipHostMalloc((void**)&sint_host, 8 * sizeof(int), hipHostMallocDefault));
+    if (!sint_host) {
+      BA_CHECK(hipHostMalloc((void**)&sint_host, 8 * sizeof(int), hipHostMallocMapped));
+      BA_CHECK(hipHostGetDevicePointer((void**)&sint_map, sint_host, 0));
+    }
     int* p = sbuf.p;
     int4* ttot = reinterpret_cast<int4*>(p);  // first: 16-byte aligned
     p += 4 * (size_t)ntiles;
@@ -2994,7 +3038,7 @@ struct LocalBA {
       hipLaunchKernelGGL(k_ba_struct_count, dim3(ntiles), dim3(kTileT), sizeof(int) * (nc + kTileT / 64), st, D, fl,
                          lvl, tcnt, ttot);
     hipLaunchKernelGGL(k_ba_struct_scan, dim3(1), dim3(kStructNT), sizeof(int) * (nc + 1 + kStructNT / 64), st, D,
-                       dfix, ntiles, tcnt, ttot, tcar, p);
+                       dfix, ntiles, tcnt, ttot, tcar, known ? p : sint_map);
     if (ntiles > 0)
       hipLaunchKernelGGL(k_ba_struct_fill, dim3(ntiles), dim3(kTileT),
                          sizeof(int) * ((1 + kTileT / 64) * (size_t)nc + kTileE + kTileT / 64), st, D, fl, lvl, tcnt,
@@ -3002,7 +3046,6 @@ struct LocalBA {
     BA_CHECK(hipGetLastError());
     const int* sz = known;
     if (!sz) {
-      BA_CHECK(hipMemcpyAsync(sint_host, p, 5 * sizeof(int), hipMemcpyDeviceToHost, st));
       BA_CHECK(hipStreamSynchronize(st));
       sz = sint_host;
     }
@@ -3048,7 +3091,8 @@ struct LocalBA {
       if (rb_host) (void)hipHostFree(rb_host);
       rb_host = nullptr;
       rb_cap = 0;
-      BA_CHECK(hipHostMalloc((void**)&rb_host, n_rb * sizeof(double), hipHostMallocDefault));
+      BA_CHECK(hipHostMalloc((void**)&rb_host, n_rb * sizeof(double), hipHostMallocMapped));
+      BA_CHECK(hipHostGetDevicePointer((void**)&rb_map, rb_host, 0));
       rb_cap = n_rb;
     }
     BA_CHECK(c.ptab.alloc(nslots));
@@ -3119,7 +3163,8 @@ struct LocalBA {
   // queues as many trials as iterations remain (every trial ends at most one
   // iteration), reads the state back once, and queues more only after
   // rejections; a finished phase turns the queued rest into empty launches.
-  LmState* lm_host = nullptr;  // pinned
+  LmState* lm_host = nullptr;  // pinned, mapped (lm_map: the device's view)
+  LmState* lm_map = nullptr;
   orbx_status optimize_dev(int iterations, const StopFlag& stop, const DevStop& dstop, hipStream_t st, int* iters,
                            double* final_chi) {
     const size_t N = 6 * (size_t)D.nposes;
@@ -3132,7 +3177,10 @@ struct LocalBA {
       D.Sw = c.Sw.p;
     }
     BA_CHECK(c.lm.alloc(1));
-    if (!lm_host) BA_CHECK(hipHostMalloc((void**)&lm_host, sizeof(LmState), hipHostMallocDefault));
+    if (!lm_host) {
+      BA_CHECK(hipHostMalloc((void**)&lm_host, sizeof(LmState), hipHostMallocMapped));
+      BA_CHECK(hipHostGetDevicePointer((void**)&lm_map, lm_host, 0));
+    }
     const int gp = std::max((D.npa + D.nposes + LBS - 1) / LBS, 1);
     const int ga = std::max((D.na + LBS - 1) / LBS, 1);
     const int ge = std::max((D.na + LBS - 1) / LBS, 1);
@@ -3152,8 +3200,7 @@ struct LocalBA {
       BA_CHECK(hipGetLastError());
       const bool fused = Dg.nbf > 0;
       if (fused)
-        BA_CHECK(hipFuncSetAttribute((const void*)k_ba_lin_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)kFuseSmem));
+        BA_CHECK(set_smem_attr((const void*)k_ba_lin_schur, kFuseSmem));
       const bool psfold = Dg.fused == 2;
       auto trial = [&](bool lin) {
         // linearisation gated on the device: only at the start of a new iteration
@@ -3176,11 +3223,15 @@ struct LocalBA {
       for (int budget = iterations, first = 1;; first = 0) {
         for (int t = 0; t < budget; t++) trial(!(first && t == 0));  // t = 0: linearised by the entry launches
         // the phase's final activeRobustChi2 of the stored errors rides on the same readback
-        // (slot 0 is not read by the trials; a batch that did not finish recomputes it later)
-        hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, D0, 0, 0);
+        // (slot 0 is not read by the trials; a batch that did not finish recomputes it later); the
+        // launch writes the readback block and the LM state into mapped memory itself
+        BaDev Dr = D0;
+        Dr.rb_out = rb_map;
+        Dr.lm_out = lm_map;
+        Dr.lm_copy = c.lm.p;
+        hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, Dr, 0, 0);
         BA_CHECK(hipGetLastError());
-        BA_CHECK(hipMemcpyAsync(lm_host, c.lm.p, sizeof(LmState), hipMemcpyDeviceToHost, st));
-        BA_CHECK(start_read(st));
+        BA_CHECK(hipEventRecord(rb_ev, st));
         BA_CHECK(finish_read(sc));
         if (lm_host->refresh) {  // paused on a NaN-rho rejection: pop, errors at the restored state, resume
           hipLaunchKernelGGL(k_ba_restore, dim3(gp), dim3(LBS), 0, st, Dg);
@@ -3590,8 +3641,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
   const BaDev* Dg = B.dev.p;
   const BaDev* D0 = B.dev.p + K;
   if (nbfM > 0)
-    BA_CHECK(hipFuncSetAttribute((const void*)k_ba_lin_schur_many, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)kFuseSmem));
+    BA_CHECK(set_smem_attr((const void*)k_ba_lin_schur_many, kFuseSmem));
   // the entry launches (D0: no LM state, nothing fused) and the gated trials: per problem either
   // k_ba_lin_schur or the three separate kernels do the point side (each returns for the other)
   auto linearize = [&](const BaDev* Ds) {
