@@ -214,6 +214,7 @@ struct LmState {
                    // phase pauses (done) until the host pops the trial, recomputes the errors at
                    // the restored state and resumes (k_ba_lm_resume), as g2o's next iteration does
   double final_chi;  // batched driver: activeRobustChi2 of the stored errors at the phase end
+  unsigned ticket;   // k_ba_errors_ctl: blocks of the current launch that have stored their partial
 };
 
 // rho's cube rounded once (std::pow(x, 3) in the reference; glibc's pow is
@@ -425,10 +426,24 @@ __device__ inline void huber(double chi, double delta, float dsqr, double rho[3]
   }
 }
 
-__device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, int dst) {
+// Relaxed agent-scope store / load of a double: written through / read past the XCD's L2, so a
+// value one block stores is seen by another block of the same launch (k_ba_errors_ctl's partials)
+__device__ inline void st_agent(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline double ld_agent(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Returns false where the block did nothing (gated launch, block past the problem): uniform per block.
+// coh: the block partial is stored write-through (st_agent) for k_ba_errors_ctl's last block.
+template <bool coh = false>
+__device__ __forceinline__ bool k_ba_errors_body(const BaDev& D, int recompute, int dst) {
   // recompute == 2: the refresh launch (only while the device LM state asks for it)
-  if (recompute == 2 ? !(D.lm && D.lm->refresh) : lm_skip(D)) return;
-  if ((int)blockIdx.x >= D.nbe) return;  // (a batched grid spans the largest problem)
+  if (recompute == 2 ? !(D.lm && D.lm->refresh) : lm_skip(D)) return false;
+  if ((int)blockIdx.x >= D.nbe) return false;  // (a batched grid spans the largest problem)
   const int k = blockIdx.x * LBS + threadIdx.x;
   double chi = 0;
   if (k < D.na) {
@@ -459,6 +474,12 @@ __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, 
     if (dst == 1 && k == 0 && D.nan_trial >= 0 && D.lm && D.lm->trials == D.nan_trial)
       chi = __builtin_nan("");
   }
+  if (coh) {
+    __shared__ double red[LBS / 64];
+    const double bs = block_sum1(chi, red);
+    if (threadIdx.x == 0) st_agent(D.scal + 8 + dst * D.nbe + blockIdx.x, bs);
+    return true;
+  }
   block_partial(chi, D.scal + 8 + dst * D.nbe, D.rb_out ? D.rb_out + 8 + dst * D.nbe : nullptr);
   if (D.rb_out && blockIdx.x == 0) {
     // the readback block's other entries (written by earlier launches), then the LM state
@@ -472,6 +493,7 @@ __device__ __forceinline__ void k_ba_errors_body(const BaDev& D, int recompute, 
         reinterpret_cast<uint32_t*>(D.lm_out)[threadIdx.x] = reinterpret_cast<const uint32_t*>(D.lm_copy)[threadIdx.x];
     }
   }
+  return true;
 }
 __global__ __launch_bounds__(LBS) void k_ba_errors(BaDev D, int recompute, int dst) { k_ba_errors_body(D, recompute, dst); }
 __global__ __launch_bounds__(LBS) void k_ba_errors_many(const BaDev* __restrict__ Ds, int recompute, int dst) {
@@ -2209,6 +2231,7 @@ __device__ inline double seq_sum_wave(const double* p, int n) {
 
 // Two such sums at once (same orders and bits as two seq_sum_wave calls): both arrays' loads are
 // in flight together and lane 0 adds the first while lane 1 adds the second (valid in lane 0).
+template <bool coh = false>  // coh: p is read with ld_agent (partials stored by this launch's other blocks)
 __device__ inline void seq_sum2_wave(const double* p, int n, const double* q, int m, double& sp, double& sq) {
   __shared__ double buf[2][512];
   double s = 0;
@@ -2219,7 +2242,7 @@ __device__ inline void seq_sum2_wave(const double* p, int n, const double* q, in
 #pragma unroll
     for (int u = 0; u < 8; u++) {  // clamped, unpredicated loads: all sixteen in flight at once
       const int i = threadIdx.x + 64 * u;
-      vp[u] = p[max(min(base + i, n - 1), 0)];
+      vp[u] = coh ? ld_agent(p + max(min(base + i, n - 1), 0)) : p[max(min(base + i, n - 1), 0)];
       vq[u] = q[max(min(base + i, m - 1), 0)];
     }
 #pragma unroll
@@ -2254,6 +2277,7 @@ __device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations
   L->stopped = 0;  // the host polled the flag just before this phase
   L->refresh = 0;
   L->done = iterations <= 0 ? 1 : 0;
+  L->ticket = 0;
 }
 __global__ __launch_bounds__(64) void k_ba_lm_init(BaDev D, int iterations) { k_ba_lm_init_body(D, iterations); }
 __global__ __launch_bounds__(64) void k_ba_lm_init_many(const BaDev* __restrict__ Ds, int iterations) {
@@ -2266,6 +2290,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_init_many(const BaDev* __restrict_
 // block order, accept (lambda *= max(1/3, min(2/3, 1-(2rho-1)^3))) or reject
 // (lambda *= ni, ni *= 2, restore), then the iteration bookkeeping: the
 // <= 10 trial budget, rho == 0, the _nBad rule and the stop flag.
+template <bool coh = false>
 __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop stop) {
   LmState* L = const_cast<LmState*>(D.lm);
   const int nbu = D.nbu;
@@ -2275,7 +2300,7 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
   const bool st = stop() || (D.raise_after >= 0 && L->trials >= D.raise_after);  // (+ test hook)
   const double* p = D.scal + 8;
   double b, u;
-  seq_sum2_wave(p + D.nbe, D.nbe, p + 2 * D.nbe, nbu, b, u);
+  seq_sum2_wave<coh>(p + D.nbe, D.nbe, p + 2 * D.nbe, nbu, b, u);
   if (threadIdx.x != 0) return;
   L->rejected = 0;
   const bool ok2 = D.scal[2] != 0.0;
@@ -2344,6 +2369,24 @@ __global__ __launch_bounds__(64) void k_ba_lm_resume_many(const BaDev* __restric
   k_ba_lm_resume_body(Ds[blockIdx.z]);
 }
 __global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, DevStop stop) { k_ba_lm_control_body(D, stop); }
+
+// A trial's k_ba_errors(D, 1, 1) and k_ba_lm_control in one launch (single-problem device LM): every
+// block stores its chi partial write-through and, once the store has landed, takes a ticket; the
+// block that takes the last one runs the verdict with wave 0, reading the partials past its L2.  Same
+// partials, same order, same arithmetic as the two launches (one dispatch less per trial).
+__global__ __launch_bounds__(LBS) void k_ba_errors_ctl(BaDev D, DevStop stop) {
+  if (!k_ba_errors_body<true>(D, 1, 1)) return;
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_s_waitcnt(0);  // the partial's write-through store is complete
+    unsigned* tk = &const_cast<LmState*>(D.lm)->ticket;
+    last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(D.nbe - 1);
+    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last || threadIdx.x >= 64) return;  // (waves 1-3 leave; wave 0's barriers count only live waves)
+  k_ba_lm_control_body<true>(D, stop);
+}
 __global__ __launch_bounds__(64) void k_ba_lm_control_many(const BaDev* __restrict__ Ds, DevStop stop) {
   k_ba_lm_control_body(Ds[blockIdx.z], stop);
 }
@@ -3215,8 +3258,7 @@ struct LocalBA {
           ldlt.launch(Dg, st);
         }
         hipLaunchKernelGGL(k_ba_update, dim3(Dg.nbu), dim3(LBS), 0, st, Dg, 0.0);
-        hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, Dg, 1, 1);
-        hipLaunchKernelGGL(k_ba_lm_control, dim3(1), dim3(64), 0, st, Dg, dstop);
+        hipLaunchKernelGGL(k_ba_errors_ctl, dim3(Dg.nbe), dim3(LBS), 0, st, Dg, dstop);
       };
       // (capturing the trial as a HIP graph and launching that instead measured slower on this
       // stack: 2.81 vs 2.76 ms per config-4 call)
