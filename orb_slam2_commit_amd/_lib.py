@@ -277,8 +277,8 @@ def ptr(a):
     """Host numpy array or torch tensor (host or device) -> void*."""
     if a is None:
         return None
-    if isinstance(a, np.ndarray):
-        return a.ctypes.data_as(C.c_void_p)
+    if isinstance(a, np.ndarray):  # (the array interface's address: half the cost of ctypes.data_as)
+        return C.c_void_p(a.__array_interface__["data"][0])
     if hasattr(a, "data_ptr"):
         return C.c_void_p(a.data_ptr())
     raise TypeError(type(a))

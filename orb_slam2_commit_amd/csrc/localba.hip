@@ -17,13 +17,14 @@
 //   k_ba_schur_fin   S block (c1,c2) = [c1==c2](Hpp+lambda I) - pair sum; bschur = bp - sum cf
 //   k_ba_ldlt        dense LDLT of the reduced camera system in LDS, solve
 //   k_ba_update      x_l = Dinv (bl - sum_e Hpl_e^T x_p), X += x_l; T = exp(x_p) T; scale terms
-//   k_ba_errors      new chi (block partials)
-//   k_ba_lm_control  the LM verdict on the device: partials summed in block order,
-//                    accept/reject, lambda/ni, trial budget, _nBad, stop flag polled
-//                    through host-mapped memory; gates the next trial's kernels
+//   k_ba_errors_ctl  new chi (block partials), then the LM verdict in the launch's last block
+//                    (k_ba_lm_control's body): partials summed in block order, accept/reject,
+//                    lambda/ni, trial budget, _nBad, stop flag polled through host-mapped
+//                    memory; gates the next trial's kernels
 // Every reduction has a fixed partition and order: results are run-to-run
-// identical, with no cross-block atomics (an agent-scope release/acquire per
-// block costs an L2 writeback/invalidate on the multi-XCD part).
+// identical.  The one cross-block hand-off (k_ba_errors_ctl) uses write-through
+// partials and a relaxed ticket, not an agent-scope release/acquire (per block
+// that costs an L2 writeback/invalidate on the multi-XCD part).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -500,19 +501,6 @@ __global__ __launch_bounds__(LBS) void k_ba_errors_many(const BaDev* __restrict_
   k_ba_errors_body(Ds[blockIdx.z], recompute, dst);
 }
 
-// Deterministic sum / max of n doubles into *out (one block).
-__global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ in, int n, double* out, int op_max) {
-  __shared__ double s[1024];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += 1024) acc = op_max ? fmax(acc, in[i]) : acc + in[i];
-  s[threadIdx.x] = acc;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) s[threadIdx.x] = op_max ? fmax(s[threadIdx.x], s[threadIdx.x + o]) : s[threadIdx.x] + s[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *out = s[0];
-}
 
 // constructQuadraticForm of one edge with DIM-dimensional error (2 mono, 3 stereo)
 // One staged output array of the linearisation: each thread's NV values go to
@@ -2279,7 +2267,23 @@ __device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations
   L->done = iterations <= 0 ? 1 : 0;
   L->ticket = 0;
 }
-__global__ __launch_bounds__(64) void k_ba_lm_init(BaDev D, int iterations) { k_ba_lm_init_body(D, iterations); }
+// Lambda init (the max of |H_jj| over dmax_p -> scal[3], a 1024-wide tree) and the LM state init in one
+// launch (single-problem device LM); the batched driver runs k_ba_dmax_many + k_ba_lm_init_many
+__global__ __launch_bounds__(1024) void k_ba_lm_start(BaDev D, int iterations) {
+  __shared__ double sm[1024];
+  const int n = D.npa + D.nposes;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) acc = fmax(acc, D.dmax_p[i]);
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) D.scal[3] = sm[0];  // (read back below by the same thread)
+  if (threadIdx.x >= 64) return;
+  k_ba_lm_init_body(D, iterations);
+}
 __global__ __launch_bounds__(64) void k_ba_lm_init_many(const BaDev* __restrict__ Ds, int iterations) {
   k_ba_lm_init_body(Ds[blockIdx.z], iterations);
 }
@@ -2368,8 +2372,6 @@ __global__ __launch_bounds__(64) void k_ba_lm_resume(BaDev D) { k_ba_lm_resume_b
 __global__ __launch_bounds__(64) void k_ba_lm_resume_many(const BaDev* __restrict__ Ds) {
   k_ba_lm_resume_body(Ds[blockIdx.z]);
 }
-__global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, DevStop stop) { k_ba_lm_control_body(D, stop); }
-
 // A trial's k_ba_errors(D, 1, 1) and k_ba_lm_control in one launch (single-problem device LM): every
 // block stores its chi partial write-through and, once the store has landed, takes a ticket; the
 // block that takes the last one runs the verdict with wave 0, reading the partials past its L2.  Same
@@ -2392,7 +2394,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_control_many(const BaDev* __restri
 }
 
 // Batched driver helpers (one block per problem, blockIdx.z): the lambda-init
-// maximum of |H_jj| (k_reduce's partition and order) and the phase's final
+// maximum of |H_jj| (k_ba_lm_start's partition and order) and the phase's final
 // chi from errors slot 0 (summed in block order, like the host readback).
 __global__ __launch_bounds__(1024) void k_ba_dmax_many(const BaDev* __restrict__ Ds) {
   const BaDev& D = Ds[blockIdx.z];
@@ -3238,8 +3240,7 @@ struct LocalBA {
     if (!(stop())) {  // the loop head's first poll (i = 0)
       hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, D0, 1, 0);
       linearize(D0, st);
-      hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, D0.dmax_p, D0.npa + D0.nposes, D0.scal + 3, 1);
-      hipLaunchKernelGGL(k_ba_lm_init, dim3(1), dim3(64), 0, st, Dg, iterations);
+      hipLaunchKernelGGL(k_ba_lm_start, dim3(1), dim3(1024), 0, st, Dg, iterations);
       BA_CHECK(hipGetLastError());
       const bool fused = Dg.nbf > 0;
       if (fused)
@@ -3546,8 +3547,12 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
                          hipStream_t st) {
   double host_build_ms = 0;
   const auto t_start = std::chrono::steady_clock::now();
+  // host-side marks for the trace line: intake, phase-1 structure, phase 1, phase-2 structure, phase 2
+  std::chrono::steady_clock::time_point tm[5];
+  for (auto& t : tm) t = t_start;
   orbx_status s0 = ba_intake(L, pb, st);
   if (s0 != ORBX_OK) return s0;
+  tm[0] = std::chrono::steady_clock::now();
   BaDev& D = L.D;
   Ctx& c = L.c;
   const int ne = pb->n_edges;
@@ -3571,9 +3576,11 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
     orbx_status s = L.build_structure(-1, st);
     const auto tb1 = std::chrono::steady_clock::now();
     host_build_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
+    tm[1] = tb1;
     if (s != ORBX_OK) return s;
     s = optimize(5, &res->iterations[0], &res->chi2[0]);
     if (s != ORBX_OK) return s;
+    tm[2] = tm[3] = tm[4] = std::chrono::steady_clock::now();
     if (!(stop()) && !L.hook_stopped) {
       // :764-802 level-1 outliers, drop robust kernels
       if (ne > 0) hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 1);
@@ -3584,10 +3591,12 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
       }
       const auto tb2 = std::chrono::steady_clock::now();
       s = L.build_structure(0, st);
-      host_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb2).count();
+      tm[3] = std::chrono::steady_clock::now();
+      host_build_ms += std::chrono::duration<double, std::milli>(tm[3] - tb2).count();
       if (s != ORBX_OK) return s;
       s = optimize(10, &res->iterations[1], &res->chi2[1]);
       if (s != ORBX_OK) return s;
+      tm[4] = std::chrono::steady_clock::now();
     }
   }
   BA_CHECK(ba_writeback(L, pb, res, ran, st));
@@ -3595,13 +3604,19 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   if (!ran) return ORBX_OK;
   BA_CHECK(hipStreamSynchronize(st));
   ba_writeback_finish(L, pb, res, ran);
-  if (ba_opts().trace)
+  if (ba_opts().trace) {
+    const auto t_end = std::chrono::steady_clock::now();
+    auto d = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
     std::fprintf(stderr,
                  "[orbx_ba] total %.3f ms, structure %.3f ms (host index %.3f, host poses %.3f, device %.3f, upload %.3f), "
-                 "iterations %d+%d, trials %d\n",
-                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(),
-                 host_build_ms, L.t_struct[0], L.t_struct[1], L.t_struct[2], L.t_struct[3], res->iterations[0],
-                 res->iterations[1], res->trials);
+                 "iterations %d+%d, trials %d; host marks: intake %.3f, struct1 %.3f, phase1 %.3f, struct2 %.3f, "
+                 "phase2 %.3f, writeback %.3f ms\n",
+                 d(t_start, t_end), host_build_ms, L.t_struct[0], L.t_struct[1], L.t_struct[2], L.t_struct[3],
+                 res->iterations[0], res->iterations[1], res->trials, d(t_start, tm[0]), d(tm[0], tm[1]),
+                 d(tm[1], tm[2]), d(tm[2], tm[3]), d(tm[3], tm[4]), d(tm[4], t_end));
+  }
   return ORBX_OK;
 }
 

@@ -612,8 +612,9 @@ class Optimizer:
         nc, npt, ne = len(a["Tcw"]), len(a["Xw"]), len(a["edge_point"])
         P = _lib.BaProblem(nc, ptr(a["Tcw"]), ptr(a["fixed"]), ptr(a["intr"]), npt, ptr(a["Xw"]), ne,
                            ptr(a["edge_point"]), ptr(a["edge_cam"]), ptr(a["obs"]), ptr(a["inv_sigma2"]))
-        out = dict(Tcw=np.zeros((nc, 12), np.float32), Xw=np.zeros((npt, 3), np.float32),
-                   edge_outlier=np.zeros(ne, np.uint8), Tcw_d=np.zeros((nc, 12)), Xw_d=np.zeros((npt, 3)))
+        # (every output element is written by the call: no zero fill)
+        out = dict(Tcw=np.empty((nc, 12), np.float32), Xw=np.empty((npt, 3), np.float32),
+                   edge_outlier=np.empty(ne, np.uint8), Tcw_d=np.empty((nc, 12)), Xw_d=np.empty((npt, 3)))
         R = _lib.BaResult(ptr(out["Tcw"]), ptr(out["Xw"]), ptr(out["edge_outlier"]), ptr(out["Tcw_d"]),
                           ptr(out["Xw_d"]))
         if isinstance(stop, np.ndarray):
@@ -638,8 +639,8 @@ class Optimizer:
             nc, npt, ne = len(a["Tcw"]), len(a["Xw"]), len(a["edge_point"])
             Ps[k] = _lib.BaProblem(nc, ptr(a["Tcw"]), ptr(a["fixed"]), ptr(a["intr"]), npt, ptr(a["Xw"]), ne,
                                    ptr(a["edge_point"]), ptr(a["edge_cam"]), ptr(a["obs"]), ptr(a["inv_sigma2"]))
-            out = dict(Tcw=np.zeros((nc, 12), np.float32), Xw=np.zeros((npt, 3), np.float32),
-                       edge_outlier=np.zeros(ne, np.uint8), Tcw_d=np.zeros((nc, 12)), Xw_d=np.zeros((npt, 3)))
+            out = dict(Tcw=np.empty((nc, 12), np.float32), Xw=np.empty((npt, 3), np.float32),
+                       edge_outlier=np.empty(ne, np.uint8), Tcw_d=np.empty((nc, 12)), Xw_d=np.empty((npt, 3)))
             Rs[k] = _lib.BaResult(ptr(out["Tcw"]), ptr(out["Xw"]), ptr(out["edge_outlier"]), ptr(out["Tcw_d"]),
                                   ptr(out["Xw_d"]))
             keep.append(a)
