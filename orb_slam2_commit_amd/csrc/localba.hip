@@ -9,7 +9,8 @@
 //                    Hpl_e = B^T W A, point (Hll,bl) and pose (Hpp,bp) terms
 //   k_ba_point_sum   Hll, bl per point (fixed edge order)
 //   k_ba_cam_sum     Hpp, bp per pose: chunk partials (pose lists split over blocks)
-//   k_ba_cam_fin     chunk partials -> Hpp, bp, max |Hpp_jj| (chunk order)
+//   k_ba_cam_fin     chunk partials -> Hpp, bp, max |Hpp_jj| (chunk order; batched driver --
+//                    the single-problem entry does it inside k_ba_lm_start)
 //   per trial:
 //   k_ba_point_schur D = Hll + lambda I, Dinv (cofactor inverse), BD_e = Hpl_e Dinv, cf_e = Hpl_e Dinv bl
 //   k_ba_pairs       chunk partials of sum_points BD_e1 Hpl_e2^T per Hschur block
@@ -285,6 +286,7 @@ struct BaDev {
   int* pblk;       // nbf+1: first active point of each fused point-side block (k_ba_lin_schur), or null
   int nbf;         // fused point-side blocks (0: the unfused kernels run)
   int fused;       // device-LM launches of a problem with nbf > 0: k_ba_lin_schur does the point side
+                   // (3: a phase's entry linearisation -- k_ba_linearize + k_ba_point_sum's outputs only)
                    // of iteration-start trials (k_ba_linearize / point_sum / point_schur skip them)
   int ldlt_pan;    // the reduced system goes through k_ba_ldlt_pan (else the column-step kernel): per
                    // problem, so a batch with both kinds launches both and each skips the other's
@@ -792,7 +794,6 @@ __device__ __forceinline__ void k_ba_cam_fin_body(const BaDev& D) {
     D.dmax_c[ci] = m;
   }
 }
-__global__ __launch_bounds__(64) void k_ba_cam_fin(BaDev D) { k_ba_cam_fin_body(D); }
 __global__ __launch_bounds__(64) void k_ba_cam_fin_many(const BaDev* __restrict__ Ds) {
   k_ba_cam_fin_body(Ds[blockIdx.z]);
 }
@@ -937,6 +938,7 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
     for (int j = 0; j < 9; j++) D.Hll[9 * i + j] = h[j];
     for (int j = 0; j < 3; j++) D.bl[3 * i + j] = h[9 + j];
     D.dmax_p[i] = fmax(fmax(fabs(h[0]), fabs(h[4])), fabs(h[8]));
+    if (D.fused == 3) return;  // (a phase's entry linearisation: no lambda yet, no Schur terms)
     double Dm[9];
     for (int j = 0; j < 9; j++) Dm[j] = h[j];
     Dm[0] += lambda;
@@ -950,6 +952,7 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
     for (int j = 0; j < 9; j++) sdi[12 * t + j] = Di[j];
   }
   }  // lin
+  if (D.fused == 3) return;  // block-uniform
   __syncthreads();
   if (act) {
     const double* Di = sdi + 12 * (D.pos_pt[k] - p0);
@@ -972,13 +975,14 @@ __global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur_many(const BaDev* __re
 constexpr size_t kFuseSmem = (size_t)kFuseNT * (12 + 21 + 18 + 12) * sizeof(double);
 
 // Per phase: pblk[b] = the first active point whose first position is >= b * kFuseStride (block b
-// then ends where block b+1's first point starts); pblk[nbf] = npa.
-__global__ __launch_bounds__(LBS) void k_ba_pblk(BaDev D) {
-  const int p = blockIdx.x * LBS + threadIdx.x;
+// then ends where block b+1's first point starts); pblk[nbf] = npa.  One thread per point, run by the
+// pair-table launch's extra blocks.
+__device__ __forceinline__ void pblk_body(const BaDev& D, int b) {
+  const int p = b * LBS + threadIdx.x;
   if (p > D.npa) return;
   const int cur = p < D.npa ? D.pt_off[p] / kFuseStride : D.nbf;
   const int prev = p == 0 ? -1 : D.pt_off[p - 1] / kFuseStride;
-  for (int b = prev + 1; b <= min(cur, D.nbf); b++) D.pblk[b] = p;
+  for (int q = prev + 1; q <= min(cur, D.nbf); q++) D.pblk[q] = p;
 }
 __global__ __launch_bounds__(LBS) void k_ba_point_schur_many(const BaDev* __restrict__ Ds, double lambda) {
   k_ba_point_schur_body(Ds[blockIdx.z], lambda);
@@ -1007,8 +1011,13 @@ __device__ inline int tri_decode(int b, int n, int& c1) {
 // block (c1, c2) and each position k1 of pose c1 (ascending, i.e. point
 // order), the first position k2 of the same point on pose c2, flagged when
 // the point has more than one.
+// grid (nblk [+ the pblk blocks], chunks): blocks past nblk fill pblk (chunk 0 only)
 __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
   const int2 bxy = xcd_block2();  // (as k_ba_pairs: one pose chunk's blocks on one XCD)
+  if (bxy.x >= D.nblk) {
+    if (bxy.y == 0) pblk_body(D, bxy.x - D.nblk);
+    return;
+  }
   int c1;
   const int c2 = tri_decode(bxy.x, D.nposes, c1);
   int lo, hi;
@@ -2267,13 +2276,37 @@ __device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations
   L->done = iterations <= 0 ? 1 : 0;
   L->ticket = 0;
 }
-// Lambda init (the max of |H_jj| over dmax_p -> scal[3], a 1024-wide tree) and the LM state init in one
-// launch (single-problem device LM); the batched driver runs k_ba_dmax_many + k_ba_lm_init_many
+// A phase's entry after k_ba_cam_sum (single-problem device LM): k_ba_cam_fin, the lambda init (the
+// max of |H_jj| over points and poses -> scal[3], a 1024-wide tree: max is order-free) and the LM
+// state init in one launch; the batched driver runs k_ba_cam_fin_many, k_ba_dmax_many and
+// k_ba_lm_init_many
 __global__ __launch_bounds__(1024) void k_ba_lm_start(BaDev D, int iterations) {
   __shared__ double sm[1024];
-  const int n = D.npa + D.nposes;
   double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += 1024) acc = fmax(acc, D.dmax_p[i]);
+  for (int i = threadIdx.x; i < D.npa; i += 1024) acc = fmax(acc, D.dmax_p[i]);
+  // k_ba_cam_fin's finalisation of the entry's pose sums: item (pose, j) sums the chunk partials of
+  // its upper-triangle / rhs entry in chunk order (Hpp both triangles, bp, and the pose's |H_jj| max,
+  // which also joins the lambda-init maximum here)
+  const int S = D.gsplit;
+  auto csum = [&](int ci, int q) {
+    double t = 0;
+    for (int c = 0; c < S; c++) t += D.gpart[((size_t)ci * S + c) * 27 + q];
+    return t;
+  };
+  for (int it = threadIdx.x; it < D.nposes * 43; it += 1024) {
+    const int ci = it / 43, j = it - ci * 43;
+    if (j < 36) {
+      const int r = min(j / 6, j % 6), c = max(j / 6, j % 6);
+      D.Hpp[36 * ci + j] = csum(ci, r * 6 - (r * (r - 1)) / 2 + (c - r));
+    } else if (j < 42) {
+      D.bp[6 * ci + (j - 36)] = csum(ci, 21 + (j - 36));
+    } else {
+      double m = 0;
+      for (int r = 0; r < 6; r++) m = fmax(m, fabs(csum(ci, r * 6 - (r * (r - 1)) / 2)));
+      D.dmax_c[ci] = m;
+      acc = fmax(acc, m);
+    }
+  }
   sm[threadIdx.x] = acc;
   __syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
@@ -2902,20 +2935,10 @@ struct LocalBA {
   }
   // computeActiveErrors is not repeated: the errors/chi stored by the trial
   // (recompute, slot 1) are the ones at the state being linearised
-  void linearize(const BaDev& Dl, hipStream_t st) {
-    lin_points(Dl, st);
-    cam_sums(Dl, st);
-  }
   static void lin_points(const BaDev& Dl, hipStream_t st) {
     const int ga = std::max((Dl.na + LBS - 1) / LBS, 1);
     if (Dl.na > 0) hipLaunchKernelGGL(k_ba_linearize, dim3(ga), dim3(LBS), 0, st, Dl);
     if (Dl.npa > 0) hipLaunchKernelGGL(k_ba_point_sum, dim3((Dl.npa + LBS - 1) / LBS), dim3(LBS), 0, st, Dl);
-  }
-  static void cam_sums(const BaDev& Dl, hipStream_t st) {
-    if (Dl.nposes > 0) {
-      hipLaunchKernelGGL(k_ba_cam_sum, dim3(Dl.nposes, Dl.gsplit), dim3(kGB), 0, st, Dl);
-      hipLaunchKernelGGL(k_ba_cam_fin, dim3(Dl.nposes), dim3(64), 0, st, Dl);
-    }
   }
   // fused point side (k_ba_lin_schur): edges grouped by point with at most kFuseMaxDeg per point
   bool fuse_ok = false;
@@ -3142,17 +3165,19 @@ struct LocalBA {
     }
     BA_CHECK(c.ptab.alloc(nslots));
     D.ptab = c.ptab.p;
-    if (D.nblk > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk, gsplit), dim3(kPB), 0, st, D);
     D.nbf = 0;
     D.pblk = nullptr;
     D.fused = 0;  // set on the device-LM copies only
     D.camfold = 0;
+    int npb = 0;  // the pblk blocks, run inside the pair-table launch
     if (fuse_ok && na > 0) {
       D.nbf = (na - 1) / kFuseStride + 1;
       BA_CHECK(pblk.alloc((size_t)D.nbf + 1));
       D.pblk = pblk.p;
-      hipLaunchKernelGGL(k_ba_pblk, dim3(npa / LBS + 1), dim3(LBS), 0, st, D);
+      npb = npa / LBS + 1;
     }
+    static_assert(kPB == LBS, "pblk blocks inside k_ba_pair_table");
+    if (D.nblk + npb > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk + npb, gsplit), dim3(kPB), 0, st, D);
     BA_CHECK(hipGetLastError());
     D.ptc = c.ptc.p;
     D.cmc = c.cmc.p;
@@ -3238,19 +3263,26 @@ struct LocalBA {
     Dg.camfold = 1;
     int it = 0;
     if (!(stop())) {  // the loop head's first poll (i = 0)
+      const bool fused = Dg.nbf > 0;
+      if (fused) BA_CHECK(set_smem_attr((const void*)k_ba_lin_schur, kFuseSmem));
+      // entry: errors, linearisation (point side through k_ba_lin_schur's entry mode when the
+      // edges are point-grouped), pose sums, then cam_fin + lambda init + LM init in one launch
       hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, D0, 1, 0);
-      linearize(D0, st);
+      if (fused) {
+        BaDev De = D0;
+        De.fused = 3;
+        hipLaunchKernelGGL(k_ba_lin_schur, dim3(De.nbf), dim3(kFuseNT), kFuseSmem, st, De);
+      } else {
+        lin_points(D0, st);
+      }
+      if (D0.nposes > 0) hipLaunchKernelGGL(k_ba_cam_sum, dim3(D0.nposes, D0.gsplit), dim3(kGB), 0, st, D0);
       hipLaunchKernelGGL(k_ba_lm_start, dim3(1), dim3(1024), 0, st, Dg, iterations);
       BA_CHECK(hipGetLastError());
-      const bool fused = Dg.nbf > 0;
-      if (fused)
-        BA_CHECK(set_smem_attr((const void*)k_ba_lin_schur, kFuseSmem));
       const bool psfold = Dg.fused == 2;
       auto trial = [&](bool lin) {
         // linearisation gated on the device: only at the start of a new iteration
         if (fused && (lin || psfold)) hipLaunchKernelGGL(k_ba_lin_schur, dim3(Dg.nbf), dim3(kFuseNT), kFuseSmem, st, Dg);
         if (lin && !fused) lin_points(Dg, st);
-        if (lin && !Dg.camfold) cam_sums(Dg, st);
         // (returns at once after k_ba_lin_schur: the point side of an iteration-start trial is done)
         if (!psfold) hipLaunchKernelGGL(k_ba_point_schur, dim3(ga), dim3(LBS), 0, st, Dg, 0.0);
         if (Dg.nposes > 0) {
