@@ -158,7 +158,7 @@ __device__ __forceinline__ void window_to_lds(const uint8_t* base, size_t stride
 //      (S[sx0]*a0 + S[sx1]*a1) >> 4 as int16 (shared by the <= 2 output rows that
 //      read each source row);
 //   3. the vertical pass for 4 output columns per item:
-//      ((b0*h0)>>16 + (b1*h1)>>16 + 2) >> 2 with v_mul_hi_u32(b<<16, h), packed
+//      ((b0*h0)>>16 + (b1*h1)>>16 + 2) >> 2 with v_mul_hi_u32_u24(b<<8, h<<8), packed
 //      into one dword store.
 __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, const ResizeX* __restrict__ xt,
                                                const ResizeY* __restrict__ yt, BatchPtrs B, int l) {
@@ -242,15 +242,24 @@ __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, c
     const int i = it / (kRzTW / 4), g = it - i * (kRzTW / 4);
     if (i >= ny || 4 * g >= nx) continue;
     const ResizeY y = yv[k];
-    const uint32_t B0 = (uint32_t)y.b0 << 16, B1 = (uint32_t)y.b1 << 16;
+    // (b * h) >> 16 as v_mul_hi_u32_u24(b << 8, h << 8): both factors stay below 2^24 (b <= 2048,
+    // 0 <= h <= 32640), so the full-rate 24-bit high multiply gives the same bits as the
+    // quarter-rate v_mul_hi_u32(b << 16, h); h << 8 comes straight out of its packed pair (v_perm)
+    const uint32_t B0 = (uint32_t)y.b0 << 8, B1 = (uint32_t)y.b1 << 8;
     const uint2 p0 = *(const uint2*)&hb[(y.sy0 - ry0) * kRzTW + 4 * g];
     const uint2 p1 = *(const uint2*)&hb[(y.sy1 - ry0) * kRzTW + 4 * g];
-    const uint32_t h0[4] = {p0.x & 0xFFFF, p0.x >> 16, p0.y & 0xFFFF, p0.y >> 16};
-    const uint32_t h1[4] = {p1.x & 0xFFFF, p1.x >> 16, p1.y & 0xFFFF, p1.y >> 16};
+    constexpr uint32_t kLo = 0x0C01000Cu, kHi = 0x0C03020Cu;  // bytes 0-1 / 2-3 -> bits 8..23
+    const uint32_t h0[4] = {__builtin_amdgcn_perm(0u, p0.x, kLo), __builtin_amdgcn_perm(0u, p0.x, kHi),
+                            __builtin_amdgcn_perm(0u, p0.y, kLo), __builtin_amdgcn_perm(0u, p0.y, kHi)};
+    const uint32_t h1[4] = {__builtin_amdgcn_perm(0u, p1.x, kLo), __builtin_amdgcn_perm(0u, p1.x, kHi),
+                            __builtin_amdgcn_perm(0u, p1.y, kLo), __builtin_amdgcn_perm(0u, p1.y, kHi)};
+    auto mulhi24 = [](uint32_t x, uint32_t z) {
+      return (uint32_t)(((uint64_t)(x & 0xFFFFFFu) * (z & 0xFFFFFFu)) >> 32);
+    };
     uint32_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const uint32_t v = (__umulhi(B0, h0[j]) + __umulhi(B1, h1[j]) + 2) >> 2;
+      const uint32_t v = (mulhi24(B0, h0[j]) + mulhi24(B1, h1[j]) + 2) >> 2;
       packed |= v << (8 * j);
     }
     const int o = (oy0 + i) * L.w + ox0 + 4 * g;
