@@ -2503,7 +2503,12 @@ __device__ inline uint64_t ba_match(int key, int nbits) {
 //  k_ba_struct_fill   per tile: act/pos_pt/pcam/pt_off/pt_id, and cam_pos as a
 //                     stable per-wave multisplit of the tile's positions by
 //                     camera (bitwise match, no atomics), ascending in a pose.
-constexpr int kTileT = 256, kStructV = 8, kTileE = kTileT * kStructV;  // kTileE < 2^16: packed scans
+#ifndef ORBX_STRUCT_V
+#define ORBX_STRUCT_V 4
+#endif
+// 4 edges per thread (1,024-edge tiles): at config 4 the three launches take 23.7 µs against 29.5 with
+// 8 (k_ba_struct_fill 14.5 -> 9.1, k_ba_struct_scan 8.7 -> 9.8 over twice the tiles; profiles/r05)
+constexpr int kTileT = 256, kStructV = ORBX_STRUCT_V, kTileE = kTileT * kStructV;  // kTileE < 2^16: packed scans
 constexpr int kStructNT = 1024, kStructMaxNc = 512, kStructMaxTiles = kStructNT;
 
 __device__ inline void ba_tile_load(const BaDev& D, const uint8_t* __restrict__ flag, int lvl, int e0, bool* a,
