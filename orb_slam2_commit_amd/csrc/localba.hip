@@ -2281,40 +2281,53 @@ __device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations
 // state init in one launch; the batched driver runs k_ba_cam_fin_many, k_ba_dmax_many and
 // k_ba_lm_init_many
 __global__ __launch_bounds__(1024) void k_ba_lm_start(BaDev D, int iterations) {
-  __shared__ double sm[1024];
+  __shared__ double wmax[16];
   double acc = 0.0;
   for (int i = threadIdx.x; i < D.npa; i += 1024) acc = fmax(acc, D.dmax_p[i]);
   // k_ba_cam_fin's finalisation of the entry's pose sums: item (pose, j) sums the chunk partials of
-  // its upper-triangle / rhs entry in chunk order (Hpp both triangles, bp, and the pose's |H_jj| max,
-  // which also joins the lambda-init maximum here)
+  // its upper-triangle / rhs entry in chunk order (Hpp both triangles, bp); the diagonal entries'
+  // |H_jj| join the lambda-init maximum here, and after the barrier each pose's thread takes its own
+  // maximum from the six diagonal entries this block just wrote
   const int S = D.gsplit;
-  auto csum = [&](int ci, int q) {
+  auto csum = [&](int ci, int q) {  // chunk order; loads in groups of 8 (clamped) before their adds
     double t = 0;
-    for (int c = 0; c < S; c++) t += D.gpart[((size_t)ci * S + c) * 27 + q];
+    for (int c0 = 0; c0 < S; c0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) v[e] = D.gpart[((size_t)ci * S + min(c0 + e, S - 1)) * 27 + q];
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if (c0 + e < S) t += v[e];
+    }
     return t;
   };
-  for (int it = threadIdx.x; it < D.nposes * 43; it += 1024) {
-    const int ci = it / 43, j = it - ci * 43;
+  for (int it = threadIdx.x; it < D.nposes * 42; it += 1024) {
+    const int ci = it / 42, j = it - ci * 42;
     if (j < 36) {
       const int r = min(j / 6, j % 6), c = max(j / 6, j % 6);
-      D.Hpp[36 * ci + j] = csum(ci, r * 6 - (r * (r - 1)) / 2 + (c - r));
-    } else if (j < 42) {
-      D.bp[6 * ci + (j - 36)] = csum(ci, 21 + (j - 36));
+      const double v = csum(ci, r * 6 - (r * (r - 1)) / 2 + (c - r));
+      D.Hpp[36 * ci + j] = v;
+      if (j / 6 == j % 6) acc = fmax(acc, fabs(v));
     } else {
-      double m = 0;
-      for (int r = 0; r < 6; r++) m = fmax(m, fabs(csum(ci, r * 6 - (r * (r - 1)) / 2)));
-      D.dmax_c[ci] = m;
-      acc = fmax(acc, m);
+      D.bp[6 * ci + (j - 36)] = csum(ci, 21 + (j - 36));
     }
   }
-  sm[threadIdx.x] = acc;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + o]);
-    __syncthreads();
+  // the maximum over the block: wave maxima by lane exchanges, then the 16 of them (max is order-free)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc = fmax(acc, __shfl_xor(acc, o, 64));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = acc;
+  __syncthreads();  // (also orders the Hpp stores above before the per-pose reads below)
+  for (int ci = threadIdx.x; ci < D.nposes; ci += 1024) {
+    double m = 0;
+    for (int r = 0; r < 6; r++) m = fmax(m, fabs(D.Hpp[36 * ci + 7 * r]));
+    D.dmax_c[ci] = m;
   }
-  if (threadIdx.x == 0) D.scal[3] = sm[0];  // (read back below by the same thread)
   if (threadIdx.x >= 64) return;
+  if (threadIdx.x == 0) {
+    double m = wmax[0];
+    for (int w = 1; w < 16; w++) m = fmax(m, wmax[w]);
+    D.scal[3] = m;  // (read back below by the same thread)
+  }
   k_ba_lm_init_body(D, iterations);
 }
 __global__ __launch_bounds__(64) void k_ba_lm_init_many(const BaDev* __restrict__ Ds, int iterations) {
@@ -3129,7 +3142,11 @@ struct LocalBA {
 
   // Sizes known: scratch allocations, readback block, Schur pair table.
   orbx_status finish_structure(int na, int npa, int nposes, int maxc, int nslots, hipStream_t st) {
-    const int gsplit = std::min(std::max((maxc + 2 * kGB - 1) / (2 * kGB), 1), 64);  // ~2 positions per thread
+#ifndef ORBX_GSPLIT_PPT
+#define ORBX_GSPLIT_PPT 2
+#endif
+    constexpr int kPpt = ORBX_GSPLIT_PPT;  // ~positions per thread of a pose chunk
+    const int gsplit = std::min(std::max((maxc + kPpt * kGB - 1) / (kPpt * kGB), 1), 64);
     const size_t N = 6 * (size_t)nposes;
     BA_CHECK(c.Hpl.alloc(18 * (size_t)na));
     BA_CHECK(c.ptc.alloc(12 * (size_t)na));
