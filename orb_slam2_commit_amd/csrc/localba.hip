@@ -1027,11 +1027,17 @@ __global__ __launch_bounds__(kPB) void k_ba_pair_table(BaDev D) {
     const int i = D.pos_pt[D.cam_pos[t]];
     const int s = D.pt_off[i], e = D.pt_off[i + 1];
     int first = -1, more = 0;
-    for (int k2 = s; k2 < e; k2++)
-      if (D.pcam[k2] == c2) {
-        more |= first >= 0;
-        first = first < 0 ? k2 : first;
-      }
+    for (int k0 = s; k0 < e; k0 += 8) {  // the point's pose indices, eight loads in flight (clamped)
+      int pc[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) pc[u] = D.pcam[min(k0 + u, e - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (k0 + u < e && pc[u] == c2) {
+          more |= first >= 0;
+          first = first < 0 ? k0 + u : first;
+        }
+    }
     tab[t] = first < 0 ? -1 : (first | (more << 30));
   }
 }
