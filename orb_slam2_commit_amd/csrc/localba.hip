@@ -2968,7 +2968,7 @@ struct LocalBA {
   bool fuse_ok = false;
   DBuf<int> pblk;
   // host scratch, reused across calls
-  std::vector<int> act, pos_pt, chidx, pose_cam, pt_off, pt_id, cam_off, cam_pos, cnt, pcam, ccnt, boff;
+  std::vector<int> act, pos_pt, chidx, pose_cam, pt_off, pt_id, cam_off, cam_pos, cnt, pcam, ccnt, ccnt4, boff;
 
   // Active set of a phase: SparseOptimizer::initializeOptimization(level) +
   // buildIndexMapping; point-major positions, pose groups (positions
@@ -3429,21 +3429,41 @@ orbx_status ba_intake(LocalBA& L, const orbx_ba_problem* pb, hipStream_t st) {
   D.nc = nc;
   D.np = np;
   D.ne = ne;
-  bool grouped = true;  // edges ordered by point (the reference adds them per MapPoint)
-  L.ccnt.assign(nc, 0);
-  int npts = 0, run = 0, max_run = 0;
-  for (int e = 0; e < ne; e++) {
-    if (pb->edge_point[e] < 0 || pb->edge_point[e] >= np || pb->edge_cam[e] < 0 || pb->edge_cam[e] >= nc)
-      return ORBX_ERR_ARG;
-    grouped &= e == 0 || pb->edge_point[e] >= pb->edge_point[e - 1];
-    const bool new_pt = e == 0 || pb->edge_point[e] != pb->edge_point[e - 1];
-    npts += new_pt;
-    run = new_pt ? 1 : run + 1;
-    max_run = std::max(max_run, run);
-    L.ccnt[pb->edge_cam[e]]++;
+  // Index checks, point order and point count in one branch-free (vectorisable) pass; the camera
+  // histogram in four interleaved counter sets (a run of one camera's edges does not serialise on one
+  // counter).  The host pass sits on the call's critical path: the device waits for its upload.
+  const int* ep = pb->edge_point;
+  const int* ec = pb->edge_cam;
+  int pmin = ne > 0 ? ep[0] : 0, pmax = pmin, cmin = ne > 0 ? ec[0] : 0, cmax = cmin, ord = 1, npts = ne > 0;
+  for (int e = 1; e < ne; e++) {
+    const int p = ep[e], q = ep[e - 1], c = ec[e];
+    pmin = std::min(pmin, p);
+    pmax = std::max(pmax, p);
+    cmin = std::min(cmin, c);
+    cmax = std::max(cmax, c);
+    ord &= p >= q;
+    npts += p != q;
   }
+  if (ne > 0 && (pmin < 0 || pmax >= np || cmin < 0 || cmax >= nc)) return ORBX_ERR_ARG;
+  const bool grouped = ord != 0;  // edges ordered by point (the reference adds them per MapPoint)
+  // grouped: some point has more than kFuseMaxDeg positions <=> ep[e] == ep[e - kFuseMaxDeg] somewhere
+  int long_run = 0;
+  if (grouped)
+    for (int e = kFuseMaxDeg; e < ne; e++) long_run |= ep[e] == ep[e - kFuseMaxDeg];
+  L.ccnt.assign(nc, 0);
+  L.ccnt4.assign(4 * (size_t)nc, 0);
+  int* h = L.ccnt4.data();
+  int e4 = 0;
+  for (; e4 + 4 <= ne; e4 += 4) {
+    h[ec[e4]]++;
+    h[nc + ec[e4 + 1]]++;
+    h[2 * nc + ec[e4 + 2]]++;
+    h[3 * nc + ec[e4 + 3]]++;
+  }
+  for (; e4 < ne; e4++) h[ec[e4]]++;
+  for (int i = 0; i < nc; i++) L.ccnt[i] = h[i] + h[nc + i] + h[2 * nc + i] + h[3 * nc + i];
   // the fused point side needs every point's positions inside one block (else the three kernels)
-  L.fuse_ok = grouped && max_run <= kFuseMaxDeg;
+  L.fuse_ok = grouped && !long_run;
   // the structure on the device when the edges arrive grouped by point (else the host build)
   L.dev_struct = grouped && nc <= kStructMaxNc && (ne + kTileE - 1) / kTileE <= kStructMaxTiles;
   if (L.dev_struct) {  // phase-1 sizes: the launches need no readback
