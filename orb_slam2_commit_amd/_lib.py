@@ -277,8 +277,13 @@ def ptr(a):
     """Host numpy array or torch tensor (host or device) -> void*."""
     if a is None:
         return None
-    if isinstance(a, np.ndarray):  # (the array interface's address: half the cost of ctypes.data_as)
-        return C.c_void_p(a.__array_interface__["data"][0])
+    if isinstance(a, np.ndarray):
+        # a writable buffer's address through ctypes.from_buffer (~1 us; ctypes.data_as ~4 us), else
+        # (read-only, empty, non-contiguous) the array interface's data pointer
+        try:
+            return C.c_void_p(C.addressof(C.c_char.from_buffer(a)))
+        except (TypeError, ValueError, BufferError):
+            return C.c_void_p(a.__array_interface__["data"][0])
     if hasattr(a, "data_ptr"):
         return C.c_void_p(a.data_ptr())
     raise TypeError(type(a))
