@@ -858,6 +858,26 @@ __global__ __launch_bounds__(LBS) void k_ba_point_schur(BaDev D, double lambda) 
 // order), then D = Hll + lambda I, D^-1 (once per point) and B D^-1, B D^-1 b_l per position from
 // the staged Hpl -- bit-identical to the three kernels, without their global round trips.
 constexpr int kFuseNT = 128, kFuseStride = 96, kFuseMaxDeg = 32;
+// n (even) doubles between 16-B aligned arrays, one 16-B pair per thread and step (half the
+// iterations of 8-B copies: these LDS <-> global loops are a block's tail)
+typedef double dpair_t __attribute__((ext_vector_type(2)));
+template <int NT>
+__device__ __forceinline__ void copy_pairs(double* __restrict__ dst, const double* __restrict__ src, int n, int t) {
+  dpair_t* d = reinterpret_cast<dpair_t*>(dst);
+  const dpair_t* q = reinterpret_cast<const dpair_t*>(src);
+  for (int j = t; j < n / 2; j += NT) d[j] = q[j];
+}
+// Phase probe (build with -DORBX_LS_PROBE only; tools/ls_probe.py): s_memtime of thread 0 of every
+// k_ba_lin_schur block at six points of the last launch, 8 words per block
+#ifdef ORBX_LS_PROBE
+__device__ unsigned long long g_ls_probe[1024 * 8];
+#define LS_TS(k)                                                                                  \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_ls_probe[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define LS_TS(k)
+#endif
 static_assert(kFuseStride - 1 + kFuseMaxDeg <= kFuseNT, "a fused block's positions fit its threads");
 __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   if (!D.fused || lm_skip(D) || (int)blockIdx.x >= D.nbf) return;
@@ -879,8 +899,9 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   const double lambda = lm_lambda(D, 0.0);
   const bool act = t < nk;
   const int k = k0 + (act ? t : 0);
+  LS_TS(0);
   if (!lin) {
-    for (int j = t; j < nk * 18; j += NT) shpl[j] = D.Hpl[18 * (size_t)k0 + j];
+    copy_pairs<NT>(shpl, D.Hpl + 18 * (size_t)k0, nk * 18, t);  // (18 k0 doubles: 16-B aligned)
     if (t < npt) {
       const int i = p0 + t;
       double Dm[9];
@@ -907,6 +928,7 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
       lin_cross_terms<2>(L.T, L.A, L.Bm, shpl + 18 * t);
     }
   }
+  LS_TS(1);
   // pose terms out through LDS in two parts of 14 and 13 (coalesced 8-B stores, as k_ba_linearize)
   double cm[kCmc];
   if (L.st) lin_pose_terms<3>(L.T, L.Bm, cm); else lin_pose_terms<2>(L.T, L.Bm, cm);
@@ -926,7 +948,8 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
     }
     __syncthreads();
   }
-  for (int j = t; j < nk * 18; j += NT) D.Hpl[18 * (size_t)k0 + j] = shpl[j];
+  LS_TS(2);
+  copy_pairs<NT>(D.Hpl + 18 * (size_t)k0, shpl, nk * 18, t);
   // point sums (k_ba_point_sum's order), D^-1 and D^-1 b_l once per point
   if (t < npt) {
     const int i = p0 + t;
@@ -953,7 +976,9 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   }
   }  // lin
   if (D.fused == 3) return;  // block-uniform
+  LS_TS(3);
   __syncthreads();
+  LS_TS(4);
   if (act) {
     const double* Di = sdi + 12 * (D.pos_pt[k] - p0);
     const double* db = Di + 9;
@@ -965,8 +990,9 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
     }
   }
   __syncthreads();
-  for (int j = t; j < nk * 18; j += NT) D.BD[18 * (size_t)k0 + j] = sout[j];
-  for (int j = t; j < nk * 6; j += NT) D.cf[6 * (size_t)k0 + j] = sout[18 * NT + j];
+  copy_pairs<NT>(D.BD + 18 * (size_t)k0, sout, nk * 18, t);
+  copy_pairs<NT>(D.cf + 6 * (size_t)k0, sout + 18 * NT, nk * 6, t);
+  LS_TS(5);
 }
 __global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur(BaDev D) { k_ba_lin_schur_body(D); }
 __global__ __launch_bounds__(kFuseNT) void k_ba_lin_schur_many(const BaDev* __restrict__ Ds) {
@@ -4073,6 +4099,11 @@ orbx_status orbx_local_ba(const orbx_ba_problem* p, orbx_ba_result* r, const vol
 
 // Debug/benchmark probe (include/orbx_debug.h): solve S x = b (N = 6 * nposes)
 // with the LocalBA LDLT kernel; ms = average kernel time over reps launches.
+#ifdef ORBX_LS_PROBE
+extern "C" int orbx_debug_ls_probe(unsigned long long* out) {  // 1024 x 8 words (probe build only)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_ls_probe), sizeof(unsigned long long) * 1024 * 8) == hipSuccess ? 0 : -3;
+}
+#endif
 extern "C" int orbx_debug_ldlt(const double* S, const double* b, int N, double* x, int reps, float* ms) {
   return orbx_debug_ldlt_ex(S, b, N, x, reps, ms, ORBX_BA_LDLT_AUTO, nullptr);
 }
