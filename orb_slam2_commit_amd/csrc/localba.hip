@@ -888,10 +888,11 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   constexpr int NT = kFuseNT;
   extern __shared__ __attribute__((aligned(16))) double fsm[];
   double* sptc = fsm;                // NT x 12 point terms; then with sbuf: BD (18) | cf (6) staging
-  double* sbuf = sptc + NT * 12;     // NT x 21: cmc staging (two halves)
-  double* shpl = sbuf + NT * 21;     // NT x 18
-  double* sdi = shpl + NT * 18;      // NT x 12: per point D^-1 (9) and D^-1 b_l (3)
+  double* sbuf = sptc + NT * 12;     // NT x 21; with sdi (before the point sums): the 27 pose terms
+  double* sdi = sbuf + NT * 21;      // NT x 12: per point D^-1 (9) and D^-1 b_l (3)
+  double* shpl = sdi + NT * 12;      // NT x 18
   double* sout = sptc;               // NT x 24 over sptc + sbuf once the point sums are done
+  static_assert(12 + 1 + kCmc <= 12 + 21 + 12, "the pose-term staging fits sbuf + sdi");
   const int b = blockIdx.x, t = threadIdx.x;
   const int p0 = D.pblk[b], p1 = D.pblk[b + 1];
   const int k0 = D.pt_off[p0], nk = D.pt_off[p1] - k0, npt = p1 - p0;
@@ -929,24 +930,24 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
     }
   }
   LS_TS(1);
-  // pose terms out through LDS in two parts of 14 and 13 (coalesced 8-B stores, as k_ba_linearize)
+  // the 27 pose terms of every position out through LDS in one pass (sbuf + sdi, free until the
+  // point sums) and 16-B pair stores; the staging starts at the global block's parity (27 k0 may be
+  // odd), so the LDS and the global pairs are aligned alike
   double cm[kCmc];
   if (L.st) lin_pose_terms<3>(L.T, L.Bm, cm); else lin_pose_terms<2>(L.T, L.Bm, cm);
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    constexpr int H0 = (kCmc + 1) / 2;
-    const int off = h ? H0 : 0, wd = h ? kCmc - H0 : H0;
+  {
+    const int par = (int)((kCmc * (size_t)k0) & 1), n = nk * kCmc;
+    double* scm = sbuf + par;
     if (act) {
 #pragma unroll
-      for (int j = 0; j < H0; j++)
-        if (j < wd) sbuf[wd * t + j] = cm[off + j];
+      for (int j = 0; j < kCmc; j++) scm[kCmc * t + j] = cm[j];
     }
     __syncthreads();
-    for (int j = t; j < nk * wd; j += NT) {
-      const int kk = j / wd, jj = j - wd * kk;
-      D.cmc[kCmc * ((size_t)k0 + kk) + off + jj] = sbuf[j];
-    }
-    __syncthreads();
+    double* dst = D.cmc + kCmc * (size_t)k0;
+    if (par && t == 0) dst[0] = scm[0];
+    copy_pairs<NT>(dst + par, scm + par, (n - par) & ~1, t);
+    if (((n - par) & 1) && t == NT - 1) dst[n - 1] = scm[n - 1];
+    __syncthreads();  // (sbuf / sdi are written again below)
   }
   LS_TS(2);
   copy_pairs<NT>(D.Hpl + 18 * (size_t)k0, shpl, nk * 18, t);
