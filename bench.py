@@ -16,9 +16,11 @@ Legs after the headline loop:
   localba   Optimizer::LocalBundleAdjustment (orbx_ba_run) on the config-4 problem
             per rank, --ba-calls times: LM iterations/s (whole job) + its roofline.
   config5   one synthetic sequence per rank: extract+match of --pipeline-steps
-            batches into the frame-record arena, LocalBA on the rank's map, then
-            ONE all-gather of the records + LocalBA summaries (RCCL over xGMI);
-            compute and all-gather timed separately.
+            batches of distinct frames into frame-record arenas, a keyframe every
+            --kf-every frames whose config-4-sized LocalBA runs on the rank's
+            LocalMapping thread (own stream) overlapping the extraction, then ONE
+            all-gather of the records + LocalBA summaries (RCCL over xGMI); the
+            sequence, its parts alone and the all-gather timed separately.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 
@@ -67,9 +69,13 @@ def parse():
     ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
     ap.add_argument("--ba-concurrent", type=int, default=8, help="LocalBA problems in flight per GPU for the "
                                                                   "throughput form (<=1: skip)")
-    ap.add_argument("--pipeline-steps", type=int, default=3, help="config-5 batches per rank (0: skip)")
+    ap.add_argument("--pipeline-steps", type=int, default=4, help="config-5 batches of distinct frames per rank (0: skip)")
+    ap.add_argument("--kf-every", type=int, default=128, help="config-5 keyframe cadence: one keyframe (and its "
+                                                                 "LocalBA) every K frames of a sequence (0: none)")
     ap.add_argument("--single-frames", type=int, default=200, help="frames of the single-frame drop-in leg (0: skip)")
     ap.add_argument("--track-steps", type=int, default=5, help="steps of the extract+match+track leg (0: skip)")
+    ap.add_argument("--c1-batch", type=int, default=256, help="config-1 (TUM mono) images per batched launch (0: skip leg)")
+    ap.add_argument("--c1-seconds", type=float, default=6.0, help="config-1 CPU reference sample length")
     ap.add_argument("--c3-steps", type=int, default=3, help="config-3 (EuRoC + PnP RANSAC) steps per rank (0: skip)")
     ap.add_argument("--c3-batch", type=int, default=128, help="config-3 frames (sequences) per step per GPU")
     ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r05_sq_counters.json"),
@@ -508,6 +514,93 @@ def single_frame_leg(args, pairs, cpu):
     return out
 
 
+# ------------------------------------------------------------------ config-1 leg
+TUM = dict(width=640, height=480, nfeatures=1000)
+
+
+def config1_leg(args, dev, oracle_mod, flags, cpus):
+    """BASELINE configs[0]: TUM fr1_xyz-shaped mono 640x480, 1,000 features -- the unit is Frame's
+    monocular constructor's ExtractORB, i.e. one ORBextractor::operator() (src/Frame.cc:186-205,
+    :273-279; mono extractor built at src/Tracking.cc:120,125).  Three numbers: the CPU reference path
+    (oracle operator() on one pinned core: the config's own "CPU reference ORBextractor" number), the
+    drop-in per-call latency through the shim's ORBextractor::operator() (host image in, host keypoints
+    and descriptors out, shim/build/frame_bench mono), and batched device extraction (--c1-batch TUM
+    images per orbx_extract_batch launch, inputs resident in HBM)."""
+    import torch
+    from orb_slam2_commit_amd import ORBextractor, synth
+    W, H, NF = TUM["width"], TUM["height"], TUM["nfeatures"]
+    imgs = [synth.mono_image(1000 * 9 + s, W, H) for s in range(8)]
+    out = dict(config=dict(workload="TUM fr1_xyz-shaped mono 640x480, 1000 features, ORBextractor::operator()",
+                           nlevels=8, scale_factor=1.2, fast_th=[20, 7]),
+               data="synthetic (8 seeded mono scenes; batched slots are distinct horizontal rolls of them)")
+    # CPU reference path: one pinned core
+    if oracle_mod is not None:
+        p = oracle_mod.params(NF, 1.2, 8, 20, 7)
+        old = os.sched_getaffinity(0) if hasattr(os, "sched_setaffinity") else None
+        try:
+            if old is not None and cpus:
+                os.sched_setaffinity(0, {cpus[0]})
+            oracle_mod.extract(p, imgs[0])
+            ts, n, t_start = [], 0, time.perf_counter()
+            while True:
+                t0 = time.perf_counter()
+                o = oracle_mod.extract(p, imgs[n % len(imgs)])
+                ts.append(time.perf_counter() - t0)
+                n += 1
+                if time.perf_counter() - t_start >= args.c1_seconds and n >= 5:
+                    break
+        finally:
+            if old is not None:
+                os.sched_setaffinity(0, old)
+        out["cpu_baseline"] = dict(value=round(n / sum(ts), 3), unit="frames/s", cores=1, kind="port",
+                                   median_ms=round(pct(ts, 50) * 1e3, 3), p90_ms=round(pct(ts, 90) * 1e3, 3),
+                                   keypoints_per_frame=len(o.keypoints),
+                                   sample="%d TUM-shaped mono images, oracle operator() built %s, 1 thread pinned"
+                                          % (n, flags))
+    # drop-in: the shim's ORBextractor::operator() per call (separate process)
+    exe = os.path.join(ROOT, "shim", "build", "frame_bench")
+    if os.path.exists(exe) and args.single_frames > 0:
+        fd, path = tempfile.mkstemp(prefix="orbx_mono_", suffix=".u8")
+        try:
+            with os.fdopen(fd, "wb") as f:
+                for im in imgs:
+                    f.write(np.ascontiguousarray(im).tobytes())
+            cmd = [exe, path, str(W), str(H), str(len(imgs)), str(args.single_frames), "20", str(NF), "0", "1", "mono"]
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            if r.returncode == 0:
+                out["drop_in"] = json.loads(r.stdout.strip().splitlines()[-1])
+                out["drop_in"].update(unit="ms per ORBextractor::operator() call (host image in, host keypoints + "
+                                           "descriptors out, mvImagePyramid refreshed)")
+            else:
+                out["drop_in"] = dict(error="frame_bench rc %d: %s" % (r.returncode, (r.stderr or r.stdout)[-300:]))
+        finally:
+            os.unlink(path)
+    # batched device extraction
+    B1 = args.c1_batch
+    ex = ORBextractor(NF, 1.2, 8, 20, 7, device=dev.index)
+    cap = ex.max_keypoints(W, H)
+    batch = torch.from_numpy(np.stack([np.roll(imgs[i % len(imgs)], 37 * (i // len(imgs)), axis=1)
+                                       for i in range(B1)])).to(dev)
+    kps = torch.empty((B1, cap, 28), dtype=torch.uint8, device=dev)
+    desc = torch.empty((B1, cap, 32), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(B1, dtype=torch.int32, device=dev)
+    st = torch.cuda.Stream(dev)
+    for _ in range(2):
+        ex.extract_batch_device(batch, kps, desc, counts, st)
+    torch.cuda.synchronize(dev)
+    steps = max(args.steps // 2, 3)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ex.extract_batch_device(batch, kps, desc, counts, st)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    ex.close()
+    out["batched"] = dict(frames_per_s=round(B1 * steps / el, 1), ms_per_step=round(el / steps * 1e3, 4),
+                          batch_images=B1, steps=steps, batches_in_flight=1,
+                          keypoints_per_image=round(float(counts.float().mean()), 1))
+    return out
+
+
 # ------------------------------------------------------------------ tracking front-end leg
 def track_leg(args, rank, world, dev, odist, ex, images, stream, pairs_host, oracle_mod=None, cpus=None):
     """Extract+match a batch, then Tracking::TrackReferenceKeyFrame's front end (src/Tracking.cc:910-969)
@@ -746,55 +839,86 @@ def config3_leg(args, rank, world, dev, odist, stream, oracle_mod=None, flags=No
 
 
 # ------------------------------------------------------------------ config-5 leg
-def config5_leg(args, rank, world, dev, odist, ex, images, stream):
-    """One sequence per rank: extract+match `pipeline_steps` batches into the frame-record arena, LocalBA
-    on the rank's map, then one all-gather of records + LocalBA summaries.  Compute and all-gather timed
-    separately (each bracketed by barrier + synchronize, max over ranks)."""
+def config5_leg(args, rank, world, dev, odist, exs, batch_images, pairs):
+    """One synthetic KITTI sequence per rank (configs[4]): the rank's Tracking loop steps through
+    --pipeline-steps batches of DISTINCT frames (frames 0 .. steps*B-1 of its sequence, in order,
+    --inflight batches in flight), and every --kf-every frames inserts a keyframe into the rank's
+    LocalMapping thread, which runs a config-4-sized LocalBundleAdjustment for it (its own solver
+    handle and HIP stream; the keyframe's local map = synth.localba_problem(seed 7 + 1000*rank + kf))
+    once the batch holding the keyframe's frame is extracted -- overlapping the next batches'
+    extraction as LocalMapping overlaps Tracking (src/LocalMapping.cc:51-101,
+    Examples/Stereo/stereo_kitti.cc:68-110).  Then ONE all-gather of the last batch's frame records and
+    every LocalBA summary.  Timed: the sequence with LocalMapping (barrier + synchronize around it,
+    max over ranks), the same batches' extraction alone, the LocalBA calls alone, and the all-gather."""
     import torch
-    from orb_slam2_commit_amd import Optimizer, pipeline, synth
+    from orb_slam2_commit_amd import pipeline, synth
     W, H, B = KITTI["width"], KITTI["height"], args.batch
-    sh = pipeline.SequenceShard(ex, B, W, H, KITTI["bf"], KITTI["bf"] / KITTI["fx"], dev)
-    P = synth.localba_problem(seed=7 + 1000 * rank)
-    opt = Optimizer(dev.index)
-    sh.step(images, stream)  # warm-up
-    rec = pipeline.ba_summary(opt.LocalBundleAdjustment(P), len(P["Tcw"]))
-    recs, _ = sh.gather(rec)  # warm-up of the collective
-    del recs
-    odist.barrier()
+    steps, K = args.pipeline_steps, args.kf_every
+    batches = [batch_images[k] if k < len(batch_images) else
+               torch.from_numpy(synth.stereo_batch(rank, B, pairs=pairs, first=k * B)).to(dev) for k in range(steps)]
+    n_kf_rank = (steps * B) // K if K > 0 else 0
+    n_kf = pipeline.agree_max(n_kf_rank)
+    probs = [synth.localba_problem(seed=7 + 1000 * rank + kf) for kf in range(n_kf_rank)]
+    sh = pipeline.SequenceShard(exs[0], B, W, H, KITTI["bf"], KITTI["bf"] / KITTI["fx"], dev, extractors=exs[1:])
+    lm = pipeline.LocalMapping(probs, dev)
+    # warm-up: the shard's arenas and the LocalMapping handle (one LocalBA on a keyframe problem)
+    sh.run_sequence(batches[:len(sh.exs)])
+    if probs:
+        lm.opt.LocalBundleAdjustment(probs[0])
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.pipeline_steps):
-        sh.step(images, stream)
-    rec = pipeline.ba_summary(opt.LocalBundleAdjustment(P), len(P["Tcw"]))
-    torch.cuda.synchronize(dev)
-    odist.barrier()
-    t_compute = odist.max_over_ranks(time.perf_counter() - t0, dev)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    recs, bas = sh.gather(rec)
-    torch.cuda.synchronize(dev)
-    odist.barrier()
-    t_gather = odist.max_over_ranks(time.perf_counter() - t1, dev)
-    opt.close()
-    # every rank checks that its own slot of the gathered records is its arena, byte for byte
-    own_ok = bool(torch.equal(recs[rank].to(sh.arena.device), sh.arena)) and bool(
-        np.array_equal(bas[rank], rec))
+
+    def timed(fn):
+        odist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize(dev)
+        odist.barrier()
+        return odist.max_over_ranks(time.perf_counter() - t0, dev), out
+
+    # the sequence: Tracking (this thread) + LocalMapping (its thread), frames numbered from 0
+    sh.frames_done = 0
+
+    def sequence():
+        n = sh.run_sequence(batches, lm, K)
+        return n, lm.finish()
+    t_seq, (n_ins, res) = timed(sequence)
+    # the same work apart: extraction alone (the same batches), LocalBA calls alone (one after another)
+    sh.frames_done = 0
+    t_ext, _ = timed(lambda: sh.run_sequence(batches))
+    t_ba, _ = timed(lambda: [lm.opt.LocalBundleAdjustment(P) for P in probs])
+    lm.opt.close()
+    rec = pipeline.ba_summaries([r for _, r in res], [len(P["Tcw"]) for P in probs], n_kf=n_kf)
+    t_gather, (recs, bas) = timed(lambda: sh.gather(rec))
+    own_ok = bool(torch.equal(recs[rank].to(sh.arena.device), sh.arena)) and bool(np.array_equal(bas[rank], rec))
     ok_all = odist.sum_over_ranks(1.0 if own_ok else 0.0, dev) == world
+    its = sum(sum(r["iterations"]) for _, r in res)
+    trials = sum(r["trials"] for _, r in res)
+    its_all = odist.sum_over_ranks(float(its), dev)
     nbytes = sh.layout.nbytes
-    frames = B * args.pipeline_steps * world
+    frames = B * steps * world
     backend = pipeline._backend() or "none (1 rank)"
-    return dict(sequences=world, frames_per_sequence=B * args.pipeline_steps, batch_frames=B,
-                extract_match_localba_s=round(t_compute, 5),
+    return dict(sequences=world, unique_frames_per_sequence=B * steps, batch_frames=B, batches_in_flight=len(sh.exs),
+                kf_every=K, keyframes_per_sequence=n_ins, localba_calls_per_sequence=len(res),
+                localba_problem="config-4 sized per keyframe (26 KFs of which 6 fixed, 8,000 points, ~43k edges; "
+                                "seed 7 + 1000*rank + kf)",
+                lm_iterations_per_sequence=its, lm_trials_per_sequence=trials,
+                sequence_s=round(t_seq, 5), extract_alone_s=round(t_ext, 5), localba_alone_s=round(t_ba, 5),
+                overlap_gain=round((t_ext + t_ba) / t_seq, 3) if t_seq > 0 else None,
+                frames_per_s_sequence=round(frames / t_seq, 2),
+                localba_iters_per_s_sequence=round(its_all / t_seq, 1),
+                frames_per_s_extract_alone=round(frames / t_ext, 2),
                 allgather_ms=round(t_gather * 1e3, 3), allgather_backend=backend,
                 record_bytes_per_rank=int(nbytes), record_bytes_per_frame=int(sh.layout.frame_bytes()),
                 allgather_bytes_received_per_rank=int(nbytes * (world - 1)),
                 allgather_algbw_GBps=round(nbytes * (world - 1) / t_gather / 1e9, 2) if world > 1 else None,
-                frames_per_s_compute=round(frames / t_compute, 2),
-                frames_per_s_with_allgather=round(frames / (t_compute + t_gather), 2),
-                localba_summary_ranks=[pipeline.parse_ba_summary(b)["iterations"] for b in bas],
+                frames_per_s_with_allgather=round(frames / (t_seq + t_gather), 2),
+                localba_summary_ranks=[[pipeline.parse_ba_summary(r)["iterations"]
+                                        for r in np.asarray(b).reshape(max(n_kf, 1), -1)[:n_kf]] for b in bas],
                 gathered_slots_match=ok_all,
-                note="the all-gather carries the LAST batch's records (the one-consumer exchange, SURVEY 8e); "
-                     "records of earlier batches are consumed in place")
+                note="frames_per_s_sequence = unique frames of all ranks / the sequence's wall time with every "
+                     "keyframe's LocalBA done (max over ranks); the all-gather carries the LAST batch's records "
+                     "(earlier batches are consumed in place) and every LocalBA summary")
 
 
 def main():
@@ -1047,7 +1171,9 @@ def main():
     if args.track_steps > 0:
         out["track"] = track_leg(args, rank, world, dev, odist, ex, images, stream, pairs)
     if args.pipeline_steps > 0:
-        out["config5"] = config5_leg(args, rank, world, dev, odist, ex, images, stream)
+        out["config5"] = config5_leg(args, rank, world, dev, odist, exs, batch_images, pairs)
+    if args.c1_batch > 0 and rank == 0 and world == 1:
+        out["config1"] = config1_leg(args, dev, oracle_mod, flags, cpus)
     if args.c3_steps > 0:
         out["config3"] = config3_leg(args, rank, world, dev, odist, stream, oracle_mod, flags, cpus)
     if rank == 0:

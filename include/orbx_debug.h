@@ -46,6 +46,8 @@ typedef struct {
   int nan_trial;        /* -1 off */
   int raise_stop_after; /* -1 off */
   int trace;            /* one timing line per call on stderr */
+  int split_ctl;        /* 1: a trial's errors and LM verdict as two launches (k_ba_errors +
+                           k_ba_lm_control) instead of k_ba_errors_ctl's one (tests compare them) */
 } orbx_ba_debug_options;
 /* NULL restores the defaults. */
 int orbx_debug_ba_options(orbx_ba* h, const orbx_ba_debug_options* options);

@@ -154,7 +154,8 @@ class TrackGather(C.Structure):
 
 
 class BaDebugOptions(C.Structure):  # include/orbx_debug.h orbx_ba_debug_options
-    _fields_ = [("ldlt", C.c_int), ("nan_trial", C.c_int), ("raise_stop_after", C.c_int), ("trace", C.c_int)]
+    _fields_ = [("ldlt", C.c_int), ("nan_trial", C.c_int), ("raise_stop_after", C.c_int), ("trace", C.c_int),
+                ("split_ctl", C.c_int)]
 
 
 class Camera(C.Structure):

@@ -570,6 +570,25 @@ __device__ __forceinline__ int ring_score1(const uint8_t* t) {
   return max(a, b);
 }
 
+#ifdef ORBX_FAST_PROBE
+// probe only: the necessary condition "4 contiguous of the 8 even ring points beyond t" (a 9-arc
+// always holds 4 or 5 consecutive even positions), counted on the compass survivors
+template <int S>
+__device__ __forceinline__ bool even8_test(const uint8_t* t, int th) {
+  constexpr int o[8] = {6 * S + 3, 5 * S + 5, 3 * S + 6, S + 5, 3, S + 1, 3 * S, 5 * S + 1};
+  const int v = t[3 * S + 3];
+  int p[8], lo2[8], hi2[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) p[k] = t[o[k]];
+#pragma unroll
+  for (int k = 0; k < 8; k++) lo2[k] = min(p[k], p[(k + 1) & 7]), hi2[k] = max(p[k], p[(k + 1) & 7]);
+  int bl = 0, bh = 255;
+#pragma unroll
+  for (int k = 0; k < 8; k++) bl = max(bl, min(lo2[k], lo2[(k + 2) & 7])), bh = min(bh, max(hi2[k], hi2[(k + 2) & 7]));
+  return bl > v + th || bh < v - th;
+}
+#endif
+
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 as_s16x2(int v) { return __builtin_bit_cast(s16x2, v); }
 __device__ __forceinline__ int as_int(s16x2 v) { return __builtin_bit_cast(int, v); }
@@ -594,8 +613,13 @@ __device__ unsigned int* fast_probe_buf;
 #define ORBX_FAST_CPW 2
 #endif
 constexpr int kFastCPW = ORBX_FAST_CPW;  // FAST cells per wave
+#ifdef ORBX_FAST_VSLIDE
+#define ORBX_FAST_ATTR __attribute__((amdgpu_waves_per_eu(8)))  // 64 VGPRs: 8 one-wave blocks per SIMD
+#else
+#define ORBX_FAST_ATTR
+#endif
 template <int S, int RP>
-__global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
+__global__ __launch_bounds__(64) ORBX_FAST_ATTR void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B, int grp) {
   // dynamic LDS sized by the launch group's largest cell (G->fg[grp])
   extern __shared__ __align__(16) uint8_t fast_smem[];
@@ -675,7 +699,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   constexpr int QU = 8 / RP;
 #ifdef ORBX_FAST_PROBE
   unsigned long long ts_mid = 0;
-  int n_compass = 0;
+  int n_compass = 0, n_even8 = 0, n_corner_ini = 0;
 #endif
   // 2.+3. FAST(window, th): compass quick test at th, row-major compaction of tile offsets, then
   // cornerScore + the corner test at th on the compass list, corners compacted in place and their
@@ -683,6 +707,75 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   // rewrites the same values).  Returns the corner count.
   auto detect = [&](int th) -> int {
     int n = 0;
+#ifdef ORBX_FAST_VSLIDE
+    // Each lane walks its column down the rows (RP == 2: lanes 0-31 the rows [0, Hh), lanes 32-63
+    // [Hh, H)), keeping the last six pixels of column x+3 in registers: per row only c0 (row y+6),
+    // c4 and c12 (row y+3) are read, cv and c8 are c0 of three and six rows earlier (3 LDS reads
+    // per pixel instead of 5).  The two halves compact into separate list regions (top at 0,
+    // bottom at Hh W), so each stays row-major; the bottom region then moves down behind the top.
+    {
+      const int Hh = RP == 2 ? (H + 1) >> 1 : H;
+      const int ys = RP == 2 ? ly * Hh : 0, ye = RP == 2 ? (ly ? H : Hh) : H;
+      const int BOFF = RP == 2 ? Hh * W : 0;
+      const uint8_t* colp = tile + ys * S + lx + 3;
+      int R[6];
+#pragma unroll
+      for (int j = 0; j < 6; j++) R[j] = colp[j * S];
+      int ntop = 0, nbot = 0;
+      for (int s0 = 0; s0 < Hh; s0 += 6) {
+        // each three rows' nine reads first (in flight together before the first use; six rows'
+        // eighteen would cost the 64-VGPR budget of eight waves per SIMD)
+        int C0[6], C4[6], C12[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+          if (j % 3 == 0) {
+#pragma unroll
+            for (int q = j; q < j + 3; q++) {
+              const uint8_t* t = tile + (ys + s0 + q) * S + lx;
+              C0[q] = t[6 * S + 3];
+              C4[q] = t[3 * S + 6];
+              C12[q] = t[3 * S];
+            }
+          }
+          const int y = ys + s0 + j;
+          const int c0 = C0[j], c4 = C4[j], c12 = C12[j];
+          const int c8 = R[j], cv = R[(j + 3) % 6];
+          R[j] = c0;
+          const int hi = min(max(c0, c8), max(c4, c12));
+          const int lo = max(min(c0, c8), min(c4, c12));
+          const int v = max(hi - cv, cv - lo) - (th + 1);  // >= 0 <=> compass hit
+          const bool hit = (~v & cw & (y - ye)) < 0;
+          const uint64_t m = __ballot(hit);
+          const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);
+          // rank among all lanes; the upper half's base drops the lower half's count
+          const int base = RP == 2 ? (ly ? BOFF + nbot - __popc(mlo) : ntop) : ntop;
+          if (hit) list[base + lane_rank(m)] = (uint16_t)(y * S + lx);
+          if constexpr (RP == 2) {
+            ntop += __popc(mlo);
+            nbot += __popc(mhi);
+          } else {
+            ntop += __popcll(m);
+          }
+        }
+      }
+      if constexpr (RP == 2) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // bottom region [BOFF, BOFF + nbot) -> [ntop, ntop + nbot): a chunk's writes stay below the
+        // next chunk's sources (ntop <= BOFF), and each chunk is read before it is written
+        for (int i0 = 0; i0 < nbot; i0 += 64) {
+          const int i = i0 + lane;
+          const uint16_t e = i < nbot ? list[BOFF + i] : (uint16_t)0;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (i < nbot) list[ntop + i] = e;
+        }
+      }
+      n = ntop + nbot;
+    }
+#else
     for (int y0r = 0; y0r < H; y0r += QU * RP) {
       const int eb = (y0r + ly) * S + lx;
       int cv[QU], c0[QU], c4[QU], c8[QU], c12[QU];
@@ -710,6 +803,7 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
         n += __popcll(m);
       }
     }
+#endif
     __syncthreads();
 #ifdef ORBX_FAST_PROBE
     if (th == ini) ts_mid = __builtin_amdgcn_s_memtime(), n_compass = n;
@@ -724,6 +818,9 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
         sc1 = ring_score1<S>(tile + e);
         corner = sc1 > th;
       }
+#ifdef ORBX_FAST_PROBE
+      if (th == ini) n_even8 += __popcll(__ballot(i < n && even8_test<S>(tile + e, th)));
+#endif
       const uint64_t m = __ballot(corner);
       __syncthreads();
       if (corner) {
@@ -751,6 +848,9 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
   FAST_TS(1);
   int nc = detect(ini);
   FAST_TS(2);
+#ifdef ORBX_FAST_PROBE
+  n_corner_ini = nc;
+#endif
   // 4. survivors at iniThFAST (verdict kept in bit 15 of the list entry)
   int cnt = 0;
   for (int i0 = 0; i0 < nc; i0 += 64) {
@@ -794,8 +894,11 @@ __global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, con
 #ifdef ORBX_FAST_PROBE
   FAST_TS(5);
   if (lane < 8 && fast_probe_buf) {
+    // word 6: empty-cell flag | corners at iniThFAST << 1 | survivors at iniThFAST << 16;
+    // word 7: compass survivors | even-8 survivors << 16 (both at iniThFAST)
     const unsigned long long t[8] = {ts1 - ts0, ts_mid - ts1, ts2 - ts_mid, ts3 - ts2, ts4 - ts3, ts5 - ts4,
-                                     (unsigned long long)(cnt == 0), (unsigned long long)n_compass};
+                                     (unsigned long long)((cnt == 0) | (n_corner_ini << 1) | (cnt << 16)),
+                                     (unsigned long long)(n_compass | (n_even8 << 16))};
     fast_probe_buf[((size_t)img * G->ncells + cell) * 8 + lane] = (unsigned int)t[lane];
   }
 #endif

@@ -1925,13 +1925,19 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
     y[r] = i < N ? ys[i] : 0.0;
   }
   static_assert(R == 2, "the two-phase row loop below: rows 64.. then 0..63");
-  auto row_ptr = [&](int k) { return Lpk + (size_t)max(k, 1) * (max(k, 1) - 1) / 2; };
+  // Rows are clamped to [1, N-1]: a row k >= N (the 8-row groups round N up) reads row N-1's
+  // entries, which are finite and meet x_k = y_k = 0, and no read leaves the kernel's LDS (the
+  // lanes past a row's k entries read the next rows or the zero-initialised panel arrays).
+  auto row_ptr = [&](int k) {
+    const int r = min(max(k, 1), max(N - 1, 1));
+    return Lpk + (size_t)r * (r - 1) / 2;
+  };
   constexpr int kAhead = 8;  // rows loaded ahead (<= 15 LDS reads in flight)
   LDLT_TS(48);
-  // phase 1: rows k = K1 .. 64 (K1 >= N - 1; rows k >= N have x_k = y_k = 0 and change nothing):
-  // x_k sits in y[1]; rows i < 64 always take the update, rows i >= 64 only when i < k
-  {
-    const int K1 = 64 + 8 * ((max(N - 64, 0) + 7) / 8) - 1;
+  // phase 1 (N > 64): rows k = K1 .. 64 (K1 >= N - 1; rows k >= N have x_k = y_k = 0 and change
+  // nothing): x_k sits in y[1]; rows i < 64 always take the update, rows i >= 64 only when i < k
+  if (N > 64) {
+    const int K1 = 64 + 8 * ((N - 64 + 7) / 8) - 1;
     double L0[kAhead], L1[kAhead];
 #pragma unroll
     for (int u = 0; u < kAhead; u++) {
@@ -1945,24 +1951,28 @@ __device__ __forceinline__ void k_ba_ldlt_pan_body(const BaDev& D) {
         const int k = k0 - u;
         const double xk = readlane_d(y[1], k - 64);
         y[0] = __builtin_fma(-L0[u], xk, y[0]);
-        y[1] = __builtin_fma(lane + 64 < k ? -L1[u] : 0.0, xk, y[1]);
+        const double y1 = __builtin_fma(-L1[u], xk, y[1]);
+        y[1] = lane + 64 < k ? y1 : y[1];  // (rows at or past k keep their value: no 0 * inf)
         const double* Lk = row_ptr(k - kAhead);  // (rows below 64 of the next group: unused)
         L0[u] = Lk[lane];
         L1[u] = Lk[lane + 64];
       }
     }
   }
-  // phase 2: rows k = 63 .. 0, x_k in y[0]; rows i >= 64 are final
+  // phase 2: rows k = K2 .. 0 (K2 = min(63, N - 1) rounded up to a group of eight), x_k in y[0];
+  // rows i >= 64 are final
   {
+    const int K2 = min(63, 8 * ((N + 7) / 8) - 1);
     double L0[kAhead];
 #pragma unroll
-    for (int u = 0; u < kAhead; u++) L0[u] = row_ptr(63 - u)[lane];
-    for (int k0 = 63; k0 >= 0; k0 -= kAhead) {
+    for (int u = 0; u < kAhead; u++) L0[u] = row_ptr(K2 - u)[lane];
+    for (int k0 = K2; k0 >= 0; k0 -= kAhead) {
 #pragma unroll
       for (int u = 0; u < kAhead; u++) {
         const int k = k0 - u;
         const double xk = readlane_d(y[0], k);
-        y[0] = __builtin_fma(lane < k ? -L0[u] : 0.0, xk, y[0]);
+        const double y0 = __builtin_fma(-L0[u], xk, y[0]);
+        y[0] = lane < k ? y0 : y[0];
         L0[u] = row_ptr(k - kAhead)[lane];  // (k - kAhead < 1: unused)
       }
     }
@@ -2261,25 +2271,30 @@ __device__ inline double seq_sum_wave(const double* p, int n) {
 
 // Two such sums at once (same orders and bits as two seq_sum_wave calls): both arrays' loads are
 // in flight together and lane 0 adds the first while lane 1 adds the second (valid in lane 0).
+// Wave 0 does the work; every other wave of the block only passes the barriers (a block of any
+// size calls it uniformly, so no barrier ever counts on exited waves).
 template <bool coh = false>  // coh: p is read with ld_agent (partials stored by this launch's other blocks)
 __device__ inline void seq_sum2_wave(const double* p, int n, const double* q, int m, double& sp, double& sq) {
   __shared__ double buf[2][512];
   double s = 0;
   const int len = max(n, m);
+  const bool w0 = threadIdx.x < 64;
   for (int base = 0; base < len; base += 512) {
     const int cn = min(512, n - base), cm = min(512, m - base);  // (may be <= 0)
-    double vp[8], vq[8];
+    if (w0) {
+      double vp[8], vq[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {  // clamped, unpredicated loads: all sixteen in flight at once
-      const int i = threadIdx.x + 64 * u;
-      vp[u] = coh ? ld_agent(p + max(min(base + i, n - 1), 0)) : p[max(min(base + i, n - 1), 0)];
-      vq[u] = q[max(min(base + i, m - 1), 0)];
-    }
+      for (int u = 0; u < 8; u++) {  // clamped, unpredicated loads: all sixteen in flight at once
+        const int i = threadIdx.x + 64 * u;
+        vp[u] = coh ? ld_agent(p + max(min(base + i, n - 1), 0)) : p[max(min(base + i, n - 1), 0)];
+        vq[u] = q[max(min(base + i, m - 1), 0)];
+      }
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int i = threadIdx.x + 64 * u;
-      if (i < cn) buf[0][i] = vp[u];
-      if (i < cm) buf[1][i] = vq[u];
+      for (int u = 0; u < 8; u++) {
+        const int i = threadIdx.x + 64 * u;
+        if (i < cn) buf[0][i] = vp[u];
+        if (i < cm) buf[1][i] = vq[u];
+      }
     }
     __syncthreads();
     if (threadIdx.x < 2) {
@@ -2380,7 +2395,8 @@ __device__ __forceinline__ void k_ba_lm_control_body(const BaDev& D, DevStop sto
   if (L->done) return;  // uniform; a finished phase keeps `rejected` for the final restore
   // the flag's host-memory read is issued first, so its latency hides behind the sums (one read
   // serves both of the loop's polls below; a flag raised after it is seen at the next trial)
-  const bool st = stop() || (D.raise_after >= 0 && L->trials >= D.raise_after);  // (+ test hook)
+  // (thread 0 alone reads it: the verdict below is thread 0's)
+  const bool st = threadIdx.x == 0 && (stop() || (D.raise_after >= 0 && L->trials >= D.raise_after));  // (+ test hook)
   const double* p = D.scal + 8;
   double b, u;
   seq_sum2_wave<coh>(p + D.nbe, D.nbe, p + 2 * D.nbe, nbu, b, u);
@@ -2452,22 +2468,26 @@ __global__ __launch_bounds__(64) void k_ba_lm_resume_many(const BaDev* __restric
   k_ba_lm_resume_body(Ds[blockIdx.z]);
 }
 // A trial's k_ba_errors(D, 1, 1) and k_ba_lm_control in one launch (single-problem device LM): every
-// block stores its chi partial write-through and, once the store has landed, takes a ticket; the
-// block that takes the last one runs the verdict with wave 0, reading the partials past its L2.  Same
-// partials, same order, same arithmetic as the two launches (one dispatch less per trial).
+// block's thread 0 stores its chi partial (agent scope) and then takes a ticket with an agent-scope
+// acq_rel RMW; the block whose ticket is the last one has thereby acquired every other block's
+// release, i.e. every partial store happens-before its reads (the block barrier carries that to the
+// rest of the block).  That block runs the verdict (wave 0 works, the other waves only pass the
+// barriers).  Same partials, same order, same arithmetic as the two launches k_ba_errors +
+// k_ba_lm_control, which the debug option split_ctl selects (tests compare the two bit for bit).
 __global__ __launch_bounds__(LBS) void k_ba_errors_ctl(BaDev D, DevStop stop) {
   if (!k_ba_errors_body<true>(D, 1, 1)) return;
   __shared__ int last;
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_s_waitcnt(0);  // the partial's write-through store is complete
     unsigned* tk = &const_cast<LmState*>(D.lm)->ticket;
-    last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(D.nbe - 1);
+    last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(D.nbe - 1);
     if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (!last || threadIdx.x >= 64) return;  // (waves 1-3 leave; wave 0's barriers count only live waves)
+  if (!last) return;  // (uniform per block)
   k_ba_lm_control_body<true>(D, stop);
 }
+// The two-launch form's verdict (debug option split_ctl): after k_ba_errors(D, 1, 1), one wave.
+__global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, DevStop stop) { k_ba_lm_control_body(D, stop); }
 __global__ __launch_bounds__(64) void k_ba_lm_control_many(const BaDev* __restrict__ Ds, DevStop stop) {
   k_ba_lm_control_body(Ds[blockIdx.z], stop);
 }
@@ -3334,6 +3354,7 @@ struct LocalBA {
       hipLaunchKernelGGL(k_ba_lm_start, dim3(1), dim3(1024), 0, st, Dg, iterations);
       BA_CHECK(hipGetLastError());
       const bool psfold = Dg.fused == 2;
+      const bool split_ctl = ba_opts().split_ctl != 0;
       auto trial = [&](bool lin) {
         // linearisation gated on the device: only at the start of a new iteration
         if (fused && (lin || psfold)) hipLaunchKernelGGL(k_ba_lin_schur, dim3(Dg.nbf), dim3(kFuseNT), kFuseSmem, st, Dg);
@@ -3346,7 +3367,12 @@ struct LocalBA {
           ldlt.launch(Dg, st);
         }
         hipLaunchKernelGGL(k_ba_update, dim3(Dg.nbu), dim3(LBS), 0, st, Dg, 0.0);
-        hipLaunchKernelGGL(k_ba_errors_ctl, dim3(Dg.nbe), dim3(LBS), 0, st, Dg, dstop);
+        if (split_ctl) {
+          hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, Dg, 1, 1);
+          hipLaunchKernelGGL(k_ba_lm_control, dim3(1), dim3(64), 0, st, Dg, dstop);
+        } else {
+          hipLaunchKernelGGL(k_ba_errors_ctl, dim3(Dg.nbe), dim3(LBS), 0, st, Dg, dstop);
+        }
       };
       // (capturing the trial as a HIP graph and launching that instead measured slower on this
       // stack: 2.81 vs 2.76 ms per config-4 call)
@@ -3961,7 +3987,7 @@ orbx_status run_local_ba_many(LocalBA* const* Ls, int K, BaBatch& B, const orbx_
 }  // namespace orbx
 
 namespace orbx {
-constexpr orbx_ba_debug_options kBaOptsDefault = {ORBX_BA_LDLT_AUTO, -1, -1, 0};
+constexpr orbx_ba_debug_options kBaOptsDefault = {ORBX_BA_LDLT_AUTO, -1, -1, 0, 0};
 thread_local const orbx_ba_debug_options* t_ba_opts = nullptr;
 inline const orbx_ba_debug_options& ba_opts() { return t_ba_opts ? *t_ba_opts : kBaOptsDefault; }
 struct BaOptScope {  // the handle's options for this call on this thread

@@ -566,7 +566,7 @@ class Optimizer:
 
     def set_debug_options(self, **kw):
         """Test options of this solver handle (include/orbx_debug.h, orbx_ba_debug_options: ldlt,
-        nan_trial, raise_stop_after, trace); no arguments restore the production defaults."""
+        nan_trial, raise_stop_after, trace, split_ctl); no arguments restore the production defaults."""
         o = _lib.BaDebugOptions(0, -1, -1, 0)
         for k, v in kw.items():
             if k not in dict(o._fields_):

@@ -15,9 +15,20 @@ with ONE all-gather each:
 * per-rank LocalBA summaries (``ba_summary``): LM iterations per phase, trials,
   final chi2 per phase, outlier count and the optimised poses (FP64).
 
+A rank's sequence is stepped in order through distinct frame batches
+(``SequenceShard.run_sequence``); every ``kf_every`` frames a keyframe is inserted into
+the rank's ``LocalMapping`` thread, which runs one LocalBundleAdjustment per keyframe on
+its own solver handle and HIP stream once the batch holding the keyframe's frame is done,
+concurrently with the extraction of the following batches (Tracking and LocalMapping as
+the reference's two threads: src/Tracking.cc:1147-1179 InsertKeyFrame,
+src/LocalMapping.cc:51-101).
+
 torch.distributed backend "nccl" is RCCL over xGMI (device tensors); "gloo" moves
 CPU tensors (CPU tests, and the one-GPU multi-rank rehearsal).
 """
+import queue
+import threading
+
 import numpy as np
 
 KP_BYTES = 28
@@ -121,30 +132,69 @@ class SequenceShard:
     layout (frames per batch, keypoint capacity) is the maximum over the ranks, so every rank's arena
     has the same size for the all-gather whatever its sequence's image size."""
 
-    def __init__(self, extractor, n_frames, width, height, bf, baseline, device):
+    def __init__(self, extractor, n_frames, width, height, bf, baseline, device, extractors=None):
+        """extractors: optional further extractor handles (each with its own record arena and HIP
+        stream) so that consecutive batches of the sequence are in flight together; batch k runs on
+        slot k % S and writes arena k % S.  `arena` is the arena of the last batch stepped."""
+        import torch
+        self.exs = [extractor] + list(extractors or [])
         self.ex = extractor
         self.layout = FrameRecords(agree_max(n_frames), agree_max(extractor.max_keypoints(width, height)))
-        self.arena = new_arena(self.layout, device)
-        self.v = self.layout.views(self.arena)
+        self.arenas = [new_arena(self.layout, device) for _ in self.exs]
+        self.views_ = [self.layout.views(a) for a in self.arenas]
+        self.streams = [torch.cuda.Stream(device) for _ in self.exs]
         self.bf, self.baseline = float(bf), float(baseline)
-        import torch
-        self.stream = torch.cuda.Stream(device)
+        self.stream = self.streams[0]
+        self.slot = 0
+        self.frames_done = 0
+        self.last_stream = None
 
-    def step(self, images, stream=None, clear=True):
+    @property
+    def arena(self):
+        return self.arenas[self.slot]
+
+    @property
+    def v(self):
+        return self.views_[self.slot]
+
+    def step(self, images, stream=None, clear=True, slot=0):
         """images: (2B, H, W) u8 device tensor ordered L0,R0,L1,R1,...  clear=True zeroes the arena first
         (canonical padding: the records of a batch do not depend on the previous batch).  The zeroing and
         the extraction are ordered on ONE stream: `stream` (a torch.cuda.Stream other than the legacy null
-        stream, which the library would replace by its handle's own stream) or the shard's own."""
+        stream, which the library would replace by its handle's own stream) or the slot's own."""
         import torch
+        self.slot = slot % len(self.exs)
         if stream is None or getattr(stream, "cuda_stream", 0) == 0:
-            stream = self.stream
+            stream = self.streams[self.slot]
         self.last_stream = stream
         if clear:
             with torch.cuda.stream(stream):
                 self.arena.zero_()
         v = self.v
-        self.ex.stereo_frames_device(images, v["kps"], v["desc"], v["counts"], self.bf, self.baseline, v["uR"],
-                                     v["depth"], v["nmatch"], stream)
+        self.exs[self.slot].stereo_frames_device(images, v["kps"], v["desc"], v["counts"], self.bf, self.baseline,
+                                                 v["uR"], v["depth"], v["nmatch"], stream)
+
+    def run_sequence(self, batches, local_mapping=None, kf_every=0):
+        """Step the rank's sequence through `batches` in order (frame numbers continue across calls), the
+        batches in flight over the shard's slots.  With a LocalMapping thread, frame f is a keyframe when
+        (f + 1) % kf_every == 0: it is inserted (keyframe id f // kf_every) together with an event
+        recorded after its batch, so its LocalBA starts once that batch's extraction has finished on
+        the device while later batches keep extracting.  Returns the number of keyframes inserted."""
+        import torch
+        n_kf = 0
+        for k, images in enumerate(batches):
+            self.step(images, slot=k)
+            nf = int(images.shape[0]) // 2
+            f0, self.frames_done = self.frames_done, self.frames_done + nf
+            if local_mapping is not None and kf_every > 0:
+                kfs = [f // kf_every for f in range(f0, f0 + nf) if (f + 1) % kf_every == 0]
+                if kfs:
+                    ev = torch.cuda.Event()
+                    ev.record(self.last_stream)
+                    for kf in kfs:
+                        local_mapping.insert_keyframe(kf, ev)
+                    n_kf += len(kfs)
+        return n_kf
 
 
     def gather(self, ba_record):
@@ -182,6 +232,74 @@ def parse_ba_summary(rec):
     n = int(rec[6])
     return dict(iterations=(int(rec[0]), int(rec[1])), trials=int(rec[2]), chi2=(rec[3], rec[4]),
                 outliers=int(rec[5]), Tcw=rec[BA_HEAD:BA_HEAD + 12 * n].reshape(n, 12))
+
+
+# ------------------------------------------------------------------ LocalMapping thread
+class LocalMapping:
+    """One rank's LocalMapping thread (src/LocalMapping.cc:51-101): keyframes arrive from the sequence
+    loop (`insert_keyframe`, as Tracking::InsertKeyFrame hands them over); for each, after the event of
+    the batch that produced its frame, Optimizer::LocalBundleAdjustment runs on this thread's own solver
+    handle -- its own HIP stream -- on `problems(kf)` (the keyframe's local map), concurrently with the
+    extraction the sequence loop keeps launching.  Every keyframe's LocalBA runs: the cadence is the
+    caller's stated kf_every, with no mbAbortBA interruption (the reference aborts a running BA when a
+    keyframe arrives so that a real-time tracker never waits; here throughput is measured instead).
+    The LocalBA calls release the GIL (ctypes), so the two threads overlap on the host too."""
+
+    def __init__(self, problems, device, optimizer=None):
+        from .orb import Optimizer
+        self.problems = problems  # callable kf -> problem dict, or a sequence indexed by kf
+        self.own = optimizer is None
+        self.opt = optimizer if optimizer is not None else Optimizer(device.index if hasattr(device, "index") else int(device))
+        self.q = queue.Queue()
+        self.results = []  # (kf, result dict) in insertion order
+        self.error = None
+        self.t = threading.Thread(target=self._run, name="LocalMapping", daemon=True)
+        self.t.start()
+
+    def insert_keyframe(self, kf, event=None):
+        self.q.put((int(kf), event))
+
+    def _problem(self, kf):
+        return self.problems(kf) if callable(self.problems) else self.problems[kf]
+
+    def _run(self):
+        try:
+            while True:
+                item = self.q.get()
+                if item is None:
+                    return
+                kf, ev = item
+                if ev is not None:
+                    ev.synchronize()  # the keyframe's frame is extracted (releases the GIL while it waits)
+                self.results.append((kf, self.opt.LocalBundleAdjustment(self._problem(kf))))
+        except BaseException as e:  # noqa: BLE001 -- re-raised by finish() on the caller's thread
+            self.error = e
+
+    def finish(self):
+        """Wait until every inserted keyframe's LocalBA has finished; returns [(kf, result)]."""
+        self.q.put(None)
+        self.t.join()
+        if self.error is not None:
+            raise self.error
+        return list(self.results)
+
+    def close(self):
+        if self.t.is_alive():
+            self.finish()
+        if self.own:
+            self.opt.close()
+
+
+def ba_summaries(results, n_cams, n_kf=None, max_cams=MAX_BA_CAMS):
+    """The fixed-size records of a rank's LocalBA calls, concatenated in keyframe order; `n_kf` (agreed
+    over the ranks with agree_max) pads with zero records so every rank sends the same length."""
+    n_kf = len(results) if n_kf is None else int(n_kf)
+    if len(results) > n_kf:
+        raise ValueError("LocalBA summaries: %d calls > n_kf %d" % (len(results), n_kf))
+    rec = np.zeros((n_kf, BA_HEAD + 12 * max_cams), np.float64)
+    for i, r in enumerate(results):
+        rec[i] = ba_summary(r, n_cams[i] if hasattr(n_cams, "__len__") else n_cams, max_cams)
+    return rec.reshape(-1)
 
 
 # ------------------------------------------------------------------ collectives

@@ -4,8 +4,11 @@
 // ORBextractor handles (src/Frame.cc:80-84), UndistortKeyPoints, ComputeStereoMatches -- on
 // host images, with results returned to host vectors.  Extractors are built once, as Tracking does.
 //
-// usage: frame_bench FILE W H N_UNIQUE N_FRAMES WARMUP NFEATURES BF FX
+// usage: frame_bench FILE W H N_UNIQUE N_FRAMES WARMUP NFEATURES BF FX [mono]
 //   FILE holds N_UNIQUE stereo pairs (L then R, W*H bytes each); frame f uses pair f % N_UNIQUE.
+//   mono (BASELINE config 1, TUM): FILE holds N_UNIQUE images and each call is one
+//   ORBextractor::operator()(image, cv::Mat(), keypoints, descriptors) -- the extraction Frame's
+//   monocular constructor makes (src/Frame.cc:186-205 -> ExtractORB, :273-279); BF/FX unused.
 // Prints one JSON line: per-frame milliseconds (after WARMUP) and the keypoint / match counts.
 #include <algorithm>
 #include <chrono>
@@ -27,7 +30,8 @@ int main(int argc, char** argv) {
   const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), U = std::atoi(argv[4]);
   const int NF = std::atoi(argv[5]), WU = std::atoi(argv[6]), nfeat = std::atoi(argv[7]);
   const float bf = (float)std::atof(argv[8]), fx = (float)std::atof(argv[9]);
-  std::vector<uint8_t> data((size_t)U * 2 * W * H);
+  const bool mono = argc > 10 && std::strcmp(argv[10], "mono") == 0;
+  std::vector<uint8_t> data((size_t)U * (mono ? 1 : 2) * W * H);
   FILE* f = std::fopen(argv[1], "rb");
   if (!f || std::fread(data.data(), 1, data.size(), f) != data.size()) {
     std::fprintf(stderr, "cannot read %s\n", argv[1]);
@@ -35,6 +39,33 @@ int main(int argc, char** argv) {
   }
   std::fclose(f);
   try {
+    if (mono) {
+      ORBextractor ex(nfeat, 1.2f, 8, 20, 7);  // Tracking's mono extractor (src/Tracking.cc:120,125)
+      std::vector<double> ms;
+      long long kp = 0;
+      std::vector<cv::KeyPoint> keys;
+      cv::Mat desc;
+      for (int i = 0; i < WU + NF; i++) {
+        cv::Mat im(H, W, CV_8U, data.data() + (size_t)(i % U) * W * H);
+        const auto t0 = std::chrono::steady_clock::now();
+        ex(im, cv::Mat(), keys, desc);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (i >= WU) {
+          ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+          kp += (long long)keys.size();
+        }
+      }
+      std::vector<double> s = ms;
+      std::sort(s.begin(), s.end());
+      double mean = 0;
+      for (double v : ms) mean += v;
+      mean /= ms.size();
+      std::printf("{\"frames\": %d, \"median_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f, \"min_ms\": %.4f, "
+                  "\"keypoints_per_frame\": %.1f}\n",
+                  NF, s[s.size() / 2], s[std::min(s.size() - 1, (size_t)(0.9 * s.size()))], mean, s.front(),
+                  (double)kp / NF);
+      return 0;
+    }
     ORBextractor exL(nfeat, 1.2f, 8, 20, 7), exR(nfeat, 1.2f, 8, 20, 7);  // Tracking's (src/Tracking.cc:120-126)
     cv::Mat K(3, 3, CV_32F), dist(4, 1, CV_32F);
     std::memset(K.data, 0, 36);

@@ -278,6 +278,53 @@ def test_gpu_reduced_system_ldlt(gpu, N, kernel):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nposes", [1, 2, 3, 4, 5])
+def test_gpu_reduced_system_ldlt_pan_few_poses(gpu, nposes):
+    """The panel kernel at 1..5 free poses (N = 6..30: its back solve rounds N up to a group of
+    eight rows and clamps the rows it reads to N-1) against the column-step kernel on the
+    same system, and both against numpy."""
+    import ctypes as C
+    from orb_slam2_commit_amd import _lib
+    N = 6 * nposes
+    rng = np.random.default_rng(100 + N)
+    M = rng.normal(size=(N, N))
+    S = np.ascontiguousarray(M @ M.T + 0.1 * N * np.eye(N))
+    b = rng.normal(size=N)
+    xs = {}
+    for kernel in ("default", "col"):
+        x = np.zeros(N)
+        ms = C.c_float(0)
+        assert _lib.lib().orbx_debug_ldlt_ex(_lib.ptr(S), _lib.ptr(b), N, _lib.ptr(x), 1, C.byref(ms),
+                                             LDLT_KIND[kernel], None) == 0
+        xs[kernel] = x
+    ref = np.linalg.solve(S, b)
+    for x in xs.values():
+        assert np.abs(x - ref).max() <= 1e-10 * max(1.0, np.abs(ref).max())
+    assert np.abs(xs["default"] - xs["col"]).max() <= 1e-12 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["config4", "rejects_a", "rejects_b", "nbad_stop", "nan_trial"])
+def test_gpu_localba_errors_ctl_equals_two_launches(ba, case):
+    """k_ba_errors_ctl (a trial's errors and the LM verdict in one launch, the partials handed to the
+    last block through an agent-scope acq_rel ticket) against the two-launch form k_ba_errors +
+    k_ba_lm_control (debug option split_ctl): bit for bit, with identical iterations, trials, chi2
+    and outliers, on config 4, the rejection / _nBad problems and a NaN-rho trial."""
+    P = synth.localba_problem(seed=7) if case in ("config4", "nan_trial") else reject_problem(case)
+    kw = dict(nan_trial=1) if case == "nan_trial" else {}
+    with ba.debug_options(**kw):
+        a = ba.LocalBundleAdjustment(P)
+    with ba.debug_options(split_ctl=1, **kw):
+        b = ba.LocalBundleAdjustment(P)
+    for k in ("Tcw", "Xw", "Tcw_d", "Xw_d", "edge_outlier"):
+        np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))
+    assert list(a["iterations"]) == list(b["iterations"]) and a["trials"] == b["trials"]
+    assert a["chi2"] == b["chi2"]
+    if case != "nan_trial":
+        _compare(a, oracle.local_ba(P))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["default", "col", "blocked"])
 def test_gpu_reduced_system_ldlt_zero_pivot(gpu, kernel):
     import ctypes as C

@@ -5,7 +5,10 @@ CPU (gloo, world 2): the records are filled by the oracle (test infrastructure),
 layout, the sharding of sequences over ranks, the gather and the unpacking: the gathered records are
 byte-equal to a single-process build of the same sequences.
 GPU (gloo rehearsal of two ranks on one MI355X): the same exchange over the HIP path, gathered records
-byte-equal to a single-process run of the same frames, and every frame equal to the oracle."""
+byte-equal to a single-process run of the same frames, and every frame equal to the oracle; and the
+config-5 per-rank workload at full size -- a 256-frame KITTI batch per rank with a config-4-sized
+LocalBA on the rank's LocalMapping thread, overlapping the extraction -- against the oracle."""
+import hashlib
 import os
 import socket
 
@@ -171,6 +174,42 @@ def test_record_layout():
     assert len(fr[1]["kpsR"]) == 7 and fr[1]["uR"].shape == (0,)
 
 
+class _OracleOptimizer:
+    """Stands in for the GPU solver handle in the CPU test of the LocalMapping thread."""
+
+    def __init__(self):
+        self.calls = []
+
+    def LocalBundleAdjustment(self, P):
+        self.calls.append(len(P["Tcw"]))
+        return oracle.local_ba(P)
+
+
+def test_local_mapping_thread_runs_every_keyframe_in_order():
+    """pipeline.LocalMapping: every inserted keyframe's LocalBA runs once, in insertion order, on the
+    thread; finish() returns them; ba_summaries pads to the agreed keyframe count."""
+    probs = {kf: _ba_problem(kf) for kf in range(3)}
+    fake = _OracleOptimizer()
+    lm = pipeline.LocalMapping(probs, "cpu", optimizer=fake)
+    for kf in range(3):
+        lm.insert_keyframe(kf)
+    res = lm.finish()
+    assert [kf for kf, _ in res] == [0, 1, 2]
+    for kf, r in res:
+        o = oracle.local_ba(probs[kf])
+        assert tuple(r["iterations"]) == tuple(o["iterations"])
+    rec = pipeline.ba_summaries([r for _, r in res], [len(probs[k]["Tcw"]) for k in range(3)], n_kf=4)
+    rows = rec.reshape(4, -1)
+    assert not rows[3].any()
+    assert pipeline.parse_ba_summary(rows[1])["iterations"] == tuple(res[1][1]["iterations"])
+    with pytest.raises(ValueError):
+        pipeline.ba_summaries([r for _, r in res], 7, n_kf=2)
+    bad = pipeline.LocalMapping(lambda kf: 1 / 0, "cpu", optimizer=fake)  # errors surface on finish()
+    bad.insert_keyframe(0)
+    with pytest.raises(ZeroDivisionError):
+        bad.finish()
+
+
 def test_ba_summary_roundtrip():
     P = _ba_problem(3)
     r = oracle.local_ba(P)
@@ -269,7 +308,7 @@ def test_gpu_bench_launcher_gloo_two_ranks(gpu):
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
            "--batch", "8", "--inflight", "1", "--unique", "2", "--profile-steps", "1", "--no-cpu-baseline",
            "--ba-calls", "0", "--single-frames", "0", "--track-steps", "0", "--c3-steps", "0",
-           "--pipeline-steps", "1"]
+           "--pipeline-steps", "1", "--kf-every", "8"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -281,4 +320,101 @@ def test_gpu_bench_launcher_gloo_two_ranks(gpu):
     assert out["config5"]["sequences"] == 2
     assert out["config5"]["allgather_backend"] == "gloo"
     assert out["config5"]["gathered_slots_match"] is True
+    assert out["config5"]["localba_calls_per_sequence"] == 1 and out["config5"]["unique_frames_per_sequence"] == 8
     assert out["value"] > 0
+
+
+# ----------------------------------------------------------------- config-5 per-rank workload, full size
+C5_B = 256  # bench.py's batch: one full KITTI batch per rank
+C5_SLOTS = (0, C5_B // 2, C5_B - 1)  # sampled slots checked against the oracle
+
+
+def _c5_problem(seq):
+    return synth.localba_problem(seed=7 + 1000 * seq)  # config 4's size (26 KFs, 8,000 points, ~43k edges)
+
+
+def _c5_run(seq, dev):
+    """One rank's config-5 workload: the sequence's first 256 frames in one batch, and the keyframe at
+    frame 255 (kf_every = 256) whose config-4-sized LocalBA runs on the LocalMapping thread once the
+    batch is extracted.  Returns (shard, LocalBA summaries, [(kf, result)])."""
+    import torch
+    from orb_slam2_commit_amd import ORBextractor
+    ex = ORBextractor(GNF, 1.2, 8, 20, 7, device=dev.index)
+    sh = pipeline.SequenceShard(ex, C5_B, GW, GH, KITTI_BF, KITTI_BF / KITTI_FX, dev)
+    imgs = torch.from_numpy(synth.stereo_batch(seq, C5_B)).to(dev)
+    P = _c5_problem(seq)
+    lm = pipeline.LocalMapping({0: P}, dev)
+    n_kf = sh.run_sequence([imgs], lm, kf_every=C5_B)
+    res = lm.finish()
+    lm.close()
+    torch.cuda.synchronize(dev)
+    assert n_kf == 1 and len(res) == 1
+    rec = pipeline.ba_summaries([r for _, r in res], len(P["Tcw"]), n_kf=pipeline.agree_max(len(res)))
+    return sh, rec, res
+
+
+def _c5_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from orb_slam2_commit_amd import dist as odist
+    odist.init("gloo", rank, world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sh, rec, _ = _c5_run(rank, dev)
+    recs, bas = sh.gather(rec)
+    rb = recs.cpu().numpy()
+    q.put((rank, hashlib.sha256(rb.tobytes()).hexdigest(), rb.shape, bas.tobytes()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_config5_rank_workload_full_size(gpu):
+    """Config 5 per rank at full size, two gloo ranks on the one card: each rank extracts + stereo-matches
+    256 distinct KITTI frames (1241x376, 2,000 features) into its record arena while its LocalMapping
+    thread runs a config-4-sized LocalBundleAdjustment (its own handle and stream) for the batch's
+    keyframe; then one all-gather of the records and LocalBA summaries.  Checked: the gathered records
+    and summaries are byte-equal to single-process runs of the same sequences; slots 0, 128 and 255
+    of each sequence are bit-exact against the oracle (keypoints, descriptors, uR, depth); each
+    rank's LocalBA matches the oracle within 1e-4 with identical iterations, trials and outliers."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c5_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    runs = [_c5_run(s, gpu) for s in range(world)]
+    single = np.stack([sh.arena.cpu().numpy() for sh, _, _ in runs])
+    single_ba = np.stack([rec for _, rec, _ in runs])
+    for rank, digest, shape, bb in res:
+        assert tuple(shape) == single.shape
+        assert digest == hashlib.sha256(single.tobytes()).hexdigest()
+        assert bb == single_ba.tobytes()
+    p = oracle.params(GNF, 1.2, 8, 20, 7)
+    lay = runs[0][0].layout
+    for s in range(world):
+        fr = lay.unpack(single[s])
+        imgs = synth.stereo_batch(s, C5_B)
+        for f in C5_SLOTS:
+            oL, oR = oracle.extract(p, imgs[2 * f]), oracle.extract(p, imgs[2 * f + 1])
+            assert fr[f]["kpsL"].tobytes() == oL.keypoints.tobytes(), (s, f)
+            assert fr[f]["descL"].tobytes() == oL.descriptors.tobytes(), (s, f)
+            assert fr[f]["kpsR"].tobytes() == oR.keypoints.tobytes(), (s, f)
+            assert fr[f]["descR"].tobytes() == oR.descriptors.tobytes(), (s, f)
+            ouR, odep = oracle.stereo_match(p, oL, oR, KITTI_BF, KITTI_BF / KITTI_FX)
+            assert fr[f]["uR"].tobytes() == ouR.tobytes(), (s, f)
+            assert fr[f]["depth"].tobytes() == odep.tobytes(), (s, f)
+        r = runs[s][2][0][1]
+        o = oracle.local_ba(_c5_problem(s))
+        assert tuple(r["iterations"]) == tuple(o["iterations"]) and r["trials"] == o["trials"]
+        np.testing.assert_array_equal(r["edge_outlier"], o["edge_outlier"])
+        np.testing.assert_allclose(r["Tcw_d"], o["Tcw_d"], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(r["Xw_d"], o["Xw_d"], atol=1e-4, rtol=0)
+        summ = pipeline.parse_ba_summary(single_ba[s].reshape(1, -1)[0])
+        assert summ["iterations"] == tuple(o["iterations"]) and summ["outliers"] == int(o["edge_outlier"].sum())

@@ -6,7 +6,7 @@
 # Counters run in passes without trace domains (gpurun rule); each pass under its own time limit.
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 OUT=${OUT:-gpurun_out/prof}
-ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --inflight 1 --profile-steps 5 --no-cpu-baseline --ba-calls 0 --pipeline-steps 0 --c3-steps 0 --single-frames 0 --track-steps 0}
+ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --inflight 1 --profile-steps 5 --no-cpu-baseline --ba-calls 0 --pipeline-steps 0 --c3-steps 0 --c1-batch 0 --single-frames 0 --track-steps 0}
 mkdir -p $OUT $OUT/ba
 set -e
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1

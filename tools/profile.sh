@@ -8,7 +8,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 OUT=${OUT:-gpurun_out/prof}
-ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --ba-calls 0 --pipeline-steps 0 --c3-steps 0 --single-frames 0 --track-steps 0}
+ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --ba-calls 0 --pipeline-steps 0 --c3-steps 0 --c1-batch 0 --single-frames 0 --track-steps 0}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 echo "trace ok"
