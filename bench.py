@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--ba-concurrent", type=int, default=8, help="LocalBA problems in flight per GPU for the "
                                                                   "throughput form (<=1: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=4, help="config-5 batches of distinct frames per rank (0: skip)")
+    ap.add_argument("--c5-depth", type=int, default=0, help="config-5 batches queued ahead of the host "
+                                                               "(0: all at once)")
     ap.add_argument("--kf-every", type=int, default=128, help="config-5 keyframe cadence: one keyframe (and its "
                                                                  "LocalBA) every K frames of a sequence (0: none)")
     ap.add_argument("--single-frames", type=int, default=200, help="frames of the single-frame drop-in leg (0: skip)")
@@ -879,13 +881,15 @@ def config5_leg(args, rank, world, dev, odist, exs, batch_images, pairs):
     # the sequence: Tracking (this thread) + LocalMapping (its thread), frames numbered from 0
     sh.frames_done = 0
 
+    depth = args.c5_depth if args.c5_depth > 0 else None
+
     def sequence():
-        n = sh.run_sequence(batches, lm, K)
+        n = sh.run_sequence(batches, lm, K, depth=depth)
         return n, lm.finish()
     t_seq, (n_ins, res) = timed(sequence)
     # the same work apart: extraction alone (the same batches), LocalBA calls alone (one after another)
     sh.frames_done = 0
-    t_ext, _ = timed(lambda: sh.run_sequence(batches))
+    t_ext, _ = timed(lambda: sh.run_sequence(batches, depth=depth))
     t_ba, _ = timed(lambda: [lm.opt.LocalBundleAdjustment(P) for P in probs])
     lm.opt.close()
     rec = pipeline.ba_summaries([r for _, r in res], [len(P["Tcw"]) for P in probs], n_kf=n_kf)
@@ -899,7 +903,7 @@ def config5_leg(args, rank, world, dev, odist, exs, batch_images, pairs):
     frames = B * steps * world
     backend = pipeline._backend() or "none (1 rank)"
     return dict(sequences=world, unique_frames_per_sequence=B * steps, batch_frames=B, batches_in_flight=len(sh.exs),
-                kf_every=K, keyframes_per_sequence=n_ins, localba_calls_per_sequence=len(res),
+                kf_every=K, tracking_depth=depth, keyframes_per_sequence=n_ins, localba_calls_per_sequence=len(res),
                 localba_problem="config-4 sized per keyframe (26 KFs of which 6 fixed, 8,000 points, ~43k edges; "
                                 "seed 7 + 1000*rank + kf)",
                 lm_iterations_per_sequence=its, lm_trials_per_sequence=trials,
@@ -1087,6 +1091,11 @@ def main():
             floor_b = per_frame * B
             stage_hbm["stereo"]["sector_floor_bytes_per_event"] = int(floor_b)
             stage_hbm["stereo"]["traffic_vs_sector_floor"] = round(tr / floor_b, 3) if tr else None
+            # the same floor at the L2's 128-B line granularity (what a miss fetches on gfx950): the SAD
+            # rows' distinct lines + the non-row part of B_st
+            per_frame_l = (fl["floor_bytes_128B_lines"] + fl["B_st_bytes"] - fl["rows_bytes_compact"]) / fl["frames_per_step"]
+            stage_hbm["stereo"]["line_floor_bytes_per_event"] = int(per_frame_l * B)
+            stage_hbm["stereo"]["traffic_vs_line_floor"] = round(tr / (per_frame_l * B), 3) if tr else None
             stage_hbm["stereo"]["sector_floor_source"] = os.path.relpath(args.stereo_floor, ROOT)
         except (OSError, KeyError, ValueError):
             stage_hbm["stereo"]["sector_floor_bytes_per_event"] = None

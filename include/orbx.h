@@ -281,6 +281,11 @@ typedef struct {
 typedef struct orbx_ba orbx_ba;
 /* A solver handle keeps its device buffers and HIP stream across calls. */
 orbx_status orbx_ba_create(int device, orbx_ba** out);
+/* The same with the handle's stream at a HIP stream priority: 0 the default, < 0 higher (clamped to
+ * the device's greatest priority).  LocalMapping's LocalBA (src/LocalMapping.cc:99-101) runs beside
+ * Tracking's extraction on the same GPU: a high-priority stream lets its short, latency-bound trial
+ * kernels take the compute units the extraction launches free up before further extraction blocks. */
+orbx_status orbx_ba_create_priority(int device, int priority, orbx_ba** out);
 orbx_status orbx_ba_destroy(orbx_ba* h);
 /* *stop_flag != 0 (the reference's pbStopFlag / setForceStopFlag) is polled
  * before the run and between LM trials -- by the device itself while the LM

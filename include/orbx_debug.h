@@ -46,8 +46,10 @@ typedef struct {
   int nan_trial;        /* -1 off */
   int raise_stop_after; /* -1 off */
   int trace;            /* one timing line per call on stderr */
-  int split_ctl;        /* 1: a trial's errors and LM verdict as two launches (k_ba_errors +
-                           k_ba_lm_control) instead of k_ba_errors_ctl's one (tests compare them) */
+  int fused_ctl;        /* 1: a trial's errors and LM verdict in ONE launch (k_ba_errors_ctl: the
+                           partials handed to the last block through a release/acquire ticket)
+                           instead of the shipped two (k_ba_errors + k_ba_lm_control); tests
+                           compare them bit for bit */
 } orbx_ba_debug_options;
 /* NULL restores the defaults. */
 int orbx_debug_ba_options(orbx_ba* h, const orbx_ba_debug_options* options);

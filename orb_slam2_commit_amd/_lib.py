@@ -155,7 +155,7 @@ class TrackGather(C.Structure):
 
 class BaDebugOptions(C.Structure):  # include/orbx_debug.h orbx_ba_debug_options
     _fields_ = [("ldlt", C.c_int), ("nan_trial", C.c_int), ("raise_stop_after", C.c_int), ("trace", C.c_int),
-                ("split_ctl", C.c_int)]
+                ("fused_ctl", C.c_int)]
 
 
 class Camera(C.Structure):
@@ -229,6 +229,7 @@ SIGNATURES = {
     "orbx_rand_seed":([C.POINTER(RandState), C.c_uint32], None),
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_ba_create_priority": ([C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "orbx_ba_destroy": ([P], C.c_int),
     "orbx_ba_run": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),
     "orbx_ba_run_bool": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),

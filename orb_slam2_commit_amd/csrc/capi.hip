@@ -208,7 +208,13 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
           c.cap = ((cw + 1) / 2) * ((ch + 1) / 2);
           c.lw = L.w;
           c.loff = (int)L.off;
-          c.cand_off = cand;
+          // inline slots: a level-dependent share of the cap (cells cover more of the scene, and
+          // keep more survivors, at the coarser levels: ~5 at level 0 to ~28 at level 7 on KITTI)
+#if ORBX_CAND_FULL  // A/B only: every slot inline (the pre-round-6 layout)
+          c.kin = (int16_t)c.cap;
+#else
+          c.kin = (int16_t)std::min(c.cap, 4 * (int)std::ceil(2.0 * std::pow(1.25, (double)l)));
+#endif
           cand += c.cap;
           P.cells.push_back(c);
         }
@@ -346,6 +352,18 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
   G.blur_bytes = (blur + 255) & ~255LL;
   G.ncells = (int)P.cells.size();
   G.cand_total = std::max(cand, 1);
+  {  // the cells' inline slots back to back, then their overflow slots (cand_total slots in all)
+    int in_off = 0, ov_off = 0;
+    for (const CellInfo& c : P.cells) in_off += c.kin;
+    const int n_in = in_off;
+    in_off = 0;
+    for (CellInfo& c : P.cells) {
+      c.cand_off = in_off;
+      c.ovf_off = n_in + ov_off;
+      in_off += c.kin;
+      ov_off += c.cap - c.kin;
+    }
+  }
   G.oct_total = oct;
   G.max_kps = oct;
   G.ntiles = ntiles;
@@ -1076,17 +1094,31 @@ extern "C" long long orbx_debug_copy(orbx_extractor* h, int what, int image, int
       src = h->cell_count.p + (size_t)image * G.ncells;
       bytes = sizeof(int) * G.ncells;
       break;
-    case ORBX_DBG_CELL_TABLE:
+    case ORBX_DBG_CELL_TABLE: {  // cand_off: the cell's slot range in ORBX_DBG_CANDIDATES' view
+      int loff = 0;
       for (const CellInfo& c : P.cells) {
-        int v[8] = {c.level, c.x0, c.y0, c.x1, c.y1, c.cand_off, c.cap, 0};
+        int v[8] = {c.level, c.x0, c.y0, c.x1, c.y1, loff, c.cap, 0};
         host.insert(host.end(), v, v + 8);
+        loff += c.cap;
       }
       device_src = false;
       break;
-    case ORBX_DBG_CANDIDATES:
-      src = h->cand.p + (size_t)image * G.cand_total;
-      bytes = sizeof(uint32_t) * G.cand_total;
+    }
+    case ORBX_DBG_CANDIDATES: {  // every cell's slots contiguous (inline then overflow), cells in order
+      std::vector<uint32_t> raw((size_t)G.cand_total);
+      if (hipMemcpy(raw.data(), h->cand.p + (size_t)image * G.cand_total, raw.size() * 4, hipMemcpyDeviceToHost) !=
+          hipSuccess)
+        return ORBX_ERR_HIP;
+      std::vector<uint32_t> logical;
+      logical.reserve(raw.size());
+      for (const CellInfo& c : P.cells)
+        for (int q = 0; q < c.cap; q++) logical.push_back(raw[cell_slot(c, q)]);
+      static_assert(sizeof(uint32_t) == sizeof(int), "host staging is int words");
+      host.resize(logical.size());
+      std::memcpy(host.data(), logical.data(), logical.size() * 4);
+      device_src = false;
       break;
+    }
     case ORBX_DBG_OCT_COUNTS:
       src = h->oct_count.p + (size_t)image * G.nlevels;
       bytes = sizeof(int) * G.nlevels;

@@ -660,6 +660,7 @@ __global__ __launch_bounds__(64) ORBX_FAST_ATTR void k_fast(const Geometry* __re
   CellInfo cn = cells[cell0];
   uint32_t vn[KMAX][4];
   load_window(cn, vn);
+#pragma unroll
   for (int q = 0; q < kFastCPW; q++) {
   const int cell = cell0 + q;
   if (cell >= cend) break;  // wave-uniform
@@ -870,7 +871,12 @@ __global__ __launch_bounds__(64) ORBX_FAST_ATTR void k_fast(const Geometry* __re
   FAST_TS(4);
   const int thr = (cnt > 0 ? ini : mint) + 1;
   // 5. row-major writes at the chosen threshold
-  uint32_t* out = B.cand + (size_t)img * G->cand_total + c.cand_off;
+  // survivor p goes to the cell's inline slot p (p < kin) or overflow slot p - kin (cell_slot)
+  // (as one offset, no select between two pointers: the pointer select made the compiler give up
+  // duplicating the cell loop, +7 % VALU per wave)
+  uint32_t* const out = B.cand + (size_t)img * G->cand_total + c.ovf_off - c.kin;
+  uint32_t* const out_in = B.cand + (size_t)img * G->cand_total + c.cand_off;
+  const int kin = c.kin;
   int pos = 0;
   for (int i0 = 0; i0 < nc; i0 += 64) {
     const int i = i0 + lane;
@@ -886,7 +892,10 @@ __global__ __launch_bounds__(64) ORBX_FAST_ATTR void k_fast(const Geometry* __re
       const int p = pos + lane_rank(m);
       const int y = e / S, x = e - y * S;
       if (p < c.cap)
-        out[p] = ((uint32_t)(smap[e + S + 1] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) | (uint32_t)(c.x0 + x);
+      {
+        const uint32_t v = ((uint32_t)(smap[e + S + 1] - 1) << 24) | ((uint32_t)(c.y0 + y) << 12) | (uint32_t)(c.x0 + x);
+        if (p < kin) out_in[p]= v; else out[p] = v;
+      }
     }
     pos += __popcll(m);
   }
@@ -1102,16 +1111,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // k = cpre[c] + i), four loads in flight at a time
     for (int c = tid; c < ncl; c += NT) {
       const int k0 = s.cpre[c], n = s.cpre[c + 1] - k0;
-      const uint32_t* src = cand + cells[L.cell_begin + c].cand_off;
+      const CellInfo& ci = cells[L.cell_begin + c];
+      const int kin = ci.kin, off = ci.cand_off, ovf = ci.ovf_off - kin;  // slot i: i < kin ? off + i : ovf + i
       int i = 0;
       for (; i + 4 <= n; i += 4) {
-        const uint32_t v0 = src[i], v1 = src[i + 1], v2 = src[i + 2], v3 = src[i + 3];
+        const uint32_t v0 = cand[(i < kin ? off : ovf) + i], v1 = cand[(i + 1 < kin ? off : ovf) + i + 1],
+                       v2 = cand[(i + 2 < kin ? off : ovf) + i + 2], v3 = cand[(i + 3 < kin ? off : ovf) + i + 3];
         put_cand(k0 + i, v0);
         put_cand(k0 + i + 1, v1);
         put_cand(k0 + i + 2, v2);
         put_cand(k0 + i + 3, v3);
       }
-      for (; i < n; i++) put_cand(k0 + i, src[i]);
+      for (; i < n; i++) put_cand(k0 + i, cand[(i < kin ? off : ovf) + i]);
     }
   } else {
     // few cells with many survivors each: one thread per candidate, its cell by binary search
@@ -1121,7 +1132,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void k_
         const int mid = (lo + hi + 1) >> 1;
         if (s.cpre[mid] <= k) lo = mid; else hi = mid - 1;
       }
-      put_cand(k, cand[cells[L.cell_begin + lo].cand_off + (k - s.cpre[lo])]);
+      put_cand(k, cand[cell_slot(cells[L.cell_begin + lo], k - s.cpre[lo])]);
     }
   }
   __syncthreads();

@@ -293,6 +293,12 @@ struct BaDev {
   int camfold;     // device-LM trials: k_ba_pairs' rhs blocks also sum the pose terms (k_ba_cam_sum's
                    // partials) and k_ba_schur_fin does k_ba_cam_fin's Hpp / bp (not launched)
   double* gpart;   // chunk partials of the pose-list gathers (summed by the *_fin kernels)
+  double* gpose;   // posepart: nbf x nposes x kCmc -- per fused block and pose, the pose terms of the
+                   // block's positions on that pose summed in position order (relinearising trials)
+  int posepart;    // relinearising device-LM trials: k_ba_lin_schur writes gpose instead of the
+                   // per-position pose terms, k_ba_pairs' rhs blocks sum gpose over the fused blocks
+  int bdfold;      // device-LM trials of a fused problem: B D^-1 is not stored; k_ba_pairs forms it
+                   // from H_pl and the point's D^-1 (the same expression, the same bits)
   int gsplit;      // chunks per pose list in the gather kernels
   int nbe;         // k_ba_errors blocks; scal[8..] holds its block partials (2 slots), then k_ba_update's
   int nbu;         // k_ba_update blocks (its LM-scale partials)
@@ -935,7 +941,40 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
   // odd), so the LDS and the global pairs are aligned alike
   double cm[kCmc];
   if (L.st) lin_pose_terms<3>(L.T, L.Bm, cm); else lin_pose_terms<2>(L.T, L.Bm, cm);
-  {
+  if (D.posepart && D.fused != 3) {
+    // per pose, the block's positions on it summed in position order (the rhs blocks of k_ba_pairs
+    // then add the fused blocks' sums in block order): one nposes x kCmc record per block instead
+    // of kCmc doubles per position.  Pose c's positions = the set bits of each wave's ballot,
+    // walked in ascending order.
+    double* scm = sbuf;                                             // NT x kCmc
+    uint64_t* pm = reinterpret_cast<uint64_t*>(sbuf + NT * kCmc);   // nposes x (NT / 64) masks
+    const int pc = act ? D.pcam[k] : -1;
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < kCmc; j++) scm[kCmc * t + j] = cm[j];
+    }
+    const int np = D.nposes;
+    for (int c = 0; c < np; c++) {
+      const uint64_t m = __ballot(pc == c);
+      if ((t & 63) == 0) pm[(NT / 64) * c + (t >> 6)] = m;
+    }
+    __syncthreads();
+    double* dst = D.gpose + (size_t)b * np * kCmc;
+    for (int it = t; it < np * kCmc; it += NT) {
+      const int c = it / kCmc, j = it - c * kCmc;
+      double acc = 0.0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; w++) {
+        uint64_t m = pm[(NT / 64) * c + w];
+        while (m) {
+          acc += scm[kCmc * (64 * w + __builtin_ctzll(m)) + j];
+          m &= m - 1;
+        }
+      }
+      dst[it] = acc;
+    }
+    __syncthreads();  // (sbuf / sdi are written again below)
+  } else {
     const int par = (int)((kCmc * (size_t)k0) & 1), n = nk * kCmc;
     double* scm = sbuf + par;
     if (act) {
@@ -991,7 +1030,7 @@ __device__ __forceinline__ void k_ba_lin_schur_body(const BaDev& D) {
     }
   }
   __syncthreads();
-  copy_pairs<NT>(D.BD + 18 * (size_t)k0, sout, nk * 18, t);
+  if (!D.bdfold) copy_pairs<NT>(D.BD + 18 * (size_t)k0, sout, nk * 18, t);
   copy_pairs<NT>(D.cf + 6 * (size_t)k0, sout + 18 * NT, nk * 6, t);
   LS_TS(5);
 }
@@ -1084,6 +1123,25 @@ static int fused_mode(int nbf, int nposes) {
   if (nbf <= 0) return 0;
   return nposes > 0 ? 2 : 1;
 }
+// The device-LM trial copy's fold flags (single and batched drivers alike, so a batched problem
+// keeps its single run's bits): with k_ba_lin_schur doing every trial's point side (fused == 2),
+// B D^-1 is formed inside k_ba_pairs (bdfold) and, where the per-block pose records fit
+// (gpose allocated), the pose terms leave k_ba_lin_schur summed per block and pose (posepart).
+#ifndef ORBX_CTL_ACQREL
+#define ORBX_CTL_ACQREL 0  // A/B only: k_ba_errors_ctl's ticket as acq_rel in every block
+#endif
+#ifndef ORBX_BA_BDFOLD
+#define ORBX_BA_BDFOLD 1
+#endif
+#ifndef ORBX_BA_POSEPART
+#define ORBX_BA_POSEPART 1
+#endif
+constexpr int kPosePartMaxPoses = 256;        // the block's per-pose masks fit k_ba_lin_schur's free LDS
+constexpr size_t kPosePartMaxDoubles = 1 << 22;  // nbf x nposes x kCmc (32 MB)
+__host__ inline void set_trial_folds(BaDev& d) {
+  d.bdfold = (ORBX_BA_BDFOLD && d.fused == 2) ? 1 : 0;
+  d.posepart = (ORBX_BA_POSEPART && d.fused == 2 && d.gpose) ? 1 : 0;
+}
 
 // pose-term chunk partials of a camfold trial, after the pair and rhs partials
 __device__ inline size_t cam_part_off(const BaDev& D) { return ((size_t)D.nblk * 36 + (size_t)D.nposes * 6) * D.gsplit; }
@@ -1107,15 +1165,25 @@ __device__ __forceinline__ void k_ba_pairs_body(const BaDev& D, int gx, int gy) 
     for (int j = 0; j < 27; j++) w[j] = 0;
     int lo, hi;
     chunk_range(D.cam_off[ci], D.cam_off[ci + 1], s, S, lo, hi);
+    const bool camp = cam && !D.posepart;
     for (int t = lo + threadIdx.x; t < hi; t += kPB) {
       const int k = D.cam_pos[t];
       const double* f = D.cf + 6 * (size_t)k;
 #pragma unroll
       for (int r = 0; r < 6; r++) v[r] += f[r];
-      if (cam) {  // k_ba_cam_sum's accumulation (same chunks, same per-thread positions)
+      if (camp) {  // k_ba_cam_sum's accumulation (same chunks, same per-thread positions)
         const double* cm = D.cmc + kCmc * (size_t)k;
 #pragma unroll
         for (int j = 0; j < kCmc; j++) w[j] += cm[j];
+      }
+    }
+    if (cam && D.posepart) {  // the fused blocks' per-pose sums, chunked over the blocks
+      int blo, bhi;
+      chunk_range(0, D.nbf, s, S, blo, bhi);
+      for (int b = blo + threadIdx.x; b < bhi; b += kPB) {
+        const double* g = D.gpose + ((size_t)b * D.nposes + ci) * kCmc;
+#pragma unroll
+        for (int j = 0; j < kCmc; j++) w[j] += g[j];
       }
     }
     const double* tot = block_sum_fixed<6, kPB / 64>(v, red);
@@ -1143,9 +1211,23 @@ __device__ __forceinline__ void k_ba_pairs_body(const BaDev& D, int gx, int gy) 
     if (v < 0) continue;
     const int first = v & ((1 << 30) - 1);
     double A[18];
-    const double* bd = D.BD + 18 * (size_t)k1;
+    if (D.bdfold) {  // B D^-1 = H_pl D^-1 of the point (k_ba_lin_schur's expression, the same bits)
+      const double* B1 = D.Hpl + 18 * (size_t)k1;
+      const double* Di = D.Dinv + 9 * (size_t)D.pos_pt[k1];
+      double h[18], di[9];
 #pragma unroll
-    for (int j = 0; j < 18; j++) A[j] = bd[j];
+      for (int j = 0; j < 18; j++) h[j] = B1[j];
+#pragma unroll
+      for (int j = 0; j < 9; j++) di[j] = Di[j];
+#pragma unroll
+      for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) A[3 * r + c] = h[3 * r] * di[c] + h[3 * r + 1] * di[3 + c] + h[3 * r + 2] * di[6 + c];
+    } else {
+      const double* bd = D.BD + 18 * (size_t)k1;
+#pragma unroll
+      for (int j = 0; j < 18; j++) A[j] = bd[j];
+    }
     pair_acc(acc, A, D.Hpl + 18 * (size_t)first);
     if (v >> 30) {
       const int e = D.pt_off[D.pos_pt[k1] + 1];
@@ -2473,20 +2555,28 @@ __global__ __launch_bounds__(64) void k_ba_lm_resume_many(const BaDev* __restric
 // release, i.e. every partial store happens-before its reads (the block barrier carries that to the
 // rest of the block).  That block runs the verdict (wave 0 works, the other waves only pass the
 // barriers).  Same partials, same order, same arithmetic as the two launches k_ba_errors +
-// k_ba_lm_control, which the debug option split_ctl selects (tests compare the two bit for bit).
+// k_ba_lm_control, which are the default (debug option fused_ctl selects this one; tests compare
+// the two bit for bit): the per-block release costs more than the dispatch it saves.
 __global__ __launch_bounds__(LBS) void k_ba_errors_ctl(BaDev D, DevStop stop) {
   if (!k_ba_errors_body<true>(D, 1, 1)) return;
   __shared__ int last;
   if (threadIdx.x == 0) {
     unsigned* tk = &const_cast<LmState*>(D.lm)->ticket;
+#if ORBX_CTL_ACQREL
     last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(D.nbe - 1);
+#else
+    // release RMW in every block (the RMWs form one release sequence); only the block that reads the
+    // last ticket needs the acquire, as a fence after its RMW (the other blocks skip the L2 invalidate)
+    last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(D.nbe - 1);
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!last) return;  // (uniform per block)
   k_ba_lm_control_body<true>(D, stop);
 }
-// The two-launch form's verdict (debug option split_ctl): after k_ba_errors(D, 1, 1), one wave.
+// The two-launch form's verdict (the default): after k_ba_errors(D, 1, 1), one wave.
 __global__ __launch_bounds__(64) void k_ba_lm_control(BaDev D, DevStop stop) { k_ba_lm_control_body(D, stop); }
 __global__ __launch_bounds__(64) void k_ba_lm_control_many(const BaDev* __restrict__ Ds, DevStop stop) {
   k_ba_lm_control_body(Ds[blockIdx.z], stop);
@@ -2882,7 +2972,7 @@ struct DBuf {
 };
 
 struct Ctx {
-  DBuf<double> cbak, Xbak, eerr, Hpl, ptc, cmc, BD, cf, Hll, bl, Dinv, dmax_p, Hpp, bp, xp, bs, S, Sw, scal, gpart;
+  DBuf<double> cbak, Xbak, eerr, Hpl, ptc, cmc, BD, cf, Hll, bl, Dinv, dmax_p, Hpp, bp, xp, bs, S, Sw, scal, gpart, gpose;
 
   DBuf<int> ptab;
   DBuf<uint8_t> flag;
@@ -3244,12 +3334,19 @@ struct LocalBA {
     D.pblk = nullptr;
     D.fused = 0;  // set on the device-LM copies only
     D.camfold = 0;
+    D.posepart = D.bdfold = 0;
+    D.gpose = nullptr;
     int npb = 0;  // the pblk blocks, run inside the pair-table launch
     if (fuse_ok && na > 0) {
       D.nbf = (na - 1) / kFuseStride + 1;
       BA_CHECK(pblk.alloc((size_t)D.nbf + 1));
       D.pblk = pblk.p;
       npb = npa / LBS + 1;
+      const size_t ng = (size_t)D.nbf * nposes * kCmc;
+      if (nposes > 0 && nposes <= kPosePartMaxPoses && ng <= kPosePartMaxDoubles) {
+        BA_CHECK(c.gpose.alloc(ng));
+        D.gpose = c.gpose.p;
+      }
     }
     static_assert(kPB == LBS, "pblk blocks inside k_ba_pair_table");
     if (D.nblk + npb > 0) hipLaunchKernelGGL(k_ba_pair_table, dim3(D.nblk + npb, gsplit), dim3(kPB), 0, st, D);
@@ -3336,6 +3433,7 @@ struct LocalBA {
     Dg.lm = c.lm.p;
     Dg.fused = fused_mode(D.nbf, D.nposes);
     Dg.camfold = 1;
+    set_trial_folds(Dg);
     int it = 0;
     if (!(stop())) {  // the loop head's first poll (i = 0)
       const bool fused = Dg.nbf > 0;
@@ -3354,7 +3452,10 @@ struct LocalBA {
       hipLaunchKernelGGL(k_ba_lm_start, dim3(1), dim3(1024), 0, st, Dg, iterations);
       BA_CHECK(hipGetLastError());
       const bool psfold = Dg.fused == 2;
-      const bool split_ctl = ba_opts().split_ctl != 0;
+      // a trial's errors and LM verdict: two launches by default.  The one-launch form
+      // (k_ba_errors_ctl, debug option fused_ctl) pays an agent-scope release per block -- an L2
+      // write-back on this multi-XCD part -- and measured 1.5-2.5 % slower per call (profiles/r06)
+      const bool split_ctl = ba_opts().fused_ctl == 0;
       auto trial = [&](bool lin) {
         // linearisation gated on the device: only at the start of a new iteration
         if (fused && (lin || psfold)) hipLaunchKernelGGL(k_ba_lin_schur, dim3(Dg.nbf), dim3(kFuseNT), kFuseSmem, st, Dg);
@@ -3823,6 +3924,7 @@ orbx_status optimize_many(LocalBA* const* Ls, int K, BaBatch& B, int iterations,
     n_ps += B.hostD[i].fused == 2 ? 0 : 1;
     n_psfold += B.hostD[i].fused == 2 ? 1 : 0;
     B.hostD[i].camfold = camfold ? 1 : 0;
+    set_trial_folds(B.hostD[i]);
     B.hostD[i].ldlt_pan = ldlt_use_pan(6 * B.hostD[i].nposes) ? 1 : 0;
     B.hostD[K + i] = Ls[i]->D;
     B.hostD[K + i].lm = nullptr;
@@ -4008,7 +4110,7 @@ struct orbx_ba {
 
 extern "C" {
 
-orbx_status orbx_ba_create(int device, orbx_ba** out) {
+orbx_status orbx_ba_create_priority(int device, int priority, orbx_ba** out) {
   if (!out) return ORBX_ERR_ARG;
   *out = nullptr;
   int n = 0;
@@ -4018,13 +4120,26 @@ orbx_status orbx_ba_create(int device, orbx_ba** out) {
   orbx_ba* h = new (std::nothrow) orbx_ba();
   if (!h) return ORBX_ERR_HIP;
   h->device = device;
-  if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
+  hipError_t e;
+  if (priority == 0) {
+    e = hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking);
+  } else {
+    int least = 0, greatest = 0;
+    e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) {
+      const int p = std::min(std::max(priority, std::min(least, greatest)), std::max(least, greatest));
+      e = hipStreamCreateWithPriority(&h->st, hipStreamNonBlocking, p);
+    }
+  }
+  if (e != hipSuccess) {
     delete h;
     return ORBX_ERR_HIP;
   }
   *out = h;
   return ORBX_OK;
 }
+
+orbx_status orbx_ba_create(int device, orbx_ba** out) { return orbx_ba_create_priority(device, 0, out); }
 
 orbx_status orbx_ba_run_many(orbx_ba* h, int n, const orbx_ba_problem* problems, orbx_ba_result* results,
                              const volatile int* stop_flag) {

@@ -71,14 +71,21 @@ struct Geometry {
 constexpr int kRzTW = 128, kRzTH = 32;  // k_resize output tile
 constexpr int kRzMaxRows = 64;
 
+// A cell's FAST survivors: the first `kin` in its inline slots at cand_off (the cells' inline slots
+// packed back to back, so the octree's per-cell reads share 128-B lines), the rest (up to `cap`) in
+// its overflow slots at ovf_off.  Both offsets are per image within one cand_total block.
 struct CellInfo {
-  int16_t level, pad;
+  int16_t level, kin;
   int16_t x0, y0, x1, y1;  // FAST detection region (inclusive, level coordinates)
   int cand_off, cap;
   int lw, loff;  // the level's width and byte offset in an image's pyramid block (level > 0):
                  // k_fast finds its window from this one record, no dependent geometry load
-  int pad2;
+  int ovf_off;
 };
+// slot p (< cap) of a cell's survivors, relative to the image's candidate block
+__host__ __device__ inline int cell_slot(const CellInfo& c, int p) {
+  return p < c.kin ? c.cand_off + p : c.ovf_off + (p - c.kin);
+}
 
 struct ResizeX {  // horizontal tap of one output column
   int sx0, sx1;

@@ -549,9 +549,11 @@ class Optimizer:
     The solver handle keeps device buffers between calls (the local mapping
     thread runs one LocalBA per new keyframe)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, priority=0):
+        """priority: HIP stream priority of the handle's stream (0 default, < 0 higher; see
+        orbx_ba_create_priority) -- the LocalMapping thread's handle runs high beside extraction."""
         h = C.c_void_p()
-        check(_lib.lib().orbx_ba_create(int(device), C.byref(h)), "orbx_ba_create")
+        check(_lib.lib().orbx_ba_create_priority(int(device), int(priority), C.byref(h)), "orbx_ba_create_priority")
         self._h = h
         self.device = int(device)
         f = C.POINTER(C.c_int)()
@@ -566,7 +568,7 @@ class Optimizer:
 
     def set_debug_options(self, **kw):
         """Test options of this solver handle (include/orbx_debug.h, orbx_ba_debug_options: ldlt,
-        nan_trial, raise_stop_after, trace, split_ctl); no arguments restore the production defaults."""
+        nan_trial, raise_stop_after, trace, fused_ctl); no arguments restore the production defaults."""
         o = _lib.BaDebugOptions(0, -1, -1, 0)
         for k, v in kw.items():
             if k not in dict(o._fields_):

@@ -174,26 +174,32 @@ class SequenceShard:
         self.exs[self.slot].stereo_frames_device(images, v["kps"], v["desc"], v["counts"], self.bf, self.baseline,
                                                  v["uR"], v["depth"], v["nmatch"], stream)
 
-    def run_sequence(self, batches, local_mapping=None, kf_every=0):
+    def run_sequence(self, batches, local_mapping=None, kf_every=0, depth=None):
         """Step the rank's sequence through `batches` in order (frame numbers continue across calls), the
         batches in flight over the shard's slots.  With a LocalMapping thread, frame f is a keyframe when
         (f + 1) % kf_every == 0: it is inserted (keyframe id f // kf_every) together with an event
         recorded after its batch, so its LocalBA starts once that batch's extraction has finished on
-        the device while later batches keep extracting.  Returns the number of keyframes inserted."""
+        the device while later batches keep extracting.  depth: at most this many batches queued on the
+        device ahead of the host (the host waits for batch k - depth before launching batch k, as a
+        tracker that consumes its frames in order would), so earlier keyframes' LocalBA can start while
+        later batches extract; None: every batch launched at once.  Returns the keyframes inserted."""
         import torch
         n_kf = 0
+        done = []
         for k, images in enumerate(batches):
+            if depth is not None and k >= depth:
+                done[k - depth].synchronize()
             self.step(images, slot=k)
+            ev_b = torch.cuda.Event()
+            ev_b.record(self.last_stream)
+            done.append(ev_b)
             nf = int(images.shape[0]) // 2
             f0, self.frames_done = self.frames_done, self.frames_done + nf
             if local_mapping is not None and kf_every > 0:
                 kfs = [f // kf_every for f in range(f0, f0 + nf) if (f + 1) % kf_every == 0]
-                if kfs:
-                    ev = torch.cuda.Event()
-                    ev.record(self.last_stream)
-                    for kf in kfs:
-                        local_mapping.insert_keyframe(kf, ev)
-                    n_kf += len(kfs)
+                for kf in kfs:
+                    local_mapping.insert_keyframe(kf, ev_b)
+                n_kf += len(kfs)
         return n_kf
 
 
@@ -245,11 +251,14 @@ class LocalMapping:
     keyframe arrives so that a real-time tracker never waits; here throughput is measured instead).
     The LocalBA calls release the GIL (ctypes), so the two threads overlap on the host too."""
 
-    def __init__(self, problems, device, optimizer=None):
+    def __init__(self, problems, device, optimizer=None, priority=-1):
+        """priority: the solver handle's HIP stream priority (default high: the LocalBA trial chain is a
+        series of short dependent launches that otherwise queue behind the extraction's blocks)."""
         from .orb import Optimizer
         self.problems = problems  # callable kf -> problem dict, or a sequence indexed by kf
         self.own = optimizer is None
-        self.opt = optimizer if optimizer is not None else Optimizer(device.index if hasattr(device, "index") else int(device))
+        self.opt = optimizer if optimizer is not None else Optimizer(
+            device.index if hasattr(device, "index") else int(device), priority=priority)
         self.q = queue.Queue()
         self.results = []  # (kf, result dict) in insertion order
         self.error = None

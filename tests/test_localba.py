@@ -307,14 +307,14 @@ def test_gpu_reduced_system_ldlt_pan_few_poses(gpu, nposes):
 @pytest.mark.parametrize("case", ["config4", "rejects_a", "rejects_b", "nbad_stop", "nan_trial"])
 def test_gpu_localba_errors_ctl_equals_two_launches(ba, case):
     """k_ba_errors_ctl (a trial's errors and the LM verdict in one launch, the partials handed to the
-    last block through an agent-scope acq_rel ticket) against the two-launch form k_ba_errors +
-    k_ba_lm_control (debug option split_ctl): bit for bit, with identical iterations, trials, chi2
-    and outliers, on config 4, the rejection / _nBad problems and a NaN-rho trial."""
+    last block through an agent-scope release/acquire ticket; debug option fused_ctl) against the
+    shipped two-launch form k_ba_errors + k_ba_lm_control: bit for bit, with identical iterations,
+    trials, chi2 and outliers, on config 4, the rejection / _nBad problems and a NaN-rho trial."""
     P = synth.localba_problem(seed=7) if case in ("config4", "nan_trial") else reject_problem(case)
     kw = dict(nan_trial=1) if case == "nan_trial" else {}
     with ba.debug_options(**kw):
         a = ba.LocalBundleAdjustment(P)
-    with ba.debug_options(split_ctl=1, **kw):
+    with ba.debug_options(fused_ctl=1, **kw):
         b = ba.LocalBundleAdjustment(P)
     for k in ("Tcw", "Xw", "Tcw_d", "Xw_d", "edge_outlier"):
         np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]))

@@ -12,6 +12,11 @@ from orb_slam2_commit_amd import Optimizer, synth  # noqa: E402
 def main(reps=10):
     P = synth.localba_problem(seed=7)
     o = Optimizer(0)
+    # A/B hook (tools only): ORBX_TOOL_BA_OPTS="split_ctl=1,..." -> orbx_ba_debug_options of the handle
+    import os
+    opts = os.environ.get("ORBX_TOOL_BA_OPTS")
+    if opts:
+        o.set_debug_options(**{k: int(v) for k, v in (kv.split("=") for kv in opts.split(","))})
     r = o.LocalBundleAdjustment(P)  # warm-up (allocations, code load)
     ts = []
     t0 = time.perf_counter()
