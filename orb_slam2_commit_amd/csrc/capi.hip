@@ -210,11 +210,7 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
           c.loff = (int)L.off;
           // inline slots: a level-dependent share of the cap (cells cover more of the scene, and
           // keep more survivors, at the coarser levels: ~5 at level 0 to ~28 at level 7 on KITTI)
-#if ORBX_CAND_FULL  // A/B only: every slot inline (the pre-round-6 layout)
-          c.kin = (int16_t)c.cap;
-#else
           c.kin = (int16_t)std::min(c.cap, 4 * (int)std::ceil(2.0 * std::pow(1.25, (double)l)));
-#endif
           cand += c.cap;
           P.cells.push_back(c);
         }

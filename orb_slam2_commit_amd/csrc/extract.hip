@@ -613,13 +613,8 @@ __device__ unsigned int* fast_probe_buf;
 #define ORBX_FAST_CPW 2
 #endif
 constexpr int kFastCPW = ORBX_FAST_CPW;  // FAST cells per wave
-#ifdef ORBX_FAST_VSLIDE
-#define ORBX_FAST_ATTR __attribute__((amdgpu_waves_per_eu(8)))  // 64 VGPRs: 8 one-wave blocks per SIMD
-#else
-#define ORBX_FAST_ATTR
-#endif
 template <int S, int RP>
-__global__ __launch_bounds__(64) ORBX_FAST_ATTR void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
+__global__ __launch_bounds__(64) void k_fast(const Geometry* __restrict__ G, const CellInfo* __restrict__ cells,
                                              BatchPtrs B, int grp) {
   // dynamic LDS sized by the launch group's largest cell (G->fg[grp])
   extern __shared__ __align__(16) uint8_t fast_smem[];
@@ -708,75 +703,6 @@ __global__ __launch_bounds__(64) ORBX_FAST_ATTR void k_fast(const Geometry* __re
   // rewrites the same values).  Returns the corner count.
   auto detect = [&](int th) -> int {
     int n = 0;
-#ifdef ORBX_FAST_VSLIDE
-    // Each lane walks its column down the rows (RP == 2: lanes 0-31 the rows [0, Hh), lanes 32-63
-    // [Hh, H)), keeping the last six pixels of column x+3 in registers: per row only c0 (row y+6),
-    // c4 and c12 (row y+3) are read, cv and c8 are c0 of three and six rows earlier (3 LDS reads
-    // per pixel instead of 5).  The two halves compact into separate list regions (top at 0,
-    // bottom at Hh W), so each stays row-major; the bottom region then moves down behind the top.
-    {
-      const int Hh = RP == 2 ? (H + 1) >> 1 : H;
-      const int ys = RP == 2 ? ly * Hh : 0, ye = RP == 2 ? (ly ? H : Hh) : H;
-      const int BOFF = RP == 2 ? Hh * W : 0;
-      const uint8_t* colp = tile + ys * S + lx + 3;
-      int R[6];
-#pragma unroll
-      for (int j = 0; j < 6; j++) R[j] = colp[j * S];
-      int ntop = 0, nbot = 0;
-      for (int s0 = 0; s0 < Hh; s0 += 6) {
-        // each three rows' nine reads first (in flight together before the first use; six rows'
-        // eighteen would cost the 64-VGPR budget of eight waves per SIMD)
-        int C0[6], C4[6], C12[6];
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-          if (j % 3 == 0) {
-#pragma unroll
-            for (int q = j; q < j + 3; q++) {
-              const uint8_t* t = tile + (ys + s0 + q) * S + lx;
-              C0[q] = t[6 * S + 3];
-              C4[q] = t[3 * S + 6];
-              C12[q] = t[3 * S];
-            }
-          }
-          const int y = ys + s0 + j;
-          const int c0 = C0[j], c4 = C4[j], c12 = C12[j];
-          const int c8 = R[j], cv = R[(j + 3) % 6];
-          R[j] = c0;
-          const int hi = min(max(c0, c8), max(c4, c12));
-          const int lo = max(min(c0, c8), min(c4, c12));
-          const int v = max(hi - cv, cv - lo) - (th + 1);  // >= 0 <=> compass hit
-          const bool hit = (~v & cw & (y - ye)) < 0;
-          const uint64_t m = __ballot(hit);
-          const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);
-          // rank among all lanes; the upper half's base drops the lower half's count
-          const int base = RP == 2 ? (ly ? BOFF + nbot - __popc(mlo) : ntop) : ntop;
-          if (hit) list[base + lane_rank(m)] = (uint16_t)(y * S + lx);
-          if constexpr (RP == 2) {
-            ntop += __popc(mlo);
-            nbot += __popc(mhi);
-          } else {
-            ntop += __popcll(m);
-          }
-        }
-      }
-      if constexpr (RP == 2) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // bottom region [BOFF, BOFF + nbot) -> [ntop, ntop + nbot): a chunk's writes stay below the
-        // next chunk's sources (ntop <= BOFF), and each chunk is read before it is written
-        for (int i0 = 0; i0 < nbot; i0 += 64) {
-          const int i = i0 + lane;
-          const uint16_t e = i < nbot ? list[BOFF + i] : (uint16_t)0;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (i < nbot) list[ntop + i] = e;
-        }
-      }
-      n = ntop + nbot;
-    }
-#else
     for (int y0r = 0; y0r < H; y0r += QU * RP) {
       const int eb = (y0r + ly) * S + lx;
       int cv[QU], c0[QU], c4[QU], c8[QU], c12[QU];
@@ -804,7 +730,6 @@ __global__ __launch_bounds__(64) ORBX_FAST_ATTR void k_fast(const Geometry* __re
         n += __popcll(m);
       }
     }
-#endif
     __syncthreads();
 #ifdef ORBX_FAST_PROBE
     if (th == ini) ts_mid = __builtin_amdgcn_s_memtime(), n_compass = n;

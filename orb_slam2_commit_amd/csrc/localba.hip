@@ -1127,9 +1127,6 @@ static int fused_mode(int nbf, int nposes) {
 // keeps its single run's bits): with k_ba_lin_schur doing every trial's point side (fused == 2),
 // B D^-1 is formed inside k_ba_pairs (bdfold) and, where the per-block pose records fit
 // (gpose allocated), the pose terms leave k_ba_lin_schur summed per block and pose (posepart).
-#ifndef ORBX_CTL_ACQREL
-#define ORBX_CTL_ACQREL 0  // A/B only: k_ba_errors_ctl's ticket as acq_rel in every block
-#endif
 #ifndef ORBX_BA_BDFOLD
 #define ORBX_BA_BDFOLD 1
 #endif
@@ -2562,14 +2559,10 @@ __global__ __launch_bounds__(LBS) void k_ba_errors_ctl(BaDev D, DevStop stop) {
   __shared__ int last;
   if (threadIdx.x == 0) {
     unsigned* tk = &const_cast<LmState*>(D.lm)->ticket;
-#if ORBX_CTL_ACQREL
-    last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(D.nbe - 1);
-#else
     // release RMW in every block (the RMWs form one release sequence); only the block that reads the
     // last ticket needs the acquire, as a fence after its RMW (the other blocks skip the L2 invalidate)
     last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(D.nbe - 1);
     if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
