@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--ba-concurrent", type=int, default=8, help="LocalBA problems in flight per GPU for the "
                                                                   "throughput form (<=1: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=4, help="config-5 batches of distinct frames per rank (0: skip)")
+    ap.add_argument("--c5-ba-cus", type=int, default=0, help="config 5: CUs reserved for LocalMapping's LocalBA "
+                                                                 "stream, the rest for extraction (0: shared)")
+    ap.add_argument("--c5-cu-layout", default="contiguous", choices=["contiguous", "strided"])
     ap.add_argument("--c5-depth", type=int, default=0, help="config-5 batches queued ahead of the host "
                                                                "(0: all at once)")
     ap.add_argument("--kf-every", type=int, default=128, help="config-5 keyframe cadence: one keyframe (and its "
@@ -80,13 +83,13 @@ def parse():
     ap.add_argument("--c1-seconds", type=float, default=6.0, help="config-1 CPU reference sample length")
     ap.add_argument("--c3-steps", type=int, default=3, help="config-3 (EuRoC + PnP RANSAC) steps per rank (0: skip)")
     ap.add_argument("--c3-batch", type=int, default=128, help="config-3 frames (sequences) per step per GPU")
-    ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r05_sq_counters.json"),
+    ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r06_sq_counters.json"),
                     help="SQ counter summary (tools/pmc_kernel.sh + tools/sq_summary.py) for issue fractions")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/profile.sh + tools/parse_prof.py); null if absent")
-    ap.add_argument("--rocprof", default=os.path.join(ROOT, "profiles", "r05_rocprof_stages.json"),
+    ap.add_argument("--rocprof", default=os.path.join(ROOT, "profiles", "r06_rocprof_stages.json"),
                     help="per-stage kernel time per step from rocprofv3 --stats (tools/rocprof_stages.py)")
-    ap.add_argument("--ba-traffic", default=os.path.join(ROOT, "profiles", "r05_localba_traffic.json"),
+    ap.add_argument("--ba-traffic", default=os.path.join(ROOT, "profiles", "r06_localba_traffic.json"),
                     help="LocalBA PMC bytes per LM iteration (tools/ba_traffic.py); null if absent")
     ap.add_argument("--stereo-floor", default=os.path.join(ROOT, "profiles", "r05_stereo_floor.json"),
                     help="measured sector floor of the stereo stage (tools/stereo_floor.py); null if absent")
@@ -861,8 +864,14 @@ def config5_leg(args, rank, world, dev, odist, exs, batch_images, pairs):
     n_kf_rank = (steps * B) // K if K > 0 else 0
     n_kf = pipeline.agree_max(n_kf_rank)
     probs = [synth.localba_problem(seed=7 + 1000 * rank + kf) for kf in range(n_kf_rank)]
-    sh = pipeline.SequenceShard(exs[0], B, W, H, KITTI["bf"], KITTI["bf"] / KITTI["fx"], dev, extractors=exs[1:])
-    lm = pipeline.LocalMapping(probs, dev)
+    ms, ba_mask = None, None
+    if args.c5_ba_cus > 0:  # LocalMapping and Tracking on disjoint CU sets
+        n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        ba_mask, ex_mask = pipeline.cu_partition(n_cus, args.c5_ba_cus, args.c5_cu_layout)
+        ms = pipeline.CUMaskedStreams(dev, len(exs), ex_mask)
+    sh = pipeline.SequenceShard(exs[0], B, W, H, KITTI["bf"], KITTI["bf"] / KITTI["fx"], dev, extractors=exs[1:],
+                                streams=ms.streams if ms else None)
+    lm = pipeline.LocalMapping(probs, dev, cu_mask=ba_mask)
     # warm-up: the shard's arenas and the LocalMapping handle (one LocalBA on a keyframe problem)
     sh.run_sequence(batches[:len(sh.exs)])
     if probs:
@@ -892,10 +901,16 @@ def config5_leg(args, rank, world, dev, odist, exs, batch_images, pairs):
     t_ext, _ = timed(lambda: sh.run_sequence(batches, depth=depth))
     t_ba, _ = timed(lambda: [lm.opt.LocalBundleAdjustment(P) for P in probs])
     lm.opt.close()
+    cu_split = None
+    if ms is not None:
+        cu_split = dict(localba_cus=args.c5_ba_cus, layout=args.c5_cu_layout)
     rec = pipeline.ba_summaries([r for _, r in res], [len(P["Tcw"]) for P in probs], n_kf=n_kf)
     t_gather, (recs, bas) = timed(lambda: sh.gather(rec))
     own_ok = bool(torch.equal(recs[rank].to(sh.arena.device), sh.arena)) and bool(np.array_equal(bas[rank], rec))
     ok_all = odist.sum_over_ranks(1.0 if own_ok else 0.0, dev) == world
+    if ms is not None:
+        torch.cuda.synchronize(dev)
+        ms.close()
     its = sum(sum(r["iterations"]) for _, r in res)
     trials = sum(r["trials"] for _, r in res)
     its_all = odist.sum_over_ranks(float(its), dev)
@@ -903,7 +918,7 @@ def config5_leg(args, rank, world, dev, odist, exs, batch_images, pairs):
     frames = B * steps * world
     backend = pipeline._backend() or "none (1 rank)"
     return dict(sequences=world, unique_frames_per_sequence=B * steps, batch_frames=B, batches_in_flight=len(sh.exs),
-                kf_every=K, tracking_depth=depth, keyframes_per_sequence=n_ins, localba_calls_per_sequence=len(res),
+                kf_every=K, tracking_depth=depth, cu_split=cu_split, keyframes_per_sequence=n_ins, localba_calls_per_sequence=len(res),
                 localba_problem="config-4 sized per keyframe (26 KFs of which 6 fixed, 8,000 points, ~43k edges; "
                                 "seed 7 + 1000*rank + kf)",
                 lm_iterations_per_sequence=its, lm_trials_per_sequence=trials,
