@@ -286,6 +286,15 @@ orbx_status orbx_ba_create(int device, orbx_ba** out);
  * Tracking's extraction on the same GPU: a high-priority stream lets its short, latency-bound trial
  * kernels take the compute units the extraction launches free up before further extraction blocks. */
 orbx_status orbx_ba_create_priority(int device, int priority, orbx_ba** out);
+/* The same with the handle's stream restricted to a set of compute units (cu_mask: cu_mask_words
+ * 32-bit words, bit i = CU i as the HIP runtime numbers them; NULL or 0 words = all CUs): a
+ * LocalMapping handle and the Tracking extraction streams (orbx_stream_create below) can take
+ * disjoint CU sets, so neither waits for units the other holds. */
+orbx_status orbx_ba_create_masked(int device, const uint32_t* cu_mask, int cu_mask_words, orbx_ba** out);
+/* A HIP stream of `device` restricted to a CU set (as above), for the *_device entry points' stream
+ * arguments; orbx_stream_destroy synchronises and releases it. */
+orbx_status orbx_stream_create(int device, const uint32_t* cu_mask, int cu_mask_words, void** stream);
+void orbx_stream_destroy(void* stream);
 orbx_status orbx_ba_destroy(orbx_ba* h);
 /* *stop_flag != 0 (the reference's pbStopFlag / setForceStopFlag) is polled
  * before the run and between LM trials -- by the device itself while the LM

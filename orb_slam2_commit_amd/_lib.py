@@ -230,6 +230,9 @@ SIGNATURES = {
     "orbx_rand_next": ([C.POINTER(RandState)], C.c_int32),
     "orbx_ba_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "orbx_ba_create_priority": ([C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_ba_create_masked": ([C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_stream_create": ([C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "orbx_stream_destroy": ([C.c_void_p], None),
     "orbx_ba_destroy": ([P], C.c_int),
     "orbx_ba_run": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),
     "orbx_ba_run_bool": ([P, C.POINTER(BaProblem), C.POINTER(BaResult), P], C.c_int),

@@ -27,6 +27,7 @@
 // partials and a relaxed ticket, not an agent-scope release/acquire (per block
 // that costs an L2 writeback/invalidate on the multi-XCD part).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <chrono>
@@ -4133,6 +4134,44 @@ orbx_status orbx_ba_create_priority(int device, int priority, orbx_ba** out) {
 }
 
 orbx_status orbx_ba_create(int device, orbx_ba** out) { return orbx_ba_create_priority(device, 0, out); }
+
+orbx_status orbx_stream_create(int device, const uint32_t* cu_mask, int cu_mask_words, void** stream) {
+  if (!stream || cu_mask_words < 0 || (cu_mask_words > 0 && !cu_mask)) return ORBX_ERR_ARG;
+  *stream = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ORBX_ERR_NODEV;
+  if (device < 0 || device >= n) return ORBX_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return ORBX_ERR_HIP;
+  hipStream_t st = nullptr;
+  const hipError_t e = cu_mask_words > 0 ? hipExtStreamCreateWithCUMask(&st, (uint32_t)cu_mask_words, cu_mask)
+                                         : hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  *stream = (void*)st;
+  return ORBX_OK;
+}
+
+void orbx_stream_destroy(void* stream) {
+  if (!stream) return;
+  (void)hipStreamSynchronize((hipStream_t)stream);
+  (void)hipStreamDestroy((hipStream_t)stream);
+}
+
+orbx_status orbx_ba_create_masked(int device, const uint32_t* cu_mask, int cu_mask_words, orbx_ba** out) {
+  if (!out) return ORBX_ERR_ARG;
+  *out = nullptr;
+  void* st = nullptr;
+  const orbx_status s = orbx_stream_create(device, cu_mask, cu_mask_words, &st);
+  if (s != ORBX_OK) return s;
+  orbx_ba* h = new (std::nothrow) orbx_ba();
+  if (!h) {
+    orbx_stream_destroy(st);
+    return ORBX_ERR_HIP;
+  }
+  h->device = device;
+  h->st = (hipStream_t)st;
+  *out = h;
+  return ORBX_OK;
+}
 
 orbx_status orbx_ba_run_many(orbx_ba* h, int n, const orbx_ba_problem* problems, orbx_ba_result* results,
                              const volatile int* stop_flag) {

@@ -549,11 +549,17 @@ class Optimizer:
     The solver handle keeps device buffers between calls (the local mapping
     thread runs one LocalBA per new keyframe)."""
 
-    def __init__(self, device=0, priority=0):
+    def __init__(self, device=0, priority=0, cu_mask=None):
         """priority: HIP stream priority of the handle's stream (0 default, < 0 higher; see
-        orbx_ba_create_priority) -- the LocalMapping thread's handle runs high beside extraction."""
+        orbx_ba_create_priority) -- the LocalMapping thread's handle runs high beside extraction.
+        cu_mask: optional sequence of 32-bit words restricting the handle's stream to a CU set
+        (orbx_ba_create_masked; the priority is then the default)."""
         h = C.c_void_p()
-        check(_lib.lib().orbx_ba_create_priority(int(device), int(priority), C.byref(h)), "orbx_ba_create_priority")
+        if cu_mask is not None:
+            m = np.ascontiguousarray(cu_mask, np.uint32)
+            check(_lib.lib().orbx_ba_create_masked(int(device), ptr(m), len(m), C.byref(h)), "orbx_ba_create_masked")
+        else:
+            check(_lib.lib().orbx_ba_create_priority(int(device), int(priority), C.byref(h)), "orbx_ba_create_priority")
         self._h = h
         self.device = int(device)
         f = C.POINTER(C.c_int)()

@@ -132,17 +132,20 @@ class SequenceShard:
     layout (frames per batch, keypoint capacity) is the maximum over the ranks, so every rank's arena
     has the same size for the all-gather whatever its sequence's image size."""
 
-    def __init__(self, extractor, n_frames, width, height, bf, baseline, device, extractors=None):
+    def __init__(self, extractor, n_frames, width, height, bf, baseline, device, extractors=None, streams=None):
         """extractors: optional further extractor handles (each with its own record arena and HIP
         stream) so that consecutive batches of the sequence are in flight together; batch k runs on
-        slot k % S and writes arena k % S.  `arena` is the arena of the last batch stepped."""
+        slot k % S and writes arena k % S.  `arena` is the arena of the last batch stepped.
+        streams: the slots' torch streams (e.g. CUMaskedStreams' ExternalStreams); default: new ones."""
         import torch
         self.exs = [extractor] + list(extractors or [])
         self.ex = extractor
         self.layout = FrameRecords(agree_max(n_frames), agree_max(extractor.max_keypoints(width, height)))
         self.arenas = [new_arena(self.layout, device) for _ in self.exs]
         self.views_ = [self.layout.views(a) for a in self.arenas]
-        self.streams = [torch.cuda.Stream(device) for _ in self.exs]
+        self.streams = list(streams) if streams is not None else [torch.cuda.Stream(device) for _ in self.exs]
+        if len(self.streams) < len(self.exs):
+            raise ValueError("SequenceShard: %d streams for %d extractor slots" % (len(self.streams), len(self.exs)))
         self.bf, self.baseline = float(bf), float(baseline)
         self.stream = self.streams[0]
         self.slot = 0
@@ -251,14 +254,15 @@ class LocalMapping:
     keyframe arrives so that a real-time tracker never waits; here throughput is measured instead).
     The LocalBA calls release the GIL (ctypes), so the two threads overlap on the host too."""
 
-    def __init__(self, problems, device, optimizer=None, priority=-1):
+    def __init__(self, problems, device, optimizer=None, priority=-1, cu_mask=None):
         """priority: the solver handle's HIP stream priority (default high: the LocalBA trial chain is a
-        series of short dependent launches that otherwise queue behind the extraction's blocks)."""
+        series of short dependent launches that otherwise queue behind the extraction's blocks).
+        cu_mask: restrict the handle's stream to a CU set instead (see cu_partition)."""
         from .orb import Optimizer
         self.problems = problems  # callable kf -> problem dict, or a sequence indexed by kf
         self.own = optimizer is None
         self.opt = optimizer if optimizer is not None else Optimizer(
-            device.index if hasattr(device, "index") else int(device), priority=priority)
+            device.index if hasattr(device, "index") else int(device), priority=priority, cu_mask=cu_mask)
         self.q = queue.Queue()
         self.results = []  # (kf, result dict) in insertion order
         self.error = None
@@ -297,6 +301,50 @@ class LocalMapping:
             self.finish()
         if self.own:
             self.opt.close()
+
+
+def cu_partition(n_cus, n_ba, layout="contiguous"):
+    """Two disjoint CU masks (lists of 32-bit words) over n_cus compute units: n_ba for LocalMapping's
+    LocalBA stream, the rest for Tracking's extraction streams.  layout "contiguous": CUs 0..n_ba-1;
+    "strided": every (n_cus // n_ba)-th CU (spread over the shader engines / XCDs)."""
+    if not 0 < n_ba < n_cus:
+        raise ValueError("cu_partition: need 0 < n_ba < n_cus (%d, %d)" % (n_ba, n_cus))
+    if layout == "contiguous":
+        ba = set(range(n_ba))
+    elif layout == "strided":
+        step = n_cus // n_ba
+        ba = set(range(0, step * n_ba, step))
+    else:
+        raise ValueError("cu_partition: layout %r" % layout)
+    words = (n_cus + 31) // 32
+    m_ba, m_ex = [0] * words, [0] * words
+    for c in range(n_cus):
+        (m_ba if c in ba else m_ex)[c >> 5] |= 1 << (c & 31)
+    return m_ba, m_ex
+
+
+class CUMaskedStreams:
+    """n HIP streams restricted to one CU set (orbx_stream_create), wrapped as torch ExternalStreams."""
+
+    def __init__(self, device, n, cu_mask):
+        import ctypes as C
+        import torch
+        from . import _lib
+        m = np.ascontiguousarray(cu_mask, np.uint32)
+        self._raw = []
+        self.streams = []
+        dev = device.index if hasattr(device, "index") else int(device)
+        for _ in range(n):
+            h = C.c_void_p()
+            _lib.check(_lib.lib().orbx_stream_create(dev, _lib.ptr(m), len(m), C.byref(h)), "orbx_stream_create")
+            self._raw.append(h)
+            self.streams.append(torch.cuda.ExternalStream(h.value, device=torch.device("cuda", dev)))
+
+    def close(self):
+        from . import _lib
+        for h in self._raw:
+            _lib.lib().orbx_stream_destroy(h)
+        self._raw, self.streams = [], []
 
 
 def ba_summaries(results, n_cams, n_kf=None, max_cams=MAX_BA_CAMS):

@@ -210,6 +210,18 @@ def test_local_mapping_thread_runs_every_keyframe_in_order():
         bad.finish()
 
 
+def test_cu_partition_masks_are_disjoint_and_cover():
+    for n_cus, n_ba, layout in ((256, 64, "contiguous"), (256, 32, "strided"), (304, 48, "strided"), (80, 1, "contiguous")):
+        ba, ex = pipeline.cu_partition(n_cus, n_ba, layout)
+        bits = lambda m: {32 * w + b for w, v in enumerate(m) for b in range(32) if v >> b & 1}
+        A, E = bits(ba), bits(ex)
+        assert len(A) == n_ba and not (A & E) and A | E == set(range(n_cus))
+    with pytest.raises(ValueError):
+        pipeline.cu_partition(256, 0)
+    with pytest.raises(ValueError):
+        pipeline.cu_partition(256, 64, "diagonal")
+
+
 def test_ba_summary_roundtrip():
     P = _ba_problem(3)
     r = oracle.local_ba(P)
