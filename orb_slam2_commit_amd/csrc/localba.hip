@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
 #include <memory>
@@ -319,6 +320,13 @@ struct BaDev {
 __device__ inline bool lm_skip(const BaDev& D) { return D.lm && D.lm->done; }
 __device__ inline bool lm_skip_lin(const BaDev& D) { return D.lm && (D.lm->done || !D.lm->relin); }
 __device__ inline double lm_lambda(const BaDev& D, double lambda) { return D.lm ? D.lm->lambda : lambda; }
+// The phase-2 launches queued speculatively behind phase 1's last trials (k_ba_outliers and the
+// structure kernels with D.lm set): they run only if phase 1 has ended on an accepted state -- done,
+// no refresh pending, no rejected trial still to pop -- which the host then reads back with phase
+// 1's state; otherwise they return at once and the host queues them again after its pop.
+__device__ inline bool spec_skip(const BaDev& D) {
+  return D.lm && !(D.lm->done && !D.lm->refresh && !D.lm->rejected);
+}
 
 // Cross-lane exchange with the partner lane for butterfly level O: xor 32 via
 // ds_bpermute, xor 16 via ds_swizzle, and the in-row levels through DPP (no
@@ -2685,6 +2693,7 @@ struct BaMin {
 
 __global__ __launch_bounds__(kTileT) void k_ba_struct_count(BaDev D, const uint8_t* __restrict__ flag, int lvl,
                                                             int* __restrict__ tcnt, int4* __restrict__ ttot) {
+  if (spec_skip(D)) return;  // (block-uniform, before any barrier)
   constexpr int V = kStructV;
   extern __shared__ int sm_sc[];
   const int nc = D.nc, t = threadIdx.x, tile = blockIdx.x;
@@ -2724,6 +2733,7 @@ __global__ __launch_bounds__(kTileT) void k_ba_struct_count(BaDev D, const uint8
 __global__ __launch_bounds__(kStructNT) void k_ba_struct_scan(BaDev D, const uint8_t* __restrict__ fixed, int ntiles,
                                                               int* __restrict__ tcnt, const int4* __restrict__ ttot,
                                                               int4* __restrict__ tcar, int* __restrict__ out) {
+  if (spec_skip(D)) return;
   constexpr int NT = kStructNT;
   extern __shared__ int sm_ss[];
   const int nc = D.nc, t = threadIdx.x;
@@ -2786,6 +2796,7 @@ __global__ __launch_bounds__(kStructNT) void k_ba_struct_scan(BaDev D, const uin
 __global__ __launch_bounds__(kTileT) void k_ba_struct_fill(BaDev D, const uint8_t* __restrict__ flag, int lvl,
                                                            const int* __restrict__ tcnt,
                                                            const int4* __restrict__ tcar) {
+  if (spec_skip(D)) return;
   constexpr int V = kStructV, NW = kTileT / 64;
   extern __shared__ int sm_sf[];
   const int nc = D.nc, t = threadIdx.x, lane = t & 63, w = t >> 6, tile = blockIdx.x;
@@ -2900,6 +2911,7 @@ __global__ __launch_bounds__(LBS) void k_ba_prep(int ne, int np, const float* __
 // phase transition (:764-802) and the final erase test (:817-847): per edge
 // chi2 of its stored error against th, and depth of the current estimate
 __global__ __launch_bounds__(LBS) void k_ba_outliers(BaDev D, uint8_t* flag, int drop_kernel) {
+  if (spec_skip(D)) return;
   const int e = blockIdx.x * LBS + threadIdx.x;
   if (e >= D.ne) return;
   const int c = D.ecam[e], p = D.ept[e];
@@ -2974,6 +2986,11 @@ struct Ctx {
   DBuf<uint8_t> prob;  // k_ba_prep outputs: FP64 points and edge arrays
 };
 
+#define HIP_TRY(x)                      \
+  do {                                  \
+    const hipError_t e_ = (x);          \
+    if (e_ != hipSuccess) return e_;    \
+  } while (0)
 #define BA_CHECK(x)                          \
   do {                                       \
     if ((x) != hipSuccess) return ORBX_ERR_HIP; \
@@ -3231,13 +3248,27 @@ struct LocalBA {
   // sizes are known: phase 1, every edge active).
   orbx_status build_structure_dev(int lvl, hipStream_t st, const int* known) {
     const auto T0 = std::chrono::steady_clock::now();
+    BA_CHECK(launch_structure_dev(lvl, st, known, nullptr));
+    const int* sz = known;
+    if (!sz) {
+      BA_CHECK(hipStreamSynchronize(st));
+      sz = sint_host;
+    }
+    const orbx_status fs = finish_structure(sz[0], sz[1], sz[2], sz[3], sz[4], st);
+    t_struct[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
+    return fs;
+  }
+  // The structure kernels alone (sizes to the mapped sint_host unless known); gate: the device LM
+  // state that gates them (spec_skip), or null.  The host reads the sizes after the stream's next
+  // synchronisation point and calls finish_structure.
+  hipError_t launch_structure_dev(int lvl, hipStream_t st, const int* known, const LmState* gate) {
     const int nc = D.nc, ne = D.ne;
     const int ntiles = (ne + kTileE - 1) / kTileE;
     const size_t nb = (size_t)nc * (nc + 1) / 2 + 1;
-    BA_CHECK(sbuf.alloc(8 * (size_t)ntiles + (size_t)ntiles * nc + 6 * (size_t)ne + 1 + 3 * (size_t)nc + 1 + nb + 8));
+    HIP_TRY(sbuf.alloc(8 * (size_t)ntiles + (size_t)ntiles * nc + 6 * (size_t)ne + 1 + 3 * (size_t)nc + 1 + nb + 8));
     if (!sint_host) {
-      BA_CHECK(hipHostMalloc((void**)&sint_host, 8 * sizeof(int), hipHostMallocMapped));
-      BA_CHECK(hipHostGetDevicePointer((void**)&sint_map, sint_host, 0));
+      HIP_TRY(hipHostMalloc((void**)&sint_host, 8 * sizeof(int), hipHostMallocMapped));
+      HIP_TRY(hipHostGetDevicePointer((void**)&sint_map, sint_host, 0));
     }
     int* p = sbuf.p;
     int4* ttot = reinterpret_cast<int4*>(p);  // first: 16-byte aligned
@@ -3257,24 +3288,18 @@ struct LocalBA {
     D.cam_off = p, p += nc + 1;
     D.boff = p, p += nb;
     const uint8_t* fl = lvl < 0 ? nullptr : (const uint8_t*)c.flag.p;
+    BaDev Ds = D;
+    Ds.lm = gate;
     if (ntiles > 0)
-      hipLaunchKernelGGL(k_ba_struct_count, dim3(ntiles), dim3(kTileT), sizeof(int) * (nc + kTileT / 64), st, D, fl,
+      hipLaunchKernelGGL(k_ba_struct_count, dim3(ntiles), dim3(kTileT), sizeof(int) * (nc + kTileT / 64), st, Ds, fl,
                          lvl, tcnt, ttot);
-    hipLaunchKernelGGL(k_ba_struct_scan, dim3(1), dim3(kStructNT), sizeof(int) * (nc + 1 + kStructNT / 64), st, D,
+    hipLaunchKernelGGL(k_ba_struct_scan, dim3(1), dim3(kStructNT), sizeof(int) * (nc + 1 + kStructNT / 64), st, Ds,
                        dfix, ntiles, tcnt, ttot, tcar, known ? p : sint_map);
     if (ntiles > 0)
       hipLaunchKernelGGL(k_ba_struct_fill, dim3(ntiles), dim3(kTileT),
-                         sizeof(int) * ((1 + kTileT / 64) * (size_t)nc + kTileE + kTileT / 64), st, D, fl, lvl, tcnt,
+                         sizeof(int) * ((1 + kTileT / 64) * (size_t)nc + kTileE + kTileT / 64), st, Ds, fl, lvl, tcnt,
                          tcar);
-    BA_CHECK(hipGetLastError());
-    const int* sz = known;
-    if (!sz) {
-      BA_CHECK(hipStreamSynchronize(st));
-      sz = sint_host;
-    }
-    const orbx_status fs = finish_structure(sz[0], sz[1], sz[2], sz[3], sz[4], st);
-    t_struct[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
-    return fs;
+    return hipGetLastError();
   }
 
   // Sizes known: scratch allocations, readback block, Schur pair table.
@@ -3401,8 +3426,10 @@ struct LocalBA {
   // rejections; a finished phase turns the queued rest into empty launches.
   LmState* lm_host = nullptr;  // pinned, mapped (lm_map: the device's view)
   LmState* lm_map = nullptr;
+  // spec (optional): launches queued behind every readback of the phase (before its event), gated on
+  // the device LM state (spec_skip) -- phase 1 queues phase 2's outlier marking and structure there
   orbx_status optimize_dev(int iterations, const StopFlag& stop, const DevStop& dstop, hipStream_t st, int* iters,
-                           double* final_chi) {
+                           double* final_chi, const std::function<hipError_t()>& spec = nullptr) {
     const size_t N = 6 * (size_t)D.nposes;
     if (ldlt_np((int)N) > kLdltMaxNp) return ORBX_ERR_SIZE;
     LdltPlan ldlt;
@@ -3482,6 +3509,7 @@ struct LocalBA {
         Dr.lm_copy = c.lm.p;
         hipLaunchKernelGGL(k_ba_errors, dim3(ge), dim3(LBS), 0, st, Dr, 0, 0);
         BA_CHECK(hipGetLastError());
+        if (spec) BA_CHECK(spec());
         BA_CHECK(hipEventRecord(rb_ev, st));
         BA_CHECK(finish_read(sc));
         if (lm_host->refresh) {  // paused on a NaN-rho rejection: pop, errors at the restored state, resume
@@ -3794,8 +3822,25 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
   L.unmap_stop();
   L.hook_stopped = false;
   if (!L.map_stop(stop, &dstop)) return ORBX_ERR_HIP;
-  auto optimize = [&](int iterations, int* iters, double* chi) {
-    return L.optimize_dev(iterations, stop, dstop, st, iters, chi);
+  auto optimize = [&](int iterations, int* iters, double* chi, const std::function<hipError_t()>& spec = nullptr) {
+    return L.optimize_dev(iterations, stop, dstop, st, iters, chi, spec);
+  };
+  // phase 2's outlier marking and structure, queued behind phase 1's readback and gated on its LM
+  // state (spec_skip): when phase 1 ends on an accepted state the one readback also brings phase
+  // 2's sizes, so the call pays one host round trip between the phases instead of two
+#ifndef ORBX_BA_SPEC2
+#define ORBX_BA_SPEC2 1
+#endif
+  const bool spec2 = ORBX_BA_SPEC2 && L.dev_struct && ne > 0;
+  BaDev Dspec = D;  // (filled below, after the phase-1 structure)
+  auto spec = [&]() -> hipError_t {
+    // the gate is read here, not when Dspec is filled: optimize_dev allocates the LM state on a
+    // handle's first call, after the phase-1 structure (an ungated launch would run mid-phase)
+    if (!c.lm.p) return hipErrorInvalidValue;
+    Dspec.lm = c.lm.p;
+    hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, Dspec, c.flag.p, 1);
+    HIP_TRY(hipGetLastError());
+    return L.launch_structure_dev(0, st, nullptr, c.lm.p);
   };
   if (!(stop())) {  // src/Optimizer.cc:749-751
     ran = true;
@@ -3806,19 +3851,27 @@ orbx_status run_local_ba(LocalBA& L, const orbx_ba_problem* pb, orbx_ba_result* 
     host_build_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
     tm[1] = tb1;
     if (s != ORBX_OK) return s;
-    s = optimize(5, &res->iterations[0], &res->chi2[0]);
+    Dspec = D;
+    s = optimize(5, &res->iterations[0], &res->chi2[0], spec2 ? std::function<hipError_t()>(spec) : nullptr);
     if (s != ORBX_OK) return s;
+    // did the speculative phase-2 launches run (phase 1 ended done, nothing to pop or refresh)?
+    const bool spec_ran = spec2 && L.lm_host->done && !L.lm_host->refresh && !L.lm_host->rejected;
     tm[2] = tm[3] = tm[4] = std::chrono::steady_clock::now();
     if (!(stop()) && !L.hook_stopped) {
-      // :764-802 level-1 outliers, drop robust kernels
-      if (ne > 0) hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 1);
+      // :764-802 level-1 outliers, drop robust kernels (already done on the device when spec_ran)
+      if (ne > 0 && !spec_ran) hipLaunchKernelGGL(k_ba_outliers, dim3(ge), dim3(LBS), 0, st, D, c.flag.p, 1);
       BA_CHECK(hipGetLastError());
       if (!L.dev_struct) {
         BA_CHECK(hipMemcpyAsync(L.level.data(), c.flag.p, ne, hipMemcpyDeviceToHost, st));
         BA_CHECK(hipStreamSynchronize(st));
       }
       const auto tb2 = std::chrono::steady_clock::now();
-      s = L.build_structure(0, st);
+      if (spec_ran) {
+        const int* sz = L.sint_host;  // written by the speculative k_ba_struct_scan before the readback's event
+        s = L.finish_structure(sz[0], sz[1], sz[2], sz[3], sz[4], st);
+      } else {
+        s = L.build_structure(0, st);
+      }
       tm[3] = std::chrono::steady_clock::now();
       host_build_ms += std::chrono::duration<double, std::milli>(tm[3] - tb2).count();
       if (s != ORBX_OK) return s;

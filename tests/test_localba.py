@@ -304,6 +304,21 @@ def test_gpu_reduced_system_ldlt_pan_few_poses(gpu, nposes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["rejects_a", "rejects_b", "nbad_stop", "small"])
+def test_gpu_localba_fresh_handle_matches_oracle(gpu, case):
+    """The first call on a fresh handle (the LM state, structure buffers and mapped readback blocks
+    are allocated during it) -- where phase 1 needs more than one readback, phase 2's outlier
+    marking and structure queued behind each readback must stay gated until phase 1 is done."""
+    from orb_slam2_commit_amd import Optimizer
+    P = small_problem(seed=4) if case == "small" else reject_problem(case)
+    o = Optimizer(0)
+    try:
+        _compare(o.LocalBundleAdjustment(P), oracle.local_ba(P))
+    finally:
+        o.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["config4", "rejects_a", "rejects_b", "nbad_stop", "nan_trial"])
 def test_gpu_localba_errors_ctl_equals_two_launches(ba, case):
     """k_ba_errors_ctl (a trial's errors and the LM verdict in one launch, the partials handed to the
