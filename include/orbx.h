@@ -22,6 +22,8 @@
  *   orbx_extract_batch_device   frame-batch form of operator() (one launch per stage for n images)
  *   orbx_stereo_match           Frame::ComputeStereoMatches     src/Frame.cc:547-788, include/Frame.h:111
  *   orbx_stereo_frames_device   extract(L)+extract(R)+ComputeStereoMatches for n stereo frames
+ *   orbx_frame_stereo           the ORB part of Frame's stereo constructor: ExtractORB(0/1) on two
+ *                               threads + ComputeStereoMatches  src/Frame.cc:62-123 (:80-84, :121)
  *   orbx_descriptor_distance_device
  *                               ORBmatcher::DescriptorDistance  src/ORBmatcher.cc:1844-1860, include/ORBmatcher.h:50
  *   orbx_search_by_bow_kf_f     ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
@@ -147,6 +149,20 @@ orbx_status orbx_extract_batch_device(orbx_extractor* h, int n_images, const uin
 orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const orbx_keypoint* kpsL,
                               const uint8_t* descL, int nL, const orbx_keypoint* kpsR, const uint8_t* descR,
                               int nR, float bf, float baseline, float* uRight, float* depth);
+
+/* The ORB part of the stereo Frame constructor in one call (src/Frame.cc:62-123: ExtractORB(0, imLeft)
+ * and ExtractORB(1, imRight) on two threads, then ComputeStereoMatches), host images in and host
+ * results out: both images go through `h` as one batch of two (the reference builds its left and
+ * right extractors with the same parameters, src/Tracking.cc:113-126; results are those of two
+ * orbx_extract calls + orbx_stereo_match), the matcher runs on the device right behind them and
+ * everything returns in one copy with one synchronisation.  nL / nR keypoints and descriptors into
+ * kpsL / descL (capacity capL) and kpsR / descR (capR); uRight[nL], depth[nL] (-1 = no match).
+ * Afterwards orbx_pyramid_level(h, 0 / 1, ...) reads the left / right pyramid, and h's last
+ * extraction is no longer an orbx_extract result (orbx_stereo_match on it returns ORBX_ERR_STATE). */
+orbx_status orbx_frame_stereo(orbx_extractor* h, const uint8_t* imL, size_t strideL, const uint8_t* imR,
+                              size_t strideR, int width, int height, float bf, float baseline, orbx_keypoint* kpsL,
+                              uint8_t* descL, int capL, int* nL, orbx_keypoint* kpsR, uint8_t* descR, int capR,
+                              int* nR, float* uRight, float* depth);
 
 /* Device-resident stereo frames: d_images holds 2*n_frames images ordered
  * L0,R0,L1,R1,... (pitch image_pitch).  Runs extraction of all 2n images and

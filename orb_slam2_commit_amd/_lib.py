@@ -185,6 +185,8 @@ SIGNATURES = {
     "orbx_pyramid_level": ([P, C.c_int, C.c_int, P, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
     "orbx_extract_batch_device": ([P, C.c_int, P, C.c_int, C.c_int, C.c_size_t, P, P, P, C.c_int, P], C.c_int),
     "orbx_stereo_match": ([P, P, P, P, C.c_int, P, P, C.c_int, C.c_float, C.c_float, P, P], C.c_int),
+    "orbx_frame_stereo": ([P, P, C.c_size_t, P, C.c_size_t, C.c_int, C.c_int, C.c_float, C.c_float, P, P, C.c_int, P,
+                           P, P, C.c_int, P, P, P], C.c_int),
     "orbx_stereo_frames_device": ([P, C.c_int, P, C.c_int, C.c_int, C.c_size_t, P, P, P, C.c_int, C.c_float,
                                    C.c_float, P, P, P, P], C.c_int),
     "orbx_descriptor_distance_device": ([P, P, C.c_int, P, P], C.c_int),

@@ -412,6 +412,10 @@ orbx_status build_plan(const orbx_extractor_params& p, const Tables& t, int W, i
     G.n_og = 0;
     group(0, split, 512, 50 * 1024, G.og[G.n_og++]);
     if (split < p.nlevels) group(split, p.nlevels, 256, 24 * 1024, G.og[G.n_og++]);
+    // one or two images (the host-API calls): every level in ONE launch of 512-thread blocks with
+    // the CU's LDS to spend -- a handful of blocks, so the groups' two launches would only run one
+    // after the other
+    group(0, p.nlevels, 512, 150 * 1024, G.og_all);
   }
   return ORBX_OK;
 }
@@ -523,6 +527,7 @@ orbx_status get_plan(orbx_extractor* h, int W, int H, Plan** out) {
     size_t mx = 0;
     for (int g = 0; g < P->G.n_og; g++)
       mx = std::max(mx, octree_smem_host(P->G.og[g].node_cap, P->G.og[g].cell_cap, P->G.og[g].kcap));
+    mx = std::max(mx, octree_smem_host(P->G.og_all.node_cap, P->G.og_all.cell_cap, P->G.og_all.kcap));
     e = octree_set_smem_limit(mx);
   }
   if (e != hipSuccess) return ORBX_ERR_HIP;
@@ -909,6 +914,75 @@ orbx_status orbx_stereo_match(orbx_extractor* left, orbx_extractor* right, const
   if (e != hipSuccess) return ORBX_ERR_HIP;
   std::memcpy(uRight, h->hstage, sizeof(float) * nL);
   std::memcpy(depth, h->hstage + sizeof(float) * nL, sizeof(float) * nL);
+  return ORBX_OK;
+}
+
+orbx_status orbx_frame_stereo(orbx_extractor* h, const uint8_t* imL, size_t strideL, const uint8_t* imR,
+                              size_t strideR, int width, int height, float bf, float baseline, orbx_keypoint* kpsL,
+                              uint8_t* descL, int capL, int* nL, orbx_keypoint* kpsR, uint8_t* descR, int capR,
+                              int* nR, float* uRight, float* depth) {
+  if (!h || !nL || !nR) return ORBX_ERR_ARG;
+  *nL = *nR = 0;
+  if (!imL || !imR || width <= 0 || height <= 0) return ORBX_ERR_ARG;
+  if (strideL < (size_t)width || strideR < (size_t)width) return ORBX_ERR_ARG;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBX_ERR_HIP;
+  Plan* P = nullptr;
+  orbx_status s = get_plan(h, width, height, &P);
+  if (s != ORBX_OK) return s;
+  const int kc = P->G.max_kps;
+  if (kc > kMaxStereoKps) return ORBX_ERR_CAPACITY;
+  // device output block: counts (L, R) and the match count | keypoints (L | R, kc each) |
+  // descriptors (L | R) | uRight | depth -- one copy back; the images go in as a batch of two
+  const size_t npx = (size_t)width * height;
+  const size_t o_kps = 256, o_desc = o_kps + (((size_t)2 * kc * sizeof(orbx_keypoint) + 255) & ~(size_t)255),
+               o_ur = o_desc + (size_t)2 * kc * 32, o_dep = o_ur + (size_t)kc * 4, o_end = o_dep + (size_t)kc * 4;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess) e = x; };
+  chk(h->in.ensure(2 * npx));
+  chk(h->out.ensure(o_end));
+  chk(h->ensure_stage(std::max(2 * npx, o_end)));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  hipStream_t st = h->stream;
+  // the left image's copy runs while the right one is staged
+  uint8_t* hs = h->hstage;
+  for (int y = 0; y < height; y++) std::memcpy(hs + (size_t)y * width, imL + (size_t)y * strideL, width);
+  chk(hipMemcpyAsync(h->in.p, hs, npx, hipMemcpyHostToDevice, st));
+  for (int y = 0; y < height; y++) std::memcpy(hs + npx + (size_t)y * width, imR + (size_t)y * strideR, width);
+  chk(hipMemcpyAsync(h->in.p + npx, hs + npx, npx, hipMemcpyHostToDevice, st));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  int32_t* d_counts = (int32_t*)h->out.p;
+  orbx_keypoint* d_kps = (orbx_keypoint*)(h->out.p + o_kps);
+  uint8_t* d_desc = h->out.p + o_desc;
+  float* d_ur = (float*)(h->out.p + o_ur);
+  float* d_dep = (float*)(h->out.p + o_dep);
+  s = run_extract(h, P, 2, h->in.p, npx, d_kps, d_desc, d_counts, kc, st);
+  if (s != ORBX_OK) return s;
+  // images 0 (left) and 1 (right) of the batch: strides 1 frame apart, as orbx_stereo_frames_device
+  s = run_stereo(h, h, 1, d_kps, d_desc, d_counts, 2 * (long long)kc, 2, d_kps + kc, d_desc + (size_t)kc * 32,
+                 d_counts + 1, 2 * (long long)kc, 2, 2, 0, 2, 1, kc, bf, baseline, d_ur, d_dep, kc, d_counts + 2, st);
+  if (s != ORBX_OK) return s;
+  chk(hipMemcpyAsync(hs, h->out.p, o_end, hipMemcpyDeviceToHost, st));
+  chk(hipStreamSynchronize(st));
+  if (e != hipSuccess) return ORBX_ERR_HIP;
+  // this handle's block no longer holds a single orbx_extract result (orbx_stereo_match refuses it);
+  // orbx_pyramid_level serves images 0 / 1 of this batch from the device
+  h->last_host = false;
+  h->hpyr_valid = false;
+  const int cl = ((const int32_t*)hs)[0], cr = ((const int32_t*)hs)[1];
+  *nL = cl;
+  *nR = cr;
+  if (cl > capL || cr > capR) return ORBX_ERR_CAPACITY;
+  const orbx_keypoint* hk = (const orbx_keypoint*)(hs + o_kps);
+  if (cl > 0) {
+    if (kpsL) std::memcpy(kpsL, hk, sizeof(orbx_keypoint) * cl);
+    if (descL) std::memcpy(descL, hs + o_desc, (size_t)32 * cl);
+    if (uRight) std::memcpy(uRight, hs + o_ur, sizeof(float) * cl);
+    if (depth) std::memcpy(depth, hs + o_dep, sizeof(float) * cl);
+  }
+  if (cr > 0) {
+    if (kpsR) std::memcpy(kpsR, hk + kc, sizeof(orbx_keypoint) * cr);
+    if (descR) std::memcpy(descR, hs + o_desc + (size_t)kc * 32, (size_t)32 * cr);
+  }
   return ORBX_OK;
 }
 

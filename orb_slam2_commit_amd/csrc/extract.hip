@@ -1650,9 +1650,11 @@ hipError_t launch_extract_stages(const Geometry& Gh, const Geometry* Gd, const C
   }
   if (Gh.ncells > 0) {
     T->begin(st);
-    // (launch order of the groups measured flat)
-    for (int gi = 0; gi < Gh.n_og; gi++) {
-      const OctGroup& og = Gh.og[gi];
+    // (launch order of the groups measured flat).  One or two images: all levels in one launch
+    // (the groups' launches would run one after the other with a few blocks each)
+    const bool one = n_img <= kOctOneLaunch;
+    for (int gi = 0; gi < (one ? 1 : Gh.n_og); gi++) {
+      const OctGroup& og = one ? Gh.og_all : Gh.og[gi];
       const size_t smem = octree_smem_bytes(og.node_cap, og.cell_cap, og.kcap);
       if (og.nt == 512)
         hipLaunchKernelGGL(k_octree<512>, dim3(n_img, og.l1 - og.l0), dim3(512), smem, st, Gd, cells, B, og);

@@ -37,6 +37,8 @@ struct LevelGeom {
   int tile_begin, tiles_x, tiles_y;  // blur tiles
 };
 
+// batches up to this many images run k_octree as one launch over every level (Geometry::og_all)
+constexpr int kOctOneLaunch = 2;
 // k_octree launch group: levels [l0, l1) as NT-thread blocks with LDS sized for those levels
 struct OctGroup {
   int l0, l1, nt;
@@ -56,6 +58,7 @@ struct Geometry {
   int oct_kcap;   // octree: candidates of a level kept in LDS (the rest in global scratch)
   OctGroup og[2];  // k_octree launch groups (levels 0..split-1 at 512 threads, the rest at 256)
   int n_og;
+  OctGroup og_all;  // every level in one launch (batches of <= kOctOneLaunch images)
   // k_fast launch groups (consecutive cell ranges, one launch each) with their LDS layout, sized by
   // the group's largest cell: row stride s of the window tile and the score map (40, 48 or 80),
   // region rows per compass instruction rp (2 when the group's cells are <= 32 wide)

@@ -173,6 +173,35 @@ def compute_stereo_matches(extractor_left, extractor_right, kps_left, desc_left,
     return uR, depth
 
 
+def frame_stereo(extractor, image_left, image_right, bf, baseline):
+    """The ORB part of Frame's stereo constructor (src/Frame.cc:62-123: ExtractORB(0/1) + ComputeStereoMatches)
+    in one call through `extractor` (both images as one batch of two, one copy back).
+
+    Returns (kps_left, desc_left, kps_right, desc_right, mvuRight, mvDepth) as ``extractor(image)`` and
+    ``compute_stereo_matches`` return them (descriptors None for an empty side)."""
+    L = np.asarray(image_left)
+    R = np.asarray(image_right)
+    assert L.dtype == np.uint8 and L.ndim == 2 and R.dtype == np.uint8 and R.shape == L.shape, "two CV_8UC1 images"
+    if L.strides[1] != 1:
+        L = np.ascontiguousarray(L)
+    if R.strides[1] != 1:
+        R = np.ascontiguousarray(R)
+    h, w = L.shape
+    cap = extractor.max_keypoints(w, h)
+    kL, kR = np.zeros(cap, KEYPOINT_DTYPE), np.zeros(cap, KEYPOINT_DTYPE)
+    dL, dR = np.zeros((cap, 32), np.uint8), np.zeros((cap, 32), np.uint8)
+    uR, depth = np.full(cap, -1.0, np.float32), np.full(cap, -1.0, np.float32)
+    nL, nR = C.c_int(0), C.c_int(0)
+    check(_lib.lib().orbx_frame_stereo(extractor._h, ptr(L), L.strides[0], ptr(R), R.strides[0], w, h, C.c_float(bf),
+                                       C.c_float(baseline), ptr(kL), ptr(dL), cap, C.byref(nL), ptr(kR), ptr(dR), cap,
+                                       C.byref(nR), ptr(uR), ptr(depth)),
+          "orbx_frame_stereo")
+    extractor._last_shape = (w, h)
+    nL, nR = nL.value, nR.value
+    return (kL[:nL].copy(), dL[:nL].copy() if nL else None, kR[:nR].copy(), dR[:nR].copy() if nR else None,
+            uR[:nL].copy(), depth[:nL].copy())
+
+
 def compute_distinctive_descriptors(desc, obs_off, device=0):
     """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:249-320) for a batch of MapPoints:
     desc[obs_off[p]:obs_off[p+1]] are point p's observed descriptors in mObservations order.

@@ -390,6 +390,11 @@ class Frame {
   int mnScaleLevels = 0;
   float mfScaleFactor = 0.f;
   std::vector<float> mvScaleFactors, mvInvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
+
+ private:
+  // src/Frame.cc:86-123 after the two ExtractORB calls; uR / dep: stereo results already computed by
+  // orbx_frame_stereo (null: ComputeStereoMatches runs)
+  void finish_stereo_frame(const std::vector<float>* uR, const std::vector<float>* dep);
 };
 
 // Free-function form of Frame::ComputeStereoMatches for callers without a Frame object:

@@ -6,4 +6,8 @@
 
 namespace ORB_SLAM2 {
 extern int gOrbxDevice;
+// The stereo Frame constructor runs its two ExtractORB calls and ComputeStereoMatches as one library
+// call (orbx_frame_stereo) when both extractors have the same parameters (default true); false keeps
+// the reference's two extraction threads followed by the matcher (same results).
+extern bool gOrbxFrameStereoFused;
 }  // namespace ORB_SLAM2

@@ -128,6 +128,46 @@ Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extrac
     : mpORBextractorLeft(extractorLeft), mpORBextractorRight(extractorRight), mbf(bf), mThDepth(thDepth) {
   mK = K.clone();
   mDistCoef = distCoef.clone();
+  ORBextractor* eL = extractorLeft;
+  ORBextractor* eR = extractorRight;
+  // Tracking builds both extractors with the same parameters (src/Tracking.cc:113-126): then the two
+  // ExtractORB calls and ComputeStereoMatches run as one library call on the left handle (both
+  // images one batch, the matcher on the device right behind them, one copy back)
+  if (gOrbxFrameStereoFused && eL && eR && eL != eR && eL->nfeatures == eR->nfeatures &&
+      eL->scaleFactor == eR->scaleFactor && eL->nlevels == eR->nlevels && eL->iniThFAST == eR->iniThFAST && eL->minThFAST == eR->minThFAST &&
+      !imLeft.empty() && !imRight.empty() && imLeft.type() == CV_8UC1 && imRight.type() == CV_8UC1 &&
+      imLeft.rows == imRight.rows && imLeft.cols == imRight.cols && K.at<float>(0, 0) != 0.f) {
+    const int cap = orbx_extractor_max_keypoints(eL->gpu(), imLeft.cols, imLeft.rows);
+    if (cap < 0) check(cap, "orbx_extractor_max_keypoints");
+    mvKeys.resize(cap);
+    mvKeysRight.resize(cap);
+    cv::Mat dL(cap > 0 ? cap : 1, 32, CV_8U), dR(cap > 0 ? cap : 1, 32, CV_8U);
+    std::vector<float> uR(cap > 0 ? cap : 1), dep(cap > 0 ? cap : 1);
+    int nL = 0, nR = 0;
+    const float fx0 = K.at<float>(0, 0);
+    check(orbx_frame_stereo(eL->gpu(), imLeft.data, imLeft.step, imRight.data, imRight.step, imLeft.cols,
+                            imLeft.rows, bf, bf / fx0, reinterpret_cast<orbx_keypoint*>(mvKeys.data()), dL.data, cap,
+                            &nL, reinterpret_cast<orbx_keypoint*>(mvKeysRight.data()), dR.data, cap, &nR, uR.data(),
+                            dep.data()),
+          "orbx_frame_stereo");
+    mvKeys.resize(nL);
+    mvKeysRight.resize(nR);
+    // ExtractForFrame's outputs: exactly n descriptor rows (none for an empty side), no pyramid kept
+    if (nL) {
+      mDescriptors.create(nL, 32, CV_8U);
+      std::memcpy(mDescriptors.data, dL.data, (size_t)32 * nL);
+    }
+    if (nR) {
+      mDescriptorsRight.create(nR, 32, CV_8U);
+      std::memcpy(mDescriptorsRight.data, dR.data, (size_t)32 * nR);
+    }
+    for (int l = 0; l < eL->nlevels; l++) {
+      eL->mvImagePyramid[l].release();
+      eR->mvImagePyramid[l].release();
+    }
+    finish_stereo_frame(&uR, &dep);
+    return;
+  }
   // two extraction threads, each on its own extractor handle / HIP stream (src/Frame.cc:80-84)
   std::exception_ptr errL, errR;
   std::thread threadLeft([&] {
@@ -140,6 +180,12 @@ Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extrac
   threadRight.join();
   if (errL) std::rethrow_exception(errL);
   if (errR) std::rethrow_exception(errR);
+  finish_stereo_frame(nullptr, nullptr);
+}
+
+// The rest of the stereo constructor after ExtractORB (src/Frame.cc:86-123); uR / dep: the stereo
+// matches orbx_frame_stereo already computed (else ComputeStereoMatches runs here)
+void Frame::finish_stereo_frame(const std::vector<float>* uR, const std::vector<float>* dep) {
   N = (int)mvKeys.size();
   // scale tables (src/Frame.cc:66-73) and the static intrinsics (:111-126)
   mnScaleLevels = mpORBextractorLeft->GetLevels();
@@ -158,7 +204,12 @@ Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, ORBextractor* extrac
   if (mvKeys.empty()) return;
   mb = mbf / fx;  // :133-134
   UndistortKeyPoints();
-  ComputeStereoMatches();
+  if (uR && dep) {  // ComputeStereoMatches' results (mvKeys, mvKeysRight, mb: the same inputs)
+    mvuRight.assign(uR->begin(), uR->begin() + N);
+    mvDepth.assign(dep->begin(), dep->begin() + N);
+  } else {
+    ComputeStereoMatches();
+  }
   mvpMapPoints.assign(N, nullptr);
   mvbOutlier.assign(N, false);
 }
@@ -168,6 +219,7 @@ float Frame::mnMinX = 0.f, Frame::mnMaxX = 0.f, Frame::mnMinY = 0.f, Frame::mnMa
 float Frame::mfGridElementWidthInv = 0.f, Frame::mfGridElementHeightInv = 0.f;
 bool Frame::mbInitialComputations = true;
 int gOrbxDevice = 0;
+bool gOrbxFrameStereoFused = true;
 
 Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, const double& timeStamp, ORBextractor* extractorLeft,
              ORBextractor* extractorRight, ORBVocabulary* voc, cv::Mat& K, cv::Mat& distCoef, const float& bf,

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "ORBextractor.h"
+#include "orbx_shim.h"
 #include "Objects.h"
 
 using namespace ORB_SLAM2;
@@ -66,6 +67,8 @@ int main(int argc, char** argv) {
                   (double)kp / NF);
       return 0;
     }
+    // "threads": the reference's two extraction threads + the matcher instead of one orbx_frame_stereo
+    gOrbxFrameStereoFused = !(argc > 10 && std::strcmp(argv[10], "threads") == 0);
     ORBextractor exL(nfeat, 1.2f, 8, 20, 7), exR(nfeat, 1.2f, 8, 20, 7);  // Tracking's (src/Tracking.cc:120-126)
     cv::Mat K(3, 3, CV_32F), dist(4, 1, CV_32F);
     std::memset(K.data, 0, 36);

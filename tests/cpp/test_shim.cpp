@@ -39,6 +39,7 @@
 #include "Optimizer.h"
 #include "PnPsolver.h"
 #include "orbx.h"
+#include "orbx_shim.h"
 
 using namespace ORB_SLAM2;
 
@@ -170,9 +171,24 @@ static int mode_stereo(const char* in, const char* out) {
   K.at<float>(0, 2) = w / 2.f;
   K.at<float>(1, 2) = h / 2.f;
   K.at<float>(2, 2) = 1.f;
-  Frame F(imL, imR, &exL, &exR, K, dist, bf, 35.f * bf / fx);
+  Frame F(imL, imR, &exL, &exR, K, dist, bf, 35.f * bf / fx);  // one orbx_frame_stereo call (gOrbxFrameStereoFused)
   REQUIRE(F.N == (int)F.mvKeys.size() && (int)F.mvuRight.size() == F.N && (int)F.mvDepth.size() == F.N);
   REQUIRE(F.mvKeysUn.size() == F.mvKeys.size());
+  {  // the reference's form -- two extraction threads, then ComputeStereoMatches -- gives the same frame
+    gOrbxFrameStereoFused = false;
+    Frame F2(imL, imR, &exL, &exR, K, dist, bf, 35.f * bf / fx);
+    gOrbxFrameStereoFused = true;
+    REQUIRE(F2.N == F.N && F2.mvKeysRight.size() == F.mvKeysRight.size());
+    REQUIRE(std::memcmp(F2.mvKeys.data(), F.mvKeys.data(), (size_t)F.N * 28) == 0);
+    REQUIRE(std::memcmp(F2.mvKeysRight.data(), F.mvKeysRight.data(), F.mvKeysRight.size() * 28) == 0);
+    REQUIRE(F2.mDescriptors.rows == F.mDescriptors.rows && F2.mDescriptorsRight.rows == F.mDescriptorsRight.rows);
+    for (int i = 0; i < F.N; i++) REQUIRE(std::memcmp(F2.mDescriptors.ptr<uint8_t>(i), F.mDescriptors.ptr<uint8_t>(i), 32) == 0);
+    for (int i = 0; i < F.mDescriptorsRight.rows; i++)
+      REQUIRE(std::memcmp(F2.mDescriptorsRight.ptr<uint8_t>(i), F.mDescriptorsRight.ptr<uint8_t>(i), 32) == 0);
+    REQUIRE(std::memcmp(F2.mvuRight.data(), F.mvuRight.data(), (size_t)F.N * 4) == 0);
+    REQUIRE(std::memcmp(F2.mvDepth.data(), F.mvDepth.data(), (size_t)F.N * 4) == 0);
+    REQUIRE(F2.mb == F.mb && F2.mvKeysUn.size() == F.mvKeysUn.size());
+  }
   Writer o(out);
   o.put<int32_t>(F.N);
   o.put<int32_t>((int32_t)F.mvKeysRight.size());
@@ -206,7 +222,14 @@ static int mode_stereo(const char* in, const char* out) {
     o.put<int32_t>(m.rows);
     for (int y = 0; y < m.rows; y++) o.raw(m.ptr<uint8_t>(y), m.cols);
   }
-  // the free-function form gives the same answer on the same extraction
+  // the free-function form gives the same answer on each extractor's last extraction (the left one
+  // just re-extracted imLeft above; the right one extracts imRight here)
+  {
+    std::vector<cv::KeyPoint> kr;
+    cv::Mat dr;
+    exR(imR, cv::Mat(), kr, dr);
+    REQUIRE(kr.size() == F.mvKeysRight.size() && std::memcmp(kr.data(), F.mvKeysRight.data(), kr.size() * 28) == 0);
+  }
   std::vector<float> uR2, d2;
   ComputeStereoMatches(exL, exR, F.mvKeys, F.mDescriptors, F.mvKeysRight, F.mDescriptorsRight, F.mbf, F.mb, uR2, d2);
   REQUIRE(uR2.size() == F.mvuRight.size() &&

@@ -28,6 +28,60 @@ def test_stereo_bitexact(gpu, seed, w, h, nf, bf, fx):
     assert np.array_equal(dep.view(np.uint32), odep.view(np.uint32))
 
 
+@pytest.mark.parametrize("seed,w,h,nf,bf,fx,pad", [(3, 1241, 376, 2000, KITTI_BF, KITTI_FX, 0),
+                                                   (4, 752, 480, 1200, EUROC_BF, EUROC_FX, 13)])
+def test_frame_stereo_bitexact(gpu, seed, w, h, nf, bf, fx, pad):
+    """orbx_frame_stereo (Frame's stereo constructor, src/Frame.cc:62-123, in one call: both images as a
+    batch of two, the matcher behind them, one copy back): keypoints, descriptors, uRight and depth bit
+    for bit the oracle's, with row-padded host images (pad bytes per row); afterwards the handle's
+    pyramid_level(l, image 0 / 1) is the left / right pyramid, and orbx_stereo_match refuses the handle
+    (its last call is no single orbx_extract any more)."""
+    from orb_slam2_commit_amd import frame_stereo
+    from orb_slam2_commit_amd._lib import ORBX_ERR_STATE, OrbxError
+    L, R = synth.stereo_pair(seed, w, h)
+    if pad:
+        Lp, Rp = np.zeros((h, w + pad), np.uint8), np.full((h, w + pad), 77, np.uint8)
+        Lp[:, :w], Rp[:, :w] = L, R
+        L, R = Lp[:, :w], Rp[:, :w]  # strided views
+    ex = ORBextractor(nf, 1.2, 8, 20, 7)
+    kL, dL, kR, dR, uR, dep = frame_stereo(ex, L, R, bf, bf / fx)
+    p = oracle.params(nf, 1.2, 8, 20, 7)
+    oL, oR = oracle.extract(p, np.ascontiguousarray(L)), oracle.extract(p, np.ascontiguousarray(R))
+    ouR, odep = oracle.stereo_match(p, oL, oR, bf, bf / fx)
+    assert np.array_equal(kL.view(np.uint8), oL.keypoints.view(np.uint8))
+    assert np.array_equal(dL, oL.descriptors)
+    assert np.array_equal(kR.view(np.uint8), oR.keypoints.view(np.uint8))
+    assert np.array_equal(dR, oR.descriptors)
+    assert (ouR >= 0).sum() > 50
+    assert np.array_equal(uR.view(np.uint32), ouR.view(np.uint32))
+    assert np.array_equal(dep.view(np.uint32), odep.view(np.uint32))
+    for l in (0, 3, 7):
+        assert np.array_equal(ex.pyramid_level(l, image=0), oL.level(l))
+        assert np.array_equal(ex.pyramid_level(l, image=1), oR.level(l))
+    with pytest.raises(OrbxError) as ei:
+        compute_stereo_matches(ex, ex, kL, dL, kR, dR, bf, bf / fx)
+    assert ei.value.code == ORBX_ERR_STATE
+    # the same handle serves orbx_extract afterwards, and a second frame_stereo repeats the first
+    kx, dx = ex(np.ascontiguousarray(L))
+    assert np.array_equal(kx.view(np.uint8), oL.keypoints.view(np.uint8)) and np.array_equal(dx, oL.descriptors)
+    again = frame_stereo(ex, L, R, bf, bf / fx)
+    assert np.array_equal(again[4].view(np.uint32), uR.view(np.uint32))
+
+
+def test_frame_stereo_empty_side(gpu):
+    """A flat right image has no keypoints: every left keypoint stays unmatched (-1), as
+    ComputeStereoMatches leaves it; a flat left image returns nothing at all."""
+    from orb_slam2_commit_amd import frame_stereo
+    L, _ = synth.stereo_pair(9, 640, 480)
+    flat = np.full_like(L, 128)
+    ex = ORBextractor(1000, 1.2, 8, 20, 7)
+    kL, dL, kR, dR, uR, dep = frame_stereo(ex, L, flat, KITTI_BF, KITTI_BF / KITTI_FX)
+    assert len(kL) > 100 and len(kR) == 0 and dR is None
+    assert (uR == -1).all() and (dep == -1).all()
+    kL, dL, kR, dR, uR, dep = frame_stereo(ex, flat, L, KITTI_BF, KITTI_BF / KITTI_FX)
+    assert len(kL) == 0 and dL is None and len(kR) > 100 and len(uR) == 0
+
+
 def test_stereo_uses_only_the_last_extraction(gpu):
     """orbx_stereo_match reads each extractor's device-resident keypoints, descriptors and pyramid
     (no upload), so it accepts only exactly what that extractor's last orbx_extract returned:
