@@ -227,7 +227,8 @@ __global__ __launch_bounds__(BS) void k_resize(const Geometry* __restrict__ G, c
   // 2. horizontal pass: thread = one output column, rows strided by BS / kRzTW
   if (hc < nx) {
     const int s0 = xc.sx0 - cx0, s1 = xc.sx1 - cx0, a0 = xc.a0, a1 = xc.a1;
-    for (int r = tid / kRzTW; r < nrows; r += BS / kRzTW) {
+    // (the first row is wave-uniform: a scalar loop, no exec-mask bookkeeping per row)
+    for (int r = __builtin_amdgcn_readfirstlane(tid / kRzTW); r < nrows; r += BS / kRzTW) {
       const uint8_t* t = tin + r * stride;
       hb[r * kRzTW + hc] = (int16_t)((t[s0] * a0 + t[s1] * a1) >> 4);
     }

@@ -26,16 +26,20 @@ __device__ __forceinline__ int xcd_block(int hw, int total) {
   return x * q + min(x, r) + i;
 }
 // logical (x, y) of a 2-D grid, x fastest
+// (unsigned divisions: the block-uniform quotients are scalar instruction sequences, and the signed
+// forms' abs / sign fix-ups made them a large part of a short kernel's scalar work)
 __device__ __forceinline__ int2 xcd_block2() {
-  const int gx = gridDim.x;
-  const int l = xcd_block(blockIdx.x + gx * blockIdx.y, gx * gridDim.y);
-  return make_int2(l % gx, l / gx);
+  const unsigned gx = gridDim.x;
+  const unsigned l = (unsigned)xcd_block(blockIdx.x + gx * blockIdx.y, gx * gridDim.y);
+  const unsigned q = l / gx;
+  return make_int2((int)(l - q * gx), (int)q);
 }
 // logical (x, y, z) of a 3-D grid, x fastest
 __device__ __forceinline__ int3 xcd_block3() {
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int l = xcd_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
-  return make_int3(l % gx, (l / gx) % gy, l / (gx * gy));
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned l = (unsigned)xcd_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const unsigned q = l / gx, z = q / gy;
+  return make_int3((int)(l - q * gx), (int)(q - z * gy), (int)z);
 }
 
 __device__ __forceinline__ int round_even(float v) { return (int)__builtin_rintf(v); }
