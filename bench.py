@@ -489,7 +489,8 @@ def single_frame_leg(args, pairs, cpu):
     thread (Examples/Stereo/stereo_kitti.cc:82-99 times that call), i.e. the C++ shim's Frame stereo
     constructor -- two extraction threads on two ORBextractor handles (src/Frame.cc:80-84),
     UndistortKeyPoints, ComputeStereoMatches -- from host images to host vectors
-    (shim/build/frame_bench, a separate process).  Reported beside the oracle's per-frame time."""
+    (shim/build/frame_bench, a separate process; the Frame makes one orbx_frame_stereo call).  Reported
+    beside the oracle's per-frame time."""
     exe = os.path.join(ROOT, "shim", "build", "frame_bench")
     if not os.path.exists(exe):
         return dict(error="shim/build/frame_bench not built")
@@ -510,8 +511,8 @@ def single_frame_leg(args, pairs, cpu):
         os.unlink(path)
     out.update(unit="ms per stereo frame (Frame constructor, host images in, host keypoints/descriptors/"
                     "uRight/depth out)", warmup_frames=20,
-               path="shim Frame(imLeft, imRight, ...) -> 2 x ORBextractor::operator() on two threads + "
-                    "UndistortKeyPoints + ComputeStereoMatches")
+               path="shim Frame(imLeft, imRight, ...) -> one orbx_frame_stereo call (both ExtractORB as one "
+                    "batch of two + ComputeStereoMatches on the device, one copy back) + UndistortKeyPoints")
     if cpu:
         out["cpu_baseline"] = dict(median_ms=cpu.get("median_ms"), p90_ms=cpu.get("p90_ms"),
                                    two_thread_median_ms=(cpu.get("two_thread") or {}).get("median_ms"),
