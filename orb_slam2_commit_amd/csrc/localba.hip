@@ -2339,11 +2339,34 @@ struct DevStop {
 };
 
 // optimize() entry: lambda = tau * max diag(H) (computeLambdaInit), chi of
-// the linearised state from errors slot 0 (block partials in block order).
-// Sum of n block partials in index order (the host loop's order): one wave
-// stages them in LDS with coalesced loads and lane 0 adds them in sequence
-// (valid in lane 0).  Block = one wave.
-__device__ inline double seq_sum_wave(const double* p, int n) {
+// the linearised state from errors slot 0 (block partials).
+// Sum of n block partials in a fixed order, by one wave: lane l adds p[l], p[l + 64], ... in index
+// order (eight loads in flight per round), then a butterfly over the 64 lanes.  Lane 0's value --
+// the one the LM verdict uses -- is the same bits on every run and in the batched driver.  (It
+// replaced lane 0 adding all partials in sequence through LDS: a ~170-add FP64 chain per sum on the
+// trial's critical path, and no barrier is needed now, so any wave of a block may call it.)
+template <bool coh = false>  // coh: p is read with ld_agent (partials stored by this launch's other blocks)
+__device__ inline double fixed_sum_wave(const double* p, int n) {
+  const int lane = threadIdx.x & 63;
+  double s = 0;
+  for (int base = 0; base < n; base += 512) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {  // clamped, unpredicated loads: all eight in flight at once
+      const int i = max(min(base + lane + 64 * u, n - 1), 0);
+      v[u] = coh ? ld_agent(p + i) : p[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) s += base + lane + 64 * u < n ? v[u] : 0.0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  return s;
+}
+__device__ inline double seq_sum_wave(const double* p, int n) { return fixed_sum_wave<false>(p, n); }
+// The host readback's order (partials added in index order, lane 0; block = one wave): the batched
+// driver's reported final chi, which must equal the single driver's host-side sum bit for bit.
+__device__ inline double index_order_sum_wave(const double* p, int n) {
   __shared__ double buf[1024];
   double s = 0;
   for (int base = 0; base < n; base += 1024) {
@@ -2356,44 +2379,11 @@ __device__ inline double seq_sum_wave(const double* p, int n) {
   }
   return s;
 }
-
-// Two such sums at once (same orders and bits as two seq_sum_wave calls): both arrays' loads are
-// in flight together and lane 0 adds the first while lane 1 adds the second (valid in lane 0).
-// Wave 0 does the work; every other wave of the block only passes the barriers (a block of any
-// size calls it uniformly, so no barrier ever counts on exited waves).
-template <bool coh = false>  // coh: p is read with ld_agent (partials stored by this launch's other blocks)
+// two such sums (the verdict's chi and LM scale); valid in lane 0 of every calling wave
+template <bool coh = false>
 __device__ inline void seq_sum2_wave(const double* p, int n, const double* q, int m, double& sp, double& sq) {
-  __shared__ double buf[2][512];
-  double s = 0;
-  const int len = max(n, m);
-  const bool w0 = threadIdx.x < 64;
-  for (int base = 0; base < len; base += 512) {
-    const int cn = min(512, n - base), cm = min(512, m - base);  // (may be <= 0)
-    if (w0) {
-      double vp[8], vq[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {  // clamped, unpredicated loads: all sixteen in flight at once
-        const int i = threadIdx.x + 64 * u;
-        vp[u] = coh ? ld_agent(p + max(min(base + i, n - 1), 0)) : p[max(min(base + i, n - 1), 0)];
-        vq[u] = q[max(min(base + i, m - 1), 0)];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int i = threadIdx.x + 64 * u;
-        if (i < cn) buf[0][i] = vp[u];
-        if (i < cm) buf[1][i] = vq[u];
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) {
-      const double* bb = buf[threadIdx.x];
-      const int c = threadIdx.x == 0 ? cn : cm;
-      for (int i = 0; i < c; i++) s += bb[i];
-    }
-    __syncthreads();
-  }
-  sp = s;
-  sq = __shfl(s, 1, 64);
+  sp = fixed_sum_wave<coh>(p, n);
+  sq = fixed_sum_wave<false>(q, m);
 }
 
 __device__ __forceinline__ void k_ba_lm_init_body(const BaDev& D, int iterations) {
@@ -2603,7 +2593,7 @@ __global__ __launch_bounds__(1024) void k_ba_dmax_many(const BaDev* __restrict__
 }
 __global__ __launch_bounds__(64) void k_ba_lm_final_many(const BaDev* __restrict__ Ds) {
   const BaDev& D = Ds[blockIdx.z];
-  const double a = seq_sum_wave(D.scal + 8, D.nbe);
+  const double a = index_order_sum_wave(D.scal + 8, D.nbe);
   if (threadIdx.x == 0) const_cast<LmState*>(D.lm)->final_chi = a;
 }
 
