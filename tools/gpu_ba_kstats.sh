@@ -8,12 +8,9 @@ mkdir -p $O
 R=$PWD
 for v in base $V; do
   lib=""; [ $v = base ] || lib=$R/build_ab/$v/liborbx.so
-  ORBX_LIB_OVERRIDE=$lib timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/$v -o ba -- python3 tools/ba_time.py 20 > /dev/null 2>&1 || exit 1
+  ORBX_LIB_OVERRIDE=$lib timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/$v -o ba --output-format csv -- python3 tools/ba_time.py 20 > /dev/null 2>&1 || exit 1
   f=$(find $O/$v -name "*kernel_stats.csv" | head -1)
-  echo "$v $(python3 -c "
-import csv,sys
-rows=list(csv.DictReader(open('$f')))
-print({r['Name'].split('(')[0].replace('orbx::','').replace('void ','')[:22]: round(float(r['AverageNs'])/1e3,2) for r in rows[:9]})")"
+  echo "$v $(python3 tools/kstats_brief.py $f)"
 done
 for rep in 1 2 3 4; do
   for v in base $V; do
