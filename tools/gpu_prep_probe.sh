@@ -1,5 +1,6 @@
 #!/bin/bash
-# k_stereo_prep phase cost on the single stereo frame: kernel durations with the kernel cut after
+# k_stereo_prep phase cost on the single stereo frame (build_ab/stopN: one-off builds of a temporary
+# patch that returned early from k_stereo_prep; the patch is not kept): kernel durations with the kernel cut after
 # the sort (stop1), after the sorted writes + octave starts (stop2), after the row table (stop3)
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 O=gpurun_out/prep_probe
