@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=5, help="steps of the second, per-stage profiled pass")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--ba-calls", type=int, default=10, help="timed LocalBA calls per rank (0: skip)")
+    ap.add_argument("--ba-calls", type=int, default=40, help="timed LocalBA calls per rank (0: skip)")
     ap.add_argument("--ba-concurrent", type=int, default=8, help="LocalBA problems in flight per GPU for the "
                                                                   "throughput form (<=1: skip)")
     ap.add_argument("--pipeline-steps", type=int, default=4, help="config-5 batches of distinct frames per rank (0: skip)")
